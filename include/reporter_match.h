@@ -1,0 +1,152 @@
+/* reporter_match.h — C-ABI of libreporter_match.so, the MI355X (gfx950) map
+ * matcher that replaces Valhalla/meili behind Open Traffic Reporter.
+ *
+ * Drop-in boundary (what the reference binds):
+ *   valhalla.Configure(conf)             reference py/reporter_service.py:284, py/simple_reporter.py:132
+ *       -> rm_configure
+ *   valhalla.SegmentMatcher()            reference py/reporter_service.py:52,  py/simple_reporter.py:133
+ *       -> rm_matcher_create / rm_matcher_destroy
+ *   SegmentMatcher.Match(json) -> json   reference py/reporter_service.py:240, py/simple_reporter.py:166
+ *       -> rm_match (+ rm_free for the returned string)
+ * The Python package `valhalla/` in this repository binds exactly these through
+ * ctypes, so reporter_service.py runs unchanged.
+ *
+ * Conventions: plain pointers and sizes, no C++ or torch types.  Return 0 on
+ * success, non-zero on error; the message is in rm_last_error() (thread-local).
+ * Distinct matchers/runners may be used concurrently from different threads;
+ * one handle must not be used by two threads at once (the reference keeps one
+ * SegmentMatcher per thread, py/reporter_service.py:28-29,51-52).
+ */
+#ifndef REPORTER_MATCH_H
+#define REPORTER_MATCH_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RM_ABI_VERSION 1
+
+/* ---------------- errors / device ---------------- */
+const char* rm_last_error(void);
+int rm_abi_version(void);
+int rm_set_device(int device);  /* device used by the next rm_configure / rm_engine_create */
+int rm_device_count(int* count);
+
+/* ---------------- drop-in boundary (valhalla module) ---------------- */
+typedef struct rm_matcher rm_matcher;
+/* Reads a Valhalla-style JSON config: "meili" defaults (+ per-mode sections) and
+ * the graph file ("reporter_amd": {"graph": path} or "mjolnir": {"tile_extract": *.rmg}),
+ * loads the graph into HBM.  err/errlen may be NULL. */
+int rm_configure(const char* conf_json_path, char* err, size_t errlen);
+rm_matcher* rm_matcher_create(void);            /* NULL on error (no configure yet) */
+void rm_matcher_destroy(rm_matcher* m);
+/* trace_json: {"uuid", "trace":[{"lat","lon","time"[,"accuracy"]}...], "match_options":{...}}
+ * *out_json: {"segments":[...]} allocated by the library; release with rm_free. */
+int rm_match(rm_matcher* m, const char* trace_json, char** out_json);
+/* n traces at once (one GPU launch sequence); outs[i] must each be freed with rm_free. */
+int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs);
+void rm_free(char* p);
+
+/* ---------------- matcher options (layout of rm::MatchOptions) ---------------- */
+typedef struct {
+  int32_t mode;  /* 0 auto, 1 bus, 2 motor_scooter, 3 bicycle, 4 pedestrian */
+  float sigma_z, beta, search_radius, gps_accuracy, breakage_distance, interpolation_distance,
+      max_route_distance_factor, max_route_time_factor, turn_penalty_factor;
+} rm_options;
+void rm_default_options(rm_options* o);
+
+/* ---------------- synthetic world (host only; no GPU needed) ---------------- */
+typedef struct {
+  uint32_t rows, cols;
+  double block_m;
+  uint64_t seed;
+  double center_lat, center_lon, jitter;
+  uint32_t arterial_every, highway_every;
+  double segment_max_m, internal_m, service_frac, oneway_frac, curve_frac, cell_m;
+} rm_world_params;
+void rm_default_world_params(rm_world_params* p);
+int rm_world_build(const rm_world_params* p, const char* out_path);
+/* counts of a graph file: nodes, edges, roads, verts, segments, cells, cell items */
+int rm_graph_info(const char* graph_path, uint64_t out[7]);
+
+typedef struct {
+  uint32_t n_traces, n_points;
+  double rate_s, noise_m;
+  uint64_t seed;
+  int32_t mode;
+  int64_t start_epoch;
+  uint32_t threads;
+} rm_trace_params;
+void rm_default_trace_params(rm_trace_params* p);
+/* Arrays sized n_traces*n_points; truth_* may be NULL. */
+int rm_traces_generate(const char* graph_path, const rm_trace_params* p, double* lon, double* lat, double* time,
+                       float* accuracy, uint32_t* truth_edge, uint32_t* truth_off_cm);
+
+/* ---------------- batched array API (bench / batch pipeline / parity tests) ---------------- */
+typedef struct rm_engine rm_engine;
+typedef struct rm_runner rm_runner;
+
+rm_engine* rm_engine_create(const char* graph_path, int device);
+void rm_engine_destroy(rm_engine* e);
+uint32_t rm_engine_n_segments(const rm_engine* e);
+int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids); /* n_segments ids (dense index -> OSMLR id) */
+
+rm_runner* rm_runner_create(rm_engine* e);
+void rm_runner_destroy(rm_runner* r);
+
+typedef struct {
+  uint32_t n_traces;
+  const uint32_t* trace_off;  /* n_traces+1 */
+  const float* lon;           /* degrees */
+  const float* lat;
+  const double* time;         /* epoch seconds */
+  const float* accuracy;      /* metres, < 0 when absent */
+  uint32_t n_opts;
+  const rm_options* opts;
+  const uint32_t* trace_opt;  /* per trace index into opts */
+} rm_batch_desc;
+
+typedef struct {
+  double threshold_sec;       /* reporter_service.py:55-58 (default 15) */
+  uint32_t report_mask;       /* bit (level+1) set when level is reported; {0,1} = 0x6 */
+  uint32_t transition_mask;
+  uint32_t* hist_dev;         /* device pointer, n_segments*16 u32 speed histogram, may be NULL */
+  int32_t do_report;          /* run the report() epilogue */
+} rm_run_params;
+void rm_default_run_params(rm_run_params* p);
+
+/* upload + run every kernel; blocks until done */
+int rm_runner_run(rm_runner* r, const rm_batch_desc* b, const rm_run_params* p);
+/* run again over the batch already resident in HBM (bench steps) */
+int rm_runner_rerun(rm_runner* r, const rm_run_params* p);
+/* out: [0] points [1] traces [2] transitions [3] path edges [4] segments [5] reports */
+int rm_runner_sizes(rm_runner* r, uint64_t out[6]);
+int rm_runner_get_states(rm_runner* r, uint32_t* n_states, uint32_t* state_orig);
+int rm_runner_get_candidates(rm_runner* r, uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
+int rm_runner_get_routes(rm_runner* r, uint32_t* trans_off, double* gc, uint32_t* route_cm);
+int rm_runner_get_viterbi(rm_runner* r, int8_t* choice, uint8_t* chain_start);
+int rm_runner_get_paths(rm_runner* r, uint32_t* path_off, uint32_t* path_cnt, uint32_t* path_edges, uint32_t* route_dist);
+/* segments: 56-byte records (rm::SegmentRec); seg_off has n_traces+1 entries */
+int rm_runner_get_segments(rm_runner* r, uint32_t* seg_off, void* segs);
+/* reports: 48-byte records (rm::ReportRec); stats: 40-byte rm::ReportStats per trace */
+int rm_runner_get_reports(rm_runner* r, uint32_t* rep_off, void* reps, void* stats);
+/* per-kernel HIP-event timing on the runner's stream */
+int rm_runner_set_timing(rm_runner* r, int on);
+int rm_runner_kernel_times(rm_runner* r, double* ms, uint64_t* launches, int n);
+int rm_runner_reset_times(rm_runner* r);
+const char* rm_kernel_name(int k);
+int rm_num_kernels(void);
+
+/* ---------------- device memory helpers (histograms without a framework) ---------------- */
+int rm_device_alloc(size_t bytes, void** dev_ptr);
+int rm_device_free(void* dev_ptr);
+int rm_device_memset(void* dev_ptr, int value, size_t bytes);
+int rm_device_download(void* host_dst, const void* dev_src, size_t bytes);
+int rm_device_synchronize(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,155 @@
+"""ORACLE — test infrastructure only (tests/, __graft_entry__.smoke(), bench.py
+cpu_baseline).  ctypes bridge to liboracle_meili.so (oracle/meili_oracle.c).
+
+Parity status (see meili_oracle.h): real meili UNPINNED (not available
+offline); report() PINNED by tests/golden/report_golden.json.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle_meili.so")
+K = 16
+
+
+class OgGraph(C.Structure):
+    _fields_ = [("n_nodes", C.c_uint32), ("n_edges", C.c_uint32), ("n_roads", C.c_uint32), ("n_verts", C.c_uint32),
+                ("n_segments", C.c_uint32)] + [(n, C.c_void_p) for n in (
+                    "node_off", "edges", "edge_seg", "edge_seg_off", "edge_way", "road_node0", "road_node1",
+                    "road_fwd", "road_rev", "road_len_cm", "road_vert_off", "verts", "seg_id", "seg_len_cm")] + [
+                ("lon0", C.c_double), ("lat0", C.c_double), ("dlon", C.c_double), ("dlat", C.c_double),
+                ("ncx", C.c_uint32), ("ncy", C.c_uint32), ("cell_off", C.c_void_p), ("cell_item", C.c_void_p)]
+
+
+class OgBatch(C.Structure):
+    _fields_ = [("n_traces", C.c_uint32)] + [(n, C.c_void_p) for n in (
+        "trace_off", "lon", "lat", "time", "accuracy", "opts", "trace_opt")]
+
+
+class OgStats(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("successful_count", "unreported_count", "successful_length_m",
+                                         "unreported_length_m", "discontinuities", "invalid_speeds",
+                                         "invalid_times", "unassociated", "shape_used", "n_reports")]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.run(["make", "-C", HERE], check=True, capture_output=True)
+        h = C.CDLL(LIB)
+        h.og_match.restype = C.c_void_p
+        h.og_match.argtypes = [C.POINTER(OgGraph), C.POINTER(OgBatch)]
+        h.og_free.argtypes = [C.c_void_p]
+        h.og_sizes.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 4
+        for n, k in (("og_get_states", 2), ("og_get_candidates", 4), ("og_get_routes", 3), ("og_get_viterbi", 2),
+                     ("og_get_paths", 4), ("og_get_segments", 2)):
+            getattr(h, n).argtypes = [C.c_void_p] + [C.c_void_p] * k
+        h.og_report_trace.restype = C.c_int
+        h.og_report_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_double, C.c_double, C.c_uint32, C.c_uint32,
+                                      C.c_void_p, C.POINTER(OgStats)]
+        h.og_pipeline.restype = C.c_uint64
+        h.og_pipeline.argtypes = [C.POINTER(OgGraph), C.POINTER(OgBatch), C.c_double, C.c_uint32, C.c_uint32,
+                                  C.c_void_p]
+        _lib = h
+    return _lib
+
+
+def make_graph(g):
+    """OgGraph from reporter_amd.graphfile.load() arrays (arrays must stay alive)."""
+    og = OgGraph()
+    og.n_nodes = len(g["node_lon"])
+    og.n_edges = len(g["edges"]) // 4
+    og.n_roads = len(g["road_len_cm"])
+    og.n_verts = len(g["verts"]) // 4
+    og.n_segments = len(g["seg_id"])
+    for n in ("node_off", "edges", "edge_seg", "edge_seg_off", "edge_way", "road_node0", "road_node1", "road_fwd",
+              "road_rev", "road_len_cm", "road_vert_off", "verts", "seg_id", "seg_len_cm", "cell_off", "cell_item"):
+        setattr(og, n, g[n].ctypes.data)
+    og.lon0, og.lat0, og.dlon, og.dlat = g.lon0, g.lat0, g.dlon, g.dlat
+    og.ncx, og.ncy = g.ncx, g.ncy
+    return og
+
+
+class Batch:
+    """Keeps the numpy inputs alive for the C side."""
+
+    def __init__(self, trace_off, lon, lat, time, accuracy, opts, trace_opt):
+        self.arrays = dict(
+            trace_off=np.ascontiguousarray(trace_off, np.uint32), lon=np.ascontiguousarray(lon, np.float32),
+            lat=np.ascontiguousarray(lat, np.float32), time=np.ascontiguousarray(time, np.float64),
+            accuracy=np.ascontiguousarray(accuracy, np.float32), opts=np.ascontiguousarray(opts),
+            trace_opt=np.ascontiguousarray(trace_opt, np.uint32))
+        a = self.arrays
+        self.c = OgBatch(len(a["trace_off"]) - 1, *(a[n].ctypes.data for n in (
+            "trace_off", "lon", "lat", "time", "accuracy", "opts", "trace_opt")))
+
+
+def match(graph, batch):
+    """Run the oracle matcher; returns every stage output as numpy arrays."""
+    h = lib()
+    og = make_graph(graph)
+    r = h.og_match(C.byref(og), C.byref(batch.c))
+    if not r:
+        raise MemoryError("oracle allocation failed")
+    try:
+        P, NT, NP, NS = (C.c_uint64() for _ in range(4))
+        h.og_sizes(r, C.byref(P), C.byref(NT), C.byref(NP), C.byref(NS))
+        P, NT, NP, NS = P.value, NT.value, NP.value, NS.value
+        T = batch.c.n_traces
+        out = {}
+        out["n_states"] = np.empty(T, np.uint32)
+        out["state_orig"] = np.empty(P, np.uint32)
+        h.og_get_states(r, out["n_states"].ctypes.data, out["state_orig"].ctypes.data)
+        out["cand_n"] = np.empty(P, np.uint8)
+        out["cand_road"] = np.empty((P, K), np.uint32)
+        out["cand_s"] = np.empty((P, K), np.uint32)
+        out["cand_sq"] = np.empty((P, K), np.float32)
+        h.og_get_candidates(r, out["cand_n"].ctypes.data, out["cand_road"].ctypes.data, out["cand_s"].ctypes.data,
+                            out["cand_sq"].ctypes.data)
+        out["trans_off"] = np.empty(P, np.uint32)
+        out["gc"] = np.empty(P, np.float64)
+        out["route"] = np.empty(max(NT, 1), np.uint32)
+        h.og_get_routes(r, out["trans_off"].ctypes.data, out["gc"].ctypes.data, out["route"].ctypes.data)
+        out["route"] = out["route"][:NT]
+        out["choice"] = np.empty(P, np.int8)
+        out["chain_start"] = np.empty(P, np.uint8)
+        h.og_get_viterbi(r, out["choice"].ctypes.data, out["chain_start"].ctypes.data)
+        out["path_off"] = np.empty(P, np.uint32)
+        out["path_cnt"] = np.empty(P, np.uint32)
+        out["path_pool"] = np.empty(max(NP, 1), np.uint32)
+        out["route_dist"] = np.empty(P, np.uint32)
+        h.og_get_paths(r, out["path_off"].ctypes.data, out["path_cnt"].ctypes.data, out["path_pool"].ctypes.data,
+                       out["route_dist"].ctypes.data)
+        from reporter_amd.engine import SEGMENT_DTYPE  # record layout only (numpy dtype)
+        out["seg_off"] = np.empty(T + 1, np.uint32)
+        out["segs"] = np.empty(max(NS, 1), SEGMENT_DTYPE)
+        h.og_get_segments(r, out["seg_off"].ctypes.data, out["segs"].ctypes.data)
+        out["segs"] = out["segs"][:NS]
+        return out
+    finally:
+        h.og_free(r)
+
+
+def report_trace(segs, trace_end_time, threshold_sec, report_mask, transition_mask):
+    """og_report_trace on SEGMENT_DTYPE records -> (reports array, stats dict)."""
+    from reporter_amd.engine import REPORT_DTYPE
+    segs = np.ascontiguousarray(segs)
+    out = np.empty(max(len(segs), 1), REPORT_DTYPE)
+    st = OgStats()
+    n = lib().og_report_trace(segs.ctypes.data if len(segs) else None, len(segs), float(trace_end_time),
+                              float(threshold_sec), report_mask, transition_mask, out.ctypes.data, C.byref(st))
+    return out[:n], {f: getattr(st, f) for f, _ in OgStats._fields_}
+
+
+def pipeline(graph, batch, threshold_sec=15.0, report_mask=0x6, transition_mask=0x6, hist=None):
+    """Whole CPU pipeline (match + report + histogram); returns #valid reports."""
+    og = make_graph(graph)
+    hp = hist.ctypes.data if hist is not None else None
+    return int(lib().og_pipeline(C.byref(og), C.byref(batch.c), threshold_sec, report_mask, transition_mask, hp))

@@ -1,0 +1,473 @@
+// capi.cpp — the extern "C" boundary of libreporter_match.so (include/reporter_match.h).
+//
+// Drop-in for the Python `valhalla` binding the reference calls:
+//   valhalla.Configure      reference py/reporter_service.py:284, py/simple_reporter.py:132
+//   valhalla.SegmentMatcher reference py/reporter_service.py:52,  py/simple_reporter.py:133
+//   SegmentMatcher.Match    reference py/reporter_service.py:240, py/simple_reporter.py:166
+// Match's reply follows the schema the reference documents at README.md:288-301
+// and consumes at py/reporter_service.py:79-179.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "../../include/reporter_match.h"
+#include "engine.hpp"
+#include "graph.hpp"
+#include "json.hpp"
+
+using namespace rm;
+
+static_assert(sizeof(rm_options) == sizeof(MatchOptions), "rm_options layout");
+static_assert(sizeof(ReportStats) == 40, "ReportStats layout");
+
+namespace {
+
+thread_local std::string g_err;
+int g_device = 0;
+
+struct Config {
+  std::shared_ptr<Engine> engine;
+  MatchOptions mode_defaults[5];
+};
+std::mutex g_mu;
+std::shared_ptr<Config> g_conf;
+
+int fail(const std::string& m) {
+  g_err = m;
+  return 1;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e.what());
+  } catch (...) {
+    return fail("unknown error");
+  }
+}
+
+int mode_from_name(const std::string& s) {
+  if (s == "auto") return kModeAuto;
+  if (s == "bus") return kModeBus;
+  if (s == "motor_scooter") return kModeMotorScooter;
+  if (s == "bicycle") return kModeBicycle;
+  if (s == "pedestrian") return kModePedestrian;
+  throw std::runtime_error("unsupported mode: " + s);
+}
+const char* kModeNames[5] = {"auto", "bus", "motor_scooter", "bicycle", "pedestrian"};
+
+void apply_options(const json::Value* o, MatchOptions& m) {
+  if (!o || o->type != json::Value::Object) return;
+  auto num = [&](const char* k, float& dst) {
+    const json::Value* v = o->get(k);
+    if (v && v->is_num()) dst = (float)v->num;
+    else if (v && v->type != json::Value::Null) throw std::runtime_error(std::string("match option ") + k + " must be a number");
+  };
+  num("sigma_z", m.sigma_z);
+  num("beta", m.beta);
+  num("search_radius", m.search_radius);
+  num("gps_accuracy", m.gps_accuracy);
+  num("breakage_distance", m.breakage_distance);
+  num("interpolation_distance", m.interpolation_distance);
+  num("max_route_distance_factor", m.max_route_distance_factor);
+  num("max_route_time_factor", m.max_route_time_factor);
+  num("turn_penalty_factor", m.turn_penalty_factor);
+  if (!(m.sigma_z > 0.f)) throw std::runtime_error("sigma_z must be positive");
+  if (!(m.beta > 0.f)) throw std::runtime_error("beta must be positive");
+  if (!(m.search_radius >= 0.f)) throw std::runtime_error("search_radius must be non-negative");
+}
+
+std::string dir_of(const std::string& p) {
+  const size_t k = p.find_last_of('/');
+  return k == std::string::npos ? std::string(".") : p.substr(0, k);
+}
+
+std::string read_file(const std::string& path) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("cannot open " + path);
+  std::string s;
+  char buf[65536];
+  size_t n;
+  while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) s.append(buf, n);
+  std::fclose(f);
+  return s;
+}
+
+// parsed trace ready for the engine
+struct ParsedTrace {
+  std::vector<float> lon, lat, acc;
+  std::vector<double> time;
+  MatchOptions opt;
+};
+
+ParsedTrace parse_trace(const char* text, const Config& conf) {
+  json::Value v = json::parse(text);
+  if (v.type != json::Value::Object) throw std::runtime_error("trace request must be a JSON object");
+  ParsedTrace t;
+  const json::Value* mo = v.get("match_options");
+  int mode = kModeAuto;
+  if (mo && mo->type == json::Value::Object) {
+    const json::Value* mv = mo->get("mode");
+    if (mv && mv->type == json::Value::String) mode = mode_from_name(mv->str);
+  }
+  t.opt = conf.mode_defaults[mode];
+  t.opt.mode = mode;
+  apply_options(mo, t.opt);
+  const json::Value* tr = v.get("trace");
+  if (!tr || tr->type != json::Value::Array) throw std::runtime_error("trace must be an array of points");
+  if (tr->arr.empty()) throw std::runtime_error("trace must contain at least one point");
+  const size_t n = tr->arr.size();
+  t.lon.resize(n); t.lat.resize(n); t.acc.resize(n); t.time.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    const json::Value& p = tr->arr[i];
+    const json::Value* la = p.get("lat");
+    const json::Value* lo = p.get("lon");
+    if (!la || !lo || !la->is_num() || !lo->is_num()) throw std::runtime_error("each trace point needs numeric lat and lon");
+    if (!(la->num >= -90.0 && la->num <= 90.0 && lo->num >= -180.0 && lo->num <= 180.0))
+      throw std::runtime_error("trace point out of range");
+    t.lat[i] = (float)la->num;   // Valhalla PointLL is float
+    t.lon[i] = (float)lo->num;
+    const json::Value* tm = p.get("time");
+    t.time[i] = (tm && tm->is_num()) ? tm->num : -1.0;
+    const json::Value* ac = p.get("accuracy");
+    t.acc[i] = (ac && ac->is_num()) ? (float)ac->num : -1.0f;
+  }
+  return t;
+}
+
+void append_num(std::string& o, double x) {
+  char buf[40];
+  if (x == -1.0) { o += "-1"; return; }
+  std::snprintf(buf, sizeof buf, "%.17g", x);
+  o += buf;
+}
+void append_u(std::string& o, uint64_t x) { o += std::to_string(x); }
+void append_i(std::string& o, int64_t x) { o += std::to_string(x); }
+
+std::string segments_json(const SegmentRec* s, uint32_t n) {
+  std::string o;
+  o.reserve(64 + n * 200);
+  o += "{\"segments\":[";
+  for (uint32_t k = 0; k < n; ++k) {
+    const SegmentRec& r = s[k];
+    if (k) o += ',';
+    o += '{';
+    if (r.flags & 2u) { o += "\"segment_id\":"; append_u(o, r.segment_id); o += ','; }
+    o += "\"way_ids\":[";
+    append_u(o, r.way_first);
+    if (r.way_last != r.way_first) { o += ','; append_u(o, r.way_last); }
+    o += "],\"start_time\":"; append_num(o, r.start_time);
+    o += ",\"end_time\":"; append_num(o, r.end_time);
+    o += ",\"queue_length\":"; append_i(o, r.queue_length);
+    o += ",\"length\":"; append_i(o, r.length);
+    o += ",\"internal\":"; o += (r.flags & 1u) ? "true" : "false";
+    o += ",\"begin_shape_index\":"; append_u(o, r.begin_shape_index);
+    o += ",\"end_shape_index\":"; append_u(o, r.end_shape_index);
+    o += '}';
+  }
+  o += "]}";
+  return o;
+}
+
+char* dup_string(const std::string& s) {
+  char* p = (char*)std::malloc(s.size() + 1);
+  if (!p) throw std::bad_alloc();
+  std::memcpy(p, s.c_str(), s.size() + 1);
+  return p;
+}
+
+}  // namespace
+
+struct rm_matcher {
+  std::shared_ptr<Config> conf;
+  std::unique_ptr<Matcher> m;
+};
+struct rm_engine {
+  std::shared_ptr<Engine> e;
+};
+struct rm_runner {
+  std::shared_ptr<Engine> e;
+  std::unique_ptr<Matcher> m;
+};
+
+extern "C" {
+
+const char* rm_last_error(void) { return g_err.c_str(); }
+int rm_abi_version(void) { return RM_ABI_VERSION; }
+int rm_set_device(int device) { g_device = device; return 0; }
+int rm_device_count(int* count) {
+  return guarded([&] { RM_HIP(hipGetDeviceCount(count)); });
+}
+
+void rm_default_options(rm_options* o) {
+  const MatchOptions d = default_options();
+  std::memcpy(o, &d, sizeof d);
+}
+
+int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
+  const int rc = guarded([&] {
+    if (!conf_json_path) throw std::runtime_error("config path is NULL");
+    const std::string path(conf_json_path);
+    const std::string text = read_file(path);
+    json::Value v = json::parse(text.c_str());
+    auto conf = std::make_shared<Config>();
+    MatchOptions base = default_options();
+    const json::Value* meili = v.get("meili");
+    if (meili) apply_options(meili->get("default"), base);
+    for (int m = 0; m < 5; ++m) {
+      conf->mode_defaults[m] = base;
+      conf->mode_defaults[m].mode = m;
+      if (meili) apply_options(meili->get(kModeNames[m]), conf->mode_defaults[m]);
+    }
+    std::string graph;
+    int device = g_device;
+    if (const json::Value* ra = v.get("reporter_amd")) {
+      if (const json::Value* gp = ra->get("graph"); gp && gp->type == json::Value::String) graph = gp->str;
+      if (const json::Value* dv = ra->get("device"); dv && dv->is_num()) device = (int)dv->num;
+    }
+    if (graph.empty()) {
+      if (const json::Value* mj = v.get("mjolnir"))
+        if (const json::Value* te = mj->get("tile_extract"); te && te->type == json::Value::String) graph = te->str;
+    }
+    if (graph.empty()) throw std::runtime_error("config names no graph (reporter_amd.graph or mjolnir.tile_extract)");
+    if (graph[0] != '/') graph = dir_of(path) + "/" + graph;
+    Graph g = Graph::load(graph);
+    conf->engine = std::make_shared<Engine>(g, device);
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_conf = conf;
+  });
+  if (rc && err && errlen) {
+    std::strncpy(err, g_err.c_str(), errlen - 1);
+    err[errlen - 1] = 0;
+  }
+  return rc;
+}
+
+rm_matcher* rm_matcher_create(void) {
+  rm_matcher* out = nullptr;
+  guarded([&] {
+    std::shared_ptr<Config> c;
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      c = g_conf;
+    }
+    if (!c) throw std::runtime_error("valhalla.Configure has not been called");
+    auto m = std::make_unique<rm_matcher>();
+    m->conf = c;
+    m->m = std::make_unique<Matcher>(c->engine.get());
+    out = m.release();
+  });
+  return out;
+}
+
+void rm_matcher_destroy(rm_matcher* m) { delete m; }
+
+int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs) {
+  return guarded([&] {
+    if (!m) throw std::runtime_error("matcher is NULL");
+    for (size_t i = 0; i < n; ++i) outs[i] = nullptr;
+    if (n == 0) return;
+    std::vector<ParsedTrace> pt;
+    pt.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+      if (!traces[i]) throw std::runtime_error("trace string is NULL");
+      pt.push_back(parse_trace(traces[i], *m->conf));
+    }
+    std::vector<uint32_t> off(n + 1, 0), topt(n);
+    std::vector<MatchOptions> opts(n);
+    for (size_t i = 0; i < n; ++i) { off[i + 1] = off[i] + (uint32_t)pt[i].lon.size(); opts[i] = pt[i].opt; topt[i] = (uint32_t)i; }
+    const uint64_t P = off[n];
+    std::vector<float> lon(P), lat(P), acc(P);
+    std::vector<double> tm(P);
+    for (size_t i = 0; i < n; ++i) {
+      std::copy(pt[i].lon.begin(), pt[i].lon.end(), lon.begin() + off[i]);
+      std::copy(pt[i].lat.begin(), pt[i].lat.end(), lat.begin() + off[i]);
+      std::copy(pt[i].acc.begin(), pt[i].acc.end(), acc.begin() + off[i]);
+      std::copy(pt[i].time.begin(), pt[i].time.end(), tm.begin() + off[i]);
+    }
+    HostBatch hb;
+    hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = lon.data(); hb.lat = lat.data();
+    hb.time = tm.data(); hb.accuracy = acc.data(); hb.n_opts = (uint32_t)n; hb.opts = opts.data();
+    hb.trace_opt = topt.data();
+    RunParams rp;
+    rp.do_report = 0;
+    m->m->run(hb, rp);
+    std::vector<uint32_t> soff(n + 1);
+    std::vector<SegmentRec> segs(m->m->count_segments());
+    m->m->get_segments(soff.data(), segs.data());
+    try {
+      for (size_t i = 0; i < n; ++i) outs[i] = dup_string(segments_json(segs.data() + soff[i], soff[i + 1] - soff[i]));
+    } catch (...) {
+      for (size_t i = 0; i < n; ++i) { std::free(outs[i]); outs[i] = nullptr; }
+      throw;
+    }
+  });
+}
+
+int rm_match(rm_matcher* m, const char* trace_json, char** out_json) {
+  if (!out_json) return fail("out_json is NULL");
+  *out_json = nullptr;
+  return rm_match_batch(m, &trace_json, 1, out_json);
+}
+
+void rm_free(char* p) { std::free(p); }
+
+// ---------------- world ----------------
+void rm_default_world_params(rm_world_params* p) {
+  WorldParams d;
+  p->rows = d.rows; p->cols = d.cols; p->block_m = d.block_m; p->seed = d.seed;
+  p->center_lat = d.center_lat; p->center_lon = d.center_lon; p->jitter = d.jitter;
+  p->arterial_every = d.arterial_every; p->highway_every = d.highway_every;
+  p->segment_max_m = d.segment_max_m; p->internal_m = d.internal_m; p->service_frac = d.service_frac;
+  p->oneway_frac = d.oneway_frac; p->curve_frac = d.curve_frac; p->cell_m = d.cell_m;
+}
+
+int rm_world_build(const rm_world_params* p, const char* out_path) {
+  return guarded([&] {
+    WorldParams w;
+    w.rows = p->rows; w.cols = p->cols; w.block_m = p->block_m; w.seed = p->seed;
+    w.center_lat = p->center_lat; w.center_lon = p->center_lon; w.jitter = p->jitter;
+    w.arterial_every = p->arterial_every; w.highway_every = p->highway_every;
+    w.segment_max_m = p->segment_max_m; w.internal_m = p->internal_m; w.service_frac = p->service_frac;
+    w.oneway_frac = p->oneway_frac; w.curve_frac = p->curve_frac; w.cell_m = p->cell_m;
+    build_world(w).save(out_path);
+  });
+}
+
+int rm_graph_info(const char* graph_path, uint64_t out[7]) {
+  return guarded([&] {
+    Graph g = Graph::load(graph_path);
+    out[0] = g.num_nodes(); out[1] = g.num_edges(); out[2] = g.num_roads(); out[3] = g.num_verts();
+    out[4] = g.num_segments(); out[5] = (uint64_t)g.grid.ncx * g.grid.ncy; out[6] = g.grid.cell_item.size();
+  });
+}
+
+void rm_default_trace_params(rm_trace_params* p) {
+  TraceParams d;
+  p->n_traces = d.n_traces; p->n_points = d.n_points; p->rate_s = d.rate_s; p->noise_m = d.noise_m;
+  p->seed = d.seed; p->mode = d.mode; p->start_epoch = d.start_epoch; p->threads = d.threads;
+}
+
+int rm_traces_generate(const char* graph_path, const rm_trace_params* p, double* lon, double* lat, double* time,
+                       float* accuracy, uint32_t* truth_edge, uint32_t* truth_off_cm) {
+  return guarded([&] {
+    Graph g = Graph::load(graph_path);
+    TraceParams t;
+    t.n_traces = p->n_traces; t.n_points = p->n_points; t.rate_s = p->rate_s; t.noise_m = p->noise_m;
+    t.seed = p->seed; t.mode = p->mode; t.start_epoch = p->start_epoch; t.threads = p->threads;
+    TraceSet ts = generate_traces(g, t);
+    const size_t P = ts.lon.size();
+    std::memcpy(lon, ts.lon.data(), P * 8); std::memcpy(lat, ts.lat.data(), P * 8);
+    std::memcpy(time, ts.time.data(), P * 8); std::memcpy(accuracy, ts.accuracy.data(), P * 4);
+    if (truth_edge) std::memcpy(truth_edge, ts.truth_edge.data(), P * 4);
+    if (truth_off_cm) std::memcpy(truth_off_cm, ts.truth_off_cm.data(), P * 4);
+  });
+}
+
+// ---------------- engine / runner ----------------
+rm_engine* rm_engine_create(const char* graph_path, int device) {
+  rm_engine* out = nullptr;
+  guarded([&] {
+    Graph g = Graph::load(graph_path);
+    auto e = std::make_unique<rm_engine>();
+    e->e = std::make_shared<Engine>(g, device);
+    out = e.release();
+  });
+  return out;
+}
+void rm_engine_destroy(rm_engine* e) { delete e; }
+uint32_t rm_engine_n_segments(const rm_engine* e) { return e ? e->e->n_segments() : 0; }
+int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids) {
+  return guarded([&] {
+    const auto& v = e->e->host().seg_id;
+    std::memcpy(ids, v.data(), v.size() * 8);
+  });
+}
+
+rm_runner* rm_runner_create(rm_engine* e) {
+  rm_runner* out = nullptr;
+  guarded([&] {
+    if (!e) throw std::runtime_error("engine is NULL");
+    auto r = std::make_unique<rm_runner>();
+    r->e = e->e;
+    r->m = std::make_unique<Matcher>(e->e.get());
+    out = r.release();
+  });
+  return out;
+}
+void rm_runner_destroy(rm_runner* r) { delete r; }
+
+void rm_default_run_params(rm_run_params* p) {
+  p->threshold_sec = 15.0; p->report_mask = 0x6; p->transition_mask = 0x6; p->hist_dev = nullptr; p->do_report = 1;
+}
+
+static RunParams to_rp(const rm_run_params* p) {
+  RunParams rp;
+  if (p) {
+    rp.threshold_sec = p->threshold_sec; rp.report_mask = p->report_mask; rp.transition_mask = p->transition_mask;
+    rp.hist = p->hist_dev; rp.do_report = p->do_report;
+  }
+  return rp;
+}
+
+int rm_runner_run(rm_runner* r, const rm_batch_desc* b, const rm_run_params* p) {
+  return guarded([&] {
+    HostBatch hb;
+    hb.n_traces = b->n_traces; hb.trace_off = b->trace_off; hb.lon = b->lon; hb.lat = b->lat; hb.time = b->time;
+    hb.accuracy = b->accuracy; hb.n_opts = b->n_opts; hb.opts = (const MatchOptions*)b->opts; hb.trace_opt = b->trace_opt;
+    r->m->run(hb, to_rp(p));
+  });
+}
+int rm_runner_rerun(rm_runner* r, const rm_run_params* p) { return guarded([&] { r->m->run_device(to_rp(p)); }); }
+int rm_runner_sizes(rm_runner* r, uint64_t out[6]) {
+  return guarded([&] {
+    out[0] = r->m->n_points(); out[1] = r->m->n_traces(); out[2] = r->m->n_trans(); out[3] = r->m->n_path_edges();
+    out[4] = r->m->count_segments(); out[5] = r->m->count_reports();
+  });
+}
+int rm_runner_get_states(rm_runner* r, uint32_t* a, uint32_t* b) { return guarded([&] { r->m->get_states(a, b); }); }
+int rm_runner_get_candidates(rm_runner* r, uint8_t* a, uint32_t* b, uint32_t* c, float* d) {
+  return guarded([&] { r->m->get_candidates(a, b, c, d); });
+}
+int rm_runner_get_routes(rm_runner* r, uint32_t* a, double* b, uint32_t* c) { return guarded([&] { r->m->get_routes(a, b, c); }); }
+int rm_runner_get_viterbi(rm_runner* r, int8_t* a, uint8_t* b) { return guarded([&] { r->m->get_viterbi(a, b); }); }
+int rm_runner_get_paths(rm_runner* r, uint32_t* a, uint32_t* b, uint32_t* c, uint32_t* d) {
+  return guarded([&] { r->m->get_paths(a, b, c, d); });
+}
+int rm_runner_get_segments(rm_runner* r, uint32_t* off, void* segs) {
+  return guarded([&] { r->m->get_segments(off, (SegmentRec*)segs); });
+}
+int rm_runner_get_reports(rm_runner* r, uint32_t* off, void* reps, void* stats) {
+  return guarded([&] { r->m->get_reports(off, (ReportRec*)reps, (ReportStats*)stats); });
+}
+int rm_runner_set_timing(rm_runner* r, int on) { return guarded([&] { r->m->set_timing(on != 0); }); }
+int rm_runner_kernel_times(rm_runner* r, double* ms, uint64_t* launches, int n) {
+  return guarded([&] {
+    double t[kNumKernels];
+    uint64_t l[kNumKernels];
+    r->m->sync();
+    r->m->kernel_times(t, l);
+    for (int i = 0; i < n && i < kNumKernels; ++i) { ms[i] = t[i]; if (launches) launches[i] = l[i]; }
+  });
+}
+int rm_runner_reset_times(rm_runner* r) { return guarded([&] { r->m->reset_kernel_times(); }); }
+const char* rm_kernel_name(int k) { return (k >= 0 && k < kNumKernels) ? kKernelNames[k] : ""; }
+int rm_num_kernels(void) { return kNumKernels; }
+
+int rm_device_alloc(size_t bytes, void** p) { return guarded([&] { RM_HIP(hipMalloc(p, bytes)); }); }
+int rm_device_free(void* p) { return guarded([&] { RM_HIP(hipFree(p)); }); }
+int rm_device_memset(void* p, int v, size_t n) { return guarded([&] { RM_HIP(hipMemset(p, v, n)); }); }
+int rm_device_download(void* dst, const void* src, size_t n) {
+  return guarded([&] { RM_HIP(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost)); });
+}
+int rm_device_synchronize(void) { return guarded([&] { RM_HIP(hipDeviceSynchronize()); }); }
+
+}  // extern "C"

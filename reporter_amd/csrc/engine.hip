@@ -1,0 +1,1311 @@
+// engine.hip — gfx950 kernels of the batched map matcher and their host driver.
+//
+// Replaces the work done inside valhalla.SegmentMatcher().Match (reference
+// py/reporter_service.py:240, py/simple_reporter.py:166): meili's candidate
+// search, transition routing, Viterbi and OSMLR segment forming, then the
+// reference's own post-match report() (py/reporter_service.py:79-179).
+//
+// Stage / kernel map (DESIGN.md §4 has the rooflines):
+//   k_states      one lane per trace: interpolation rule -> state layers
+//   k_candidates  K1, one wave per state: LDS-staged grid cells, point-to-polyline
+//                 projection, per-road min in an LDS hash, top-16 by rank
+//   k_routes      K2, one wave per layer pair: multi-source bounded label-correcting
+//                 search on the CSR with an LDS hash of (source, node) labels and
+//                 ballot/atomic frontier compaction; exact u64 (dist, time) keys
+//   k_viterbi     K3, one 16-lane group per trace: fp64 costs in registers,
+//                 shuffle broadcast of the previous layer, back-pointers, backtrace
+//   k_paths       one wave per chosen transition: re-search + canonical predecessors
+//   k_segments    K4, one lane per trace: traversals, time interpolation, OSMLR runs
+//   k_report      A8 epilogue, one lane per trace: report() + speed histogram
+//
+// All arithmetic follows rm_common.hpp; compiled with -ffp-contract=off so the
+// results are bit-identical to oracle/meili_oracle.c.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+
+#include "engine.hpp"
+
+namespace rm {
+
+const char* const kKernelNames[kNumKernels] = {"states", "candidates", "scan", "routes",
+                                               "viterbi", "paths", "segments", "report"};
+
+namespace {
+
+constexpr uint32_t kEmpty = 0xffffffffu;
+constexpr int kWave = 64;
+constexpr int kSmallH = 256;    // LDS hash slots, fast tier
+constexpr int kBigH = 4096;     // LDS hash slots, retry tier (one source at a time)
+constexpr int kCandH = 256;     // road hash slots in the candidate kernel
+constexpr int kInlinePath = 8;  // path edges stored inline per slot (no allocation)
+constexpr uint32_t kMaxBoundCm = 100000000u;
+constexpr double kQueueSpeedMps = 2.7777777777777777;  // 10 km/h
+
+struct DevBatch {  // POD view of the workspace for kernels
+  uint32_t T;
+  uint64_t P;
+  const uint32_t* trace_off; const float* lon; const float* lat; const double* time; const float* acc;
+  const MatchOptions* opts; const uint32_t* trace_opt;
+  uint32_t* slot_trace; uint32_t* n_states; uint32_t* state_orig;
+  uint8_t* cand_n; uint32_t* cand_road; uint32_t* cand_s; float* cand_sq;
+  uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route;
+  int8_t* choice; uint8_t* chain_start; uint8_t* bp;
+  uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
+  SegmentRec* segs; uint32_t* seg_base; uint32_t* seg_cnt;
+  ReportRec* reps; uint32_t* rep_cnt; ReportStats* stats;
+  uint32_t* ctl; uint32_t* retry_routes; uint32_t* retry_paths;
+};
+
+__device__ __forceinline__ bool edge_ok(uint32_t info, uint32_t acc) { return (((info >> 16) & 7u) & acc) != 0u; }
+__device__ __forceinline__ uint64_t edge_key(const uint4& r, int mode) {
+  return make_key(r.y, time_ms(r.y, mode_speed_dkph(mode, r.z & 0xffffu)));
+}
+__device__ __forceinline__ float as_f(uint32_t u) { return __uint_as_float(u); }
+
+__device__ __forceinline__ float point_radius(const MatchOptions& o, float acc) {
+  float r = o.search_radius;
+  if (acc >= 0.0f && acc > r) r = acc;
+  if (r > kMaxSearchRadius) r = kMaxSearchRadius;
+  if (!(r > 0.0f)) r = 0.0f;
+  return r;
+}
+
+// bound on route distance (cm) for a layer pair: min(factor * gc, breakage)
+__device__ __forceinline__ uint32_t route_bound(double gc, const MatchOptions& o) {
+  double maxd = gc * (double)o.max_route_distance_factor;
+  if ((double)o.breakage_distance < maxd) maxd = (double)o.breakage_distance;
+  double bcm = floor(maxd * 100.0);
+  if (!(bcm >= 0.0)) bcm = 0.0;
+  return bcm > (double)kMaxBoundCm ? kMaxBoundCm : (uint32_t)bcm;
+}
+__device__ __forceinline__ uint32_t time_bound(double dt, const MatchOptions& o) {
+  if (!(dt > 0.0)) return 0xffffffffu;
+  const double tm = floor(dt * (double)o.max_route_time_factor * 1000.0);
+  return tm >= 4294967295.0 ? 0xffffffffu : (uint32_t)tm;
+}
+
+// ------------------------------------------------------------------------------------------
+// k_states: interpolation rule (points closer than interpolation_distance to the last
+// state are not states; meili MapMatcher::OfflineMatch)
+__global__ void __launch_bounds__(64) k_states(DevBatch b) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= b.T) return;
+  const uint32_t o = b.trace_off[k], n = b.trace_off[k + 1] - o;
+  const MatchOptions op = b.opts[b.trace_opt[k]];
+  const double interp = (double)op.interpolation_distance;
+  uint32_t ns = 0, last = 0;
+  float llon = 0.f, llat = 0.f;
+  for (uint32_t i = 0; i < n; ++i) {
+    b.slot_trace[o + i] = k;
+    const float lo = b.lon[o + i], la = b.lat[o + i];
+    if (i > 0 && gc_distance(llon, llat, lo, la) < interp) continue;
+    b.state_orig[o + ns++] = i;
+    last = i; llon = lo; llat = la;
+  }
+  (void)last;
+  b.n_states[k] = ns;
+}
+
+// ------------------------------------------------------------------------------------------
+// K1 k_candidates: one wave (64 lanes) per state slot.
+struct CandSmem {
+  uint32_t road[kCandH];
+  unsigned long long best[kCandH];  // (sq bits << 32) | vertex  — lexicographic min per road
+  uint32_t cell_lo[64], cell_hi[64];
+  uint32_t used, ovf, ncell, slot_n;
+  uint32_t list[kCandH];
+};
+
+__device__ __forceinline__ void project(const uint4 A, const uint4 B, float lon, float lat, float mlon, float mlat,
+                                        float& sq, uint32_t& s) {
+  const float ax = (as_f(A.x) - lon) * mlon, ay = (as_f(A.y) - lat) * mlat;
+  const float bx = (as_f(B.x) - lon) * mlon, by = (as_f(B.y) - lat) * mlat;
+  const float dx = bx - ax, dy = by - ay;
+  const float l2 = dx * dx + dy * dy;
+  float t = 0.0f;
+  if (l2 > 0.0f) {
+    t = -(ax * dx + ay * dy) / l2;
+    if (t < 0.0f) t = 0.0f;
+    if (t > 1.0f) t = 1.0f;
+  }
+  const float cx = ax + t * dx, cy = ay + t * dy;
+  sq = cx * cx + cy * cy;
+  const float along = (float)A.z + t * (float)(B.z - A.z);
+  uint32_t v = (uint32_t)rintf(along);
+  if (v < A.z) v = A.z;
+  if (v > B.z) v = B.z;
+  s = v;
+}
+
+__global__ void __launch_bounds__(64) k_candidates(DevGraph g, DevBatch b) {
+  __shared__ CandSmem sm;
+  const uint64_t p = blockIdx.x;
+  const int lane = threadIdx.x;
+  const uint32_t k = b.slot_trace[p];
+  const uint32_t o = b.trace_off[k];
+  const uint32_t s = (uint32_t)(p - o);
+  if (s >= b.n_states[k]) return;
+  const MatchOptions op = b.opts[b.trace_opt[k]];
+  const uint32_t acc = mode_access(op.mode);
+  const uint32_t pt = o + b.state_orig[p];
+  const float lon = b.lon[pt], lat = b.lat[pt];
+  const float r = point_radius(op, b.acc[pt]);
+  const float mlon = meters_per_lon(lat);
+  const float mlat = (float)kMetersPerDegLat;
+  const float r2 = r * r;
+  const float pad = r * 1.01f + 0.5f;
+  const float qlon = pad / mlon, qlat = pad / mlat;
+  const double fx0 = floor(((double)(lon - qlon) - g.lon0) / g.dlon);
+  const double fx1 = floor(((double)(lon + qlon) - g.lon0) / g.dlon);
+  const double fy0 = floor(((double)(lat - qlat) - g.lat0) / g.dlat);
+  const double fy1 = floor(((double)(lat + qlat) - g.lat0) / g.dlat);
+  for (int h = lane; h < kCandH; h += kWave) { sm.road[h] = kEmpty; sm.best[h] = ~0ull; }
+  if (lane == 0) { sm.used = 0; sm.ovf = 0; }
+  __syncthreads();
+  uint32_t n_found = 0;
+  if (!(fx1 < 0 || fy1 < 0 || fx0 > (double)(g.ncx - 1) || fy0 > (double)(g.ncy - 1))) {
+    const uint32_t x0 = fx0 < 0 ? 0u : (uint32_t)fx0, y0 = fy0 < 0 ? 0u : (uint32_t)fy0;
+    const uint32_t x1 = fx1 > (double)(g.ncx - 1) ? g.ncx - 1 : (uint32_t)fx1;
+    const uint32_t y1 = fy1 > (double)(g.ncy - 1) ? g.ncy - 1 : (uint32_t)fy1;
+    const uint32_t nx = x1 - x0 + 1, ncell = nx * (y1 - y0 + 1);
+    // stage the covered cells' item ranges in LDS, 64 cells at a time
+    for (uint32_t c0 = 0; c0 < ncell; c0 += kWave) {
+      const uint32_t c = c0 + lane;
+      if (c < ncell) {
+        const uint32_t cell = (y0 + c / nx) * g.ncx + (x0 + c % nx);
+        sm.cell_lo[lane] = g.cell_off[cell];
+        sm.cell_hi[lane] = g.cell_off[cell + 1];
+      }
+      __syncthreads();
+      const uint32_t nc = min(ncell - c0, (uint32_t)kWave);
+      for (uint32_t ci = 0; ci < nc; ++ci) {
+        const uint32_t lo = sm.cell_lo[ci], hi = sm.cell_hi[ci];
+        for (uint32_t it = lo + lane; it < hi; it += kWave) {
+          const uint32_t v = g.cell_item[it];
+          const uint4 A = g.verts[v], B = g.verts[v + 1];
+          const uint32_t road = A.w;
+          const uint32_t ef = g.road_fwd[road], er = g.road_rev[road];
+          const bool ok = (ef != kNone && edge_ok(g.edges[ef].z, acc)) || (er != kNone && edge_ok(g.edges[er].z, acc));
+          if (!ok) continue;
+          float sq; uint32_t sc;
+          project(A, B, lon, lat, mlon, mlat, sq, sc);
+          if (!(sq <= r2)) continue;
+          // per-road min (sq, vertex) in the LDS hash
+          uint32_t h = (road * 2654435761u) & (kCandH - 1);
+          for (int probe = 0; probe < kCandH; ++probe) {
+            uint32_t cur = sm.road[h];
+            if (cur == kEmpty) {
+              cur = atomicCAS(&sm.road[h], kEmpty, road);
+              if (cur == kEmpty) {
+                const uint32_t u = atomicAdd(&sm.used, 1u);
+                sm.list[u] = h;
+                cur = road;
+              }
+            }
+            if (cur == road) {
+              atomicMin(&sm.best[h], ((unsigned long long)__float_as_uint(sq) << 32) | v);
+              break;
+            }
+            h = (h + 1) & (kCandH - 1);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    n_found = sm.used;
+  }
+  if (n_found > kCandH * 3 / 4) {  // too many roads inside the radius
+    if (lane == 0) atomicOr(&b.ctl[2], kErrCandOverflow);
+    n_found = 0;
+  }
+  // rank by (sq, road); keep the first 16
+  for (uint32_t q = lane; q < n_found; q += kWave) {
+    const uint32_t h = sm.list[q];
+    const uint32_t road = sm.road[h];
+    const unsigned long long bst = sm.best[h];
+    const uint32_t sqb = (uint32_t)(bst >> 32);
+    uint32_t rank = 0;
+    for (uint32_t q2 = 0; q2 < n_found; ++q2) {
+      const uint32_t h2 = sm.list[q2];
+      const uint32_t sqb2 = (uint32_t)(sm.best[h2] >> 32), road2 = sm.road[h2];
+      rank += (sqb2 < sqb || (sqb2 == sqb && road2 < road)) ? 1u : 0u;
+    }
+    if (rank < (uint32_t)kMaxCand) {
+      const uint32_t v = (uint32_t)bst;
+      float sq; uint32_t sc;
+      project(g.verts[v], g.verts[v + 1], lon, lat, mlon, mlat, sq, sc);
+      b.cand_road[p * kMaxCand + rank] = road;
+      b.cand_s[p * kMaxCand + rank] = sc;
+      b.cand_sq[p * kMaxCand + rank] = sq;
+    }
+  }
+  if (lane == 0) b.cand_n[p] = (uint8_t)min(n_found, (uint32_t)kMaxCand);
+}
+
+// ------------------------------------------------------------------------------------------
+// transition counts for the exclusive scan that lays out route[] compactly
+__global__ void k_trans_count(DevBatch b) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
+  const uint32_t k = b.slot_trace[p];
+  const uint32_t s = (uint32_t)(p - b.trace_off[k]);
+  uint32_t c = 0;
+  if (s >= 1 && s < b.n_states[k]) c = (uint32_t)b.cand_n[p - 1] * (uint32_t)b.cand_n[p];
+  b.trans_cnt[p] = c;
+}
+
+// ------------------------------------------------------------------------------------------
+// Bounded search shared by K2 (routes) and the path kernel.
+template <int H, bool PATH>
+struct SearchSmem {
+  uint32_t key[H];                 // (source << 28) | node
+  unsigned long long lab[H];       // u64 (dist cm, time ms) key
+  uint16_t fa[H], fb[H];           // frontier (slot ids), ping-pong
+  uint32_t inq[H];
+  uint32_t pred[PATH ? H : 1];
+  uint32_t nf, nn, used, ovf;
+};
+
+template <int H, bool PATH>
+__device__ __forceinline__ int h_insert(SearchSmem<H, PATH>& sm, uint32_t key) {
+  uint32_t h = (key * 2654435761u) & (H - 1);
+  for (int probe = 0; probe < H; ++probe) {
+    uint32_t cur = sm.key[h];
+    if (cur == key) return (int)h;
+    if (cur == kEmpty) {
+      cur = atomicCAS(&sm.key[h], kEmpty, key);
+      if (cur == kEmpty) {
+        if (atomicAdd(&sm.used, 1u) >= (uint32_t)(H * 3 / 4)) sm.ovf = 1u;
+        return (int)h;
+      }
+      if (cur == key) return (int)h;
+    }
+    h = (h + 1) & (H - 1);
+  }
+  sm.ovf = 1u;
+  return -1;
+}
+
+template <int H, bool PATH>
+__device__ __forceinline__ int h_find(const SearchSmem<H, PATH>& sm, uint32_t key) {
+  uint32_t h = (key * 2654435761u) & (H - 1);
+  for (int probe = 0; probe < H; ++probe) {
+    const uint32_t cur = sm.key[h];
+    if (cur == key) return (int)h;
+    if (cur == kEmpty) return -1;
+    h = (h + 1) & (H - 1);
+  }
+  return -1;
+}
+
+template <int H, bool PATH>
+__device__ __forceinline__ unsigned long long h_label(const SearchSmem<H, PATH>& sm, uint32_t key) {
+  const int h = h_find(sm, key);
+  return h < 0 ? kKeyInf : sm.lab[h];
+}
+
+// Exact lexicographic shortest (dist, time) keys from the exits of n_src source
+// candidates (source ids 0..n_src-1) to every node within `bound` cm, by
+// synchronous label-correcting rounds over an LDS frontier.  All 64 lanes call it.
+template <int H, bool PATH>
+__device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int mode, uint32_t bound,
+                               const uint32_t* roads, const uint32_t* offs, uint32_t n_src) {
+  const int lane = threadIdx.x;
+  const uint32_t acc = mode_access(mode);
+  for (int h = lane; h < H; h += kWave) {
+    sm.key[h] = kEmpty; sm.lab[h] = kKeyInf; sm.inq[h] = 0u;
+    if (PATH) sm.pred[h] = kNone;
+  }
+  if (lane == 0) { sm.nf = 0; sm.nn = 0; sm.used = 0; sm.ovf = 0; }
+  __syncthreads();
+  if ((uint32_t)lane < 2u * n_src) {  // roots: two exits per source
+    const uint32_t i = lane >> 1;
+    const uint32_t road = roads[i], s = offs[i];
+    const uint32_t L = g.road_len[road];
+    const uint32_t e = (lane & 1) ? g.road_rev[road] : g.road_fwd[road];
+    if (e != kNone) {
+      const uint4 rec = g.edges[e];
+      const uint32_t d = (lane & 1) ? s : L - s;
+      if (edge_ok(rec.z, acc) && d <= bound) {
+        const uint32_t node = (lane & 1) ? g.road_node0[road] : g.road_node1[road];
+        const unsigned long long kk = make_key(d, time_ms(d, mode_speed_dkph(mode, rec.z & 0xffffu)));
+        const int slot = h_insert(sm, (i << 28) | node);
+        if (slot >= 0) {
+          const unsigned long long old = atomicMin(&sm.lab[slot], kk);
+          if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[atomicAdd(&sm.nf, 1u)] = (uint16_t)slot;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int round = 0;; ++round) {
+    const uint32_t nf = sm.nf;
+    if (nf == 0 || sm.ovf) break;
+    if (round > 4 * H) { if (lane == 0) sm.ovf = 2u; break; }
+    uint16_t* cur = (round & 1) ? sm.fb : sm.fa;
+    uint16_t* nxt = (round & 1) ? sm.fa : sm.fb;
+    for (uint32_t q = lane; q < nf; q += kWave) sm.inq[cur[q]] = 0u;
+    __syncthreads();
+    for (uint32_t q = lane; q < nf; q += kWave) {
+      const int slot = cur[q];
+      const uint32_t kk = sm.key[slot];
+      const uint32_t node = kk & 0x0fffffffu, srcbits = kk & 0xf0000000u;
+      const unsigned long long lab = sm.lab[slot];
+      const uint32_t e0 = g.node_off[node], e1 = g.node_off[node + 1];
+      for (uint32_t e = e0; e < e1; ++e) {
+        const uint4 rec = g.edges[e];
+        if (!edge_ok(rec.z, acc)) continue;
+        const unsigned long long nk = lab + edge_key(rec, mode);
+        if (key_dist(nk) > bound) continue;
+        const int t = h_insert(sm, srcbits | rec.x);
+        if (t < 0) continue;
+        const unsigned long long old = atomicMin(&sm.lab[t], nk);
+        if (nk < old && atomicExch(&sm.inq[t], 1u) == 0u) nxt[atomicAdd(&sm.nn, 1u)] = (uint16_t)t;
+      }
+    }
+    __syncthreads();
+    if (lane == 0) { sm.nf = sm.nn; sm.nn = 0; }
+    __syncthreads();
+  }
+  __syncthreads();
+}
+
+// route key from searched source `src` to target candidate (rb, sb); combo as in the oracle
+template <int H, bool PATH>
+__device__ unsigned long long route_to(const SearchSmem<H, PATH>& sm, const DevGraph& g, int mode, uint32_t src,
+                                       uint32_t ra, uint32_t sa, uint32_t rb, uint32_t sb, int* combo) {
+  const uint32_t acc = mode_access(mode);
+  const uint32_t ef = g.road_fwd[rb], er = g.road_rev[rb], L = g.road_len[rb];
+  const uint32_t inf_f = ef != kNone ? g.edges[ef].z : 0u, inf_r = er != kNone ? g.edges[er].z : 0u;
+  const bool okf = ef != kNone && edge_ok(inf_f, acc), okr = er != kNone && edge_ok(inf_r, acc);
+  const uint32_t spf = mode_speed_dkph(mode, inf_f & 0xffffu), spr = mode_speed_dkph(mode, inf_r & 0xffffu);
+  unsigned long long best = kKeyInf;
+  int bc = -1;
+  if (ra == rb) {
+    if (okf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
+    if (okr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
+  }
+  if (okf) {
+    const unsigned long long lab = h_label(sm, (src << 28) | g.road_node0[rb]);
+    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(sb, time_ms(sb, spf)); if (k < best) { best = k; bc = 2; } }
+  }
+  if (okr) {
+    const unsigned long long lab = h_label(sm, (src << 28) | g.road_node1[rb]);
+    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(L - sb, time_ms(L - sb, spr)); if (k < best) { best = k; bc = 3; } }
+  }
+  if (combo) *combo = bc;
+  return best;
+}
+
+// ------------------------------------------------------------------------------------------
+// K2 k_routes: one wave per layer pair (s-1 -> s).  SMALL tier searches all sources at
+// once in a 256-slot hash; a pair that overflows is queued for the BIG tier, which
+// searches one source at a time in a 4096-slot hash.
+template <bool BIG>
+__global__ void __launch_bounds__(64) k_routes(DevGraph g, DevBatch b) {
+  constexpr int H = BIG ? kBigH : kSmallH;
+  __shared__ SearchSmem<H, false> sm;
+  __shared__ uint32_t s_road[kMaxCand], s_off[kMaxCand];
+  const int lane = threadIdx.x;
+  const uint32_t n_items = BIG ? min(b.ctl[3], (uint32_t)b.P) : (uint32_t)b.P;
+  for (uint64_t item = blockIdx.x; item < n_items; item += (BIG ? gridDim.x : n_items)) {
+    const uint64_t p = BIG ? b.retry_routes[item] : item;
+    const uint32_t k = b.slot_trace[p];
+    const uint32_t o = b.trace_off[k];
+    const uint32_t s = (uint32_t)(p - o);
+    if (s < 1 || s >= b.n_states[k]) continue;
+    const MatchOptions op = b.opts[b.trace_opt[k]];
+    const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
+    const double gc = gc_distance(b.lon[pa], b.lat[pa], b.lon[pb], b.lat[pb]);
+    if (!BIG && lane == 0) b.gc[p] = gc;
+    const uint32_t KA = b.cand_n[p - 1], KB = b.cand_n[p];
+    if (KA == 0 || KB == 0) continue;
+    const uint32_t bound = route_bound(gc, op);
+    const uint32_t tmax = time_bound(b.time[pb] - b.time[pa], op);
+    const uint32_t base = b.trans_off[p];
+    if (lane < (int)KA) {
+      s_road[lane] = b.cand_road[(p - 1) * kMaxCand + lane];
+      s_off[lane] = b.cand_s[(p - 1) * kMaxCand + lane];
+    }
+    __syncthreads();
+    if (!BIG) {
+      bounded_search<H, false>(sm, g, op.mode, bound, s_road, s_off, KA);
+      if (sm.ovf) {
+        if (lane == 0) {
+          const uint32_t q = atomicAdd(&b.ctl[3], 1u);
+          b.retry_routes[q] = (uint32_t)p;
+        }
+        __syncthreads();
+        continue;
+      }
+      for (uint32_t t = lane; t < KA * KB; t += kWave) {
+        const uint32_t i = t / KB, j = t - i * KB;
+        const uint32_t rb = b.cand_road[p * kMaxCand + j], sb = b.cand_s[p * kMaxCand + j];
+        const unsigned long long key = route_to(sm, g, op.mode, i, s_road[i], s_off[i], rb, sb, nullptr);
+        uint32_t out = kRouteInvalid;
+        if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
+        b.route[base + t] = out;
+      }
+    } else {
+      for (uint32_t i = 0; i < KA; ++i) {
+        bounded_search<H, false>(sm, g, op.mode, bound, s_road + i, s_off + i, 1);
+        if (sm.ovf) { if (lane == 0) atomicOr(&b.ctl[2], kErrSearchOverflow); break; }
+        for (uint32_t j = lane; j < KB; j += kWave) {
+          const uint32_t rb = b.cand_road[p * kMaxCand + j], sb = b.cand_s[p * kMaxCand + j];
+          const unsigned long long key = route_to(sm, g, op.mode, 0, s_road[i], s_off[i], rb, sb, nullptr);
+          uint32_t out = kRouteInvalid;
+          if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
+          b.route[base + i * KB + j] = out;
+        }
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K3 k_viterbi: 16 lanes per trace (4 traces per wave), lane j owns candidate j.
+__device__ __forceinline__ double shfl_d(double v, int src) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __shfl((int)(uint32_t)u, src, 16), hi = __shfl((int)(uint32_t)(u >> 32), src, 16);
+  return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ void backtrace_chain(const DevBatch& b, uint32_t o, uint32_t end, uint32_t K, double cost, int j) {
+  // argmin over the group's lanes, lowest j on ties
+  double bc = (j < (int)K) ? cost : __longlong_as_double(0x7ff0000000000000ll);
+  int bj = (j < (int)K) ? j : 1 << 20;
+  for (int off = 8; off > 0; off >>= 1) {
+    const double oc = shfl_d(bc, (threadIdx.x & 48) | ((j + off) & 15));
+    const int oj = __shfl(bj, (j + off) & 15, 16);
+    if (oc < bc || (oc == bc && oj < bj)) { bc = oc; bj = oj; }
+  }
+  bj = __shfl(bj, 0, 16);
+  __threadfence_block();
+  if (j == 0) {
+    int w = bj;
+    uint32_t t = end;
+    for (;;) {
+      b.choice[o + t] = (int8_t)w;
+      if (b.chain_start[o + t]) break;
+      w = b.bp[(uint64_t)(o + t) * kMaxCand + w];
+      --t;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
+  const int j = threadIdx.x & 15;
+  const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 4);
+  if (k >= b.T) return;
+  const uint32_t o = b.trace_off[k], S = b.n_states[k];
+  const MatchOptions op = b.opts[b.trace_opt[k]];
+  const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
+  const double beta = (double)op.beta;
+  const double brk = (double)op.breakage_distance;
+  const double INF = __longlong_as_double(0x7ff0000000000000ll);
+  bool prev_ok = false;
+  double cost = INF;
+  uint32_t prevK = 0;
+  for (uint32_t s = 0; s < S; ++s) {
+    const uint64_t l = o + s;
+    const uint32_t KB = b.cand_n[l];
+    bool start = !prev_ok || (s > 0 && b.gc[l] > brk);
+    double best = INF;
+    int arg = -1;
+    if (KB && !start) {
+      const uint32_t base = b.trans_off[l];
+      const double gcl = b.gc[l];
+      for (uint32_t i = 0; i < prevK; ++i) {
+        const double ci = shfl_d(cost, (threadIdx.x & 48) | i);
+        if (j < (int)KB && ci != INF) {
+          const uint32_t rc = b.route[base + i * KB + j];
+          if (rc != kRouteInvalid) {
+            const double c = ci + fabs((double)rc * 0.01 - gcl) / beta;
+            if (c < best) { best = c; arg = (int)i; }
+          }
+        }
+      }
+      const unsigned long long any = __ballot(j < (int)KB && arg >= 0);
+      if (((any >> (threadIdx.x & 48)) & 0xffffull) == 0) start = true;
+    }
+    if (s > 0 && prev_ok && (KB == 0 || start)) backtrace_chain(b, o, s - 1, prevK, cost, j);
+    if (KB == 0) {
+      if (j == 0) b.chain_start[l] = 1;
+      prev_ok = false; prevK = 0; cost = INF;
+      continue;
+    }
+    const double em = (j < (int)KB) ? (double)b.cand_sq[l * kMaxCand + j] * inv2s2 : INF;
+    double nc;
+    uint8_t bpj;
+    if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255; }
+    else { nc = (j < (int)KB && arg >= 0) ? best + em : INF; bpj = arg >= 0 ? (uint8_t)arg : (uint8_t)255; }
+    if (j < (int)KB) b.bp[l * kMaxCand + j] = bpj;
+    if (j == 0) b.chain_start[l] = start ? 1 : 0;
+    cost = nc;
+    prev_ok = true;
+    prevK = KB;
+  }
+  if (prev_ok) backtrace_chain(b, o, S - 1, prevK, cost, j);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_paths: one wave per chosen transition; re-run the search for (i*, j*), compute
+// canonical predecessors and write the directed-edge path into the pool.
+template <bool BIG>
+__global__ void __launch_bounds__(64) k_paths(DevGraph g, DevBatch b) {
+  constexpr int H = BIG ? kBigH : kSmallH;
+  __shared__ SearchSmem<H, true> sm;
+  __shared__ uint32_t s_road[1], s_off[1];
+  const int lane = threadIdx.x;
+  const uint32_t n_items = BIG ? min(b.ctl[4], (uint32_t)b.P) : (uint32_t)b.P;
+  for (uint64_t item = blockIdx.x; item < n_items; item += (BIG ? gridDim.x : n_items)) {
+    const uint64_t p = BIG ? b.retry_paths[item] : item;
+    const uint32_t k = b.slot_trace[p];
+    const uint32_t o = b.trace_off[k];
+    const uint32_t s = (uint32_t)(p - o);
+    if (s < 1 || s >= b.n_states[k]) continue;
+    if (b.chain_start[p] || b.choice[p] < 0) continue;
+    const MatchOptions op = b.opts[b.trace_opt[k]];
+    const int mode = op.mode;
+    const uint32_t acc = mode_access(mode);
+    const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+    const uint32_t ra = b.cand_road[(p - 1) * kMaxCand + i], sa = b.cand_s[(p - 1) * kMaxCand + i];
+    const uint32_t rb = b.cand_road[p * kMaxCand + j], sb = b.cand_s[p * kMaxCand + j];
+    const uint32_t bound = route_bound(b.gc[p], op);
+    if (lane == 0) { s_road[0] = ra; s_off[0] = sa; }
+    __syncthreads();
+    bounded_search<H, true>(sm, g, mode, bound, s_road, s_off, 1);
+    if (sm.ovf) {
+      if (!BIG) {
+        if (lane == 0) { const uint32_t q = atomicAdd(&b.ctl[4], 1u); b.retry_paths[q] = (uint32_t)p; }
+      } else if (lane == 0) {
+        atomicOr(&b.ctl[2], kErrSearchOverflow);
+      }
+      __syncthreads();
+      continue;
+    }
+    int combo = -1;
+    const unsigned long long key = route_to(sm, g, mode, 0, ra, sa, rb, sb, &combo);
+    // root keys of the source exits (only roots within the bound exist)
+    const uint32_t La = g.road_len[ra];
+    unsigned long long rk1 = kKeyInf, rk0 = kKeyInf;
+    {
+      const uint32_t ef = g.road_fwd[ra], er = g.road_rev[ra];
+      if (ef != kNone) { const uint32_t z = g.edges[ef].z; if (edge_ok(z, acc) && La - sa <= bound) rk1 = make_key(La - sa, time_ms(La - sa, mode_speed_dkph(mode, z & 0xffffu))); }
+      if (er != kNone) { const uint32_t z = g.edges[er].z; if (edge_ok(z, acc) && sa <= bound) rk0 = make_key(sa, time_ms(sa, mode_speed_dkph(mode, z & 0xffffu))); }
+    }
+    const uint32_t n1a = g.road_node1[ra], n0a = g.road_node0[ra];
+    if (combo >= 2) {
+      // canonical predecessors: min edge id among tight in-edges of non-root nodes
+      for (int h = lane; h < H; h += kWave) {
+        const uint32_t ku = sm.key[h];
+        if (ku == kEmpty) continue;
+        const unsigned long long lu = sm.lab[h];
+        if (lu == kKeyInf) continue;
+        const uint32_t u = ku & 0x0fffffffu;
+        for (uint32_t e = g.node_off[u]; e < g.node_off[u + 1]; ++e) {
+          const uint4 rec = g.edges[e];
+          if (!edge_ok(rec.z, acc)) continue;
+          const int hv = h_find(sm, rec.x);
+          if (hv < 0) continue;
+          const unsigned long long lv = sm.lab[hv];
+          if (lv == kKeyInf) continue;
+          if ((rec.x == n1a && lv == rk1) || (rec.x == n0a && lv == rk0)) continue;
+          if (lu + edge_key(rec, mode) == lv) atomicMin(&sm.pred[hv], e);
+        }
+      }
+      __syncthreads();
+    }
+    // walk the canonical predecessors once (lane 0) into an LDS buffer that reuses the
+    // frontier arrays (H u32), then copy in travel order: inline slot when short, pool else
+    uint32_t* pbuf = reinterpret_cast<uint32_t*>(sm.fa);
+    if (lane == 0) {
+      uint32_t n = 0;
+      if (combo <= 1) {
+        pbuf[n++] = combo == 0 ? g.road_fwd[ra] : g.road_rev[ra];
+      } else {
+        pbuf[n++] = combo == 2 ? g.road_fwd[rb] : g.road_rev[rb];   // entry edge (reversed order)
+        uint32_t x = combo == 2 ? g.road_node0[rb] : g.road_node1[rb];
+        for (;;) {
+          const int hx = h_find(sm, x);
+          if (hx < 0 || n + 2 > (uint32_t)H) { atomicOr(&b.ctl[2], kErrRounds); n = 0; break; }
+          const unsigned long long lx = sm.lab[hx];
+          if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
+          const uint32_t e = sm.pred[hx];
+          if (e == kNone) { atomicOr(&b.ctl[2], kErrRounds); n = 0; break; }
+          pbuf[n++] = e;
+          x = g.edge_src[e];
+        }
+        if (n) pbuf[n++] = (x == n1a) ? g.road_fwd[ra] : g.road_rev[ra];  // exit edge
+      }
+      uint32_t at = 0;
+      if (n > (uint32_t)kInlinePath) {
+        at = atomicAdd(&b.ctl[0], n);
+        if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); at = kNone; }
+      }
+      b.path_cnt[p] = n;
+      b.path_off[p] = at;
+      b.route_dist[p] = key_dist(key);
+      sm.nf = n;
+      sm.nn = at;
+    }
+    __syncthreads();
+    {
+      const uint32_t n = sm.nf, at = sm.nn;
+      uint32_t* dst = n <= (uint32_t)kInlinePath ? b.path_inline + p * kInlinePath : (at == kNone ? nullptr : b.path_pool + at);
+      if (dst)
+        for (uint32_t q = lane; q < n; q += kWave) dst[q] = pbuf[n - 1 - q];
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K4 k_segments: one lane per trace.  Streams traversals of each chain, merges pieces that
+// continue through a state point, and forms OSMLR runs (meili form_segments analogue).
+struct Trav { uint32_t e, b, en; double tb, te; uint32_t sb, se; };
+
+struct RunState {
+  bool open;
+  uint32_t sd, f_e, f_b, l_e, l_en, sb, se, way_first, way_last;
+  bool internal;
+  double tb, te;
+  uint64_t tot, q;
+};
+
+__device__ __forceinline__ void run_close(const DevGraph& g, RunState& R, SegmentRec* out, uint32_t& n) {
+  if (!R.open) return;
+  const uint32_t sd = R.sd;
+  const uint32_t llen = g.edges[R.l_e].y;
+  const bool start_ok = R.f_b == 0 && (sd == kNone || g.edge_seg_off[R.f_e] == 0);
+  const bool end_ok = R.l_en == llen && (sd == kNone || g.edge_seg_off[R.l_e] + llen == g.seg_len[sd]);
+  SegmentRec s;
+  s.segment_id = sd == kNone ? kInvalidSegmentId : g.seg_id[sd];
+  s.start_time = start_ok ? R.tb : -1.0;
+  s.end_time = end_ok ? R.te : -1.0;
+  if (sd != kNone) s.length = (start_ok && end_ok) ? (int32_t)((g.seg_len[sd] + 50u) / 100u) : -1;
+  else s.length = (int32_t)((R.tot + 50u) / 100u);
+  s.queue_length = (int32_t)((R.q + 50u) / 100u);
+  s.flags = (sd == kNone && R.internal ? 1u : 0u) | (sd != kNone ? 2u : 0u);
+  s.begin_shape_index = R.sb;
+  s.end_shape_index = R.se;
+  s.seg_dense = sd;
+  s.way_first = R.way_first;
+  s.way_last = R.way_last;
+  out[n++] = s;
+  R.open = false;
+}
+
+__device__ __forceinline__ void run_feed(const DevGraph& g, RunState& R, const Trav& t, SegmentRec* out, uint32_t& n) {
+  const uint32_t sd = g.edge_seg[t.e];
+  const uint4 rec = g.edges[t.e];
+  const bool internal = (rec.z & kFlagInternal) != 0u;
+  bool cont = R.open && sd == R.sd;
+  if (cont && sd == kNone && internal != R.internal) cont = false;
+  if (cont) {
+    const uint32_t plen = g.edges[R.l_e].y;
+    if (R.l_en != plen || t.b != 0) cont = false;
+    else if (sd != kNone && g.edge_seg_off[t.e] != g.edge_seg_off[R.l_e] + plen) cont = false;
+  }
+  const uint32_t d = t.en - t.b;
+  const double dt = t.te - t.tb;
+  const bool slow = dt > 0.0 && ((double)d * 0.01) / dt < kQueueSpeedMps;
+  const uint32_t way = g.edge_way[t.e];
+  if (!cont) {
+    run_close(g, R, out, n);
+    R.open = true; R.sd = sd; R.internal = internal;
+    R.f_e = t.e; R.f_b = t.b; R.tb = t.tb; R.sb = t.sb;
+    R.tot = 0; R.q = 0; R.way_first = way; R.way_last = way;
+  } else if (way != R.way_first) {
+    R.way_last = way;
+  }
+  R.l_e = t.e; R.l_en = t.en; R.te = t.te; R.se = t.se;
+  R.tot += d;
+  R.q = slow ? R.q + d : 0;
+}
+
+__device__ __forceinline__ double interp_time(double ta, double tb, uint64_t x, uint64_t D) {
+  if (D == 0) return ta;
+  return ta + (tb - ta) * ((double)x / (double)D);
+}
+
+// upper bound of segments per trace (one per path edge) -> exclusive scan -> seg_base
+__global__ void __launch_bounds__(64) k_seg_bound(DevBatch b) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= b.T) return;
+  const uint32_t o = b.trace_off[k], S = b.n_states[k];
+  uint32_t bound = 0;
+  for (uint32_t s = 1; s < S; ++s) {
+    const uint64_t l = o + s;
+    if (!b.chain_start[l] && b.choice[l] >= 0) bound += b.path_cnt[l];
+  }
+  b.seg_cnt[k] = bound;
+}
+
+__global__ void __launch_bounds__(64) k_segments(DevGraph g, DevBatch b) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= b.T) return;
+  const uint32_t o = b.trace_off[k], S = b.n_states[k];
+  SegmentRec* out = b.segs + b.seg_base[k];
+  uint32_t n = 0;
+  RunState R;
+  R.open = false;
+  Trav pend;
+  bool has_pend = false;
+  for (uint32_t s = 0; s < S; ++s) {
+    const uint64_t l = o + s;
+    if (b.chain_start[l] || b.choice[l] < 0) {
+      if (has_pend) { run_feed(g, R, pend, out, n); has_pend = false; }
+      run_close(g, R, out, n);
+      continue;
+    }
+    const uint32_t i = (uint32_t)b.choice[l - 1], j = (uint32_t)b.choice[l];
+    const uint32_t sa = b.cand_s[(l - 1) * kMaxCand + i], sb = b.cand_s[l * kMaxCand + j];
+    const uint32_t oa = b.state_orig[l - 1], ob = b.state_orig[l];
+    const double ta = b.time[o + oa], tb = b.time[o + ob];
+    const uint32_t D = b.route_dist[l];
+    const uint32_t ns = b.path_cnt[l];
+    const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
+    uint64_t x = 0;
+    for (uint32_t q = 0; q < ns; ++q) {
+      const uint32_t e = pe[q];
+      const uint4 rec = g.edges[e];
+      const uint32_t L = rec.y;
+      const bool rev = (rec.w & 1u) != 0u;
+      uint32_t b0 = 0, b1 = L;
+      if (q == 0) b0 = rev ? L - sa : sa;
+      if (q + 1 == ns) b1 = rev ? L - sb : sb;
+      Trav t;
+      t.e = e; t.b = b0; t.en = b1;
+      t.tb = interp_time(ta, tb, x, D);
+      x += (uint64_t)(b1 - b0);
+      t.te = interp_time(ta, tb, x, D);
+      t.sb = oa;
+      t.se = (q + 1 == ns) ? ob : oa;
+      if (t.en == t.b) continue;
+      if (has_pend && pend.e == t.e && pend.en == t.b) { pend.en = t.en; pend.te = t.te; pend.se = t.se; continue; }
+      if (has_pend) run_feed(g, R, pend, out, n);
+      pend = t;
+      has_pend = true;
+    }
+  }
+  if (has_pend) run_feed(g, R, pend, out, n);
+  run_close(g, R, out, n);
+  b.seg_cnt[k] = n;
+}
+
+// ------------------------------------------------------------------------------------------
+// A8 k_report: reference report() per trace (py/reporter_service.py:79-179) + the batch
+// filter (py/simple_reporter.py:177) + per-segment 10 km/h speed histogram.
+__global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uint32_t rmask, uint32_t tmask,
+                                               uint32_t* hist) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= b.T) return;
+  const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
+  const SegmentRec* segs = b.segs + b.seg_base[k];
+  const uint32_t n = b.seg_cnt[k];
+  ReportRec* out = b.reps + b.seg_base[k];
+  ReportStats st;
+  st.successful_count = st.unreported_count = 0;
+  st.successful_length_m = st.unreported_length_m = -1;
+  st.discontinuities = st.invalid_speeds = st.invalid_times = st.unassociated = 0;
+  st.shape_used = -1;
+  int nrep = 0;
+  if (npts > 0) {
+    const double end_time = b.time[o + npts - 1];
+    int last = (int)n - 1;
+    while (last >= 0 && end_time - segs[last].start_time < threshold) --last;
+    if (last >= 0 && segs[last].begin_shape_index != 0) st.shape_used = (int32_t)segs[last].begin_shape_index;
+    bool have_prior = false, p_has_id = false;
+    uint64_t p_id = 0; double p_t0 = 0, p_t1 = 0; int32_t p_len = 0, p_q = 0; int p_lvl = -1; uint32_t p_dense = kNone;
+    for (int q = 0; q <= last; ++q) {
+      const SegmentRec& s = segs[q];
+      const bool has_id = (s.flags & 2u) != 0u, internal = (s.flags & 1u) != 0u;
+      if (q != 0 && s.start_time == -1.0 && segs[q - 1].end_time == -1.0) st.discontinuities++;
+      const int lvl = has_id ? (int)(s.segment_id & 7ull) : -1;
+      if (have_prior && p_has_id && p_len > 0 && !internal) {
+        if (p_lvl >= 0 && ((rmask >> (p_lvl + 1)) & 1u)) {
+          const bool to_next = ((tmask >> (lvl + 1)) & 1u) != 0u;
+          ReportRec r;
+          r.id = p_id; r.t0 = p_t0; r.t1 = to_next ? s.start_time : p_t1;
+          r.length = p_len; r.queue_length = p_q; r.seg_dense = p_dense; r.pad = 0;
+          r.next_id = (to_next && has_id) ? s.segment_id : kInvalidSegmentId;
+          const double dt = r.t1 - r.t0;
+          if (dt <= 0 || isinf(dt) || isnan(dt)) st.invalid_times++;
+          else if (((double)p_len / dt) * 3.6 > 160.0) st.invalid_speeds++;
+          else {
+            out[nrep++] = r;
+            st.successful_count++;
+            st.successful_length_m = p_len;
+            if (hist && r.t0 > 0 && r.t1 > 0 && dt > 0.5 && r.length > 0 && r.queue_length >= 0 && p_dense != kNone) {
+              int bin = (int)(((double)r.length / dt) * 3.6 / 10.0);
+              bin = bin > kHistBins - 1 ? kHistBins - 1 : (bin < 0 ? 0 : bin);
+              atomicAdd(&hist[(uint64_t)p_dense * kHistBins + (uint32_t)bin], 1u);
+            }
+          }
+        } else {
+          st.unreported_count++;
+          st.unreported_length_m = p_len;
+        }
+      }
+      if (!(internal && q != 0)) {
+        have_prior = true; p_has_id = has_id; p_id = s.segment_id; p_t0 = s.start_time; p_t1 = s.end_time;
+        p_len = s.length; p_q = s.queue_length; p_lvl = lvl; p_dense = s.seg_dense;
+      }
+      if (!has_id && !internal) st.unassociated++;
+    }
+  }
+  st.n_reports = nrep;
+  b.rep_cnt[k] = (uint32_t)nrep;
+  b.stats[k] = st;
+}
+
+__global__ void k_fill_edge_src(const uint32_t* node_off, uint32_t n_nodes, uint32_t* edge_src) {
+  const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes) return;
+  for (uint32_t e = node_off[n]; e < node_off[n + 1]; ++e) edge_src[e] = n;
+}
+
+template <class T>
+T* dalloc(std::vector<void*>& list, uint64_t n) {
+  void* p = nullptr;
+  if (n == 0) n = 1;
+  RM_HIP(hipMalloc(&p, n * sizeof(T)));
+  list.push_back(p);
+  return (T*)p;
+}
+
+template <class T>
+T* upload(std::vector<void*>& list, const std::vector<T>& v) {
+  T* p = dalloc<T>(list, v.size());
+  if (!v.empty()) RM_HIP(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return p;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// Engine
+
+Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
+  RM_HIP(hipSetDevice(device));
+  if (g.num_nodes() >= (1u << 28)) throw std::runtime_error("graph has too many nodes (limit 2^28)");
+  dg_.node_off = upload(allocs_, g.node_off);
+  dg_.edges = (const uint4*)upload(allocs_, g.edges);
+  uint32_t* esrc = dalloc<uint32_t>(allocs_, g.num_edges());
+  dg_.edge_src = esrc;
+  dg_.edge_seg = upload(allocs_, g.edge_seg);
+  dg_.edge_seg_off = upload(allocs_, g.edge_seg_off);
+  dg_.edge_way = upload(allocs_, g.edge_way);
+  dg_.road_node0 = upload(allocs_, g.road_node0);
+  dg_.road_node1 = upload(allocs_, g.road_node1);
+  dg_.road_fwd = upload(allocs_, g.road_fwd);
+  dg_.road_rev = upload(allocs_, g.road_rev);
+  dg_.road_len = upload(allocs_, g.road_len_cm);
+  dg_.verts = (const uint4*)upload(allocs_, g.verts);
+  dg_.seg_id = (const unsigned long long*)upload(allocs_, g.seg_id);
+  dg_.seg_len = upload(allocs_, g.seg_len_cm);
+  dg_.cell_off = upload(allocs_, g.grid.cell_off);
+  dg_.cell_item = upload(allocs_, g.grid.cell_item);
+  dg_.lon0 = g.grid.lon0; dg_.lat0 = g.grid.lat0; dg_.dlon = g.grid.dlon; dg_.dlat = g.grid.dlat;
+  dg_.ncx = g.grid.ncx; dg_.ncy = g.grid.ncy;
+  dg_.n_nodes = g.num_nodes(); dg_.n_edges = g.num_edges(); dg_.n_segments = g.num_segments();
+  if (g.num_nodes()) {
+    hipLaunchKernelGGL(k_fill_edge_src, dim3((g.num_nodes() + 255) / 256), dim3(256), 0, 0, dg_.node_off,
+                       g.num_nodes(), esrc);
+    RM_HIP(hipGetLastError());
+  }
+  RM_HIP(hipDeviceSynchronize());
+}
+
+Engine::~Engine() {
+  (void)hipSetDevice(device_);
+  for (void* p : allocs_) (void)hipFree(p);
+}
+
+// ==========================================================================================
+// Workspace / Matcher
+
+Workspace::~Workspace() { release(); }
+void Workspace::release() {
+  for (void* p : allocs) (void)hipFree(p);
+  allocs.clear();
+  cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = 0;
+}
+
+Matcher::Matcher(Engine* e) : eng_(e) {
+  RM_HIP(hipSetDevice(e->device()));
+  RM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+}
+
+Matcher::~Matcher() {
+  (void)hipSetDevice(eng_->device());
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  for (auto& ev : pending_) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
+  for (auto& ev : free_ev_) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
+  ws_.release();
+  if (stream_) (void)hipStreamDestroy(stream_);
+  if (hctl_) (void)hipHostFree(hctl_);
+}
+
+void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
+  Workspace& w = ws_;
+  if (points <= w.cap_points && traces <= w.cap_traces && nopts <= w.cap_opts && w.ctl) return;
+  // grow everything sized by points/traces (trans/path pools are grown separately)
+  const uint64_t cp = std::max<uint64_t>(points, w.cap_points) + 64;
+  const uint64_t ct = std::max<uint64_t>(traces, w.cap_traces) + 16;
+  const uint64_t co = std::max<uint64_t>(nopts, w.cap_opts) + 4;
+  const uint64_t keep_trans = w.cap_trans, keep_path = w.cap_path, keep_segs = w.cap_segs;
+  w.release();
+  std::vector<void*>& L = w.allocs;
+  w.trace_off = dalloc<uint32_t>(L, ct + 1);
+  w.lon = dalloc<float>(L, cp); w.lat = dalloc<float>(L, cp); w.time = dalloc<double>(L, cp);
+  w.acc = dalloc<float>(L, cp); w.opts = dalloc<MatchOptions>(L, co); w.trace_opt = dalloc<uint32_t>(L, ct);
+  w.slot_trace = dalloc<uint32_t>(L, cp); w.n_states = dalloc<uint32_t>(L, ct); w.state_orig = dalloc<uint32_t>(L, cp);
+  w.cand_n = dalloc<uint8_t>(L, cp); w.cand_road = dalloc<uint32_t>(L, cp * kMaxCand);
+  w.cand_s = dalloc<uint32_t>(L, cp * kMaxCand); w.cand_sq = dalloc<float>(L, cp * kMaxCand);
+  w.trans_cnt = dalloc<uint32_t>(L, cp); w.trans_off = dalloc<uint32_t>(L, cp); w.gc = dalloc<double>(L, cp);
+  w.choice = dalloc<int8_t>(L, cp); w.chain_start = dalloc<uint8_t>(L, cp); w.bp = dalloc<uint8_t>(L, cp * kMaxCand);
+  w.path_off = dalloc<uint32_t>(L, cp); w.path_cnt = dalloc<uint32_t>(L, cp); w.route_dist = dalloc<uint32_t>(L, cp);
+  w.path_inline = dalloc<uint32_t>(L, cp * kInlinePath);
+  w.seg_base = dalloc<uint32_t>(L, ct); w.seg_cnt = dalloc<uint32_t>(L, ct);
+  w.rep_cnt = dalloc<uint32_t>(L, ct); w.stats = dalloc<ReportStats>(L, ct);
+  w.ctl = dalloc<uint32_t>(L, 8);
+  w.retry_routes = dalloc<uint32_t>(L, cp); w.retry_paths = dalloc<uint32_t>(L, cp);
+  size_t tmp = 0;
+  RM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, w.trans_cnt, w.trans_off, (int)cp, stream_));
+  w.scan_tmp_bytes = tmp;
+  w.scan_tmp = dalloc<char>(L, tmp);
+  w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
+  w.route = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr;
+  w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0;
+  ensure_trans(std::max<uint64_t>(keep_trans, 1));
+  ensure_path(std::max<uint64_t>(keep_path, cp / 8 + 1024));
+  ensure_segs(std::max<uint64_t>(keep_segs, cp / 2 + 1024));
+}
+
+void Matcher::ensure_trans(uint64_t n) {
+  Workspace& w = ws_;
+  if (n <= w.cap_trans && w.route) return;
+  if (w.route) { (void)hipFree(w.route); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.route)); }
+  const uint64_t c = n + n / 4 + 1024;
+  w.route = dalloc<uint32_t>(w.allocs, c);
+  w.cap_trans = c;
+}
+
+static void free_one(Workspace& w, void* q) {
+  if (!q) return;
+  (void)hipFree(q);
+  w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), q));
+}
+
+void Matcher::ensure_path(uint64_t n) {
+  Workspace& w = ws_;
+  if (n <= w.cap_path && w.path_pool) return;
+  free_one(w, w.path_pool);
+  const uint64_t c = n + n / 4 + 1024;
+  w.path_pool = dalloc<uint32_t>(w.allocs, c);
+  w.cap_path = c;
+}
+
+void Matcher::ensure_segs(uint64_t n) {
+  Workspace& w = ws_;
+  if (n <= w.cap_segs && w.segs) return;
+  free_one(w, w.segs);
+  free_one(w, w.reps);
+  const uint64_t c = n + n / 4 + 1024;
+  w.segs = dalloc<SegmentRec>(w.allocs, c);
+  w.reps = dalloc<ReportRec>(w.allocs, c);
+  w.cap_segs = c;
+}
+
+void Matcher::tic(int k) {
+  if (!timing_) return;
+  Ev ev;
+  if (!free_ev_.empty()) { ev = free_ev_.back(); free_ev_.pop_back(); }
+  else { RM_HIP(hipEventCreate(&ev.a)); RM_HIP(hipEventCreate(&ev.b)); }
+  ev.k = k;
+  RM_HIP(hipEventRecord(ev.a, stream_));
+  pending_.push_back(ev);
+}
+void Matcher::toc(int k) {
+  if (!timing_ || pending_.empty()) return;
+  (void)k;
+  RM_HIP(hipEventRecord(pending_.back().b, stream_));
+}
+void Matcher::harvest_times() {
+  for (auto& ev : pending_) {
+    float ms = 0.f;
+    RM_HIP(hipEventElapsedTime(&ms, ev.a, ev.b));
+    kms_[ev.k] += ms;
+    klaunch_[ev.k] += 1;
+    free_ev_.push_back(ev);
+  }
+  pending_.clear();
+}
+void Matcher::kernel_times(double* ms, uint64_t* launches) {
+  for (int i = 0; i < kNumKernels; ++i) { ms[i] = kms_[i]; if (launches) launches[i] = klaunch_[i]; }
+}
+void Matcher::reset_kernel_times() {
+  for (int i = 0; i < kNumKernels; ++i) { kms_[i] = 0; klaunch_[i] = 0; }
+}
+
+void Matcher::sync() {
+  RM_HIP(hipStreamSynchronize(stream_));
+  harvest_times();
+}
+
+static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
+  DevBatch v;
+  v.T = T; v.P = P;
+  v.trace_off = w.trace_off; v.lon = w.lon; v.lat = w.lat; v.time = w.time; v.acc = w.acc;
+  v.opts = w.opts; v.trace_opt = w.trace_opt;
+  v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig;
+  v.cand_n = w.cand_n; v.cand_road = w.cand_road; v.cand_s = w.cand_s; v.cand_sq = w.cand_sq;
+  v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route;
+  v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
+  v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
+  v.path_pool = w.path_pool; v.path_cap = w.cap_path;
+  v.route_dist = w.route_dist;
+  v.segs = w.segs; v.seg_base = w.seg_base; v.seg_cnt = w.seg_cnt;
+  v.reps = w.reps; v.rep_cnt = w.rep_cnt; v.stats = w.stats;
+  v.ctl = w.ctl; v.retry_routes = w.retry_routes; v.retry_paths = w.retry_paths;
+  return v;
+}
+
+void Matcher::run(const HostBatch& hb, const RunParams& rp) {
+  RM_HIP(hipSetDevice(eng_->device()));
+  const uint32_t T = hb.n_traces;
+  if (T == 0) { n_traces_ = 0; n_points_ = 0; n_trans_ = 0; n_path_ = 0; seg_used_ = 0; return; }
+  const uint64_t P = hb.trace_off[T];
+  if (P >= 0xffffffffull) throw std::runtime_error("batch too large (points >= 2^32)");
+  for (uint32_t k = 0; k < T; ++k) {
+    if (hb.trace_off[k + 1] < hb.trace_off[k]) throw std::runtime_error("trace offsets not monotone");
+    if (hb.trace_opt[k] >= hb.n_opts) throw std::runtime_error("trace option index out of range");
+  }
+  for (uint32_t q = 0; q < hb.n_opts; ++q)
+    if (hb.opts[q].mode < 0 || hb.opts[q].mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+  ensure(P, T, hb.n_opts);
+  Workspace& w = ws_;
+  hipStream_t st = stream_;
+  RM_HIP(hipMemcpyAsync(w.trace_off, hb.trace_off, (T + 1) * 4ull, hipMemcpyHostToDevice, st));
+  RM_HIP(hipMemcpyAsync(w.lon, hb.lon, P * 4, hipMemcpyHostToDevice, st));
+  RM_HIP(hipMemcpyAsync(w.lat, hb.lat, P * 4, hipMemcpyHostToDevice, st));
+  RM_HIP(hipMemcpyAsync(w.time, hb.time, P * 8, hipMemcpyHostToDevice, st));
+  RM_HIP(hipMemcpyAsync(w.acc, hb.accuracy, P * 4, hipMemcpyHostToDevice, st));
+  RM_HIP(hipMemcpyAsync(w.opts, hb.opts, hb.n_opts * sizeof(MatchOptions), hipMemcpyHostToDevice, st));
+  RM_HIP(hipMemcpyAsync(w.trace_opt, hb.trace_opt, T * 4ull, hipMemcpyHostToDevice, st));
+  n_traces_ = T;
+  n_points_ = P;
+  run_device(rp);
+}
+
+void Matcher::run_device(const RunParams& rp) {
+  RM_HIP(hipSetDevice(eng_->device()));
+  const uint32_t T = n_traces_;
+  const uint64_t P = n_points_;
+  if (T == 0) return;
+  Workspace& w = ws_;
+  hipStream_t st = stream_;
+  const DevGraph& g = eng_->dev();
+  if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 16 * sizeof(uint32_t), hipHostMallocDefault));
+  RM_HIP(hipMemsetAsync(w.ctl, 0, 8 * sizeof(uint32_t), st));
+  RM_HIP(hipMemsetAsync(w.choice, 0xff, P, st));
+  DevBatch v = make_view(w, T, P);
+
+  tic(kKStates);
+  hipLaunchKernelGGL(k_states, dim3((T + 63) / 64), dim3(64), 0, st, v);
+  toc(kKStates);
+  tic(kKCandidates);
+  hipLaunchKernelGGL(k_candidates, dim3((uint32_t)P), dim3(64), 0, st, g, v);
+  toc(kKCandidates);
+  tic(kKScan);
+  hipLaunchKernelGGL(k_trans_count, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
+  size_t tmp = w.scan_tmp_bytes;
+  RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.trans_cnt, w.trans_off, (int)P, st));
+  toc(kKScan);
+  RM_HIP(hipMemcpyAsync(hctl_ + 8, w.trans_off + (P - 1), 4, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipMemcpyAsync(hctl_ + 9, w.trans_cnt + (P - 1), 4, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipStreamSynchronize(st));
+  const uint64_t total = (uint64_t)hctl_[8] + hctl_[9];
+  if (total >= 0xffffffffull) throw std::runtime_error("batch too large (transitions >= 2^32); split it");
+  n_trans_ = total;
+  ensure_trans(total);
+  v.route = w.route;
+
+  tic(kKRoutes);
+  hipLaunchKernelGGL(k_routes<false>, dim3((uint32_t)P), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes<true>, dim3(1024), dim3(64), 0, st, g, v);
+  toc(kKRoutes);
+  tic(kKViterbi);
+  hipLaunchKernelGGL(k_viterbi, dim3((T + 3) / 4), dim3(64), 0, st, v);
+  toc(kKViterbi);
+  for (int attempt = 0;; ++attempt) {
+    tic(kKPaths);
+    hipLaunchKernelGGL(k_paths<false>, dim3((uint32_t)P), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths<true>, dim3(1024), dim3(64), 0, st, g, v);
+    toc(kKPaths);
+    RM_HIP(hipMemcpyAsync(hctl_, w.ctl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    RM_HIP(hipStreamSynchronize(st));
+    if (!(hctl_[2] & kErrPathOverflow)) break;
+    if (attempt > 3) throw std::runtime_error("path pool overflow persists");
+    ensure_path((uint64_t)hctl_[0]);
+    v.path_pool = w.path_pool; v.path_cap = w.cap_path;
+    const uint32_t clear_bits = ~kErrPathOverflow;
+    (void)clear_bits;
+    RM_HIP(hipMemsetAsync(w.ctl, 0, sizeof(uint32_t), st));          // path_used
+    RM_HIP(hipMemsetAsync(w.ctl + 4, 0, sizeof(uint32_t), st));      // retry count (paths)
+    uint32_t flags = hctl_[2] & ~kErrPathOverflow;
+    RM_HIP(hipMemcpyAsync(w.ctl + 2, &flags, sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    RM_HIP(hipStreamSynchronize(st));
+  }
+  tic(kKSegments);
+  hipLaunchKernelGGL(k_seg_bound, dim3((T + 63) / 64), dim3(64), 0, st, v);
+  tmp = w.scan_tmp_bytes;
+  RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.seg_cnt, w.seg_base, (int)T, st));
+  RM_HIP(hipMemcpyAsync(hctl_ + 10, w.seg_base + (T - 1), 4, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipMemcpyAsync(hctl_ + 11, w.seg_cnt + (T - 1), 4, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipStreamSynchronize(st));
+  const uint64_t seg_total = (uint64_t)hctl_[10] + hctl_[11];
+  n_path_ = seg_total;  // one segment slot per chained path edge
+  ensure_segs(seg_total);
+  v.segs = w.segs; v.reps = w.reps;
+  hipLaunchKernelGGL(k_segments, dim3((T + 63) / 64), dim3(64), 0, st, g, v);
+  toc(kKSegments);
+  if (rp.do_report) {
+    tic(kKReport);
+    hipLaunchKernelGGL(k_report, dim3((T + 63) / 64), dim3(64), 0, st, v, rp.threshold_sec, rp.report_mask,
+                       rp.transition_mask, rp.hist);
+    toc(kKReport);
+  }
+  RM_HIP(hipGetLastError());
+  RM_HIP(hipMemcpyAsync(hctl_, w.ctl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  sync();
+  seg_used_ = seg_total;
+  const uint32_t err = hctl_[2];
+  if (err & kErrCandOverflow) throw std::runtime_error("too many candidate roads inside the search radius (limit 192)");
+  if (err & kErrSearchOverflow) throw std::runtime_error("route search exceeded its label capacity (bound too large for this graph)");
+  if (err & kErrRounds) throw std::runtime_error("route search did not converge / path reconstruction failed");
+  has_report_ = rp.do_report != 0;
+}
+
+// ---- downloads ----
+void Matcher::get_states(uint32_t* n_states, uint32_t* state_orig) {
+  sync();
+  RM_HIP(hipMemcpy(n_states, ws_.n_states, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(state_orig, ws_.state_orig, n_points_ * 4, hipMemcpyDeviceToHost));
+}
+void Matcher::get_candidates(uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq) {
+  sync();
+  RM_HIP(hipMemcpy(cand_n, ws_.cand_n, n_points_, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(road, ws_.cand_road, n_points_ * kMaxCand * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(s_cm, ws_.cand_s, n_points_ * kMaxCand * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(sq, ws_.cand_sq, n_points_ * kMaxCand * 4, hipMemcpyDeviceToHost));
+}
+void Matcher::get_routes(uint32_t* trans_off, double* gc, uint32_t* route) {
+  sync();
+  RM_HIP(hipMemcpy(trans_off, ws_.trans_off, n_points_ * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(gc, ws_.gc, n_points_ * 8, hipMemcpyDeviceToHost));
+  if (n_trans_) RM_HIP(hipMemcpy(route, ws_.route, n_trans_ * 4, hipMemcpyDeviceToHost));
+}
+void Matcher::get_viterbi(int8_t* choice, uint8_t* chain_start) {
+  sync();
+  RM_HIP(hipMemcpy(choice, ws_.choice, n_points_, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(chain_start, ws_.chain_start, n_points_, hipMemcpyDeviceToHost));
+}
+void Matcher::get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, uint32_t* route_dist) {
+  // device layout: short paths inline per slot, long ones in the pool; returned compacted in slot order
+  sync();
+  const uint64_t P = n_points_;
+  std::vector<uint32_t> off(P), inl(P * kInlinePath), used(1, 0);
+  RM_HIP(hipMemcpy(off.data(), ws_.path_off, P * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(path_cnt, ws_.path_cnt, P * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(inl.data(), ws_.path_inline, P * kInlinePath * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(route_dist, ws_.route_dist, P * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(used.data(), ws_.ctl, 4, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> dpool(used[0]);
+  if (used[0]) RM_HIP(hipMemcpy(dpool.data(), ws_.path_pool, used[0] * 4ull, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> choice_ok(P, 0);
+  {
+    std::vector<int8_t> ch(P);
+    std::vector<uint8_t> cs(P);
+    RM_HIP(hipMemcpy(ch.data(), ws_.choice, P, hipMemcpyDeviceToHost));
+    RM_HIP(hipMemcpy(cs.data(), ws_.chain_start, P, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> tro(n_traces_ + 1), ns(n_traces_);
+    RM_HIP(hipMemcpy(tro.data(), ws_.trace_off, (n_traces_ + 1) * 4ull, hipMemcpyDeviceToHost));
+    RM_HIP(hipMemcpy(ns.data(), ws_.n_states, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < n_traces_; ++k)
+      for (uint32_t s = 1; s < ns[k]; ++s) {
+        const uint64_t l = tro[k] + s;
+        choice_ok[l] = (!cs[l] && ch[l] >= 0) ? 1u : 0u;
+      }
+  }
+  uint64_t at = 0;
+  for (uint64_t p = 0; p < P; ++p) {
+    if (!choice_ok[p]) { path_off[p] = (uint32_t)at; path_cnt[p] = 0; continue; }
+    const uint32_t n = path_cnt[p];
+    path_off[p] = (uint32_t)at;
+    const uint32_t* src = n <= (uint32_t)kInlinePath ? inl.data() + p * kInlinePath : dpool.data() + off[p];
+    std::memcpy(pool + at, src, n * 4ull);
+    at += n;
+  }
+}
+
+uint64_t Matcher::count_segments() {
+  sync();
+  std::vector<uint32_t> cnt(n_traces_);
+  if (n_traces_) RM_HIP(hipMemcpy(cnt.data(), ws_.seg_cnt, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+  uint64_t t = 0;
+  for (uint32_t c : cnt) t += c;
+  return t;
+}
+void Matcher::get_segments(uint32_t* seg_off, SegmentRec* segs) {
+  sync();
+  std::vector<uint32_t> base(n_traces_), cnt(n_traces_);
+  if (!n_traces_) { seg_off[0] = 0; return; }
+  RM_HIP(hipMemcpy(base.data(), ws_.seg_base, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(cnt.data(), ws_.seg_cnt, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+  std::vector<SegmentRec> pool(seg_used_);
+  if (seg_used_) RM_HIP(hipMemcpy(pool.data(), ws_.segs, seg_used_ * sizeof(SegmentRec), hipMemcpyDeviceToHost));
+  uint64_t at = 0;
+  for (uint32_t k = 0; k < n_traces_; ++k) {
+    seg_off[k] = (uint32_t)at;
+    if (cnt[k]) std::memcpy(segs + at, pool.data() + base[k], cnt[k] * sizeof(SegmentRec));
+    at += cnt[k];
+  }
+  seg_off[n_traces_] = (uint32_t)at;
+}
+uint64_t Matcher::count_reports() {
+  sync();
+  if (!has_report_) return 0;
+  std::vector<uint32_t> cnt(n_traces_);
+  if (n_traces_) RM_HIP(hipMemcpy(cnt.data(), ws_.rep_cnt, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+  uint64_t t = 0;
+  for (uint32_t c : cnt) t += c;
+  return t;
+}
+void Matcher::get_reports(uint32_t* rep_off, ReportRec* reps, ReportStats* stats) {
+  sync();
+  if (!has_report_) throw std::runtime_error("the last run did not compute reports");
+  if (!n_traces_) { rep_off[0] = 0; return; }
+  std::vector<uint32_t> base(n_traces_), cnt(n_traces_);
+  RM_HIP(hipMemcpy(base.data(), ws_.seg_base, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(cnt.data(), ws_.rep_cnt, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(stats, ws_.stats, n_traces_ * sizeof(ReportStats), hipMemcpyDeviceToHost));
+  std::vector<ReportRec> pool(seg_used_);
+  if (seg_used_) RM_HIP(hipMemcpy(pool.data(), ws_.reps, seg_used_ * sizeof(ReportRec), hipMemcpyDeviceToHost));
+  uint64_t at = 0;
+  for (uint32_t k = 0; k < n_traces_; ++k) {
+    rep_off[k] = (uint32_t)at;
+    if (cnt[k]) std::memcpy(reps + at, pool.data() + base[k], cnt[k] * sizeof(ReportRec));
+    at += cnt[k];
+  }
+  rep_off[n_traces_] = (uint32_t)at;
+}
+
+}  // namespace rm

@@ -1,0 +1,183 @@
+// engine.hpp — MI355X map-matching engine: the graph resident in HBM and the
+// per-batch device workspace that the gfx950 kernels (engine.hip) run over.
+//
+// One Engine per process/GPU holds the read-only graph.  Each Matcher (one per
+// calling thread, the threading contract of reference py/reporter_service.py:28-64)
+// owns a HIP stream and a grow-only Workspace, so distinct matchers run
+// concurrently without sharing mutable device state.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "graph.hpp"
+#include "rm_common.hpp"
+
+namespace rm {
+
+#define RM_HIP(x)                                                                                \
+  do {                                                                                           \
+    hipError_t _e = (x);                                                                         \
+    if (_e != hipSuccess)                                                                        \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " #x);   \
+  } while (0)
+
+struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
+  const uint32_t* node_off;
+  const uint4* edges;            // EdgeRec
+  const uint32_t* edge_src;      // source node of each directed edge
+  const uint32_t* edge_seg;
+  const uint32_t* edge_seg_off;
+  const uint32_t* edge_way;
+  const uint32_t* road_node0;
+  const uint32_t* road_node1;
+  const uint32_t* road_fwd;
+  const uint32_t* road_rev;
+  const uint32_t* road_len;
+  const uint4* verts;            // VertRec
+  const unsigned long long* seg_id;
+  const uint32_t* seg_len;
+  const uint32_t* cell_off;
+  const uint32_t* cell_item;
+  double lon0, lat0, dlon, dlat;
+  uint32_t ncx, ncy, n_nodes, n_edges, n_segments, pad;
+};
+
+// Host-side description of one batch of traces (arrays live in host memory).
+struct HostBatch {
+  uint32_t n_traces = 0;
+  const uint32_t* trace_off = nullptr;  // n_traces + 1
+  const float* lon = nullptr;
+  const float* lat = nullptr;
+  const double* time = nullptr;
+  const float* accuracy = nullptr;      // < 0 when absent
+  uint32_t n_opts = 0;
+  const MatchOptions* opts = nullptr;
+  const uint32_t* trace_opt = nullptr;  // per trace
+};
+
+struct RunParams {
+  double threshold_sec = 15.0;          // reporter_service.py:55-58
+  uint32_t report_mask = 0b0110;        // levels {0,1}: bit (level+1)
+  uint32_t transition_mask = 0b0110;
+  uint32_t* hist = nullptr;             // device, n_segments * 16 u32 (may be null)
+  int do_report = 1;
+};
+
+// Kernel ids for per-kernel HIP-event timing.
+enum KernelId { kKStates = 0, kKCandidates, kKScan, kKRoutes, kKViterbi, kKPaths, kKSegments, kKReport, kNumKernels };
+extern const char* const kKernelNames[kNumKernels];
+
+// Device workspace of one batch.  All arrays are indexed by point slot p
+// (state s of trace k lives at slot trace_off[k] + s).
+struct Workspace {
+  uint64_t cap_points = 0, cap_traces = 0, cap_trans = 0, cap_path = 0, cap_opts = 0, cap_segs = 0;
+  // inputs
+  uint32_t* trace_off = nullptr; float* lon = nullptr; float* lat = nullptr; double* time = nullptr;
+  float* acc = nullptr; MatchOptions* opts = nullptr; uint32_t* trace_opt = nullptr;
+  // per slot
+  uint32_t* slot_trace = nullptr; uint32_t* n_states = nullptr; uint32_t* state_orig = nullptr;
+  uint8_t* cand_n = nullptr; uint32_t* cand_road = nullptr; uint32_t* cand_s = nullptr; float* cand_sq = nullptr;
+  uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr;
+  int8_t* choice = nullptr; uint8_t* chain_start = nullptr; uint8_t* bp = nullptr;
+  uint32_t* path_off = nullptr; uint32_t* path_cnt = nullptr; uint32_t* path_pool = nullptr; uint32_t* route_dist = nullptr;
+  uint32_t* path_inline = nullptr;  // kInlinePath edges per slot
+  // per trace outputs
+  SegmentRec* segs = nullptr; uint32_t* seg_base = nullptr; uint32_t* seg_cnt = nullptr;
+  ReportRec* reps = nullptr; uint32_t* rep_cnt = nullptr; ReportStats* stats = nullptr;
+  // control words: [0] path_used [1] seg_used [2] error flags [3] retry count (routes)
+  // [4] retry count (paths) [5] cand overflow [6..7] spare
+  uint32_t* ctl = nullptr;
+  uint32_t* retry_routes = nullptr; uint32_t* retry_paths = nullptr;
+  void* scan_tmp = nullptr; size_t scan_tmp_bytes = 0;
+  std::vector<void*> allocs;
+  ~Workspace();
+  void release();
+};
+
+// error bits in ctl[2]
+constexpr uint32_t kErrCandOverflow = 1u, kErrSearchOverflow = 2u, kErrPathOverflow = 4u, kErrRounds = 8u;
+
+class Engine;
+
+class Matcher {
+ public:
+  explicit Matcher(Engine* e);
+  ~Matcher();
+  Matcher(const Matcher&) = delete;
+  Matcher& operator=(const Matcher&) = delete;
+
+  // Upload a batch and run every stage on this matcher's stream (asynchronous
+  // except for the two size read-backs).  Throws on error.
+  void run(const HostBatch& b, const RunParams& rp);
+  // Run every stage over the batch already resident in HBM (inputs of the last run()).
+  void run_device(const RunParams& rp);
+  void sync();
+  // sizes of the last run
+  uint32_t n_traces() const { return n_traces_; }
+  uint64_t n_points() const { return n_points_; }
+  uint64_t n_trans() const { return n_trans_; }
+  uint64_t n_path_edges() const { return n_path_; }
+  uint64_t seg_pool_used() const { return seg_used_; }
+  // downloads of the last run (host buffers sized by the caller)
+  void get_states(uint32_t* n_states, uint32_t* state_orig);
+  void get_candidates(uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
+  void get_routes(uint32_t* trans_off, double* gc, uint32_t* route);
+  void get_viterbi(int8_t* choice, uint8_t* chain_start);
+  void get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, uint32_t* route_dist);
+  // segments compacted per trace: seg_off (T+1), segs (seg_off[T])
+  void get_segments(uint32_t* seg_off, SegmentRec* segs);
+  uint64_t count_segments();
+  void get_reports(uint32_t* rep_off, ReportRec* reps, ReportStats* stats);
+  uint64_t count_reports();
+  // accumulated kernel time (ms) per KernelId since the last reset
+  void kernel_times(double* ms, uint64_t* launches);
+  void reset_kernel_times();
+  void set_timing(bool on) { timing_ = on; }
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  void ensure(uint64_t points, uint32_t traces, uint32_t nopts);
+  void ensure_trans(uint64_t n);
+  void ensure_path(uint64_t n);
+  void ensure_segs(uint64_t n);
+  void tic(int k);
+  void toc(int k);
+  void harvest_times();
+
+  Engine* eng_;
+  hipStream_t stream_ = nullptr;
+  Workspace ws_;
+  uint32_t n_traces_ = 0;
+  uint64_t n_points_ = 0, n_trans_ = 0, n_path_ = 0, seg_used_ = 0;
+  bool timing_ = false;
+  bool has_report_ = false;
+  uint32_t* hctl_ = nullptr;  // pinned host mirror of the control words
+  struct Ev { hipEvent_t a, b; int k; };
+  std::vector<Ev> pending_, free_ev_;
+  double kms_[kNumKernels] = {0};
+  uint64_t klaunch_[kNumKernels] = {0};
+};
+
+class Engine {
+ public:
+  Engine(const Graph& g, int device);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+  const DevGraph& dev() const { return dg_; }
+  int device() const { return device_; }
+  const Graph& host() const { return host_; }
+  uint32_t n_segments() const { return host_.num_segments(); }
+
+ private:
+  int device_;
+  Graph host_;
+  DevGraph dg_{};
+  std::vector<void*> allocs_;
+};
+
+}  // namespace rm

@@ -1,0 +1,94 @@
+// graph.hpp — host-side road graph: CSR of directed edges tagged with OSMLR
+// segment ids, road shapes, and a uniform spatial grid index.
+//
+// This is the engine's replacement for the Valhalla tile/graph layer the
+// reference reads through meili (tile hierarchy: reference py/get_tiles.py:30-39;
+// segment-id bit layout: py/simple_reporter.py:37-49).  The same arrays are
+// written to a flat binary file (".rmg") that the GPU runtime uploads to HBM
+// and that oracle/ reads as plain arrays.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+#include "rm_common.hpp"
+
+namespace rm {
+
+struct GridIndex {
+  double lon0 = 0, lat0 = 0, dlon = 1, dlat = 1;  // origin + cell size (degrees)
+  uint32_t ncx = 1, ncy = 1;
+  std::vector<uint32_t> cell_off;   // ncx*ncy + 1
+  std::vector<uint32_t> cell_item;  // vertex index of a shape segment's first vertex
+};
+
+struct Graph {
+  // nodes
+  std::vector<float> node_lon, node_lat;
+  std::vector<uint32_t> node_off;       // CSR offsets, size N+1
+  // directed edges (CSR order)
+  std::vector<EdgeRec> edges;
+  std::vector<uint32_t> edge_seg;       // dense OSMLR segment index or kNone
+  std::vector<uint32_t> edge_seg_off;   // cm from the segment's start to this edge's start
+  std::vector<uint32_t> edge_way;       // way id
+  // roads (undirected shape owners)
+  std::vector<uint32_t> road_node0, road_node1, road_fwd, road_rev, road_len_cm, road_vert_off;
+  // shape vertices
+  std::vector<VertRec> verts;
+  // OSMLR segments
+  std::vector<uint64_t> seg_id;
+  std::vector<uint32_t> seg_len_cm;
+  GridIndex grid;
+
+  uint32_t num_nodes() const { return (uint32_t)node_lon.size(); }
+  uint32_t num_edges() const { return (uint32_t)edges.size(); }
+  uint32_t num_roads() const { return (uint32_t)road_len_cm.size(); }
+  uint32_t num_verts() const { return (uint32_t)verts.size(); }
+  uint32_t num_segments() const { return (uint32_t)seg_id.size(); }
+
+  void save(const std::string& path) const;     // throws std::runtime_error
+  static Graph load(const std::string& path);   // throws std::runtime_error
+  void validate() const;                        // throws on a malformed graph
+};
+
+struct WorldParams {
+  uint32_t rows = 40, cols = 40;
+  double block_m = 100.0;
+  uint64_t seed = 1;
+  double center_lat = 47.0, center_lon = 8.0;
+  double jitter = 0.15;            // node jitter, fraction of a block
+  uint32_t arterial_every = 10;    // every 10th line is level 1
+  uint32_t highway_every = 40;     // every 40th line is level 0
+  double segment_max_m = 1000.0;   // OSMLR segments are chained up to this length
+  double internal_m = 15.0;        // internal edge length at major intersections
+  double service_frac = 0.05;      // local edges without OSMLR association
+  double oneway_frac = 0.10;       // local roads that are one-way for vehicles
+  double curve_frac = 0.30;        // roads given a curved mid vertex
+  double cell_m = 100.0;           // grid-index cell size
+};
+
+Graph build_world(const WorldParams& p);
+
+// Synthetic GPS traces (restating reference py/generate_test_trace.py:35-104,120-149):
+// a random drive on the graph at edge speed, resampled every `rate_s` seconds,
+// with the generator's correlated noise (first-quadrant lock + moving average).
+struct TraceParams {
+  uint32_t n_traces = 1, n_points = 100;
+  double rate_s = 1.0;
+  double noise_m = 5.0;
+  uint64_t seed = 1;
+  int32_t mode = kModeAuto;
+  int64_t start_epoch = 1483228800;  // fixed (replaces time.time()-86400 at line 60)
+  uint32_t threads = 0;              // 0 = hardware concurrency
+};
+
+struct TraceSet {
+  std::vector<double> lon, lat, time;   // 6-dp rounded degrees, epoch seconds
+  std::vector<float> accuracy;          // per point (generate_test_trace.py:40)
+  std::vector<uint32_t> trace_off;      // n_traces + 1
+  std::vector<uint32_t> truth_edge;     // directed edge under the true position
+  std::vector<uint32_t> truth_off_cm;   // offset along that edge
+};
+
+TraceSet generate_traces(const Graph& g, const TraceParams& p);
+
+}  // namespace rm

@@ -1,0 +1,176 @@
+// rm_common.hpp — constants, record layouts and deterministic math shared by
+// the host runtime and the gfx950 kernels of the reporter map-matching engine.
+//
+// The matcher replaces valhalla.SegmentMatcher().Match (called at
+// reference py/reporter_service.py:240 and py/simple_reporter.py:166).  Every
+// numeric rule below is part of the engine's written specification
+// (DESIGN.md §3); oracle/meili_oracle.c restates the same rules independently.
+//
+// Build rule: every translation unit is compiled with -ffp-contract=off and
+// without fast-math, so fp32/fp64 results are bit-identical between the host
+// oracle (gcc, SSE) and the device (hipcc, gfx950).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIP__) || defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RM_HD __host__ __device__ __forceinline__
+#else
+#define RM_HD static inline
+#endif
+
+namespace rm {
+
+// ---- id semantics (reference py/simple_reporter.py:37-49, Segment.java:16) ----
+constexpr int kLevelBits = 3;
+constexpr int kTileIndexBits = 22;
+constexpr int kSegmentIndexBits = 21;
+constexpr uint64_t kInvalidSegmentId = 0x3fffffffffffull;  // Segment.java:16
+constexpr uint32_t kNone = 0xffffffffu;
+
+// ---- distance approximation (Valhalla-2.x-style PointLL float geometry) ----
+constexpr double kMetersPerDegLat = 110567.0;  // meters per degree latitude
+constexpr double kMetersPerDegLonEq = 111320.0;  // meters per degree longitude at the equator
+constexpr double kDegToRad = 0.017453292519943295;
+
+// cos(x) for |x| <= pi/2 by a fixed Horner polynomial in x^2 (Taylor to x^20).
+// Pure IEEE add/mul in a fixed order: identical bits on host and device.
+RM_HD double det_cos(double x) {
+  const double z = x * x;
+  double p = 1.0 / 2432902008176640000.0;   // 1/20!
+  p = p * z - 1.0 / 6402373705728000.0;     // 1/18!
+  p = p * z + 1.0 / 20922789888000.0;       // 1/16!
+  p = p * z - 1.0 / 87178291200.0;          // 1/14!
+  p = p * z + 1.0 / 479001600.0;            // 1/12!
+  p = p * z - 1.0 / 3628800.0;              // 1/10!
+  p = p * z + 1.0 / 40320.0;                // 1/8!
+  p = p * z - 1.0 / 720.0;                  // 1/6!
+  p = p * z + 1.0 / 24.0;                   // 1/4!
+  p = p * z - 0.5;                          // 1/2!
+  p = p * z + 1.0;
+  return p;
+}
+
+// meters per degree of longitude at latitude lat (degrees), as float.
+RM_HD float meters_per_lon(float lat) {
+  return (float)(kMetersPerDegLonEq * det_cos((double)lat * kDegToRad));
+}
+
+// "great-circle" distance between two measurements: equirectangular at the
+// mean latitude, fp64.
+RM_HD double gc_distance(float lon_a, float lat_a, float lon_b, float lat_b) {
+  const double mlat = 0.5 * ((double)lat_a + (double)lat_b);
+  const double dy = ((double)lat_b - (double)lat_a) * kMetersPerDegLat;
+  const double dx = ((double)lon_b - (double)lon_a) * (kMetersPerDegLonEq * det_cos(mlat * kDegToRad));
+  return __builtin_sqrt(dx * dx + dy * dy);
+}
+
+// ---- directed-edge record (16 B, one dwordx4 load in the route kernel) ----
+// info bits: [0,16) speed in 0.1 km/h, [16,19) access mask, bit 19 internal, bit 20 service
+struct EdgeRec {
+  uint32_t target;   // end node
+  uint32_t len_cm;   // integer centimetres (>= 1)
+  uint32_t info;     // speed / access / flags
+  uint32_t road;     // (road id << 1) | reversed
+};
+constexpr uint32_t kAccessAuto = 1u, kAccessBicycle = 2u, kAccessPedestrian = 4u;
+constexpr uint32_t kFlagInternal = 1u << 19, kFlagService = 1u << 20;
+RM_HD uint32_t edge_speed_dkph(uint32_t info) { return info & 0xffffu; }
+RM_HD uint32_t edge_access(uint32_t info) { return (info >> 16) & 7u; }
+
+// ---- shape vertex record (16 B) ----
+struct VertRec {
+  float lon, lat;
+  uint32_t cum_cm;   // distance of this vertex from the road's first vertex (cm)
+  uint32_t road;     // owning road; kNone for the last vertex of a road
+};
+
+// ---- travel modes ----
+enum Mode : int { kModeAuto = 0, kModeBus = 1, kModeMotorScooter = 2, kModeBicycle = 3, kModePedestrian = 4 };
+RM_HD uint32_t mode_access(int mode) {
+  return mode == kModeBicycle ? kAccessBicycle : (mode == kModePedestrian ? kAccessPedestrian : kAccessAuto);
+}
+// speed used for routing time on an edge, in 0.1 km/h
+RM_HD uint32_t mode_speed_dkph(int mode, uint32_t edge_dkph) {
+  uint32_t cap = 0xffffu;
+  if (mode == kModeBicycle) cap = 180;
+  else if (mode == kModePedestrian) cap = 51;
+  else if (mode == kModeMotorScooter) cap = 450;
+  return edge_dkph < cap ? edge_dkph : cap;
+}
+// milliseconds to cover d_cm at speed dkph (floor)
+RM_HD uint32_t time_ms(uint32_t d_cm, uint32_t dkph) {
+  return (uint32_t)(((uint64_t)d_cm * 360ull) / (uint64_t)(dkph ? dkph : 1u));
+}
+
+// ---- route keys: lexicographic (distance cm, time ms) in one u64 ----
+RM_HD uint64_t make_key(uint32_t d_cm, uint32_t t_ms) { return ((uint64_t)d_cm << 32) | t_ms; }
+RM_HD uint32_t key_dist(uint64_t k) { return (uint32_t)(k >> 32); }
+RM_HD uint32_t key_time(uint64_t k) { return (uint32_t)k; }
+constexpr uint64_t kKeyInf = ~0ull;
+
+// ---- matcher limits ----
+constexpr int kMaxCand = 16;            // K: candidates kept per state (nearest first)
+constexpr float kMaxSearchRadius = 200.f;
+constexpr uint32_t kRouteInvalid = 0xffffffffu;
+
+// Per-request matcher options (meili defaults: Dockerfile:14-17, generate_test_trace.py:36-38).
+struct MatchOptions {
+  int32_t mode;
+  float sigma_z;                    // 4.07
+  float beta;                       // 3
+  float search_radius;              // 50 m
+  float gps_accuracy;               // 5 m (default accuracy when a point has none)
+  float breakage_distance;          // 2000 m
+  float interpolation_distance;     // 10 m
+  float max_route_distance_factor;  // 5
+  float max_route_time_factor;      // 2
+  float turn_penalty_factor;        // 0 (only 0 is supported)
+};
+
+RM_HD MatchOptions default_options() {
+  MatchOptions o;
+  o.mode = kModeAuto; o.sigma_z = 4.07f; o.beta = 3.f; o.search_radius = 50.f; o.gps_accuracy = 5.f;
+  o.breakage_distance = 2000.f; o.interpolation_distance = 10.f; o.max_route_distance_factor = 5.f;
+  o.max_route_time_factor = 2.f; o.turn_penalty_factor = 0.f;
+  return o;
+}
+
+// ---- segment record produced by the engine (one matched OSMLR run) ----
+struct SegmentRec {
+  uint64_t segment_id;      // kInvalidSegmentId when the run has no OSMLR id
+  double start_time;        // -1 when entered mid-segment
+  double end_time;          // -1 when left mid-segment
+  int32_t length;           // metres; -1 when partial
+  int32_t queue_length;     // metres
+  uint32_t flags;           // bit0 internal, bit1 has_id
+  uint32_t begin_shape_index;
+  uint32_t end_shape_index;
+  uint32_t seg_dense;       // dense segment index (kNone if none)
+  uint32_t way_first;       // way id of the run's first traversal
+  uint32_t way_last;        // last way id differing from way_first (== way_first if none)
+};
+static_assert(sizeof(SegmentRec) == 56, "SegmentRec layout is shared with oracle/meili_oracle.h");
+
+// ---- report record produced by the report epilogue (reporter_service.py:79-179) ----
+struct ReportRec {
+  uint64_t id;
+  uint64_t next_id;         // kInvalidSegmentId when absent
+  double t0, t1;
+  int32_t length, queue_length;
+  uint32_t seg_dense;
+  uint32_t pad;
+};
+static_assert(sizeof(ReportRec) == 48, "ReportRec layout is shared with oracle/meili_oracle.h");
+
+struct ReportStats {        // per trace (reporter_service.py:164-177)
+  int32_t successful_count, unreported_count;
+  int32_t successful_length_m, unreported_length_m;  // last assigned length (m), -1 if never
+  int32_t discontinuities, invalid_speeds, invalid_times, unassociated;
+  int32_t shape_used;       // -1 when absent
+  int32_t n_reports;
+};
+
+constexpr int kHistBins = 16;           // 10 km/h bins, 0..160 (reporter_service.py:133)
+
+}  // namespace rm

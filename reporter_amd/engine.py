@@ -1,0 +1,247 @@
+"""Batched array API over the HIP engine (rm_engine / rm_runner of the C-ABI).
+
+This is the high-throughput path the bench and the batch pipeline use: traces
+go in as flat numpy arrays (CSR offsets per trace), every stage runs on the GPU,
+and stage outputs can be downloaded for parity checks.  Requires a GPU.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _lib
+
+SEGMENT_DTYPE = np.dtype([
+    ("segment_id", "<u8"), ("start_time", "<f8"), ("end_time", "<f8"), ("length", "<i4"),
+    ("queue_length", "<i4"), ("flags", "<u4"), ("begin_shape_index", "<u4"), ("end_shape_index", "<u4"),
+    ("seg_dense", "<u4"), ("way_first", "<u4"), ("way_last", "<u4")])
+assert SEGMENT_DTYPE.itemsize == 56
+
+REPORT_DTYPE = np.dtype([
+    ("id", "<u8"), ("next_id", "<u8"), ("t0", "<f8"), ("t1", "<f8"), ("length", "<i4"),
+    ("queue_length", "<i4"), ("seg_dense", "<u4"), ("pad", "<u4")])
+assert REPORT_DTYPE.itemsize == 48
+
+STATS_DTYPE = np.dtype([
+    ("successful_count", "<i4"), ("unreported_count", "<i4"), ("successful_length_m", "<i4"),
+    ("unreported_length_m", "<i4"), ("discontinuities", "<i4"), ("invalid_speeds", "<i4"),
+    ("invalid_times", "<i4"), ("unassociated", "<i4"), ("shape_used", "<i4"), ("n_reports", "<i4")])
+assert STATS_DTYPE.itemsize == 40
+
+OPTIONS_DTYPE = np.dtype([
+    ("mode", "<i4"), ("sigma_z", "<f4"), ("beta", "<f4"), ("search_radius", "<f4"), ("gps_accuracy", "<f4"),
+    ("breakage_distance", "<f4"), ("interpolation_distance", "<f4"), ("max_route_distance_factor", "<f4"),
+    ("max_route_time_factor", "<f4"), ("turn_penalty_factor", "<f4")])
+assert OPTIONS_DTYPE.itemsize == 40
+
+MAX_CAND = 16
+INVALID_SEGMENT_ID = 0x3FFFFFFFFFFF  # Segment.java:16, simple_reporter.py:43
+
+
+def default_options(n=1, **over):
+    o = _lib.RmOptions()
+    _lib.lib().rm_default_options(C.byref(o))
+    a = np.zeros(n, OPTIONS_DTYPE)
+    for name, _ in _lib.RmOptions._fields_:
+        a[name] = getattr(o, name)
+    for k, v in over.items():
+        a[k] = v
+    return a
+
+
+def levels_mask(levels):
+    """bit (level+1) per level, as the kernels and the oracle expect."""
+    m = 0
+    for lv in levels:
+        if 0 <= int(lv) <= 7:
+            m |= 1 << (int(lv) + 1)
+    return m
+
+
+class Engine:
+    """The road graph resident in one GPU's HBM."""
+
+    def __init__(self, graph_path, device=0):
+        self._h = _lib.lib().rm_engine_create(os.fsencode(graph_path), int(device))
+        if not self._h:
+            raise _lib.RmError(_lib.last_error())
+        self.graph_path = graph_path
+        self.device = device
+
+    @property
+    def n_segments(self):
+        return int(_lib.lib().rm_engine_n_segments(self._h))
+
+    def segment_ids(self):
+        ids = np.empty(self.n_segments, np.uint64)
+        _lib.check(_lib.lib().rm_engine_segment_ids(self._h, ids.ctypes.data))
+        return ids
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().rm_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class BatchMatcher:
+    """One HIP stream + device workspace; runs whole batches of traces."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        self._h = _lib.lib().rm_runner_create(engine._h)
+        if not self._h:
+            raise _lib.RmError(_lib.last_error())
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().rm_runner_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @staticmethod
+    def run_params(threshold_sec=15.0, report_levels=(0, 1), transition_levels=(0, 1), hist_dev=None,
+                   do_report=True):
+        rp = _lib.RmRunParams()
+        rp.threshold_sec = threshold_sec
+        rp.report_mask = levels_mask(report_levels)
+        rp.transition_mask = levels_mask(transition_levels)
+        rp.hist_dev = hist_dev or None
+        rp.do_report = 1 if do_report else 0
+        return rp
+
+    def run(self, trace_off, lon, lat, time, accuracy=None, opts=None, trace_opt=None, **rp_kw):
+        """Upload a batch and run every stage (blocks until done)."""
+        trace_off = _c(trace_off, np.uint32)
+        T = len(trace_off) - 1
+        P = int(trace_off[-1])
+        lon = _c(lon, np.float32)
+        lat = _c(lat, np.float32)
+        time = _c(time, np.float64)
+        accuracy = _c(np.full(P, -1.0, np.float32) if accuracy is None else accuracy, np.float32)
+        opts = default_options(1) if opts is None else _c(opts, OPTIONS_DTYPE)
+        trace_opt = np.zeros(T, np.uint32) if trace_opt is None else _c(trace_opt, np.uint32)
+        if not (len(lon) == len(lat) == len(time) == len(accuracy) == P):
+            raise ValueError("point arrays must all have trace_off[-1] elements")
+        if len(trace_opt) != T:
+            raise ValueError("trace_opt must have one entry per trace")
+        d = _lib.RmBatchDesc(T, trace_off.ctypes.data, lon.ctypes.data, lat.ctypes.data, time.ctypes.data,
+                             accuracy.ctypes.data, len(opts), opts.ctypes.data, trace_opt.ctypes.data)
+        self._keep = (trace_off, lon, lat, time, accuracy, opts, trace_opt)
+        rp = self.run_params(**rp_kw)
+        _lib.check(_lib.lib().rm_runner_run(self._h, C.byref(d), C.byref(rp)))
+        return self
+
+    def rerun(self, **rp_kw):
+        """Run every stage again over the batch already in HBM."""
+        rp = self.run_params(**rp_kw)
+        _lib.check(_lib.lib().rm_runner_rerun(self._h, C.byref(rp)))
+
+    def sizes(self):
+        out = (C.c_uint64 * 6)()
+        _lib.check(_lib.lib().rm_runner_sizes(self._h, out))
+        return dict(zip(("points", "traces", "transitions", "path_edges", "segments", "reports"), [int(x) for x in out]))
+
+    # ---- stage outputs (parity tests) ----
+    def states(self):
+        s = self.sizes()
+        n_states = np.empty(s["traces"], np.uint32)
+        orig = np.empty(s["points"], np.uint32)
+        _lib.check(_lib.lib().rm_runner_get_states(self._h, n_states.ctypes.data, orig.ctypes.data))
+        return n_states, orig
+
+    def candidates(self):
+        P = self.sizes()["points"]
+        n = np.empty(P, np.uint8)
+        road = np.empty(P * MAX_CAND, np.uint32)
+        s = np.empty(P * MAX_CAND, np.uint32)
+        sq = np.empty(P * MAX_CAND, np.float32)
+        _lib.check(_lib.lib().rm_runner_get_candidates(self._h, n.ctypes.data, road.ctypes.data, s.ctypes.data,
+                                                       sq.ctypes.data))
+        return n, road.reshape(P, MAX_CAND), s.reshape(P, MAX_CAND), sq.reshape(P, MAX_CAND)
+
+    def routes(self):
+        sz = self.sizes()
+        off = np.empty(sz["points"], np.uint32)
+        gc = np.empty(sz["points"], np.float64)
+        route = np.empty(max(sz["transitions"], 1), np.uint32)
+        _lib.check(_lib.lib().rm_runner_get_routes(self._h, off.ctypes.data, gc.ctypes.data, route.ctypes.data))
+        return off, gc, route[: sz["transitions"]]
+
+    def viterbi(self):
+        P = self.sizes()["points"]
+        choice = np.empty(P, np.int8)
+        cs = np.empty(P, np.uint8)
+        _lib.check(_lib.lib().rm_runner_get_viterbi(self._h, choice.ctypes.data, cs.ctypes.data))
+        return choice, cs
+
+    def paths(self):
+        sz = self.sizes()
+        off = np.empty(sz["points"], np.uint32)
+        cnt = np.empty(sz["points"], np.uint32)
+        pool = np.empty(max(sz["path_edges"], 1), np.uint32)
+        dist = np.empty(sz["points"], np.uint32)
+        _lib.check(_lib.lib().rm_runner_get_paths(self._h, off.ctypes.data, cnt.ctypes.data, pool.ctypes.data,
+                                                  dist.ctypes.data))
+        return off, cnt, pool, dist
+
+    def segments(self):
+        sz = self.sizes()
+        off = np.empty(sz["traces"] + 1, np.uint32)
+        segs = np.empty(max(sz["segments"], 1), SEGMENT_DTYPE)
+        _lib.check(_lib.lib().rm_runner_get_segments(self._h, off.ctypes.data, segs.ctypes.data))
+        return off, segs[: sz["segments"]]
+
+    def reports(self):
+        sz = self.sizes()
+        off = np.empty(sz["traces"] + 1, np.uint32)
+        reps = np.empty(max(sz["reports"], 1), REPORT_DTYPE)
+        stats = np.empty(sz["traces"], STATS_DTYPE)
+        _lib.check(_lib.lib().rm_runner_get_reports(self._h, off.ctypes.data, reps.ctypes.data, stats.ctypes.data))
+        return off, reps[: sz["reports"]], stats
+
+    # ---- timing ----
+    def set_timing(self, on=True):
+        _lib.check(_lib.lib().rm_runner_set_timing(self._h, 1 if on else 0))
+
+    def reset_times(self):
+        _lib.check(_lib.lib().rm_runner_reset_times(self._h))
+
+    def kernel_times(self):
+        n = _lib.lib().rm_num_kernels()
+        ms = np.zeros(n, np.float64)
+        la = np.zeros(n, np.uint64)
+        _lib.check(_lib.lib().rm_runner_kernel_times(self._h, ms.ctypes.data, la.ctypes.data, n))
+        names = [_lib.lib().rm_kernel_name(i).decode() for i in range(n)]
+        return {names[i]: (float(ms[i]), int(la[i])) for i in range(n)}
+
+
+def segment_dicts(segs):
+    """Match-reply segments (README.md:288-301 schema) from SEGMENT_DTYPE records."""
+    out = []
+    for r in segs:
+        d = {}
+        if int(r["flags"]) & 2:
+            d["segment_id"] = int(r["segment_id"])
+        ways = [int(r["way_first"])]
+        if int(r["way_last"]) != int(r["way_first"]):
+            ways.append(int(r["way_last"]))
+        d["way_ids"] = ways
+        d["start_time"] = float(r["start_time"]) if r["start_time"] != -1 else -1
+        d["end_time"] = float(r["end_time"]) if r["end_time"] != -1 else -1
+        d["queue_length"] = int(r["queue_length"])
+        d["length"] = int(r["length"])
+        d["internal"] = bool(int(r["flags"]) & 1)
+        d["begin_shape_index"] = int(r["begin_shape_index"])
+        d["end_shape_index"] = int(r["end_shape_index"])
+        out.append(d)
+    return out

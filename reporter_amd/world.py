@@ -1,0 +1,90 @@
+"""Synthetic world + trace generation (host side; no GPU required).
+
+Configurations follow BASELINE.json ``configs`` / SURVEY.md §8d:
+
+  C1  1 trace x 1,000 pts @1 Hz, 40x40 grid @100 m
+  C2  10,000 traces x 600 pts @1 Hz, 200x200 grid @100 m   (the bench workload)
+  C3  1,000,000 traces x 40 pts @30 s, 500x500 grid @200 m, radius 100 m
+  C4  4,000x4,000 grid @250 m, 1,000,000 traces x 120 pts @5 s
+  C5  C2 graph, auto/bicycle/pedestrian, sigma_z in {2, 4.07, 8, 16}
+
+The trace generator restates reference py/generate_test_trace.py:35-104 and
+:120-149 (see reporter_amd/csrc/world.cpp).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _lib
+
+CONFIGS = {
+    "C1": dict(rows=40, cols=40, block_m=100.0, n_traces=1, n_points=1000, rate_s=1.0, noise_m=5.0,
+               search_radius=50.0, cell_m=100.0),
+    "C2": dict(rows=200, cols=200, block_m=100.0, n_traces=10000, n_points=600, rate_s=1.0, noise_m=5.0,
+               search_radius=50.0, cell_m=100.0),
+    "C3": dict(rows=500, cols=500, block_m=200.0, n_traces=1000000, n_points=40, rate_s=30.0, noise_m=5.0,
+               search_radius=100.0, cell_m=200.0),
+    "C4": dict(rows=4000, cols=4000, block_m=250.0, n_traces=1000000, n_points=120, rate_s=5.0, noise_m=5.0,
+               search_radius=50.0, cell_m=250.0),
+    "C5": dict(rows=200, cols=200, block_m=100.0, n_traces=10000, n_points=600, rate_s=1.0, noise_m=5.0,
+               search_radius=50.0, cell_m=100.0),
+}
+
+MODES = {"auto": 0, "bus": 1, "motor_scooter": 2, "bicycle": 3, "pedestrian": 4}
+
+
+def world_params(rows, cols, block_m=100.0, seed=1, cell_m=None, **kw):
+    p = _lib.RmWorldParams()
+    _lib.lib().rm_default_world_params(C.byref(p))
+    p.rows, p.cols, p.block_m, p.seed = rows, cols, block_m, seed
+    p.cell_m = cell_m if cell_m is not None else block_m
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def build_world(path, rows, cols, block_m=100.0, seed=1, cell_m=None, **kw):
+    """Write a synthetic .rmg graph to ``path`` and return the path."""
+    p = world_params(rows, cols, block_m, seed, cell_m, **kw)
+    _lib.check(_lib.lib().rm_world_build(C.byref(p), os.fsencode(path)))
+    return path
+
+
+def graph_info(path):
+    out = (C.c_uint64 * 7)()
+    _lib.check(_lib.lib().rm_graph_info(os.fsencode(path), out))
+    keys = ("nodes", "edges", "roads", "verts", "segments", "cells", "cell_items")
+    return dict(zip(keys, [int(x) for x in out]))
+
+
+def generate_traces(graph_path, n_traces, n_points, rate_s=1.0, noise_m=5.0, seed=1, mode="auto",
+                    start_epoch=1483228800, threads=0):
+    """Seeded GPS traces on the graph.  Returns a dict of numpy arrays:
+    lon/lat (6-dp degrees, f64), time (epoch s, f64), accuracy (f32),
+    trace_off (u32, n_traces+1), truth_edge / truth_off_cm (u32)."""
+    p = _lib.RmTraceParams()
+    _lib.lib().rm_default_trace_params(C.byref(p))
+    p.n_traces, p.n_points, p.rate_s, p.noise_m = n_traces, n_points, rate_s, noise_m
+    p.seed, p.mode, p.start_epoch, p.threads = seed, MODES[mode] if isinstance(mode, str) else int(mode), start_epoch, threads
+    n = n_traces * n_points
+    out = {k: np.empty(n, np.float64) for k in ("lon", "lat", "time")}
+    out["accuracy"] = np.empty(n, np.float32)
+    out["truth_edge"] = np.empty(n, np.uint32)
+    out["truth_off_cm"] = np.empty(n, np.uint32)
+    _lib.check(_lib.lib().rm_traces_generate(
+        os.fsencode(graph_path), C.byref(p), out["lon"].ctypes.data, out["lat"].ctypes.data,
+        out["time"].ctypes.data, out["accuracy"].ctypes.data, out["truth_edge"].ctypes.data,
+        out["truth_off_cm"].ctypes.data))
+    out["trace_off"] = (np.arange(n_traces + 1, dtype=np.uint64) * n_points).astype(np.uint32)
+    return out
+
+
+def trace_to_request(tr, k, uuid=None, mode="auto", report_levels=(0, 1), transition_levels=(0, 1), **opts):
+    """The /report JSON request for trace k (reporter_service.py:184-235 contract)."""
+    o0, o1 = int(tr["trace_off"][k]), int(tr["trace_off"][k + 1])
+    pts = [{"lat": float(tr["lat"][i]), "lon": float(tr["lon"][i]), "time": int(tr["time"][i]),
+            "accuracy": float(tr["accuracy"][i])} for i in range(o0, o1)]
+    mo = {"mode": mode, "report_levels": list(report_levels), "transition_levels": list(transition_levels)}
+    mo.update(opts)
+    return {"uuid": uuid or str(k), "trace": pts, "match_options": mo}

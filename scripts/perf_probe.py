@@ -1,0 +1,37 @@
+"""Quick engine timing on a BASELINE config (diagnostic; bench.py is the contract)."""
+import argparse, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+from reporter_amd import engine, world
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="C2")
+ap.add_argument("--traces", type=int, default=0)
+ap.add_argument("--reps", type=int, default=3)
+a = ap.parse_args()
+c = dict(world.CONFIGS[a.config])
+if a.traces:
+    c["n_traces"] = a.traces
+os.makedirs("/tmp/rmprobe", exist_ok=True)
+gp = "/tmp/rmprobe/%s.rmg" % a.config
+t = time.time()
+world.build_world(gp, c["rows"], c["cols"], c["block_m"], seed=1, cell_m=c["cell_m"])
+print("world", world.graph_info(gp), "%.1fs" % (time.time() - t), flush=True)
+t = time.time()
+tr = world.generate_traces(gp, c["n_traces"], c["n_points"], c["rate_s"], c["noise_m"], seed=7)
+print("traces %d pts %.1fs" % (len(tr["lon"]), time.time() - t), flush=True)
+eng = engine.Engine(gp, 0)
+bm = engine.BatchMatcher(eng)
+opts = engine.default_options(1, search_radius=c["search_radius"])
+t = time.time()
+bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts)
+print("first run %.3fs" % (time.time() - t), bm.sizes(), flush=True)
+bm.set_timing(True)
+for r in range(a.reps):
+    bm.reset_times()
+    t = time.time()
+    bm.rerun()
+    dt = time.time() - t
+    kt = bm.kernel_times()
+    print("rerun %.4fs  %.1f Mpts/s  " % (dt, len(tr["lon"]) / dt / 1e6) +
+          " ".join("%s=%.2fms" % (k, v[0]) for k, v in kt.items()), flush=True)

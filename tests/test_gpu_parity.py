@@ -1,0 +1,194 @@
+"""GPU parity: the HIP engine against the CPU oracle, bit-exact at every stage.
+
+Inputs are seeded synthetic worlds/traces (BASELINE.json configs, scaled so
+the oracle finishes in seconds).  Exactness bar: integer/index outputs equal,
+fp32/fp64 outputs equal bit for bit (the engine and the oracle share one
+written arithmetic spec; -ffp-contract=off on both sides).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import meili_oracle as mo
+import report_oracle
+from parity_util import compare_all
+from reporter_amd import engine, graphfile, world
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c1(small_world):
+    eng = engine.Engine(small_world, 0)
+    return small_world, graphfile.load(small_world), eng
+
+
+def _run_both(graph_path, g, eng, tr, opts, trace_opt, **rp):
+    bm = engine.BatchMatcher(eng)
+    bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt, **rp)
+    ref = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt))
+    return bm, ref
+
+
+def _check_reports(bm, ref, tr, rl=(0, 1), tl=(0, 1), threshold=15.0):
+    off, reps, stats = bm.reports()
+    rmask, tmask = engine.levels_mask(rl), engine.levels_mask(tl)
+    T = len(tr["trace_off"]) - 1
+    n = 0
+    for k in range(T):
+        s0, s1 = ref["seg_off"][k], ref["seg_off"][k + 1]
+        end_t = tr["time"][tr["trace_off"][k + 1] - 1]
+        want, wst = mo.report_trace(ref["segs"][s0:s1], end_t, threshold, rmask, tmask)
+        got = reps[off[k]:off[k + 1]]
+        assert len(got) == len(want), "trace %d: %d reports vs %d" % (k, len(got), len(want))
+        for f in want.dtype.names:
+            a, b = got[f], want[f]
+            if a.dtype.kind == "f":
+                a, b = a.view(np.uint64), b.view(np.uint64)
+            np.testing.assert_array_equal(a, b, "report field " + f)
+        for f in stats.dtype.names:
+            assert int(stats[k][f]) == int(wst[f]), "trace %d stat %s" % (k, f)
+        n += len(got)
+    return n
+
+
+def test_c1_dense_1hz(c1):
+    path, g, eng = c1
+    tr = world.generate_traces(path, n_traces=64, n_points=400, rate_s=1.0, noise_m=5.0, seed=11)
+    opts = engine.default_options(1)
+    bm, ref = _run_both(path, g, eng, tr, opts, np.zeros(64, np.uint32))
+    c = compare_all(bm, ref, tr["trace_off"])
+    assert c["chained"] > 1000 and c["segments"] > 100
+    nrep = _check_reports(bm, ref, tr)
+    assert nrep > 0
+    print("C1 parity", c, "reports", nrep)
+
+
+def test_sparse_30s_large_radius(built_lib, tmpdir_session):
+    """C3-like: 30 s sampling, 200 m blocks, radius 100 m -> long bounded searches (retry tier)."""
+    path = str(tmpdir_session / "c3s.rmg")
+    world.build_world(path, 60, 60, 200.0, seed=3, cell_m=200.0)
+    g = graphfile.load(path)
+    eng = engine.Engine(path, 0)
+    tr = world.generate_traces(path, n_traces=64, n_points=40, rate_s=30.0, noise_m=5.0, seed=5)
+    opts = engine.default_options(1, search_radius=100.0)
+    bm, ref = _run_both(path, g, eng, tr, opts, np.zeros(64, np.uint32))
+    c = compare_all(bm, ref, tr["trace_off"])
+    _check_reports(bm, ref, tr)
+    print("sparse parity", c)
+
+
+def test_mixed_modes_sigma_sweep(c1):
+    """C5-like: auto/bicycle/pedestrian traces, sigma_z in {2, 4.07, 8, 16}, noise = sigma."""
+    path, g, eng = c1
+    parts, opts = [], []
+    for mi, mode in enumerate(("auto", "bicycle", "pedestrian")):
+        for si, sz in enumerate((2.0, 4.07, 8.0, 16.0)):
+            tr = world.generate_traces(path, n_traces=4, n_points=200, rate_s=1.0, noise_m=sz, seed=100 + mi * 10 + si,
+                                       mode=mode)
+            parts.append(tr)
+            opts.append(engine.default_options(1, mode=world.MODES[mode], sigma_z=sz,
+                                               search_radius=max(50.0, 3 * sz))[0])
+    tr = {k: np.concatenate([p[k] for p in parts]) for k in ("lon", "lat", "time", "accuracy")}
+    tr["trace_off"] = (np.arange(len(parts) * 4 + 1) * 200).astype(np.uint32)
+    trace_opt = np.repeat(np.arange(len(parts), dtype=np.uint32), 4)
+    opts = np.array(opts, engine.OPTIONS_DTYPE)
+    bm, ref = _run_both(path, g, eng, tr, opts, trace_opt, report_levels=(0, 1, 2), transition_levels=(0, 1, 2))
+    c = compare_all(bm, ref, tr["trace_off"])
+    _check_reports(bm, ref, tr, rl=(0, 1, 2), tl=(0, 1, 2))
+    print("mixed parity", c)
+
+
+def test_edge_cases(c1):
+    """Points off the graph (no candidates -> chain breaks), duplicates (interpolation),
+    a 1-point trace, non-increasing times, a long gap (breakage)."""
+    path, g, eng = c1
+    tr = world.generate_traces(path, n_traces=6, n_points=120, rate_s=1.0, noise_m=3.0, seed=77)
+    lon, lat, tm = tr["lon"].copy(), tr["lat"].copy(), tr["time"].copy()
+    lon[130:135] += 1.0                     # trace 1: 5 points far away
+    lon[250:260] = lon[249]; lat[250:260] = lat[249]  # trace 2: stationary
+    tm[370:380] = tm[369]                    # trace 3: frozen clock
+    lat[540:600] += 0.02                     # trace 4: jump > breakage in the middle
+    off = list(tr["trace_off"])
+    # append a single-point trace
+    lon = np.append(lon, lon[0]); lat = np.append(lat, lat[0]); tm = np.append(tm, tm[0])
+    acc = np.append(tr["accuracy"], -1.0).astype(np.float32)
+    off.append(off[-1] + 1)
+    trd = dict(lon=lon, lat=lat, time=tm, accuracy=acc, trace_off=np.array(off, np.uint32))
+    opts = engine.default_options(1)
+    bm, ref = _run_both(path, g, eng, trd, opts, np.zeros(len(off) - 1, np.uint32))
+    compare_all(bm, ref, trd["trace_off"])
+    _check_reports(bm, ref, trd)
+    choice, cs = bm.viterbi()
+    assert cs.sum() > 7  # breaks happened
+
+
+def test_histogram_matches_cpu_pipeline(c1):
+    path, g, eng = c1
+    tr = world.generate_traces(path, n_traces=128, n_points=300, rate_s=1.0, noise_m=5.0, seed=21)
+    opts = engine.default_options(1)
+    nseg = eng.n_segments
+    import ctypes
+    from reporter_amd import _lib
+    dptr = ctypes.c_void_p()
+    _lib.check(_lib.lib().rm_device_alloc(nseg * 16 * 4, ctypes.byref(dptr)))
+    try:
+        _lib.check(_lib.lib().rm_device_memset(dptr, 0, nseg * 16 * 4))
+        bm = engine.BatchMatcher(eng)
+        bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts,
+               np.zeros(128, np.uint32), hist_dev=dptr.value, report_levels=(0, 1, 2), transition_levels=(0, 1, 2))
+        hist = np.empty(nseg * 16, np.uint32)
+        _lib.check(_lib.lib().rm_device_download(hist.ctypes.data, dptr, hist.nbytes))
+    finally:
+        _lib.lib().rm_device_free(dptr)
+    want = np.zeros(nseg * 16, np.uint32)
+    nvalid = mo.pipeline(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts,
+                                     np.zeros(128, np.uint32)), 15.0, 0xE, 0xE, want)
+    np.testing.assert_array_equal(hist, want)
+    assert int(hist.sum()) == nvalid > 0
+
+
+def test_valhalla_dropin_json(c1, tmpdir_session):
+    """The drop-in module: Configure + SegmentMatcher().Match, then the reference's
+    report() restatement on the reply, as reporter_service.py:240-242 does."""
+    path, g, eng = c1
+    import valhalla
+    conf = valhalla.write_config(str(tmpdir_session / "conf.json"), path, device=0)
+    valhalla.Configure(conf)
+    sm = valhalla.SegmentMatcher()
+    tr = world.generate_traces(path, n_traces=8, n_points=150, rate_s=1.0, noise_m=5.0, seed=31)
+    opts = engine.default_options(1)
+    ref = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts,
+                               np.zeros(8, np.uint32)))
+    reqs = [world.trace_to_request(tr, k) for k in range(8)]
+    outs = [sm.Match(json.dumps(r, separators=(",", ":"))) for r in reqs]
+    outs2 = sm.MatchMany([json.dumps(r) for r in reqs])
+    for k in range(8):
+        got = json.loads(outs[k])
+        assert got == json.loads(outs2[k])
+        want = engine.segment_dicts(ref["segs"][ref["seg_off"][k]:ref["seg_off"][k + 1]])
+        assert got["segments"] == want
+        rep = report_oracle.report(got, reqs[k], 15, {0, 1}, {0, 1})
+        assert "datastore" in rep and rep["segment_matcher"]["mode"] == "auto"
+    # error path -> RuntimeError (service answers 500, reporter_service.py:244-245)
+    with pytest.raises(RuntimeError):
+        sm.Match('{"uuid":"x","trace":[]}')
+    with pytest.raises(RuntimeError):
+        sm.Match('{"uuid":"x","trace":[{"lat":1.0}]}')
+    with pytest.raises(RuntimeError):
+        sm.Match("not json")
+
+
+def test_rerun_is_deterministic(c1):
+    path, g, eng = c1
+    tr = world.generate_traces(path, n_traces=32, n_points=200, rate_s=1.0, noise_m=5.0, seed=41)
+    bm = engine.BatchMatcher(eng)
+    bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"])
+    o1, s1 = bm.segments()
+    for _ in range(3):
+        bm.rerun()
+        o2, s2 = bm.segments()
+        np.testing.assert_array_equal(o1, o2)
+        assert s1.tobytes() == s2.tobytes()

@@ -1,0 +1,87 @@
+"""Drop-in replacement for the ``valhalla`` Python module used by Open Traffic Reporter.
+
+The reference imports ``valhalla`` and calls exactly three things
+(SURVEY.md §8b):
+
+  valhalla.Configure(conf_path)          py/reporter_service.py:284, py/simple_reporter.py:132
+  valhalla.SegmentMatcher()              py/reporter_service.py:52,  py/simple_reporter.py:133
+  SegmentMatcher().Match(json) -> json   py/reporter_service.py:240, py/simple_reporter.py:166
+
+Here they bind to libreporter_match.so (the MI355X engine) through ctypes —
+no PyTorch.  Errors surface as RuntimeError so the service's 500 path
+(py/reporter_service.py:244-245) and the batch skip path
+(py/simple_reporter.py:169-173) behave as before.  There is no CPU fallback.
+"""
+import ctypes as C
+import json as _json
+import os as _os
+
+from reporter_amd import _lib
+
+__all__ = ["Configure", "SegmentMatcher"]
+
+
+def Configure(conf_path):
+    """Load the matcher config + graph into HBM (process-global)."""
+    err = C.create_string_buffer(1024)
+    rc = _lib.lib().rm_configure(_os.fsencode(conf_path), err, len(err))
+    if rc != 0:
+        raise RuntimeError(err.value.decode("utf-8", "replace"))
+
+
+class SegmentMatcher(object):
+    """One matcher per thread (the reference keeps it in threading.local)."""
+
+    def __init__(self):
+        self._h = _lib.lib().rm_matcher_create()
+        if not self._h:
+            raise RuntimeError(_lib.last_error())
+
+    def Match(self, trace_json):
+        """trace JSON string in, {"segments": [...]} JSON string out."""
+        if isinstance(trace_json, str):
+            trace_json = trace_json.encode("utf-8")
+        out = C.c_void_p()
+        rc = _lib.lib().rm_match(self._h, trace_json, C.byref(out))
+        if rc != 0:
+            raise RuntimeError(_lib.last_error())
+        try:
+            return C.string_at(out.value).decode("utf-8")
+        finally:
+            _lib.lib().rm_free(out)
+
+    def MatchMany(self, trace_jsons):
+        """Batched Match: many traces in one GPU pass (request coalescing)."""
+        n = len(trace_jsons)
+        if n == 0:
+            return []
+        arr = (C.c_char_p * n)(*[t.encode("utf-8") if isinstance(t, str) else t for t in trace_jsons])
+        outs = (C.c_void_p * n)()
+        rc = _lib.lib().rm_match_batch(self._h, arr, n, outs)
+        if rc != 0:
+            raise RuntimeError(_lib.last_error())
+        try:
+            return [C.string_at(o).decode("utf-8") for o in outs]
+        finally:
+            for o in outs:
+                _lib.lib().rm_free(o)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().rm_matcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def write_config(path, graph_path, device=0, **meili_default):
+    """Write a Valhalla-style config naming the engine's graph file."""
+    conf = {"meili": {"default": dict(meili_default)},
+            "reporter_amd": {"graph": _os.path.abspath(graph_path), "device": int(device)}}
+    with open(path, "w") as f:
+        _json.dump(conf, f, indent=1)
+    return path
