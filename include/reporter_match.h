@@ -114,6 +114,7 @@ typedef struct {
   uint32_t transition_mask;
   uint32_t* hist_dev;         /* device pointer, n_segments*16 u32 speed histogram, may be NULL */
   int32_t do_report;          /* run the report() epilogue */
+  int32_t zero_hist;          /* zero hist_dev on the runner's stream before the epilogue */
 } rm_run_params;
 void rm_default_run_params(rm_run_params* p);
 
@@ -138,6 +139,20 @@ int rm_runner_kernel_times(rm_runner* r, double* ms, uint64_t* launches, int n);
 int rm_runner_reset_times(rm_runner* r);
 const char* rm_kernel_name(int k);
 int rm_num_kernels(void);
+
+/* ---------------- RCCL over xGMI (multi-GPU histogram exchange) ----------------
+ * One process per GPU.  Replaces the reference's keyed Kafka repartition of
+ * "id next_id" reports (BatchingProcessor.java:126) with one all-reduce of the
+ * per-OSMLR-segment speed histogram.  Rank 0 creates the id, every rank inits. */
+typedef struct rm_comm rm_comm;
+int rm_comm_unique_id(uint8_t id_out[128]);
+rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device);
+void rm_comm_destroy(rm_comm* c);
+/* dtype: 0 u32, 1 u64, 2 f64; op: 0 sum, 1 max.  In place on a device buffer; blocks until done. */
+int rm_comm_allreduce(rm_comm* c, void* dev_buf, size_t count, int dtype, int op);
+/* all-reduce of one host double (op as above) */
+int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op);
+int rm_comm_barrier(rm_comm* c);
 
 /* ---------------- device memory helpers (histograms without a framework) ---------------- */
 int rm_device_alloc(size_t bytes, void** dev_ptr);

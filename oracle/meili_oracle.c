@@ -78,6 +78,14 @@ static int e_ok(const og_graph* g, uint32_t e, uint32_t acc) {
 static uint32_t e_speed(const og_graph* g, uint32_t e, int mode) { return mode_speed(mode, e_info(g, e) & 0xffffu); }
 static uint64_t mk(uint32_t d, uint32_t t) { return ((uint64_t)d << 32) | t; }
 
+/* ---------------- algorithmic work counters (roofline of K1/K2) ----------------
+ * [0] searches [1] settled nodes [2] scanned edges [3] label writes
+ * [4] target label lookups [5] route writes [6] candidate items tested [7] states */
+static uint64_t og_cnt[8];
+static int og_counting = 0;
+void og_reset_counters(void) { memset(og_cnt, 0, sizeof og_cnt); }
+void og_get_counters(uint64_t* out) { memcpy(out, og_cnt, sizeof og_cnt); }
+
 /* ---------------- result container ---------------- */
 struct og_result {
   uint64_t P, T, n_trans, n_path, n_seg;
@@ -172,10 +180,12 @@ static void search_from(const og_graph* g, search_ws* w, uint32_t road, uint32_t
     w->rootkey[v] = k;
     if (k < w->label[v]) { w->label[v] = k; heap_push(w, k, v); }
   }
+  if (og_counting) og_cnt[0]++;
   while (w->hn) {
     hitem it = heap_pop(w);
     if (it.key != w->label[it.node]) continue;       /* stale */
     const uint32_t u = it.node;
+    if (og_counting) { og_cnt[1]++; og_cnt[2] += g->node_off[u + 1] - g->node_off[u]; }
     for (uint32_t e = g->node_off[u]; e < g->node_off[u + 1]; ++e) {
       if (!e_ok(g, e, acc)) continue;
       const uint32_t len = e_len(g, e);
@@ -183,7 +193,7 @@ static void search_from(const og_graph* g, search_ws* w, uint32_t road, uint32_t
       if ((uint32_t)(nk >> 32) > bound) continue;
       const uint32_t v = e_target(g, e);
       ws_touch(w, v);
-      if (nk < w->label[v]) { w->label[v] = nk; heap_push(w, nk, v); }
+      if (nk < w->label[v]) { w->label[v] = nk; heap_push(w, nk, v); if (og_counting) og_cnt[3]++; }
     }
   }
 }
@@ -294,6 +304,7 @@ static uint32_t find_candidates(const og_graph* g, float lon, float lat, float r
         const uint32_t* A = g->verts + 4 * (size_t)v;
         const uint32_t* B = A + 4;
         const uint32_t road = A[3];
+        og_cnt[6]++;
         if (!e_ok(g, g->road_fwd[road], acc) && !e_ok(g, g->road_rev[road], acc)) continue;
         const float ax = (f32_of(A[0]) - lon) * mlon, ay = (f32_of(A[1]) - lat) * mlat;
         const float bx = (f32_of(B[0]) - lon) * mlon, by = (f32_of(B[1]) - lat) * mlat;
@@ -460,6 +471,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
       last = i;
     }
     R->n_states[k] = ns;
+    og_cnt[7] += ns;
     for (uint32_t s = 0; s < ns; ++s) {
       const uint32_t p = o + R->state_orig[o + s];
       const float r = point_radius(op, b->accuracy[p]);
@@ -506,6 +518,9 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
         const double tm = floor(dt * (double)op->max_route_time_factor * 1000.0);
         tmax = tm >= 4294967295.0 ? 0xffffffffu : (uint32_t)tm;
       }
+      og_cnt[4] += 2ull * KA * KB;
+      og_cnt[5] += (uint64_t)KA * KB;
+      og_counting = 1;
       for (uint32_t i = 0; i < KA; ++i) {
         const uint32_t ra = R->cand_road[la * (uint64_t)OG_K + i], sa = R->cand_s[la * (uint64_t)OG_K + i];
         search_from(g, &ws, ra, sa, op->mode, bound);
@@ -520,6 +535,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
     }
   }
 
+  og_counting = 0;
   /* S3 viterbi */
   double* cost = (double*)malloc(sizeof(double) * (P * OG_K + 1));
   uint8_t* bp = (uint8_t*)malloc(P * OG_K + 1);

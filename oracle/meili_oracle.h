@@ -108,6 +108,12 @@ int og_report_trace(const og_segment* segs, uint32_t n_segs, double trace_end_ti
 uint64_t og_pipeline(const og_graph* g, const og_batch* b, double threshold_sec, uint32_t report_mask,
                      uint32_t transition_mask, uint32_t* hist);
 
+/* Algorithmic work of the searches/candidate scans since the last reset:
+ * [0] searches [1] settled nodes [2] scanned edges [3] label writes
+ * [4] target label lookups [5] route writes [6] candidate items tested [7] states */
+void og_reset_counters(void);
+void og_get_counters(uint64_t* out8);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,8 +57,38 @@ def lib():
         h.og_pipeline.restype = C.c_uint64
         h.og_pipeline.argtypes = [C.POINTER(OgGraph), C.POINTER(OgBatch), C.c_double, C.c_uint32, C.c_uint32,
                                   C.c_void_p]
+        h.og_reset_counters.argtypes = []
+        h.og_get_counters.argtypes = [C.c_void_p]
         _lib = h
     return _lib
+
+
+COUNTER_NAMES = ("searches", "settled", "scanned", "label_writes", "target_lookups", "route_writes",
+                 "cand_items", "states")
+
+
+def reset_counters():
+    lib().og_reset_counters()
+
+
+def counters():
+    out = np.zeros(8, np.uint64)
+    lib().og_get_counters(out.ctypes.data)
+    return dict(zip(COUNTER_NAMES, (int(x) for x in out)))
+
+
+def routes_algorithmic_bytes(c):
+    """K2 algorithmic bytes: 8 B CSR offsets per settled node, 16 B edge record per
+    scanned edge, 12 B per label write, 8 B per target label lookup, 4 B per route write,
+    24 B per search (source candidate + its road record)."""
+    return (8 * c["settled"] + 16 * c["scanned"] + 12 * c["label_writes"] + 8 * c["target_lookups"]
+            + 4 * c["route_writes"] + 24 * c["searches"])
+
+
+def candidates_algorithmic_bytes(c):
+    """K1 algorithmic bytes: 16 B point per state + 36 B per tested cell item (item id +
+    two 16 B vertex records) + 24 B per state for up to 16 candidates written at 12 B each (avg)."""
+    return 16 * c["states"] + 36 * c["cand_items"]
 
 
 def make_graph(g):

@@ -64,7 +64,7 @@ def build(force=False, verbose=False):
     with cf.ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if force or _newer(LIB, objs):
-        cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-o", LIB] + objs + ["-lpthread"]
+        cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-o", LIB] + objs + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))

@@ -7,6 +7,7 @@
 // Match's reply follows the schema the reference documents at README.md:288-301
 // and consumes at py/reporter_service.py:79-179.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -407,13 +408,14 @@ void rm_runner_destroy(rm_runner* r) { delete r; }
 
 void rm_default_run_params(rm_run_params* p) {
   p->threshold_sec = 15.0; p->report_mask = 0x6; p->transition_mask = 0x6; p->hist_dev = nullptr; p->do_report = 1;
+  p->zero_hist = 0;
 }
 
 static RunParams to_rp(const rm_run_params* p) {
   RunParams rp;
   if (p) {
     rp.threshold_sec = p->threshold_sec; rp.report_mask = p->report_mask; rp.transition_mask = p->transition_mask;
-    rp.hist = p->hist_dev; rp.do_report = p->do_report;
+    rp.hist = p->hist_dev; rp.do_report = p->do_report; rp.zero_hist = p->zero_hist;
   }
   return rp;
 }
@@ -461,6 +463,89 @@ int rm_runner_kernel_times(rm_runner* r, double* ms, uint64_t* launches, int n) 
 int rm_runner_reset_times(rm_runner* r) { return guarded([&] { r->m->reset_kernel_times(); }); }
 const char* rm_kernel_name(int k) { return (k >= 0 && k < kNumKernels) ? kKernelNames[k] : ""; }
 int rm_num_kernels(void) { return kNumKernels; }
+
+// ---------------- RCCL ----------------
+}  // extern "C"
+
+struct rm_comm {
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  void* scratch = nullptr;  // 8 bytes for host-value reductions and barriers
+  int device = 0;
+};
+
+namespace {
+void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+}  // namespace
+
+extern "C" {
+
+int rm_comm_unique_id(uint8_t id_out[128]) {
+  return guarded([&] {
+    ncclUniqueId id;
+    nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    std::memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+  });
+}
+
+rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device) {
+  rm_comm* out = nullptr;
+  guarded([&] {
+    auto c = std::make_unique<rm_comm>();
+    c->device = device;
+    RM_HIP(hipSetDevice(device));
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    nccl_check(ncclCommInitRank(&c->comm, nranks, uid, rank), "ncclCommInitRank");
+    RM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    RM_HIP(hipMalloc(&c->scratch, 8));
+    out = c.release();
+  });
+  return out;
+}
+
+void rm_comm_destroy(rm_comm* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->scratch) (void)hipFree(c->scratch);
+  delete c;
+}
+
+int rm_comm_allreduce(rm_comm* c, void* buf, size_t count, int dtype, int op) {
+  return guarded([&] {
+    if (!c) throw std::runtime_error("comm is NULL");
+    const ncclDataType_t dt = dtype == 0 ? ncclUint32 : (dtype == 1 ? ncclUint64 : ncclFloat64);
+    const ncclRedOp_t ro = op == 0 ? ncclSum : ncclMax;
+    RM_HIP(hipSetDevice(c->device));
+    nccl_check(ncclAllReduce(buf, buf, count, dt, ro, c->comm, c->stream), "ncclAllReduce");
+    RM_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op) {
+  return guarded([&] {
+    if (!c) throw std::runtime_error("comm is NULL");
+    RM_HIP(hipSetDevice(c->device));
+    RM_HIP(hipMemcpyAsync(c->scratch, value, 8, hipMemcpyHostToDevice, c->stream));
+    nccl_check(ncclAllReduce(c->scratch, c->scratch, 1, ncclFloat64, op == 0 ? ncclSum : ncclMax, c->comm, c->stream),
+               "ncclAllReduce");
+    RM_HIP(hipMemcpyAsync(value, c->scratch, 8, hipMemcpyDeviceToHost, c->stream));
+    RM_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rm_comm_barrier(rm_comm* c) {
+  double one = 1.0;
+  const int rc = rm_comm_allreduce_host_f64(c, &one, 0);
+  if (rc == 0) {
+    return guarded([&] { RM_HIP(hipDeviceSynchronize()); });
+  }
+  return rc;
+}
 
 int rm_device_alloc(size_t bytes, void** p) { return guarded([&] { RM_HIP(hipMalloc(p, bytes)); }); }
 int rm_device_free(void* p) { return guarded([&] { RM_HIP(hipFree(p)); }); }

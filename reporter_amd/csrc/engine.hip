@@ -1178,6 +1178,8 @@ void Matcher::run_device(const RunParams& rp) {
   hipLaunchKernelGGL(k_segments, dim3((T + 63) / 64), dim3(64), 0, st, g, v);
   toc(kKSegments);
   if (rp.do_report) {
+    if (rp.hist && rp.zero_hist)
+      RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)eng_->n_segments() * kHistBins * sizeof(uint32_t), st));
     tic(kKReport);
     hipLaunchKernelGGL(k_report, dim3((T + 63) / 64), dim3(64), 0, st, v, rp.threshold_sec, rp.report_mask,
                        rp.transition_mask, rp.hist);

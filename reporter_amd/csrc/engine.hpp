@@ -65,6 +65,7 @@ struct RunParams {
   uint32_t transition_mask = 0b0110;
   uint32_t* hist = nullptr;             // device, n_segments * 16 u32 (may be null)
   int do_report = 1;
+  int zero_hist = 0;                    // memset hist on the stream before the epilogue
 };
 
 // Kernel ids for per-kernel HIP-event timing.

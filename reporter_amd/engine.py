@@ -110,13 +110,14 @@ class BatchMatcher:
 
     @staticmethod
     def run_params(threshold_sec=15.0, report_levels=(0, 1), transition_levels=(0, 1), hist_dev=None,
-                   do_report=True):
+                   do_report=True, zero_hist=False):
         rp = _lib.RmRunParams()
         rp.threshold_sec = threshold_sec
         rp.report_mask = levels_mask(report_levels)
         rp.transition_mask = levels_mask(transition_levels)
         rp.hist_dev = hist_dev or None
         rp.do_report = 1 if do_report else 0
+        rp.zero_hist = 1 if zero_hist else 0
         return rp
 
     def run(self, trace_off, lon, lat, time, accuracy=None, opts=None, trace_opt=None, **rp_kw):
