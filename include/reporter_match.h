@@ -122,8 +122,10 @@ void rm_default_run_params(rm_run_params* p);
 int rm_runner_run(rm_runner* r, const rm_batch_desc* b, const rm_run_params* p);
 /* run again over the batch already resident in HBM (bench steps) */
 int rm_runner_rerun(rm_runner* r, const rm_run_params* p);
-/* out: [0] points [1] traces [2] transitions [3] path edges [4] segments [5] reports */
-int rm_runner_sizes(rm_runner* r, uint64_t out[6]);
+/* out: [0] points [1] traces [2] transitions [3] path edges [4] segments [5] reports
+ *      [6] route pairs sent to the wave tier [7] ... to the single-source tier
+ *      [8] transitions sent to the path wave tier [9] states sent to the candidate wave tier */
+int rm_runner_sizes(rm_runner* r, uint64_t out[10]);
 int rm_runner_get_states(rm_runner* r, uint32_t* n_states, uint32_t* state_orig);
 int rm_runner_get_candidates(rm_runner* r, uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
 int rm_runner_get_routes(rm_runner* r, uint32_t* trans_off, double* gc, uint32_t* route_cm);

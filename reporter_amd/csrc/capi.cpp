@@ -429,10 +429,13 @@ int rm_runner_run(rm_runner* r, const rm_batch_desc* b, const rm_run_params* p) 
   });
 }
 int rm_runner_rerun(rm_runner* r, const rm_run_params* p) { return guarded([&] { r->m->run_device(to_rp(p)); }); }
-int rm_runner_sizes(rm_runner* r, uint64_t out[6]) {
+int rm_runner_sizes(rm_runner* r, uint64_t out[10]) {
   return guarded([&] {
     out[0] = r->m->n_points(); out[1] = r->m->n_traces(); out[2] = r->m->n_trans(); out[3] = r->m->n_path_edges();
     out[4] = r->m->count_segments(); out[5] = r->m->count_reports();
+    uint32_t t[4];
+    r->m->tier_counts(t);
+    for (int i = 0; i < 4; ++i) out[6 + i] = t[i];
   });
 }
 int rm_runner_get_states(rm_runner* r, uint32_t* a, uint32_t* b) { return guarded([&] { r->m->get_states(a, b); }); }

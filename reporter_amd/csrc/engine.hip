@@ -52,11 +52,16 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint32_t* slot_trace; uint32_t* n_states; uint32_t* state_orig;
   uint8_t* cand_n; uint32_t* cand_road; uint32_t* cand_s; float* cand_sq;
   uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route;
+  uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
   SegmentRec* segs; uint32_t* seg_base; uint32_t* seg_cnt;
+  TravRec* trav; uint32_t* trav_off;
   ReportRec* reps; uint32_t* rep_cnt; ReportStats* stats;
-  uint32_t* ctl; uint32_t* retry_routes; uint32_t* retry_paths;
+  // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
+  // [5] routes list B [6] paths list B [7] candidates list
+  uint32_t* ctl; uint32_t* rl_routes_a; uint32_t* rl_routes_b; uint32_t* rl_paths_a; uint32_t* rl_paths_b;
+  uint32_t* rl_cand;
 };
 
 __device__ __forceinline__ bool edge_ok(uint32_t info, uint32_t acc) { return (((info >> 16) & 7u) & acc) != 0u; }
@@ -140,14 +145,96 @@ __device__ __forceinline__ void project(const uint4 A, const uint4 B, float lon,
   s = v;
 }
 
-__global__ void __launch_bounds__(64) k_candidates(DevGraph g, DevBatch b) {
-  __shared__ CandSmem sm;
-  const uint64_t p = blockIdx.x;
-  const int lane = threadIdx.x;
+// K1 lane tier: one lane per state.  Per-road minima live in 16 registers; a state with
+// more roads inside its radius is queued for the wave tier (k_candidates_wave).
+__global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
   const uint32_t k = b.slot_trace[p];
   const uint32_t o = b.trace_off[k];
   const uint32_t s = (uint32_t)(p - o);
   if (s >= b.n_states[k]) return;
+  const MatchOptions op = b.opts[b.trace_opt[k]];
+  const uint32_t acc = mode_access(op.mode);
+  const uint32_t pt = o + b.state_orig[p];
+  const float lon = b.lon[pt], lat = b.lat[pt];
+  const float r = point_radius(op, b.acc[pt]);
+  const float mlon = meters_per_lon(lat);
+  const float mlat = (float)kMetersPerDegLat;
+  const float r2 = r * r;
+  const float pad = r * 1.01f + 0.5f;
+  const float qlon = pad / mlon, qlat = pad / mlat;
+  const double fx0 = floor(((double)(lon - qlon) - g.lon0) / g.dlon);
+  const double fx1 = floor(((double)(lon + qlon) - g.lon0) / g.dlon);
+  const double fy0 = floor(((double)(lat - qlat) - g.lat0) / g.dlat);
+  const double fy1 = floor(((double)(lat + qlat) - g.lat0) / g.dlat);
+  uint32_t rroad[kMaxCand];
+  unsigned long long rbest[kMaxCand];
+  uint32_t n = 0;
+  bool ovf = false;
+  if (!(fx1 < 0 || fy1 < 0 || fx0 > (double)(g.ncx - 1) || fy0 > (double)(g.ncy - 1))) {
+    const uint32_t x0 = fx0 < 0 ? 0u : (uint32_t)fx0, y0 = fy0 < 0 ? 0u : (uint32_t)fy0;
+    const uint32_t x1 = fx1 > (double)(g.ncx - 1) ? g.ncx - 1 : (uint32_t)fx1;
+    const uint32_t y1 = fy1 > (double)(g.ncy - 1) ? g.ncy - 1 : (uint32_t)fy1;
+    for (uint32_t cy = y0; cy <= y1 && !ovf; ++cy)
+      for (uint32_t cx = x0; cx <= x1 && !ovf; ++cx) {
+        const uint32_t c = cy * g.ncx + cx;
+        const uint32_t it0 = g.cell_off[c], it1 = g.cell_off[c + 1];
+        for (uint32_t it = it0; it < it1; ++it) {
+          const uint32_t v = g.cell_item[it];
+          const uint4 A = g.verts[v], B = g.verts[v + 1];
+          float sq; uint32_t sc;
+          project(A, B, lon, lat, mlon, mlat, sq, sc);
+          if (!(sq <= r2)) continue;
+          const uint32_t road = A.w;
+          const uint32_t ef = g.road_fwd[road], er = g.road_rev[road];
+          const bool ok = (ef != kNone && edge_ok(g.edges[ef].z, acc)) || (er != kNone && edge_ok(g.edges[er].z, acc));
+          if (!ok) continue;
+          const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | v;
+          bool found = false;
+#pragma unroll
+          for (int x = 0; x < kMaxCand; ++x)
+            if (x < (int)n && rroad[x] == road) { found = true; if (key < rbest[x]) rbest[x] = key; }
+          if (found) continue;
+          if (n >= (uint32_t)kMaxCand) { ovf = true; break; }
+#pragma unroll
+          for (int x = 0; x < kMaxCand; ++x)
+            if (x == (int)n) { rroad[x] = road; rbest[x] = key; }
+          ++n;
+        }
+      }
+  }
+  if (ovf) {
+    const uint32_t q = atomicAdd(&b.ctl[7], 1u);
+    b.rl_cand[q] = (uint32_t)p;
+    return;
+  }
+#pragma unroll
+  for (int x = 0; x < kMaxCand; ++x) {
+    if (x >= (int)n) continue;
+    const uint32_t sqb = (uint32_t)(rbest[x] >> 32);
+    uint32_t rank = 0;
+#pragma unroll
+    for (int y = 0; y < kMaxCand; ++y) {
+      if (y >= (int)n) continue;
+      const uint32_t sqb2 = (uint32_t)(rbest[y] >> 32);
+      rank += (sqb2 < sqb || (sqb2 == sqb && rroad[y] < rroad[x])) ? 1u : 0u;
+    }
+    const uint32_t v = (uint32_t)rbest[x];
+    float sq; uint32_t sc;
+    project(g.verts[v], g.verts[v + 1], lon, lat, mlon, mlat, sq, sc);
+    b.cand_road[p * kMaxCand + rank] = rroad[x];
+    b.cand_s[p * kMaxCand + rank] = sc;
+    b.cand_sq[p * kMaxCand + rank] = sq;
+  }
+  b.cand_n[p] = (uint8_t)n;
+}
+
+// wave tier of K1: states whose radius holds more roads than the lane tier keeps
+__device__ void cand_wave_one(const DevGraph& g, const DevBatch& b, CandSmem& sm, uint64_t p) {
+  const int lane = threadIdx.x;
+  const uint32_t k = b.slot_trace[p];
+  const uint32_t o = b.trace_off[k];
   const MatchOptions op = b.opts[b.trace_opt[k]];
   const uint32_t acc = mode_access(op.mode);
   const uint32_t pt = o + b.state_orig[p];
@@ -245,16 +332,41 @@ __global__ void __launch_bounds__(64) k_candidates(DevGraph g, DevBatch b) {
   if (lane == 0) b.cand_n[p] = (uint8_t)min(n_found, (uint32_t)kMaxCand);
 }
 
+__global__ void __launch_bounds__(64) k_candidates_wave(DevGraph g, DevBatch b) {
+  __shared__ CandSmem sm;
+  const uint32_t n_items = min(b.ctl[7], (uint32_t)b.P);
+  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    cand_wave_one(g, b, sm, b.rl_cand[item]);
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // transition counts for the exclusive scan that lays out route[] compactly
 __global__ void k_trans_count(DevBatch b) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
   const uint32_t k = b.slot_trace[p];
-  const uint32_t s = (uint32_t)(p - b.trace_off[k]);
-  uint32_t c = 0;
-  if (s >= 1 && s < b.n_states[k]) c = (uint32_t)b.cand_n[p - 1] * (uint32_t)b.cand_n[p];
+  const uint32_t o = b.trace_off[k];
+  const uint32_t s = (uint32_t)(p - o);
+  uint32_t c = 0, ns = 0;
+  if (s >= 1 && s < b.n_states[k]) {
+    const uint32_t KA = b.cand_n[p - 1], KB = b.cand_n[p];
+    c = KA * KB;
+    ns = KB ? KA : 0u;
+    const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
+    b.gc[p] = gc_distance(b.lon[pa], b.lat[pa], b.lon[pb], b.lat[pb]);
+  }
   b.trans_cnt[p] = c;
+  b.src_cnt[p] = ns;
+}
+
+// one work item per (layer pair, source candidate): item -> pair slot
+__global__ void k_src_items(DevBatch b) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
+  const uint32_t n = b.src_cnt[p], at = b.src_off[p];
+  for (uint32_t i = 0; i < n; ++i) b.src_item[at + i] = (uint32_t)p;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -401,28 +513,266 @@ __device__ unsigned long long route_to(const SearchSmem<H, PATH>& sm, const DevG
 }
 
 // ------------------------------------------------------------------------------------------
+// Lane tier: one lane runs one whole bounded Dijkstra with its labels in registers.
+// C2-class searches settle ~1.5 nodes and touch ~5 (profiles/r01), so a wave-wide
+// search wastes 60 lanes and pays LDS init + barriers; 16 register slots hold the
+// common case and anything larger goes to the wave tiers above.  Same exact keys.
+constexpr int kLaneCap = 8;
+
+struct LaneSearch {
+  uint32_t node[kLaneCap];
+  unsigned long long key[kLaneCap];
+  uint32_t n, settled;
+  bool ovf;
+};
+
+__device__ __forceinline__ unsigned long long ls_label(const LaneSearch& s, uint32_t v) {
+  unsigned long long k = kKeyInf;
+#pragma unroll
+  for (int x = 0; x < kLaneCap; ++x)
+    if (x < (int)s.n && s.node[x] == v) k = s.key[x];
+  return k;
+}
+
+__device__ __forceinline__ int ls_index(const LaneSearch& s, uint32_t v) {
+  int f = -1;
+#pragma unroll
+  for (int x = 0; x < kLaneCap; ++x)
+    if (x < (int)s.n && s.node[x] == v) f = x;
+  return f;
+}
+
+__device__ __forceinline__ void ls_relax(LaneSearch& s, uint32_t v, unsigned long long k) {
+  bool found = false;
+#pragma unroll
+  for (int x = 0; x < kLaneCap; ++x)
+    if (x < (int)s.n && s.node[x] == v) {
+      found = true;
+      if (k < s.key[x]) s.key[x] = k;
+    }
+  if (found) return;
+  if (s.n >= (uint32_t)kLaneCap) { s.ovf = true; return; }
+#pragma unroll
+  for (int x = 0; x < kLaneCap; ++x)
+    if (x == (int)s.n) { s.node[x] = v; s.key[x] = k; }
+  s.n++;
+}
+
+// bounded Dijkstra from the exits of candidate (road, s); returns the root keys
+__device__ void lane_search(LaneSearch& S, const DevGraph& g, int mode, uint32_t acc, uint32_t bound,
+                            uint32_t road, uint32_t s, unsigned long long& rk1, unsigned long long& rk0) {
+  S.n = 0; S.settled = 0; S.ovf = false;
+  rk1 = kKeyInf; rk0 = kKeyInf;
+  const uint32_t L = g.road_len[road];
+  const uint32_t ef = g.road_fwd[road], er = g.road_rev[road];
+  if (ef != kNone) {
+    const uint32_t z = g.edges[ef].z;
+    if (edge_ok(z, acc) && L - s <= bound) {
+      rk1 = make_key(L - s, time_ms(L - s, mode_speed_dkph(mode, z & 0xffffu)));
+      ls_relax(S, g.road_node1[road], rk1);
+    }
+  }
+  if (er != kNone) {
+    const uint32_t z = g.edges[er].z;
+    if (edge_ok(z, acc) && s <= bound) {
+      rk0 = make_key(s, time_ms(s, mode_speed_dkph(mode, z & 0xffffu)));
+      ls_relax(S, g.road_node0[road], rk0);
+    }
+  }
+  for (;;) {
+    int bi = -1;
+    unsigned long long bk = kKeyInf;
+    uint32_t u = 0;
+#pragma unroll
+    for (int x = 0; x < kLaneCap; ++x)
+      if (x < (int)S.n && !((S.settled >> x) & 1u) && S.key[x] < bk) { bk = S.key[x]; bi = x; u = S.node[x]; }
+    if (bi < 0) break;
+    S.settled |= 1u << bi;
+    const uint32_t e0 = g.node_off[u], e1 = g.node_off[u + 1];
+    for (uint32_t e = e0; e < e1; ++e) {
+      const uint4 rec = g.edges[e];
+      if (!edge_ok(rec.z, acc)) continue;
+      const unsigned long long nk = bk + edge_key(rec, mode);
+      if (key_dist(nk) > bound) continue;
+      ls_relax(S, rec.x, nk);
+    }
+    if (S.ovf) break;
+  }
+}
+
+__device__ __forceinline__ unsigned long long lane_route_to(const LaneSearch& S, const DevGraph& g, int mode,
+                                                            uint32_t acc, uint32_t ra, uint32_t sa, uint32_t rb,
+                                                            uint32_t sb, int* combo) {
+  const uint32_t ef = g.road_fwd[rb], er = g.road_rev[rb], L = g.road_len[rb];
+  const uint32_t inf_f = ef != kNone ? g.edges[ef].z : 0u, inf_r = er != kNone ? g.edges[er].z : 0u;
+  const bool okf = ef != kNone && edge_ok(inf_f, acc), okr = er != kNone && edge_ok(inf_r, acc);
+  const uint32_t spf = mode_speed_dkph(mode, inf_f & 0xffffu), spr = mode_speed_dkph(mode, inf_r & 0xffffu);
+  unsigned long long best = kKeyInf;
+  int bc = -1;
+  if (ra == rb) {
+    if (okf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
+    if (okr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
+  }
+  if (okf) {
+    const unsigned long long lab = ls_label(S, g.road_node0[rb]);
+    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(sb, time_ms(sb, spf)); if (k < best) { best = k; bc = 2; } }
+  }
+  if (okr) {
+    const unsigned long long lab = ls_label(S, g.road_node1[rb]);
+    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(L - sb, time_ms(L - sb, spr)); if (k < best) { best = k; bc = 3; } }
+  }
+  if (combo) *combo = bc;
+  return best;
+}
+
+// K2 lane tier: one lane per (layer pair, source) item.  A pair any of whose searches
+// outgrows the registers is queued once (the src_cnt word is consumed as a flag) for
+// the wave tier, which recomputes the whole pair.
+__global__ void __launch_bounds__(256) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_items) return;
+  const uint32_t p = b.src_item[t];
+  const uint32_t i = t - b.src_off[p];
+  const uint32_t k = b.slot_trace[p];
+  const uint32_t o = b.trace_off[k];
+  const MatchOptions op = b.opts[b.trace_opt[k]];
+  const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
+  const double gc = b.gc[p];
+  const uint32_t KB = b.cand_n[p];
+  const int mode = op.mode;
+  const uint32_t acc = mode_access(mode);
+  const uint32_t bound = route_bound(gc, op);
+  const uint32_t tmax = time_bound(b.time[pb] - b.time[pa], op);
+  const uint32_t ra = b.cand_road[(uint64_t)(p - 1) * kMaxCand + i], sa = b.cand_s[(uint64_t)(p - 1) * kMaxCand + i];
+  LaneSearch S;
+  unsigned long long rk1, rk0;
+  lane_search(S, g, mode, acc, bound, ra, sa, rk1, rk0);
+  if (S.ovf) {
+    if (atomicExch(&b.src_cnt[p], 0u) != 0u) {
+      const uint32_t q = atomicAdd(&b.ctl[3], 1u);
+      b.rl_routes_a[q] = p;
+    }
+    return;
+  }
+  uint32_t* out = b.route + b.trans_off[p] + i * KB;
+  for (uint32_t j = 0; j < KB; ++j) {
+    const uint32_t rb = b.cand_road[(uint64_t)p * kMaxCand + j], sb = b.cand_s[(uint64_t)p * kMaxCand + j];
+    const unsigned long long key = lane_route_to(S, g, mode, acc, ra, sa, rb, sb, nullptr);
+    uint32_t r = kRouteInvalid;
+    if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
+    out[j] = r;
+  }
+}
+
+// path lane tier: one lane per chosen transition; canonical predecessors in registers.
+__global__ void __launch_bounds__(256) k_paths_lane(DevGraph g, DevBatch b) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
+  const uint32_t k = b.slot_trace[p];
+  const uint32_t o = b.trace_off[k];
+  const uint32_t s = (uint32_t)(p - o);
+  if (s < 1 || s >= b.n_states[k]) return;
+  if (b.chain_start[p] || b.choice[p] < 0) return;
+  const MatchOptions op = b.opts[b.trace_opt[k]];
+  const int mode = op.mode;
+  const uint32_t acc = mode_access(mode);
+  const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+  const uint32_t ra = b.cand_road[(p - 1) * kMaxCand + i], sa = b.cand_s[(p - 1) * kMaxCand + i];
+  const uint32_t rb = b.cand_road[p * kMaxCand + j], sb = b.cand_s[p * kMaxCand + j];
+  const uint32_t bound = route_bound(b.gc[p], op);
+  LaneSearch S;
+  unsigned long long rk1, rk0;
+  lane_search(S, g, mode, acc, bound, ra, sa, rk1, rk0);
+  if (S.ovf) {
+    const uint32_t q = atomicAdd(&b.ctl[4], 1u);
+    b.rl_paths_a[q] = (uint32_t)p;
+    return;
+  }
+  int combo = -1;
+  const unsigned long long key = lane_route_to(S, g, mode, acc, ra, sa, rb, sb, &combo);
+  const uint32_t n1a = g.road_node1[ra], n0a = g.road_node0[ra];
+  b.route_dist[p] = key_dist(key);
+  uint32_t* inl = b.path_inline + p * kInlinePath;
+  if (combo <= 1) {
+    inl[0] = combo == 0 ? g.road_fwd[ra] : g.road_rev[ra];
+    b.path_cnt[p] = 1;
+    b.path_off[p] = 0;
+    return;
+  }
+  // walk back from the entry node; the canonical predecessor of a non-root node is the
+  // smallest-id tight in-edge from a labelled node (in-edges are sorted by edge id)
+  const uint32_t entry_e = combo == 2 ? g.road_fwd[rb] : g.road_rev[rb];
+  const uint32_t v0 = combo == 2 ? g.road_node0[rb] : g.road_node1[rb];
+  uint32_t n = 1, x = v0;
+  inl[0] = entry_e;                               // reversed order while walking
+  for (int guard = 0;; ++guard) {
+    const unsigned long long lx = ls_label(S, x);
+    if (lx == kKeyInf || guard > kLaneCap) { atomicOr(&b.ctl[2], kErrRounds); return; }
+    if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
+    uint32_t pe = kNone, pu = 0;
+    for (uint32_t q = g.in_off[x]; q < g.in_off[x + 1]; ++q) {
+      const uint32_t e = g.in_edge[q];
+      const uint4 rec = g.edges[e];
+      if (!edge_ok(rec.z, acc)) continue;
+      const uint32_t u = g.edge_src[e];
+      const unsigned long long lu = ls_label(S, u);
+      if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { pe = e; pu = u; break; }
+    }
+    if (pe == kNone) { atomicOr(&b.ctl[2], kErrRounds); return; }
+    if (n < (uint32_t)kInlinePath) inl[n] = pe;
+    ++n;
+    x = pu;
+  }
+  const uint32_t exit_e = (x == n1a) ? g.road_fwd[ra] : g.road_rev[ra];
+  if (n < (uint32_t)kInlinePath) inl[n] = exit_e;
+  ++n;
+  b.path_cnt[p] = n;
+  if (n <= (uint32_t)kInlinePath) {
+    for (uint32_t a = 0, c = n - 1; a < c; ++a, --c) { const uint32_t t = inl[a]; inl[a] = inl[c]; inl[c] = t; }
+    b.path_off[p] = 0;
+    return;
+  }
+  // long path: pool slot, second walk writing in travel order
+  const uint32_t at = atomicAdd(&b.ctl[0], n);
+  if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); b.path_off[p] = kNone; return; }
+  b.path_off[p] = at;
+  uint32_t* dst = b.path_pool + at;
+  dst[n - 1] = entry_e;
+  dst[0] = exit_e;
+  x = v0;
+  for (uint32_t q = n - 2; q >= 1; --q) {
+    const unsigned long long lx = ls_label(S, x);
+    for (uint32_t r = g.in_off[x]; r < g.in_off[x + 1]; ++r) {
+      const uint32_t e = g.in_edge[r];
+      const uint4 rec = g.edges[e];
+      if (!edge_ok(rec.z, acc)) continue;
+      const uint32_t u = g.edge_src[e];
+      const unsigned long long lu = ls_label(S, u);
+      if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { dst[q] = e; x = u; break; }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // K2 k_routes: one wave per layer pair (s-1 -> s).  SMALL tier searches all sources at
 // once in a 256-slot hash; a pair that overflows is queued for the BIG tier, which
 // searches one source at a time in a 4096-slot hash.
 template <bool BIG>
-__global__ void __launch_bounds__(64) k_routes(DevGraph g, DevBatch b) {
+__global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
   constexpr int H = BIG ? kBigH : kSmallH;
   __shared__ SearchSmem<H, false> sm;
   __shared__ uint32_t s_road[kMaxCand], s_off[kMaxCand];
   const int lane = threadIdx.x;
-  const uint32_t n_items = BIG ? min(b.ctl[3], (uint32_t)b.P) : (uint32_t)b.P;
-  for (uint64_t item = blockIdx.x; item < n_items; item += (BIG ? gridDim.x : n_items)) {
-    const uint64_t p = BIG ? b.retry_routes[item] : item;
+  const uint32_t n_items = min(b.ctl[BIG ? 5 : 3], (uint32_t)b.P);
+  const uint32_t* list = BIG ? b.rl_routes_b : b.rl_routes_a;
+  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const uint64_t p = list[item];
     const uint32_t k = b.slot_trace[p];
     const uint32_t o = b.trace_off[k];
-    const uint32_t s = (uint32_t)(p - o);
-    if (s < 1 || s >= b.n_states[k]) continue;
     const MatchOptions op = b.opts[b.trace_opt[k]];
     const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
-    const double gc = gc_distance(b.lon[pa], b.lat[pa], b.lon[pb], b.lat[pb]);
-    if (!BIG && lane == 0) b.gc[p] = gc;
+    const double gc = b.gc[p];
     const uint32_t KA = b.cand_n[p - 1], KB = b.cand_n[p];
-    if (KA == 0 || KB == 0) continue;
     const uint32_t bound = route_bound(gc, op);
     const uint32_t tmax = time_bound(b.time[pb] - b.time[pa], op);
     const uint32_t base = b.trans_off[p];
@@ -435,8 +785,8 @@ __global__ void __launch_bounds__(64) k_routes(DevGraph g, DevBatch b) {
       bounded_search<H, false>(sm, g, op.mode, bound, s_road, s_off, KA);
       if (sm.ovf) {
         if (lane == 0) {
-          const uint32_t q = atomicAdd(&b.ctl[3], 1u);
-          b.retry_routes[q] = (uint32_t)p;
+          const uint32_t q = atomicAdd(&b.ctl[5], 1u);
+          b.rl_routes_b[q] = (uint32_t)p;
         }
         __syncthreads();
         continue;
@@ -500,6 +850,7 @@ __device__ void backtrace_chain(const DevBatch& b, uint32_t o, uint32_t end, uin
 
 __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
   const int j = threadIdx.x & 15;
+  const int gbase = threadIdx.x & 48;
   const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 4);
   if (k >= b.T) return;
   const uint32_t o = b.trace_off[k], S = b.n_states[k];
@@ -511,27 +862,42 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
   bool prev_ok = false;
   double cost = INF;
   uint32_t prevK = 0;
+  // one-layer-ahead prefetch of the per-layer scalars and this lane's emission input
+  uint32_t KBn = 0, basen = 0;
+  double gcn = 0.0;
+  float sqn = 0.f;
+  if (S) { KBn = b.cand_n[o]; sqn = b.cand_sq[(uint64_t)o * kMaxCand + j]; }
   for (uint32_t s = 0; s < S; ++s) {
     const uint64_t l = o + s;
-    const uint32_t KB = b.cand_n[l];
-    bool start = !prev_ok || (s > 0 && b.gc[l] > brk);
+    const uint32_t KB = KBn, base = basen;
+    const double gcl = gcn;
+    const float sq = sqn;
+    if (s + 1 < S) {
+      KBn = b.cand_n[l + 1];
+      gcn = b.gc[l + 1];
+      basen = b.trans_off[l + 1];
+      sqn = b.cand_sq[(l + 1) * kMaxCand + j];
+    }
+    bool start = !prev_ok || (s > 0 && gcl > brk);
     double best = INF;
     int arg = -1;
     if (KB && !start) {
-      const uint32_t base = b.trans_off[l];
-      const double gcl = b.gc[l];
-      for (uint32_t i = 0; i < prevK; ++i) {
-        const double ci = shfl_d(cost, (threadIdx.x & 48) | i);
-        if (j < (int)KB && ci != INF) {
-          const uint32_t rc = b.route[base + i * KB + j];
-          if (rc != kRouteInvalid) {
-            const double c = ci + fabs((double)rc * 0.01 - gcl) / beta;
-            if (c < best) { best = c; arg = (int)i; }
-          }
+      // issue every route load of this layer at once, then reduce
+      uint32_t rv[kMaxCand];
+#pragma unroll
+      for (int i = 0; i < kMaxCand; ++i)
+        rv[i] = (i < (int)prevK && j < (int)KB) ? b.route[base + i * KB + j] : kRouteInvalid;
+#pragma unroll
+      for (int i = 0; i < kMaxCand; ++i) {
+        if (i >= (int)prevK) break;
+        const double ci = shfl_d(cost, gbase | i);
+        if (ci != INF && rv[i] != kRouteInvalid) {
+          const double c = ci + fabs((double)rv[i] * 0.01 - gcl) / beta;
+          if (c < best) { best = c; arg = i; }
         }
       }
       const unsigned long long any = __ballot(j < (int)KB && arg >= 0);
-      if (((any >> (threadIdx.x & 48)) & 0xffffull) == 0) start = true;
+      if (((any >> gbase) & 0xffffull) == 0) start = true;
     }
     if (s > 0 && prev_ok && (KB == 0 || start)) backtrace_chain(b, o, s - 1, prevK, cost, j);
     if (KB == 0) {
@@ -539,7 +905,7 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
       prev_ok = false; prevK = 0; cost = INF;
       continue;
     }
-    const double em = (j < (int)KB) ? (double)b.cand_sq[l * kMaxCand + j] * inv2s2 : INF;
+    const double em = (j < (int)KB) ? (double)sq * inv2s2 : INF;
     double nc;
     uint8_t bpj;
     if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255; }
@@ -557,19 +923,16 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
 // k_paths: one wave per chosen transition; re-run the search for (i*, j*), compute
 // canonical predecessors and write the directed-edge path into the pool.
 template <bool BIG>
-__global__ void __launch_bounds__(64) k_paths(DevGraph g, DevBatch b) {
+__global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
   constexpr int H = BIG ? kBigH : kSmallH;
   __shared__ SearchSmem<H, true> sm;
   __shared__ uint32_t s_road[1], s_off[1];
   const int lane = threadIdx.x;
-  const uint32_t n_items = BIG ? min(b.ctl[4], (uint32_t)b.P) : (uint32_t)b.P;
-  for (uint64_t item = blockIdx.x; item < n_items; item += (BIG ? gridDim.x : n_items)) {
-    const uint64_t p = BIG ? b.retry_paths[item] : item;
+  const uint32_t n_items = min(b.ctl[BIG ? 6 : 4], (uint32_t)b.P);
+  const uint32_t* list = BIG ? b.rl_paths_b : b.rl_paths_a;
+  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const uint64_t p = list[item];
     const uint32_t k = b.slot_trace[p];
-    const uint32_t o = b.trace_off[k];
-    const uint32_t s = (uint32_t)(p - o);
-    if (s < 1 || s >= b.n_states[k]) continue;
-    if (b.chain_start[p] || b.choice[p] < 0) continue;
     const MatchOptions op = b.opts[b.trace_opt[k]];
     const int mode = op.mode;
     const uint32_t acc = mode_access(mode);
@@ -582,7 +945,7 @@ __global__ void __launch_bounds__(64) k_paths(DevGraph g, DevBatch b) {
     bounded_search<H, true>(sm, g, mode, bound, s_road, s_off, 1);
     if (sm.ovf) {
       if (!BIG) {
-        if (lane == 0) { const uint32_t q = atomicAdd(&b.ctl[4], 1u); b.retry_paths[q] = (uint32_t)p; }
+        if (lane == 0) { const uint32_t q = atomicAdd(&b.ctl[6], 1u); b.rl_paths_b[q] = (uint32_t)p; }
       } else if (lane == 0) {
         atomicOr(&b.ctl[2], kErrSearchOverflow);
       }
@@ -666,14 +1029,15 @@ __global__ void __launch_bounds__(64) k_paths(DevGraph g, DevBatch b) {
 }
 
 // ------------------------------------------------------------------------------------------
-// K4 k_segments: one lane per trace.  Streams traversals of each chain, merges pieces that
-// continue through a state point, and forms OSMLR runs (meili form_segments analogue).
-struct Trav { uint32_t e, b, en; double tb, te; uint32_t sb, se; };
-
+// K4 (segments), in two passes:
+//   k_traversals  one lane per chosen transition: expands its path into 64-byte traversal
+//                 records (edge, [b,en] cm, interpolated times, state indices, OSMLR tags);
+//                 all dependent graph lookups happen here, in parallel
+//   k_segments    one lane per trace: streams its records, merges pieces that continue
+//                 through a state point and forms OSMLR runs (meili form_segments analogue)
 struct RunState {
-  bool open;
-  uint32_t sd, f_e, f_b, l_e, l_en, sb, se, way_first, way_last;
-  bool internal;
+  bool open, internal;
+  uint32_t sd, f_b, f_soff, l_en, l_len, l_soff, seg_len, sb, se, way_first, way_last;
   double tb, te;
   uint64_t tot, q;
 };
@@ -681,14 +1045,13 @@ struct RunState {
 __device__ __forceinline__ void run_close(const DevGraph& g, RunState& R, SegmentRec* out, uint32_t& n) {
   if (!R.open) return;
   const uint32_t sd = R.sd;
-  const uint32_t llen = g.edges[R.l_e].y;
-  const bool start_ok = R.f_b == 0 && (sd == kNone || g.edge_seg_off[R.f_e] == 0);
-  const bool end_ok = R.l_en == llen && (sd == kNone || g.edge_seg_off[R.l_e] + llen == g.seg_len[sd]);
+  const bool start_ok = R.f_b == 0 && (sd == kNone || R.f_soff == 0);
+  const bool end_ok = R.l_en == R.l_len && (sd == kNone || R.l_soff + R.l_len == R.seg_len);
   SegmentRec s;
   s.segment_id = sd == kNone ? kInvalidSegmentId : g.seg_id[sd];
   s.start_time = start_ok ? R.tb : -1.0;
   s.end_time = end_ok ? R.te : -1.0;
-  if (sd != kNone) s.length = (start_ok && end_ok) ? (int32_t)((g.seg_len[sd] + 50u) / 100u) : -1;
+  if (sd != kNone) s.length = (start_ok && end_ok) ? (int32_t)((R.seg_len + 50u) / 100u) : -1;
   else s.length = (int32_t)((R.tot + 50u) / 100u);
   s.queue_length = (int32_t)((R.q + 50u) / 100u);
   s.flags = (sd == kNone && R.internal ? 1u : 0u) | (sd != kNone ? 2u : 0u);
@@ -701,30 +1064,26 @@ __device__ __forceinline__ void run_close(const DevGraph& g, RunState& R, Segmen
   R.open = false;
 }
 
-__device__ __forceinline__ void run_feed(const DevGraph& g, RunState& R, const Trav& t, SegmentRec* out, uint32_t& n) {
-  const uint32_t sd = g.edge_seg[t.e];
-  const uint4 rec = g.edges[t.e];
-  const bool internal = (rec.z & kFlagInternal) != 0u;
-  bool cont = R.open && sd == R.sd;
-  if (cont && sd == kNone && internal != R.internal) cont = false;
+__device__ __forceinline__ void run_feed(const DevGraph& g, RunState& R, const TravRec& t, SegmentRec* out, uint32_t& n) {
+  const bool internal = t.internal != 0u;
+  bool cont = R.open && t.sd == R.sd;
+  if (cont && t.sd == kNone && internal != R.internal) cont = false;
   if (cont) {
-    const uint32_t plen = g.edges[R.l_e].y;
-    if (R.l_en != plen || t.b != 0) cont = false;
-    else if (sd != kNone && g.edge_seg_off[t.e] != g.edge_seg_off[R.l_e] + plen) cont = false;
+    if (R.l_en != R.l_len || t.b != 0) cont = false;
+    else if (t.sd != kNone && t.soff != R.l_soff + R.l_len) cont = false;
   }
   const uint32_t d = t.en - t.b;
   const double dt = t.te - t.tb;
   const bool slow = dt > 0.0 && ((double)d * 0.01) / dt < kQueueSpeedMps;
-  const uint32_t way = g.edge_way[t.e];
   if (!cont) {
     run_close(g, R, out, n);
-    R.open = true; R.sd = sd; R.internal = internal;
-    R.f_e = t.e; R.f_b = t.b; R.tb = t.tb; R.sb = t.sb;
-    R.tot = 0; R.q = 0; R.way_first = way; R.way_last = way;
-  } else if (way != R.way_first) {
-    R.way_last = way;
+    R.open = true; R.sd = t.sd; R.internal = internal; R.seg_len = t.seg_len;
+    R.f_b = t.b; R.f_soff = t.soff; R.tb = t.tb; R.sb = t.sb;
+    R.tot = 0; R.q = 0; R.way_first = t.way; R.way_last = t.way;
+  } else if (t.way != R.way_first) {
+    R.way_last = t.way;
   }
-  R.l_e = t.e; R.l_en = t.en; R.te = t.te; R.se = t.se;
+  R.l_en = t.en; R.l_len = t.len; R.l_soff = t.soff; R.te = t.te; R.se = t.se;
   R.tot += d;
   R.q = slow ? R.q + d : 0;
 }
@@ -734,65 +1093,74 @@ __device__ __forceinline__ double interp_time(double ta, double tb, uint64_t x, 
   return ta + (tb - ta) * ((double)x / (double)D);
 }
 
-// upper bound of segments per trace (one per path edge) -> exclusive scan -> seg_base
-__global__ void __launch_bounds__(64) k_seg_bound(DevBatch b) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= b.T) return;
-  const uint32_t o = b.trace_off[k], S = b.n_states[k];
-  uint32_t bound = 0;
-  for (uint32_t s = 1; s < S; ++s) {
-    const uint64_t l = o + s;
-    if (!b.chain_start[l] && b.choice[l] >= 0) bound += b.path_cnt[l];
+__global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
+  const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= b.P) return;
+  const uint32_t ns = b.path_cnt[l];
+  if (ns == 0) return;  // not a chosen transition
+  const uint32_t k = b.slot_trace[l];
+  const uint32_t o = b.trace_off[k];
+  const uint32_t i = (uint32_t)b.choice[l - 1], j = (uint32_t)b.choice[l];
+  const uint32_t sa = b.cand_s[(l - 1) * kMaxCand + i], sb = b.cand_s[l * kMaxCand + j];
+  const uint32_t oa = b.state_orig[l - 1], ob = b.state_orig[l];
+  const double ta = b.time[o + oa], tb = b.time[o + ob];
+  const uint32_t D = b.route_dist[l];
+  const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
+  TravRec* out = b.trav + b.trav_off[l];
+  uint64_t x = 0;
+  for (uint32_t q = 0; q < ns; ++q) {
+    const uint32_t e = pe[q];
+    const uint4 rec = g.edges[e];
+    const uint32_t L = rec.y;
+    const bool rev = (rec.w & 1u) != 0u;
+    uint32_t b0 = 0, b1 = L;
+    if (q == 0) b0 = rev ? L - sa : sa;
+    if (q + 1 == ns) b1 = rev ? L - sb : sb;
+    TravRec t;
+    t.e = e; t.b = b0; t.en = b1; t.slot = (uint32_t)l;
+    t.tb = interp_time(ta, tb, x, D);
+    x += (uint64_t)(b1 - b0);
+    t.te = interp_time(ta, tb, x, D);
+    t.sb = oa;
+    t.se = (q + 1 == ns) ? ob : oa;
+    t.sd = g.edge_seg[e];
+    t.soff = g.edge_seg_off[e];
+    t.len = L;
+    t.way = g.edge_way[e];
+    t.internal = (rec.z & kFlagInternal) ? 1u : 0u;
+    t.seg_len = t.sd != kNone ? g.seg_len[t.sd] : 0u;
+    out[q] = t;
   }
-  b.seg_cnt[k] = bound;
 }
 
-__global__ void __launch_bounds__(64) k_segments(DevGraph g, DevBatch b) {
+__global__ void __launch_bounds__(64) k_segments(DevGraph g, DevBatch b, uint32_t total) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= b.T) return;
-  const uint32_t o = b.trace_off[k], S = b.n_states[k];
-  SegmentRec* out = b.segs + b.seg_base[k];
+  const uint32_t r0 = b.trav_off[b.trace_off[k]];
+  const uint32_t r1 = (k + 1 < b.T) ? b.trav_off[b.trace_off[k + 1]] : total;
+  b.seg_base[k] = r0;
+  SegmentRec* out = b.segs + r0;
   uint32_t n = 0;
   RunState R;
   R.open = false;
-  Trav pend;
+  TravRec pend;
   bool has_pend = false;
-  for (uint32_t s = 0; s < S; ++s) {
-    const uint64_t l = o + s;
-    if (b.chain_start[l] || b.choice[l] < 0) {
+  uint32_t prev_slot = 0;
+  TravRec nxt;
+  if (r0 < r1) nxt = b.trav[r0];
+  for (uint32_t r = r0; r < r1; ++r) {
+    const TravRec t = nxt;
+    if (r + 1 < r1) nxt = b.trav[r + 1];          // prefetch: records are independent
+    if (r > r0 && t.slot != prev_slot && t.slot != prev_slot + 1) {  // a chain boundary lies between
       if (has_pend) { run_feed(g, R, pend, out, n); has_pend = false; }
       run_close(g, R, out, n);
-      continue;
     }
-    const uint32_t i = (uint32_t)b.choice[l - 1], j = (uint32_t)b.choice[l];
-    const uint32_t sa = b.cand_s[(l - 1) * kMaxCand + i], sb = b.cand_s[l * kMaxCand + j];
-    const uint32_t oa = b.state_orig[l - 1], ob = b.state_orig[l];
-    const double ta = b.time[o + oa], tb = b.time[o + ob];
-    const uint32_t D = b.route_dist[l];
-    const uint32_t ns = b.path_cnt[l];
-    const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
-    uint64_t x = 0;
-    for (uint32_t q = 0; q < ns; ++q) {
-      const uint32_t e = pe[q];
-      const uint4 rec = g.edges[e];
-      const uint32_t L = rec.y;
-      const bool rev = (rec.w & 1u) != 0u;
-      uint32_t b0 = 0, b1 = L;
-      if (q == 0) b0 = rev ? L - sa : sa;
-      if (q + 1 == ns) b1 = rev ? L - sb : sb;
-      Trav t;
-      t.e = e; t.b = b0; t.en = b1;
-      t.tb = interp_time(ta, tb, x, D);
-      x += (uint64_t)(b1 - b0);
-      t.te = interp_time(ta, tb, x, D);
-      t.sb = oa;
-      t.se = (q + 1 == ns) ? ob : oa;
-      if (t.en == t.b) continue;
-      if (has_pend && pend.e == t.e && pend.en == t.b) { pend.en = t.en; pend.te = t.te; pend.se = t.se; continue; }
-      if (has_pend) run_feed(g, R, pend, out, n);
-      pend = t;
-      has_pend = true;
-    }
+    prev_slot = t.slot;
+    if (t.en == t.b) continue;
+    if (has_pend && pend.e == t.e && pend.en == t.b) { pend.en = t.en; pend.te = t.te; pend.se = t.se; continue; }
+    if (has_pend) run_feed(g, R, pend, out, n);
+    pend = t;
+    has_pend = true;
   }
   if (has_pend) run_feed(g, R, pend, out, n);
   run_close(g, R, out, n);
@@ -899,6 +1267,16 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   dg_.edges = (const uint4*)upload(allocs_, g.edges);
   uint32_t* esrc = dalloc<uint32_t>(allocs_, g.num_edges());
   dg_.edge_src = esrc;
+  {
+    // in-edge CSR sorted by target, edge ids ascending within a node (canonical predecessors)
+    std::vector<uint32_t> in_off(g.num_nodes() + 1, 0), in_edge(g.num_edges());
+    for (uint32_t e = 0; e < g.num_edges(); ++e) in_off[g.edges[e].target + 1]++;
+    for (uint32_t n = 0; n < g.num_nodes(); ++n) in_off[n + 1] += in_off[n];
+    std::vector<uint32_t> fill(in_off.begin(), in_off.end() - 1);
+    for (uint32_t e = 0; e < g.num_edges(); ++e) in_edge[fill[g.edges[e].target]++] = e;
+    dg_.in_off = upload(allocs_, in_off);
+    dg_.in_edge = upload(allocs_, in_edge);
+  }
   dg_.edge_seg = upload(allocs_, g.edge_seg);
   dg_.edge_seg_off = upload(allocs_, g.edge_seg_off);
   dg_.edge_way = upload(allocs_, g.edge_way);
@@ -935,7 +1313,7 @@ Workspace::~Workspace() { release(); }
 void Workspace::release() {
   for (void* p : allocs) (void)hipFree(p);
   allocs.clear();
-  cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = 0;
+  cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = cap_src = 0;
 }
 
 Matcher::Matcher(Engine* e) : eng_(e) {
@@ -960,7 +1338,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   const uint64_t cp = std::max<uint64_t>(points, w.cap_points) + 64;
   const uint64_t ct = std::max<uint64_t>(traces, w.cap_traces) + 16;
   const uint64_t co = std::max<uint64_t>(nopts, w.cap_opts) + 4;
-  const uint64_t keep_trans = w.cap_trans, keep_path = w.cap_path, keep_segs = w.cap_segs;
+  const uint64_t keep_trans = w.cap_trans, keep_path = w.cap_path, keep_segs = w.cap_segs, keep_src = w.cap_src;
   w.release();
   std::vector<void*>& L = w.allocs;
   w.trace_off = dalloc<uint32_t>(L, ct + 1);
@@ -970,32 +1348,43 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.cand_n = dalloc<uint8_t>(L, cp); w.cand_road = dalloc<uint32_t>(L, cp * kMaxCand);
   w.cand_s = dalloc<uint32_t>(L, cp * kMaxCand); w.cand_sq = dalloc<float>(L, cp * kMaxCand);
   w.trans_cnt = dalloc<uint32_t>(L, cp); w.trans_off = dalloc<uint32_t>(L, cp); w.gc = dalloc<double>(L, cp);
+  w.src_cnt = dalloc<uint32_t>(L, cp); w.src_off = dalloc<uint32_t>(L, cp);
   w.choice = dalloc<int8_t>(L, cp); w.chain_start = dalloc<uint8_t>(L, cp); w.bp = dalloc<uint8_t>(L, cp * kMaxCand);
   w.path_off = dalloc<uint32_t>(L, cp); w.path_cnt = dalloc<uint32_t>(L, cp); w.route_dist = dalloc<uint32_t>(L, cp);
   w.path_inline = dalloc<uint32_t>(L, cp * kInlinePath);
+  w.trav_off = dalloc<uint32_t>(L, cp);
   w.seg_base = dalloc<uint32_t>(L, ct); w.seg_cnt = dalloc<uint32_t>(L, ct);
   w.rep_cnt = dalloc<uint32_t>(L, ct); w.stats = dalloc<ReportStats>(L, ct);
   w.ctl = dalloc<uint32_t>(L, 8);
-  w.retry_routes = dalloc<uint32_t>(L, cp); w.retry_paths = dalloc<uint32_t>(L, cp);
+  w.rl_routes_a = dalloc<uint32_t>(L, cp); w.rl_routes_b = dalloc<uint32_t>(L, cp);
+  w.rl_paths_a = dalloc<uint32_t>(L, cp); w.rl_paths_b = dalloc<uint32_t>(L, cp);
+  w.rl_cand = dalloc<uint32_t>(L, cp);
   size_t tmp = 0;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, w.trans_cnt, w.trans_off, (int)cp, stream_));
   w.scan_tmp_bytes = tmp;
   w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
-  w.route = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr;
-  w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0;
-  ensure_trans(std::max<uint64_t>(keep_trans, 1));
+  w.route = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
+  w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
+  ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
   ensure_path(std::max<uint64_t>(keep_path, cp / 8 + 1024));
   ensure_segs(std::max<uint64_t>(keep_segs, cp / 2 + 1024));
 }
 
-void Matcher::ensure_trans(uint64_t n) {
+void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
   Workspace& w = ws_;
-  if (n <= w.cap_trans && w.route) return;
-  if (w.route) { (void)hipFree(w.route); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.route)); }
-  const uint64_t c = n + n / 4 + 1024;
-  w.route = dalloc<uint32_t>(w.allocs, c);
-  w.cap_trans = c;
+  if (!(n <= w.cap_trans && w.route)) {
+    if (w.route) { (void)hipFree(w.route); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.route)); }
+    const uint64_t c = n + n / 4 + 1024;
+    w.route = dalloc<uint32_t>(w.allocs, c);
+    w.cap_trans = c;
+  }
+  if (!(n_src <= w.cap_src && w.src_item)) {
+    if (w.src_item) { (void)hipFree(w.src_item); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.src_item)); }
+    const uint64_t c = n_src + n_src / 4 + 1024;
+    w.src_item = dalloc<uint32_t>(w.allocs, c);
+    w.cap_src = c;
+  }
 }
 
 static void free_one(Workspace& w, void* q) {
@@ -1018,9 +1407,11 @@ void Matcher::ensure_segs(uint64_t n) {
   if (n <= w.cap_segs && w.segs) return;
   free_one(w, w.segs);
   free_one(w, w.reps);
+  free_one(w, w.trav);
   const uint64_t c = n + n / 4 + 1024;
   w.segs = dalloc<SegmentRec>(w.allocs, c);
   w.reps = dalloc<ReportRec>(w.allocs, c);
+  w.trav = dalloc<TravRec>(w.allocs, c);
   w.cap_segs = c;
 }
 
@@ -1068,13 +1459,16 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig;
   v.cand_n = w.cand_n; v.cand_road = w.cand_road; v.cand_s = w.cand_s; v.cand_sq = w.cand_sq;
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route;
+  v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
   v.path_pool = w.path_pool; v.path_cap = w.cap_path;
   v.route_dist = w.route_dist;
   v.segs = w.segs; v.seg_base = w.seg_base; v.seg_cnt = w.seg_cnt;
+  v.trav = w.trav; v.trav_off = w.trav_off;
   v.reps = w.reps; v.rep_cnt = w.rep_cnt; v.stats = w.stats;
-  v.ctl = w.ctl; v.retry_routes = w.retry_routes; v.retry_paths = w.retry_paths;
+  v.ctl = w.ctl; v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b;
+  v.rl_paths_a = w.rl_paths_a; v.rl_paths_b = w.rl_paths_b; v.rl_cand = w.rl_cand;
   return v;
 }
 
@@ -1116,40 +1510,59 @@ void Matcher::run_device(const RunParams& rp) {
   if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 16 * sizeof(uint32_t), hipHostMallocDefault));
   RM_HIP(hipMemsetAsync(w.ctl, 0, 8 * sizeof(uint32_t), st));
   RM_HIP(hipMemsetAsync(w.choice, 0xff, P, st));
+  RM_HIP(hipMemsetAsync(w.path_cnt, 0, P * sizeof(uint32_t), st));
   DevBatch v = make_view(w, T, P);
 
   tic(kKStates);
   hipLaunchKernelGGL(k_states, dim3((T + 63) / 64), dim3(64), 0, st, v);
   toc(kKStates);
   tic(kKCandidates);
-  hipLaunchKernelGGL(k_candidates, dim3((uint32_t)P), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_candidates_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, g, v);
   toc(kKCandidates);
   tic(kKScan);
   hipLaunchKernelGGL(k_trans_count, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
   size_t tmp = w.scan_tmp_bytes;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.trans_cnt, w.trans_off, (int)P, st));
+  tmp = w.scan_tmp_bytes;
+  RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.src_cnt, w.src_off, (int)P, st));
   toc(kKScan);
   RM_HIP(hipMemcpyAsync(hctl_ + 8, w.trans_off + (P - 1), 4, hipMemcpyDeviceToHost, st));
   RM_HIP(hipMemcpyAsync(hctl_ + 9, w.trans_cnt + (P - 1), 4, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipMemcpyAsync(hctl_ + 12, w.src_off + (P - 1), 4, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipMemcpyAsync(hctl_ + 13, w.src_cnt + (P - 1), 4, hipMemcpyDeviceToHost, st));
   RM_HIP(hipStreamSynchronize(st));
   const uint64_t total = (uint64_t)hctl_[8] + hctl_[9];
+  const uint64_t n_src = (uint64_t)hctl_[12] + hctl_[13];
   if (total >= 0xffffffffull) throw std::runtime_error("batch too large (transitions >= 2^32); split it");
   n_trans_ = total;
-  ensure_trans(total);
+  ensure_trans(total, n_src);
   v.route = w.route;
+  v.src_item = w.src_item;
 
   tic(kKRoutes);
-  hipLaunchKernelGGL(k_routes<false>, dim3((uint32_t)P), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes<true>, dim3(1024), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
+  if (n_src)
+    hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
+  hipLaunchKernelGGL(k_routes_wave<false>, dim3(2048), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave<true>, dim3(1024), dim3(64), 0, st, g, v);
   toc(kKRoutes);
   tic(kKViterbi);
   hipLaunchKernelGGL(k_viterbi, dim3((T + 3) / 4), dim3(64), 0, st, v);
   toc(kKViterbi);
   for (int attempt = 0;; ++attempt) {
     tic(kKPaths);
-    hipLaunchKernelGGL(k_paths<false>, dim3((uint32_t)P), dim3(64), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths<true>, dim3(1024), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_wave<false>, dim3(2048), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_wave<true>, dim3(1024), dim3(64), 0, st, g, v);
     toc(kKPaths);
+    // traversal records are laid out by a scan of path_cnt (0 for slots without a chosen transition)
+    tic(kKSegments);
+    tmp = w.scan_tmp_bytes;
+    RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
+    toc(kKSegments);
+    RM_HIP(hipMemcpyAsync(hctl_ + 10, w.trav_off + (P - 1), 4, hipMemcpyDeviceToHost, st));
+    RM_HIP(hipMemcpyAsync(hctl_ + 11, w.path_cnt + (P - 1), 4, hipMemcpyDeviceToHost, st));
     RM_HIP(hipMemcpyAsync(hctl_, w.ctl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     RM_HIP(hipStreamSynchronize(st));
     if (!(hctl_[2] & kErrPathOverflow)) break;
@@ -1159,23 +1572,20 @@ void Matcher::run_device(const RunParams& rp) {
     const uint32_t clear_bits = ~kErrPathOverflow;
     (void)clear_bits;
     RM_HIP(hipMemsetAsync(w.ctl, 0, sizeof(uint32_t), st));          // path_used
-    RM_HIP(hipMemsetAsync(w.ctl + 4, 0, sizeof(uint32_t), st));      // retry count (paths)
+    RM_HIP(hipMemsetAsync(w.ctl + 4, 0, sizeof(uint32_t), st));      // paths list A
+    RM_HIP(hipMemsetAsync(w.ctl + 6, 0, sizeof(uint32_t), st));      // paths list B
     uint32_t flags = hctl_[2] & ~kErrPathOverflow;
     RM_HIP(hipMemcpyAsync(w.ctl + 2, &flags, sizeof(uint32_t), hipMemcpyHostToDevice, st));
     RM_HIP(hipStreamSynchronize(st));
   }
-  tic(kKSegments);
-  hipLaunchKernelGGL(k_seg_bound, dim3((T + 63) / 64), dim3(64), 0, st, v);
-  tmp = w.scan_tmp_bytes;
-  RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.seg_cnt, w.seg_base, (int)T, st));
-  RM_HIP(hipMemcpyAsync(hctl_ + 10, w.seg_base + (T - 1), 4, hipMemcpyDeviceToHost, st));
-  RM_HIP(hipMemcpyAsync(hctl_ + 11, w.seg_cnt + (T - 1), 4, hipMemcpyDeviceToHost, st));
-  RM_HIP(hipStreamSynchronize(st));
   const uint64_t seg_total = (uint64_t)hctl_[10] + hctl_[11];
-  n_path_ = seg_total;  // one segment slot per chained path edge
+  if (seg_total >= 0xffffffffull) throw std::runtime_error("batch too large (path edges >= 2^32); split it");
+  n_path_ = seg_total;  // one traversal record (and at most one segment) per chosen path edge
   ensure_segs(seg_total);
-  v.segs = w.segs; v.reps = w.reps;
-  hipLaunchKernelGGL(k_segments, dim3((T + 63) / 64), dim3(64), 0, st, g, v);
+  v.segs = w.segs; v.reps = w.reps; v.trav = w.trav;
+  tic(kKSegments);
+  hipLaunchKernelGGL(k_traversals, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_segments, dim3((T + 63) / 64), dim3(64), 0, st, g, v, (uint32_t)seg_total);
   toc(kKSegments);
   if (rp.do_report) {
     if (rp.hist && rp.zero_hist)
@@ -1256,6 +1666,13 @@ void Matcher::get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, 
     std::memcpy(pool + at, src, n * 4ull);
     at += n;
   }
+}
+
+void Matcher::tier_counts(uint32_t* out4) {
+  sync();
+  uint32_t c[8];
+  RM_HIP(hipMemcpy(c, ws_.ctl, sizeof c, hipMemcpyDeviceToHost));
+  out4[0] = c[3]; out4[1] = c[5]; out4[2] = c[4]; out4[3] = c[7];
 }
 
 uint64_t Matcher::count_segments() {

@@ -29,6 +29,8 @@ struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   const uint32_t* node_off;
   const uint4* edges;            // EdgeRec
   const uint32_t* edge_src;      // source node of each directed edge
+  const uint32_t* in_off;        // in-edge CSR offsets (N+1)
+  const uint32_t* in_edge;       // edge ids by target node, ascending
   const uint32_t* edge_seg;
   const uint32_t* edge_seg_off;
   const uint32_t* edge_way;
@@ -75,7 +77,7 @@ extern const char* const kKernelNames[kNumKernels];
 // Device workspace of one batch.  All arrays are indexed by point slot p
 // (state s of trace k lives at slot trace_off[k] + s).
 struct Workspace {
-  uint64_t cap_points = 0, cap_traces = 0, cap_trans = 0, cap_path = 0, cap_opts = 0, cap_segs = 0;
+  uint64_t cap_points = 0, cap_traces = 0, cap_trans = 0, cap_path = 0, cap_opts = 0, cap_segs = 0, cap_src = 0;
   // inputs
   uint32_t* trace_off = nullptr; float* lon = nullptr; float* lat = nullptr; double* time = nullptr;
   float* acc = nullptr; MatchOptions* opts = nullptr; uint32_t* trace_opt = nullptr;
@@ -83,16 +85,19 @@ struct Workspace {
   uint32_t* slot_trace = nullptr; uint32_t* n_states = nullptr; uint32_t* state_orig = nullptr;
   uint8_t* cand_n = nullptr; uint32_t* cand_road = nullptr; uint32_t* cand_s = nullptr; float* cand_sq = nullptr;
   uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr;
+  uint32_t* src_cnt = nullptr; uint32_t* src_off = nullptr; uint32_t* src_item = nullptr;
   int8_t* choice = nullptr; uint8_t* chain_start = nullptr; uint8_t* bp = nullptr;
   uint32_t* path_off = nullptr; uint32_t* path_cnt = nullptr; uint32_t* path_pool = nullptr; uint32_t* route_dist = nullptr;
   uint32_t* path_inline = nullptr;  // kInlinePath edges per slot
   // per trace outputs
   SegmentRec* segs = nullptr; uint32_t* seg_base = nullptr; uint32_t* seg_cnt = nullptr;
+  TravRec* trav = nullptr; uint32_t* trav_off = nullptr;  // traversal records (K4 pass 1)
   ReportRec* reps = nullptr; uint32_t* rep_cnt = nullptr; ReportStats* stats = nullptr;
-  // control words: [0] path_used [1] seg_used [2] error flags [3] retry count (routes)
-  // [4] retry count (paths) [5] cand overflow [6..7] spare
+  // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
+  // [5] routes list B [6] paths list B [7] candidates list (overflow lists of the lane tiers)
   uint32_t* ctl = nullptr;
-  uint32_t* retry_routes = nullptr; uint32_t* retry_paths = nullptr;
+  uint32_t* rl_routes_a = nullptr; uint32_t* rl_routes_b = nullptr;
+  uint32_t* rl_paths_a = nullptr; uint32_t* rl_paths_b = nullptr; uint32_t* rl_cand = nullptr;
   void* scan_tmp = nullptr; size_t scan_tmp_bytes = 0;
   std::vector<void*> allocs;
   ~Workspace();
@@ -136,13 +141,15 @@ class Matcher {
   uint64_t count_reports();
   // accumulated kernel time (ms) per KernelId since the last reset
   void kernel_times(double* ms, uint64_t* launches);
+  // overflow-list sizes of the last run: routes A, routes B, paths A, candidates
+  void tier_counts(uint32_t* out4);
   void reset_kernel_times();
   void set_timing(bool on) { timing_ = on; }
   hipStream_t stream() const { return stream_; }
 
  private:
   void ensure(uint64_t points, uint32_t traces, uint32_t nopts);
-  void ensure_trans(uint64_t n);
+  void ensure_trans(uint64_t n, uint64_t n_src);
   void ensure_path(uint64_t n);
   void ensure_segs(uint64_t n);
   void tic(int k);

@@ -163,6 +163,15 @@ struct ReportRec {
 };
 static_assert(sizeof(ReportRec) == 48, "ReportRec layout is shared with oracle/meili_oracle.h");
 
+// ---- traversal record: one piece of a chosen path with its times and OSMLR tags ----
+struct TravRec {
+  uint32_t e, b, en, slot;          // directed edge, [b, en] cm along it, transition slot
+  double tb, te;                    // interpolated epoch times at b and en
+  uint32_t sb, se, sd, soff;        // state indices at/before b and en, dense segment, edge offset in segment
+  uint32_t len, way, internal, seg_len;
+};
+static_assert(sizeof(TravRec) == 64, "TravRec is four dwordx4");
+
 struct ReportStats {        // per trace (reporter_service.py:164-177)
   int32_t successful_count, unreported_count;
   int32_t successful_length_m, unreported_length_m;  // last assigned length (m), -1 if never

@@ -148,9 +148,10 @@ class BatchMatcher:
         _lib.check(_lib.lib().rm_runner_rerun(self._h, C.byref(rp)))
 
     def sizes(self):
-        out = (C.c_uint64 * 6)()
+        out = (C.c_uint64 * 10)()
         _lib.check(_lib.lib().rm_runner_sizes(self._h, out))
-        return dict(zip(("points", "traces", "transitions", "path_edges", "segments", "reports"), [int(x) for x in out]))
+        return dict(zip(("points", "traces", "transitions", "path_edges", "segments", "reports", "routes_tier2",
+                         "routes_tier3", "paths_tier2", "cand_tier2"), [int(x) for x in out]))
 
     # ---- stage outputs (parity tests) ----
     def states(self):
