@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--traces", type=int, default=0, help="override traces per rank")
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (default min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_routes_c2.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_routes_c2.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per routes launch (optional)")
     return ap.parse_args()
 
@@ -212,7 +212,7 @@ def main():
                                % (world, nseg),
             },
             "roofline": {
-                "kernel": "k_routes (K2, bounded route search; small + retry tier per step)",
+                "kernel": "K2 route stage: k_src_items + k_routes_lane + overflow wave tiers (one launch each per step)",
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,

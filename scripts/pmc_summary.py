@@ -69,12 +69,17 @@ def main():
         summary[k] = e
     with open(os.path.join(a.out, "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
-    r = summary.get("k_routes<false>", {})
-    rt = {"config": a.config, "traces": a.traces, "kernel": "k_routes<false>",
-          "hbm_bytes_per_launch": (r.get("hbm_read_bytes_corrected", 0) + r.get("hbm_write_bytes", 0)) or None,
-          "hbm_read_bytes_raw": r.get("hbm_read_bytes_raw"), "hbm_write_bytes": r.get("hbm_write_bytes"),
-          "l2_hit_rate": r.get("l2_hit_rate"),
-          "note": "per-dispatch averages from separate --pmc passes; read side doubled per MI355X_MICROARCH.md HBM"}
+    # the K2 stage = every kernel bench.py times as "routes" (each runs once per step)
+    stage = [k for k in summary if k in ("k_src_items", "k_routes_lane", "k_routes_wave<false>", "k_routes_wave<true>",
+                                         "k_routes<false>", "k_routes<true>")]
+    tot = lambda key: sum(summary[k].get(key, 0) for k in stage)
+    hits, miss = tot("TCC_HIT_sum"), tot("TCC_MISS_sum")
+    rt = {"config": a.config, "traces": a.traces, "kernels": sorted(stage),
+          "hbm_bytes_per_launch": (tot("hbm_read_bytes_corrected") + tot("hbm_write_bytes")) or None,
+          "hbm_read_bytes_raw": tot("hbm_read_bytes_raw"), "hbm_write_bytes": tot("hbm_write_bytes"),
+          "l2_hit_rate": hits / (hits + miss) if hits + miss else None,
+          "note": "per-step sums of per-dispatch averages from separate --pmc passes; read side doubled per "
+                  "MI355X_MICROARCH.md HBM"}
     with open(os.path.join(a.out, "pmc_routes_%s.json" % a.config.lower()), "w") as f:
         json.dump(rt, f, indent=1)
     for k in sorted(summary, key=lambda x: -summary[x].get("FETCH_SIZE", 0))[:12]:
