@@ -15,7 +15,8 @@
 //   k_viterbi     K3, one 16-lane group per trace: fp64 costs in registers,
 //                 shuffle broadcast of the previous layer, back-pointers, backtrace
 //   k_paths       one wave per chosen transition: re-search + canonical predecessors
-//   k_segments    K4, one lane per trace: traversals, time interpolation, OSMLR runs
+//   k_traversals / k_run_flags / k_runs   K4: traversal records, time interpolation,
+//                 OSMLR runs (parallel over records and runs)
 //   k_report      A8 epilogue, one lane per trace: report() + speed histogram
 //
 // All arithmetic follows rm_common.hpp; compiled with -ffp-contract=off so the
@@ -51,12 +52,13 @@ struct DevBatch {  // POD view of the workspace for kernels
   const MatchOptions* opts; const uint32_t* trace_opt;
   uint32_t* slot_trace; uint32_t* n_states; uint32_t* state_orig;
   uint8_t* cand_n; uint32_t* cand_road; uint32_t* cand_s; float* cand_sq;
-  uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route;
+  uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route; double* tcost;
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
   SegmentRec* segs; uint32_t* seg_base; uint32_t* seg_cnt;
   TravRec* trav; uint32_t* trav_off;
+  uint8_t* run_kind; uint32_t* run_head; uint32_t* run_idx; uint32_t* run_pos;
   ReportRec* reps; uint32_t* rep_cnt; ReportStats* stats;
   // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list
@@ -95,22 +97,39 @@ __device__ __forceinline__ uint32_t time_bound(double dt, const MatchOptions& o)
 // ------------------------------------------------------------------------------------------
 // k_states: interpolation rule (points closer than interpolation_distance to the last
 // state are not states; meili MapMatcher::OfflineMatch)
+// One lane per trace (the last-state chain is sequential); coordinates are prefetched
+// eight points ahead so the fp64 distance chain does not wait on memory.
 __global__ void __launch_bounds__(64) k_states(DevBatch b) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= b.T) return;
   const uint32_t o = b.trace_off[k], n = b.trace_off[k + 1] - o;
   const MatchOptions op = b.opts[b.trace_opt[k]];
   const double interp = (double)op.interpolation_distance;
-  uint32_t ns = 0, last = 0;
+  uint32_t ns = 0;
   float llon = 0.f, llat = 0.f;
-  for (uint32_t i = 0; i < n; ++i) {
-    b.slot_trace[o + i] = k;
-    const float lo = b.lon[o + i], la = b.lat[o + i];
-    if (i > 0 && gc_distance(llon, llat, lo, la) < interp) continue;
-    b.state_orig[o + ns++] = i;
-    last = i; llon = lo; llat = la;
+  float clo[8], cla[8], nlo[8], nla[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { clo[q] = q < (int)n ? b.lon[o + q] : 0.f; cla[q] = q < (int)n ? b.lat[o + q] : 0.f; }
+  for (uint32_t i0 = 0; i0 < n; i0 += 8) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t i = i0 + 8 + q;
+      nlo[q] = i < n ? b.lon[o + i] : 0.f;
+      nla[q] = i < n ? b.lat[o + i] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t i = i0 + q;
+      if (i >= n) break;
+      b.slot_trace[o + i] = k;
+      const float lo = clo[q], la = cla[q];
+      if (i > 0 && gc_distance(llon, llat, lo, la) < interp) continue;
+      b.state_orig[o + ns++] = i;
+      llon = lo; llat = la;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { clo[q] = nlo[q]; cla[q] = nla[q]; }
   }
-  (void)last;
   b.n_states[k] = ns;
 }
 
@@ -367,6 +386,13 @@ __global__ void k_src_items(DevBatch b) {
   if (p >= b.P) return;
   const uint32_t n = b.src_cnt[p], at = b.src_off[p];
   for (uint32_t i = 0; i < n; ++i) b.src_item[at + i] = (uint32_t)p;
+}
+
+// transition cost |route_m - gc| / beta (meili TransitionCostModel restatement, fp64),
+// +inf for an invalid route; computed where the route is, so K3's inner step is one add
+__device__ __forceinline__ double trans_cost(uint32_t r, double gc, double beta) {
+  if (r == kRouteInvalid) return __longlong_as_double(0x7ff0000000000000ll);
+  return fabs((double)r * 0.01 - gc) / beta;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -628,7 +654,7 @@ __device__ __forceinline__ unsigned long long lane_route_to(const LaneSearch& S,
 // K2 lane tier: one lane per (layer pair, source) item.  A pair any of whose searches
 // outgrows the registers is queued once (the src_cnt word is consumed as a flag) for
 // the wave tier, which recomputes the whole pair.
-__global__ void __launch_bounds__(256) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_items) return;
   const uint32_t p = b.src_item[t];
@@ -654,18 +680,37 @@ __global__ void __launch_bounds__(256) k_routes_lane(DevGraph g, DevBatch b, uin
     }
     return;
   }
-  uint32_t* out = b.route + b.trans_off[p] + i * KB;
+  // targets four at a time with clamped (branch-free) loads; results go to LDS and are
+  // stored after the last load (a store before a load-use costs a full round trip)
+  __shared__ uint32_t s_res[kMaxCand][256];
+  const uint64_t rowb = (uint64_t)p * kMaxCand;
+  for (uint32_t j0 = 0; j0 < KB; j0 += 4) {
+    uint32_t rb[4], sb[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const uint32_t jc = min(j0 + x, KB - 1u);
+      rb[x] = b.cand_road[rowb + jc];
+      sb[x] = b.cand_s[rowb + jc];
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const unsigned long long key = lane_route_to(S, g, mode, acc, ra, sa, rb[x], sb[x], nullptr);
+      uint32_t r = kRouteInvalid;
+      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
+      s_res[(j0 + x) & (kMaxCand - 1)][threadIdx.x] = r;
+    }
+  }
+  const uint64_t ob = (uint64_t)b.trans_off[p] + i * KB;
+  const double beta = (double)op.beta;
   for (uint32_t j = 0; j < KB; ++j) {
-    const uint32_t rb = b.cand_road[(uint64_t)p * kMaxCand + j], sb = b.cand_s[(uint64_t)p * kMaxCand + j];
-    const unsigned long long key = lane_route_to(S, g, mode, acc, ra, sa, rb, sb, nullptr);
-    uint32_t r = kRouteInvalid;
-    if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
-    out[j] = r;
+    const uint32_t r = s_res[j][threadIdx.x];
+    b.route[ob + j] = r;
+    b.tcost[ob + j] = trans_cost(r, gc, beta);
   }
 }
 
 // path lane tier: one lane per chosen transition; canonical predecessors in registers.
-__global__ void __launch_bounds__(256) k_paths_lane(DevGraph g, DevBatch b) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_paths_lane(DevGraph g, DevBatch b) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
   const uint32_t k = b.slot_trace[p];
@@ -691,20 +736,25 @@ __global__ void __launch_bounds__(256) k_paths_lane(DevGraph g, DevBatch b) {
   int combo = -1;
   const unsigned long long key = lane_route_to(S, g, mode, acc, ra, sa, rb, sb, &combo);
   const uint32_t n1a = g.road_node1[ra], n0a = g.road_node0[ra];
-  b.route_dist[p] = key_dist(key);
   uint32_t* inl = b.path_inline + p * kInlinePath;
   if (combo <= 1) {
-    inl[0] = combo == 0 ? g.road_fwd[ra] : g.road_rev[ra];
+    const uint32_t e = combo == 0 ? g.road_fwd[ra] : g.road_rev[ra];
+    b.route_dist[p] = key_dist(key);
+    inl[0] = e;
     b.path_cnt[p] = 1;
     b.path_off[p] = 0;
     return;
   }
   // walk back from the entry node; the canonical predecessor of a non-root node is the
-  // smallest-id tight in-edge from a labelled node (in-edges are sorted by edge id)
+  // smallest-id tight in-edge from a labelled node (in-edges are sorted by edge id).
+  // Edges are shifted into registers (front = travel order) and stored after the walk:
+  // a store inside the walk would make every following load wait for it (shared vmcnt).
   const uint32_t entry_e = combo == 2 ? g.road_fwd[rb] : g.road_rev[rb];
   const uint32_t v0 = combo == 2 ? g.road_node0[rb] : g.road_node1[rb];
   uint32_t n = 1, x = v0;
-  inl[0] = entry_e;                               // reversed order while walking
+  uint32_t pr[kInlinePath];
+#pragma unroll
+  for (int q = 0; q < kInlinePath; ++q) pr[q] = entry_e;
   for (int guard = 0;; ++guard) {
     const unsigned long long lx = ls_label(S, x);
     if (lx == kKeyInf || guard > kLaneCap) { atomicOr(&b.ctl[2], kErrRounds); return; }
@@ -719,16 +769,23 @@ __global__ void __launch_bounds__(256) k_paths_lane(DevGraph g, DevBatch b) {
       if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { pe = e; pu = u; break; }
     }
     if (pe == kNone) { atomicOr(&b.ctl[2], kErrRounds); return; }
-    if (n < (uint32_t)kInlinePath) inl[n] = pe;
+#pragma unroll
+    for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
+    pr[0] = pe;
     ++n;
     x = pu;
   }
   const uint32_t exit_e = (x == n1a) ? g.road_fwd[ra] : g.road_rev[ra];
-  if (n < (uint32_t)kInlinePath) inl[n] = exit_e;
+#pragma unroll
+  for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
+  pr[0] = exit_e;
   ++n;
+  b.route_dist[p] = key_dist(key);
   b.path_cnt[p] = n;
   if (n <= (uint32_t)kInlinePath) {
-    for (uint32_t a = 0, c = n - 1; a < c; ++a, --c) { const uint32_t t = inl[a]; inl[a] = inl[c]; inl[c] = t; }
+#pragma unroll
+    for (int q = 0; q < kInlinePath; ++q)
+      if ((uint32_t)q < n) inl[q] = pr[q];
     b.path_off[p] = 0;
     return;
   }
@@ -798,6 +855,7 @@ __global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
         uint32_t out = kRouteInvalid;
         if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
         b.route[base + t] = out;
+        b.tcost[base + t] = trans_cost(out, gc, (double)op.beta);
       }
     } else {
       for (uint32_t i = 0; i < KA; ++i) {
@@ -809,6 +867,7 @@ __global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
           uint32_t out = kRouteInvalid;
           if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
           b.route[base + i * KB + j] = out;
+          b.tcost[base + i * KB + j] = trans_cost(out, gc, (double)op.beta);
         }
         __syncthreads();
       }
@@ -825,8 +884,44 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
   return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-__device__ void backtrace_chain(const DevBatch& b, uint32_t o, uint32_t end, uint32_t K, double cost, int j) {
-  // argmin over the group's lanes, lowest j on ties
+// LDS per 16-lane trace group.  The forward pass never touches global memory inside a
+// layer: on gfx9 loads and stores share vmcnt, so one pending store would make the next
+// load-use wait for it.  Each chunk of <=16 layers is staged with branch-free loads,
+// processed out of LDS (routes, emissions, previous-layer costs), and its back-pointer
+// rows and chain flags are flushed with one coalesced store per lane at the chunk end.
+constexpr int kVitChunk = 16;      // layers per staged chunk (one per lane of the group)
+constexpr int kVitRouteCap = 160;  // transition costs per staged chunk
+constexpr int kVitBpBlock = 16;    // layers per staged back-pointer block (backtrace)
+struct VitGroupSmem {
+  double tc[kVitRouteCap];             // transition costs (reads use clamped indices)
+  float sq[kVitChunk][16];
+  double cost[16];                     // costs of the previous layer
+  uint32_t kb[kVitChunk], rel[kVitChunk];
+  double gc[kVitChunk];
+  uint8_t bpo[kVitChunk][16];          // this chunk's back-pointer rows
+  uint8_t cs[kVitChunk];               // this chunk's chain-start flags
+  uint4 bp[kVitBpBlock];               // backtrace staging
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// write rows [s0, s0+n) of the chunk to global (lane q owns layer s0+q)
+__device__ __forceinline__ void vit_flush(const DevBatch& b, const VitGroupSmem& gs, uint64_t l0, uint32_t n, int j) {
+  if ((uint32_t)j < n) {
+    *reinterpret_cast<uint4*>(b.bp + (l0 + j) * kMaxCand) = *reinterpret_cast<const uint4*>(gs.bpo[j]);
+    b.chain_start[l0 + j] = gs.cs[j];
+  }
+}
+
+// Backtrace of the chain ending at layer `end` (costs of that layer in `cost`).  The winner
+// is the lowest-cost candidate (lowest j on ties); back-pointers are staged 64 layers at a
+// time; a layer whose winner's back-pointer is 255 starts the chain.
+__device__ void backtrace_chain(const DevBatch& b, VitGroupSmem& gs, uint32_t o, uint32_t end, uint32_t K,
+                                double cost, int j) {
   double bc = (j < (int)K) ? cost : __longlong_as_double(0x7ff0000000000000ll);
   int bj = (j < (int)K) ? j : 1 << 20;
   for (int off = 8; off > 0; off >>= 1) {
@@ -834,89 +929,155 @@ __device__ void backtrace_chain(const DevBatch& b, uint32_t o, uint32_t end, uin
     const int oj = __shfl(bj, (j + off) & 15, 16);
     if (oc < bc || (oc == bc && oj < bj)) { bc = oc; bj = oj; }
   }
-  bj = __shfl(bj, 0, 16);
-  __threadfence_block();
-  if (j == 0) {
-    int w = bj;
-    uint32_t t = end;
-    for (;;) {
-      b.choice[o + t] = (int8_t)w;
-      if (b.chain_start[o + t]) break;
-      w = b.bp[(uint64_t)(o + t) * kMaxCand + w];
-      --t;
+  int w = __shfl(bj, 0, 16);
+  __threadfence_block();  // this wave's bp stores are visible to its loads
+  int t = (int)end;
+  bool done = false;
+  while (!done) {
+    const int lo = t - (kVitBpBlock - 1) < 0 ? 0 : t - (kVitBpBlock - 1);
+    {
+      uint4 rows[kVitBpBlock / 16];
+#pragma unroll
+      for (int x = 0; x < kVitBpBlock / 16; ++x) {
+        const int r = min(lo + j + 16 * x, t);   // clamped: no divergent loads
+        rows[x] = *reinterpret_cast<const uint4*>(b.bp + (uint64_t)(o + r) * kMaxCand);
+      }
+#pragma unroll
+      for (int x = 0; x < kVitBpBlock / 16; ++x) gs.bp[j + 16 * x] = rows[x];
     }
+    wave_sync();
+    if (j == 0) {
+      for (; t >= lo; --t) {
+        b.choice[o + t] = (int8_t)w;
+        const uint4 row = gs.bp[t - lo];
+        const uint32_t word = w < 4 ? row.x : (w < 8 ? row.y : (w < 12 ? row.z : row.w));
+        const uint32_t nb = (word >> (8 * (w & 3))) & 0xffu;
+        if (nb == 255u) { done = true; break; }
+        w = (int)nb;
+      }
+    }
+    t = __shfl(t, 0, 16);
+    w = __shfl(w, 0, 16);
+    done = __shfl((int)done, 0, 16) != 0;
+    wave_sync();
   }
 }
 
 __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
+  __shared__ VitGroupSmem smem[4];
   const int j = threadIdx.x & 15;
   const int gbase = threadIdx.x & 48;
+  VitGroupSmem& gs = smem[threadIdx.x >> 4];
   const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 4);
   if (k >= b.T) return;
   const uint32_t o = b.trace_off[k], S = b.n_states[k];
   const MatchOptions op = b.opts[b.trace_opt[k]];
   const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
-  const double beta = (double)op.beta;
   const double brk = (double)op.breakage_distance;
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   bool prev_ok = false;
   double cost = INF;
   uint32_t prevK = 0;
-  // one-layer-ahead prefetch of the per-layer scalars and this lane's emission input
-  uint32_t KBn = 0, basen = 0;
-  double gcn = 0.0;
-  float sqn = 0.f;
-  if (S) { KBn = b.cand_n[o]; sqn = b.cand_sq[(uint64_t)o * kMaxCand + j]; }
-  for (uint32_t s = 0; s < S; ++s) {
-    const uint64_t l = o + s;
-    const uint32_t KB = KBn, base = basen;
-    const double gcl = gcn;
-    const float sq = sqn;
-    if (s + 1 < S) {
-      KBn = b.cand_n[l + 1];
-      gcn = b.gc[l + 1];
-      basen = b.trans_off[l + 1];
-      sqn = b.cand_sq[(l + 1) * kMaxCand + j];
+  for (uint32_t s0 = 0; s0 < S;) {
+    // ---- chunk descriptors: lane q describes layer s0+q (clamped, branch-free loads)
+    const uint32_t sq_ = s0 + j;
+    const bool vq = sq_ < S;
+    const uint64_t lq = o + min(sq_, S - 1);
+    const uint64_t lp = lq == o ? o : lq - 1;
+    const uint32_t kb_raw = b.cand_n[lq], ka_raw = b.cand_n[lp];
+    const double gc_raw = b.gc[lq];
+    const uint32_t off_raw = b.trans_off[lq];
+    const bool hasprev = vq && sq_ >= 1;
+    const uint32_t kbq = vq ? kb_raw : 0u;
+    const uint32_t tcq = hasprev ? ka_raw * kbq : 0u;
+    const double gcq = hasprev ? gc_raw : 0.0;
+    const uint32_t offq = hasprev ? off_raw : 0u;
+    uint32_t incl = tcq;
+    for (int d = 1; d < 16; d <<= 1) {
+      const uint32_t u = __shfl_up(incl, d, 16);
+      if (j >= d) incl += u;
     }
-    bool start = !prev_ok || (s > 0 && gcl > brk);
-    double best = INF;
-    int arg = -1;
-    if (KB && !start) {
-      // issue every route load of this layer at once, then reduce
-      uint32_t rv[kMaxCand];
+    const uint32_t excl = incl - tcq;
+    const unsigned long long fit = __ballot(vq && incl <= (uint32_t)kVitRouteCap);
+    const uint32_t gfit = (uint32_t)((fit >> gbase) & 0xffffull);
+    const uint32_t C = (uint32_t)__builtin_ctz(~gfit);  // leading layers whose routes fit (>= 1)
+    const int p0 = (s0 == 0) ? 1 : 0;                     // layer 0 has no incoming routes
+    const uint32_t rstart = (C > (uint32_t)p0) ? (__shfl(offq, p0, 16) - __shfl(excl, p0, 16)) : 0u;
+    const uint32_t total = __shfl(incl, (int)C - 1, 16);
+    {
+      const uint32_t tm1 = total ? total - 1u : 0u;
+      double rv[kVitRouteCap / 16];
 #pragma unroll
-      for (int i = 0; i < kMaxCand; ++i)
-        rv[i] = (i < (int)prevK && j < (int)KB) ? b.route[base + i * KB + j] : kRouteInvalid;
+      for (int x = 0; x < kVitRouteCap / 16; ++x) rv[x] = b.tcost[rstart + min((uint32_t)j + 16u * x, tm1)];
+      float sv[kVitChunk];
 #pragma unroll
-      for (int i = 0; i < kMaxCand; ++i) {
-        if (i >= (int)prevK) break;
-        const double ci = shfl_d(cost, gbase | i);
-        if (ci != INF && rv[i] != kRouteInvalid) {
-          const double c = ci + fabs((double)rv[i] * 0.01 - gcl) / beta;
-          if (c < best) { best = c; arg = i; }
+      for (int t = 0; t < kVitChunk; ++t) sv[t] = b.cand_sq[(o + s0 + min((uint32_t)t, C - 1)) * kMaxCand + j];
+#pragma unroll
+      for (int x = 0; x < kVitRouteCap / 16; ++x) gs.tc[j + 16 * x] = rv[x];
+#pragma unroll
+      for (int t = 0; t < kVitChunk; ++t) gs.sq[t][j] = sv[t];
+      gs.kb[j] = kbq; gs.rel[j] = excl; gs.gc[j] = gcq;
+    }
+    wave_sync();
+    // ---- the layers of the chunk, in order, out of LDS
+    for (uint32_t t = 0; t < C; ++t) {
+      const uint32_t s = s0 + t;
+      const uint32_t KB = gs.kb[t];
+      const double gcl = gs.gc[t];
+      const uint32_t rel = gs.rel[t];
+      bool start = !prev_ok || (s > 0 && gcl > brk);
+      double best = INF;
+      int arg = -1;
+      if (KB && !start) {
+        const uint32_t jj = min((uint32_t)j, KB - 1u);
+        for (uint32_t i0 = 0; i0 < prevK; i0 += 4) {
+          double ci[4], tcx[4];
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const uint32_t i = min(i0 + x, prevK - 1u);
+            ci[x] = gs.cost[i];
+            tcx[x] = gs.tc[rel + i * KB + jj];
+          }
+          // an invalid route or unreachable source gives +inf, which never wins
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const double c = ci[x] + tcx[x];
+            if (i0 + x < prevK && c < best) { best = c; arg = (int)(i0 + x); }
+          }
         }
+        if (j >= (int)KB) { best = INF; arg = -1; }
+        const unsigned long long any = __ballot(j < (int)KB && arg >= 0);
+        if (((any >> gbase) & 0xffffull) == 0) start = true;
       }
-      const unsigned long long any = __ballot(j < (int)KB && arg >= 0);
-      if (((any >> gbase) & 0xffffull) == 0) start = true;
+      if (s > 0 && prev_ok && (KB == 0 || start)) {
+        vit_flush(b, gs, o + s0, t, j);   // rows [s0, s) are needed by the backtrace
+        backtrace_chain(b, gs, o, s - 1, prevK, cost, j);
+      }
+      if (KB == 0) {
+        gs.bpo[t][j] = 255;
+        if (j == 0) gs.cs[t] = 1;
+        prev_ok = false; prevK = 0; cost = INF;
+        continue;
+      }
+      const double em = (j < (int)KB) ? (double)gs.sq[t][j] * inv2s2 : INF;
+      double nc;
+      uint8_t bpj;
+      if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255; }
+      else { nc = (j < (int)KB && arg >= 0) ? best + em : INF; bpj = arg >= 0 ? (uint8_t)arg : (uint8_t)255; }
+      gs.bpo[t][j] = bpj;
+      if (j == 0) gs.cs[t] = start ? 1 : 0;
+      gs.cost[j] = nc;
+      wave_sync();
+      cost = nc;
+      prev_ok = true;
+      prevK = KB;
     }
-    if (s > 0 && prev_ok && (KB == 0 || start)) backtrace_chain(b, o, s - 1, prevK, cost, j);
-    if (KB == 0) {
-      if (j == 0) b.chain_start[l] = 1;
-      prev_ok = false; prevK = 0; cost = INF;
-      continue;
-    }
-    const double em = (j < (int)KB) ? (double)sq * inv2s2 : INF;
-    double nc;
-    uint8_t bpj;
-    if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255; }
-    else { nc = (j < (int)KB && arg >= 0) ? best + em : INF; bpj = arg >= 0 ? (uint8_t)arg : (uint8_t)255; }
-    if (j < (int)KB) b.bp[l * kMaxCand + j] = bpj;
-    if (j == 0) b.chain_start[l] = start ? 1 : 0;
-    cost = nc;
-    prev_ok = true;
-    prevK = KB;
+    wave_sync();
+    vit_flush(b, gs, o + s0, C, j);
+    wave_sync();
+    s0 += C;
   }
-  if (prev_ok) backtrace_chain(b, o, S - 1, prevK, cost, j);
+  if (prev_ok) backtrace_chain(b, gs, o, S - 1, prevK, cost, j);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1033,8 +1194,8 @@ __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
 //   k_traversals  one lane per chosen transition: expands its path into 64-byte traversal
 //                 records (edge, [b,en] cm, interpolated times, state indices, OSMLR tags);
 //                 all dependent graph lookups happen here, in parallel
-//   k_segments    one lane per trace: streams its records, merges pieces that continue
-//                 through a state point and forms OSMLR runs (meili form_segments analogue)
+//   k_run_flags / k_runs  merge pieces that continue through a state point and form
+//                 OSMLR runs (meili form_segments analogue), parallel over records
 struct RunState {
   bool open, internal;
   uint32_t sd, f_b, f_soff, l_en, l_len, l_soff, seg_len, sb, se, way_first, way_last;
@@ -1108,63 +1269,177 @@ __global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
   const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
   TravRec* out = b.trav + b.trav_off[l];
   uint64_t x = 0;
-  for (uint32_t q = 0; q < ns; ++q) {
-    const uint32_t e = pe[q];
-    const uint4 rec = g.edges[e];
-    const uint32_t L = rec.y;
-    const bool rev = (rec.w & 1u) != 0u;
-    uint32_t b0 = 0, b1 = L;
-    if (q == 0) b0 = rev ? L - sa : sa;
-    if (q + 1 == ns) b1 = rev ? L - sb : sb;
-    TravRec t;
-    t.e = e; t.b = b0; t.en = b1; t.slot = (uint32_t)l;
-    t.tb = interp_time(ta, tb, x, D);
-    x += (uint64_t)(b1 - b0);
-    t.te = interp_time(ta, tb, x, D);
-    t.sb = oa;
-    t.se = (q + 1 == ns) ? ob : oa;
-    t.sd = g.edge_seg[e];
-    t.soff = g.edge_seg_off[e];
-    t.len = L;
-    t.way = g.edge_way[e];
-    t.internal = (rec.z & kFlagInternal) ? 1u : 0u;
-    t.seg_len = t.sd != kNone ? g.seg_len[t.sd] : 0u;
-    out[q] = t;
+  // four path edges per group: every graph load of a group is issued before its record
+  // stores (loads after a pending store wait for it: shared vmcnt)
+  for (uint32_t q0 = 0; q0 < ns; q0 += 4) {
+    uint32_t e[4], sd[4], soff[4], way[4], sl[4];
+    uint4 rec[4];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      e[y] = pe[min(q0 + y, ns - 1u)];
+    }
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      rec[y] = g.edges[e[y]];
+      sd[y] = g.edge_seg[e[y]];
+      soff[y] = g.edge_seg_off[e[y]];
+      way[y] = g.edge_way[e[y]];
+    }
+#pragma unroll
+    for (int y = 0; y < 4; ++y) sl[y] = g.seg_len[sd[y] != kNone ? sd[y] : 0u];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const uint32_t q = q0 + y;
+      if (q >= ns) break;
+      const uint32_t L = rec[y].y;
+      const bool rev = (rec[y].w & 1u) != 0u;
+      uint32_t b0 = 0, b1 = L;
+      if (q == 0) b0 = rev ? L - sa : sa;
+      if (q + 1 == ns) b1 = rev ? L - sb : sb;
+      TravRec t;
+      t.e = e[y]; t.b = b0; t.en = b1; t.slot = (uint32_t)l;
+      t.tb = interp_time(ta, tb, x, D);
+      x += (uint64_t)(b1 - b0);
+      t.te = interp_time(ta, tb, x, D);
+      t.sb = oa;
+      t.se = (q + 1 == ns) ? ob : oa;
+      t.sd = sd[y];
+      t.soff = soff[y];
+      t.len = L;
+      t.way = way[y];
+      t.internal = (rec[y].z & kFlagInternal) ? 1u : 0u;
+      t.seg_len = sd[y] != kNone ? sl[y] : 0u;
+      out[q] = t;
+    }
   }
 }
 
-__global__ void __launch_bounds__(64) k_segments(DevGraph g, DevBatch b, uint32_t total) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= b.T) return;
-  const uint32_t r0 = b.trav_off[b.trace_off[k]];
-  const uint32_t r1 = (k + 1 < b.T) ? b.trav_off[b.trace_off[k + 1]] : total;
-  b.seg_base[k] = r0;
-  SegmentRec* out = b.segs + r0;
-  uint32_t n = 0;
-  RunState R;
-  R.open = false;
-  TravRec pend;
-  bool has_pend = false;
-  uint32_t prev_slot = 0;
-  TravRec nxt;
-  if (r0 < r1) nxt = b.trav[r0];
-  for (uint32_t r = r0; r < r1; ++r) {
-    const TravRec t = nxt;
-    if (r + 1 < r1) nxt = b.trav[r + 1];          // prefetch: records are independent
-    if (r > r0 && t.slot != prev_slot && t.slot != prev_slot + 1) {  // a chain boundary lies between
-      if (has_pend) { run_feed(g, R, pend, out, n); has_pend = false; }
-      run_close(g, R, out, n);
+// The meili merge / run rules only ever compare a record with the previous kept record
+// of its chain, so run boundaries are local and K4 needs no per-trace serial loop:
+//   k_run_flags   one lane per record: kind (skip / new traversal / merged piece) and
+//                 run-head flag
+//   (scan)        exclusive sum of the head flags = each run's output index
+//   k_runs        one lane per run head: walks its run (a few records) and writes the
+//                 segment; one lane per trace records seg_base / seg_cnt
+enum : uint8_t { kRecSkip = 0, kRecNew = 1, kRecMerged = 2 };
+
+__device__ __forceinline__ bool same_chain(uint32_t slot_prev, uint32_t slot_next) {
+  // traversal records of a chain come from consecutive transition slots; traces are
+  // at least two slots apart, so this also separates traces
+  return slot_next == slot_prev || slot_next == slot_prev + 1;
+}
+
+__global__ void __launch_bounds__(256) k_run_flags(DevBatch b, uint32_t total) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > total) return;
+  if (r == total) { b.run_head[r] = 0; return; }
+  const TravRec& t = b.trav[r];
+  const uint32_t tb = t.b, ten = t.en, tslot = t.slot;
+  uint8_t kind = kRecSkip;
+  uint32_t head = 0;
+  if (ten != tb) {
+    // previous kept record of the same chain
+    int64_t p = (int64_t)r - 1;
+    uint32_t nslot = tslot;
+    bool has = false;
+    while (p >= 0) {
+      const uint32_t ps = b.trav[p].slot;
+      if (!same_chain(ps, nslot)) break;
+      if (b.trav[p].en != b.trav[p].b) { has = true; break; }
+      nslot = ps;
+      --p;
     }
-    prev_slot = t.slot;
-    if (t.en == t.b) continue;
-    if (has_pend && pend.e == t.e && pend.en == t.b) { pend.en = t.en; pend.te = t.te; pend.se = t.se; continue; }
-    if (has_pend) run_feed(g, R, pend, out, n);
-    pend = t;
-    has_pend = true;
+    if (has) {
+      const TravRec& u = b.trav[p];
+      if (u.e == t.e && u.en == tb) {
+        kind = kRecMerged;
+      } else {
+        kind = kRecNew;
+        bool cont = u.sd == t.sd;
+        if (cont && t.sd == kNone && u.internal != t.internal) cont = false;
+        if (cont) {
+          if (u.en != u.len || tb != 0) cont = false;
+          else if (t.sd != kNone && t.soff != u.soff + u.len) cont = false;
+        }
+        head = cont ? 0u : 1u;
+      }
+    } else {
+      kind = kRecNew;
+      head = 1;
+    }
   }
-  if (has_pend) run_feed(g, R, pend, out, n);
-  run_close(g, R, out, n);
-  b.seg_cnt[k] = n;
+  b.run_kind[r] = kind;
+  b.run_head[r] = head;
+}
+
+// scatter: run head record of every run, in run order (runs are contiguous in record order)
+__global__ void __launch_bounds__(256) k_run_heads(DevBatch b, uint32_t total) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < total && b.run_head[r]) b.run_pos[b.run_idx[r]] = r;
+}
+
+__device__ __forceinline__ void run_piece(RunState& R, const TravRec& t, uint8_t kind, uint32_t& md, double& mtb,
+                                          double& mte) {
+  if (kind == kRecMerged) {
+    md += t.en - t.b;
+    mte = t.te;
+  } else {
+    const double dt = mte - mtb;
+    const bool slow = dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
+    R.tot += md;
+    R.q = slow ? R.q + md : 0;
+    md = t.en - t.b; mtb = t.tb; mte = t.te;
+    if (t.way != R.way_first) R.way_last = t.way;
+  }
+  R.l_en = t.en; R.l_len = t.len; R.l_soff = t.soff; R.te = t.te; R.se = t.se;
+}
+
+// one lane per run: records [run_pos[i], run_pos[i+1]) (skips and merged pieces inside)
+__global__ void __launch_bounds__(256) k_runs(DevGraph g, DevBatch b, uint32_t total) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n_runs = b.run_idx[total];
+  if (i < b.T) {  // per-trace range of the compacted segments
+    const uint32_t p0 = b.trace_off[i], p1 = b.trace_off[i + 1];
+    const uint32_t r0 = p0 < b.P ? b.trav_off[p0] : total;   // empty trailing traces start at P
+    const uint32_t r1 = p1 < b.P ? b.trav_off[p1] : total;
+    const uint32_t i0 = b.run_idx[r0];
+    b.seg_base[i] = i0;
+    b.seg_cnt[i] = b.run_idx[r1] - i0;
+  }
+  if (i >= n_runs) return;
+  const uint32_t r = b.run_pos[i];
+  const uint32_t end = (i + 1 < n_runs) ? b.run_pos[i + 1] : total;
+  const TravRec f = b.trav[r];
+  RunState R;
+  R.open = true; R.sd = f.sd; R.internal = f.internal != 0u; R.seg_len = f.seg_len;
+  R.f_b = f.b; R.f_soff = f.soff; R.tb = f.tb; R.sb = f.sb;
+  R.tot = 0; R.q = 0; R.way_first = f.way; R.way_last = f.way;
+  uint32_t md = f.en - f.b;
+  double mtb = f.tb, mte = f.te;
+  R.l_en = f.en; R.l_len = f.len; R.l_soff = f.soff; R.te = f.te; R.se = f.se;
+  // records are consumed four at a time so their loads overlap
+  uint32_t q = r + 1;
+  for (; q + 4 <= end; q += 4) {
+    uint8_t kd[4];
+    TravRec t[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) { kd[x] = b.run_kind[q + x]; t[x] = b.trav[q + x]; }
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+      if (kd[x] != kRecSkip) run_piece(R, t[x], kd[x], md, mtb, mte);
+  }
+  for (; q < end; ++q) {
+    const uint8_t kd = b.run_kind[q];
+    if (kd != kRecSkip) run_piece(R, b.trav[q], kd, md, mtb, mte);
+  }
+  {
+    const double dt = mte - mtb;
+    const bool slow = dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
+    R.tot += md;
+    R.q = slow ? R.q + md : 0;
+  }
+  uint32_t n = 0;
+  run_close(g, R, b.segs + i, n);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1364,7 +1639,8 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.scan_tmp_bytes = tmp;
   w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
-  w.route = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
+  w.route = nullptr; w.tcost = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
+  w.run_kind = nullptr; w.run_head = nullptr; w.run_idx = nullptr; w.run_pos = nullptr; w.seg_scan_tmp = nullptr;
   w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
   ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
   ensure_path(std::max<uint64_t>(keep_path, cp / 8 + 1024));
@@ -1375,8 +1651,10 @@ void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
   Workspace& w = ws_;
   if (!(n <= w.cap_trans && w.route)) {
     if (w.route) { (void)hipFree(w.route); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.route)); }
+    if (w.tcost) { (void)hipFree(w.tcost); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.tcost)); }
     const uint64_t c = n + n / 4 + 1024;
     w.route = dalloc<uint32_t>(w.allocs, c);
+    w.tcost = dalloc<double>(w.allocs, c);
     w.cap_trans = c;
   }
   if (!(n_src <= w.cap_src && w.src_item)) {
@@ -1408,10 +1686,23 @@ void Matcher::ensure_segs(uint64_t n) {
   free_one(w, w.segs);
   free_one(w, w.reps);
   free_one(w, w.trav);
+  free_one(w, w.run_kind);
+  free_one(w, w.run_head);
+  free_one(w, w.run_idx);
+  free_one(w, w.run_pos);
+  free_one(w, w.seg_scan_tmp);
   const uint64_t c = n + n / 4 + 1024;
   w.segs = dalloc<SegmentRec>(w.allocs, c);
   w.reps = dalloc<ReportRec>(w.allocs, c);
   w.trav = dalloc<TravRec>(w.allocs, c);
+  w.run_kind = dalloc<uint8_t>(w.allocs, c + 1);
+  w.run_head = dalloc<uint32_t>(w.allocs, c + 1);
+  w.run_idx = dalloc<uint32_t>(w.allocs, c + 1);
+  w.run_pos = dalloc<uint32_t>(w.allocs, c + 1);
+  size_t tmp = 0;
+  RM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, w.run_head, w.run_idx, (int)(c + 1), stream_));
+  w.seg_scan_tmp_bytes = tmp;
+  w.seg_scan_tmp = dalloc<char>(w.allocs, tmp);
   w.cap_segs = c;
 }
 
@@ -1458,7 +1749,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.opts = w.opts; v.trace_opt = w.trace_opt;
   v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig;
   v.cand_n = w.cand_n; v.cand_road = w.cand_road; v.cand_s = w.cand_s; v.cand_sq = w.cand_sq;
-  v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route;
+  v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.tcost = w.tcost;
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
@@ -1538,6 +1829,7 @@ void Matcher::run_device(const RunParams& rp) {
   n_trans_ = total;
   ensure_trans(total, n_src);
   v.route = w.route;
+  v.tcost = w.tcost;
   v.src_item = w.src_item;
 
   tic(kKRoutes);
@@ -1583,9 +1875,16 @@ void Matcher::run_device(const RunParams& rp) {
   n_path_ = seg_total;  // one traversal record (and at most one segment) per chosen path edge
   ensure_segs(seg_total);
   v.segs = w.segs; v.reps = w.reps; v.trav = w.trav;
+  v.run_kind = w.run_kind; v.run_head = w.run_head; v.run_idx = w.run_idx; v.run_pos = w.run_pos;
   tic(kKSegments);
   hipLaunchKernelGGL(k_traversals, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_segments, dim3((T + 63) / 64), dim3(64), 0, st, g, v, (uint32_t)seg_total);
+  hipLaunchKernelGGL(k_run_flags, dim3((uint32_t)((seg_total + 1 + 255) / 256)), dim3(256), 0, st, v, (uint32_t)seg_total);
+  tmp = w.seg_scan_tmp_bytes;
+  RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.seg_scan_tmp, tmp, w.run_head, w.run_idx, (int)(seg_total + 1), st));
+  hipLaunchKernelGGL(k_run_heads, dim3((uint32_t)((seg_total + 255) / 256)), dim3(256), 0, st, v, (uint32_t)seg_total);
+  // runs <= records: the grid covers both bounds, n_runs is read on the device
+  hipLaunchKernelGGL(k_runs, dim3((uint32_t)((std::max<uint64_t>(seg_total, T) + 255) / 256)), dim3(256), 0, st, g, v,
+                     (uint32_t)seg_total);
   toc(kKSegments);
   if (rp.do_report) {
     if (rp.hist && rp.zero_hist)

@@ -84,7 +84,7 @@ struct Workspace {
   // per slot
   uint32_t* slot_trace = nullptr; uint32_t* n_states = nullptr; uint32_t* state_orig = nullptr;
   uint8_t* cand_n = nullptr; uint32_t* cand_road = nullptr; uint32_t* cand_s = nullptr; float* cand_sq = nullptr;
-  uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr;
+  uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr; double* tcost = nullptr;
   uint32_t* src_cnt = nullptr; uint32_t* src_off = nullptr; uint32_t* src_item = nullptr;
   int8_t* choice = nullptr; uint8_t* chain_start = nullptr; uint8_t* bp = nullptr;
   uint32_t* path_off = nullptr; uint32_t* path_cnt = nullptr; uint32_t* path_pool = nullptr; uint32_t* route_dist = nullptr;
@@ -92,6 +92,8 @@ struct Workspace {
   // per trace outputs
   SegmentRec* segs = nullptr; uint32_t* seg_base = nullptr; uint32_t* seg_cnt = nullptr;
   TravRec* trav = nullptr; uint32_t* trav_off = nullptr;  // traversal records (K4 pass 1)
+  uint8_t* run_kind = nullptr; uint32_t* run_head = nullptr; uint32_t* run_idx = nullptr; uint32_t* run_pos = nullptr;  // K4 run flags
+  void* seg_scan_tmp = nullptr; size_t seg_scan_tmp_bytes = 0;
   ReportRec* reps = nullptr; uint32_t* rep_cnt = nullptr; ReportStats* stats = nullptr;
   // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list (overflow lists of the lane tiers)

@@ -8,6 +8,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="C2")
 ap.add_argument("--traces", type=int, default=0)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--split", type=int, default=0, help="also time M concurrent runners (streams) over sub-batches")
 a = ap.parse_args()
 c = dict(world.CONFIGS[a.config])
 if a.traces:
@@ -35,3 +36,26 @@ for r in range(a.reps):
     kt = bm.kernel_times()
     print("rerun %.4fs  %.1f Mpts/s  " % (dt, len(tr["lon"]) / dt / 1e6) +
           " ".join("%s=%.2fms" % (k, v[0]) for k, v in kt.items()), flush=True)
+
+if a.split > 1:
+    import threading
+    T = len(tr["trace_off"]) - 1
+    bounds = np.linspace(0, T, a.split + 1).astype(int)
+    bms = []
+    for m in range(a.split):
+        t0, t1 = bounds[m], bounds[m + 1]
+        o0, o1 = int(tr["trace_off"][t0]), int(tr["trace_off"][t1])
+        sub = {k: tr[k][o0:o1] for k in ("lon", "lat", "time", "accuracy")}
+        off = tr["trace_off"][t0:t1 + 1] - o0
+        b2 = engine.BatchMatcher(eng)
+        b2.run(off, sub["lon"], sub["lat"], sub["time"], sub["accuracy"], opts)
+        bms.append(b2)
+    for r in range(a.reps + 1):
+        ths = [threading.Thread(target=b2.rerun) for b2 in bms]
+        t = time.time()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.time() - t
+        print("split %d: %.4fs  %.1f Mpts/s" % (a.split, dt, len(tr["lon"]) / dt / 1e6), flush=True)
