@@ -68,9 +68,10 @@ struct WorldParams {
 
 Graph build_world(const WorldParams& p);
 
-// Synthetic GPS traces (restating reference py/generate_test_trace.py:35-104,120-149):
-// a random drive on the graph at edge speed, resampled every `rate_s` seconds,
-// with the generator's correlated noise (first-quadrant lock + moving average).
+// Synthetic GPS traces (restating reference py/generate_test_trace.py:35-104,120-164):
+// fastest routes (A* on travel time) to random destinations, driven at edge speed and
+// resampled every `rate_s` seconds, with the generator's correlated noise
+// (first-quadrant lock + moving average).
 struct TraceParams {
   uint32_t n_traces = 1, n_points = 100;
   double rate_s = 1.0;

@@ -8,8 +8,8 @@
 //   * ~5 % local service roads with no OSMLR association, ~10 % one-way local roads
 //   * segment ids: level | tile_index << 3 | segment_index << 25 with Valhalla's
 //     tile sizes 4/1/0.25 degrees (reference py/get_tiles.py:35-39, py/simple_reporter.py:37-49)
-// The trace generator restates reference py/generate_test_trace.py:35-104 (noise)
-// and :120-149 (1 s resampling at edge speed) on this world.
+// The trace generator restates reference py/generate_test_trace.py:35-104 (noise),
+// :120-149 (1 s resampling at edge speed) and :151-164 (routed drives) on this world.
 #include <algorithm>
 #include <cmath>
 #include <stdexcept>
@@ -353,13 +353,108 @@ void position_on_edge(const Graph& g, uint32_t e, uint32_t off_cm, double& lon, 
   lon = g.verts[v1 - 1].lon; lat = g.verts[v1 - 1].lat;
 }
 
-void gen_one(const Graph& g, const TraceParams& p, uint32_t k, TraceSet& ts, const std::vector<uint32_t>& starts) {
+// Fastest-route planner for the trace generator.  The reference generator drives a
+// Valhalla /route answer between two locations with auto costing
+// (py/generate_test_trace.py:151-164, then the :166-179 edge walk); here the same role
+// is played by an A* search on edge travel time (mode speeds) to a random destination,
+// so traces follow the fast road classes the way routed traffic does.
+struct RoutePlanner {
+  const Graph& g;
+  int mode;
+  uint32_t acc, vmax_dkph;
+  std::vector<uint32_t> stamp, done, cost, pedge;
+  std::vector<std::pair<uint64_t, uint32_t>> heap;
+  uint32_t gen = 0;
+  static constexpr uint32_t kSettleCap = 400000;
+
+  RoutePlanner(const Graph& gr, int m)
+      : g(gr), mode(m), acc(mode_access(m)), vmax_dkph(mode_speed_dkph(m, 900u)),
+        stamp(gr.num_nodes(), 0), done(gr.num_nodes(), 0), cost(gr.num_nodes(), 0), pedge(gr.num_nodes(), kNone) {}
+
+  uint32_t h_ms(uint32_t n, uint32_t dst) const {
+    const double d = piece_m(g.node_lon[n], g.node_lat[n], g.node_lon[dst], g.node_lat[dst]);
+    return (uint32_t)(0.95 * d * 36000.0 / (double)vmax_dkph);
+  }
+
+  // edges of the fastest route src -> dst whose first edge is not on road `avoid_road`
+  bool plan(uint32_t src, uint32_t avoid_road, uint32_t dst, std::vector<uint32_t>& out) {
+    out.clear();
+    if (src == dst) return false;
+    if (++gen == 0) {
+      std::fill(stamp.begin(), stamp.end(), 0u);
+      std::fill(done.begin(), done.end(), 0u);
+      gen = 1;
+    }
+    typedef std::pair<uint64_t, uint32_t> Item;  // ((f << 32) | node) orders ties by node id
+    heap.clear();
+    auto push = [&](uint32_t v, uint32_t gcost) {
+      const uint64_t f = (uint64_t)gcost + h_ms(v, dst);
+      heap.push_back(Item((f << 32) | v, v));
+      std::push_heap(heap.begin(), heap.end(), std::greater<Item>());
+    };
+    stamp[src] = gen; cost[src] = 0; pedge[src] = kNone;
+    push(src, 0);
+    uint32_t settled = 0;
+    while (!heap.empty()) {
+      std::pop_heap(heap.begin(), heap.end(), std::greater<Item>());
+      const uint32_t u = heap.back().second;
+      heap.pop_back();
+      if (done[u] == gen) continue;
+      done[u] = gen;
+      if (u == dst) break;
+      if (++settled > kSettleCap) return false;
+      for (uint32_t e = g.node_off[u]; e < g.node_off[u + 1]; ++e) {
+        const EdgeRec& er = g.edges[e];
+        if (!(edge_access(er.info) & acc)) continue;
+        if (u == src && (er.road >> 1) == avoid_road) continue;
+        const uint32_t v = er.target;
+        if (done[v] == gen) continue;
+        const uint32_t nc = cost[u] + time_ms(er.len_cm, mode_speed_dkph(mode, edge_speed_dkph(er.info)));
+        if (stamp[v] != gen || nc < cost[v]) {
+          stamp[v] = gen; cost[v] = nc; pedge[v] = e;
+          push(v, nc);
+        }
+      }
+    }
+    if (done[dst] != gen) return false;
+    for (uint32_t x = dst; x != src;) {
+      const uint32_t e = pedge[x];
+      out.push_back(e);
+      const uint32_t road = g.edges[e].road >> 1;  // source node of e = far end of its twin
+      x = (g.edges[e].road & 1u) ? g.road_node1[road] : g.road_node0[road];
+    }
+    std::reverse(out.begin(), out.end());
+    return true;
+  }
+};
+
+// random destination node at a driving distance that fits the rest of the trace
+uint32_t pick_destination(const Graph& g, Rng& r, uint32_t from, double remaining_s) {
+  const double want = std::min(6000.0, std::max(400.0, remaining_s * 12.0));
+  uint32_t best = kNone;
+  double best_err = 1e300;
+  for (int tries = 0; tries < 24; ++tries) {
+    const uint32_t n = r.below(g.num_nodes());
+    if (n == from) continue;
+    const double d = piece_m(g.node_lon[from], g.node_lat[from], g.node_lon[n], g.node_lat[n]);
+    const double err = std::fabs(d - want);
+    if (err < best_err) { best_err = err; best = n; }
+    if (d >= 0.5 * want && d <= 1.5 * want) break;
+  }
+  return best;
+}
+
+void gen_one(const Graph& g, const TraceParams& p, uint32_t k, TraceSet& ts, const std::vector<uint32_t>& starts,
+             RoutePlanner& planner) {
   Rng r(mix(p.seed, 0x7472616365ull + k));
   const uint32_t acc = mode_access(p.mode);
   const uint32_t base = ts.trace_off[k];
   // start edge
   uint32_t e = starts[r.below((uint32_t)starts.size())];
   double off_m = r.uniform() * g.edges[e].len_cm * 0.01;
+  std::vector<uint32_t> route;
+  size_t ri = 0;
+  const double t_total = (p.n_points ? p.n_points - 1 : 0) * p.rate_s;
   const int lookback = (int)std::ceil(30.0 / (p.rate_s + 2.0));
   std::vector<double> hx, hy;
   int qx = 0, qy = 0;
@@ -375,9 +470,18 @@ void gen_one(const Graph& g, const TraceParams& p, uint32_t k, TraceSet& ts, con
       const double t_end = t_now + (len_m - off_m) / v;
       if (t_end >= t_target) { off_m += (t_target - t_now) * v; t_now = t_target; break; }
       t_now = t_end;
-      // choose next edge: straight on the same way with p=0.6, else uniform; avoid U-turns
       const uint32_t node = g.edges[e].target;
       const uint32_t road = g.edges[e].road >> 1;
+      // follow the planned route; plan a new one to a fresh destination when it ends
+      if (ri >= route.size()) {
+        route.clear();
+        ri = 0;
+        const uint32_t dst = pick_destination(g, r, node, t_total - t_now);
+        if (dst != kNone) planner.plan(node, road, dst, route);
+      }
+      if (ri < route.size()) { e = route[ri++]; off_m = 0.0; continue; }
+      // no route from here (island / one-way trap): random continuation as a fallback,
+      // straight on the same way with p=0.6, else uniform; avoid U-turns
       uint32_t opts[16]; uint32_t no = 0; uint32_t straight = kNone;
       for (uint32_t x = g.node_off[node]; x < g.node_off[node + 1] && no < 16; ++x) {
         if (!(edge_access(g.edges[x].info) & acc) || (g.edges[x].road >> 1) == road) continue;
@@ -443,10 +547,14 @@ TraceSet generate_traces(const Graph& g, const TraceParams& p) {
   unsigned nt = p.threads ? p.threads : std::max(1u, std::thread::hardware_concurrency());
   nt = std::min<unsigned>(nt, 64);
   if (p.n_traces < 64) nt = 1;
+  // each thread owns a route planner (16 B per node); keep them within ~4 GiB
+  const uint64_t per = 16ull * std::max<uint32_t>(g.num_nodes(), 1u);
+  nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nt, (4ull << 30) / per));
   std::vector<std::thread> th;
   for (unsigned t = 0; t < nt; ++t)
     th.emplace_back([&, t] {
-      for (uint32_t k = t; k < p.n_traces; k += nt) gen_one(g, p, k, ts, starts);
+      RoutePlanner planner(g, p.mode);
+      for (uint32_t k = t; k < p.n_traces; k += nt) gen_one(g, p, k, ts, starts, planner);
     });
   for (auto& x : th) x.join();
   return ts;
