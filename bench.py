@@ -220,6 +220,8 @@ def main():
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "frac_vs_measured_copy": (achieved / HBM_MEASURED_GBS) if achieved else None,
                 "traffic": traffic,
+                "traffic_source": (os.path.relpath(a.traffic_json, ROOT) + " (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE "
+                                   "passes of this bench, read side x2 per MI355X_MICROARCH.md)") if traffic else None,
                 "algorithmic_bytes_per_launch": abytes,
                 "avg_launch_ms": routes_ms,
                 "counts": counts,

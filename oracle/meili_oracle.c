@@ -543,7 +543,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
     const uint32_t o = b->trace_off[k], S = R->n_states[k];
     const og_options* op = &b->opts[b->trace_opt[k]];
     const double inv2s2 = 1.0 / (2.0 * (double)op->sigma_z * (double)op->sigma_z);
-    const double beta = (double)op->beta;
+    const double inv_beta = 1.0 / (double)op->beta;
     int prev_ok = 0;
     for (uint32_t s = 0; s < S; ++s) {
       const uint32_t l = o + s, KB = R->cand_n[l];
@@ -558,7 +558,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
             const double ci = cost[(l - 1) * (uint64_t)OG_K + i];
             const uint32_t rc = R->route[R->trans_off[l] + i * KB + j];
             if (ci == INFINITY || rc == OG_ROUTE_INVALID) continue;
-            const double c = ci + fabs((double)rc * 0.01 - R->gc[l]) / beta;
+            const double c = ci + fabs((double)rc * 0.01 - R->gc[l]) * inv_beta;
             if (c < best) { best = c; arg = (int)i; }
           }
           const double em = (double)R->cand_sq[l * (uint64_t)OG_K + j] * inv2s2;

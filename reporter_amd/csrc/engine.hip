@@ -42,6 +42,10 @@ constexpr int kSmallH = 256;    // LDS hash slots, fast tier
 constexpr int kBigH = 4096;     // LDS hash slots, retry tier (one source at a time)
 constexpr int kCandH = 256;     // road hash slots in the candidate kernel
 constexpr int kInlinePath = 8;  // path edges stored inline per slot (no allocation)
+#ifndef RM_WAVE_GRID
+#define RM_WAVE_GRID 8192
+#endif
+constexpr int kWaveGrid = RM_WAVE_GRID;  // blocks of the small wave tiers (grid-stride over their work lists)
 constexpr uint32_t kMaxBoundCm = 100000000u;
 constexpr double kQueueSpeedMps = 2.7777777777777777;  // 10 km/h
 
@@ -51,8 +55,8 @@ struct DevBatch {  // POD view of the workspace for kernels
   const uint32_t* trace_off; const float* lon; const float* lat; const double* time; const float* acc;
   const MatchOptions* opts; const uint32_t* trace_opt;
   uint32_t* slot_trace; uint32_t* n_states; uint32_t* state_orig;
-  uint8_t* cand_n; uint32_t* cand_road; uint32_t* cand_s; float* cand_sq;
-  uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route; double* tcost;
+  uint8_t* cand_n; uint4* cand_desc; float* cand_sq;
+  uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route; uint4* pair_info;
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
@@ -143,10 +147,13 @@ struct CandSmem {
   uint32_t list[kCandH];
 };
 
-__device__ __forceinline__ void project(const uint4 A, const uint4 B, float lon, float lat, float mlon, float mlat,
-                                        float& sq, uint32_t& s) {
-  const float ax = (as_f(A.x) - lon) * mlon, ay = (as_f(A.y) - lat) * mlat;
-  const float bx = (as_f(B.x) - lon) * mlon, by = (as_f(B.y) - lat) * mlat;
+// projection of the point onto the shape piece A->B in the point's local metric frame
+// (A = {lon, lat, cum_cm}, B likewise); squared distance in m^2 and the offset along
+// the road in cm.  Fixed operation order: bit-identical to oracle/meili_oracle.c.
+__device__ __forceinline__ void project(float alon, float alat, uint32_t acum, float blon, float blat, uint32_t bcum,
+                                        float lon, float lat, float mlon, float mlat, float& sq, uint32_t& s) {
+  const float ax = (alon - lon) * mlon, ay = (alat - lat) * mlat;
+  const float bx = (blon - lon) * mlon, by = (blat - lat) * mlat;
   const float dx = bx - ax, dy = by - ay;
   const float l2 = dx * dx + dy * dy;
   float t = 0.0f;
@@ -157,15 +164,42 @@ __device__ __forceinline__ void project(const uint4 A, const uint4 B, float lon,
   }
   const float cx = ax + t * dx, cy = ay + t * dy;
   sq = cx * cx + cy * cy;
-  const float along = (float)A.z + t * (float)(B.z - A.z);
+  const float along = (float)acum + t * (float)(bcum - acum);
   uint32_t v = (uint32_t)rintf(along);
-  if (v < A.z) v = A.z;
-  if (v > B.z) v = B.z;
+  if (v < acum) v = acum;
+  if (v > bcum) v = bcum;
   s = v;
 }
 
-// K1 lane tier: one lane per state.  Per-road minima live in 16 registers; a state with
-// more roads inside its radius is queued for the wave tier (k_candidates_wave).
+// candidate descriptor of (road, s) for a travel mode: everything the route and path
+// kernels need about a candidate in two dwordx4 (no dependent graph loads there)
+__device__ __forceinline__ void make_desc(const DevGraph& g, uint32_t road, uint32_t s, int mode, uint4& d0,
+                                          uint4& d1) {
+  const uint4 a = g.road_rec[2 * (uint64_t)road], c = g.road_rec[2 * (uint64_t)road + 1];
+  const uint32_t acc = mode_access(mode);
+  uint32_t spf = (a.w != kNone && edge_ok(c.y, acc)) ? mode_speed_dkph(mode, c.y & 0xffffu) : 0u;
+  uint32_t spr = (c.x != kNone && edge_ok(c.z, acc)) ? mode_speed_dkph(mode, c.z & 0xffffu) : 0u;
+  // a usable edge is never speed 0 here; time_ms() treats 0 as 1, so 1 keeps every result
+  if (a.w != kNone && edge_ok(c.y, acc) && spf == 0u) spf = 1u;
+  if (c.x != kNone && edge_ok(c.z, acc) && spr == 0u) spr = 1u;
+  d0 = make_uint4(road, s, a.z, spf | (spr << 16));
+  d1 = make_uint4(a.x, a.y, a.w, c.x);
+}
+
+__device__ __forceinline__ void put_cand(const DevGraph& g, const DevBatch& b, uint64_t p, uint32_t rank, uint32_t road,
+                                         uint32_t s, float sq, int mode) {
+  uint4 d0, d1;
+  make_desc(g, road, s, mode, d0, d1);
+  const uint64_t at = p * kMaxCand + rank;
+  b.cand_desc[2 * at] = d0;
+  b.cand_desc[2 * at + 1] = d1;
+  b.cand_sq[at] = sq;
+}
+
+// K1 lane tier: one lane per state.  Cell items are read as cell-major 32-byte records
+// (both shape vertices + road + access bits), so a test is two dwordx4 loads with no
+// dependent lookup.  Per-road minima live in 16 registers; a state with more roads
+// inside its radius is queued for the wave tier (k_candidates_wave).
 __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
@@ -187,7 +221,7 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
   const double fx1 = floor(((double)(lon + qlon) - g.lon0) / g.dlon);
   const double fy0 = floor(((double)(lat - qlat) - g.lat0) / g.dlat);
   const double fy1 = floor(((double)(lat + qlat) - g.lat0) / g.dlat);
-  uint32_t rroad[kMaxCand];
+  uint32_t rroad[kMaxCand], rs[kMaxCand];
   unsigned long long rbest[kMaxCand];
   uint32_t n = 0;
   bool ovf = false;
@@ -200,25 +234,25 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
         const uint32_t c = cy * g.ncx + cx;
         const uint32_t it0 = g.cell_off[c], it1 = g.cell_off[c + 1];
         for (uint32_t it = it0; it < it1; ++it) {
-          const uint32_t v = g.cell_item[it];
-          const uint4 A = g.verts[v], B = g.verts[v + 1];
+          const uint4 r0 = g.cell_rec[2 * (uint64_t)it], r1 = g.cell_rec[2 * (uint64_t)it + 1];
+          if (!((r1.z >> 29) & acc)) continue;
           float sq; uint32_t sc;
-          project(A, B, lon, lat, mlon, mlat, sq, sc);
+          project(as_f(r0.x), as_f(r0.y), r1.x, as_f(r0.z), as_f(r0.w), r1.y, lon, lat, mlon, mlat, sq, sc);
           if (!(sq <= r2)) continue;
-          const uint32_t road = A.w;
-          const uint32_t ef = g.road_fwd[road], er = g.road_rev[road];
-          const bool ok = (ef != kNone && edge_ok(g.edges[ef].z, acc)) || (er != kNone && edge_ok(g.edges[er].z, acc));
-          if (!ok) continue;
-          const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | v;
+          const uint32_t road = r1.z & 0x1fffffffu;
+          const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | r1.w;
           bool found = false;
 #pragma unroll
           for (int x = 0; x < kMaxCand; ++x)
-            if (x < (int)n && rroad[x] == road) { found = true; if (key < rbest[x]) rbest[x] = key; }
+            if (x < (int)n && rroad[x] == road) {
+              found = true;
+              if (key < rbest[x]) { rbest[x] = key; rs[x] = sc; }
+            }
           if (found) continue;
           if (n >= (uint32_t)kMaxCand) { ovf = true; break; }
 #pragma unroll
           for (int x = 0; x < kMaxCand; ++x)
-            if (x == (int)n) { rroad[x] = road; rbest[x] = key; }
+            if (x == (int)n) { rroad[x] = road; rbest[x] = key; rs[x] = sc; }
           ++n;
         }
       }
@@ -239,12 +273,7 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
       const uint32_t sqb2 = (uint32_t)(rbest[y] >> 32);
       rank += (sqb2 < sqb || (sqb2 == sqb && rroad[y] < rroad[x])) ? 1u : 0u;
     }
-    const uint32_t v = (uint32_t)rbest[x];
-    float sq; uint32_t sc;
-    project(g.verts[v], g.verts[v + 1], lon, lat, mlon, mlat, sq, sc);
-    b.cand_road[p * kMaxCand + rank] = rroad[x];
-    b.cand_s[p * kMaxCand + rank] = sc;
-    b.cand_sq[p * kMaxCand + rank] = sq;
+    put_cand(g, b, p, rank, rroad[x], rs[x], __uint_as_float(sqb), op.mode);
   }
   b.cand_n[p] = (uint8_t)n;
 }
@@ -290,15 +319,12 @@ __device__ void cand_wave_one(const DevGraph& g, const DevBatch& b, CandSmem& sm
       for (uint32_t ci = 0; ci < nc; ++ci) {
         const uint32_t lo = sm.cell_lo[ci], hi = sm.cell_hi[ci];
         for (uint32_t it = lo + lane; it < hi; it += kWave) {
-          const uint32_t v = g.cell_item[it];
-          const uint4 A = g.verts[v], B = g.verts[v + 1];
-          const uint32_t road = A.w;
-          const uint32_t ef = g.road_fwd[road], er = g.road_rev[road];
-          const bool ok = (ef != kNone && edge_ok(g.edges[ef].z, acc)) || (er != kNone && edge_ok(g.edges[er].z, acc));
-          if (!ok) continue;
+          const uint4 r0 = g.cell_rec[2 * (uint64_t)it], r1 = g.cell_rec[2 * (uint64_t)it + 1];
+          if (!((r1.z >> 29) & acc)) continue;
           float sq; uint32_t sc;
-          project(A, B, lon, lat, mlon, mlat, sq, sc);
+          project(as_f(r0.x), as_f(r0.y), r1.x, as_f(r0.z), as_f(r0.w), r1.y, lon, lat, mlon, mlat, sq, sc);
           if (!(sq <= r2)) continue;
+          const uint32_t road = r1.z & 0x1fffffffu, v = r1.w;
           // per-road min (sq, vertex) in the LDS hash
           uint32_t h = (road * 2654435761u) & (kCandH - 1);
           for (int probe = 0; probe < kCandH; ++probe) {
@@ -341,11 +367,10 @@ __device__ void cand_wave_one(const DevGraph& g, const DevBatch& b, CandSmem& sm
     }
     if (rank < (uint32_t)kMaxCand) {
       const uint32_t v = (uint32_t)bst;
+      const uint4 A = g.verts[v], B = g.verts[v + 1];
       float sq; uint32_t sc;
-      project(g.verts[v], g.verts[v + 1], lon, lat, mlon, mlat, sq, sc);
-      b.cand_road[p * kMaxCand + rank] = road;
-      b.cand_s[p * kMaxCand + rank] = sc;
-      b.cand_sq[p * kMaxCand + rank] = sq;
+      project(as_f(A.x), as_f(A.y), A.z, as_f(B.x), as_f(B.y), B.z, lon, lat, mlon, mlat, sq, sc);
+      put_cand(g, b, p, rank, road, sc, sq, op.mode);
     }
   }
   if (lane == 0) b.cand_n[p] = (uint8_t)min(n_found, (uint32_t)kMaxCand);
@@ -361,7 +386,8 @@ __global__ void __launch_bounds__(64) k_candidates_wave(DevGraph g, DevBatch b) 
 }
 
 // ------------------------------------------------------------------------------------------
-// transition counts for the exclusive scan that lays out route[] compactly
+// transition counts for the exclusive scan that lays out route[] compactly, plus the
+// per-pair constants K2 needs (bounds, candidate counts, mode) in one dwordx4
 __global__ void k_trans_count(DevBatch b) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
@@ -374,7 +400,11 @@ __global__ void k_trans_count(DevBatch b) {
     c = KA * KB;
     ns = KB ? KA : 0u;
     const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
-    b.gc[p] = gc_distance(b.lon[pa], b.lat[pa], b.lon[pb], b.lat[pb]);
+    const double gc = gc_distance(b.lon[pa], b.lat[pa], b.lon[pb], b.lat[pb]);
+    b.gc[p] = gc;
+    const MatchOptions op = b.opts[b.trace_opt[k]];
+    b.pair_info[p] = make_uint4(route_bound(gc, op), time_bound(b.time[pb] - b.time[pa], op),
+                                KA | (KB << 8) | ((uint32_t)op.mode << 16), 0u);
   }
   b.trans_cnt[p] = c;
   b.src_cnt[p] = ns;
@@ -388,15 +418,53 @@ __global__ void k_src_items(DevBatch b) {
   for (uint32_t i = 0; i < n; ++i) b.src_item[at + i] = (uint32_t)p;
 }
 
-// transition cost |route_m - gc| / beta (meili TransitionCostModel restatement, fp64),
-// +inf for an invalid route; computed where the route is, so K3's inner step is one add
-__device__ __forceinline__ double trans_cost(uint32_t r, double gc, double beta) {
+// transition cost |route_m - gc| * (1/beta) (meili TransitionCostModel restatement, fp64),
+// +inf for an invalid route.  K2 stores only the route length (4 B per transition);
+// K3 evaluates this where it consumes the route.
+__device__ __forceinline__ double trans_cost(uint32_t r, double gc, double inv_beta) {
   if (r == kRouteInvalid) return __longlong_as_double(0x7ff0000000000000ll);
-  return fabs((double)r * 0.01 - gc) / beta;
+  return fabs((double)r * 0.01 - gc) * inv_beta;
+}
+
+// descriptor field access (see Workspace::cand_desc)
+__device__ __forceinline__ uint32_t d_spf(const uint4& d0) { return d0.w & 0xffffu; }
+__device__ __forceinline__ uint32_t d_spr(const uint4& d0) { return d0.w >> 16; }
+
+// route key from a source candidate a to a target candidate b given a label lookup
+// (dist, time of the shortest route to a node); combos in the oracle's fixed order:
+// direct forward, direct reverse, entry forward (via node0), entry reverse (via node1)
+template <class Label>
+__device__ __forceinline__ unsigned long long route_key(const Label& label, const uint4& a0, const uint4& b0,
+                                                        const uint4& b1, int* combo) {
+  const uint32_t sa = a0.y, rb = b0.x, sb = b0.y, L = b0.z, spf = d_spf(b0), spr = d_spr(b0);
+  unsigned long long best = kKeyInf;
+  int bc = -1;
+  if (a0.x == rb) {
+    if (spf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
+    if (spr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
+  }
+  if (spf) {
+    const unsigned long long lab = label(b1.x);
+    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(sb, time_ms(sb, spf)); if (k < best) { best = k; bc = 2; } }
+  }
+  if (spr) {
+    const unsigned long long lab = label(b1.y);
+    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(L - sb, time_ms(L - sb, spr)); if (k < best) { best = k; bc = 3; } }
+  }
+  if (combo) *combo = bc;
+  return best;
+}
+
+// root keys of a source candidate's two exits (forward to node1, reverse to node0)
+__device__ __forceinline__ void exit_keys(const uint4& a0, uint32_t bound, unsigned long long& rk1,
+                                          unsigned long long& rk0) {
+  const uint32_t s = a0.y, L = a0.z, spf = d_spf(a0), spr = d_spr(a0);
+  rk1 = (spf && L - s <= bound) ? make_key(L - s, time_ms(L - s, spf)) : kKeyInf;
+  rk0 = (spr && s <= bound) ? make_key(s, time_ms(s, spr)) : kKeyInf;
 }
 
 // ------------------------------------------------------------------------------------------
-// Bounded search shared by K2 (routes) and the path kernel.
+// Bounded search shared by the wave tiers of K2 (routes) and of the path kernel.
 template <int H, bool PATH>
 struct SearchSmem {
   uint32_t key[H];                 // (source << 28) | node
@@ -446,11 +514,11 @@ __device__ __forceinline__ unsigned long long h_label(const SearchSmem<H, PATH>&
 }
 
 // Exact lexicographic shortest (dist, time) keys from the exits of n_src source
-// candidates (source ids 0..n_src-1) to every node within `bound` cm, by
-// synchronous label-correcting rounds over an LDS frontier.  All 64 lanes call it.
+// candidates (descriptors src[0..n_src), source ids 0..n_src-1) to every node within
+// `bound` cm, by synchronous label-correcting rounds over an LDS frontier.  All 64 lanes call it.
 template <int H, bool PATH>
 __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int mode, uint32_t bound,
-                               const uint32_t* roads, const uint32_t* offs, uint32_t n_src) {
+                               const uint4* src, uint32_t n_src) {
   const int lane = threadIdx.x;
   const uint32_t acc = mode_access(mode);
   for (int h = lane; h < H; h += kWave) {
@@ -461,20 +529,16 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
   __syncthreads();
   if ((uint32_t)lane < 2u * n_src) {  // roots: two exits per source
     const uint32_t i = lane >> 1;
-    const uint32_t road = roads[i], s = offs[i];
-    const uint32_t L = g.road_len[road];
-    const uint32_t e = (lane & 1) ? g.road_rev[road] : g.road_fwd[road];
-    if (e != kNone) {
-      const uint4 rec = g.edges[e];
-      const uint32_t d = (lane & 1) ? s : L - s;
-      if (edge_ok(rec.z, acc) && d <= bound) {
-        const uint32_t node = (lane & 1) ? g.road_node0[road] : g.road_node1[road];
-        const unsigned long long kk = make_key(d, time_ms(d, mode_speed_dkph(mode, rec.z & 0xffffu)));
-        const int slot = h_insert(sm, (i << 28) | node);
-        if (slot >= 0) {
-          const unsigned long long old = atomicMin(&sm.lab[slot], kk);
-          if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[atomicAdd(&sm.nf, 1u)] = (uint16_t)slot;
-        }
+    const uint4 a0 = src[2 * i], a1 = src[2 * i + 1];
+    unsigned long long rk1, rk0;
+    exit_keys(a0, bound, rk1, rk0);
+    const unsigned long long kk = (lane & 1) ? rk0 : rk1;
+    if (kk != kKeyInf) {
+      const uint32_t node = (lane & 1) ? a1.x : a1.y;
+      const int slot = h_insert(sm, (i << 28) | node);
+      if (slot >= 0) {
+        const unsigned long long old = atomicMin(&sm.lab[slot], kk);
+        if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[atomicAdd(&sm.nf, 1u)] = (uint16_t)slot;
       }
     }
   }
@@ -511,39 +575,22 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
   __syncthreads();
 }
 
-// route key from searched source `src` to target candidate (rb, sb); combo as in the oracle
 template <int H, bool PATH>
-__device__ unsigned long long route_to(const SearchSmem<H, PATH>& sm, const DevGraph& g, int mode, uint32_t src,
-                                       uint32_t ra, uint32_t sa, uint32_t rb, uint32_t sb, int* combo) {
-  const uint32_t acc = mode_access(mode);
-  const uint32_t ef = g.road_fwd[rb], er = g.road_rev[rb], L = g.road_len[rb];
-  const uint32_t inf_f = ef != kNone ? g.edges[ef].z : 0u, inf_r = er != kNone ? g.edges[er].z : 0u;
-  const bool okf = ef != kNone && edge_ok(inf_f, acc), okr = er != kNone && edge_ok(inf_r, acc);
-  const uint32_t spf = mode_speed_dkph(mode, inf_f & 0xffffu), spr = mode_speed_dkph(mode, inf_r & 0xffffu);
-  unsigned long long best = kKeyInf;
-  int bc = -1;
-  if (ra == rb) {
-    if (okf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
-    if (okr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
-  }
-  if (okf) {
-    const unsigned long long lab = h_label(sm, (src << 28) | g.road_node0[rb]);
-    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(sb, time_ms(sb, spf)); if (k < best) { best = k; bc = 2; } }
-  }
-  if (okr) {
-    const unsigned long long lab = h_label(sm, (src << 28) | g.road_node1[rb]);
-    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(L - sb, time_ms(L - sb, spr)); if (k < best) { best = k; bc = 3; } }
-  }
-  if (combo) *combo = bc;
-  return best;
-}
+struct HashLabel {
+  const SearchSmem<H, PATH>& sm;
+  uint32_t srcbits;
+  __device__ unsigned long long operator()(uint32_t node) const { return h_label(sm, srcbits | node); }
+};
 
 // ------------------------------------------------------------------------------------------
 // Lane tier: one lane runs one whole bounded Dijkstra with its labels in registers.
-// C2-class searches settle ~1.5 nodes and touch ~5 (profiles/r01), so a wave-wide
-// search wastes 60 lanes and pays LDS init + barriers; 16 register slots hold the
-// common case and anything larger goes to the wave tiers above.  Same exact keys.
-constexpr int kLaneCap = 8;
+// Most searches settle a handful of nodes, so a wave-wide search would waste 60 lanes
+// and pay LDS init + barriers; kLaneCap register slots hold the common case and anything
+// larger goes to the wave tiers below.  Same exact keys.
+#ifndef RM_LANE_CAP
+#define RM_LANE_CAP 8
+#endif
+constexpr int kLaneCap = RM_LANE_CAP;
 
 struct LaneSearch {
   uint32_t node[kLaneCap];
@@ -560,13 +607,10 @@ __device__ __forceinline__ unsigned long long ls_label(const LaneSearch& s, uint
   return k;
 }
 
-__device__ __forceinline__ int ls_index(const LaneSearch& s, uint32_t v) {
-  int f = -1;
-#pragma unroll
-  for (int x = 0; x < kLaneCap; ++x)
-    if (x < (int)s.n && s.node[x] == v) f = x;
-  return f;
-}
+struct LaneLabel {
+  const LaneSearch& s;
+  __device__ unsigned long long operator()(uint32_t node) const { return ls_label(s, node); }
+};
 
 __device__ __forceinline__ void ls_relax(LaneSearch& s, uint32_t v, unsigned long long k) {
   bool found = false;
@@ -584,27 +628,13 @@ __device__ __forceinline__ void ls_relax(LaneSearch& s, uint32_t v, unsigned lon
   s.n++;
 }
 
-// bounded Dijkstra from the exits of candidate (road, s); returns the root keys
+// bounded Dijkstra from the exits of the candidate described by (a0, a1)
 __device__ void lane_search(LaneSearch& S, const DevGraph& g, int mode, uint32_t acc, uint32_t bound,
-                            uint32_t road, uint32_t s, unsigned long long& rk1, unsigned long long& rk0) {
+                            const uint4& a0, const uint4& a1, unsigned long long& rk1, unsigned long long& rk0) {
   S.n = 0; S.settled = 0; S.ovf = false;
-  rk1 = kKeyInf; rk0 = kKeyInf;
-  const uint32_t L = g.road_len[road];
-  const uint32_t ef = g.road_fwd[road], er = g.road_rev[road];
-  if (ef != kNone) {
-    const uint32_t z = g.edges[ef].z;
-    if (edge_ok(z, acc) && L - s <= bound) {
-      rk1 = make_key(L - s, time_ms(L - s, mode_speed_dkph(mode, z & 0xffffu)));
-      ls_relax(S, g.road_node1[road], rk1);
-    }
-  }
-  if (er != kNone) {
-    const uint32_t z = g.edges[er].z;
-    if (edge_ok(z, acc) && s <= bound) {
-      rk0 = make_key(s, time_ms(s, mode_speed_dkph(mode, z & 0xffffu)));
-      ls_relax(S, g.road_node0[road], rk0);
-    }
-  }
+  exit_keys(a0, bound, rk1, rk0);
+  if (rk1 != kKeyInf) ls_relax(S, a1.y, rk1);
+  if (rk0 != kKeyInf) ls_relax(S, a1.x, rk0);
   for (;;) {
     int bi = -1;
     unsigned long long bk = kKeyInf;
@@ -626,53 +656,25 @@ __device__ void lane_search(LaneSearch& S, const DevGraph& g, int mode, uint32_t
   }
 }
 
-__device__ __forceinline__ unsigned long long lane_route_to(const LaneSearch& S, const DevGraph& g, int mode,
-                                                            uint32_t acc, uint32_t ra, uint32_t sa, uint32_t rb,
-                                                            uint32_t sb, int* combo) {
-  const uint32_t ef = g.road_fwd[rb], er = g.road_rev[rb], L = g.road_len[rb];
-  const uint32_t inf_f = ef != kNone ? g.edges[ef].z : 0u, inf_r = er != kNone ? g.edges[er].z : 0u;
-  const bool okf = ef != kNone && edge_ok(inf_f, acc), okr = er != kNone && edge_ok(inf_r, acc);
-  const uint32_t spf = mode_speed_dkph(mode, inf_f & 0xffffu), spr = mode_speed_dkph(mode, inf_r & 0xffffu);
-  unsigned long long best = kKeyInf;
-  int bc = -1;
-  if (ra == rb) {
-    if (okf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
-    if (okr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
-  }
-  if (okf) {
-    const unsigned long long lab = ls_label(S, g.road_node0[rb]);
-    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(sb, time_ms(sb, spf)); if (k < best) { best = k; bc = 2; } }
-  }
-  if (okr) {
-    const unsigned long long lab = ls_label(S, g.road_node1[rb]);
-    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(L - sb, time_ms(L - sb, spr)); if (k < best) { best = k; bc = 3; } }
-  }
-  if (combo) *combo = bc;
-  return best;
-}
-
-// K2 lane tier: one lane per (layer pair, source) item.  A pair any of whose searches
-// outgrows the registers is queued once (the src_cnt word is consumed as a flag) for
-// the wave tier, which recomputes the whole pair.
+// K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
+// one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A pair any of
+// whose searches outgrows the registers is queued once (the src_cnt word is consumed as a
+// flag) for the wave tier, which recomputes the whole pair.
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_items) return;
   const uint32_t p = b.src_item[t];
+  const uint4 pi = b.pair_info[p];
   const uint32_t i = t - b.src_off[p];
-  const uint32_t k = b.slot_trace[p];
-  const uint32_t o = b.trace_off[k];
-  const MatchOptions op = b.opts[b.trace_opt[k]];
-  const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
-  const double gc = b.gc[p];
-  const uint32_t KB = b.cand_n[p];
-  const int mode = op.mode;
+  const uint32_t base = b.trans_off[p];
+  const uint32_t bound = pi.x, tmax = pi.y, KB = (pi.z >> 8) & 0xffu;
+  const int mode = (int)(pi.z >> 16);
   const uint32_t acc = mode_access(mode);
-  const uint32_t bound = route_bound(gc, op);
-  const uint32_t tmax = time_bound(b.time[pb] - b.time[pa], op);
-  const uint32_t ra = b.cand_road[(uint64_t)(p - 1) * kMaxCand + i], sa = b.cand_s[(uint64_t)(p - 1) * kMaxCand + i];
+  const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+  const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
   LaneSearch S;
   unsigned long long rk1, rk0;
-  lane_search(S, g, mode, acc, bound, ra, sa, rk1, rk0);
+  lane_search(S, g, mode, acc, bound, a0, a1, rk1, rk0);
   if (S.ovf) {
     if (atomicExch(&b.src_cnt[p], 0u) != 0u) {
       const uint32_t q = atomicAdd(&b.ctl[3], 1u);
@@ -683,30 +685,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   // targets four at a time with clamped (branch-free) loads; results go to LDS and are
   // stored after the last load (a store before a load-use costs a full round trip)
   __shared__ uint32_t s_res[kMaxCand][256];
-  const uint64_t rowb = (uint64_t)p * kMaxCand;
+  const uint64_t brow = (uint64_t)p * kMaxCand * 2;
+  const LaneLabel lab{S};
   for (uint32_t j0 = 0; j0 < KB; j0 += 4) {
-    uint32_t rb[4], sb[4];
+    uint4 t0[4], t1[4];
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
       const uint32_t jc = min(j0 + x, KB - 1u);
-      rb[x] = b.cand_road[rowb + jc];
-      sb[x] = b.cand_s[rowb + jc];
+      t0[x] = b.cand_desc[brow + 2 * jc];
+      t1[x] = b.cand_desc[brow + 2 * jc + 1];
     }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
-      const unsigned long long key = lane_route_to(S, g, mode, acc, ra, sa, rb[x], sb[x], nullptr);
+      const unsigned long long key = route_key(lab, a0, t0[x], t1[x], nullptr);
       uint32_t r = kRouteInvalid;
       if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
       s_res[(j0 + x) & (kMaxCand - 1)][threadIdx.x] = r;
     }
   }
-  const uint64_t ob = (uint64_t)b.trans_off[p] + i * KB;
-  const double beta = (double)op.beta;
-  for (uint32_t j = 0; j < KB; ++j) {
-    const uint32_t r = s_res[j][threadIdx.x];
-    b.route[ob + j] = r;
-    b.tcost[ob + j] = trans_cost(r, gc, beta);
-  }
+  const uint64_t ob = (uint64_t)base + i * KB;
+  for (uint32_t j = 0; j < KB; ++j) b.route[ob + j] = s_res[j][threadIdx.x];
 }
 
 // path lane tier: one lane per chosen transition; canonical predecessors in registers.
@@ -718,29 +716,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const uint32_t s = (uint32_t)(p - o);
   if (s < 1 || s >= b.n_states[k]) return;
   if (b.chain_start[p] || b.choice[p] < 0) return;
-  const MatchOptions op = b.opts[b.trace_opt[k]];
-  const int mode = op.mode;
+  const uint4 pi = b.pair_info[p];
+  const int mode = (int)(pi.z >> 16);
   const uint32_t acc = mode_access(mode);
+  const uint32_t bound = pi.x;
   const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
-  const uint32_t ra = b.cand_road[(p - 1) * kMaxCand + i], sa = b.cand_s[(p - 1) * kMaxCand + i];
-  const uint32_t rb = b.cand_road[p * kMaxCand + j], sb = b.cand_s[p * kMaxCand + j];
-  const uint32_t bound = route_bound(b.gc[p], op);
+  const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
+  const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
   LaneSearch S;
   unsigned long long rk1, rk0;
-  lane_search(S, g, mode, acc, bound, ra, sa, rk1, rk0);
+  lane_search(S, g, mode, acc, bound, a0, a1, rk1, rk0);
   if (S.ovf) {
     const uint32_t q = atomicAdd(&b.ctl[4], 1u);
     b.rl_paths_a[q] = (uint32_t)p;
     return;
   }
   int combo = -1;
-  const unsigned long long key = lane_route_to(S, g, mode, acc, ra, sa, rb, sb, &combo);
-  const uint32_t n1a = g.road_node1[ra], n0a = g.road_node0[ra];
+  const unsigned long long key = route_key(LaneLabel{S}, a0, b0, b1, &combo);
+  const uint32_t n1a = a1.y, n0a = a1.x;
   uint32_t* inl = b.path_inline + p * kInlinePath;
   if (combo <= 1) {
-    const uint32_t e = combo == 0 ? g.road_fwd[ra] : g.road_rev[ra];
     b.route_dist[p] = key_dist(key);
-    inl[0] = e;
+    inl[0] = combo == 0 ? a1.z : a1.w;
     b.path_cnt[p] = 1;
     b.path_off[p] = 0;
     return;
@@ -749,8 +746,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   // smallest-id tight in-edge from a labelled node (in-edges are sorted by edge id).
   // Edges are shifted into registers (front = travel order) and stored after the walk:
   // a store inside the walk would make every following load wait for it (shared vmcnt).
-  const uint32_t entry_e = combo == 2 ? g.road_fwd[rb] : g.road_rev[rb];
-  const uint32_t v0 = combo == 2 ? g.road_node0[rb] : g.road_node1[rb];
+  const uint32_t entry_e = combo == 2 ? b1.z : b1.w;
+  const uint32_t v0 = combo == 2 ? b1.x : b1.y;
   uint32_t n = 1, x = v0;
   uint32_t pr[kInlinePath];
 #pragma unroll
@@ -775,7 +772,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     ++n;
     x = pu;
   }
-  const uint32_t exit_e = (x == n1a) ? g.road_fwd[ra] : g.road_rev[ra];
+  const uint32_t exit_e = (x == n1a) ? a1.z : a1.w;
 #pragma unroll
   for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
   pr[0] = exit_e;
@@ -811,35 +808,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 }
 
 // ------------------------------------------------------------------------------------------
-// K2 k_routes: one wave per layer pair (s-1 -> s).  SMALL tier searches all sources at
+// K2 wave tiers: one wave per layer pair (s-1 -> s).  SMALL tier searches all sources at
 // once in a 256-slot hash; a pair that overflows is queued for the BIG tier, which
 // searches one source at a time in a 4096-slot hash.
 template <bool BIG>
 __global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
   constexpr int H = BIG ? kBigH : kSmallH;
   __shared__ SearchSmem<H, false> sm;
-  __shared__ uint32_t s_road[kMaxCand], s_off[kMaxCand];
+  __shared__ uint4 s_src[2 * kMaxCand];
   const int lane = threadIdx.x;
   const uint32_t n_items = min(b.ctl[BIG ? 5 : 3], (uint32_t)b.P);
   const uint32_t* list = BIG ? b.rl_routes_b : b.rl_routes_a;
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const uint64_t p = list[item];
-    const uint32_t k = b.slot_trace[p];
-    const uint32_t o = b.trace_off[k];
-    const MatchOptions op = b.opts[b.trace_opt[k]];
-    const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
-    const double gc = b.gc[p];
-    const uint32_t KA = b.cand_n[p - 1], KB = b.cand_n[p];
-    const uint32_t bound = route_bound(gc, op);
-    const uint32_t tmax = time_bound(b.time[pb] - b.time[pa], op);
+    const uint4 pi = b.pair_info[p];
+    const uint32_t KA = pi.z & 0xffu, KB = (pi.z >> 8) & 0xffu;
+    const int mode = (int)(pi.z >> 16);
+    const uint32_t bound = pi.x, tmax = pi.y;
     const uint32_t base = b.trans_off[p];
-    if (lane < (int)KA) {
-      s_road[lane] = b.cand_road[(p - 1) * kMaxCand + lane];
-      s_off[lane] = b.cand_s[(p - 1) * kMaxCand + lane];
-    }
+    if (lane < (int)(2 * KA)) s_src[lane] = b.cand_desc[(p - 1) * kMaxCand * 2 + lane];
     __syncthreads();
     if (!BIG) {
-      bounded_search<H, false>(sm, g, op.mode, bound, s_road, s_off, KA);
+      bounded_search<H, false>(sm, g, mode, bound, s_src, KA);
       if (sm.ovf) {
         if (lane == 0) {
           const uint32_t q = atomicAdd(&b.ctl[5], 1u);
@@ -850,24 +840,22 @@ __global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
       }
       for (uint32_t t = lane; t < KA * KB; t += kWave) {
         const uint32_t i = t / KB, j = t - i * KB;
-        const uint32_t rb = b.cand_road[p * kMaxCand + j], sb = b.cand_s[p * kMaxCand + j];
-        const unsigned long long key = route_to(sm, g, op.mode, i, s_road[i], s_off[i], rb, sb, nullptr);
+        const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+        const unsigned long long key = route_key(HashLabel<H, false>{sm, i << 28}, s_src[2 * i], t0, t1, nullptr);
         uint32_t out = kRouteInvalid;
         if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
         b.route[base + t] = out;
-        b.tcost[base + t] = trans_cost(out, gc, (double)op.beta);
       }
     } else {
       for (uint32_t i = 0; i < KA; ++i) {
-        bounded_search<H, false>(sm, g, op.mode, bound, s_road + i, s_off + i, 1);
+        bounded_search<H, false>(sm, g, mode, bound, s_src + 2 * i, 1);
         if (sm.ovf) { if (lane == 0) atomicOr(&b.ctl[2], kErrSearchOverflow); break; }
         for (uint32_t j = lane; j < KB; j += kWave) {
-          const uint32_t rb = b.cand_road[p * kMaxCand + j], sb = b.cand_s[p * kMaxCand + j];
-          const unsigned long long key = route_to(sm, g, op.mode, 0, s_road[i], s_off[i], rb, sb, nullptr);
+          const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+          const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[2 * i], t0, t1, nullptr);
           uint32_t out = kRouteInvalid;
           if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
           b.route[base + i * KB + j] = out;
-          b.tcost[base + i * KB + j] = trans_cost(out, gc, (double)op.beta);
         }
         __syncthreads();
       }
@@ -877,30 +865,32 @@ __global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
 }
 
 // ------------------------------------------------------------------------------------------
-// K3 k_viterbi: 16 lanes per trace (4 traces per wave), lane j owns candidate j.
-__device__ __forceinline__ double shfl_d(double v, int src) {
-  const unsigned long long u = __double_as_longlong(v);
-  const int lo = __shfl((int)(uint32_t)u, src, 16), hi = __shfl((int)(uint32_t)(u >> 32), src, 16);
-  return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
-// LDS per 16-lane trace group.  The forward pass never touches global memory inside a
-// layer: on gfx9 loads and stores share vmcnt, so one pending store would make the next
-// load-use wait for it.  Each chunk of <=16 layers is staged with branch-free loads,
-// processed out of LDS (routes, emissions, previous-layer costs), and its back-pointer
-// rows and chain flags are flushed with one coalesced store per lane at the chunk end.
-constexpr int kVitChunk = 16;      // layers per staged chunk (one per lane of the group)
-constexpr int kVitRouteCap = 160;  // transition costs per staged chunk
-constexpr int kVitBpBlock = 16;    // layers per staged back-pointer block (backtrace)
-struct VitGroupSmem {
-  double tc[kVitRouteCap];             // transition costs (reads use clamped indices)
+// K3 k_viterbi: 16 lanes per trace, 4 traces per wave; lane j owns candidate j of the
+// current layer.  A wave64 VALU instruction costs a SIMD four cycles, so the layer
+// recurrence is packed four traces to an instruction (one trace per wave would spend
+// ~4x the issue slots on the same work).  Each group streams its trace through LDS in
+// chunks of <= 16 layers / <= kVitRoutes routes: one lane describes one layer, a 16-lane
+// scan lays the chunk out, and routes / emission rows arrive with coalesced loads while
+// the next chunk's descriptor is already in flight.  No global store is issued inside a
+// chunk (gfx9 loads and stores share vmcnt): back-pointer rows and chain flags are
+// buffered in LDS and flushed once per chunk.
+constexpr int kVitChunk = 16;     // layers per staged chunk (one per lane of the group)
+#ifndef RM_VIT_ROUTES
+#define RM_VIT_ROUTES 256
+#endif
+constexpr int kVitRoutes = RM_VIT_ROUTES;  // routes per staged chunk and group
+constexpr int kVitBt = 64;        // layers per backtrace staging block
+struct VitGroup {
+  uint32_t route[kVitRoutes];
   float sq[kVitChunk][16];
-  double cost[16];                     // costs of the previous layer
-  uint32_t kb[kVitChunk], rel[kVitChunk];
   double gc[kVitChunk];
-  uint8_t bpo[kVitChunk][16];          // this chunk's back-pointer rows
-  uint8_t cs[kVitChunk];               // this chunk's chain-start flags
-  uint4 bp[kVitBpBlock];               // backtrace staging
+  double cost[16];                // costs of the previous layer
+  uint32_t kb[kVitChunk], rel[kVitChunk];
+  uint4 bpo[kVitChunk];           // this chunk's back-pointer rows (16 x u8)
+  uint4 bst[kVitBt];              // backtrace staging
+  uint8_t cs[kVitChunk];          // this chunk's chain-start flags
+  uint8_t ch[kVitBt];             // choices of one backtrace block
+  uint32_t nch, done, w, pad;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -909,118 +899,149 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// write rows [s0, s0+n) of the chunk to global (lane q owns layer s0+q)
-__device__ __forceinline__ void vit_flush(const DevBatch& b, const VitGroupSmem& gs, uint64_t l0, uint32_t n, int j) {
+__device__ __forceinline__ double shfl_xor_d(double v, int m, int width) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __shfl_xor((int)(uint32_t)u, m, width), hi = __shfl_xor((int)(uint32_t)(u >> 32), m, width);
+  return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// write back-pointer rows / chain flags of chunk layers [0, n) (layer l at slot l0 + l)
+__device__ __forceinline__ void vit_flush(const DevBatch& b, const VitGroup& gs, uint64_t l0, uint32_t n, int j) {
   if ((uint32_t)j < n) {
-    *reinterpret_cast<uint4*>(b.bp + (l0 + j) * kMaxCand) = *reinterpret_cast<const uint4*>(gs.bpo[j]);
+    *reinterpret_cast<uint4*>(b.bp + (l0 + j) * kMaxCand) = gs.bpo[j];
     b.chain_start[l0 + j] = gs.cs[j];
   }
 }
 
-// Backtrace of the chain ending at layer `end` (costs of that layer in `cost`).  The winner
-// is the lowest-cost candidate (lowest j on ties); back-pointers are staged 64 layers at a
-// time; a layer whose winner's back-pointer is 255 starts the chain.
-__device__ void backtrace_chain(const DevBatch& b, VitGroupSmem& gs, uint32_t o, uint32_t end, uint32_t K,
-                                double cost, int j) {
-  double bc = (j < (int)K) ? cost : __longlong_as_double(0x7ff0000000000000ll);
+// Backtrace of the chain ending at layer `end` (costs of that layer in gs.cost, K
+// candidates).  Winner = lowest cost, ties to the lowest j.  Rows are staged 64 layers
+// per block (four coalesced loads per lane); lane 0 of the group walks them in LDS and
+// the block's choices leave as one store per lane.
+__device__ void backtrace_chain(const DevBatch& b, VitGroup& gs, uint32_t o, uint32_t end, uint32_t K, int j) {
+  double bc = (j < (int)K) ? gs.cost[j] : __longlong_as_double(0x7ff0000000000000ll);
   int bj = (j < (int)K) ? j : 1 << 20;
-  for (int off = 8; off > 0; off >>= 1) {
-    const double oc = shfl_d(bc, (threadIdx.x & 48) | ((j + off) & 15));
-    const int oj = __shfl(bj, (j + off) & 15, 16);
+  for (int m = 1; m < 16; m <<= 1) {
+    const double oc = shfl_xor_d(bc, m, 16);
+    const int oj = __shfl_xor(bj, m, 16);
     if (oc < bc || (oc == bc && oj < bj)) { bc = oc; bj = oj; }
   }
-  int w = __shfl(bj, 0, 16);
+  uint32_t w = (uint32_t)bj;
   __threadfence_block();  // this wave's bp stores are visible to its loads
   int t = (int)end;
-  bool done = false;
-  while (!done) {
-    const int lo = t - (kVitBpBlock - 1) < 0 ? 0 : t - (kVitBpBlock - 1);
-    {
-      uint4 rows[kVitBpBlock / 16];
+  for (;;) {
 #pragma unroll
-      for (int x = 0; x < kVitBpBlock / 16; ++x) {
-        const int r = min(lo + j + 16 * x, t);   // clamped: no divergent loads
-        rows[x] = *reinterpret_cast<const uint4*>(b.bp + (uint64_t)(o + r) * kMaxCand);
-      }
-#pragma unroll
-      for (int x = 0; x < kVitBpBlock / 16; ++x) gs.bp[j + 16 * x] = rows[x];
+    for (int x = 0; x < kVitBt / 16; ++x) {
+      const int lay = t - (j + 16 * x);
+      uint4 row = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+      if (lay >= 0) row = *reinterpret_cast<const uint4*>(b.bp + (uint64_t)(o + lay) * kMaxCand);
+      gs.bst[j + 16 * x] = row;
     }
     wave_sync();
     if (j == 0) {
-      for (; t >= lo; --t) {
-        b.choice[o + t] = (int8_t)w;
-        const uint4 row = gs.bp[t - lo];
-        const uint32_t word = w < 4 ? row.x : (w < 8 ? row.y : (w < 12 ? row.z : row.w));
-        const uint32_t nb = (word >> (8 * (w & 3))) & 0xffu;
-        if (nb == 255u) { done = true; break; }
-        w = (int)nb;
+      uint32_t l = 0, done = 0;
+      for (; l < (uint32_t)kVitBt && t - (int)l >= 0;) {
+        gs.ch[l] = (uint8_t)w;
+        const uint32_t nb = reinterpret_cast<const uint8_t*>(&gs.bst[l])[w];
+        ++l;
+        if (nb == 255u) { done = 1; break; }
+        w = nb;
       }
+      if (t - (int)l < 0) done = 1;
+      gs.nch = l; gs.done = done; gs.w = w;
     }
-    t = __shfl(t, 0, 16);
-    w = __shfl(w, 0, 16);
-    done = __shfl((int)done, 0, 16) != 0;
     wave_sync();
+    const uint32_t n = gs.nch;
+#pragma unroll
+    for (int x = 0; x < kVitBt / 16; ++x)
+      if ((uint32_t)(j + 16 * x) < n) b.choice[o + t - (j + 16 * x)] = (int8_t)gs.ch[j + 16 * x];
+    const bool done = gs.done != 0;
+    w = gs.w;
+    t -= (int)n;
+    wave_sync();
+    if (done) break;
   }
 }
 
 __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
-  __shared__ VitGroupSmem smem[4];
-  const int j = threadIdx.x & 15;
-  const int gbase = threadIdx.x & 48;
-  VitGroupSmem& gs = smem[threadIdx.x >> 4];
-  const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 4);
-  if (k >= b.T) return;
-  const uint32_t o = b.trace_off[k], S = b.n_states[k];
-  const MatchOptions op = b.opts[b.trace_opt[k]];
+  __shared__ VitGroup smem[4];
+  const int lane = threadIdx.x;
+  const int j = lane & 15, gb = lane & 48;
+  VitGroup& gs = smem[lane >> 4];
+  const uint32_t k = blockIdx.x * 4 + (lane >> 4);
+  const bool active = k < b.T;
+  const uint32_t o = active ? b.trace_off[k] : 0u, S = active ? b.n_states[k] : 0u;
+  const MatchOptions op = b.opts[active ? b.trace_opt[k] : 0u];
   const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
+  const double inv_beta = 1.0 / (double)op.beta;
   const double brk = (double)op.breakage_distance;
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   bool prev_ok = false;
-  double cost = INF;
   uint32_t prevK = 0;
-  for (uint32_t s0 = 0; s0 < S;) {
-    // ---- chunk descriptors: lane q describes layer s0+q (clamped, branch-free loads)
-    const uint32_t sq_ = s0 + j;
-    const bool vq = sq_ < S;
-    const uint64_t lq = o + min(sq_, S - 1);
+  // chunk descriptor: lane j describes layer s0 + j (clamped, branch-free loads)
+  uint32_t kbq = 0, cntq = 0, offq = 0;
+  double gcq = 0.0;
+  auto describe = [&](uint32_t s0) {
+    const uint32_t sl = s0 + j;
+    const bool vq = sl < S;
+    const uint64_t lq = o + min(sl, S - 1);
     const uint64_t lp = lq == o ? o : lq - 1;
     const uint32_t kb_raw = b.cand_n[lq], ka_raw = b.cand_n[lp];
-    const double gc_raw = b.gc[lq];
-    const uint32_t off_raw = b.trans_off[lq];
-    const bool hasprev = vq && sq_ >= 1;
-    const uint32_t kbq = vq ? kb_raw : 0u;
-    const uint32_t tcq = hasprev ? ka_raw * kbq : 0u;
-    const double gcq = hasprev ? gc_raw : 0.0;
-    const uint32_t offq = hasprev ? off_raw : 0u;
-    uint32_t incl = tcq;
+    const double g_raw = b.gc[lq];
+    offq = b.trans_off[lq];
+    kbq = vq ? kb_raw : 0u;
+    cntq = (vq && sl >= 1) ? ka_raw * kbq : 0u;
+    gcq = (vq && sl >= 1) ? g_raw : 0.0;
+  };
+  if (S) describe(0);
+  uint32_t s0 = 0;
+  for (;;) {
+    const bool live = s0 < S;
+    if (__ballot(live) == 0ull) break;
+    // ---- lay the chunk out: inclusive scan of route counts over the group's 16 layers
+    uint32_t incl = cntq;
+#pragma unroll
     for (int d = 1; d < 16; d <<= 1) {
       const uint32_t u = __shfl_up(incl, d, 16);
       if (j >= d) incl += u;
     }
-    const uint32_t excl = incl - tcq;
-    const unsigned long long fit = __ballot(vq && incl <= (uint32_t)kVitRouteCap);
-    const uint32_t gfit = (uint32_t)((fit >> gbase) & 0xffffull);
-    const uint32_t C = (uint32_t)__builtin_ctz(~gfit);  // leading layers whose routes fit (>= 1)
-    const int p0 = (s0 == 0) ? 1 : 0;                     // layer 0 has no incoming routes
-    const uint32_t rstart = (C > (uint32_t)p0) ? (__shfl(offq, p0, 16) - __shfl(excl, p0, 16)) : 0u;
-    const uint32_t total = __shfl(incl, (int)C - 1, 16);
-    {
-      const uint32_t tm1 = total ? total - 1u : 0u;
-      double rv[kVitRouteCap / 16];
+    const uint32_t excl = incl - cntq;
+    const uint32_t fit = (uint32_t)((__ballot(live && s0 + j < S && incl <= (uint32_t)kVitRoutes) >> gb) & 0xffffull);
+    const uint32_t C = live ? (uint32_t)__builtin_ctz(~fit | 0x10000u) : 0u;   // leading layers that fit
+    const uint32_t nroutes = C ? (uint32_t)__shfl(incl, (int)C - 1, 16) : 0u;
+    const uint32_t rbase = (uint32_t)__shfl(offq, 0, 16);                     // routes of layer s0 start here
+    // ---- coalesced loads of the chunk's routes and emission rows
+    uint32_t rv[kVitRoutes / 16];
+    const uint32_t rlast = nroutes ? nroutes - 1u : 0u;
 #pragma unroll
-      for (int x = 0; x < kVitRouteCap / 16; ++x) rv[x] = b.tcost[rstart + min((uint32_t)j + 16u * x, tm1)];
-      float sv[kVitChunk];
+    for (int x = 0; x < kVitRoutes / 16; ++x)
+      if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
+    float4 sv[4];
+    if (C) {
+      const uint64_t f0 = (uint64_t)(o + s0) * (kMaxCand / 4), flast = f0 + (uint64_t)C * (kMaxCand / 4) - 1;
+      const float4* src = reinterpret_cast<const float4*>(b.cand_sq);
 #pragma unroll
-      for (int t = 0; t < kVitChunk; ++t) sv[t] = b.cand_sq[(o + s0 + min((uint32_t)t, C - 1)) * kMaxCand + j];
-#pragma unroll
-      for (int x = 0; x < kVitRouteCap / 16; ++x) gs.tc[j + 16 * x] = rv[x];
-#pragma unroll
-      for (int t = 0; t < kVitChunk; ++t) gs.sq[t][j] = sv[t];
-      gs.kb[j] = kbq; gs.rel[j] = excl; gs.gc[j] = gcq;
+      for (int x = 0; x < 4; ++x) sv[x] = src[min(f0 + j + 16u * x, flast)];
     }
+    const uint32_t kb_here = kbq, rel_here = excl;
+    const double gc_here = gcq;
+    // ---- descriptor of the next chunk (its loads overlap this chunk's work)
+    if (live && s0 + C < S) describe(s0 + C);
+    // ---- chunk -> LDS
+#pragma unroll
+    for (int x = 0; x < kVitRoutes / 16; ++x)
+      if ((uint32_t)j + 16u * x < nroutes) gs.route[j + 16 * x] = rv[x];
+    if (C) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        if ((uint32_t)(j + 16 * x) < C * (kMaxCand / 4)) reinterpret_cast<float4*>(&gs.sq[0][0])[j + 16 * x] = sv[x];
+    }
+    if ((uint32_t)j < C) { gs.kb[j] = kb_here; gs.rel[j] = rel_here; gs.gc[j] = gc_here; }
     wave_sync();
-    // ---- the layers of the chunk, in order, out of LDS
-    for (uint32_t t = 0; t < C; ++t) {
+    uint32_t maxC = max(C, (uint32_t)__shfl_xor((int)C, 16));
+    maxC = max(maxC, (uint32_t)__shfl_xor((int)maxC, 32));
+    // ---- the layers of the chunk, in order, out of LDS (groups with fewer layers idle)
+    for (uint32_t t = 0; t < maxC; ++t) {
+      if (t >= C) continue;
       const uint32_t s = s0 + t;
       const uint32_t KB = gs.kb[t];
       const double gcl = gs.gc[t];
@@ -1031,44 +1052,47 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
       if (KB && !start) {
         const uint32_t jj = min((uint32_t)j, KB - 1u);
         for (uint32_t i0 = 0; i0 < prevK; i0 += 4) {
-          double ci[4], tcx[4];
+          double ci[4];
+          uint32_t rr[4];
 #pragma unroll
           for (int x = 0; x < 4; ++x) {
             const uint32_t i = min(i0 + x, prevK - 1u);
             ci[x] = gs.cost[i];
-            tcx[x] = gs.tc[rel + i * KB + jj];
+            rr[x] = gs.route[rel + i * KB + jj];
           }
-          // an invalid route or unreachable source gives +inf, which never wins
+          // an invalid route or an unreachable source gives +inf, which never wins
 #pragma unroll
           for (int x = 0; x < 4; ++x) {
-            const double c = ci[x] + tcx[x];
+            const double c = ci[x] + trans_cost(rr[x], gcl, inv_beta);
             if (i0 + x < prevK && c < best) { best = c; arg = (int)(i0 + x); }
           }
         }
         if (j >= (int)KB) { best = INF; arg = -1; }
-        const unsigned long long any = __ballot(j < (int)KB && arg >= 0);
-        if (((any >> gbase) & 0xffffull) == 0) start = true;
+        if (((__ballot(j < (int)KB && arg >= 0) >> gb) & 0xffffull) == 0ull) start = true;
       }
       if (s > 0 && prev_ok && (KB == 0 || start)) {
         vit_flush(b, gs, o + s0, t, j);   // rows [s0, s) are needed by the backtrace
-        backtrace_chain(b, gs, o, s - 1, prevK, cost, j);
+        backtrace_chain(b, gs, o, s - 1, prevK, j);
       }
+      uint8_t* row = reinterpret_cast<uint8_t*>(&gs.bpo[t]);
       if (KB == 0) {
-        gs.bpo[t][j] = 255;
+        row[j] = 255;
         if (j == 0) gs.cs[t] = 1;
-        prev_ok = false; prevK = 0; cost = INF;
+        prev_ok = false;
+        prevK = 0;
+        wave_sync();
         continue;
       }
       const double em = (j < (int)KB) ? (double)gs.sq[t][j] * inv2s2 : INF;
       double nc;
-      uint8_t bpj;
-      if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255; }
-      else { nc = (j < (int)KB && arg >= 0) ? best + em : INF; bpj = arg >= 0 ? (uint8_t)arg : (uint8_t)255; }
-      gs.bpo[t][j] = bpj;
-      if (j == 0) gs.cs[t] = start ? 1 : 0;
+      uint32_t bpj;
+      if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255u; }
+      else { nc = (j < (int)KB && arg >= 0) ? best + em : INF; bpj = arg >= 0 ? (uint32_t)arg : 255u; }
+      wave_sync();   // every lane's reads of gs.cost precede the overwrite
       gs.cost[j] = nc;
+      row[j] = (uint8_t)bpj;
+      if (j == 0) gs.cs[t] = start ? 1 : 0;
       wave_sync();
-      cost = nc;
       prev_ok = true;
       prevK = KB;
     }
@@ -1077,33 +1101,33 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
     wave_sync();
     s0 += C;
   }
-  if (prev_ok) backtrace_chain(b, gs, o, S - 1, prevK, cost, j);
+  if (prev_ok) backtrace_chain(b, gs, o, S - 1, prevK, j);
 }
 
 // ------------------------------------------------------------------------------------------
-// k_paths: one wave per chosen transition; re-run the search for (i*, j*), compute
-// canonical predecessors and write the directed-edge path into the pool.
+// k_paths wave tiers: one wave per chosen transition whose search outgrew the lane tier;
+// re-run the search for (i*, j*), compute canonical predecessors and write the
+// directed-edge path.
 template <bool BIG>
 __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
   constexpr int H = BIG ? kBigH : kSmallH;
   __shared__ SearchSmem<H, true> sm;
-  __shared__ uint32_t s_road[1], s_off[1];
+  __shared__ uint4 s_src[2];
   const int lane = threadIdx.x;
   const uint32_t n_items = min(b.ctl[BIG ? 6 : 4], (uint32_t)b.P);
   const uint32_t* list = BIG ? b.rl_paths_b : b.rl_paths_a;
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const uint64_t p = list[item];
-    const uint32_t k = b.slot_trace[p];
-    const MatchOptions op = b.opts[b.trace_opt[k]];
-    const int mode = op.mode;
+    const uint4 pi = b.pair_info[p];
+    const int mode = (int)(pi.z >> 16);
     const uint32_t acc = mode_access(mode);
+    const uint32_t bound = pi.x;
     const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
-    const uint32_t ra = b.cand_road[(p - 1) * kMaxCand + i], sa = b.cand_s[(p - 1) * kMaxCand + i];
-    const uint32_t rb = b.cand_road[p * kMaxCand + j], sb = b.cand_s[p * kMaxCand + j];
-    const uint32_t bound = route_bound(b.gc[p], op);
-    if (lane == 0) { s_road[0] = ra; s_off[0] = sa; }
+    const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+    if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
     __syncthreads();
-    bounded_search<H, true>(sm, g, mode, bound, s_road, s_off, 1);
+    const uint4 a0 = s_src[0], a1 = s_src[1];
+    bounded_search<H, true>(sm, g, mode, bound, s_src, 1);
     if (sm.ovf) {
       if (!BIG) {
         if (lane == 0) { const uint32_t q = atomicAdd(&b.ctl[6], 1u); b.rl_paths_b[q] = (uint32_t)p; }
@@ -1114,16 +1138,10 @@ __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
       continue;
     }
     int combo = -1;
-    const unsigned long long key = route_to(sm, g, mode, 0, ra, sa, rb, sb, &combo);
-    // root keys of the source exits (only roots within the bound exist)
-    const uint32_t La = g.road_len[ra];
-    unsigned long long rk1 = kKeyInf, rk0 = kKeyInf;
-    {
-      const uint32_t ef = g.road_fwd[ra], er = g.road_rev[ra];
-      if (ef != kNone) { const uint32_t z = g.edges[ef].z; if (edge_ok(z, acc) && La - sa <= bound) rk1 = make_key(La - sa, time_ms(La - sa, mode_speed_dkph(mode, z & 0xffffu))); }
-      if (er != kNone) { const uint32_t z = g.edges[er].z; if (edge_ok(z, acc) && sa <= bound) rk0 = make_key(sa, time_ms(sa, mode_speed_dkph(mode, z & 0xffffu))); }
-    }
-    const uint32_t n1a = g.road_node1[ra], n0a = g.road_node0[ra];
+    const unsigned long long key = route_key(HashLabel<H, true>{sm, 0u}, a0, b0, b1, &combo);
+    unsigned long long rk1, rk0;
+    exit_keys(a0, bound, rk1, rk0);   // root keys of the source exits (only roots within the bound exist)
+    const uint32_t n1a = a1.y, n0a = a1.x;
     if (combo >= 2) {
       // canonical predecessors: min edge id among tight in-edges of non-root nodes
       for (int h = lane; h < H; h += kWave) {
@@ -1151,10 +1169,10 @@ __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
     if (lane == 0) {
       uint32_t n = 0;
       if (combo <= 1) {
-        pbuf[n++] = combo == 0 ? g.road_fwd[ra] : g.road_rev[ra];
+        pbuf[n++] = combo == 0 ? a1.z : a1.w;
       } else {
-        pbuf[n++] = combo == 2 ? g.road_fwd[rb] : g.road_rev[rb];   // entry edge (reversed order)
-        uint32_t x = combo == 2 ? g.road_node0[rb] : g.road_node1[rb];
+        pbuf[n++] = combo == 2 ? b1.z : b1.w;   // entry edge (reversed order)
+        uint32_t x = combo == 2 ? b1.x : b1.y;
         for (;;) {
           const int hx = h_find(sm, x);
           if (hx < 0 || n + 2 > (uint32_t)H) { atomicOr(&b.ctl[2], kErrRounds); n = 0; break; }
@@ -1165,7 +1183,7 @@ __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
           pbuf[n++] = e;
           x = g.edge_src[e];
         }
-        if (n) pbuf[n++] = (x == n1a) ? g.road_fwd[ra] : g.road_rev[ra];  // exit edge
+        if (n) pbuf[n++] = (x == n1a) ? a1.z : a1.w;  // exit edge
       }
       uint32_t at = 0;
       if (n > (uint32_t)kInlinePath) {
@@ -1225,29 +1243,6 @@ __device__ __forceinline__ void run_close(const DevGraph& g, RunState& R, Segmen
   R.open = false;
 }
 
-__device__ __forceinline__ void run_feed(const DevGraph& g, RunState& R, const TravRec& t, SegmentRec* out, uint32_t& n) {
-  const bool internal = t.internal != 0u;
-  bool cont = R.open && t.sd == R.sd;
-  if (cont && t.sd == kNone && internal != R.internal) cont = false;
-  if (cont) {
-    if (R.l_en != R.l_len || t.b != 0) cont = false;
-    else if (t.sd != kNone && t.soff != R.l_soff + R.l_len) cont = false;
-  }
-  const uint32_t d = t.en - t.b;
-  const double dt = t.te - t.tb;
-  const bool slow = dt > 0.0 && ((double)d * 0.01) / dt < kQueueSpeedMps;
-  if (!cont) {
-    run_close(g, R, out, n);
-    R.open = true; R.sd = t.sd; R.internal = internal; R.seg_len = t.seg_len;
-    R.f_b = t.b; R.f_soff = t.soff; R.tb = t.tb; R.sb = t.sb;
-    R.tot = 0; R.q = 0; R.way_first = t.way; R.way_last = t.way;
-  } else if (t.way != R.way_first) {
-    R.way_last = t.way;
-  }
-  R.l_en = t.en; R.l_len = t.len; R.l_soff = t.soff; R.te = t.te; R.se = t.se;
-  R.tot += d;
-  R.q = slow ? R.q + d : 0;
-}
 
 __device__ __forceinline__ double interp_time(double ta, double tb, uint64_t x, uint64_t D) {
   if (D == 0) return ta;
@@ -1262,7 +1257,7 @@ __global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
   const uint32_t k = b.slot_trace[l];
   const uint32_t o = b.trace_off[k];
   const uint32_t i = (uint32_t)b.choice[l - 1], j = (uint32_t)b.choice[l];
-  const uint32_t sa = b.cand_s[(l - 1) * kMaxCand + i], sb = b.cand_s[l * kMaxCand + j];
+  const uint32_t sa = b.cand_desc[((l - 1) * kMaxCand + i) * 2].y, sb = b.cand_desc[(l * kMaxCand + j) * 2].y;
   const uint32_t oa = b.state_orig[l - 1], ob = b.state_orig[l];
   const double ta = b.time[o + oa], tb = b.time[o + ob];
   const uint32_t D = b.route_dist[l];
@@ -1565,6 +1560,33 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   dg_.seg_len = upload(allocs_, g.seg_len_cm);
   dg_.cell_off = upload(allocs_, g.grid.cell_off);
   dg_.cell_item = upload(allocs_, g.grid.cell_item);
+  {
+    // K1 reads cell items as self-contained records (no item -> vertex -> road chain)
+    if (g.num_roads() >= (1u << 29)) throw std::runtime_error("graph has too many roads (limit 2^29)");
+    auto acc_of = [&](uint32_t e) { return e == kNone ? 0u : edge_access(g.edges[e].info); };
+    std::vector<uint32_t> rec(8 * (size_t)g.grid.cell_item.size());
+    for (size_t it = 0; it < g.grid.cell_item.size(); ++it) {
+      const uint32_t v = g.grid.cell_item[it];
+      const VertRec& A = g.verts[v];
+      const VertRec& B = g.verts[v + 1];
+      const uint32_t road = A.road;
+      const uint32_t acc = acc_of(g.road_fwd[road]) | acc_of(g.road_rev[road]);
+      uint32_t* r = rec.data() + 8 * it;
+      std::memcpy(r + 0, &A.lon, 4); std::memcpy(r + 1, &A.lat, 4);
+      std::memcpy(r + 2, &B.lon, 4); std::memcpy(r + 3, &B.lat, 4);
+      r[4] = A.cum_cm; r[5] = B.cum_cm; r[6] = road | (acc << 29); r[7] = v;
+    }
+    dg_.cell_rec = (const uint4*)upload(allocs_, rec);
+    // per-road record: both endpoints, length and both directed edges with their info words
+    std::vector<uint32_t> rr(8 * (size_t)g.num_roads());
+    for (uint32_t r = 0; r < g.num_roads(); ++r) {
+      const uint32_t ef = g.road_fwd[r], er = g.road_rev[r];
+      uint32_t* x = rr.data() + 8 * (size_t)r;
+      x[0] = g.road_node0[r]; x[1] = g.road_node1[r]; x[2] = g.road_len_cm[r]; x[3] = ef;
+      x[4] = er; x[5] = ef == kNone ? 0u : g.edges[ef].info; x[6] = er == kNone ? 0u : g.edges[er].info; x[7] = 0;
+    }
+    dg_.road_rec = (const uint4*)upload(allocs_, rr);
+  }
   dg_.lon0 = g.grid.lon0; dg_.lat0 = g.grid.lat0; dg_.dlon = g.grid.dlon; dg_.dlat = g.grid.dlat;
   dg_.ncx = g.grid.ncx; dg_.ncy = g.grid.ncy;
   dg_.n_nodes = g.num_nodes(); dg_.n_edges = g.num_edges(); dg_.n_segments = g.num_segments();
@@ -1620,8 +1642,8 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.lon = dalloc<float>(L, cp); w.lat = dalloc<float>(L, cp); w.time = dalloc<double>(L, cp);
   w.acc = dalloc<float>(L, cp); w.opts = dalloc<MatchOptions>(L, co); w.trace_opt = dalloc<uint32_t>(L, ct);
   w.slot_trace = dalloc<uint32_t>(L, cp); w.n_states = dalloc<uint32_t>(L, ct); w.state_orig = dalloc<uint32_t>(L, cp);
-  w.cand_n = dalloc<uint8_t>(L, cp); w.cand_road = dalloc<uint32_t>(L, cp * kMaxCand);
-  w.cand_s = dalloc<uint32_t>(L, cp * kMaxCand); w.cand_sq = dalloc<float>(L, cp * kMaxCand);
+  w.cand_n = dalloc<uint8_t>(L, cp); w.cand_desc = dalloc<uint4>(L, cp * kMaxCand * 2);
+  w.cand_sq = dalloc<float>(L, cp * kMaxCand); w.pair_info = dalloc<uint4>(L, cp);
   w.trans_cnt = dalloc<uint32_t>(L, cp); w.trans_off = dalloc<uint32_t>(L, cp); w.gc = dalloc<double>(L, cp);
   w.src_cnt = dalloc<uint32_t>(L, cp); w.src_off = dalloc<uint32_t>(L, cp);
   w.choice = dalloc<int8_t>(L, cp); w.chain_start = dalloc<uint8_t>(L, cp); w.bp = dalloc<uint8_t>(L, cp * kMaxCand);
@@ -1639,7 +1661,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.scan_tmp_bytes = tmp;
   w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
-  w.route = nullptr; w.tcost = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
+  w.route = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
   w.run_kind = nullptr; w.run_head = nullptr; w.run_idx = nullptr; w.run_pos = nullptr; w.seg_scan_tmp = nullptr;
   w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
   ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
@@ -1651,10 +1673,8 @@ void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
   Workspace& w = ws_;
   if (!(n <= w.cap_trans && w.route)) {
     if (w.route) { (void)hipFree(w.route); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.route)); }
-    if (w.tcost) { (void)hipFree(w.tcost); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.tcost)); }
     const uint64_t c = n + n / 4 + 1024;
     w.route = dalloc<uint32_t>(w.allocs, c);
-    w.tcost = dalloc<double>(w.allocs, c);
     w.cap_trans = c;
   }
   if (!(n_src <= w.cap_src && w.src_item)) {
@@ -1748,8 +1768,8 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.trace_off = w.trace_off; v.lon = w.lon; v.lat = w.lat; v.time = w.time; v.acc = w.acc;
   v.opts = w.opts; v.trace_opt = w.trace_opt;
   v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig;
-  v.cand_n = w.cand_n; v.cand_road = w.cand_road; v.cand_s = w.cand_s; v.cand_sq = w.cand_sq;
-  v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.tcost = w.tcost;
+  v.cand_n = w.cand_n; v.cand_desc = w.cand_desc; v.cand_sq = w.cand_sq;
+  v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
@@ -1829,14 +1849,13 @@ void Matcher::run_device(const RunParams& rp) {
   n_trans_ = total;
   ensure_trans(total, n_src);
   v.route = w.route;
-  v.tcost = w.tcost;
   v.src_item = w.src_item;
 
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
   if (n_src)
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
-  hipLaunchKernelGGL(k_routes_wave<false>, dim3(2048), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave<false>, dim3(kWaveGrid), dim3(64), 0, st, g, v);
   hipLaunchKernelGGL(k_routes_wave<true>, dim3(1024), dim3(64), 0, st, g, v);
   toc(kKRoutes);
   tic(kKViterbi);
@@ -1845,7 +1864,7 @@ void Matcher::run_device(const RunParams& rp) {
   for (int attempt = 0;; ++attempt) {
     tic(kKPaths);
     hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_wave<false>, dim3(2048), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_wave<false>, dim3(kWaveGrid), dim3(64), 0, st, g, v);
     hipLaunchKernelGGL(k_paths_wave<true>, dim3(1024), dim3(64), 0, st, g, v);
     toc(kKPaths);
     // traversal records are laid out by a scan of path_cnt (0 for slots without a chosen transition)
@@ -1914,8 +1933,11 @@ void Matcher::get_states(uint32_t* n_states, uint32_t* state_orig) {
 void Matcher::get_candidates(uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq) {
   sync();
   RM_HIP(hipMemcpy(cand_n, ws_.cand_n, n_points_, hipMemcpyDeviceToHost));
-  RM_HIP(hipMemcpy(road, ws_.cand_road, n_points_ * kMaxCand * 4, hipMemcpyDeviceToHost));
-  RM_HIP(hipMemcpy(s_cm, ws_.cand_s, n_points_ * kMaxCand * 4, hipMemcpyDeviceToHost));
+  {
+    std::vector<uint4> desc(n_points_ * kMaxCand * 2);
+    RM_HIP(hipMemcpy(desc.data(), ws_.cand_desc, desc.size() * sizeof(uint4), hipMemcpyDeviceToHost));
+    for (uint64_t x = 0; x < n_points_ * kMaxCand; ++x) { road[x] = desc[2 * x].x; s_cm[x] = desc[2 * x].y; }
+  }
   RM_HIP(hipMemcpy(sq, ws_.cand_sq, n_points_ * kMaxCand * 4, hipMemcpyDeviceToHost));
 }
 void Matcher::get_routes(uint32_t* trans_off, double* gc, uint32_t* route) {

@@ -44,6 +44,8 @@ struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   const uint32_t* seg_len;
   const uint32_t* cell_off;
   const uint32_t* cell_item;
+  const uint4* cell_rec;         // per cell item, 2 x uint4: {A.lon, A.lat, B.lon, B.lat}, {A.cum, B.cum, road | acc << 29, vertex}
+  const uint4* road_rec;         // per road, 2 x uint4: {node0, node1, len_cm, fwd edge}, {rev edge, info fwd, info rev, 0}
   double lon0, lat0, dlon, dlat;
   uint32_t ncx, ncy, n_nodes, n_edges, n_segments, pad;
 };
@@ -83,8 +85,11 @@ struct Workspace {
   float* acc = nullptr; MatchOptions* opts = nullptr; uint32_t* trace_opt = nullptr;
   // per slot
   uint32_t* slot_trace = nullptr; uint32_t* n_states = nullptr; uint32_t* state_orig = nullptr;
-  uint8_t* cand_n = nullptr; uint32_t* cand_road = nullptr; uint32_t* cand_s = nullptr; float* cand_sq = nullptr;
-  uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr; double* tcost = nullptr;
+  // candidate descriptors, 2 x uint4 per (slot, rank): {road, s_cm, len_cm, spf | spr << 16}, {node0, node1, fwd edge, rev edge}
+  // (sp* = mode-capped speed of the directed edge in 0.1 km/h, 0 when the mode cannot use it)
+  uint8_t* cand_n = nullptr; uint4* cand_desc = nullptr; float* cand_sq = nullptr;
+  uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr;
+  uint4* pair_info = nullptr;  // per layer pair slot: {route bound cm, time bound ms, KA | KB << 8 | mode << 16, 0}
   uint32_t* src_cnt = nullptr; uint32_t* src_off = nullptr; uint32_t* src_item = nullptr;
   int8_t* choice = nullptr; uint8_t* chain_start = nullptr; uint8_t* bp = nullptr;
   uint32_t* path_off = nullptr; uint32_t* path_cnt = nullptr; uint32_t* path_pool = nullptr; uint32_t* route_dist = nullptr;

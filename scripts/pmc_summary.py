@@ -39,7 +39,8 @@ def main():
     ap.add_argument("--traces", type=int, default=10000)
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
-    stats = list(csv.DictReader(open(os.path.join(a.src, "prof_kt", "run_kernel_stats.csv"))))
+    ks = os.path.join(a.src, "prof_kt", "run_kernel_stats.csv")
+    stats = list(csv.DictReader(open(ks))) if os.path.exists(ks) else []
     lines = ["| kernel | calls | avg (us) | min (us) | max (us) | % of GPU time |", "|---|---|---|---|---|---|"]
     for r in stats:
         lines.append("| %s | %s | %.1f | %.1f | %.1f | %.2f |" % (short(r["Name"]), r["Calls"], float(r["AverageNs"]) / 1e3,
