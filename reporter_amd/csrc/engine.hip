@@ -42,10 +42,10 @@ constexpr int kSmallH = 256;    // LDS hash slots, fast tier
 constexpr int kBigH = 4096;     // LDS hash slots, retry tier (one source at a time)
 constexpr int kCandH = 256;     // road hash slots in the candidate kernel
 constexpr int kInlinePath = 8;  // path edges stored inline per slot (no allocation)
-#ifndef RM_WAVE_GRID
-#define RM_WAVE_GRID 8192
+#ifndef RM_LDS_GRID
+#define RM_LDS_GRID 2048
 #endif
-constexpr int kWaveGrid = RM_WAVE_GRID;  // blocks of the small wave tiers (grid-stride over their work lists)
+constexpr int kLdsGrid = RM_LDS_GRID;  // blocks of the LDS lane tiers (grid-stride over their work lists)
 constexpr uint32_t kMaxBoundCm = 100000000u;
 constexpr double kQueueSpeedMps = 2.7777777777777777;  // 10 km/h
 
@@ -583,110 +583,143 @@ struct HashLabel {
 };
 
 // ------------------------------------------------------------------------------------------
-// Lane tier: one lane runs one whole bounded Dijkstra with its labels in registers.
-// Most searches settle a handful of nodes, so a wave-wide search would waste 60 lanes
-// and pay LDS init + barriers; kLaneCap register slots hold the common case and anything
-// larger goes to the wave tiers below.  Same exact keys.
+// Lane tiers: one lane runs one whole bounded Dijkstra.  Most searches settle a handful
+// of nodes, so a wave-wide search would waste 60 lanes and pay LDS init + barriers.
+// Edges are read as per-mode relax records {target, len_cm | kNoLen, time_ms, target's
+// CSR range}: a settled node's label already holds its out-edge range, so each settle is
+// ONE dependent round trip (the node's edge records), not two (offsets, then edges).
+// Labels live in registers (kLaneCap slots, the common case) or, for searches that
+// outgrow them, in LDS (kLdsCap slots per lane); keys are exact, so every store agrees.
 #ifndef RM_LANE_CAP
 #define RM_LANE_CAP 8
 #endif
 constexpr int kLaneCap = RM_LANE_CAP;
+constexpr int kLdsCap = 32;
+constexpr uint32_t kNoLen = 0xffffffffu;
 
-struct LaneSearch {
-  uint32_t node[kLaneCap];
+struct RegLabels {
+  uint32_t node[kLaneCap], rng[kLaneCap];
   unsigned long long key[kLaneCap];
   uint32_t n, settled;
   bool ovf;
-};
-
-__device__ __forceinline__ unsigned long long ls_label(const LaneSearch& s, uint32_t v) {
-  unsigned long long k = kKeyInf;
-#pragma unroll
-  for (int x = 0; x < kLaneCap; ++x)
-    if (x < (int)s.n && s.node[x] == v) k = s.key[x];
-  return k;
-}
-
-struct LaneLabel {
-  const LaneSearch& s;
-  __device__ unsigned long long operator()(uint32_t node) const { return ls_label(s, node); }
-};
-
-__device__ __forceinline__ void ls_relax(LaneSearch& s, uint32_t v, unsigned long long k) {
-  bool found = false;
-#pragma unroll
-  for (int x = 0; x < kLaneCap; ++x)
-    if (x < (int)s.n && s.node[x] == v) {
-      found = true;
-      if (k < s.key[x]) s.key[x] = k;
-    }
-  if (found) return;
-  if (s.n >= (uint32_t)kLaneCap) { s.ovf = true; return; }
-#pragma unroll
-  for (int x = 0; x < kLaneCap; ++x)
-    if (x == (int)s.n) { s.node[x] = v; s.key[x] = k; }
-  s.n++;
-}
-
-// bounded Dijkstra from the exits of the candidate described by (a0, a1)
-__device__ void lane_search(LaneSearch& S, const DevGraph& g, int mode, uint32_t acc, uint32_t bound,
-                            const uint4& a0, const uint4& a1, unsigned long long& rk1, unsigned long long& rk0) {
-  S.n = 0; S.settled = 0; S.ovf = false;
-  exit_keys(a0, bound, rk1, rk0);
-  if (rk1 != kKeyInf) ls_relax(S, a1.y, rk1);
-  if (rk0 != kKeyInf) ls_relax(S, a1.x, rk0);
-  for (;;) {
-    int bi = -1;
-    unsigned long long bk = kKeyInf;
-    uint32_t u = 0;
+  __device__ __forceinline__ void init() { n = 0; settled = 0; ovf = false; }
+  __device__ __forceinline__ unsigned long long label(uint32_t v) const {
+    unsigned long long k = kKeyInf;
 #pragma unroll
     for (int x = 0; x < kLaneCap; ++x)
-      if (x < (int)S.n && !((S.settled >> x) & 1u) && S.key[x] < bk) { bk = S.key[x]; bi = x; u = S.node[x]; }
-    if (bi < 0) break;
-    S.settled |= 1u << bi;
-    const uint32_t e0 = g.node_off[u], e1 = g.node_off[u + 1];
-    for (uint32_t e = e0; e < e1; ++e) {
-      const uint4 rec = g.edges[e];
-      if (!edge_ok(rec.z, acc)) continue;
-      const unsigned long long nk = bk + edge_key(rec, mode);
-      if (key_dist(nk) > bound) continue;
-      ls_relax(S, rec.x, nk);
+      if (x < (int)n && node[x] == v) k = key[x];
+    return k;
+  }
+  __device__ __forceinline__ void relax(uint32_t v, unsigned long long k, uint32_t r) {
+    bool found = false;
+#pragma unroll
+    for (int x = 0; x < kLaneCap; ++x)
+      if (x < (int)n && node[x] == v) {
+        found = true;
+        if (k < key[x]) key[x] = k;
+      }
+    if (found) return;
+    if (n >= (uint32_t)kLaneCap) { ovf = true; return; }
+#pragma unroll
+    for (int x = 0; x < kLaneCap; ++x)
+      if (x == (int)n) { node[x] = v; key[x] = k; rng[x] = r; }
+    n++;
+  }
+  // settle the unsettled label with the smallest key; false when none is left
+  __device__ __forceinline__ bool pick(unsigned long long& bk, uint32_t& r) {
+    int bi = -1;
+    bk = kKeyInf;
+#pragma unroll
+    for (int x = 0; x < kLaneCap; ++x)
+      if (x < (int)n && !((settled >> x) & 1u) && key[x] < bk) { bk = key[x]; bi = x; r = rng[x]; }
+    if (bi < 0) return false;
+    settled |= 1u << bi;
+    return true;
+  }
+};
+
+// labels in LDS, lane-minor ([slot][64]) so a wave's accesses to one slot are conflict-free
+struct LdsLabels {
+  uint32_t* node;
+  uint32_t* rng;
+  unsigned long long* key;
+  uint32_t n;
+  unsigned long long settled;
+  bool ovf;
+  __device__ __forceinline__ void init() { n = 0; settled = 0; ovf = false; }
+  __device__ __forceinline__ unsigned long long label(uint32_t v) const {
+    for (uint32_t x = 0; x < n; ++x)
+      if (node[x * kWave] == v) return key[x * kWave];
+    return kKeyInf;
+  }
+  __device__ __forceinline__ void relax(uint32_t v, unsigned long long k, uint32_t r) {
+    for (uint32_t x = 0; x < n; ++x)
+      if (node[x * kWave] == v) {
+        if (k < key[x * kWave]) key[x * kWave] = k;
+        return;
+      }
+    if (n >= (uint32_t)kLdsCap) { ovf = true; return; }
+    node[n * kWave] = v; key[n * kWave] = k; rng[n * kWave] = r;
+    n++;
+  }
+  __device__ __forceinline__ bool pick(unsigned long long& bk, uint32_t& r) {
+    int bi = -1;
+    bk = kKeyInf;
+    for (uint32_t x = 0; x < n; ++x) {
+      const unsigned long long kx = key[x * kWave];
+      if (!((settled >> x) & 1ull) && kx < bk) { bk = kx; bi = (int)x; }
+    }
+    if (bi < 0) return false;
+    settled |= 1ull << bi;
+    r = rng[bi * kWave];
+    return true;
+  }
+};
+
+template <class L>
+struct StoreLabel {
+  const L& s;
+  __device__ unsigned long long operator()(uint32_t node) const { return s.label(node); }
+};
+
+// bounded Dijkstra from the exits of the candidate described by (a0, a1)
+template <class L>
+__device__ __forceinline__ void lane_search(L& S, const DevGraph& g, const uint4* E, uint32_t bound,
+                                            const uint4& a0, const uint4& a1, unsigned long long& rk1,
+                                            unsigned long long& rk0) {
+  S.init();
+  exit_keys(a0, bound, rk1, rk0);
+  const uint32_t r1 = rk1 != kKeyInf ? g.node_rng[a1.y] : 0u;
+  const uint32_t r0 = rk0 != kKeyInf ? g.node_rng[a1.x] : 0u;
+  if (rk1 != kKeyInf) S.relax(a1.y, rk1, r1);
+  if (rk0 != kKeyInf) S.relax(a1.x, rk0, r0);
+  unsigned long long bk;
+  uint32_t r = 0;
+  while (S.pick(bk, r)) {
+    const uint32_t e0 = r >> 5, deg = r & 31u;
+    for (uint32_t q0 = 0; q0 < deg; q0 += 4) {
+      uint4 rec[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rec[x] = E[e0 + min(q0 + x, deg - 1u)];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        if (q0 + x >= deg || rec[x].y == kNoLen) continue;
+        const unsigned long long nk = bk + make_key(rec[x].y, rec[x].z);
+        if (key_dist(nk) <= bound) S.relax(rec[x].x, nk, rec[x].w);
+      }
     }
     if (S.ovf) break;
   }
 }
 
-// K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
-// one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A pair any of
-// whose searches outgrows the registers is queued once (the src_cnt word is consumed as a
-// flag) for the wave tier, which recomputes the whole pair.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_items) return;
-  const uint32_t p = b.src_item[t];
-  const uint4 pi = b.pair_info[p];
-  const uint32_t i = t - b.src_off[p];
-  const uint32_t base = b.trans_off[p];
-  const uint32_t bound = pi.x, tmax = pi.y, KB = (pi.z >> 8) & 0xffu;
-  const int mode = (int)(pi.z >> 16);
-  const uint32_t acc = mode_access(mode);
-  const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
-  const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
-  LaneSearch S;
-  unsigned long long rk1, rk0;
-  lane_search(S, g, mode, acc, bound, a0, a1, rk1, rk0);
-  if (S.ovf) {
-    if (atomicExch(&b.src_cnt[p], 0u) != 0u) {
-      const uint32_t q = atomicAdd(&b.ctl[3], 1u);
-      b.rl_routes_a[q] = p;
-    }
-    return;
-  }
-  // targets four at a time with clamped (branch-free) loads; results go to LDS and are
-  // stored after the last load (a store before a load-use costs a full round trip)
-  __shared__ uint32_t s_res[kMaxCand][256];
-  const uint64_t brow = (uint64_t)p * kMaxCand * 2;
-  const LaneLabel lab{S};
+// routes from source a0 to the KB targets of pair slot p; results staged in LDS
+// (res[j * stride]) and stored after the last load (a store before a load-use costs a
+// full round trip: gfx9 loads and stores share vmcnt)
+template <class Label>
+__device__ __forceinline__ void route_targets(const DevBatch& b, const Label& lab, const uint4& a0, uint64_t p,
+                                              uint32_t KB, uint32_t bound, uint32_t tmax, uint64_t ob, uint32_t* res,
+                                              int stride) {
+  const uint64_t brow = p * kMaxCand * 2;
   for (uint32_t j0 = 0; j0 < KB; j0 += 4) {
     uint4 t0[4], t1[4];
 #pragma unroll
@@ -700,22 +733,73 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       const unsigned long long key = route_key(lab, a0, t0[x], t1[x], nullptr);
       uint32_t r = kRouteInvalid;
       if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
-      s_res[(j0 + x) & (kMaxCand - 1)][threadIdx.x] = r;
+      res[((j0 + x) & (kMaxCand - 1)) * stride] = r;
     }
   }
-  const uint64_t ob = (uint64_t)base + i * KB;
-  for (uint32_t j = 0; j < KB; ++j) b.route[ob + j] = s_res[j][threadIdx.x];
+  for (uint32_t j = 0; j < KB; ++j) b.route[ob + j] = res[j * stride];
 }
 
-// path lane tier: one lane per chosen transition; canonical predecessors in registers.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_paths_lane(DevGraph g, DevBatch b) {
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= b.P) return;
-  const uint32_t k = b.slot_trace[p];
-  const uint32_t o = b.trace_off[k];
-  const uint32_t s = (uint32_t)(p - o);
-  if (s < 1 || s >= b.n_states[k]) return;
-  if (b.chain_start[p] || b.choice[p] < 0) return;
+// K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
+// one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A search
+// that outgrows the registers is queued (as its item) for the LDS lane tier.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_items) return;
+  const uint32_t p = b.src_item[t];
+  const uint4 pi = b.pair_info[p];
+  const uint32_t i = t - b.src_off[p];
+  const uint32_t base = b.trans_off[p];
+  const uint32_t bound = pi.x, tmax = pi.y, KB = (pi.z >> 8) & 0xffu;
+  const int mode = (int)(pi.z >> 16);
+  const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+  const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+  RegLabels S;
+  unsigned long long rk1, rk0;
+  lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
+  if (S.ovf) {
+    const uint32_t q = atomicAdd(&b.ctl[3], 1u);
+    b.rl_routes_a[q] = t;
+    return;
+  }
+  __shared__ uint32_t s_res[kMaxCand][256];
+  route_targets(b, StoreLabel<RegLabels>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256);
+}
+
+// K2 LDS lane tier: the items the register tier queued, kLdsCap labels per lane in LDS.
+// Grid-stride over the device-side list; what still overflows goes to the wave tier.
+__global__ void __launch_bounds__(64) k_routes_lds(DevGraph g, DevBatch b) {
+  __shared__ uint32_t s_node[kLdsCap][kWave], s_rng[kLdsCap][kWave];
+  __shared__ unsigned long long s_key[kLdsCap][kWave];
+  __shared__ uint32_t s_res[kMaxCand][kWave];
+  const int lane = threadIdx.x;
+  const uint32_t n_items = b.ctl[3];
+  for (uint32_t q = blockIdx.x * kWave + lane; q < n_items; q += gridDim.x * kWave) {
+    const uint32_t t = b.rl_routes_a[q];
+    const uint32_t p = b.src_item[t];
+    const uint4 pi = b.pair_info[p];
+    const uint32_t i = t - b.src_off[p];
+    const uint32_t base = b.trans_off[p];
+    const uint32_t bound = pi.x, tmax = pi.y, KB = (pi.z >> 8) & 0xffu;
+    const int mode = (int)(pi.z >> 16);
+    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+    LdsLabels S{&s_node[0][lane], &s_rng[0][lane], &s_key[0][lane], 0, 0, false};
+    unsigned long long rk1, rk0;
+    lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
+    if (S.ovf) {
+      const uint32_t x = atomicAdd(&b.ctl[5], 1u);
+      b.rl_routes_b[x] = t;
+      continue;
+    }
+    route_targets(b, StoreLabel<LdsLabels>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB, &s_res[0][lane], kWave);
+  }
+}
+
+// path of one chosen transition (slot p) with a lane-resident search: canonical
+// predecessors (smallest-id tight in-edge from a labelled node) walked back from the
+// entry node.  Returns false when the search outgrew its label store (caller queues p).
+template <class L>
+__device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, uint64_t p, L& S, int cap) {
   const uint4 pi = b.pair_info[p];
   const int mode = (int)(pi.z >> 16);
   const uint32_t acc = mode_access(mode);
@@ -723,16 +807,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
   const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
   const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-  LaneSearch S;
   unsigned long long rk1, rk0;
-  lane_search(S, g, mode, acc, bound, a0, a1, rk1, rk0);
-  if (S.ovf) {
-    const uint32_t q = atomicAdd(&b.ctl[4], 1u);
-    b.rl_paths_a[q] = (uint32_t)p;
-    return;
-  }
+  lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
+  if (S.ovf) return false;
   int combo = -1;
-  const unsigned long long key = route_key(LaneLabel{S}, a0, b0, b1, &combo);
+  const unsigned long long key = route_key(StoreLabel<L>{S}, a0, b0, b1, &combo);
   const uint32_t n1a = a1.y, n0a = a1.x;
   uint32_t* inl = b.path_inline + p * kInlinePath;
   if (combo <= 1) {
@@ -740,12 +819,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     inl[0] = combo == 0 ? a1.z : a1.w;
     b.path_cnt[p] = 1;
     b.path_off[p] = 0;
-    return;
+    return true;
   }
-  // walk back from the entry node; the canonical predecessor of a non-root node is the
-  // smallest-id tight in-edge from a labelled node (in-edges are sorted by edge id).
-  // Edges are shifted into registers (front = travel order) and stored after the walk:
-  // a store inside the walk would make every following load wait for it (shared vmcnt).
+  // walk back from the entry node.  Edges are shifted into registers (front = travel
+  // order) and stored after the walk: a store inside the walk would make every following
+  // load wait for it (shared vmcnt).
   const uint32_t entry_e = combo == 2 ? b1.z : b1.w;
   const uint32_t v0 = combo == 2 ? b1.x : b1.y;
   uint32_t n = 1, x = v0;
@@ -753,8 +831,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
   for (int q = 0; q < kInlinePath; ++q) pr[q] = entry_e;
   for (int guard = 0;; ++guard) {
-    const unsigned long long lx = ls_label(S, x);
-    if (lx == kKeyInf || guard > kLaneCap) { atomicOr(&b.ctl[2], kErrRounds); return; }
+    const unsigned long long lx = S.label(x);
+    if (lx == kKeyInf || guard > cap) { atomicOr(&b.ctl[2], kErrRounds); return true; }
     if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
     uint32_t pe = kNone, pu = 0;
     for (uint32_t q = g.in_off[x]; q < g.in_off[x + 1]; ++q) {
@@ -762,10 +840,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       const uint4 rec = g.edges[e];
       if (!edge_ok(rec.z, acc)) continue;
       const uint32_t u = g.edge_src[e];
-      const unsigned long long lu = ls_label(S, u);
+      const unsigned long long lu = S.label(u);
       if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { pe = e; pu = u; break; }
     }
-    if (pe == kNone) { atomicOr(&b.ctl[2], kErrRounds); return; }
+    if (pe == kNone) { atomicOr(&b.ctl[2], kErrRounds); return true; }
 #pragma unroll
     for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
     pr[0] = pe;
@@ -784,80 +862,92 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     for (int q = 0; q < kInlinePath; ++q)
       if ((uint32_t)q < n) inl[q] = pr[q];
     b.path_off[p] = 0;
-    return;
+    return true;
   }
   // long path: pool slot, second walk writing in travel order
   const uint32_t at = atomicAdd(&b.ctl[0], n);
-  if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); b.path_off[p] = kNone; return; }
+  if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); b.path_off[p] = kNone; return true; }
   b.path_off[p] = at;
   uint32_t* dst = b.path_pool + at;
   dst[n - 1] = entry_e;
   dst[0] = exit_e;
   x = v0;
   for (uint32_t q = n - 2; q >= 1; --q) {
-    const unsigned long long lx = ls_label(S, x);
+    const unsigned long long lx = S.label(x);
     for (uint32_t r = g.in_off[x]; r < g.in_off[x + 1]; ++r) {
       const uint32_t e = g.in_edge[r];
       const uint4 rec = g.edges[e];
       if (!edge_ok(rec.z, acc)) continue;
       const uint32_t u = g.edge_src[e];
-      const unsigned long long lu = ls_label(S, u);
+      const unsigned long long lu = S.label(u);
       if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { dst[q] = e; x = u; break; }
+    }
+  }
+  return true;
+}
+
+// path lane tier: one lane per chosen transition, labels in registers
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_paths_lane(DevGraph g, DevBatch b) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
+  const uint32_t k = b.slot_trace[p];
+  const uint32_t o = b.trace_off[k];
+  const uint32_t s = (uint32_t)(p - o);
+  if (s < 1 || s >= b.n_states[k]) return;
+  if (b.chain_start[p] || b.choice[p] < 0) return;
+  RegLabels S;
+  if (!lane_path(g, b, p, S, kLaneCap)) {
+    const uint32_t q = atomicAdd(&b.ctl[4], 1u);
+    b.rl_paths_a[q] = (uint32_t)p;
+  }
+}
+
+// path LDS lane tier: the transitions the register tier queued
+__global__ void __launch_bounds__(64) k_paths_lds(DevGraph g, DevBatch b) {
+  __shared__ uint32_t s_node[kLdsCap][kWave], s_rng[kLdsCap][kWave];
+  __shared__ unsigned long long s_key[kLdsCap][kWave];
+  const int lane = threadIdx.x;
+  const uint32_t n_items = b.ctl[4];
+  for (uint32_t q = blockIdx.x * kWave + lane; q < n_items; q += gridDim.x * kWave) {
+    const uint32_t p = b.rl_paths_a[q];
+    LdsLabels S{&s_node[0][lane], &s_rng[0][lane], &s_key[0][lane], 0, 0, false};
+    if (!lane_path(g, b, p, S, kLdsCap)) {
+      const uint32_t x = atomicAdd(&b.ctl[6], 1u);
+      b.rl_paths_b[x] = p;
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// K2 wave tiers: one wave per layer pair (s-1 -> s).  SMALL tier searches all sources at
-// once in a 256-slot hash; a pair that overflows is queued for the BIG tier, which
-// searches one source at a time in a 4096-slot hash.
-template <bool BIG>
+// K2 wave tier: one wave per (pair, source) item that outgrew both lane tiers; the
+// source is searched alone in a 4096-slot LDS hash.
 __global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
-  constexpr int H = BIG ? kBigH : kSmallH;
+  constexpr int H = kBigH;
   __shared__ SearchSmem<H, false> sm;
-  __shared__ uint4 s_src[2 * kMaxCand];
+  __shared__ uint4 s_src[2];
   const int lane = threadIdx.x;
-  const uint32_t n_items = min(b.ctl[BIG ? 5 : 3], (uint32_t)b.P);
-  const uint32_t* list = BIG ? b.rl_routes_b : b.rl_routes_a;
+  const uint32_t n_items = b.ctl[5];
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const uint64_t p = list[item];
+    const uint32_t t = b.rl_routes_b[item];
+    const uint64_t p = b.src_item[t];
     const uint4 pi = b.pair_info[p];
-    const uint32_t KA = pi.z & 0xffu, KB = (pi.z >> 8) & 0xffu;
+    const uint32_t i = t - b.src_off[p];
+    const uint32_t KB = (pi.z >> 8) & 0xffu;
     const int mode = (int)(pi.z >> 16);
     const uint32_t bound = pi.x, tmax = pi.y;
     const uint32_t base = b.trans_off[p];
-    if (lane < (int)(2 * KA)) s_src[lane] = b.cand_desc[(p - 1) * kMaxCand * 2 + lane];
+    if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
     __syncthreads();
-    if (!BIG) {
-      bounded_search<H, false>(sm, g, mode, bound, s_src, KA);
-      if (sm.ovf) {
-        if (lane == 0) {
-          const uint32_t q = atomicAdd(&b.ctl[5], 1u);
-          b.rl_routes_b[q] = (uint32_t)p;
-        }
-        __syncthreads();
-        continue;
-      }
-      for (uint32_t t = lane; t < KA * KB; t += kWave) {
-        const uint32_t i = t / KB, j = t - i * KB;
+    bounded_search<H, false>(sm, g, mode, bound, s_src, 1);
+    if (sm.ovf) {
+      if (lane == 0) atomicOr(&b.ctl[2], kErrSearchOverflow);
+    } else {
+      for (uint32_t j = lane; j < KB; j += kWave) {
         const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-        const unsigned long long key = route_key(HashLabel<H, false>{sm, i << 28}, s_src[2 * i], t0, t1, nullptr);
+        const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, nullptr);
         uint32_t out = kRouteInvalid;
         if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
-        b.route[base + t] = out;
-      }
-    } else {
-      for (uint32_t i = 0; i < KA; ++i) {
-        bounded_search<H, false>(sm, g, mode, bound, s_src + 2 * i, 1);
-        if (sm.ovf) { if (lane == 0) atomicOr(&b.ctl[2], kErrSearchOverflow); break; }
-        for (uint32_t j = lane; j < KB; j += kWave) {
-          const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-          const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[2 * i], t0, t1, nullptr);
-          uint32_t out = kRouteInvalid;
-          if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
-          b.route[base + i * KB + j] = out;
-        }
-        __syncthreads();
+        b.route[base + i * KB + j] = out;
       }
     }
     __syncthreads();
@@ -1114,8 +1204,9 @@ __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
   __shared__ SearchSmem<H, true> sm;
   __shared__ uint4 s_src[2];
   const int lane = threadIdx.x;
-  const uint32_t n_items = min(b.ctl[BIG ? 6 : 4], (uint32_t)b.P);
-  const uint32_t* list = BIG ? b.rl_paths_b : b.rl_paths_a;
+  static_assert(BIG, "the small path wave tier was replaced by the LDS lane tier");
+  const uint32_t n_items = b.ctl[6];
+  const uint32_t* list = b.rl_paths_b;
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const uint64_t p = list[item];
     const uint4 pi = b.pair_info[p];
@@ -1586,6 +1677,30 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
       x[4] = er; x[5] = ef == kNone ? 0u : g.edges[ef].info; x[6] = er == kNone ? 0u : g.edges[er].info; x[7] = 0;
     }
     dg_.road_rec = (const uint4*)upload(allocs_, rr);
+    // per-node CSR ranges and per-mode relax records (K2 / path lane tiers)
+    const uint32_t N = g.num_nodes(), E = g.num_edges();
+    if (E >= (1u << 27)) throw std::runtime_error("graph has too many directed edges for the relax records (limit 2^27)");
+    std::vector<uint32_t> nr(N);
+    for (uint32_t n = 0; n < N; ++n) {
+      const uint32_t deg = g.node_off[n + 1] - g.node_off[n];
+      if (deg > 31) throw std::runtime_error("node out-degree above 31 is not supported by the relax records");
+      nr[n] = (g.node_off[n] << 5) | deg;
+    }
+    dg_.node_rng = upload(allocs_, nr);
+    std::vector<uint32_t> rel(4 * (size_t)E);
+    for (int mode = 0; mode <= kModePedestrian; ++mode) {
+      const uint32_t acc = mode_access(mode);
+      for (uint32_t e = 0; e < E; ++e) {
+        const EdgeRec& er = g.edges[e];
+        const bool ok = (edge_access(er.info) & acc) != 0u;
+        uint32_t* x = rel.data() + 4 * (size_t)e;
+        x[0] = er.target;
+        x[1] = ok ? er.len_cm : 0xffffffffu;
+        x[2] = ok ? time_ms(er.len_cm, mode_speed_dkph(mode, edge_speed_dkph(er.info))) : 0u;
+        x[3] = nr[er.target];
+      }
+      dg_.relax[mode] = (const uint4*)upload(allocs_, rel);
+    }
   }
   dg_.lon0 = g.grid.lon0; dg_.lat0 = g.grid.lat0; dg_.dlon = g.grid.dlon; dg_.dlat = g.grid.dlat;
   dg_.ncx = g.grid.ncx; dg_.ncy = g.grid.ncy;
@@ -1653,7 +1768,6 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.seg_base = dalloc<uint32_t>(L, ct); w.seg_cnt = dalloc<uint32_t>(L, ct);
   w.rep_cnt = dalloc<uint32_t>(L, ct); w.stats = dalloc<ReportStats>(L, ct);
   w.ctl = dalloc<uint32_t>(L, 8);
-  w.rl_routes_a = dalloc<uint32_t>(L, cp); w.rl_routes_b = dalloc<uint32_t>(L, cp);
   w.rl_paths_a = dalloc<uint32_t>(L, cp); w.rl_paths_b = dalloc<uint32_t>(L, cp);
   w.rl_cand = dalloc<uint32_t>(L, cp);
   size_t tmp = 0;
@@ -1661,7 +1775,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.scan_tmp_bytes = tmp;
   w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
-  w.route = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
+  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
   w.run_kind = nullptr; w.run_head = nullptr; w.run_idx = nullptr; w.run_pos = nullptr; w.seg_scan_tmp = nullptr;
   w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
   ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
@@ -1679,8 +1793,12 @@ void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
   }
   if (!(n_src <= w.cap_src && w.src_item)) {
     if (w.src_item) { (void)hipFree(w.src_item); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.src_item)); }
+    if (w.rl_routes_a) { (void)hipFree(w.rl_routes_a); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_a)); }
+    if (w.rl_routes_b) { (void)hipFree(w.rl_routes_b); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_b)); }
     const uint64_t c = n_src + n_src / 4 + 1024;
     w.src_item = dalloc<uint32_t>(w.allocs, c);
+    w.rl_routes_a = dalloc<uint32_t>(w.allocs, c);   // overflow lists hold (pair, source) items
+    w.rl_routes_b = dalloc<uint32_t>(w.allocs, c);
     w.cap_src = c;
   }
 }
@@ -1850,13 +1968,15 @@ void Matcher::run_device(const RunParams& rp) {
   ensure_trans(total, n_src);
   v.route = w.route;
   v.src_item = w.src_item;
+  v.rl_routes_a = w.rl_routes_a;
+  v.rl_routes_b = w.rl_routes_b;
 
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
   if (n_src)
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
-  hipLaunchKernelGGL(k_routes_wave<false>, dim3(kWaveGrid), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave<true>, dim3(1024), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave, dim3(1024), dim3(64), 0, st, g, v);
   toc(kKRoutes);
   tic(kKViterbi);
   hipLaunchKernelGGL(k_viterbi, dim3((T + 3) / 4), dim3(64), 0, st, v);
@@ -1864,7 +1984,7 @@ void Matcher::run_device(const RunParams& rp) {
   for (int attempt = 0;; ++attempt) {
     tic(kKPaths);
     hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_wave<false>, dim3(kWaveGrid), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
     hipLaunchKernelGGL(k_paths_wave<true>, dim3(1024), dim3(64), 0, st, g, v);
     toc(kKPaths);
     // traversal records are laid out by a scan of path_cnt (0 for slots without a chosen transition)

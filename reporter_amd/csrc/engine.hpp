@@ -46,6 +46,9 @@ struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   const uint32_t* cell_item;
   const uint4* cell_rec;         // per cell item, 2 x uint4: {A.lon, A.lat, B.lon, B.lat}, {A.cum, B.cum, road | acc << 29, vertex}
   const uint4* road_rec;         // per road, 2 x uint4: {node0, node1, len_cm, fwd edge}, {rev edge, info fwd, info rev, 0}
+  const uint4* relax[5];         // per travel mode, per directed edge: {target, len_cm | 0xffffffff if the mode
+                                 // cannot use it, time_ms at the mode's speed, CSR range of the target}
+  const uint32_t* node_rng;      // per node: first out-edge << 5 | out-degree
   double lon0, lat0, dlon, dlat;
   uint32_t ncx, ncy, n_nodes, n_edges, n_segments, pad;
 };
