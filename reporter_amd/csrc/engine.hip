@@ -173,10 +173,8 @@ __device__ __forceinline__ void project(float alon, float alat, uint32_t acum, f
 
 // candidate descriptor of (road, s) for a travel mode: everything the route and path
 // kernels need about a candidate in two dwordx4 (no dependent graph loads there)
-__device__ __forceinline__ void make_desc(const DevGraph& g, uint32_t road, uint32_t s, int mode, uint4& d0,
-                                          uint4& d1) {
-  const uint4 a = g.road_rec[2 * (uint64_t)road], c = g.road_rec[2 * (uint64_t)road + 1];
-  const uint32_t acc = mode_access(mode);
+__device__ __forceinline__ void desc_from_rec(const uint4& a, const uint4& c, uint32_t road, uint32_t s, int mode,
+                                              uint32_t acc, uint4& d0, uint4& d1) {
   uint32_t spf = (a.w != kNone && edge_ok(c.y, acc)) ? mode_speed_dkph(mode, c.y & 0xffffu) : 0u;
   uint32_t spr = (c.x != kNone && edge_ok(c.z, acc)) ? mode_speed_dkph(mode, c.z & 0xffffu) : 0u;
   // a usable edge is never speed 0 here; time_ms() treats 0 as 1, so 1 keeps every result
@@ -184,6 +182,12 @@ __device__ __forceinline__ void make_desc(const DevGraph& g, uint32_t road, uint
   if (c.x != kNone && edge_ok(c.z, acc) && spr == 0u) spr = 1u;
   d0 = make_uint4(road, s, a.z, spf | (spr << 16));
   d1 = make_uint4(a.x, a.y, a.w, c.x);
+}
+
+__device__ __forceinline__ void make_desc(const DevGraph& g, uint32_t road, uint32_t s, int mode, uint4& d0,
+                                          uint4& d1) {
+  desc_from_rec(g.road_rec[2 * (uint64_t)road], g.road_rec[2 * (uint64_t)road + 1], road, s, mode, mode_access(mode),
+                d0, d1);
 }
 
 __device__ __forceinline__ void put_cand(const DevGraph& g, const DevBatch& b, uint64_t p, uint32_t rank, uint32_t road,
@@ -229,18 +233,29 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
     const uint32_t x0 = fx0 < 0 ? 0u : (uint32_t)fx0, y0 = fy0 < 0 ? 0u : (uint32_t)fy0;
     const uint32_t x1 = fx1 > (double)(g.ncx - 1) ? g.ncx - 1 : (uint32_t)fx1;
     const uint32_t y1 = fy1 > (double)(g.ncy - 1) ? g.ncy - 1 : (uint32_t)fy1;
-    for (uint32_t cy = y0; cy <= y1 && !ovf; ++cy)
-      for (uint32_t cx = x0; cx <= x1 && !ovf; ++cx) {
-        const uint32_t c = cy * g.ncx + cx;
-        const uint32_t it0 = g.cell_off[c], it1 = g.cell_off[c + 1];
-        for (uint32_t it = it0; it < it1; ++it) {
-          const uint4 r0 = g.cell_rec[2 * (uint64_t)it], r1 = g.cell_rec[2 * (uint64_t)it + 1];
-          if (!((r1.z >> 29) & acc)) continue;
+    // the items of cells x0..x1 of one grid row are one contiguous range (cell-major CSR);
+    // they are read four records at a time with clamped, branch-free loads so the loads
+    // of a batch overlap instead of paying one round trip per item
+    for (uint32_t cy = y0; cy <= y1 && !ovf; ++cy) {
+      const uint32_t lo = g.cell_off[cy * g.ncx + x0], hi = g.cell_off[cy * g.ncx + x1 + 1];
+      for (uint32_t it0 = lo; it0 < hi && !ovf; it0 += 4) {
+        uint4 r0[4], r1[4];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const uint64_t it = min(it0 + y, hi - 1u);
+          r0[y] = g.cell_rec[2 * it];
+          r1[y] = g.cell_rec[2 * it + 1];
+        }
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          if (it0 + y >= hi || ovf) break;
+          if (!((r1[y].z >> 29) & acc)) continue;
           float sq; uint32_t sc;
-          project(as_f(r0.x), as_f(r0.y), r1.x, as_f(r0.z), as_f(r0.w), r1.y, lon, lat, mlon, mlat, sq, sc);
+          project(as_f(r0[y].x), as_f(r0[y].y), r1[y].x, as_f(r0[y].z), as_f(r0[y].w), r1[y].y, lon, lat, mlon, mlat,
+                  sq, sc);
           if (!(sq <= r2)) continue;
-          const uint32_t road = r1.z & 0x1fffffffu;
-          const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | r1.w;
+          const uint32_t road = r1[y].z & 0x1fffffffu;
+          const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | r1[y].w;
           bool found = false;
 #pragma unroll
           for (int x = 0; x < kMaxCand; ++x)
@@ -256,24 +271,45 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
           ++n;
         }
       }
+    }
   }
   if (ovf) {
     const uint32_t q = atomicAdd(&b.ctl[7], 1u);
     b.rl_cand[q] = (uint32_t)p;
     return;
   }
+  // rank by (sq, road); descriptors are written four at a time after their road records
+  // have all arrived (a store between two loads would serialise them: shared vmcnt)
+  const uint32_t cacc = mode_access(op.mode);
 #pragma unroll
-  for (int x = 0; x < kMaxCand; ++x) {
-    if (x >= (int)n) continue;
-    const uint32_t sqb = (uint32_t)(rbest[x] >> 32);
-    uint32_t rank = 0;
+  for (int x0 = 0; x0 < kMaxCand; x0 += 4) {
+    if (x0 >= (int)n) break;
+    uint4 ra[4], rc[4];
 #pragma unroll
-    for (int y = 0; y < kMaxCand; ++y) {
-      if (y >= (int)n) continue;
-      const uint32_t sqb2 = (uint32_t)(rbest[y] >> 32);
-      rank += (sqb2 < sqb || (sqb2 == sqb && rroad[y] < rroad[x])) ? 1u : 0u;
+    for (int y = 0; y < 4; ++y) {
+      const uint64_t road = rroad[min(x0 + y, (int)n - 1)];
+      ra[y] = g.road_rec[2 * road];
+      rc[y] = g.road_rec[2 * road + 1];
     }
-    put_cand(g, b, p, rank, rroad[x], rs[x], __uint_as_float(sqb), op.mode);
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int x = x0 + y;
+      if (x >= (int)n) break;
+      const uint32_t sqb = (uint32_t)(rbest[x] >> 32);
+      uint32_t rank = 0;
+#pragma unroll
+      for (int z = 0; z < kMaxCand; ++z) {
+        if (z >= (int)n) continue;
+        const uint32_t sqb2 = (uint32_t)(rbest[z] >> 32);
+        rank += (sqb2 < sqb || (sqb2 == sqb && rroad[z] < rroad[x])) ? 1u : 0u;
+      }
+      uint4 d0, d1;
+      desc_from_rec(ra[y], rc[y], rroad[x], rs[x], op.mode, cacc, d0, d1);
+      const uint64_t at = p * kMaxCand + rank;
+      b.cand_desc[2 * at] = d0;
+      b.cand_desc[2 * at + 1] = d1;
+      b.cand_sq[at] = __uint_as_float(sqb);
+    }
   }
   b.cand_n[p] = (uint8_t)n;
 }
@@ -594,7 +630,10 @@ struct HashLabel {
 #define RM_LANE_CAP 8
 #endif
 constexpr int kLaneCap = RM_LANE_CAP;
-constexpr int kLdsCap = 32;
+#ifndef RM_LDS_CAP
+#define RM_LDS_CAP 16
+#endif
+constexpr int kLdsCap = RM_LDS_CAP;
 constexpr uint32_t kNoLen = 0xffffffffu;
 
 struct RegLabels {
@@ -764,6 +803,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   __shared__ uint32_t s_res[kMaxCand][256];
   route_targets(b, StoreLabel<RegLabels>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256);
 }
+
+#ifdef RM_ALL_LDS
+__global__ void k_all_items(DevBatch b, uint32_t n) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) b.rl_routes_a[t] = t;
+  if (t == 0) b.ctl[3] = n;
+}
+#endif
 
 // K2 LDS lane tier: the items the register tier queued, kLdsCap labels per lane in LDS.
 // Grid-stride over the device-side list; what still overflows goes to the wave tier.
@@ -1052,6 +1099,27 @@ __device__ void backtrace_chain(const DevBatch& b, VitGroup& gs, uint32_t o, uin
   }
 }
 
+struct VitLayerDesc {
+  uint32_t kb, cnt, off;
+  double gc;
+};
+
+// layer s0 + j of a trace: candidate count, route count, route offset, gc
+__device__ __forceinline__ VitLayerDesc vit_describe(const DevBatch& b, uint32_t o, uint32_t S, uint32_t s0, int j) {
+  const uint32_t sl = s0 + j;
+  const bool vq = sl < S;
+  const uint64_t lq = o + min(sl, S - 1);
+  const uint64_t lp = lq == o ? o : lq - 1;
+  const uint32_t kb_raw = b.cand_n[lq], ka_raw = b.cand_n[lp];
+  const double g_raw = b.gc[lq];
+  VitLayerDesc d;
+  d.off = b.trans_off[lq];
+  d.kb = vq ? kb_raw : 0u;
+  d.cnt = (vq && sl >= 1) ? ka_raw * d.kb : 0u;
+  d.gc = (vq && sl >= 1) ? g_raw : 0.0;
+  return d;
+}
+
 __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
   __shared__ VitGroup smem[4];
   const int lane = threadIdx.x;
@@ -1068,62 +1136,51 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
   bool prev_ok = false;
   uint32_t prevK = 0;
   // chunk descriptor: lane j describes layer s0 + j (clamped, branch-free loads)
-  uint32_t kbq = 0, cntq = 0, offq = 0;
-  double gcq = 0.0;
-  auto describe = [&](uint32_t s0) {
-    const uint32_t sl = s0 + j;
-    const bool vq = sl < S;
-    const uint64_t lq = o + min(sl, S - 1);
-    const uint64_t lp = lq == o ? o : lq - 1;
-    const uint32_t kb_raw = b.cand_n[lq], ka_raw = b.cand_n[lp];
-    const double g_raw = b.gc[lq];
-    offq = b.trans_off[lq];
-    kbq = vq ? kb_raw : 0u;
-    cntq = (vq && sl >= 1) ? ka_raw * kbq : 0u;
-    gcq = (vq && sl >= 1) ? g_raw : 0.0;
-  };
-  if (S) describe(0);
+  VitLayerDesc dq{0u, 0u, 0u, 0.0};
+  if (S) dq = vit_describe(b, o, S, 0, j);
   uint32_t s0 = 0;
   for (;;) {
     const bool live = s0 < S;
     if (__ballot(live) == 0ull) break;
     // ---- lay the chunk out: inclusive scan of route counts over the group's 16 layers
-    uint32_t incl = cntq;
+    uint32_t incl = dq.cnt;
 #pragma unroll
     for (int d = 1; d < 16; d <<= 1) {
       const uint32_t u = __shfl_up(incl, d, 16);
       if (j >= d) incl += u;
     }
-    const uint32_t excl = incl - cntq;
+    const uint32_t excl = incl - dq.cnt;
     const uint32_t fit = (uint32_t)((__ballot(live && s0 + j < S && incl <= (uint32_t)kVitRoutes) >> gb) & 0xffffull);
     const uint32_t C = live ? (uint32_t)__builtin_ctz(~fit | 0x10000u) : 0u;   // leading layers that fit
     const uint32_t nroutes = C ? (uint32_t)__shfl(incl, (int)C - 1, 16) : 0u;
-    const uint32_t rbase = (uint32_t)__shfl(offq, 0, 16);                     // routes of layer s0 start here
+    const uint32_t rbase = (uint32_t)__shfl(dq.off, 0, 16);                   // routes of layer s0 start here
     // ---- coalesced loads of the chunk's routes and emission rows
     uint32_t rv[kVitRoutes / 16];
     const uint32_t rlast = nroutes ? nroutes - 1u : 0u;
 #pragma unroll
     for (int x = 0; x < kVitRoutes / 16; ++x)
       if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
-    float4 sv[4];
-    if (C) {
-      const uint64_t f0 = (uint64_t)(o + s0) * (kMaxCand / 4), flast = f0 + (uint64_t)C * (kMaxCand / 4) - 1;
-      const float4* src = reinterpret_cast<const float4*>(b.cand_sq);
-#pragma unroll
-      for (int x = 0; x < 4; ++x) sv[x] = src[min(f0 + j + 16u * x, flast)];
-    }
-    const uint32_t kb_here = kbq, rel_here = excl;
-    const double gc_here = gcq;
+    // emission rows (16 floats per layer), four float4 per lane, clamped to the chunk
+    const uint64_t f0 = C ? (uint64_t)(o + s0) * (kMaxCand / 4) : 0u;
+    const uint64_t flast = f0 + (C ? (uint64_t)C * (kMaxCand / 4) - 1 : 0u);
+    const float4* sqsrc = reinterpret_cast<const float4*>(b.cand_sq);
+    const float4 sv0 = sqsrc[min(f0 + j, flast)], sv1 = sqsrc[min(f0 + j + 16u, flast)];
+    const float4 sv2 = sqsrc[min(f0 + j + 32u, flast)], sv3 = sqsrc[min(f0 + j + 48u, flast)];
+    const uint32_t kb_here = dq.kb, rel_here = excl;
+    const double gc_here = dq.gc;
     // ---- descriptor of the next chunk (its loads overlap this chunk's work)
-    if (live && s0 + C < S) describe(s0 + C);
+    if (live && s0 + C < S) dq = vit_describe(b, o, S, s0 + C, j);
     // ---- chunk -> LDS
 #pragma unroll
     for (int x = 0; x < kVitRoutes / 16; ++x)
       if ((uint32_t)j + 16u * x < nroutes) gs.route[j + 16 * x] = rv[x];
-    if (C) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-        if ((uint32_t)(j + 16 * x) < C * (kMaxCand / 4)) reinterpret_cast<float4*>(&gs.sq[0][0])[j + 16 * x] = sv[x];
+    {
+      float4* sqdst = reinterpret_cast<float4*>(&gs.sq[0][0]);
+      const uint32_t nf = C * (kMaxCand / 4);
+      if ((uint32_t)j < nf) sqdst[j] = sv0;
+      if ((uint32_t)j + 16u < nf) sqdst[j + 16] = sv1;
+      if ((uint32_t)j + 32u < nf) sqdst[j + 32] = sv2;
+      if ((uint32_t)j + 48u < nf) sqdst[j + 48] = sv3;
     }
     if ((uint32_t)j < C) { gs.kb[j] = kb_here; gs.rel[j] = rel_here; gs.gc[j] = gc_here; }
     wave_sync();
@@ -1973,8 +2030,13 @@ void Matcher::run_device(const RunParams& rp) {
 
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
+#ifdef RM_ALL_LDS
+  if (n_src)
+    hipLaunchKernelGGL(k_all_items, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, v, (uint32_t)n_src);
+#else
   if (n_src)
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
+#endif
   hipLaunchKernelGGL(k_routes_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
   hipLaunchKernelGGL(k_routes_wave, dim3(1024), dim3(64), 0, st, g, v);
   toc(kKRoutes);
