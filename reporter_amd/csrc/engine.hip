@@ -181,7 +181,8 @@ __device__ __forceinline__ void desc_from_rec(const uint4& a, const uint4& c, ui
   if (a.w != kNone && edge_ok(c.y, acc) && spf == 0u) spf = 1u;
   if (c.x != kNone && edge_ok(c.z, acc) && spr == 0u) spr = 1u;
   d0 = make_uint4(road, s, a.z, spf | (spr << 16));
-  d1 = make_uint4(a.x, a.y, a.w, c.x);
+  // d1 = {node0, node1, time_ms(s) entering forward from node0, time_ms(L - s) entering reverse from node1}
+  d1 = make_uint4(a.x, a.y, spf ? time_ms(s, spf) : 0xffffffffu, spr ? time_ms(a.z - s, spr) : 0xffffffffu);
 }
 
 __device__ __forceinline__ void make_desc(const DevGraph& g, uint32_t road, uint32_t s, int mode, uint4& d0,
@@ -481,11 +482,11 @@ __device__ __forceinline__ unsigned long long route_key(const Label& label, cons
   }
   if (spf) {
     const unsigned long long lab = label(b1.x);
-    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(sb, time_ms(sb, spf)); if (k < best) { best = k; bc = 2; } }
+    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(sb, b1.z); if (k < best) { best = k; bc = 2; } }
   }
   if (spr) {
     const unsigned long long lab = label(b1.y);
-    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(L - sb, time_ms(L - sb, spr)); if (k < best) { best = k; bc = 3; } }
+    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(L - sb, b1.w); if (k < best) { best = k; bc = 3; } }
   }
   if (combo) *combo = bc;
   return best;
@@ -627,9 +628,12 @@ struct HashLabel {
 // Labels live in registers (kLaneCap slots, the common case) or, for searches that
 // outgrow them, in LDS (kLdsCap slots per lane); keys are exact, so every store agrees.
 #ifndef RM_LANE_CAP
-#define RM_LANE_CAP 8
+#define RM_LANE_CAP 7
 #endif
 constexpr int kLaneCap = RM_LANE_CAP;
+#ifndef RM_LANE_WPE
+#define RM_LANE_WPE 4   // waves per SIMD the register lane tiers are compiled for
+#endif
 #ifndef RM_LDS_CAP
 #define RM_LDS_CAP 16
 #endif
@@ -637,7 +641,7 @@ constexpr int kLdsCap = RM_LDS_CAP;
 constexpr uint32_t kNoLen = 0xffffffffu;
 
 struct RegLabels {
-  uint32_t node[kLaneCap], rng[kLaneCap];
+  uint32_t node[kLaneCap], rng[kLaneCap], par[kLaneCap];
   unsigned long long key[kLaneCap];
   uint32_t n, settled;
   bool ovf;
@@ -649,28 +653,29 @@ struct RegLabels {
       if (x < (int)n && node[x] == v) k = key[x];
     return k;
   }
-  __device__ __forceinline__ void relax(uint32_t v, unsigned long long k, uint32_t r) {
+  __device__ __forceinline__ void relax(uint32_t v, unsigned long long k, uint32_t r, uint32_t from) {
     bool found = false;
 #pragma unroll
     for (int x = 0; x < kLaneCap; ++x)
       if (x < (int)n && node[x] == v) {
         found = true;
-        if (k < key[x]) key[x] = k;
+        if (k < key[x]) { key[x] = k; par[x] = from; }
       }
     if (found) return;
     if (n >= (uint32_t)kLaneCap) { ovf = true; return; }
 #pragma unroll
     for (int x = 0; x < kLaneCap; ++x)
-      if (x == (int)n) { node[x] = v; key[x] = k; rng[x] = r; }
+      if (x == (int)n) { node[x] = v; key[x] = k; rng[x] = r; par[x] = from; }
     n++;
   }
-  // settle the unsettled label with the smallest key; false when none is left
-  __device__ __forceinline__ bool pick(unsigned long long& bk, uint32_t& r) {
+  // settle the unsettled label with the smallest key; false when none is left.  `from`
+  // is the settled node that gave it its final key (kNone for a root).
+  __device__ __forceinline__ bool pick(unsigned long long& bk, uint32_t& r, uint32_t& u, uint32_t& from) {
     int bi = -1;
     bk = kKeyInf;
 #pragma unroll
     for (int x = 0; x < kLaneCap; ++x)
-      if (x < (int)n && !((settled >> x) & 1u) && key[x] < bk) { bk = key[x]; bi = x; r = rng[x]; }
+      if (x < (int)n && !((settled >> x) & 1u) && key[x] < bk) { bk = key[x]; bi = x; r = rng[x]; u = node[x]; from = par[x]; }
     if (bi < 0) return false;
     settled |= 1u << bi;
     return true;
@@ -691,7 +696,7 @@ struct LdsLabels {
       if (node[x * kWave] == v) return key[x * kWave];
     return kKeyInf;
   }
-  __device__ __forceinline__ void relax(uint32_t v, unsigned long long k, uint32_t r) {
+  __device__ __forceinline__ void relax(uint32_t v, unsigned long long k, uint32_t r, uint32_t) {
     for (uint32_t x = 0; x < n; ++x)
       if (node[x * kWave] == v) {
         if (k < key[x * kWave]) key[x * kWave] = k;
@@ -701,7 +706,7 @@ struct LdsLabels {
     node[n * kWave] = v; key[n * kWave] = k; rng[n * kWave] = r;
     n++;
   }
-  __device__ __forceinline__ bool pick(unsigned long long& bk, uint32_t& r) {
+  __device__ __forceinline__ bool pick(unsigned long long& bk, uint32_t& r, uint32_t& u, uint32_t& from) {
     int bi = -1;
     bk = kKeyInf;
     for (uint32_t x = 0; x < n; ++x) {
@@ -711,6 +716,8 @@ struct LdsLabels {
     if (bi < 0) return false;
     settled |= 1ull << bi;
     r = rng[bi * kWave];
+    u = node[bi * kWave];
+    from = kNone;   // no parent kept here: every out-edge is relaxed
     return true;
   }
 };
@@ -730,11 +737,11 @@ __device__ __forceinline__ void lane_search(L& S, const DevGraph& g, const uint4
   exit_keys(a0, bound, rk1, rk0);
   const uint32_t r1 = rk1 != kKeyInf ? g.node_rng[a1.y] : 0u;
   const uint32_t r0 = rk0 != kKeyInf ? g.node_rng[a1.x] : 0u;
-  if (rk1 != kKeyInf) S.relax(a1.y, rk1, r1);
-  if (rk0 != kKeyInf) S.relax(a1.x, rk0, r0);
+  if (rk1 != kKeyInf) S.relax(a1.y, rk1, r1, kNone);
+  if (rk0 != kKeyInf) S.relax(a1.x, rk0, r0, kNone);
   unsigned long long bk;
-  uint32_t r = 0;
-  while (S.pick(bk, r)) {
+  uint32_t r = 0, u = 0, from = kNone;
+  while (S.pick(bk, r, u, from)) {
     const uint32_t e0 = r >> 5, deg = r & 31u;
     for (uint32_t q0 = 0; q0 < deg; q0 += 4) {
       uint4 rec[4];
@@ -742,9 +749,10 @@ __device__ __forceinline__ void lane_search(L& S, const DevGraph& g, const uint4
       for (int x = 0; x < 4; ++x) rec[x] = E[e0 + min(q0 + x, deg - 1u)];
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
-        if (q0 + x >= deg || rec[x].y == kNoLen) continue;
+        // an edge back to the settled node that gave u its key can never improve it
+        if (q0 + x >= deg || rec[x].y == kNoLen || rec[x].x == from) continue;
         const unsigned long long nk = bk + make_key(rec[x].y, rec[x].z);
-        if (key_dist(nk) <= bound) S.relax(rec[x].x, nk, rec[x].w);
+        if (key_dist(nk) <= bound) S.relax(rec[x].x, nk, rec[x].w, u);
       }
     }
     if (S.ovf) break;
@@ -781,7 +789,7 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
 // K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
 // one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A search
 // that outgrows the registers is queued (as its item) for the LDS lane tier.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_items) return;
   const uint32_t p = b.src_item[t];
@@ -863,7 +871,7 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
   uint32_t* inl = b.path_inline + p * kInlinePath;
   if (combo <= 1) {
     b.route_dist[p] = key_dist(key);
-    inl[0] = combo == 0 ? a1.z : a1.w;
+    inl[0] = combo == 0 ? g.road_fwd[a0.x] : g.road_rev[a0.x];
     b.path_cnt[p] = 1;
     b.path_off[p] = 0;
     return true;
@@ -871,7 +879,7 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
   // walk back from the entry node.  Edges are shifted into registers (front = travel
   // order) and stored after the walk: a store inside the walk would make every following
   // load wait for it (shared vmcnt).
-  const uint32_t entry_e = combo == 2 ? b1.z : b1.w;
+  const uint32_t entry_e = combo == 2 ? g.road_fwd[b0.x] : g.road_rev[b0.x];
   const uint32_t v0 = combo == 2 ? b1.x : b1.y;
   uint32_t n = 1, x = v0;
   uint32_t pr[kInlinePath];
@@ -897,7 +905,7 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
     ++n;
     x = pu;
   }
-  const uint32_t exit_e = (x == n1a) ? a1.z : a1.w;
+  const uint32_t exit_e = (x == n1a) ? g.road_fwd[a0.x] : g.road_rev[a0.x];
 #pragma unroll
   for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
   pr[0] = exit_e;
@@ -934,7 +942,7 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
 }
 
 // path lane tier: one lane per chosen transition, labels in registers
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_paths_lane(DevGraph g, DevBatch b) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_paths_lane(DevGraph g, DevBatch b) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
   const uint32_t k = b.slot_trace[p];
@@ -1317,9 +1325,9 @@ __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
     if (lane == 0) {
       uint32_t n = 0;
       if (combo <= 1) {
-        pbuf[n++] = combo == 0 ? a1.z : a1.w;
+        pbuf[n++] = combo == 0 ? g.road_fwd[a0.x] : g.road_rev[a0.x];
       } else {
-        pbuf[n++] = combo == 2 ? b1.z : b1.w;   // entry edge (reversed order)
+        pbuf[n++] = combo == 2 ? g.road_fwd[b0.x] : g.road_rev[b0.x];   // entry edge (reversed order)
         uint32_t x = combo == 2 ? b1.x : b1.y;
         for (;;) {
           const int hx = h_find(sm, x);
@@ -1331,7 +1339,7 @@ __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
           pbuf[n++] = e;
           x = g.edge_src[e];
         }
-        if (n) pbuf[n++] = (x == n1a) ? a1.z : a1.w;  // exit edge
+        if (n) pbuf[n++] = (x == n1a) ? g.road_fwd[a0.x] : g.road_rev[a0.x];  // exit edge
       }
       uint32_t at = 0;
       if (n > (uint32_t)kInlinePath) {
