@@ -142,11 +142,48 @@ int rm_runner_reset_times(rm_runner* r);
 const char* rm_kernel_name(int k);
 int rm_num_kernels(void);
 
+/* ---------------- batch-pipeline stages around the matcher (reference py/simple_reporter.py) ----------------
+ * rm_runner_run_points replaces the per-vehicle grouping, time sort and inactivity
+ * windowing of simple_reporter.match (py/simple_reporter.py:137-164) with a device sort,
+ * then matches every window of >= 2 points (as rm_runner_run).
+ * rm_runner_tiles replaces the hour bucketing of the valid reports (:176-196) and the
+ * report phase's sort, privacy cull and CSV (:211-254): it returns, per tile file,
+ * "name\0body\0" where name is "<start>_<end>/<level>/<tile index>" and body the text
+ * the reference uploads.  With a communicator the rows of every rank are all-gathered
+ * and each rank returns the files it owns (file key hashed over ranks). */
+typedef struct rm_comm rm_comm;
+typedef struct {
+  uint64_t n_points;
+  const uint32_t* uuid;       /* dense vehicle index per point (< n_uuids) */
+  const double* time;         /* epoch seconds (integers in the reference, :140) */
+  const float* lon;
+  const float* lat;
+  const float* accuracy;      /* may be NULL */
+  double inactivity_sec;      /* --inactivity, default 120 (:344) */
+  uint32_t n_uuids;
+  uint32_t n_opts;
+  const rm_options* opts;
+  const uint32_t* uuid_opt;   /* per vehicle index into opts; NULL = opts[0] for all */
+} rm_points_desc;
+int rm_runner_run_points(rm_runner* r, const rm_points_desc* d, const rm_run_params* p);
+/* vehicle index of each matched window of the last rm_runner_run_points (n_traces entries) */
+int rm_runner_get_trace_uuid(rm_runner* r, uint32_t* uuid);
+/* the batch the last run matched: trace_off (n_traces+1), lon, lat, time, accuracy (n_points) */
+int rm_runner_get_batch(rm_runner* r, uint32_t* trace_off, float* lon, float* lat, double* time, float* accuracy);
+typedef struct {
+  uint32_t quantisation;      /* --quantisation, default 3600 (:343) */
+  uint32_t privacy;           /* --privacy, default 2 (:345) */
+  const char* source;         /* --source-id, default "smpl_rprt" (:346) */
+  const char* mode;           /* vehicle type column, upper-cased (:194) */
+} rm_tile_params;
+void rm_default_tile_params(rm_tile_params* p);
+/* blob is library-allocated (free with rm_free); comm may be NULL */
+int rm_runner_tiles(rm_runner* r, const rm_tile_params* p, rm_comm* comm, char** blob, size_t* len);
+
 /* ---------------- RCCL over xGMI (multi-GPU histogram exchange) ----------------
  * One process per GPU.  Replaces the reference's keyed Kafka repartition of
  * "id next_id" reports (BatchingProcessor.java:126) with one all-reduce of the
  * per-OSMLR-segment speed histogram.  Rank 0 creates the id, every rank inits. */
-typedef struct rm_comm rm_comm;
 int rm_comm_unique_id(uint8_t id_out[128]);
 rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device);
 void rm_comm_destroy(rm_comm* c);

@@ -47,6 +47,16 @@ class RmRunParams(C.Structure):
                 ("hist_dev", C.c_void_p), ("do_report", C.c_int32), ("zero_hist", C.c_int32)]
 
 
+class RmPointsDesc(C.Structure):
+    _fields_ = [("n_points", C.c_uint64), ("uuid", C.c_void_p), ("time", C.c_void_p), ("lon", C.c_void_p),
+                ("lat", C.c_void_p), ("accuracy", C.c_void_p), ("inactivity_sec", C.c_double),
+                ("n_uuids", C.c_uint32), ("n_opts", C.c_uint32), ("opts", C.c_void_p), ("uuid_opt", C.c_void_p)]
+
+
+class RmTileParams(C.Structure):
+    _fields_ = [("quantisation", C.c_uint32), ("privacy", C.c_uint32), ("source", C.c_char_p), ("mode", C.c_char_p)]
+
+
 P = C.c_void_p
 U32P = C.POINTER(C.c_uint32)
 
@@ -90,6 +100,11 @@ PROTOTYPES = [
     ("rm_runner_reset_times", C.c_int, [P]),
     ("rm_kernel_name", C.c_char_p, [C.c_int]),
     ("rm_num_kernels", C.c_int, []),
+    ("rm_runner_run_points", C.c_int, [P, C.POINTER(RmPointsDesc), C.POINTER(RmRunParams)]),
+    ("rm_runner_get_trace_uuid", C.c_int, [P, P]),
+    ("rm_runner_get_batch", C.c_int, [P, P, P, P, P, P]),
+    ("rm_default_tile_params", None, [C.POINTER(RmTileParams)]),
+    ("rm_runner_tiles", C.c_int, [P, C.POINTER(RmTileParams), P, C.POINTER(P), C.POINTER(C.c_size_t)]),
     ("rm_comm_unique_id", C.c_int, [P]),
     ("rm_comm_init", P, [C.c_int, C.c_int, P, C.c_int]),
     ("rm_comm_destroy", None, [P]),

@@ -19,7 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libreporter_match.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-SOURCES = ["engine.hip", "capi.cpp", "graph.cpp", "world.cpp"]
+SOURCES = ["engine.hip", "stages.hip", "capi.cpp", "graph.cpp", "world.cpp"]
 HEADERS = ["engine.hpp", "graph.hpp", "json.hpp", "rm_common.hpp"]
 
 

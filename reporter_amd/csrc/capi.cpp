@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -467,7 +468,6 @@ int rm_runner_reset_times(rm_runner* r) { return guarded([&] { r->m->reset_kerne
 const char* rm_kernel_name(int k) { return (k >= 0 && k < kNumKernels) ? kKernelNames[k] : ""; }
 int rm_num_kernels(void) { return kNumKernels; }
 
-// ---------------- RCCL ----------------
 }  // extern "C"
 
 struct rm_comm {
@@ -475,7 +475,58 @@ struct rm_comm {
   hipStream_t stream = nullptr;
   void* scratch = nullptr;  // 8 bytes for host-value reductions and barriers
   int device = 0;
+  int rank = 0, nranks = 1;
 };
+
+extern "C" {
+
+// ---------------- batch-pipeline stages ----------------
+int rm_runner_run_points(rm_runner* r, const rm_points_desc* d, const rm_run_params* p) {
+  return guarded([&] {
+    if (!r || !d) throw std::runtime_error("runner or points descriptor is NULL");
+    PointsDesc pd;
+    pd.n_points = d->n_points; pd.uuid = d->uuid; pd.time = d->time; pd.lon = d->lon; pd.lat = d->lat;
+    pd.accuracy = d->accuracy; pd.inactivity = d->inactivity_sec; pd.n_uuids = d->n_uuids; pd.n_opts = d->n_opts;
+    pd.opts = (const MatchOptions*)d->opts; pd.uuid_opt = d->uuid_opt;
+    if (pd.n_points && (!pd.uuid || !pd.time || !pd.lon || !pd.lat)) throw std::runtime_error("point arrays are NULL");
+    r->m->run_points(pd, to_rp(p));
+  });
+}
+int rm_runner_get_trace_uuid(rm_runner* r, uint32_t* uuid) { return guarded([&] { r->m->get_trace_uuid(uuid); }); }
+int rm_runner_get_batch(rm_runner* r, uint32_t* off, float* lon, float* lat, double* time, float* acc) {
+  return guarded([&] { r->m->get_batch(off, lon, lat, time, acc); });
+}
+
+void rm_default_tile_params(rm_tile_params* p) {
+  p->quantisation = 3600; p->privacy = 2; p->source = "smpl_rprt"; p->mode = "auto";
+}
+
+int rm_runner_tiles(rm_runner* r, const rm_tile_params* p, rm_comm* comm, char** blob, size_t* len) {
+  if (!blob || !len) return fail("blob/len is NULL");
+  *blob = nullptr;
+  *len = 0;
+  return guarded([&] {
+    if (!r || !p) throw std::runtime_error("runner or tile params is NULL");
+    TileParams tp;
+    tp.quantisation = p->quantisation;
+    tp.privacy = p->privacy;
+    tp.source = p->source ? p->source : "";
+    std::string mode = p->mode ? p->mode : "auto";
+    for (char& ch : mode) ch = (char)std::toupper((unsigned char)ch);   // mode.upper() (:194)
+    tp.mode = mode;
+    TileComm tc;
+    if (comm) { tc.nccl = comm->comm; tc.rank = comm->rank; tc.nranks = comm->nranks; }
+    const std::string out = r->m->tiles(tp, comm ? &tc : nullptr);
+    char* b = (char*)std::malloc(out.size() + 1);
+    if (!b) throw std::bad_alloc();
+    std::memcpy(b, out.data(), out.size());
+    b[out.size()] = 0;
+    *blob = b;
+    *len = out.size();
+  });
+}
+
+}  // extern "C"
 
 namespace {
 void nccl_check(ncclResult_t r, const char* what) {
@@ -498,6 +549,8 @@ rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device) {
   guarded([&] {
     auto c = std::make_unique<rm_comm>();
     c->device = device;
+    c->rank = rank;
+    c->nranks = nranks;
     RM_HIP(hipSetDevice(device));
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);

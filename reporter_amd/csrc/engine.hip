@@ -2181,8 +2181,8 @@ void Matcher::get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, 
 
 void Matcher::tier_counts(uint32_t* out4) {
   sync();
-  uint32_t c[8];
-  RM_HIP(hipMemcpy(c, ws_.ctl, sizeof c, hipMemcpyDeviceToHost));
+  uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (ws_.ctl && n_traces_) RM_HIP(hipMemcpy(c, ws_.ctl, sizeof c, hipMemcpyDeviceToHost));
   out4[0] = c[3]; out4[1] = c[5]; out4[2] = c[4]; out4[3] = c[7];
 }
 

@@ -115,10 +115,72 @@ struct Workspace {
   void release();
 };
 
+// Raw per-vehicle point stream (the trace files simple_reporter's download phase writes:
+// uuid, time, lat, lon, accuracy per line, reference py/simple_reporter.py:113,139-140).
+struct PointsDesc {
+  uint64_t n_points = 0;
+  const uint32_t* uuid = nullptr;      // dense vehicle index per point
+  const double* time = nullptr;        // epoch seconds (integers in the reference)
+  const float* lon = nullptr;
+  const float* lat = nullptr;
+  const float* accuracy = nullptr;     // < 0 when absent
+  double inactivity = 120.0;           // --inactivity (simple_reporter.py:344)
+  uint32_t n_uuids = 0;
+  uint32_t n_opts = 0;
+  const MatchOptions* opts = nullptr;
+  const uint32_t* uuid_opt = nullptr;  // per vehicle index into opts (NULL: all use opts[0])
+};
+
+// Time-tile stage parameters (simple_reporter.py:176-196, 211-254; CLI defaults :343,345,346)
+struct TileParams {
+  uint32_t quantisation = 3600;
+  uint32_t privacy = 2;
+  std::string source = "smpl_rprt";
+  std::string mode = "AUTO";
+};
+
+// one CSV row of a time tile (simple_reporter.py:192-195) plus its sort keys
+struct TileRow {
+  uint64_t id, next_id;
+  int64_t start, end;                  // floor(t0), ceil(t1)
+  int32_t duration, length, queue;
+  uint32_t bucket;                     // floor(time / quantisation)
+  uint32_t tile;                       // level | tile index << 3 (id & 0x1FFFFFF)
+  uint32_t pad[3];
+};
+static_assert(sizeof(TileRow) == 64, "TileRow is four dwordx4");
+
+struct StageBufs {  // grow-only device buffers of the windowing and tile stages
+  std::vector<void*> allocs;
+  uint64_t cap_pts = 0, cap_rows = 0;
+  uint32_t cap_tr = 0;
+  uint32_t* derr = nullptr;
+  uint32_t* p_uuid = nullptr; double* p_time = nullptr; float* p_lon = nullptr; float* p_lat = nullptr;
+  float* p_acc = nullptr; uint32_t* p_uopt = nullptr; MatchOptions* p_opts = nullptr;
+  unsigned long long* k0 = nullptr; unsigned long long* k1 = nullptr; uint32_t* v0 = nullptr; uint32_t* v1 = nullptr;
+  uint32_t* flag = nullptr; uint32_t* idx = nullptr; uint32_t* wstart = nullptr; uint32_t* wcnt = nullptr;
+  uint32_t* wofs = nullptr; uint32_t* wflag = nullptr; uint32_t* widx = nullptr;
+  uint32_t* trace_uuid = nullptr;
+  TileRow* rows = nullptr; TileRow* rows2 = nullptr;
+  unsigned long long* rk = nullptr; unsigned long long* rk2 = nullptr;
+  uint32_t* rperm = nullptr; uint32_t* rperm2 = nullptr; uint32_t* rflag = nullptr; uint32_t* ridx = nullptr;
+  uint32_t* gpos = nullptr; uint8_t* gkeep = nullptr; uint32_t* tcnt = nullptr; uint32_t* tofs = nullptr;
+  void* tmp = nullptr; size_t tmp_bytes = 0;
+  uint32_t* hctl = nullptr;            // pinned read-back words
+  uint32_t cap_uuids = 0;
+  ~StageBufs();
+};
+
 // error bits in ctl[2]
 constexpr uint32_t kErrCandOverflow = 1u, kErrSearchOverflow = 2u, kErrPathOverflow = 4u, kErrRounds = 8u;
 
 class Engine;
+
+// RCCL communicator handed to the tile stage (one process per GPU)
+struct TileComm {
+  void* nccl;          // ncclComm_t
+  int rank, nranks;
+};
 
 class Matcher {
  public:
@@ -158,6 +220,18 @@ class Matcher {
   void set_timing(bool on) { timing_ = on; }
   hipStream_t stream() const { return stream_; }
 
+  // Raw point stream -> per-vehicle time sort and inactivity windows of >= 2 points on the
+  // GPU (simple_reporter.py:137-164), then every matching stage over the windows.
+  void run_points(const PointsDesc& pd, const RunParams& rp);
+  // vehicle index of every window of the last run_points (n_traces entries)
+  void get_trace_uuid(uint32_t* out);
+  // the batch the last run matched (after run_points: the windows built on the device)
+  void get_batch(uint32_t* trace_off, float* lon, float* lat, double* time, float* acc);
+  // Time tiles of the last run's reports: hour buckets, sort, privacy cull of (id, next_id)
+  // runs and CSV text (simple_reporter.py:176-254).  Returns "name\0body\0" per file.  With
+  // a communicator, rows of every rank are all-gathered and each rank emits the files it owns.
+  std::string tiles(const TileParams& tp, struct TileComm* comm = nullptr);
+
  private:
   void ensure(uint64_t points, uint32_t traces, uint32_t nopts);
   void ensure_trans(uint64_t n, uint64_t n_src);
@@ -175,6 +249,10 @@ class Matcher {
   bool timing_ = false;
   bool has_report_ = false;
   uint32_t* hctl_ = nullptr;  // pinned host mirror of the control words
+  StageBufs sb_;
+  bool from_points_ = false;
+  void ensure_points(uint64_t n, uint32_t n_uuids, uint32_t n_opts);
+  void ensure_rows(uint64_t n, uint32_t traces);
   struct Ev { hipEvent_t a, b; int k; };
   std::vector<Ev> pending_, free_ev_;
   double kms_[kNumKernels] = {0};

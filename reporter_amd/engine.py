@@ -142,6 +142,65 @@ class BatchMatcher:
         _lib.check(_lib.lib().rm_runner_run(self._h, C.byref(d), C.byref(rp)))
         return self
 
+    def run_points(self, uuid, time, lon, lat, accuracy=None, inactivity=120.0, opts=None, uuid_opt=None, n_uuids=None,
+                   **rp_kw):
+        """Raw per-vehicle points (any order) -> device time sort + inactivity windows of
+        >= 2 points (reference py/simple_reporter.py:137-164) -> every matching stage.
+        `uuid` is a dense vehicle index per point.  Blocks until done."""
+        uuid = _c(uuid, np.uint32)
+        n = len(uuid)
+        time = _c(time, np.float64)
+        lon = _c(lon, np.float32)
+        lat = _c(lat, np.float32)
+        accuracy = None if accuracy is None else _c(accuracy, np.float32)
+        if not (len(time) == len(lon) == len(lat) == n) or (accuracy is not None and len(accuracy) != n):
+            raise ValueError("point arrays must have equal lengths")
+        nu = int(n_uuids if n_uuids is not None else (int(uuid.max()) + 1 if n else 0))
+        opts = default_options(1) if opts is None else _c(opts, OPTIONS_DTYPE)
+        uuid_opt = None if uuid_opt is None else _c(uuid_opt, np.uint32)
+        if uuid_opt is not None and len(uuid_opt) != nu:
+            raise ValueError("uuid_opt must have one entry per vehicle")
+        d = _lib.RmPointsDesc(n, uuid.ctypes.data, time.ctypes.data, lon.ctypes.data, lat.ctypes.data,
+                              accuracy.ctypes.data if accuracy is not None else None, float(inactivity), nu, len(opts),
+                              opts.ctypes.data, uuid_opt.ctypes.data if uuid_opt is not None else None)
+        self._keep = (uuid, time, lon, lat, accuracy, opts, uuid_opt)
+        rp = self.run_params(**rp_kw)
+        _lib.check(_lib.lib().rm_runner_run_points(self._h, C.byref(d), C.byref(rp)))
+        return self
+
+    def trace_uuid(self):
+        """Vehicle index of every matched window of the last run_points."""
+        out = np.empty(self.sizes()["traces"], np.uint32)
+        _lib.check(_lib.lib().rm_runner_get_trace_uuid(self._h, out.ctypes.data))
+        return out
+
+    def batch(self):
+        """The batch the last run matched (after run_points: the device-built windows)."""
+        sz = self.sizes()
+        P, T = sz["points"], sz["traces"]
+        off = np.empty(T + 1, np.uint32)
+        lon, lat, acc = (np.empty(P, np.float32) for _ in range(3))
+        time = np.empty(P, np.float64)
+        _lib.check(_lib.lib().rm_runner_get_batch(self._h, off.ctypes.data, lon.ctypes.data, lat.ctypes.data,
+                                                  time.ctypes.data, acc.ctypes.data))
+        return dict(trace_off=off, lon=lon, lat=lat, time=time, accuracy=acc)
+
+    def tiles(self, quantisation=3600, privacy=2, source="smpl_rprt", mode="auto", comm=None):
+        """Time tiles of the last run's reports: {"<start>_<end>/<level>/<index>": CSV text}
+        exactly as the reference's report phase uploads them (py/simple_reporter.py:176-254).
+        With a dist.Comm, rows of every rank are all-gathered and this rank's files returned."""
+        tp = _lib.RmTileParams(int(quantisation), int(privacy), source.encode(), mode.encode())
+        blob = C.c_void_p()
+        n = C.c_size_t()
+        _lib.check(_lib.lib().rm_runner_tiles(self._h, C.byref(tp), comm._h if comm is not None else None,
+                                              C.byref(blob), C.byref(n)))
+        try:
+            raw = C.string_at(blob.value, n.value) if n.value else b""
+        finally:
+            _lib.lib().rm_free(blob)
+        parts = raw.split(b"\0")
+        return {parts[i].decode(): parts[i + 1].decode() for i in range(0, len(parts) - 1, 2)}
+
     def rerun(self, **rp_kw):
         """Run every stage again over the batch already in HBM."""
         rp = self.run_params(**rp_kw)
