@@ -7,6 +7,8 @@ The oracle side is tiles_oracle.split_windows + the C matcher oracle + report() 
 + tiles_oracle.tile_lines / tile_body (the last pinned by the reference's own report()).
 Exactness bar: windows and every matcher stage bit-exact; tile files byte-identical.
 """
+import json
+
 import numpy as np
 import pytest
 
@@ -107,3 +109,30 @@ def test_tiles_empty_and_errors(small_world):
     assert bm.sizes()["traces"] == 0
     with pytest.raises(RuntimeError):
         bm.run_points(np.array([0, 5], np.uint32), np.array([1.0, 2.0]), np.zeros(2), np.zeros(2), n_uuids=2)
+
+
+def test_batch_cli_end_to_end(small_world, tmp_path):
+    """reporter_amd.batch over trace files in the reference's on-disk format."""
+    from reporter_amd import batch
+    g = graphfile.load(small_world)
+    pts = _stream(small_world, n_veh=24, seed=8)
+    tdir = tmp_path / "traces"
+    tdir.mkdir()
+    for f in range(3):   # points of a vehicle may be spread over files (appends from several downloads)
+        sel = np.arange(len(pts["uuid"])) % 3 == f
+        with open(tdir / ("%03x" % f), "w") as fh:
+            for u, t, la, lo, a in zip(pts["uuid"][sel], pts["time"][sel], pts["lat"][sel], pts["lon"][sel],
+                                       pts["accuracy"][sel]):
+                fh.write("v%d,%d,%.6f,%.6f,%d\n" % (u, int(t), la, lo, int(a)))
+    conf = tmp_path / "conf.json"
+    conf.write_text(json.dumps({"meili": {"default": {}}, "reporter_amd": {"graph": small_world}}))
+    files = batch.run([str(p) for p in tdir.iterdir()], str(conf), str(tmp_path / "out"), privacy=2)
+    # oracle over the same parsed points (file order, dense ids in first-seen order)
+    uuids, parsed = batch.read_trace_files(sorted(str(p) for p in tdir.iterdir()))
+    idx, _ = batch.dense_ids(uuids)
+    op = dict(uuid=idx, time=parsed["time"], lon=parsed["lon"], lat=parsed["lat"], accuracy=parsed["accuracy"])
+    _, tr, ref = _oracle(g, op)
+    want = _oracle_tiles(ref, tr, 2)
+    assert files == want and len(files) > 0
+    for name, body in want.items():
+        assert (tmp_path / "out" / name).read_text() == body
