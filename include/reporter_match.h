@@ -48,6 +48,12 @@ int rm_match(rm_matcher* m, const char* trace_json, char** out_json);
 /* n traces at once (one GPU launch sequence); outs[i] must each be freed with rm_free. */
 int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs);
 void rm_free(char* p);
+/* Request coalescing (on unless the config sets "reporter_amd": {"coalesce": false}):
+ * concurrent rm_match calls from many threads are queued and run as one GPU batch by a
+ * dispatcher thread; "coalesce_window_ms" (default 0: take whatever queued while the
+ * previous batch ran) and "coalesce_max_traces" (16384) shape the batches.
+ * out: [0] batches run [1] requests served [2] largest batch [3] requests queued now. */
+int rm_coalesce_stats(uint64_t out[4]);
 
 /* ---------------- matcher options (layout of rm::MatchOptions) ---------------- */
 typedef struct {

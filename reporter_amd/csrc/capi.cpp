@@ -10,7 +10,12 @@
 #include <rccl/rccl.h>
 
 #include <cctype>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <thread>
+#include <vector>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -32,9 +37,14 @@ namespace {
 thread_local std::string g_err;
 int g_device = 0;
 
+struct ParsedTrace;
+class Coalescer;
+
 struct Config {
   std::shared_ptr<Engine> engine;
   MatchOptions mode_defaults[5];
+  std::unique_ptr<Coalescer> coalescer;   // request coalescing for concurrent Match calls
+  ~Config();
 };
 std::mutex g_mu;
 std::shared_ptr<Config> g_conf;
@@ -179,11 +189,143 @@ std::string segments_json(const SegmentRec* s, uint32_t n) {
   return o;
 }
 
+// Request coalescing (HTTP front end): the reference's service answers
+// each /report on its own worker thread with its own matcher (py/reporter_service.py:28-64,
+// 240).  Here every thread's Match is parsed on the calling thread, queued, and a single
+// dispatcher thread runs whatever is queued as ONE GPU batch; requests that arrive while a
+// batch runs form the next one, so nothing waits for a timer at low load and the batch
+// grows with the load (optionally held open for window_ms to fill).  Each caller gets its
+// own segments or its own error; the Java caller's 10 s socket timeout
+// (HttpClient.java:80-87) bounds the useful batch size, not the GPU.
+struct MatchRequest {
+  ParsedTrace* trace;
+  std::string out, err;
+  bool done = false;
+};
+
+class Coalescer {
+ public:
+  Coalescer(std::shared_ptr<Engine> e, double window_ms, size_t max_traces)
+      : eng_(std::move(e)), window_ms_(window_ms), max_(max_traces ? max_traces : 1) {
+    th_ = std::thread([this] { loop(); });
+  }
+  ~Coalescer() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_req_.notify_all();
+    th_.join();
+  }
+  std::string submit(ParsedTrace* t) {
+    MatchRequest r;
+    r.trace = t;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (stop_) throw std::runtime_error("matcher is shutting down");
+      q_.push_back(&r);
+    }
+    cv_req_.notify_one();
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_done_.wait(lk, [&] { return r.done; });
+    if (!r.err.empty()) throw std::runtime_error(r.err);
+    return std::move(r.out);
+  }
+  void stats(uint64_t out[4]) {
+    std::lock_guard<std::mutex> lk(mu_);
+    out[0] = batches_; out[1] = requests_; out[2] = max_seen_; out[3] = (uint64_t)q_.size();
+  }
+
+ private:
+  void loop();
+  std::shared_ptr<Engine> eng_;
+  double window_ms_;
+  size_t max_;
+  std::mutex mu_;
+  std::condition_variable cv_req_, cv_done_;
+  std::deque<MatchRequest*> q_;
+  bool stop_ = false;
+  uint64_t batches_ = 0, requests_ = 0, max_seen_ = 0;
+  std::thread th_;
+};
+
+Config::~Config() { coalescer.reset(); }
+
 char* dup_string(const std::string& s) {
   char* p = (char*)std::malloc(s.size() + 1);
   if (!p) throw std::bad_alloc();
   std::memcpy(p, s.c_str(), s.size() + 1);
   return p;
+}
+
+// run a list of parsed traces as one batch on matcher m; per-trace JSON replies
+std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*>& pt) {
+  const size_t n = pt.size();
+  std::vector<uint32_t> off(n + 1, 0), topt(n);
+  std::vector<MatchOptions> opts(n);
+  for (size_t i = 0; i < n; ++i) { off[i + 1] = off[i] + (uint32_t)pt[i]->lon.size(); opts[i] = pt[i]->opt; topt[i] = (uint32_t)i; }
+  const uint64_t P = off[n];
+  std::vector<float> lon(P), lat(P), acc(P);
+  std::vector<double> tm(P);
+  for (size_t i = 0; i < n; ++i) {
+    std::copy(pt[i]->lon.begin(), pt[i]->lon.end(), lon.begin() + off[i]);
+    std::copy(pt[i]->lat.begin(), pt[i]->lat.end(), lat.begin() + off[i]);
+    std::copy(pt[i]->acc.begin(), pt[i]->acc.end(), acc.begin() + off[i]);
+    std::copy(pt[i]->time.begin(), pt[i]->time.end(), tm.begin() + off[i]);
+  }
+  HostBatch hb;
+  hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = lon.data(); hb.lat = lat.data();
+  hb.time = tm.data(); hb.accuracy = acc.data(); hb.n_opts = (uint32_t)n; hb.opts = opts.data();
+  hb.trace_opt = topt.data();
+  RunParams rp;
+  rp.do_report = 0;
+  m.run(hb, rp);
+  std::vector<uint32_t> soff(n + 1);
+  std::vector<SegmentRec> segs(m.count_segments());
+  m.get_segments(soff.data(), segs.data());
+  std::vector<std::string> out(n);
+  for (size_t i = 0; i < n; ++i) out[i] = segments_json(segs.data() + soff[i], soff[i + 1] - soff[i]);
+  return out;
+}
+
+void Coalescer::loop() {
+  std::unique_ptr<Matcher> m;
+  for (;;) {
+    std::vector<MatchRequest*> batch;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_req_.wait(lk, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty() && stop_) break;
+      if (window_ms_ > 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds((int64_t)(window_ms_ * 1000));
+        while (!stop_ && q_.size() < max_ && cv_req_.wait_until(lk, until) != std::cv_status::timeout) {}
+      }
+      while (!q_.empty() && batch.size() < max_) { batch.push_back(q_.front()); q_.pop_front(); }
+      batches_++;
+      requests_ += batch.size();
+      max_seen_ = std::max<uint64_t>(max_seen_, batch.size());
+    }
+    std::vector<std::string> outs;
+    std::string err;
+    try {
+      if (!m) m = std::make_unique<Matcher>(eng_.get());
+      std::vector<ParsedTrace*> pt;
+      for (MatchRequest* r : batch) pt.push_back(r->trace);
+      outs = match_parsed(*m, pt);
+    } catch (const std::exception& e) {
+      err = e.what();
+      m.reset();   // a fresh workspace for the next batch
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t i = 0; i < batch.size(); ++i) {
+        if (err.empty()) batch[i]->out = std::move(outs[i]);
+        else batch[i]->err = err;
+        batch[i]->done = true;
+      }
+    }
+    cv_done_.notify_all();
+  }
 }
 
 }  // namespace
@@ -241,8 +383,17 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
     }
     if (graph.empty()) throw std::runtime_error("config names no graph (reporter_amd.graph or mjolnir.tile_extract)");
     if (graph[0] != '/') graph = dir_of(path) + "/" + graph;
+    bool coalesce = true;
+    double window_ms = 0.0;
+    size_t max_traces = 16384;
+    if (const json::Value* ra = v.get("reporter_amd")) {
+      if (const json::Value* c = ra->get("coalesce"); c && c->type == json::Value::Bool) coalesce = c->b;
+      if (const json::Value* w = ra->get("coalesce_window_ms"); w && w->is_num()) window_ms = w->num;
+      if (const json::Value* mx = ra->get("coalesce_max_traces"); mx && mx->is_num()) max_traces = (size_t)mx->num;
+    }
     Graph g = Graph::load(graph);
     conf->engine = std::make_shared<Engine>(g, device);
+    if (coalesce) conf->coalescer = std::make_unique<Coalescer>(conf->engine, window_ms, max_traces);
     std::lock_guard<std::mutex> lk(g_mu);
     g_conf = conf;
   });
@@ -264,7 +415,7 @@ rm_matcher* rm_matcher_create(void) {
     if (!c) throw std::runtime_error("valhalla.Configure has not been called");
     auto m = std::make_unique<rm_matcher>();
     m->conf = c;
-    m->m = std::make_unique<Matcher>(c->engine.get());
+    if (!c->coalescer) m->m = std::make_unique<Matcher>(c->engine.get());   // else created on first batch call
     out = m.release();
   });
   return out;
@@ -283,30 +434,17 @@ int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** ou
       if (!traces[i]) throw std::runtime_error("trace string is NULL");
       pt.push_back(parse_trace(traces[i], *m->conf));
     }
-    std::vector<uint32_t> off(n + 1, 0), topt(n);
-    std::vector<MatchOptions> opts(n);
-    for (size_t i = 0; i < n; ++i) { off[i + 1] = off[i] + (uint32_t)pt[i].lon.size(); opts[i] = pt[i].opt; topt[i] = (uint32_t)i; }
-    const uint64_t P = off[n];
-    std::vector<float> lon(P), lat(P), acc(P);
-    std::vector<double> tm(P);
-    for (size_t i = 0; i < n; ++i) {
-      std::copy(pt[i].lon.begin(), pt[i].lon.end(), lon.begin() + off[i]);
-      std::copy(pt[i].lat.begin(), pt[i].lat.end(), lat.begin() + off[i]);
-      std::copy(pt[i].acc.begin(), pt[i].acc.end(), acc.begin() + off[i]);
-      std::copy(pt[i].time.begin(), pt[i].time.end(), tm.begin() + off[i]);
+    std::vector<std::string> js;
+    if (n == 1 && m->conf->coalescer) {
+      js.push_back(m->conf->coalescer->submit(&pt[0]));
+    } else {
+      if (!m->m) m->m = std::make_unique<Matcher>(m->conf->engine.get());
+      std::vector<ParsedTrace*> pp;
+      for (auto& t : pt) pp.push_back(&t);
+      js = match_parsed(*m->m, pp);
     }
-    HostBatch hb;
-    hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = lon.data(); hb.lat = lat.data();
-    hb.time = tm.data(); hb.accuracy = acc.data(); hb.n_opts = (uint32_t)n; hb.opts = opts.data();
-    hb.trace_opt = topt.data();
-    RunParams rp;
-    rp.do_report = 0;
-    m->m->run(hb, rp);
-    std::vector<uint32_t> soff(n + 1);
-    std::vector<SegmentRec> segs(m->m->count_segments());
-    m->m->get_segments(soff.data(), segs.data());
     try {
-      for (size_t i = 0; i < n; ++i) outs[i] = dup_string(segments_json(segs.data() + soff[i], soff[i + 1] - soff[i]));
+      for (size_t i = 0; i < n; ++i) outs[i] = dup_string(js[i]);
     } catch (...) {
       for (size_t i = 0; i < n; ++i) { std::free(outs[i]); outs[i] = nullptr; }
       throw;
@@ -321,6 +459,18 @@ int rm_match(rm_matcher* m, const char* trace_json, char** out_json) {
 }
 
 void rm_free(char* p) { std::free(p); }
+
+int rm_coalesce_stats(uint64_t out[4]) {
+  return guarded([&] {
+    std::shared_ptr<Config> c;
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      c = g_conf;
+    }
+    for (int i = 0; i < 4; ++i) out[i] = 0;
+    if (c && c->coalescer) c->coalescer->stats(out);
+  });
+}
 
 // ---------------- world ----------------
 void rm_default_world_params(rm_world_params* p) {

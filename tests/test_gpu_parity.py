@@ -192,3 +192,48 @@ def test_rerun_is_deterministic(c1):
         o2, s2 = bm.segments()
         np.testing.assert_array_equal(o1, o2)
         assert s1.tobytes() == s2.tobytes()
+
+
+def test_coalesced_match_from_threads(c1, tmpdir_session):
+    """The service's threading model (one SegmentMatcher per worker thread,
+    py/reporter_service.py:28-64) over the coalescing drop-in: concurrent Match calls
+    are served by shared GPU batches and every caller gets its own exact reply."""
+    import threading
+    import valhalla
+    path, g, eng = c1
+    conf = valhalla.write_config(str(tmpdir_session / "conf_coalesce.json"), path, device=0, coalesce=True,
+                                 coalesce_window_ms=3.0)
+    valhalla.Configure(conf)
+    before = valhalla.coalesce_stats()
+    n = 96
+    tr = world.generate_traces(path, n_traces=n, n_points=120, rate_s=1.0, noise_m=5.0, seed=61)
+    ref = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"],
+                               engine.default_options(1), np.zeros(n, np.uint32)))
+    reqs = [json.dumps(world.trace_to_request(tr, k), separators=(",", ":")) for k in range(n)]
+    out = [None] * n
+    errors = []
+
+    def worker(tid):
+        try:
+            sm = valhalla.SegmentMatcher()
+            for k in range(tid, n, 12):
+                out[k] = sm.Match(reqs[k])
+            with pytest.raises(RuntimeError):   # a bad request fails alone (HTTP 500 path)
+                sm.Match('{"uuid":"x","trace":[]}')
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(12)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errors, errors
+    for k in range(n):
+        want = engine.segment_dicts(ref["segs"][ref["seg_off"][k]:ref["seg_off"][k + 1]])
+        assert json.loads(out[k])["segments"] == want
+    st = valhalla.coalesce_stats()
+    served = st["requests"] - before["requests"]
+    assert served == n
+    assert st["batches"] - before["batches"] < served and st["max_batch"] > 1
+    print("coalescing", st)

@@ -18,7 +18,7 @@ import os as _os
 
 from reporter_amd import _lib
 
-__all__ = ["Configure", "SegmentMatcher"]
+__all__ = ["Configure", "SegmentMatcher", "coalesce_stats"]
 
 
 def Configure(conf_path):
@@ -78,10 +78,19 @@ class SegmentMatcher(object):
             pass
 
 
-def write_config(path, graph_path, device=0, **meili_default):
+def coalesce_stats():
+    """Request coalescing counters: batches run, requests served, largest batch, queued now."""
+    out = (C.c_uint64 * 4)()
+    if _lib.lib().rm_coalesce_stats(out) != 0:
+        raise RuntimeError(_lib.last_error())
+    return dict(zip(("batches", "requests", "max_batch", "queued"), [int(x) for x in out]))
+
+
+def write_config(path, graph_path, device=0, coalesce=True, coalesce_window_ms=0.0, **meili_default):
     """Write a Valhalla-style config naming the engine's graph file."""
     conf = {"meili": {"default": dict(meili_default)},
-            "reporter_amd": {"graph": _os.path.abspath(graph_path), "device": int(device)}}
+            "reporter_amd": {"graph": _os.path.abspath(graph_path), "device": int(device), "coalesce": bool(coalesce),
+                             "coalesce_window_ms": float(coalesce_window_ms)}}
     with open(path, "w") as f:
         _json.dump(conf, f, indent=1)
     return path
