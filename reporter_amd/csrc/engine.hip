@@ -640,9 +640,11 @@ constexpr int kLaneCap = RM_LANE_CAP;
 constexpr int kLdsCap = RM_LDS_CAP;
 constexpr uint32_t kNoLen = 0xffffffffu;
 
-struct RegLabels {
-  uint32_t node[kLaneCap], rng[kLaneCap], par[kLaneCap];
-  unsigned long long key[kLaneCap];
+template <int CAP>
+struct RegLabelsT {
+  static constexpr int kLaneCap = CAP;
+  uint32_t node[CAP], rng[CAP], par[CAP];
+  unsigned long long key[CAP];
   uint32_t n, settled;
   bool ovf;
   __device__ __forceinline__ void init() { n = 0; settled = 0; ovf = false; }
@@ -681,6 +683,7 @@ struct RegLabels {
     return true;
   }
 };
+using RegLabels = RegLabelsT<kLaneCap>;
 
 // labels in LDS, lane-minor ([slot][64]) so a wave's accesses to one slot are conflict-free
 struct LdsLabels {
@@ -820,6 +823,38 @@ __global__ void k_all_items(DevBatch b, uint32_t n) {
 }
 #endif
 
+// K2 second register tier: the items the first tier queued, RM_TIER2_CAP labels per lane
+// (compiled for fewer waves per SIMD); what still overflows goes to the wave tier.
+#ifndef RM_TIER2_CAP
+#define RM_TIER2_CAP 12
+#endif
+constexpr int kTier2Cap = RM_TIER2_CAP;
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_routes_reg2(DevGraph g, DevBatch b) {
+  __shared__ uint32_t s_res[kMaxCand][256];
+  const uint32_t n_items = b.ctl[3];
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n_items; q += gridDim.x * blockDim.x) {
+    const uint32_t t = b.rl_routes_a[q];
+    const uint32_t p = b.src_item[t];
+    const uint4 pi = b.pair_info[p];
+    const uint32_t i = t - b.src_off[p];
+    const uint32_t base = b.trans_off[p];
+    const uint32_t bound = pi.x, tmax = pi.y, KB = (pi.z >> 8) & 0xffu;
+    const int mode = (int)(pi.z >> 16);
+    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+    RegLabelsT<kTier2Cap> S;
+    unsigned long long rk1, rk0;
+    lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
+    if (S.ovf) {
+      const uint32_t x = atomicAdd(&b.ctl[5], 1u);
+      b.rl_routes_b[x] = t;
+      continue;
+    }
+    route_targets(b, StoreLabel<RegLabelsT<kTier2Cap>>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB,
+                  &s_res[0][threadIdx.x], 256);
+  }
+}
+
 // K2 LDS lane tier: the items the register tier queued, kLdsCap labels per lane in LDS.
 // Grid-stride over the device-side list; what still overflows goes to the wave tier.
 __global__ void __launch_bounds__(64) k_routes_lds(DevGraph g, DevBatch b) {
@@ -954,6 +989,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
   if (!lane_path(g, b, p, S, kLaneCap)) {
     const uint32_t q = atomicAdd(&b.ctl[4], 1u);
     b.rl_paths_a[q] = (uint32_t)p;
+  }
+}
+
+// path second register tier
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_paths_reg2(DevGraph g, DevBatch b) {
+  const uint32_t n_items = b.ctl[4];
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n_items; q += gridDim.x * blockDim.x) {
+    const uint32_t p = b.rl_paths_a[q];
+    RegLabelsT<kTier2Cap> S;
+    if (!lane_path(g, b, p, S, kTier2Cap)) {
+      const uint32_t x = atomicAdd(&b.ctl[6], 1u);
+      b.rl_paths_b[x] = p;
+    }
   }
 }
 
@@ -2045,7 +2093,11 @@ void Matcher::run_device(const RunParams& rp) {
   if (n_src)
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
 #endif
+#ifdef RM_TIER2_LDS
   hipLaunchKernelGGL(k_routes_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
+#else
+  hipLaunchKernelGGL(k_routes_reg2, dim3(kLdsGrid / 4), dim3(256), 0, st, g, v);
+#endif
   hipLaunchKernelGGL(k_routes_wave, dim3(1024), dim3(64), 0, st, g, v);
   toc(kKRoutes);
   tic(kKViterbi);
@@ -2054,7 +2106,11 @@ void Matcher::run_device(const RunParams& rp) {
   for (int attempt = 0;; ++attempt) {
     tic(kKPaths);
     hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
+#ifdef RM_TIER2_LDS
     hipLaunchKernelGGL(k_paths_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
+#else
+    hipLaunchKernelGGL(k_paths_reg2, dim3(kLdsGrid / 4), dim3(256), 0, st, g, v);
+#endif
     hipLaunchKernelGGL(k_paths_wave<true>, dim3(1024), dim3(64), 0, st, g, v);
     toc(kKPaths);
     // traversal records are laid out by a scan of path_cnt (0 for slots without a chosen transition)
