@@ -98,6 +98,20 @@ rm_engine* rm_engine_create(const char* graph_path, int device);
 void rm_engine_destroy(rm_engine* e);
 uint32_t rm_engine_n_segments(const rm_engine* e);
 int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids); /* n_segments ids (dense index -> OSMLR id) */
+/* Route balls (K2's lookup tier): per node and travel mode, exact shortest (dist, time) keys
+ * to every node within `radius_m`, built once per mode on first use.  Transitions whose
+ * route bound fits the radius are answered by table probes instead of a bounded search;
+ * results are identical either way.  radius_m 0 disables the tier.  Set before the first
+ * run (modes already built keep their tables).  Default 400 m (env RM_BALL_RADIUS_M). */
+int rm_engine_set_ball_radius(rm_engine* e, double radius_m);
+/* out[5]: radius m, keys stored, table entries (16 B each), nodes without a table, build ms */
+int rm_engine_ball_stats(const rm_engine* e, int mode, double out[5]);
+/* Host-only check of the ball tables (no GPU): builds the balls of `mode` for the graph
+ * file and looks up n (from, to) node pairs the way the K2 kernel probes them; keys[i] =
+ * dist_cm << 32 | time_ms, or all-ones when `to` is outside the ball of `from` (or `from`
+ * has no table).  Returns 0 / -1. */
+int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t n, const uint32_t* from,
+                    const uint32_t* to, uint64_t* keys);
 
 rm_runner* rm_runner_create(rm_engine* e);
 void rm_runner_destroy(rm_runner* r);
@@ -132,6 +146,9 @@ int rm_runner_rerun(rm_runner* r, const rm_run_params* p);
  *      [6] route pairs sent to the wave tier [7] ... to the single-source tier
  *      [8] transitions sent to the path wave tier [9] states sent to the candidate wave tier */
 int rm_runner_sizes(rm_runner* r, uint64_t out[10]);
+/* K2 tier hand-overs of the last run: [0] items the ball tier passed to the search tiers,
+ * [1] items the register search tier passed on, [2] items the second register tier passed on */
+int rm_runner_route_tiers(rm_runner* r, uint64_t out[3]);
 int rm_runner_get_states(rm_runner* r, uint32_t* n_states, uint32_t* state_orig);
 int rm_runner_get_candidates(rm_runner* r, uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
 int rm_runner_get_routes(rm_runner* r, uint32_t* trans_off, double* gc, uint32_t* route_cm);

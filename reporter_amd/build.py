@@ -19,8 +19,8 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libreporter_match.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-SOURCES = ["engine.hip", "stages.hip", "capi.cpp", "graph.cpp", "world.cpp"]
-HEADERS = ["engine.hpp", "graph.hpp", "json.hpp", "rm_common.hpp"]
+SOURCES = ["engine.hip", "stages.hip", "capi.cpp", "graph.cpp", "world.cpp", "balls.cpp"]
+HEADERS = ["engine.hpp", "graph.hpp", "json.hpp", "rm_common.hpp", "balls.hpp"]
 
 
 def _hipcc():

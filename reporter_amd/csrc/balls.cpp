@@ -1,0 +1,138 @@
+// balls.cpp — host build of the per-node route balls (see balls.hpp).
+//
+// One Dijkstra per node over the mode's directed edges, keys (dist cm, time ms) packed in
+// a u64 exactly as the matcher's searches add them (rm_common.hpp make_key), pruned at
+// distance > radius.  Two passes over the nodes (count, then fill) so the tables are laid
+// out contiguously without holding every ball in memory at once.
+#include "balls.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <functional>
+#include <queue>
+#include <stdexcept>
+#include <thread>
+#include <utility>
+
+namespace rm {
+namespace {
+
+struct EdgeKey {
+  uint32_t target;
+  uint64_t key;   // kKeyInf when the mode cannot use the edge
+};
+
+// per-thread Dijkstra scratch: dense labels, touched list for O(ball) reset
+struct Scratch {
+  std::vector<uint64_t> lab;
+  std::vector<uint32_t> touched;
+  std::vector<std::pair<uint32_t, uint64_t>> out;  // settled (node, key)
+  using Item = std::pair<uint64_t, uint32_t>;
+  std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
+  explicit Scratch(uint32_t n) : lab(n, kKeyInf) {}
+
+  // settled keys of the ball of u; false when it holds more than max_keys nodes
+  bool run(const Graph& g, const std::vector<EdgeKey>& ek, uint32_t u, uint32_t radius, uint32_t max_keys) {
+    for (uint32_t v : touched) lab[v] = kKeyInf;
+    touched.clear();
+    out.clear();
+    while (!pq.empty()) pq.pop();
+    lab[u] = 0;
+    touched.push_back(u);
+    pq.push({0ull, u});
+    bool ok = true;
+    while (!pq.empty()) {
+      const Item it = pq.top();
+      pq.pop();
+      if (it.first != lab[it.second]) continue;   // stale entry
+      out.push_back({it.second, it.first});
+      if (out.size() > max_keys) { ok = false; break; }
+      for (uint32_t e = g.node_off[it.second]; e < g.node_off[it.second + 1]; ++e) {
+        if (ek[e].key == kKeyInf) continue;
+        const uint64_t nk = it.first + ek[e].key;
+        if (key_dist(nk) > radius) continue;
+        const uint32_t v = ek[e].target;
+        if (nk < lab[v]) {
+          if (lab[v] == kKeyInf) touched.push_back(v);
+          lab[v] = nk;
+          pq.push({nk, v});
+        }
+      }
+    }
+    return ok;
+  }
+};
+
+uint32_t table_bits(uint64_t keys) {
+  uint32_t bits = 1;
+  while ((1ull << bits) < 2 * keys) ++bits;
+  return bits;
+}
+
+template <class F>
+void parallel_nodes(uint32_t n, int threads, F&& f) {
+  threads = std::max(1, std::min<int>(threads, (int)((n + 1023) / 1024)));
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([&, t] {
+      for (uint32_t u = (uint32_t)t; u < n; u += (uint32_t)threads) f(t, u);
+    });
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys, int threads, BallTables& out) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t N = g.num_nodes(), E = g.num_edges();
+  const uint32_t acc = mode_access(mode);
+  std::vector<EdgeKey> ek(E);
+  for (uint32_t e = 0; e < E; ++e) {
+    const EdgeRec& r = g.edges[e];
+    const bool ok = (edge_access(r.info) & acc) != 0u;
+    ek[e] = {r.target, ok ? make_key(r.len_cm, time_ms(r.len_cm, mode_speed_dkph(mode, edge_speed_dkph(r.info)))) : kKeyInf};
+  }
+  threads = std::max(1, threads);
+  std::vector<Scratch> scr;
+  scr.reserve(threads);
+  for (int t = 0; t < threads; ++t) scr.emplace_back(N);
+  // pass 1: table size per node
+  std::vector<uint32_t> bits(N, 0);
+  parallel_nodes(N, threads, [&](int t, uint32_t u) {
+    bits[u] = scr[t].run(g, ek, u, radius_cm, max_keys) ? table_bits(scr[t].out.size()) : 0u;
+  });
+  out.hdr.assign(2 * (size_t)N, 0);
+  uint64_t total = 0;
+  out.n_skipped = 0;
+  for (uint32_t u = 0; u < N; ++u) {
+    out.hdr[2 * (size_t)u] = (uint32_t)total;
+    out.hdr[2 * (size_t)u + 1] = bits[u];
+    if (bits[u]) total += 1ull << bits[u];
+    else out.n_skipped++;
+    if (total >= 0xffffffffull) throw std::runtime_error("route balls too large (entries >= 2^32); lower the radius");
+  }
+  out.ent.assign(4 * total, 0);
+  for (uint64_t i = 0; i < total; ++i) out.ent[4 * i] = kNone;
+  // pass 2: fill (tables are disjoint, so threads write without locks)
+  std::vector<uint64_t> keys(threads, 0);
+  parallel_nodes(N, threads, [&](int t, uint32_t u) {
+    if (!bits[u]) return;
+    scr[t].run(g, ek, u, radius_cm, max_keys);
+    const uint32_t b = bits[u], mask = (1u << b) - 1u;
+    uint32_t* tab = out.ent.data() + 4 * (size_t)out.hdr[2 * (size_t)u];
+    for (const auto& kv : scr[t].out) {
+      uint32_t s = ball_slot(kv.first, b);
+      while (tab[4 * s] != kNone) s = (s + 1) & mask;
+      tab[4 * s] = kv.first;
+      tab[4 * s + 1] = key_dist(kv.second);
+      tab[4 * s + 2] = key_time(kv.second);
+    }
+    keys[t] += scr[t].out.size();
+  });
+  out.n_keys = 0;
+  for (uint64_t k : keys) out.n_keys += k;
+  out.radius_cm = radius_cm;
+  out.build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace rm

@@ -544,6 +544,42 @@ int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids) {
   });
 }
 
+int rm_engine_set_ball_radius(rm_engine* e, double radius_m) {
+  return guarded([&] {
+    if (!(radius_m >= 0.0) || radius_m > 40000.0) throw std::runtime_error("ball radius out of range (0..40000 m)");
+    e->e->set_ball_radius((uint32_t)(radius_m * 100.0));
+  });
+}
+int rm_engine_ball_stats(const rm_engine* e, int mode, double out[5]) {
+  return guarded([&] {
+    if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    out[0] = e->e->ball_radius() / 100.0;
+    e->e->ball_stats(mode, out + 1);
+  });
+}
+
+int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t n, const uint32_t* from,
+                    const uint32_t* to, uint64_t* keys) {
+  return guarded([&] {
+    if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    Graph g = Graph::load(graph_path);
+    BallTables bt;
+    build_balls(g, mode, (uint32_t)(radius_m * 100.0), kBallMaxKeysHost, 4, bt);
+    for (uint64_t i = 0; i < n; ++i) {
+      keys[i] = kKeyInf;
+      if (from[i] >= g.num_nodes()) throw std::runtime_error("node out of range");
+      const uint32_t off = bt.hdr[2 * (size_t)from[i]], bits = bt.hdr[2 * (size_t)from[i] + 1];
+      if (!bits) continue;
+      const uint32_t mask = (1u << bits) - 1u;
+      for (uint32_t s = ball_slot(to[i], bits);; s = (s + 1) & mask) {
+        const uint32_t* e = bt.ent.data() + 4 * ((size_t)off + s);
+        if (e[0] == to[i]) { keys[i] = make_key(e[1], e[2]); break; }
+        if (e[0] == kNone) break;
+      }
+    }
+  });
+}
+
 rm_runner* rm_runner_create(rm_engine* e) {
   rm_runner* out = nullptr;
   guarded([&] {
@@ -587,6 +623,13 @@ int rm_runner_sizes(rm_runner* r, uint64_t out[10]) {
     uint32_t t[4];
     r->m->tier_counts(t);
     for (int i = 0; i < 4; ++i) out[6 + i] = t[i];
+  });
+}
+int rm_runner_route_tiers(rm_runner* r, uint64_t out[3]) {
+  return guarded([&] {
+    uint32_t c[8];
+    r->m->ctl_words(c);
+    out[0] = c[1]; out[1] = c[3]; out[2] = c[5];
   });
 }
 int rm_runner_get_states(rm_runner* r, uint32_t* a, uint32_t* b) { return guarded([&] { r->m->get_states(a, b); }); }

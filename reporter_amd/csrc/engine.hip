@@ -25,7 +25,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "engine.hpp"
 
@@ -66,6 +68,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   ReportRec* reps; uint32_t* rep_cnt; ReportStats* stats;
   // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list
+  uint32_t* rl_routes_0;  // items the K2 ball tier hands to the search tiers (count ctl[1])
   uint32_t* ctl; uint32_t* rl_routes_a; uint32_t* rl_routes_b; uint32_t* rl_paths_a; uint32_t* rl_paths_b;
   uint32_t* rl_cand;
 };
@@ -470,9 +473,10 @@ __device__ __forceinline__ uint32_t d_spr(const uint4& d0) { return d0.w >> 16; 
 // route key from a source candidate a to a target candidate b given a label lookup
 // (dist, time of the shortest route to a node); combos in the oracle's fixed order:
 // direct forward, direct reverse, entry forward (via node0), entry reverse (via node1)
-template <class Label>
-__device__ __forceinline__ unsigned long long route_key(const Label& label, const uint4& a0, const uint4& b0,
-                                                        const uint4& b1, int* combo) {
+// (lab0, lab1 = labels of the target road's node0 / node1; read only when the direction is usable)
+__device__ __forceinline__ unsigned long long route_key_vals(const uint4& a0, const uint4& b0, const uint4& b1,
+                                                             unsigned long long lab0, unsigned long long lab1,
+                                                             int* combo) {
   const uint32_t sa = a0.y, rb = b0.x, sb = b0.y, L = b0.z, spf = d_spf(b0), spr = d_spr(b0);
   unsigned long long best = kKeyInf;
   int bc = -1;
@@ -480,16 +484,18 @@ __device__ __forceinline__ unsigned long long route_key(const Label& label, cons
     if (spf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
     if (spr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
   }
-  if (spf) {
-    const unsigned long long lab = label(b1.x);
-    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(sb, b1.z); if (k < best) { best = k; bc = 2; } }
-  }
-  if (spr) {
-    const unsigned long long lab = label(b1.y);
-    if (lab != kKeyInf) { const unsigned long long k = lab + make_key(L - sb, b1.w); if (k < best) { best = k; bc = 3; } }
-  }
+  if (spf && lab0 != kKeyInf) { const unsigned long long k = lab0 + make_key(sb, b1.z); if (k < best) { best = k; bc = 2; } }
+  if (spr && lab1 != kKeyInf) { const unsigned long long k = lab1 + make_key(L - sb, b1.w); if (k < best) { best = k; bc = 3; } }
   if (combo) *combo = bc;
   return best;
+}
+
+template <class Label>
+__device__ __forceinline__ unsigned long long route_key(const Label& label, const uint4& a0, const uint4& b0,
+                                                        const uint4& b1, int* combo) {
+  const unsigned long long lab0 = d_spf(b0) ? label(b1.x) : kKeyInf;
+  const unsigned long long lab1 = d_spr(b0) ? label(b1.y) : kKeyInf;
+  return route_key_vals(a0, b0, b1, lab0, lab1, combo);
 }
 
 // root keys of a source candidate's two exits (forward to node1, reverse to node0)
@@ -789,12 +795,108 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
   for (uint32_t j = 0; j < KB; ++j) b.route[ob + j] = res[j * stride];
 }
 
+// ------------------------------------------------------------------------------------------
+// K2 ball tier (balls.hpp): when the pair's bound fits in the mode's ball radius, the
+// source's bounded search is replaced by table probes: label(v) = min over the exits x of
+// rk_x + key(x -> v).  The first probe of every (exit, entry node) lookup of four targets
+// is issued together (4 independent 16-byte loads per target in flight per lane); collisions
+// continue by linear probing (tables are at most half full, so an empty slot ends it).
+constexpr uint32_t kBallMaxKeys = kBallMaxKeysHost;
+#ifndef RM_BALL_BATCH
+#define RM_BALL_BATCH 2
+#endif
+constexpr int kBallBatch = RM_BALL_BATCH;   // targets whose first probes are issued together
+
+__device__ __forceinline__ unsigned long long ball_resolve(const uint4* ent, const uint2& h, uint32_t v, uint4 e) {
+  if (e.x == v) return make_key(e.y, e.z);
+  if (e.x == kNone) return kKeyInf;
+  const uint32_t mask = (1u << h.y) - 1u;
+  uint32_t s = ball_slot(v, h.y);
+  for (;;) {
+    s = (s + 1u) & mask;
+    e = ent[h.x + s];
+    if (e.x == v) return make_key(e.y, e.z);
+    if (e.x == kNone) return kKeyInf;
+  }
+}
+
+__device__ __forceinline__ uint4 ball_first(const uint4* ent, const uint2& h, uint32_t v, bool use) {
+  return use ? ent[h.x + ball_slot(v, h.y)] : make_uint4(kNone, 0u, 0u, 0u);
+}
+
+__device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1, unsigned long long d1,
+                                                         unsigned long long rk0, unsigned long long d0) {
+  unsigned long long k = kKeyInf;
+  if (d1 != kKeyInf) k = rk1 + d1;
+  if (d0 != kKeyInf && rk0 + d0 < k) k = rk0 + d0;
+  return k;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_ball(DevGraph g, DevBatch b, uint32_t n_items) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_items) return;
+  const uint32_t p = b.src_item[t];
+  const uint4 pi = b.pair_info[p];
+  const uint32_t i = t - b.src_off[p];
+  const uint32_t base = b.trans_off[p];
+  const uint32_t bound = pi.x, tmax = pi.y, KB = (pi.z >> 8) & 0xffu;
+  const int mode = (int)(pi.z >> 16);
+  const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+  const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+  unsigned long long rk1, rk0;
+  exit_keys(a0, bound, rk1, rk0);
+  const uint4* ent = g.ball_ent[mode];
+  const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
+  const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+  if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {   // search tiers take it
+    b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+    return;
+  }
+  const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
+  __shared__ uint32_t s_res[kMaxCand][256];
+  uint32_t* res = &s_res[0][threadIdx.x];
+  const uint64_t brow = p * kMaxCand * 2;
+  for (uint32_t j0 = 0; j0 < KB; j0 += kBallBatch) {
+    uint4 t0[kBallBatch], t1[kBallBatch];
+#pragma unroll
+    for (int x = 0; x < kBallBatch; ++x) {
+      const uint32_t jc = min(j0 + x, KB - 1u);
+      t0[x] = b.cand_desc[brow + 2 * jc];
+      t1[x] = b.cand_desc[brow + 2 * jc + 1];
+    }
+    uint4 e[kBallBatch][4];   // first probes: exit1 -> node0, exit1 -> node1, exit0 -> node0, exit0 -> node1
+#pragma unroll
+    for (int x = 0; x < kBallBatch; ++x) {
+      const bool f = d_spf(t0[x]) != 0u, r = d_spr(t0[x]) != 0u;
+      e[x][0] = ball_first(ent, h1, t1[x].x, u1 && f);
+      e[x][1] = ball_first(ent, h1, t1[x].y, u1 && r);
+      e[x][2] = ball_first(ent, h0, t1[x].x, u0 && f);
+      e[x][3] = ball_first(ent, h0, t1[x].y, u0 && r);
+    }
+#pragma unroll
+    for (int x = 0; x < kBallBatch; ++x) {
+      const unsigned long long lab0 = ball_label(rk1, ball_resolve(ent, h1, t1[x].x, e[x][0]), rk0,
+                                                 ball_resolve(ent, h0, t1[x].x, e[x][2]));
+      const unsigned long long lab1 = ball_label(rk1, ball_resolve(ent, h1, t1[x].y, e[x][1]), rk0,
+                                                 ball_resolve(ent, h0, t1[x].y, e[x][3]));
+      const unsigned long long key = route_key_vals(a0, t0[x], t1[x], lab0, lab1, nullptr);
+      uint32_t rt = kRouteInvalid;
+      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = key_dist(key);
+      res[((j0 + x) & (kMaxCand - 1)) * 256] = rt;
+    }
+  }
+  const uint64_t ob = (uint64_t)base + i * KB;
+  for (uint32_t j = 0; j < KB; ++j) b.route[ob + j] = res[j * 256];
+}
+
 // K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
 // one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A search
 // that outgrows the registers is queued (as its item) for the LDS lane tier.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_items) return;
+// With `listed`, thread q takes the q-th item the ball tier handed over (rl_routes_0, ctl[1]).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items, int listed) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (listed ? b.ctl[1] : n_items)) return;
+  const uint32_t t = listed ? b.rl_routes_0[q] : q;
   const uint32_t p = b.src_item[t];
   const uint4 pi = b.pair_info[p];
   const uint32_t i = t - b.src_off[p];
@@ -807,8 +909,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
   unsigned long long rk1, rk0;
   lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
   if (S.ovf) {
-    const uint32_t q = atomicAdd(&b.ctl[3], 1u);
-    b.rl_routes_a[q] = t;
+    b.rl_routes_a[atomicAdd(&b.ctl[3], 1u)] = t;
     return;
   }
   __shared__ uint32_t s_res[kMaxCand][256];
@@ -1736,6 +1837,7 @@ T* upload(std::vector<void*>& list, const std::vector<T>& v) {
 
 Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   RM_HIP(hipSetDevice(device));
+  if (const char* r = std::getenv("RM_BALL_RADIUS_M")) ball_radius_cm_ = (uint32_t)(std::max(0.0, std::atof(r)) * 100.0);
   if (g.num_nodes() >= (1u << 28)) throw std::runtime_error("graph has too many nodes (limit 2^28)");
   dg_.node_off = upload(allocs_, g.node_off);
   dg_.edges = (const uint4*)upload(allocs_, g.edges);
@@ -1831,6 +1933,45 @@ Engine::~Engine() {
   for (void* p : allocs_) (void)hipFree(p);
 }
 
+DevGraph Engine::dev_snapshot() const {
+  std::lock_guard<std::mutex> lk(ball_mu_);
+  return dg_;
+}
+
+void Engine::set_ball_radius(uint32_t radius_cm) {
+  std::lock_guard<std::mutex> lk(ball_mu_);
+  ball_radius_cm_ = radius_cm;
+}
+
+void Engine::ball_stats(int mode, double* out4) const {
+  std::lock_guard<std::mutex> lk(ball_mu_);
+  for (int i = 0; i < 4; ++i) out4[i] = (mode >= 0 && mode <= kModePedestrian) ? ball_info_[mode][i] : 0.0;
+}
+
+void Engine::ensure_balls(uint32_t mode_mask) {
+  std::lock_guard<std::mutex> lk(ball_mu_);
+  if (ball_radius_cm_ == 0 || host_.num_nodes() == 0) return;
+  const uint32_t todo = mode_mask & ~ball_built_ & 0x1fu;
+  if (!todo) return;
+  RM_HIP(hipSetDevice(device_));
+  const int threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  for (int mode = 0; mode <= kModePedestrian; ++mode) {
+    if (!((todo >> mode) & 1u)) continue;
+    BallTables bt;
+    build_balls(host_, mode, ball_radius_cm_, kBallMaxKeys, threads, bt);
+    dg_.ball_hdr[mode] = (const uint2*)upload(allocs_, bt.hdr);
+    dg_.ball_ent[mode] = (const uint4*)upload(allocs_, bt.ent);
+    dg_.ball_radius[mode] = bt.radius_cm;
+    dg_.ball_mask |= 1u << mode;
+    ball_built_ |= 1u << mode;
+    ball_info_[mode][0] = (double)bt.n_keys;
+    ball_info_[mode][1] = (double)(bt.ent.size() / 4);
+    ball_info_[mode][2] = (double)bt.n_skipped;
+    ball_info_[mode][3] = bt.build_ms;
+  }
+  RM_HIP(hipDeviceSynchronize());
+}
+
 // ==========================================================================================
 // Workspace / Matcher
 
@@ -1888,7 +2029,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.scan_tmp_bytes = tmp;
   w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
-  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
+  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
   w.run_kind = nullptr; w.run_head = nullptr; w.run_idx = nullptr; w.run_pos = nullptr; w.seg_scan_tmp = nullptr;
   w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
   ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
@@ -1908,10 +2049,12 @@ void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
     if (w.src_item) { (void)hipFree(w.src_item); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.src_item)); }
     if (w.rl_routes_a) { (void)hipFree(w.rl_routes_a); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_a)); }
     if (w.rl_routes_b) { (void)hipFree(w.rl_routes_b); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_b)); }
+    if (w.rl_routes_0) { (void)hipFree(w.rl_routes_0); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_0)); }
     const uint64_t c = n_src + n_src / 4 + 1024;
     w.src_item = dalloc<uint32_t>(w.allocs, c);
     w.rl_routes_a = dalloc<uint32_t>(w.allocs, c);   // overflow lists hold (pair, source) items
     w.rl_routes_b = dalloc<uint32_t>(w.allocs, c);
+    w.rl_routes_0 = dalloc<uint32_t>(w.allocs, c);
     w.cap_src = c;
   }
 }
@@ -2009,7 +2152,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.segs = w.segs; v.seg_base = w.seg_base; v.seg_cnt = w.seg_cnt;
   v.trav = w.trav; v.trav_off = w.trav_off;
   v.reps = w.reps; v.rep_cnt = w.rep_cnt; v.stats = w.stats;
-  v.ctl = w.ctl; v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b;
+  v.ctl = w.ctl; v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
   v.rl_paths_a = w.rl_paths_a; v.rl_paths_b = w.rl_paths_b; v.rl_cand = w.rl_cand;
   return v;
 }
@@ -2024,8 +2167,11 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
     if (hb.trace_off[k + 1] < hb.trace_off[k]) throw std::runtime_error("trace offsets not monotone");
     if (hb.trace_opt[k] >= hb.n_opts) throw std::runtime_error("trace option index out of range");
   }
-  for (uint32_t q = 0; q < hb.n_opts; ++q)
+  mode_mask_ = 0;
+  for (uint32_t q = 0; q < hb.n_opts; ++q) {
     if (hb.opts[q].mode < 0 || hb.opts[q].mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    mode_mask_ |= 1u << hb.opts[q].mode;
+  }
   ensure(P, T, hb.n_opts);
   Workspace& w = ws_;
   hipStream_t st = stream_;
@@ -2048,7 +2194,8 @@ void Matcher::run_device(const RunParams& rp) {
   if (T == 0) return;
   Workspace& w = ws_;
   hipStream_t st = stream_;
-  const DevGraph& g = eng_->dev();
+  eng_->ensure_balls(mode_mask_);
+  const DevGraph g = eng_->dev_snapshot();
   if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 16 * sizeof(uint32_t), hipHostMallocDefault));
   RM_HIP(hipMemsetAsync(w.ctl, 0, 8 * sizeof(uint32_t), st));
   RM_HIP(hipMemsetAsync(w.choice, 0xff, P, st));
@@ -2083,6 +2230,7 @@ void Matcher::run_device(const RunParams& rp) {
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a;
   v.rl_routes_b = w.rl_routes_b;
+  v.rl_routes_0 = w.rl_routes_0;
 
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
@@ -2090,8 +2238,12 @@ void Matcher::run_device(const RunParams& rp) {
   if (n_src)
     hipLaunchKernelGGL(k_all_items, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, v, (uint32_t)n_src);
 #else
-  if (n_src)
-    hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
+  if (n_src && (mode_mask_ & ~g.ball_mask) == 0u) {   // every mode of the batch has its balls
+    hipLaunchKernelGGL(k_routes_ball, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
+    hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, 0u, 1);
+  } else if (n_src) {
+    hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
+  }
 #endif
 #ifdef RM_TIER2_LDS
   hipLaunchKernelGGL(k_routes_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
@@ -2235,10 +2387,15 @@ void Matcher::get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, 
   }
 }
 
-void Matcher::tier_counts(uint32_t* out4) {
+void Matcher::ctl_words(uint32_t* out8) {
   sync();
-  uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (ws_.ctl && n_traces_) RM_HIP(hipMemcpy(c, ws_.ctl, sizeof c, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 8; ++i) out8[i] = 0;
+  if (ws_.ctl && n_traces_) RM_HIP(hipMemcpy(out8, ws_.ctl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+}
+
+void Matcher::tier_counts(uint32_t* out4) {
+  uint32_t c[8];
+  ctl_words(c);
   out4[0] = c[3]; out4[1] = c[5]; out4[2] = c[4]; out4[3] = c[7];
 }
 

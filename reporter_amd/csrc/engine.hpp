@@ -9,10 +9,12 @@
 #include <hip/hip_runtime.h>
 
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "balls.hpp"
 #include "graph.hpp"
 #include "rm_common.hpp"
 
@@ -49,6 +51,12 @@ struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   const uint4* relax[5];         // per travel mode, per directed edge: {target, len_cm | 0xffffffff if the mode
                                  // cannot use it, time_ms at the mode's speed, CSR range of the target}
   const uint32_t* node_rng;      // per node: first out-edge << 5 | out-degree
+  // route balls per travel mode (balls.hpp): per node {first entry, log2 table size or 0},
+  // entries {node | kNone, dist cm, time ms, 0}; radius 0 = not built (K2 searches instead)
+  const uint2* ball_hdr[5];
+  const uint4* ball_ent[5];
+  uint32_t ball_radius[5];
+  uint32_t ball_mask;            // modes whose balls are built
   double lon0, lat0, dlon, dlat;
   uint32_t ncx, ncy, n_nodes, n_edges, n_segments, pad;
 };
@@ -104,10 +112,10 @@ struct Workspace {
   uint8_t* run_kind = nullptr; uint32_t* run_head = nullptr; uint32_t* run_idx = nullptr; uint32_t* run_pos = nullptr;  // K4 run flags
   void* seg_scan_tmp = nullptr; size_t seg_scan_tmp_bytes = 0;
   ReportRec* reps = nullptr; uint32_t* rep_cnt = nullptr; ReportStats* stats = nullptr;
-  // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
+  // control words: [0] path pool used [1] K2 ball-tier hand-over list [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list (overflow lists of the lane tiers)
   uint32_t* ctl = nullptr;
-  uint32_t* rl_routes_a = nullptr; uint32_t* rl_routes_b = nullptr;
+  uint32_t* rl_routes_a = nullptr; uint32_t* rl_routes_b = nullptr; uint32_t* rl_routes_0 = nullptr;
   uint32_t* rl_paths_a = nullptr; uint32_t* rl_paths_b = nullptr; uint32_t* rl_cand = nullptr;
   void* scan_tmp = nullptr; size_t scan_tmp_bytes = 0;
   std::vector<void*> allocs;
@@ -216,6 +224,8 @@ class Matcher {
   void kernel_times(double* ms, uint64_t* launches);
   // overflow-list sizes of the last run: routes A, routes B, paths A, candidates
   void tier_counts(uint32_t* out4);
+  // the eight control words of the last run (zeros before any run)
+  void ctl_words(uint32_t* out8);
   void reset_kernel_times();
   void set_timing(bool on) { timing_ = on; }
   hipStream_t stream() const { return stream_; }
@@ -251,6 +261,7 @@ class Matcher {
   uint32_t* hctl_ = nullptr;  // pinned host mirror of the control words
   StageBufs sb_;
   bool from_points_ = false;
+  uint32_t mode_mask_ = 0;   // travel modes of the batch (bit per Mode): which route balls K2 needs
   void ensure_points(uint64_t n, uint32_t n_uuids, uint32_t n_opts);
   void ensure_rows(uint64_t n, uint32_t traces);
   struct Ev { hipEvent_t a, b; int k; };
@@ -266,15 +277,28 @@ class Engine {
   Engine(const Engine&) = delete;
   Engine& operator=(const Engine&) = delete;
   const DevGraph& dev() const { return dg_; }
+  // copy of the device view taken under the ball lock (tables may be added concurrently)
+  DevGraph dev_snapshot() const;
   int device() const { return device_; }
   const Graph& host() const { return host_; }
   uint32_t n_segments() const { return host_.num_segments(); }
+  // build (once) the route balls of every mode in `mode_mask` (bit per Mode); thread-safe
+  void ensure_balls(uint32_t mode_mask);
+  // ball radius in cm for modes built from now on (0 disables the ball tier)
+  void set_ball_radius(uint32_t radius_cm);
+  uint32_t ball_radius() const { return ball_radius_cm_; }
+  // stats of one mode's tables: {keys, table entries, nodes without a table, build ms}
+  void ball_stats(int mode, double* out4) const;
 
  private:
   int device_;
   Graph host_;
   DevGraph dg_{};
   std::vector<void*> allocs_;
+  mutable std::mutex ball_mu_;
+  uint32_t ball_radius_cm_ = 40000;
+  uint32_t ball_built_ = 0;             // mode bits
+  double ball_info_[5][4] = {};
 };
 
 }  // namespace rm

@@ -109,6 +109,9 @@ RM_HD uint32_t key_dist(uint64_t k) { return (uint32_t)(k >> 32); }
 RM_HD uint32_t key_time(uint64_t k) { return (uint32_t)k; }
 constexpr uint64_t kKeyInf = ~0ull;
 
+// home slot of node v in a route-ball table of 2^bits entries (balls.hpp; bits >= 1)
+RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) { return (v * 2654435761u) >> (32u - bits); }
+
 // ---- matcher limits ----
 constexpr int kMaxCand = 16;            // K: candidates kept per state (nearest first)
 constexpr float kMaxSearchRadius = 200.f;

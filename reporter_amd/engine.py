@@ -77,6 +77,15 @@ class Engine:
         _lib.check(_lib.lib().rm_engine_segment_ids(self._h, ids.ctypes.data))
         return ids
 
+    def set_ball_radius(self, meters):
+        """Radius of the route balls (K2 lookup tier; 0 disables it).  Call before the first run."""
+        _lib.check(_lib.lib().rm_engine_set_ball_radius(self._h, float(meters)))
+
+    def ball_stats(self, mode=0):
+        out = np.zeros(5, np.float64)
+        _lib.check(_lib.lib().rm_engine_ball_stats(self._h, int(mode), out.ctypes.data))
+        return dict(zip(("radius_m", "keys", "entries", "nodes_without_table", "build_ms"), out.tolist()))
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib().rm_engine_destroy(self._h)
@@ -211,6 +220,12 @@ class BatchMatcher:
         _lib.check(_lib.lib().rm_runner_sizes(self._h, out))
         return dict(zip(("points", "traces", "transitions", "path_edges", "segments", "reports", "routes_tier2",
                          "routes_tier3", "paths_tier2", "cand_tier2"), [int(x) for x in out]))
+
+    def route_tiers(self):
+        """K2 hand-overs of the last run: ball tier -> search, register tier -> tier 2, tier 2 -> wave."""
+        out = (C.c_uint64 * 3)()
+        _lib.check(_lib.lib().rm_runner_route_tiers(self._h, out))
+        return dict(zip(("ball_to_search", "lane_to_tier2", "tier2_to_wave"), [int(x) for x in out]))
 
     # ---- stage outputs (parity tests) ----
     def states(self):

@@ -27,6 +27,7 @@ opts = engine.default_options(1, search_radius=c["search_radius"])
 t = time.time()
 bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts)
 print("first run %.3fs" % (time.time() - t), bm.sizes(), flush=True)
+print("route tiers", bm.route_tiers(), "balls", eng.ball_stats(0), flush=True)
 bm.set_timing(True)
 for r in range(a.reps):
     bm.reset_times()

@@ -66,6 +66,33 @@ def test_c1_dense_1hz(c1):
     print("C1 parity", c, "reports", nrep)
 
 
+@pytest.mark.parametrize("radius_m", [0.0, 60.0, 400.0])
+def test_route_ball_tier_radius(small_world, radius_m):
+    """K2 answered by the route balls (table probes), by the bounded searches (radius 0),
+    and by both (a radius most bounds exceed): routes identical to the oracle's searches."""
+    g = graphfile.load(small_world)
+    eng = engine.Engine(small_world, 0)
+    eng.set_ball_radius(radius_m)
+    tr = world.generate_traces(small_world, n_traces=48, n_points=300, rate_s=2.0, noise_m=5.0, seed=21)
+    opts = engine.default_options(2)
+    opts[1]["mode"] = 3   # bicycle: a second mode's tables
+    trace_opt = (np.arange(48) % 2).astype(np.uint32)
+    bm, ref = _run_both(small_world, g, eng, tr, opts, trace_opt)
+    c = compare_all(bm, ref, tr["trace_off"])
+    assert c["chained"] > 500
+    tiers = bm.route_tiers()
+    st = eng.ball_stats(0)
+    if radius_m == 0.0:
+        assert st["keys"] == 0
+    else:
+        assert st["keys"] > 0 and eng.ball_stats(3)["keys"] > 0
+    if radius_m == 60.0:
+        assert tiers["ball_to_search"] > 0    # the mixed case really mixes
+    print("ball radius", radius_m, tiers, st)
+    bm.close()
+    eng.close()
+
+
 def test_sparse_30s_large_radius(built_lib, tmpdir_session):
     """C3-like: 30 s sampling, 200 m blocks, radius 100 m -> long bounded searches (retry tier)."""
     path = str(tmpdir_session / "c3s.rmg")
