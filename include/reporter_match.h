@@ -102,16 +102,16 @@ int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids); /* n_segments ids 
  * to every node within `radius_m`, built once per mode on first use.  Transitions whose
  * route bound fits the radius are answered by table probes instead of a bounded search;
  * results are identical either way.  radius_m 0 disables the tier.  Set before the first
- * run (modes already built keep their tables).  Default 400 m (env RM_BALL_RADIUS_M). */
+ * run (modes already built keep their tables).  0..655.34 m, default 400 m (env RM_BALL_RADIUS_M). */
 int rm_engine_set_ball_radius(rm_engine* e, double radius_m);
 /* out[5]: radius m, keys stored, table entries (16 B each), nodes without a table, build ms */
 int rm_engine_ball_stats(const rm_engine* e, int mode, double out[5]);
 /* Host-only check of the ball tables (no GPU): builds the balls of `mode` for the graph
- * file and looks up n (from, to) node pairs the way the K2 kernel probes them; keys[i] =
- * dist_cm << 32 | time_ms, or all-ones when `to` is outside the ball of `from` (or `from`
- * has no table).  Returns 0 / -1. */
+ * file and looks up n (from node, road) pairs the way the K2 kernel probes them;
+ * keys[2i], keys[2i+1] = dist_cm << 32 | time_ms from `from` to the road's node0 / node1,
+ * all-ones for an endpoint outside the ball (or `from` without a table).  Returns 0 / -1. */
 int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t n, const uint32_t* from,
-                    const uint32_t* to, uint64_t* keys);
+                    const uint32_t* road, uint64_t* keys);
 
 rm_runner* rm_runner_create(rm_engine* e);
 void rm_runner_destroy(rm_runner* r);

@@ -2,8 +2,9 @@
 //
 // One Dijkstra per node over the mode's directed edges, keys (dist cm, time ms) packed in
 // a u64 exactly as the matcher's searches add them (rm_common.hpp make_key), pruned at
-// distance > radius.  Two passes over the nodes (count, then fill) so the tables are laid
-// out contiguously without holding every ball in memory at once.
+// distance > radius; the settled nodes are then folded into one row per incident road.
+// Two passes over the nodes (count, then fill) so the tables are laid out contiguously
+// without holding every ball in memory at once.
 #include "balls.hpp"
 
 #include <algorithm>
@@ -63,6 +64,27 @@ struct Scratch {
   }
 };
 
+// roads touched by a ball: every road with an endpoint in it, with the keys of both
+// endpoints (kKeyInf for an endpoint outside the ball)
+struct RoadAcc {
+  std::vector<uint32_t> pos;      // road -> index in rows (kNone when untouched)
+  std::vector<uint32_t> roads;
+  std::vector<uint64_t> k0, k1;
+  explicit RoadAcc(uint32_t n_roads) : pos(n_roads, kNone) {}
+  void collect(const Graph& g, const std::vector<uint32_t>& inc_off, const std::vector<uint32_t>& inc,
+               const std::vector<std::pair<uint32_t, uint64_t>>& settled) {
+    for (uint32_t r : roads) pos[r] = kNone;
+    roads.clear(); k0.clear(); k1.clear();
+    for (const auto& kv : settled)
+      for (uint32_t q = inc_off[kv.first]; q < inc_off[kv.first + 1]; ++q) {
+        const uint32_t r = inc[q];
+        if (pos[r] == kNone) { pos[r] = (uint32_t)roads.size(); roads.push_back(r); k0.push_back(kKeyInf); k1.push_back(kKeyInf); }
+        if (g.road_node0[r] == kv.first) k0[pos[r]] = kv.second;
+        if (g.road_node1[r] == kv.first) k1[pos[r]] = kv.second;
+      }
+  }
+};
+
 uint32_t table_bits(uint64_t keys) {
   uint32_t bits = 1;
   while ((1ull << bits) < 2 * keys) ++bits;
@@ -92,14 +114,35 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
     const bool ok = (edge_access(r.info) & acc) != 0u;
     ek[e] = {r.target, ok ? make_key(r.len_cm, time_ms(r.len_cm, mode_speed_dkph(mode, edge_speed_dkph(r.info)))) : kKeyInf};
   }
+  if (radius_cm > kBallMaxRadiusCm) throw std::runtime_error("ball radius above 655 m (16-bit distances)");
+  // node -> incident roads
+  const uint32_t R = g.num_roads();
+  std::vector<uint32_t> inc_off(N + 1, 0), inc;
+  for (uint32_t r = 0; r < R; ++r) {
+    inc_off[g.road_node0[r] + 1]++;
+    if (g.road_node1[r] != g.road_node0[r]) inc_off[g.road_node1[r] + 1]++;
+  }
+  for (uint32_t n = 0; n < N; ++n) inc_off[n + 1] += inc_off[n];
+  inc.resize(inc_off[N]);
+  {
+    std::vector<uint32_t> fill(inc_off.begin(), inc_off.end() - 1);
+    for (uint32_t r = 0; r < R; ++r) {
+      inc[fill[g.road_node0[r]]++] = r;
+      if (g.road_node1[r] != g.road_node0[r]) inc[fill[g.road_node1[r]]++] = r;
+    }
+  }
   threads = std::max(1, threads);
   std::vector<Scratch> scr;
+  std::vector<RoadAcc> acc_r;
   scr.reserve(threads);
-  for (int t = 0; t < threads; ++t) scr.emplace_back(N);
+  acc_r.reserve(threads);
+  for (int t = 0; t < threads; ++t) { scr.emplace_back(N); acc_r.emplace_back(R); }
   // pass 1: table size per node
   std::vector<uint32_t> bits(N, 0);
   parallel_nodes(N, threads, [&](int t, uint32_t u) {
-    bits[u] = scr[t].run(g, ek, u, radius_cm, max_keys) ? table_bits(scr[t].out.size()) : 0u;
+    if (!scr[t].run(g, ek, u, radius_cm, max_keys)) { bits[u] = 0; return; }
+    acc_r[t].collect(g, inc_off, inc, scr[t].out);
+    bits[u] = acc_r[t].roads.size() > 2 * (size_t)max_keys ? 0u : table_bits(acc_r[t].roads.size());
   });
   out.hdr.assign(2 * (size_t)N, 0);
   uint64_t total = 0;
@@ -118,16 +161,20 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
   parallel_nodes(N, threads, [&](int t, uint32_t u) {
     if (!bits[u]) return;
     scr[t].run(g, ek, u, radius_cm, max_keys);
+    RoadAcc& ra = acc_r[t];
+    ra.collect(g, inc_off, inc, scr[t].out);
     const uint32_t b = bits[u], mask = (1u << b) - 1u;
     uint32_t* tab = out.ent.data() + 4 * (size_t)out.hdr[2 * (size_t)u];
-    for (const auto& kv : scr[t].out) {
-      uint32_t s = ball_slot(kv.first, b);
+    for (size_t q = 0; q < ra.roads.size(); ++q) {
+      uint32_t s = ball_slot(ra.roads[q], b);
       while (tab[4 * s] != kNone) s = (s + 1) & mask;
-      tab[4 * s] = kv.first;
-      tab[4 * s + 1] = key_dist(kv.second);
-      tab[4 * s + 2] = key_time(kv.second);
+      const uint64_t a = ra.k0[q], c = ra.k1[q];
+      tab[4 * s] = ra.roads[q];
+      tab[4 * s + 1] = (a == kKeyInf ? kBallNoDist : key_dist(a)) | ((c == kKeyInf ? kBallNoDist : key_dist(c)) << 16);
+      tab[4 * s + 2] = a == kKeyInf ? 0u : key_time(a);
+      tab[4 * s + 3] = c == kKeyInf ? 0u : key_time(c);
     }
-    keys[t] += scr[t].out.size();
+    keys[t] += ra.roads.size();
   });
   out.n_keys = 0;
   for (uint64_t k : keys) out.n_keys += k;

@@ -9,7 +9,9 @@
 // multi-root bounded search from the two exits of a source candidate equals
 //     label(v) = min over exits x of  rk_x + key(x -> v)
 // for every v whose key has distance <= bound, so when bound <= radius the search is
-// replaced by two table probes per target entry node.  Built once per graph and mode
+// replaced by table probes.  A node's table is keyed by ROAD: the row of road r holds the
+// keys to both of r's endpoints, so one 16-byte probe per (exit, target candidate) gives
+// both entry labels the target's route combinations need.  Built once per graph and mode
 // (the engine's graph-load step); the tables live in HBM next to the graph.
 #pragma once
 #include <cstdint>
@@ -21,9 +23,10 @@ namespace rm {
 
 struct BallTables {
   std::vector<uint32_t> hdr;   // 2 per node: first entry, log2(table size) (0: no table, node's ball too big)
-  std::vector<uint32_t> ent;   // 4 per entry: node (kEmpty when free), dist cm, time ms, 0
+  std::vector<uint32_t> ent;   // 4 per row: road (kNone when free), dist0 | dist1 << 16 (cm, 0xffff: endpoint
+                               // outside the ball), time0 ms, time1 ms (to the road's node0 / node1)
   uint32_t radius_cm = 0;
-  uint64_t n_keys = 0;         // (node, node) keys stored
+  uint64_t n_keys = 0;         // (node, road) rows stored
   uint32_t n_skipped = 0;      // nodes whose ball exceeded max_keys (their searches use the search tiers)
   double build_ms = 0;
 };
@@ -31,7 +34,9 @@ struct BallTables {
 // Balls of `mode` with radius `radius_cm` (keys with distance <= radius are kept),
 // tables sized to the next power of two >= 2 x keys; nodes with more than `max_keys`
 // keys get no table.  `threads` host threads.
-constexpr uint32_t kBallMaxKeysHost = 4096;   // keys per node above which a node gets no table
+constexpr uint32_t kBallMaxKeysHost = 4096;   // ball nodes above which a node gets no table
+constexpr uint32_t kBallMaxRadiusCm = 65534;   // distances are stored in 16 bits
+constexpr uint32_t kBallNoDist = 0xffffu;
 
 void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys, int threads, BallTables& out);
 

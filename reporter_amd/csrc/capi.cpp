@@ -546,7 +546,7 @@ int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids) {
 
 int rm_engine_set_ball_radius(rm_engine* e, double radius_m) {
   return guarded([&] {
-    if (!(radius_m >= 0.0) || radius_m > 40000.0) throw std::runtime_error("ball radius out of range (0..40000 m)");
+    if (!(radius_m >= 0.0) || radius_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..655.34 m)");
     e->e->set_ball_radius((uint32_t)(radius_m * 100.0));
   });
 }
@@ -559,22 +559,27 @@ int rm_engine_ball_stats(const rm_engine* e, int mode, double out[5]) {
 }
 
 int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t n, const uint32_t* from,
-                    const uint32_t* to, uint64_t* keys) {
+                    const uint32_t* road, uint64_t* keys) {
   return guarded([&] {
     if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    if (!(radius_m >= 0.0) || radius_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..655.34 m)");
     Graph g = Graph::load(graph_path);
     BallTables bt;
     build_balls(g, mode, (uint32_t)(radius_m * 100.0), kBallMaxKeysHost, 4, bt);
     for (uint64_t i = 0; i < n; ++i) {
-      keys[i] = kKeyInf;
-      if (from[i] >= g.num_nodes()) throw std::runtime_error("node out of range");
+      keys[2 * i] = keys[2 * i + 1] = kKeyInf;
+      if (from[i] >= g.num_nodes() || road[i] >= g.num_roads()) throw std::runtime_error("node or road out of range");
       const uint32_t off = bt.hdr[2 * (size_t)from[i]], bits = bt.hdr[2 * (size_t)from[i] + 1];
       if (!bits) continue;
       const uint32_t mask = (1u << bits) - 1u;
-      for (uint32_t s = ball_slot(to[i], bits);; s = (s + 1) & mask) {
+      for (uint32_t s = ball_slot(road[i], bits);; s = (s + 1) & mask) {
         const uint32_t* e = bt.ent.data() + 4 * ((size_t)off + s);
-        if (e[0] == to[i]) { keys[i] = make_key(e[1], e[2]); break; }
         if (e[0] == kNone) break;
+        if (e[0] != road[i]) continue;
+        const uint32_t d0 = e[1] & 0xffffu, d1 = e[1] >> 16;
+        if (d0 != kBallNoDist) keys[2 * i] = make_key(d0, e[2]);
+        if (d1 != kBallNoDist) keys[2 * i + 1] = make_key(d1, e[3]);
+        break;
       }
     }
   });

@@ -801,27 +801,37 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
 // rk_x + key(x -> v).  The first probe of every (exit, entry node) lookup of four targets
 // is issued together (4 independent 16-byte loads per target in flight per lane); collisions
 // continue by linear probing (tables are at most half full, so an empty slot ends it).
+// A table is keyed by road, so one probe per exit gives the labels of both entry nodes.
 constexpr uint32_t kBallMaxKeys = kBallMaxKeysHost;
 #ifndef RM_BALL_BATCH
 #define RM_BALL_BATCH 2
 #endif
 constexpr int kBallBatch = RM_BALL_BATCH;   // targets whose first probes are issued together
 
-__device__ __forceinline__ unsigned long long ball_resolve(const uint4* ent, const uint2& h, uint32_t v, uint4 e) {
-  if (e.x == v) return make_key(e.y, e.z);
-  if (e.x == kNone) return kKeyInf;
+// row of `road` in a node's table (balls.hpp), continuing the probe from first-probe row e
+__device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, uint32_t road, uint4 e) {
+  if (e.x == road || e.x == kNone) return e;
   const uint32_t mask = (1u << h.y) - 1u;
-  uint32_t s = ball_slot(v, h.y);
+  uint32_t s = ball_slot(road, h.y);
   for (;;) {
     s = (s + 1u) & mask;
     e = ent[h.x + s];
-    if (e.x == v) return make_key(e.y, e.z);
-    if (e.x == kNone) return kKeyInf;
+    if (e.x == road || e.x == kNone) return e;
   }
 }
 
-__device__ __forceinline__ uint4 ball_first(const uint4* ent, const uint2& h, uint32_t v, bool use) {
-  return use ? ent[h.x + ball_slot(v, h.y)] : make_uint4(kNone, 0u, 0u, 0u);
+__device__ __forceinline__ uint4 ball_first(const uint4* ent, const uint2& h, uint32_t road, bool use) {
+  return use ? ent[h.x + ball_slot(road, h.y)] : make_uint4(kNone, kBallNoDist * 0x10001u, 0u, 0u);
+}
+
+// keys from a row (kKeyInf for an endpoint outside the ball or a road not in the table)
+__device__ __forceinline__ unsigned long long row_key0(const uint4& e) {
+  const uint32_t d = e.y & 0xffffu;
+  return (e.x == kNone || d == kBallNoDist) ? kKeyInf : make_key(d, e.z);
+}
+__device__ __forceinline__ unsigned long long row_key1(const uint4& e) {
+  const uint32_t d = e.y >> 16;
+  return (e.x == kNone || d == kBallNoDist) ? kKeyInf : make_key(d, e.w);
 }
 
 __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1, unsigned long long d1,
@@ -864,21 +874,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
       t0[x] = b.cand_desc[brow + 2 * jc];
       t1[x] = b.cand_desc[brow + 2 * jc + 1];
     }
-    uint4 e[kBallBatch][4];   // first probes: exit1 -> node0, exit1 -> node1, exit0 -> node0, exit0 -> node1
+    uint4 e1[kBallBatch], e0[kBallBatch];   // first probes of the target road in both exits' tables
 #pragma unroll
     for (int x = 0; x < kBallBatch; ++x) {
-      const bool f = d_spf(t0[x]) != 0u, r = d_spr(t0[x]) != 0u;
-      e[x][0] = ball_first(ent, h1, t1[x].x, u1 && f);
-      e[x][1] = ball_first(ent, h1, t1[x].y, u1 && r);
-      e[x][2] = ball_first(ent, h0, t1[x].x, u0 && f);
-      e[x][3] = ball_first(ent, h0, t1[x].y, u0 && r);
+      const bool any = t0[x].w != 0u;   // some direction of the target road is usable
+      e1[x] = ball_first(ent, h1, t0[x].x, u1 && any);
+      e0[x] = ball_first(ent, h0, t0[x].x, u0 && any);
     }
 #pragma unroll
     for (int x = 0; x < kBallBatch; ++x) {
-      const unsigned long long lab0 = ball_label(rk1, ball_resolve(ent, h1, t1[x].x, e[x][0]), rk0,
-                                                 ball_resolve(ent, h0, t1[x].x, e[x][2]));
-      const unsigned long long lab1 = ball_label(rk1, ball_resolve(ent, h1, t1[x].y, e[x][1]), rk0,
-                                                 ball_resolve(ent, h0, t1[x].y, e[x][3]));
+      const uint4 r1 = ball_resolve(ent, h1, t0[x].x, e1[x]);
+      const uint4 r0 = ball_resolve(ent, h0, t0[x].x, e0[x]);
+      const unsigned long long lab0 = ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
+      const unsigned long long lab1 = ball_label(rk1, row_key1(r1), rk0, row_key1(r0));
       const unsigned long long key = route_key_vals(a0, t0[x], t1[x], lab0, lab1, nullptr);
       uint32_t rt = kRouteInvalid;
       if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = key_dist(key);
@@ -1837,7 +1845,8 @@ T* upload(std::vector<void*>& list, const std::vector<T>& v) {
 
 Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   RM_HIP(hipSetDevice(device));
-  if (const char* r = std::getenv("RM_BALL_RADIUS_M")) ball_radius_cm_ = (uint32_t)(std::max(0.0, std::atof(r)) * 100.0);
+  if (const char* r = std::getenv("RM_BALL_RADIUS_M"))
+    ball_radius_cm_ = (uint32_t)std::min((double)kBallMaxRadiusCm, std::max(0.0, std::atof(r)) * 100.0);
   if (g.num_nodes() >= (1u << 28)) throw std::runtime_error("graph has too many nodes (limit 2^28)");
   dg_.node_off = upload(allocs_, g.node_off);
   dg_.edges = (const uint4*)upload(allocs_, g.edges);

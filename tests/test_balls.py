@@ -1,9 +1,9 @@
 """Route balls (K2's lookup tier, reporter_amd/csrc/balls.cpp) on the CPU.
 
-The tables must hold, for every node u and every node v whose shortest lexicographic
-(dist cm, time ms) key from u has distance <= radius, exactly that key — the value a
-bounded Dijkstra of the reference matcher (meili, simple_reporter.py:166) settles v
-with when started at u with key 0 — and nothing for nodes beyond the radius.  Checked
+The table of node u must hold, for every road with an endpoint whose shortest
+lexicographic (dist cm, time ms) key from u has distance <= radius, exactly those keys —
+the values a bounded Dijkstra of the reference matcher (meili, simple_reporter.py:166)
+settles the endpoints with when started at u with key 0 — and nothing beyond the radius.  Checked
 here against an independent heapq Dijkstra over the graph file, per travel mode, through
 the same probe sequence the GPU kernel uses (rm_balls_lookup).
 """
@@ -53,46 +53,49 @@ def _dijkstra(g, tgt, key, u, radius_cm):
     return done
 
 
-def _lookup(path, mode, radius_m, fr, to):
+def _lookup(path, mode, radius_m, fr, road):
     fr = np.ascontiguousarray(fr, np.uint32)
-    to = np.ascontiguousarray(to, np.uint32)
-    out = np.empty(len(fr), np.uint64)
+    road = np.ascontiguousarray(road, np.uint32)
+    out = np.empty(2 * len(fr), np.uint64)
     _lib.check(_lib.lib().rm_balls_lookup(os.fsencode(path), mode, radius_m, len(fr), fr.ctypes.data,
-                                          to.ctypes.data, out.ctypes.data))
-    return out
+                                          road.ctypes.data, out.ctypes.data))
+    return out.reshape(-1, 2)
 
 
-@pytest.mark.parametrize("mode,radius_m", [(0, 400.0), (0, 150.0), (3, 400.0), (4, 250.0)])
-def test_ball_keys_match_dijkstra(small_world, mode, radius_m):
+@pytest.mark.parametrize("mode,radius_m", [(0, 400.0), (0, 150.0), (3, 400.0), (4, 250.0), (0, 655.0)])
+def test_ball_rows_match_dijkstra(small_world, mode, radius_m):
+    """Row of road r in the table of node u = keys from u to r's node0 and node1."""
     g = graphfile.load(small_world)
     tgt, key = _edge_keys(g, mode)
+    n0, n1 = g["road_node0"], g["road_node1"]
+    R = len(n0)
     rng = np.random.default_rng(mode * 7 + int(radius_m))
-    fr, to, want = [], [], []
-    n = g.n_nodes
-    for u in rng.choice(n, 60, replace=False):
+    fr, roads, want = [], [], []
+    for u in rng.choice(g.n_nodes, 50, replace=False):
         done = _dijkstra(g, tgt, key, int(u), int(radius_m * 100))
-        inside = list(done.items())
-        outside = rng.choice(n, 20)
-        for v, k in inside:
-            fr.append(u); to.append(v); want.append(k)
-        for v in outside:
-            if int(v) not in done:
-                fr.append(u); to.append(v); want.append(KEY_INF)
-    got = _lookup(small_world, mode, radius_m, fr, to)
+        near = np.nonzero(np.isin(n0, list(done)) | np.isin(n1, list(done)))[0]
+        for r in np.concatenate([near, rng.choice(R, 20)]):
+            fr.append(u)
+            roads.append(r)
+            want.append((done.get(int(n0[r]), KEY_INF), done.get(int(n1[r]), KEY_INF)))
+    got = _lookup(small_world, mode, radius_m, fr, roads)
     np.testing.assert_array_equal(got, np.array(want, np.uint64))
-    assert sum(1 for k in want if k != KEY_INF) > 200
+    assert int(np.sum(got != np.uint64(KEY_INF))) > 200
 
 
 def test_ball_radius_zero_keeps_only_self(small_world):
-    got = _lookup(small_world, 0, 0.0, [0, 0, 5], [0, 1, 5])
-    assert list(got) == [0, KEY_INF, 0]
+    g = graphfile.load(small_world)
+    r = int(np.nonzero(g["road_node0"] == 0)[0][0])
+    other = int(g["road_node1"][r])
+    got = _lookup(small_world, 0, 0.0, [0, other], [r, r])
+    assert list(got[0]) == [0, KEY_INF] and list(got[1]) == [KEY_INF, 0]
 
 
 def test_ball_lookup_errors(small_world):
     one = np.zeros(1, np.uint32)
-    out = np.zeros(1, np.uint64)
-    assert _lib.lib().rm_balls_lookup(os.fsencode(small_world), 9, 100.0, 1, one.ctypes.data, one.ctypes.data,
-                                      out.ctypes.data) != 0
+    out = np.zeros(2, np.uint64)
+    L = _lib.lib()
+    assert L.rm_balls_lookup(os.fsencode(small_world), 9, 100.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
+    assert L.rm_balls_lookup(os.fsencode(small_world), 0, 700.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
     big = np.array([10 ** 9], np.uint32)
-    assert _lib.lib().rm_balls_lookup(os.fsencode(small_world), 0, 100.0, 1, big.ctypes.data, one.ctypes.data,
-                                      out.ctypes.data) != 0
+    assert L.rm_balls_lookup(os.fsencode(small_world), 0, 100.0, 1, big.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
