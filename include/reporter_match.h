@@ -147,8 +147,9 @@ int rm_runner_rerun(rm_runner* r, const rm_run_params* p);
  *      [8] transitions sent to the path wave tier [9] states sent to the candidate wave tier */
 int rm_runner_sizes(rm_runner* r, uint64_t out[10]);
 /* K2 tier hand-overs of the last run: [0] items the ball tier passed to the search tiers,
- * [1] items the register search tier passed on, [2] items the second register tier passed on */
-int rm_runner_route_tiers(rm_runner* r, uint64_t out[3]);
+ * [1] items the register search tier passed on, [2] items the second register tier passed on,
+ * [3] chosen transitions the path ball tier passed to the path search tiers */
+int rm_runner_route_tiers(rm_runner* r, uint64_t out[4]);
 int rm_runner_get_states(rm_runner* r, uint32_t* n_states, uint32_t* state_orig);
 int rm_runner_get_candidates(rm_runner* r, uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
 int rm_runner_get_routes(rm_runner* r, uint32_t* trans_off, double* gc, uint32_t* route_cm);

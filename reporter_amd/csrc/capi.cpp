@@ -632,9 +632,9 @@ int rm_runner_sizes(rm_runner* r, uint64_t out[10]) {
 }
 int rm_runner_route_tiers(rm_runner* r, uint64_t out[3]) {
   return guarded([&] {
-    uint32_t c[8];
+    uint32_t c[kCtlWords];
     r->m->ctl_words(c);
-    out[0] = c[1]; out[1] = c[3]; out[2] = c[5];
+    out[0] = c[1]; out[1] = c[3]; out[2] = c[5]; out[3] = c[8];
   });
 }
 int rm_runner_get_states(rm_runner* r, uint32_t* a, uint32_t* b) { return guarded([&] { r->m->get_states(a, b); }); }

@@ -804,7 +804,7 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
 // A table is keyed by road, so one probe per exit gives the labels of both entry nodes.
 constexpr uint32_t kBallMaxKeys = kBallMaxKeysHost;
 #ifndef RM_BALL_BATCH
-#define RM_BALL_BATCH 2
+#define RM_BALL_BATCH 1
 #endif
 constexpr int kBallBatch = RM_BALL_BATCH;   // targets whose first probes are issued together
 
@@ -842,7 +842,10 @@ __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1,
   return k;
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_ball(DevGraph g, DevBatch b, uint32_t n_items) {
+#ifndef RM_BALL_WPE
+#define RM_BALL_WPE 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball(DevGraph g, DevBatch b, uint32_t n_items) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_items) return;
   const uint32_t p = b.src_item[t];
@@ -872,8 +875,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
     for (int x = 0; x < kBallBatch; ++x) {
       const uint32_t jc = min(j0 + x, KB - 1u);
       t0[x] = b.cand_desc[brow + 2 * jc];
+#ifndef RM_BALL_CALC_T1
       t1[x] = b.cand_desc[brow + 2 * jc + 1];
+#endif
     }
+#ifdef RM_BALL_CALC_T1
+#pragma unroll
+    for (int x = 0; x < kBallBatch; ++x) {   // entry times recomputed (Workspace::cand_desc second half)
+      const uint32_t spf = d_spf(t0[x]), spr = d_spr(t0[x]);
+      t1[x] = make_uint4(0u, 0u, spf ? time_ms(t0[x].y, spf) : 0u, spr ? time_ms(t0[x].z - t0[x].y, spr) : 0u);
+    }
+#endif
     uint4 e1[kBallBatch], e0[kBallBatch];   // first probes of the target road in both exits' tables
 #pragma unroll
     for (int x = 0; x < kBallBatch; ++x) {
@@ -997,20 +1009,24 @@ __global__ void __launch_bounds__(64) k_routes_lds(DevGraph g, DevBatch b) {
 // path of one chosen transition (slot p) with a lane-resident search: canonical
 // predecessors (smallest-id tight in-edge from a labelled node) walked back from the
 // entry node.  Returns false when the search outgrew its label store (caller queues p).
+// labels for the path walk: label of node x, which is the `side` endpoint (0: node0,
+// 1: node1) of `road` (the ball tier probes by road; the search tiers ignore both)
 template <class L>
-__device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, uint64_t p, L& S, int cap) {
-  const uint4 pi = b.pair_info[p];
-  const int mode = (int)(pi.z >> 16);
+struct SearchPathLabels {
+  const L& s;
+  __device__ unsigned long long operator()(uint32_t x, uint32_t, uint32_t) const { return s.label(x); }
+};
+
+// Walk the chosen transition's route back from its entry node by canonical predecessors
+// (smallest-id usable in-edge from a labelled node whose label + edge key equals the
+// node's label) and write its edges.  `key`/`combo` are the transition's route key and
+// combination (route_key_vals).
+template <class PL>
+__device__ __forceinline__ void path_walk(const DevGraph& g, const DevBatch& b, uint64_t p, const PL& lab, int mode,
+                                          const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1,
+                                          unsigned long long rk1, unsigned long long rk0, unsigned long long key,
+                                          int combo, int cap) {
   const uint32_t acc = mode_access(mode);
-  const uint32_t bound = pi.x;
-  const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
-  const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
-  const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-  unsigned long long rk1, rk0;
-  lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
-  if (S.ovf) return false;
-  int combo = -1;
-  const unsigned long long key = route_key(StoreLabel<L>{S}, a0, b0, b1, &combo);
   const uint32_t n1a = a1.y, n0a = a1.x;
   uint32_t* inl = b.path_inline + p * kInlinePath;
   if (combo <= 1) {
@@ -1018,7 +1034,7 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
     inl[0] = combo == 0 ? g.road_fwd[a0.x] : g.road_rev[a0.x];
     b.path_cnt[p] = 1;
     b.path_off[p] = 0;
-    return true;
+    return;
   }
   // walk back from the entry node.  Edges are shifted into registers (front = travel
   // order) and stored after the walk: a store inside the walk would make every following
@@ -1026,28 +1042,31 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
   const uint32_t entry_e = combo == 2 ? g.road_fwd[b0.x] : g.road_rev[b0.x];
   const uint32_t v0 = combo == 2 ? b1.x : b1.y;
   uint32_t n = 1, x = v0;
+  unsigned long long lx = lab(v0, b0.x, combo == 2 ? 0u : 1u);
   uint32_t pr[kInlinePath];
 #pragma unroll
   for (int q = 0; q < kInlinePath; ++q) pr[q] = entry_e;
   for (int guard = 0;; ++guard) {
-    const unsigned long long lx = S.label(x);
-    if (lx == kKeyInf || guard > cap) { atomicOr(&b.ctl[2], kErrRounds); return true; }
+    if (lx == kKeyInf || guard > cap) { atomicOr(&b.ctl[2], kErrRounds); return; }
     if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
     uint32_t pe = kNone, pu = 0;
+    unsigned long long plu = kKeyInf;
     for (uint32_t q = g.in_off[x]; q < g.in_off[x + 1]; ++q) {
       const uint32_t e = g.in_edge[q];
       const uint4 rec = g.edges[e];
       if (!edge_ok(rec.z, acc)) continue;
       const uint32_t u = g.edge_src[e];
-      const unsigned long long lu = S.label(u);
-      if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { pe = e; pu = u; break; }
+      // u is the edge's start: node0 of its road when the edge runs forward
+      const unsigned long long lu = lab(u, rec.w >> 1, rec.w & 1u);
+      if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { pe = e; pu = u; plu = lu; break; }
     }
-    if (pe == kNone) { atomicOr(&b.ctl[2], kErrRounds); return true; }
+    if (pe == kNone) { atomicOr(&b.ctl[2], kErrRounds); return; }
 #pragma unroll
     for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
     pr[0] = pe;
     ++n;
     x = pu;
+    lx = plu;
   }
   const uint32_t exit_e = (x == n1a) ? g.road_fwd[a0.x] : g.road_rev[a0.x];
 #pragma unroll
@@ -1061,32 +1080,64 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
     for (int q = 0; q < kInlinePath; ++q)
       if ((uint32_t)q < n) inl[q] = pr[q];
     b.path_off[p] = 0;
-    return true;
+    return;
   }
   // long path: pool slot, second walk writing in travel order
   const uint32_t at = atomicAdd(&b.ctl[0], n);
-  if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); b.path_off[p] = kNone; return true; }
+  if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); b.path_off[p] = kNone; return; }
   b.path_off[p] = at;
   uint32_t* dst = b.path_pool + at;
   dst[n - 1] = entry_e;
   dst[0] = exit_e;
   x = v0;
+  lx = lab(v0, b0.x, combo == 2 ? 0u : 1u);
   for (uint32_t q = n - 2; q >= 1; --q) {
-    const unsigned long long lx = S.label(x);
     for (uint32_t r = g.in_off[x]; r < g.in_off[x + 1]; ++r) {
       const uint32_t e = g.in_edge[r];
       const uint4 rec = g.edges[e];
       if (!edge_ok(rec.z, acc)) continue;
       const uint32_t u = g.edge_src[e];
-      const unsigned long long lu = S.label(u);
-      if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { dst[q] = e; x = u; break; }
+      const unsigned long long lu = lab(u, rec.w >> 1, rec.w & 1u);
+      if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { dst[q] = e; x = u; lx = lu; break; }
     }
   }
+}
+
+// path of one chosen transition (slot p) with a lane-resident search.  Returns false when
+// the search outgrew its label store (caller queues p).
+template <class L>
+__device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, uint64_t p, L& S, int cap) {
+  const uint4 pi = b.pair_info[p];
+  const int mode = (int)(pi.z >> 16);
+  const uint32_t bound = pi.x;
+  const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+  const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
+  const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+  unsigned long long rk1, rk0;
+  lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
+  if (S.ovf) return false;
+  int combo = -1;
+  const unsigned long long key = route_key(StoreLabel<L>{S}, a0, b0, b1, &combo);
+  path_walk(g, b, p, SearchPathLabels<L>{S}, mode, a0, a1, b0, b1, rk1, rk0, key, combo, cap);
   return true;
 }
 
-// path lane tier: one lane per chosen transition, labels in registers
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_paths_lane(DevGraph g, DevBatch b) {
+// labels from the route balls of the two exits (see k_routes_ball)
+struct BallPathLabels {
+  const uint4* ent;
+  uint2 h1, h0;
+  unsigned long long rk1, rk0;
+  __device__ unsigned long long operator()(uint32_t, uint32_t road, uint32_t side) const {
+    const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
+    const uint4 r1 = ball_resolve(ent, h1, road, ball_first(ent, h1, road, u1));
+    const uint4 r0 = ball_resolve(ent, h0, road, ball_first(ent, h0, road, u0));
+    return side ? ball_label(rk1, row_key1(r1), rk0, row_key1(r0)) : ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
+  }
+};
+
+// path ball tier: one lane per chosen transition whose bound fits the ball radius; the
+// others go to the search tiers (rl_routes_0 reused after K2, count ctl[8])
+__global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
   const uint32_t k = b.slot_trace[p];
@@ -1094,6 +1145,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
   const uint32_t s = (uint32_t)(p - o);
   if (s < 1 || s >= b.n_states[k]) return;
   if (b.chain_start[p] || b.choice[p] < 0) return;
+  const uint4 pi = b.pair_info[p];
+  const int mode = (int)(pi.z >> 16);
+  const uint32_t bound = pi.x;
+  const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+  const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
+  const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+  unsigned long long rk1, rk0;
+  exit_keys(a0, bound, rk1, rk0);
+  const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
+  const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+  if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {
+    b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
+    return;
+  }
+  const BallPathLabels lab{g.ball_ent[mode], h1, h0, rk1, rk0};
+  const unsigned long long lab0 = d_spf(b0) ? lab(b1.x, b0.x, 0u) : kKeyInf;
+  const unsigned long long lab1 = d_spr(b0) ? lab(b1.y, b0.x, 1u) : kKeyInf;
+  int combo = -1;
+  const unsigned long long key = route_key_vals(a0, b0, b1, lab0, lab1, &combo);
+  path_walk(g, b, p, lab, mode, a0, a1, b0, b1, rk1, rk0, key, combo, (int)kBallMaxKeys);
+}
+
+// path lane tier: one lane per chosen transition, labels in registers.  With `listed`,
+// thread q takes the q-th transition the ball tier handed over.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_paths_lane(DevGraph g, DevBatch b, int listed) {
+  const uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t p = q0;
+  if (listed) {
+    if (q0 >= b.ctl[8]) return;
+    p = b.rl_routes_0[q0];
+  } else {
+    if (p >= b.P) return;
+    const uint32_t k = b.slot_trace[p];
+    const uint32_t o = b.trace_off[k];
+    const uint32_t s = (uint32_t)(p - o);
+    if (s < 1 || s >= b.n_states[k]) return;
+    if (b.chain_start[p] || b.choice[p] < 0) return;
+  }
   RegLabels S;
   if (!lane_path(g, b, p, S, kLaneCap)) {
     const uint32_t q = atomicAdd(&b.ctl[4], 1u);
@@ -2030,7 +2119,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.trav_off = dalloc<uint32_t>(L, cp);
   w.seg_base = dalloc<uint32_t>(L, ct); w.seg_cnt = dalloc<uint32_t>(L, ct);
   w.rep_cnt = dalloc<uint32_t>(L, ct); w.stats = dalloc<ReportStats>(L, ct);
-  w.ctl = dalloc<uint32_t>(L, 8);
+  w.ctl = dalloc<uint32_t>(L, kCtlWords);
   w.rl_paths_a = dalloc<uint32_t>(L, cp); w.rl_paths_b = dalloc<uint32_t>(L, cp);
   w.rl_cand = dalloc<uint32_t>(L, cp);
   size_t tmp = 0;
@@ -2206,7 +2295,7 @@ void Matcher::run_device(const RunParams& rp) {
   eng_->ensure_balls(mode_mask_);
   const DevGraph g = eng_->dev_snapshot();
   if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 16 * sizeof(uint32_t), hipHostMallocDefault));
-  RM_HIP(hipMemsetAsync(w.ctl, 0, 8 * sizeof(uint32_t), st));
+  RM_HIP(hipMemsetAsync(w.ctl, 0, kCtlWords * sizeof(uint32_t), st));
   RM_HIP(hipMemsetAsync(w.choice, 0xff, P, st));
   RM_HIP(hipMemsetAsync(w.path_cnt, 0, P * sizeof(uint32_t), st));
   DevBatch v = make_view(w, T, P);
@@ -2241,13 +2330,14 @@ void Matcher::run_device(const RunParams& rp) {
   v.rl_routes_b = w.rl_routes_b;
   v.rl_routes_0 = w.rl_routes_0;
 
+  const bool balls = (mode_mask_ & ~g.ball_mask) == 0u;   // every mode of the batch has its route balls
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
 #ifdef RM_ALL_LDS
   if (n_src)
     hipLaunchKernelGGL(k_all_items, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, v, (uint32_t)n_src);
 #else
-  if (n_src && (mode_mask_ & ~g.ball_mask) == 0u) {   // every mode of the batch has its balls
+  if (n_src && balls) {
     hipLaunchKernelGGL(k_routes_ball, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, 0u, 1);
   } else if (n_src) {
@@ -2266,7 +2356,13 @@ void Matcher::run_device(const RunParams& rp) {
   toc(kKViterbi);
   for (int attempt = 0;; ++attempt) {
     tic(kKPaths);
-    hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
+    if (balls) {
+      RM_HIP(hipMemsetAsync(w.ctl + 8, 0, sizeof(uint32_t), st));
+      hipLaunchKernelGGL(k_paths_ball, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
+      hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 1);
+    } else {
+      hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 0);
+    }
 #ifdef RM_TIER2_LDS
     hipLaunchKernelGGL(k_paths_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
 #else
@@ -2396,14 +2492,14 @@ void Matcher::get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, 
   }
 }
 
-void Matcher::ctl_words(uint32_t* out8) {
+void Matcher::ctl_words(uint32_t* out) {
   sync();
-  for (int i = 0; i < 8; ++i) out8[i] = 0;
-  if (ws_.ctl && n_traces_) RM_HIP(hipMemcpy(out8, ws_.ctl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  for (int i = 0; i < kCtlWords; ++i) out[i] = 0;
+  if (ws_.ctl && n_traces_) RM_HIP(hipMemcpy(out, ws_.ctl, kCtlWords * sizeof(uint32_t), hipMemcpyDeviceToHost));
 }
 
 void Matcher::tier_counts(uint32_t* out4) {
-  uint32_t c[8];
+  uint32_t c[kCtlWords];
   ctl_words(c);
   out4[0] = c[3]; out4[1] = c[5]; out4[2] = c[4]; out4[3] = c[7];
 }

@@ -89,6 +89,8 @@ extern const char* const kKernelNames[kNumKernels];
 
 // Device workspace of one batch.  All arrays are indexed by point slot p
 // (state s of trace k lives at slot trace_off[k] + s).
+constexpr int kCtlWords = 16;
+
 struct Workspace {
   uint64_t cap_points = 0, cap_traces = 0, cap_trans = 0, cap_path = 0, cap_opts = 0, cap_segs = 0, cap_src = 0;
   // inputs
@@ -112,7 +114,7 @@ struct Workspace {
   uint8_t* run_kind = nullptr; uint32_t* run_head = nullptr; uint32_t* run_idx = nullptr; uint32_t* run_pos = nullptr;  // K4 run flags
   void* seg_scan_tmp = nullptr; size_t seg_scan_tmp_bytes = 0;
   ReportRec* reps = nullptr; uint32_t* rep_cnt = nullptr; ReportStats* stats = nullptr;
-  // control words: [0] path pool used [1] K2 ball-tier hand-over list [2] error flags [3] routes list A [4] paths list A
+  // control words (kCtlWords): [0] path pool used [1] K2 ball-tier hand-over list [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list (overflow lists of the lane tiers)
   uint32_t* ctl = nullptr;
   uint32_t* rl_routes_a = nullptr; uint32_t* rl_routes_b = nullptr; uint32_t* rl_routes_0 = nullptr;
@@ -224,8 +226,8 @@ class Matcher {
   void kernel_times(double* ms, uint64_t* launches);
   // overflow-list sizes of the last run: routes A, routes B, paths A, candidates
   void tier_counts(uint32_t* out4);
-  // the eight control words of the last run (zeros before any run)
-  void ctl_words(uint32_t* out8);
+  // the kCtlWords control words of the last run (zeros before any run)
+  void ctl_words(uint32_t* out);
   void reset_kernel_times();
   void set_timing(bool on) { timing_ = on; }
   hipStream_t stream() const { return stream_; }

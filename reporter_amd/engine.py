@@ -222,10 +222,12 @@ class BatchMatcher:
                          "routes_tier3", "paths_tier2", "cand_tier2"), [int(x) for x in out]))
 
     def route_tiers(self):
-        """K2 hand-overs of the last run: ball tier -> search, register tier -> tier 2, tier 2 -> wave."""
-        out = (C.c_uint64 * 3)()
+        """Hand-overs of the last run: K2 ball tier -> search, register tier -> tier 2, tier 2 -> wave;
+        path ball tier -> path search tiers."""
+        out = (C.c_uint64 * 4)()
         _lib.check(_lib.lib().rm_runner_route_tiers(self._h, out))
-        return dict(zip(("ball_to_search", "lane_to_tier2", "tier2_to_wave"), [int(x) for x in out]))
+        return dict(zip(("ball_to_search", "lane_to_tier2", "tier2_to_wave", "paths_ball_to_search"),
+                        [int(x) for x in out]))
 
     # ---- stage outputs (parity tests) ----
     def states(self):
