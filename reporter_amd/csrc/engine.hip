@@ -204,6 +204,14 @@ __device__ __forceinline__ void put_cand(const DevGraph& g, const DevBatch& b, u
   b.cand_sq[at] = sq;
 }
 
+// Unrolled loops over the per-lane slot arrays stop as soon as no active lane needs the
+// slot (a scalar branch on a ballot) instead of always walking all kMaxCand slots.
+#ifdef RM_K1_NO_UNIFORM
+#define K1_UNIFORM_STOP(c) false
+#else
+#define K1_UNIFORM_STOP(c) (__ballot(c) == 0ull)
+#endif
+
 // K1 lane tier: one lane per state.  Cell items are read as cell-major 32-byte records
 // (both shape vertices + road + access bits), so a test is two dwordx4 loads with no
 // dependent lookup.  Per-road minima live in 16 registers; a state with more roads
@@ -262,16 +270,20 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
           const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | r1[y].w;
           bool found = false;
 #pragma unroll
-          for (int x = 0; x < kMaxCand; ++x)
+          for (int x = 0; x < kMaxCand; ++x) {
+            if (K1_UNIFORM_STOP(x < (int)n)) break;   // no active lane holds slot x yet
             if (x < (int)n && rroad[x] == road) {
               found = true;
               if (key < rbest[x]) { rbest[x] = key; rs[x] = sc; }
             }
+          }
           if (found) continue;
           if (n >= (uint32_t)kMaxCand) { ovf = true; break; }
 #pragma unroll
-          for (int x = 0; x < kMaxCand; ++x)
+          for (int x = 0; x < kMaxCand; ++x) {
+            if (K1_UNIFORM_STOP(x <= (int)n)) break;
             if (x == (int)n) { rroad[x] = road; rbest[x] = key; rs[x] = sc; }
+          }
           ++n;
         }
       }
@@ -287,6 +299,7 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
   const uint32_t cacc = mode_access(op.mode);
 #pragma unroll
   for (int x0 = 0; x0 < kMaxCand; x0 += 4) {
+    if (K1_UNIFORM_STOP(x0 < (int)n)) break;
     if (x0 >= (int)n) break;
     uint4 ra[4], rc[4];
 #pragma unroll
@@ -303,6 +316,7 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
       uint32_t rank = 0;
 #pragma unroll
       for (int z = 0; z < kMaxCand; ++z) {
+        if (K1_UNIFORM_STOP(z < (int)n)) break;
         if (z >= (int)n) continue;
         const uint32_t sqb2 = (uint32_t)(rbest[z] >> 32);
         rank += (sqb2 < sqb || (sqb2 == sqb && rroad[z] < rroad[x])) ? 1u : 0u;
