@@ -177,7 +177,17 @@ def main():
         steps = max(a.steps, 1)
         routes_ms = kt["routes"][0] / steps
         counts = cpu["counts"] if cpu else {}
-        abytes = mo.routes_algorithmic_bytes(counts) if counts else None
+        balls = eng.ball_stats(0)
+        tiers = bm.route_tiers()
+        ball_tier = balls["radius_m"] > 0 and balls["keys"] > 0
+        # bytes of the formulation the launch runs: route-ball probes (every item answered by
+        # the tables when nothing was handed over), else the bounded searches
+        if counts and ball_tier and tiers["ball_to_search"] == 0:
+            abytes, formulation = mo.routes_ball_algorithmic_bytes(counts), "route-ball table probes"
+        elif counts:
+            abytes, formulation = mo.routes_algorithmic_bytes(counts), "bounded searches"
+        else:
+            abytes, formulation = None, None
         achieved = abytes / (routes_ms * 1e-3) / 1e9 if abytes else None
         traffic = None
         if os.path.exists(a.traffic_json):
@@ -212,7 +222,9 @@ def main():
                                % (world, nseg),
             },
             "roofline": {
-                "kernel": "K2 route stage: k_src_items + k_routes_lane + overflow wave tiers (one launch each per step)",
+                "kernel": "K2 route stage: k_src_items + k_routes_ball + search tiers for hand-overs (one launch "
+                          "each per step)",
+                "formulation": formulation,
                 "bound": "hbm",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
@@ -223,8 +235,11 @@ def main():
                 "traffic_source": (os.path.relpath(a.traffic_json, ROOT) + " (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE "
                                    "passes of this bench, read side x2 per MI355X_MICROARCH.md)") if traffic else None,
                 "algorithmic_bytes_per_launch": abytes,
+                "search_equivalent_bytes_per_launch": mo.routes_algorithmic_bytes(counts) if counts else None,
                 "avg_launch_ms": routes_ms,
                 "counts": counts,
+                "route_tiers": tiers,
+                "route_balls": balls,
             },
             "kernels_ms_per_step": {k: v[0] / steps for k, v in kt.items()},
             "sizes_per_gpu": sizes,

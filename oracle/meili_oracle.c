@@ -80,8 +80,13 @@ static uint64_t mk(uint32_t d, uint32_t t) { return ((uint64_t)d << 32) | t; }
 
 /* ---------------- algorithmic work counters (roofline of K1/K2) ----------------
  * [0] searches [1] settled nodes [2] scanned edges [3] label writes
- * [4] target label lookups [5] route writes [6] candidate items tested [7] states */
-static uint64_t og_cnt[8];
+ * [4] target label lookups [5] route writes [6] candidate items tested [7] states
+ * [8] route-ball rows a table formulation of K2 reads: per (source, target with a usable
+ *     direction), one per usable exit of the source [9] candidate descriptors read by K2
+ *     (KA sources + KB targets per layer pair) */
+#define OG_NCNT 10
+static uint64_t og_cnt[OG_NCNT];
+static uint32_t og_roots;   /* usable exits of the last search_from */
 static int og_counting = 0;
 void og_reset_counters(void) { memset(og_cnt, 0, sizeof og_cnt); }
 void og_get_counters(uint64_t* out) { memcpy(out, og_cnt, sizeof og_cnt); }
@@ -166,6 +171,7 @@ static void search_from(const og_graph* g, search_ws* w, uint32_t road, uint32_t
   if (w->gen == 0) { memset(w->stamp, 0, sizeof(uint32_t) * w->n); w->gen = 1; }
   const uint32_t L = g->road_len_cm[road];
   const uint32_t ef = g->road_fwd[road], er = g->road_rev[road];
+  og_roots = (uint32_t)(e_ok(g, ef, acc) && L - s <= bound) + (uint32_t)(e_ok(g, er, acc) && s <= bound);
   if (e_ok(g, ef, acc) && L - s <= bound) {          /* exit forward to node1 */
     const uint32_t v = g->road_node1[road];
     const uint64_t k = mk(L - s, t_ms(L - s, e_speed(g, ef, mode)));
@@ -520,12 +526,15 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
       }
       og_cnt[4] += 2ull * KA * KB;
       og_cnt[5] += (uint64_t)KA * KB;
+      og_cnt[9] += (uint64_t)KA + KB;
       og_counting = 1;
       for (uint32_t i = 0; i < KA; ++i) {
         const uint32_t ra = R->cand_road[la * (uint64_t)OG_K + i], sa = R->cand_s[la * (uint64_t)OG_K + i];
         search_from(g, &ws, ra, sa, op->mode, bound);
         for (uint32_t j = 0; j < KB; ++j) {
           const uint32_t rb = R->cand_road[lb * (uint64_t)OG_K + j], sb = R->cand_s[lb * (uint64_t)OG_K + j];
+          if (e_ok(g, g->road_fwd[rb], mode_access(op->mode)) || e_ok(g, g->road_rev[rb], mode_access(op->mode)))
+            og_cnt[8] += og_roots;
           const uint64_t key = route_to(g, &ws, ra, sa, rb, sb, op->mode, NULL);
           uint32_t out = OG_ROUTE_INVALID;
           if (key != OG_KEY_INF && (uint32_t)(key >> 32) <= bound && (uint32_t)key <= tmax) out = (uint32_t)(key >> 32);

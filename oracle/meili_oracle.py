@@ -64,7 +64,7 @@ def lib():
 
 
 COUNTER_NAMES = ("searches", "settled", "scanned", "label_writes", "target_lookups", "route_writes",
-                 "cand_items", "states")
+                 "cand_items", "states", "ball_rows", "desc_reads")
 
 
 def reset_counters():
@@ -72,7 +72,7 @@ def reset_counters():
 
 
 def counters():
-    out = np.zeros(8, np.uint64)
+    out = np.zeros(len(COUNTER_NAMES), np.uint64)
     lib().og_get_counters(out.ctypes.data)
     return dict(zip(COUNTER_NAMES, (int(x) for x in out)))
 
@@ -83,6 +83,13 @@ def routes_algorithmic_bytes(c):
     24 B per search (source candidate + its road record)."""
     return (8 * c["settled"] + 16 * c["scanned"] + 12 * c["label_writes"] + 8 * c["target_lookups"]
             + 4 * c["route_writes"] + 24 * c["searches"])
+
+
+def routes_ball_algorithmic_bytes(c):
+    """K2 algorithmic bytes of the route-ball formulation: 16 B table row per
+    (source exit, target) probe, 32 B descriptor per candidate read (KA sources + KB targets
+    per layer pair), 16 B per source for its two exits' table headers, 4 B per route write."""
+    return 16 * c["ball_rows"] + 32 * c["desc_reads"] + 16 * c["searches"] + 4 * c["route_writes"]
 
 
 def candidates_algorithmic_bytes(c):

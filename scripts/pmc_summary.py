@@ -71,8 +71,8 @@ def main():
     with open(os.path.join(a.out, "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     # the K2 stage = every kernel bench.py times as "routes" (each runs once per step)
-    stage = [k for k in summary if k in ("k_src_items", "k_routes_lane", "k_routes_wave<false>", "k_routes_wave<true>",
-                                         "k_routes<false>", "k_routes<true>")]
+    stage = [k for k in summary if k in ("k_src_items", "k_routes_ball", "k_routes_lane", "k_routes_reg2",
+                                         "k_routes_wave")]
     tot = lambda key: sum(summary[k].get(key, 0) for k in stage)
     hits, miss = tot("TCC_HIT_sum"), tot("TCC_MISS_sum")
     rt = {"config": a.config, "traces": a.traces, "kernels": sorted(stage),
