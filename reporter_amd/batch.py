@@ -94,6 +94,10 @@ def run(trace_files, conf, dest_dir, mode="auto", report_levels=(0, 1), transiti
     uuids, pts = read_trace_files(mine)
     idx, names = dense_ids(uuids)
     eng = engine.Engine(graph, device)
+    with open(conf) as f:
+        radius = json.load(f).get("reporter_amd", {}).get("ball_radius")
+    if radius is not None:
+        eng.set_ball_radius(float(radius))
     bm = engine.BatchMatcher(eng)
     try:
         bm.run_points(idx, pts["time"], pts["lon"], pts["lat"], pts["accuracy"], inactivity=inactivity, opts=opts,

@@ -386,13 +386,20 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
     bool coalesce = true;
     double window_ms = 0.0;
     size_t max_traces = 16384;
+    double ball_radius_m = -1.0;   // < 0: engine default (400 m or RM_BALL_RADIUS_M)
     if (const json::Value* ra = v.get("reporter_amd")) {
+      if (const json::Value* br = ra->get("ball_radius"); br && br->is_num()) {
+        ball_radius_m = br->num;
+        if (!(ball_radius_m >= 0.0) || ball_radius_m * 100.0 > kBallMaxRadiusCm)
+          throw std::runtime_error("reporter_amd.ball_radius out of range (0..655.34 m)");
+      }
       if (const json::Value* c = ra->get("coalesce"); c && c->type == json::Value::Bool) coalesce = c->b;
       if (const json::Value* w = ra->get("coalesce_window_ms"); w && w->is_num()) window_ms = w->num;
       if (const json::Value* mx = ra->get("coalesce_max_traces"); mx && mx->is_num()) max_traces = (size_t)mx->num;
     }
     Graph g = Graph::load(graph);
     conf->engine = std::make_shared<Engine>(g, device);
+    if (ball_radius_m >= 0.0) conf->engine->set_ball_radius((uint32_t)(ball_radius_m * 100.0));
     if (coalesce) conf->coalescer = std::make_unique<Coalescer>(conf->engine, window_ms, max_traces);
     std::lock_guard<std::mutex> lk(g_mu);
     g_conf = conf;

@@ -86,11 +86,15 @@ def coalesce_stats():
     return dict(zip(("batches", "requests", "max_batch", "queued"), [int(x) for x in out]))
 
 
-def write_config(path, graph_path, device=0, coalesce=True, coalesce_window_ms=0.0, **meili_default):
-    """Write a Valhalla-style config naming the engine's graph file."""
+def write_config(path, graph_path, device=0, coalesce=True, coalesce_window_ms=0.0, ball_radius=None,
+                 **meili_default):
+    """Write a Valhalla-style config naming the engine's graph file (ball_radius: route-ball radius
+    in metres, 0..655.34, None = engine default)."""
     conf = {"meili": {"default": dict(meili_default)},
             "reporter_amd": {"graph": _os.path.abspath(graph_path), "device": int(device), "coalesce": bool(coalesce),
                              "coalesce_window_ms": float(coalesce_window_ms)}}
+    if ball_radius is not None:
+        conf["reporter_amd"]["ball_radius"] = float(ball_radius)
     with open(path, "w") as f:
         _json.dump(conf, f, indent=1)
     return path
