@@ -889,17 +889,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     for (int x = 0; x < kBallBatch; ++x) {
       const uint32_t jc = min(j0 + x, KB - 1u);
       t0[x] = b.cand_desc[brow + 2 * jc];
-#ifndef RM_BALL_CALC_T1
       t1[x] = b.cand_desc[brow + 2 * jc + 1];
-#endif
     }
-#ifdef RM_BALL_CALC_T1
-#pragma unroll
-    for (int x = 0; x < kBallBatch; ++x) {   // entry times recomputed (Workspace::cand_desc second half)
-      const uint32_t spf = d_spf(t0[x]), spr = d_spr(t0[x]);
-      t1[x] = make_uint4(0u, 0u, spf ? time_ms(t0[x].y, spf) : 0u, spr ? time_ms(t0[x].z - t0[x].y, spr) : 0u);
-    }
-#endif
     uint4 e1[kBallBatch], e0[kBallBatch];   // first probes of the target road in both exits' tables
 #pragma unroll
     for (int x = 0; x < kBallBatch; ++x) {
