@@ -400,6 +400,7 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
     Graph g = Graph::load(graph);
     conf->engine = std::make_shared<Engine>(g, device);
     if (ball_radius_m >= 0.0) conf->engine->set_ball_radius((uint32_t)(ball_radius_m * 100.0));
+    conf->engine->ensure_balls(1u << kModeAuto);   // the service's default mode: no build on the first request
     if (coalesce) conf->coalescer = std::make_unique<Coalescer>(conf->engine, window_ms, max_traces);
     std::lock_guard<std::mutex> lk(g_mu);
     g_conf = conf;

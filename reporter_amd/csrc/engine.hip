@@ -834,6 +834,18 @@ __device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, 
   }
 }
 
+// XCD-aware block order: the dispatcher deals workgroups round-robin over the 8 XCDs
+// (block i runs on XCD i % 8), so consecutive work (the pairs of one trace) would land
+// in 8 different L2s.  Renumber so each XCD gets one contiguous range of logical blocks.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t i, uint32_t n) {
+#ifdef RM_NO_XCD_REMAP
+  return i;
+#else
+  const uint32_t x = i & 7u, idx = i >> 3, q = n >> 3, r = n & 7u;
+  return x < r ? x * (q + 1u) + idx : r * (q + 1u) + (x - r) * q + idx;
+#endif
+}
+
 __device__ __forceinline__ uint4 ball_first(const uint4* ent, const uint2& h, uint32_t road, bool use) {
   return use ? ent[h.x + ball_slot(road, h.y)] : make_uint4(kNone, kBallNoDist * 0x10001u, 0u, 0u);
 }
@@ -860,7 +872,7 @@ __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1,
 #define RM_BALL_WPE 4
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball(DevGraph g, DevBatch b, uint32_t n_items) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= n_items) return;
   const uint32_t p = b.src_item[t];
   const uint4 pi = b.pair_info[p];
@@ -2061,7 +2073,9 @@ void Engine::ensure_balls(uint32_t mode_mask) {
   for (int mode = 0; mode <= kModePedestrian; ++mode) {
     if (!((todo >> mode) & 1u)) continue;
     BallTables bt;
-    build_balls(host_, mode, ball_radius_cm_, kBallMaxKeys, threads, bt);
+    uint32_t max_keys = kBallMaxKeys;   // env RM_BALL_MAX_KEYS: tuning / tests of the no-table path
+    if (const char* e = std::getenv("RM_BALL_MAX_KEYS")) max_keys = (uint32_t)std::max(1, std::atoi(e));
+    build_balls(host_, mode, ball_radius_cm_, max_keys, threads, bt);
     dg_.ball_hdr[mode] = (const uint2*)upload(allocs_, bt.hdr);
     dg_.ball_ent[mode] = (const uint4*)upload(allocs_, bt.ent);
     dg_.ball_radius[mode] = bt.radius_cm;

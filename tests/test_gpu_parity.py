@@ -93,6 +93,25 @@ def test_route_ball_tier_radius(small_world, radius_m):
     eng.close()
 
 
+def test_route_ball_nodes_without_table(small_world, monkeypatch):
+    """Nodes whose ball is too large get no table; transitions leaving through them are
+    handed to the search tiers (K2 and paths) with identical results."""
+    monkeypatch.setenv("RM_BALL_MAX_KEYS", "8")   # 200 m balls hold ~5-13 nodes on this grid: a mix
+    g = graphfile.load(small_world)
+    eng = engine.Engine(small_world, 0)
+    eng.set_ball_radius(200.0)
+    tr = world.generate_traces(small_world, n_traces=32, n_points=300, rate_s=1.0, noise_m=5.0, seed=23)
+    bm, ref = _run_both(small_world, g, eng, tr, engine.default_options(1), np.zeros(32, np.uint32))
+    c = compare_all(bm, ref, tr["trace_off"])
+    st, tiers = eng.ball_stats(0), bm.route_tiers()
+    assert st["nodes_without_table"] > 0 and st["keys"] > 0
+    assert tiers["ball_to_search"] > 0 and tiers["paths_ball_to_search"] > 0
+    assert c["chained"] > 500
+    print("no-table nodes", st, tiers)
+    bm.close()
+    eng.close()
+
+
 def test_sparse_30s_large_radius(built_lib, tmpdir_session):
     """C3-like: 30 s sampling, 200 m blocks, radius 100 m -> long bounded searches (retry tier)."""
     path = str(tmpdir_session / "c3s.rmg")
