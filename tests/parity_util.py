@@ -12,6 +12,17 @@ def state_slots(trace_off, n_states):
     return m
 
 
+def _ranges(starts, lens):
+    """Concatenated index ranges [starts[i], starts[i] + lens[i]) (vectorised)."""
+    starts = np.asarray(starts, np.int64)
+    lens = np.asarray(lens, np.int64)
+    total = int(lens.sum())
+    if total == 0:
+        return np.zeros(0, np.int64)
+    first = np.cumsum(lens) - lens
+    return np.repeat(starts - first, lens) + np.arange(total, dtype=np.int64)
+
+
 def compare_all(gpu, ref, trace_off, check_reports=True):
     """Assert bit-exact agreement of every stage; returns a dict of counts."""
     n_states, orig = gpu.states()
@@ -43,11 +54,16 @@ def compare_all(gpu, ref, trace_off, check_reports=True):
     inchain = tm & (cs == 0) & (choice >= 0)
     np.testing.assert_array_equal(pcnt[inchain], ref["path_cnt"][inchain], "path_cnt")
     np.testing.assert_array_equal(rdist[inchain], ref["route_dist"][inchain], "route_dist")
-    for p in np.nonzero(inchain)[0]:
-        a = pool[poff[p]:poff[p] + pcnt[p]]
-        b = ref["path_pool"][ref["path_off"][p]:ref["path_off"][p] + ref["path_cnt"][p]]
-        if not np.array_equal(a, b):
-            raise AssertionError("path edges differ at slot %d: gpu %s oracle %s" % (p, a, b))
+    sel = np.nonzero(inchain)[0]
+    lens = pcnt[sel].astype(np.int64)
+    a = pool[_ranges(poff[sel], lens)]
+    b = ref["path_pool"][_ranges(ref["path_off"][sel], lens)]
+    if not np.array_equal(a, b):
+        bad = np.nonzero(a != b)[0][0]
+        p = sel[np.searchsorted(np.cumsum(lens), bad, side="right")]
+        raise AssertionError("path edges differ at slot %d: gpu %s oracle %s" % (
+            p, pool[poff[p]:poff[p] + pcnt[p]],
+            ref["path_pool"][ref["path_off"][p]:ref["path_off"][p] + ref["path_cnt"][p]]))
 
     soff, segs = gpu.segments()
     np.testing.assert_array_equal(soff, ref["seg_off"], "seg_off")
@@ -59,3 +75,36 @@ def compare_all(gpu, ref, trace_off, check_reports=True):
             np.testing.assert_array_equal(a, b, "segments." + f)
     return dict(points=int(trace_off[-1]), states=int(sm.sum()), transitions=len(route),
                 chained=int(inchain.sum()), segments=len(segs))
+
+
+def _levels_mask(levels):
+    from reporter_amd import engine
+    return engine.levels_mask(levels)
+
+
+def check_reports(bm, ref, tr, rl=(0, 1), tl=(0, 1), threshold=15.0):
+    """report() per trace: GPU k_report against the oracle's og_report_trace, bit for bit."""
+    import meili_oracle as mo
+    off, reps, stats = bm.reports()
+    rmask, tmask = _levels_mask(rl), _levels_mask(tl)
+    T = len(tr["trace_off"]) - 1
+    wants, wsts = [], []
+    for k in range(T):
+        s0, s1 = ref["seg_off"][k], ref["seg_off"][k + 1]
+        end_t = tr["time"][tr["trace_off"][k + 1] - 1]
+        want, wst = mo.report_trace(ref["segs"][s0:s1], end_t, threshold, rmask, tmask)
+        if off[k + 1] - off[k] != len(want):
+            raise AssertionError("trace %d: %d reports vs %d" % (k, off[k + 1] - off[k], len(want)))
+        wants.append(want)
+        wsts.append(wst)
+    want = np.concatenate(wants) if wants else reps[:0]
+    got = reps[off[0]:off[T]]
+    for f in want.dtype.names:
+        a, b = got[f], want[f]
+        if a.dtype.kind == "f":
+            a, b = a.view(np.uint64), b.view(np.uint64)
+        np.testing.assert_array_equal(a, b, "report field " + f)
+    for f in stats.dtype.names:
+        np.testing.assert_array_equal(stats[f][:T].astype(np.int64), np.array([w[f] for w in wsts], np.int64),
+                                      "stat " + f)
+    return len(got)

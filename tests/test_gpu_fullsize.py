@@ -1,0 +1,118 @@
+"""GPU parity at BASELINE.json's full graph sizes.
+
+test_gpu_parity.py covers the configs on graphs scaled so every corner case is
+cheap; here the graphs are the configs' own (C2/C5: 200x200 @100 m, C3:
+500x500 @200 m, C4: a 1000x1000 @250 m country slice of the 4000x4000 graph —
+the full one takes a minute to generate on the host), and the C2 batch is the
+bench's exact rank-0 workload (10,000 traces x 600 points, seed 1000): every
+stage of every trajectory must equal the oracle bit for bit, and the speed
+histogram must equal the CPU pipeline's.  C3/C4/C5 check bounded trace
+samples (the oracle's long 30 s searches run ~8k points/s on one core).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import meili_oracle as mo
+from parity_util import check_reports, compare_all
+from reporter_amd import _lib, engine, graphfile, world
+
+pytestmark = pytest.mark.gpu
+
+
+def _world(tmpdir_session, name, rows=None, cols=None):
+    cfg = dict(world.CONFIGS[name])
+    path = str(tmpdir_session / ("full_%s_%s.rmg" % (name, rows or cfg["rows"])))
+    world.build_world(path, rows or cfg["rows"], cols or cfg["cols"], cfg["block_m"], seed=1, cell_m=cfg["cell_m"])
+    return path, cfg
+
+
+def _match_and_compare(path, tr, opts, trace_opt, rl=(0, 1), tl=(0, 1), hist=False):
+    g = graphfile.load(path)
+    eng = engine.Engine(path, 0)
+    T = len(tr["trace_off"]) - 1
+    if trace_opt is None:
+        trace_opt = np.zeros(T, np.uint32)
+    nseg = eng.n_segments
+    dptr = ctypes.c_void_p()
+    rp = dict(report_levels=rl, transition_levels=tl)
+    if hist:
+        _lib.check(_lib.lib().rm_device_alloc(nseg * 16 * 4, ctypes.byref(dptr)))
+        _lib.check(_lib.lib().rm_device_memset(dptr, 0, nseg * 16 * 4))
+        rp["hist_dev"] = dptr.value
+    try:
+        bm = engine.BatchMatcher(eng)
+        bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt, **rp)
+        if hist:
+            got_hist = np.empty(nseg * 16, np.uint32)
+            _lib.check(_lib.lib().rm_device_download(got_hist.ctypes.data, dptr, got_hist.nbytes))
+    finally:
+        if hist:
+            _lib.lib().rm_device_free(dptr)
+    batch = mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt)
+    ref = mo.match(g, batch)
+    c = compare_all(bm, ref, tr["trace_off"])
+    c["reports"] = check_reports(bm, ref, tr, rl=rl, tl=tl)
+    if hist:
+        want = np.zeros(nseg * 16, np.uint32)
+        nvalid = mo.pipeline(g, batch, 15.0, engine.levels_mask(rl), engine.levels_mask(tl), want)
+        np.testing.assert_array_equal(got_hist, want, "speed histogram")
+        assert int(got_hist.sum()) == nvalid
+        c["valid_reports"] = nvalid
+    c["traces"] = T
+    c["route_tiers"] = bm.route_tiers()
+    bm.close()
+    eng.close()
+    return c
+
+
+@pytest.mark.timeout(400)
+def test_c2_full_bench_workload(built_lib, tmpdir_session):
+    """C2 exactly as bench.py rank 0 runs it: all 10,000 trajectories bit-exact."""
+    path, cfg = _world(tmpdir_session, "C2")
+    tr = world.generate_traces(path, cfg["n_traces"], cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=1000)
+    opts = engine.default_options(1, search_radius=cfg["search_radius"])
+    c = _match_and_compare(path, tr, opts, None, hist=True)
+    assert c["points"] == 6_000_000 and c["segments"] > 200_000 and c["valid_reports"] > 50_000, c
+    print("C2 full parity", c)
+
+
+def test_c3_full_graph_sample(built_lib, tmpdir_session):
+    """C3 graph (500x500 @200 m), 30 s sampling, radius 100 m: searches beyond the ball radius."""
+    path, cfg = _world(tmpdir_session, "C3")
+    tr = world.generate_traces(path, 1500, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=3000)
+    opts = engine.default_options(1, search_radius=cfg["search_radius"])
+    c = _match_and_compare(path, tr, opts, None, hist=True)
+    assert c["chained"] > 40_000, c
+    print("C3 sample parity", c)
+
+
+def test_c4_country_slice_sample(built_lib, tmpdir_session):
+    """C4 block size and sampling (250 m, 5 s) on a 1000x1000 slice (1 M nodes)."""
+    path, cfg = _world(tmpdir_session, "C4", rows=1000, cols=1000)
+    tr = world.generate_traces(path, 2000, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=4000)
+    opts = engine.default_options(1, search_radius=cfg["search_radius"])
+    c = _match_and_compare(path, tr, opts, None, hist=True)
+    assert c["segments"] > 20_000, c
+    print("C4 slice parity", c)
+
+
+def test_c5_full_graph_modes_sigma(built_lib, tmpdir_session):
+    """C5: C2 graph, auto/bicycle/pedestrian x sigma_z {2, 4.07, 8, 16}, radius max(50, 3 sigma)."""
+    path, cfg = _world(tmpdir_session, "C5")
+    parts, opts = [], []
+    per = 100
+    for mi, mode in enumerate(("auto", "bicycle", "pedestrian")):
+        for si, sz in enumerate((2.0, 4.07, 8.0, 16.0)):
+            parts.append(world.generate_traces(path, n_traces=per, n_points=cfg["n_points"], rate_s=1.0, noise_m=sz,
+                                               seed=5000 + mi * 10 + si, mode=mode))
+            opts.append(engine.default_options(1, mode=world.MODES[mode], sigma_z=sz,
+                                               search_radius=max(50.0, 3 * sz))[0])
+    tr = {k: np.concatenate([p[k] for p in parts]) for k in ("lon", "lat", "time", "accuracy")}
+    tr["trace_off"] = (np.arange(len(parts) * per + 1) * cfg["n_points"]).astype(np.uint32)
+    trace_opt = np.repeat(np.arange(len(parts), dtype=np.uint32), per)
+    opts = np.array(opts, engine.OPTIONS_DTYPE)
+    c = _match_and_compare(path, tr, opts, trace_opt, rl=(0, 1, 2), tl=(0, 1, 2), hist=True)
+    assert c["traces"] == 1200 and c["segments"] > 10_000, c
+    print("C5 parity", c)

@@ -13,7 +13,7 @@ import pytest
 
 import meili_oracle as mo
 import report_oracle
-from parity_util import compare_all
+from parity_util import check_reports as _check_reports, compare_all
 from reporter_amd import engine, graphfile, world
 
 pytestmark = pytest.mark.gpu
@@ -30,28 +30,6 @@ def _run_both(graph_path, g, eng, tr, opts, trace_opt, **rp):
     bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt, **rp)
     ref = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt))
     return bm, ref
-
-
-def _check_reports(bm, ref, tr, rl=(0, 1), tl=(0, 1), threshold=15.0):
-    off, reps, stats = bm.reports()
-    rmask, tmask = engine.levels_mask(rl), engine.levels_mask(tl)
-    T = len(tr["trace_off"]) - 1
-    n = 0
-    for k in range(T):
-        s0, s1 = ref["seg_off"][k], ref["seg_off"][k + 1]
-        end_t = tr["time"][tr["trace_off"][k + 1] - 1]
-        want, wst = mo.report_trace(ref["segs"][s0:s1], end_t, threshold, rmask, tmask)
-        got = reps[off[k]:off[k + 1]]
-        assert len(got) == len(want), "trace %d: %d reports vs %d" % (k, len(got), len(want))
-        for f in want.dtype.names:
-            a, b = got[f], want[f]
-            if a.dtype.kind == "f":
-                a, b = a.view(np.uint64), b.view(np.uint64)
-            np.testing.assert_array_equal(a, b, "report field " + f)
-        for f in stats.dtype.names:
-            assert int(stats[k][f]) == int(wst[f]), "trace %d stat %s" % (k, f)
-        n += len(got)
-    return n
 
 
 def test_c1_dense_1hz(c1):
