@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--traces", type=int, default=0, help="override traces per rank")
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (default min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ball-radius", type=float, default=None,
+                    help="route-ball radius in m (default: the config's, else the engine's automatic radius)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_routes_c2.json"),
                     help="rocprofv3 PMC summary giving HBM bytes per routes launch (optional)")
     return ap.parse_args()
@@ -138,6 +140,9 @@ def main():
 
     comm = dist.Comm(rank, world, local, token=os.environ.get("RM_RDZV_TOKEN")) if world > 1 else None
     eng = engine.Engine(gpath, local)
+    radius = a.ball_radius if a.ball_radius is not None else cfg.get("ball_radius_m")
+    if radius is not None:
+        eng.set_ball_radius(radius)   # else the engine's automatic radius (balls.hpp auto_ball_radius_cm)
     bm = engine.BatchMatcher(eng)
     nseg = eng.n_segments
     hist = dist.DeviceBuffer(nseg * 16 * 4)

@@ -102,8 +102,13 @@ int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids); /* n_segments ids 
  * to every node within `radius_m`, built once per mode on first use.  Transitions whose
  * route bound fits the radius are answered by table probes instead of a bounded search;
  * results are identical either way.  radius_m 0 disables the tier.  Set before the first
- * run (modes already built keep their tables).  0..655.34 m, default 400 m (env RM_BALL_RADIUS_M). */
+ * run (modes already built keep their tables).  0..10000 m.  Default: env RM_BALL_RADIUS_M,
+ * else rm_graph_auto_ball_radius of the graph. */
 int rm_engine_set_ball_radius(rm_engine* e, double radius_m);
+/* Host-only: the engine's automatic radius for a graph file — the largest of 2000 m (meili's
+ * default breakage distance, so every default-bounded transition is a table probe), 1500,
+ * 1000, 700, 500 m whose estimated tables stay within 16 GiB per mode; else 400 m. */
+int rm_graph_auto_ball_radius(const char* graph_path, double* radius_m);
 /* out[5]: radius m, keys stored, table entries (16 B each), nodes without a table, build ms */
 int rm_engine_ball_stats(const rm_engine* e, int mode, double out[5]);
 /* Host-only check of the ball tables (no GPU): builds the balls of `mode` for the graph

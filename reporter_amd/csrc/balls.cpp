@@ -8,6 +8,7 @@
 #include "balls.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <chrono>
 #include <functional>
 #include <queue>
@@ -104,6 +105,29 @@ void parallel_nodes(uint32_t n, int threads, F&& f) {
 
 }  // namespace
 
+uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes) {
+  const uint32_t N = g.num_nodes();
+  if (N < 2) return 40000u;
+  float lo0 = g.node_lon[0], lo1 = lo0, la0 = g.node_lat[0], la1 = la0;
+  for (uint32_t n = 1; n < N; ++n) {
+    lo0 = std::min(lo0, g.node_lon[n]); lo1 = std::max(lo1, g.node_lon[n]);
+    la0 = std::min(la0, g.node_lat[n]); la1 = std::max(la1, g.node_lat[n]);
+  }
+  const double mid = 0.5 * ((double)la0 + (double)la1) * 3.14159265358979323846 / 180.0;
+  const double w = std::max(1.0, ((double)lo1 - lo0) * 111320.0 * std::cos(mid));
+  const double h = std::max(1.0, ((double)la1 - la0) * 110567.0);
+  const double rho = (double)N / (w * h);                                 // nodes per m^2
+  const double roads_per_node = 1.3 * (double)g.num_roads() / (double)N;  // + roads crossing the rim
+  for (const uint32_t r : {200000u, 150000u, 100000u, 70000u, 50000u}) {
+    const double rm = r / 100.0;
+    const double nodes = std::min((double)N, rho * 3.14159265358979323846 * rm * rm);
+    const double rows = std::max(1.0, nodes * roads_per_node);
+    const double table = (double)(1ull << table_bits((uint64_t)rows));
+    if (nodes <= kBallMaxKeysHost && (double)N * table * 16.0 <= (double)budget_bytes) return r;
+  }
+  return 40000u;
+}
+
 void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys, int threads, BallTables& out) {
   const auto t0 = std::chrono::steady_clock::now();
   const uint32_t N = g.num_nodes(), E = g.num_edges();
@@ -114,7 +138,7 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
     const bool ok = (edge_access(r.info) & acc) != 0u;
     ek[e] = {r.target, ok ? make_key(r.len_cm, time_ms(r.len_cm, mode_speed_dkph(mode, edge_speed_dkph(r.info)))) : kKeyInf};
   }
-  if (radius_cm > kBallMaxRadiusCm) throw std::runtime_error("ball radius above 655 m (16-bit distances)");
+  if (radius_cm > kBallMaxRadiusCm) throw std::runtime_error("ball radius above 10 km");
   // node -> incident roads
   const uint32_t R = g.num_roads();
   std::vector<uint32_t> inc_off(N + 1, 0), inc;
@@ -141,6 +165,8 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
   std::vector<uint32_t> bits(N, 0);
   parallel_nodes(N, threads, [&](int t, uint32_t u) {
     if (!scr[t].run(g, ek, u, radius_cm, max_keys)) { bits[u] = 0; return; }
+    for (const auto& kv : scr[t].out)
+      if (!ball_key_fits(kv.second)) { bits[u] = 0; return; }
     acc_r[t].collect(g, inc_off, inc, scr[t].out);
     bits[u] = acc_r[t].roads.size() > 2 * (size_t)max_keys ? 0u : table_bits(acc_r[t].roads.size());
   });
@@ -168,11 +194,8 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
     for (size_t q = 0; q < ra.roads.size(); ++q) {
       uint32_t s = ball_slot(ra.roads[q], b);
       while (tab[4 * s] != kNone) s = (s + 1) & mask;
-      const uint64_t a = ra.k0[q], c = ra.k1[q];
       tab[4 * s] = ra.roads[q];
-      tab[4 * s + 1] = (a == kKeyInf ? kBallNoDist : key_dist(a)) | ((c == kKeyInf ? kBallNoDist : key_dist(c)) << 16);
-      tab[4 * s + 2] = a == kKeyInf ? 0u : key_time(a);
-      tab[4 * s + 3] = c == kKeyInf ? 0u : key_time(c);
+      ball_pack(ra.k0[q], ra.k1[q], tab[4 * s + 1], tab[4 * s + 2], tab[4 * s + 3]);
     }
     keys[t] += ra.roads.size();
   });

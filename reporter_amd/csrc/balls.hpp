@@ -23,8 +23,8 @@ namespace rm {
 
 struct BallTables {
   std::vector<uint32_t> hdr;   // 2 per node: first entry, log2(table size) (0: no table, node's ball too big)
-  std::vector<uint32_t> ent;   // 4 per row: road (kNone when free), dist0 | dist1 << 16 (cm, 0xffff: endpoint
-                               // outside the ball), time0 ms, time1 ms (to the road's node0 / node1)
+  std::vector<uint32_t> ent;   // 4 per row: road (kNone when free) and the keys to the road's node0 / node1
+                               // (24-bit cm distances and ms times, rm_common.hpp ball_pack)
   uint32_t radius_cm = 0;
   uint64_t n_keys = 0;         // (node, road) rows stored
   uint32_t n_skipped = 0;      // nodes whose ball exceeded max_keys (their searches use the search tiers)
@@ -33,10 +33,16 @@ struct BallTables {
 
 // Balls of `mode` with radius `radius_cm` (keys with distance <= radius are kept),
 // tables sized to the next power of two >= 2 x keys; nodes with more than `max_keys`
-// keys get no table.  `threads` host threads.
+// keys, or a key beyond the row's 24-bit fields, get no table.  `threads` host threads.
 constexpr uint32_t kBallMaxKeysHost = 4096;   // ball nodes above which a node gets no table
-constexpr uint32_t kBallMaxRadiusCm = 65534;   // distances are stored in 16 bits
-constexpr uint32_t kBallNoDist = 0xffffu;
+constexpr uint32_t kBallMaxRadiusCm = 1000000;   // 10 km knob cap (rows hold 24-bit distances)
+
+// Default radius for a graph: the largest of {2000 (meili's default breakage distance, so
+// every default-bounded transition is a table probe), 1500, 1000, 700, 500} m whose
+// estimated tables (from the graph's node density) stay within `budget_bytes` per mode;
+// 400 m when none does.
+constexpr uint64_t kBallAutoBudget = 16ull << 30;
+uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes = kBallAutoBudget);
 
 void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys, int threads, BallTables& out);
 

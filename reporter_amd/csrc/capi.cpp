@@ -386,12 +386,12 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
     bool coalesce = true;
     double window_ms = 0.0;
     size_t max_traces = 16384;
-    double ball_radius_m = -1.0;   // < 0: engine default (400 m or RM_BALL_RADIUS_M)
+    double ball_radius_m = -1.0;   // < 0: engine default (automatic from the graph's density, or RM_BALL_RADIUS_M)
     if (const json::Value* ra = v.get("reporter_amd")) {
       if (const json::Value* br = ra->get("ball_radius"); br && br->is_num()) {
         ball_radius_m = br->num;
         if (!(ball_radius_m >= 0.0) || ball_radius_m * 100.0 > kBallMaxRadiusCm)
-          throw std::runtime_error("reporter_amd.ball_radius out of range (0..655.34 m)");
+          throw std::runtime_error("reporter_amd.ball_radius out of range (0..10000 m)");
       }
       if (const json::Value* c = ra->get("coalesce"); c && c->type == json::Value::Bool) coalesce = c->b;
       if (const json::Value* w = ra->get("coalesce_window_ms"); w && w->is_num()) window_ms = w->num;
@@ -554,7 +554,7 @@ int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids) {
 
 int rm_engine_set_ball_radius(rm_engine* e, double radius_m) {
   return guarded([&] {
-    if (!(radius_m >= 0.0) || radius_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..655.34 m)");
+    if (!(radius_m >= 0.0) || radius_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..10000 m)");
     e->e->set_ball_radius((uint32_t)(radius_m * 100.0));
   });
 }
@@ -566,11 +566,18 @@ int rm_engine_ball_stats(const rm_engine* e, int mode, double out[5]) {
   });
 }
 
+int rm_graph_auto_ball_radius(const char* graph_path, double* radius_m) {
+  return guarded([&] {
+    if (!radius_m) throw std::runtime_error("radius_m is NULL");
+    *radius_m = auto_ball_radius_cm(Graph::load(graph_path)) / 100.0;
+  });
+}
+
 int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t n, const uint32_t* from,
                     const uint32_t* road, uint64_t* keys) {
   return guarded([&] {
     if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
-    if (!(radius_m >= 0.0) || radius_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..655.34 m)");
+    if (!(radius_m >= 0.0) || radius_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..10000 m)");
     Graph g = Graph::load(graph_path);
     BallTables bt;
     build_balls(g, mode, (uint32_t)(radius_m * 100.0), kBallMaxKeysHost, 4, bt);
@@ -584,9 +591,8 @@ int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t 
         const uint32_t* e = bt.ent.data() + 4 * ((size_t)off + s);
         if (e[0] == kNone) break;
         if (e[0] != road[i]) continue;
-        const uint32_t d0 = e[1] & 0xffffu, d1 = e[1] >> 16;
-        if (d0 != kBallNoDist) keys[2 * i] = make_key(d0, e[2]);
-        if (d1 != kBallNoDist) keys[2 * i + 1] = make_key(d1, e[3]);
+        keys[2 * i] = ball_key0(e[0], e[1], e[3]);
+        keys[2 * i + 1] = ball_key1(e[0], e[2], e[3]);
         break;
       }
     }

@@ -847,18 +847,12 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t i, uint32_t n) {
 }
 
 __device__ __forceinline__ uint4 ball_first(const uint4* ent, const uint2& h, uint32_t road, bool use) {
-  return use ? ent[h.x + ball_slot(road, h.y)] : make_uint4(kNone, kBallNoDist * 0x10001u, 0u, 0u);
+  return use ? ent[h.x + ball_slot(road, h.y)] : make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
 }
 
 // keys from a row (kKeyInf for an endpoint outside the ball or a road not in the table)
-__device__ __forceinline__ unsigned long long row_key0(const uint4& e) {
-  const uint32_t d = e.y & 0xffffu;
-  return (e.x == kNone || d == kBallNoDist) ? kKeyInf : make_key(d, e.z);
-}
-__device__ __forceinline__ unsigned long long row_key1(const uint4& e) {
-  const uint32_t d = e.y >> 16;
-  return (e.x == kNone || d == kBallNoDist) ? kKeyInf : make_key(d, e.w);
-}
+__device__ __forceinline__ unsigned long long row_key0(const uint4& e) { return ball_key0(e.x, e.y, e.w); }
+__device__ __forceinline__ unsigned long long row_key1(const uint4& e) { return ball_key1(e.x, e.z, e.w); }
 
 __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1, unsigned long long d1,
                                                          unsigned long long rk0, unsigned long long d0) {
@@ -1951,6 +1945,7 @@ T* upload(std::vector<void*>& list, const std::vector<T>& v) {
 
 Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   RM_HIP(hipSetDevice(device));
+  ball_radius_cm_ = auto_ball_radius_cm(g);
   if (const char* r = std::getenv("RM_BALL_RADIUS_M"))
     ball_radius_cm_ = (uint32_t)std::min((double)kBallMaxRadiusCm, std::max(0.0, std::atof(r)) * 100.0);
   if (g.num_nodes() >= (1u << 28)) throw std::runtime_error("graph has too many nodes (limit 2^28)");

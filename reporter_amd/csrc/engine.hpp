@@ -298,7 +298,7 @@ class Engine {
   DevGraph dg_{};
   std::vector<void*> allocs_;
   mutable std::mutex ball_mu_;
-  uint32_t ball_radius_cm_ = 40000;
+  uint32_t ball_radius_cm_ = 40000;   // set from auto_ball_radius_cm(graph) at construction
   uint32_t ball_built_ = 0;             // mode bits
   double ball_info_[5][4] = {};
 };

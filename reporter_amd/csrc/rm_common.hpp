@@ -112,6 +112,33 @@ constexpr uint64_t kKeyInf = ~0ull;
 // home slot of node v in a route-ball table of 2^bits entries (balls.hpp; bits >= 1)
 RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) { return (v * 2654435761u) >> (32u - bits); }
 
+// Route-ball row (balls.hpp), 16 bytes: the keys from the table's node to both endpoints
+// of road x, as 24-bit cm distances and 24-bit ms times split over the words:
+//   x = road (kNone: free slot)
+//   y = d0 | t0[7:0] << 24      z = d1 | t1[7:0] << 24      w = t0[23:8] | t1[23:8] << 16
+// d = kBallNoDist: that endpoint is outside the ball.  24 bits hold 167 km / 4.6 h, so any
+// radius up to the breakage distance fits in one row (the build gives a node no table when
+// a key does not fit).
+constexpr uint32_t kBallNoDist = 0xffffffu;
+constexpr uint32_t kBallMaxField = 0xfffffeu;   // largest storable distance / time
+RM_HD uint64_t ball_key0(uint32_t x, uint32_t y, uint32_t w) {
+  const uint32_t d = y & 0xffffffu;
+  return (x == 0xffffffffu || d == kBallNoDist) ? ~0ull : make_key(d, (y >> 24) | ((w & 0xffffu) << 8));
+}
+RM_HD uint64_t ball_key1(uint32_t x, uint32_t z, uint32_t w) {
+  const uint32_t d = z & 0xffffffu;
+  return (x == 0xffffffffu || d == kBallNoDist) ? ~0ull : make_key(d, (z >> 24) | ((w >> 16) << 8));
+}
+// pack the keys k0 / k1 (kKeyInf: outside) of one row; both fit (callers check ball_key_fits)
+RM_HD void ball_pack(uint64_t k0, uint64_t k1, uint32_t& y, uint32_t& z, uint32_t& w) {
+  const uint32_t d0 = k0 == ~0ull ? kBallNoDist : key_dist(k0), t0 = k0 == ~0ull ? 0u : key_time(k0);
+  const uint32_t d1 = k1 == ~0ull ? kBallNoDist : key_dist(k1), t1 = k1 == ~0ull ? 0u : key_time(k1);
+  y = d0 | (t0 & 0xffu) << 24;
+  z = d1 | (t1 & 0xffu) << 24;
+  w = (t0 >> 8) | (t1 >> 8) << 16;
+}
+RM_HD bool ball_key_fits(uint64_t k) { return key_dist(k) <= kBallMaxField && key_time(k) <= kBallMaxField; }
+
 // ---- matcher limits ----
 constexpr int kMaxCand = 16;            // K: candidates kept per state (nearest first)
 constexpr float kMaxSearchRadius = 200.f;

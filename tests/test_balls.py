@@ -62,7 +62,7 @@ def _lookup(path, mode, radius_m, fr, road):
     return out.reshape(-1, 2)
 
 
-@pytest.mark.parametrize("mode,radius_m", [(0, 400.0), (0, 150.0), (3, 400.0), (4, 250.0), (0, 655.0)])
+@pytest.mark.parametrize("mode,radius_m", [(0, 400.0), (0, 150.0), (3, 400.0), (4, 250.0), (0, 655.0), (0, 2000.0), (4, 2000.0)])
 def test_ball_rows_match_dijkstra(small_world, mode, radius_m):
     """Row of road r in the table of node u = keys from u to r's node0 and node1."""
     g = graphfile.load(small_world)
@@ -91,11 +91,26 @@ def test_ball_radius_zero_keeps_only_self(small_world):
     assert list(got[0]) == [0, KEY_INF] and list(got[1]) == [KEY_INF, 0]
 
 
+def test_auto_radius_covers_default_breakage(small_world, tmpdir_session):
+    """A city graph gets 2000 m balls (meili's default breakage distance: every default
+    bound is a probe); a graph too large for 16 GiB tables per mode gets a smaller radius."""
+    import ctypes
+    r = ctypes.c_double()
+    _lib.check(_lib.lib().rm_graph_auto_ball_radius(os.fsencode(small_world), ctypes.byref(r)))
+    assert r.value == 2000.0
+    from reporter_amd import world
+    big = str(tmpdir_session / "auto_r_big.rmg")
+    world.build_world(big, 1400, 1400, 250.0, seed=2, cell_m=250.0)   # 2 M nodes
+    _lib.check(_lib.lib().rm_graph_auto_ball_radius(os.fsencode(big), ctypes.byref(r)))
+    assert 400.0 <= r.value < 2000.0
+    assert _lib.lib().rm_graph_auto_ball_radius(b"/nonexistent.rmg", ctypes.byref(r)) != 0
+
+
 def test_ball_lookup_errors(small_world):
     one = np.zeros(1, np.uint32)
     out = np.zeros(2, np.uint64)
     L = _lib.lib()
     assert L.rm_balls_lookup(os.fsencode(small_world), 9, 100.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
-    assert L.rm_balls_lookup(os.fsencode(small_world), 0, 700.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
+    assert L.rm_balls_lookup(os.fsencode(small_world), 0, 20000.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
     big = np.array([10 ** 9], np.uint32)
     assert L.rm_balls_lookup(os.fsencode(small_world), 0, 100.0, 1, big.ctypes.data, one.ctypes.data, out.ctypes.data) != 0

@@ -28,9 +28,11 @@ def _world(tmpdir_session, name, rows=None, cols=None):
     return path, cfg
 
 
-def _match_and_compare(path, tr, opts, trace_opt, rl=(0, 1), tl=(0, 1), hist=False):
+def _match_and_compare(path, tr, opts, trace_opt, rl=(0, 1), tl=(0, 1), hist=False, ball_radius=None):
     g = graphfile.load(path)
     eng = engine.Engine(path, 0)
+    if ball_radius is not None:
+        eng.set_ball_radius(ball_radius)
     T = len(tr["trace_off"]) - 1
     if trace_opt is None:
         trace_opt = np.zeros(T, np.uint32)
@@ -62,6 +64,7 @@ def _match_and_compare(path, tr, opts, trace_opt, rl=(0, 1), tl=(0, 1), hist=Fal
         c["valid_reports"] = nvalid
     c["traces"] = T
     c["route_tiers"] = bm.route_tiers()
+    c["ball_stats"] = eng.ball_stats(0)
     bm.close()
     eng.close()
     return c
@@ -78,13 +81,16 @@ def test_c2_full_bench_workload(built_lib, tmpdir_session):
     print("C2 full parity", c)
 
 
-def test_c3_full_graph_sample(built_lib, tmpdir_session):
-    """C3 graph (500x500 @200 m), 30 s sampling, radius 100 m: searches beyond the ball radius."""
+@pytest.mark.parametrize("ball_radius", [400.0, 2000.0])
+def test_c3_full_graph_sample(built_lib, tmpdir_session, ball_radius):
+    """C3 graph (500x500 @200 m), 30 s sampling, radius 100 m: route bounds up to the 2 km
+    breakage distance, answered by the search tiers (400 m balls) or by the ball tier (2 km)."""
     path, cfg = _world(tmpdir_session, "C3")
     tr = world.generate_traces(path, 1500, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=3000)
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
-    c = _match_and_compare(path, tr, opts, None, hist=True)
+    c = _match_and_compare(path, tr, opts, None, hist=True, ball_radius=ball_radius)
     assert c["chained"] > 40_000, c
+    assert (c["route_tiers"]["ball_to_search"] == 0) == (ball_radius >= 2000.0), c
     print("C3 sample parity", c)
 
 
@@ -93,7 +99,7 @@ def test_c4_country_slice_sample(built_lib, tmpdir_session):
     path, cfg = _world(tmpdir_session, "C4", rows=1000, cols=1000)
     tr = world.generate_traces(path, 2000, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=4000)
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
-    c = _match_and_compare(path, tr, opts, None, hist=True)
+    c = _match_and_compare(path, tr, opts, None, hist=True, ball_radius=cfg["ball_radius_m"])
     assert c["segments"] > 20_000, c
     print("C4 slice parity", c)
 

@@ -89,7 +89,7 @@ def coalesce_stats():
 def write_config(path, graph_path, device=0, coalesce=True, coalesce_window_ms=0.0, ball_radius=None,
                  **meili_default):
     """Write a Valhalla-style config naming the engine's graph file (ball_radius: route-ball radius
-    in metres, 0..655.34, None = engine default)."""
+    in metres, 0..10000, None = engine default)."""
     conf = {"meili": {"default": dict(meili_default)},
             "reporter_amd": {"graph": _os.path.abspath(graph_path), "device": int(device), "coalesce": bool(coalesce),
                              "coalesce_window_ms": float(coalesce_window_ms)}}
