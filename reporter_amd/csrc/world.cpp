@@ -376,6 +376,31 @@ struct RoutePlanner {
     return (uint32_t)(0.95 * d * 36000.0 / (double)vmax_dkph);
   }
 
+  // a uniform draw among the nodes whose straight-line distance from `from` is in
+  // [lo_m, hi_m], found by a breadth-first walk that stops at hi_m (kNone when empty)
+  uint32_t ring_node(uint32_t from, double lo_m, double hi_m, Rng& r) {
+    if (++gen == 0) {
+      std::fill(stamp.begin(), stamp.end(), 0u);
+      std::fill(done.begin(), done.end(), 0u);
+      gen = 1;
+    }
+    std::vector<uint32_t> q{from}, hits;
+    stamp[from] = gen;
+    for (size_t h = 0; h < q.size() && q.size() < 400000; ++h) {
+      const uint32_t u = q[h];
+      for (uint32_t e = g.node_off[u]; e < g.node_off[u + 1]; ++e) {
+        const uint32_t v = g.edges[e].target;
+        if (stamp[v] == gen) continue;
+        stamp[v] = gen;
+        const double d = piece_m(g.node_lon[from], g.node_lat[from], g.node_lon[v], g.node_lat[v]);
+        if (d > hi_m) continue;
+        q.push_back(v);
+        if (d >= lo_m) hits.push_back(v);
+      }
+    }
+    return hits.empty() ? kNone : hits[r.below((uint32_t)hits.size())];
+  }
+
   // edges of the fastest route src -> dst whose first edge is not on road `avoid_road`
   bool plan(uint32_t src, uint32_t avoid_road, uint32_t dst, std::vector<uint32_t>& out) {
     out.clear();
@@ -429,7 +454,7 @@ struct RoutePlanner {
 };
 
 // random destination node at a driving distance that fits the rest of the trace
-uint32_t pick_destination(const Graph& g, Rng& r, uint32_t from, double remaining_s) {
+uint32_t pick_destination(const Graph& g, Rng& r, uint32_t from, double remaining_s, RoutePlanner& planner) {
   const double want = std::min(6000.0, std::max(400.0, remaining_s * 12.0));
   uint32_t best = kNone;
   double best_err = 1e300;
@@ -439,9 +464,13 @@ uint32_t pick_destination(const Graph& g, Rng& r, uint32_t from, double remainin
     const double d = piece_m(g.node_lon[from], g.node_lat[from], g.node_lon[n], g.node_lat[n]);
     const double err = std::fabs(d - want);
     if (err < best_err) { best_err = err; best = n; }
-    if (d >= 0.5 * want && d <= 1.5 * want) break;
+    if (d >= 0.5 * want && d <= 1.5 * want) return n;
   }
-  return best;
+  // graphs much wider than the trace's reach (C4 country scale): uniform draws miss the
+  // distance window, and the nearest miss may be hundreds of km away (an A* to it would
+  // settle the planner's whole cap).  Draw from the ring of nodes around `from` instead.
+  const uint32_t ring = planner.ring_node(from, 0.5 * want, 1.5 * want, r);
+  return ring != kNone ? ring : best;
 }
 
 void gen_one(const Graph& g, const TraceParams& p, uint32_t k, TraceSet& ts, const std::vector<uint32_t>& starts,
@@ -476,7 +505,7 @@ void gen_one(const Graph& g, const TraceParams& p, uint32_t k, TraceSet& ts, con
       if (ri >= route.size()) {
         route.clear();
         ri = 0;
-        const uint32_t dst = pick_destination(g, r, node, t_total - t_now);
+        const uint32_t dst = pick_destination(g, r, node, t_total - t_now, planner);
         if (dst != kNone) planner.plan(node, road, dst, route);
       }
       if (ri < route.size()) { e = route[ri++]; off_m = 0.0; continue; }
