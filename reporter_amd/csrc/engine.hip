@@ -812,15 +812,10 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
 // ------------------------------------------------------------------------------------------
 // K2 ball tier (balls.hpp): when the pair's bound fits in the mode's ball radius, the
 // source's bounded search is replaced by table probes: label(v) = min over the exits x of
-// rk_x + key(x -> v).  The first probe of every (exit, entry node) lookup of four targets
-// is issued together (4 independent 16-byte loads per target in flight per lane); collisions
+// rk_x + key(x -> v).  Both exits' first probes of a target are issued together; collisions
 // continue by linear probing (tables are at most half full, so an empty slot ends it).
 // A table is keyed by road, so one probe per exit gives the labels of both entry nodes.
 constexpr uint32_t kBallMaxKeys = kBallMaxKeysHost;
-#ifndef RM_BALL_BATCH
-#define RM_BALL_BATCH 1
-#endif
-constexpr int kBallBatch = RM_BALL_BATCH;   // targets whose first probes are issued together
 
 // row of `road` in a node's table (balls.hpp), continuing the probe from first-probe row e
 __device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, uint32_t road, uint4 e) {
@@ -865,59 +860,66 @@ __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1,
 #ifndef RM_BALL_WPE
 #define RM_BALL_WPE 4
 #endif
+// The items of a block are consecutive, so their routes form ONE contiguous range of
+// b.route: results are staged in LDS at their final offsets and the block writes the range
+// with coalesced stores (a lane-per-item store loop would touch ~10 lines per instruction).
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball(DevGraph g, DevBatch b, uint32_t n_items) {
-  const uint32_t t = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  if (t >= n_items) return;
-  const uint32_t p = b.src_item[t];
-  const uint4 pi = b.pair_info[p];
-  const uint32_t i = t - b.src_off[p];
-  const uint32_t base = b.trans_off[p];
-  const uint32_t bound = pi.x, tmax = pi.y, KB = (pi.z >> 8) & 0xffu;
-  const int mode = (int)(pi.z >> 16);
-  const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
-  const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
-  unsigned long long rk1, rk0;
-  exit_keys(a0, bound, rk1, rk0);
-  const uint4* ent = g.ball_ent[mode];
-  const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
-  const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
-  if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {   // search tiers take it
-    b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
-    return;
+  const uint32_t tb = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
+  const uint32_t t = tb + threadIdx.x;
+  const uint32_t tl = min(n_items, tb + blockDim.x) - 1u;   // last item of this block
+  __shared__ uint32_t s_out[256 * kMaxCand];
+  __shared__ uint32_t s_lo, s_hi;
+  const bool live = t <= tl;
+  uint32_t p = 0, i = 0, KB = 0, base = 0;
+  uint4 pi = make_uint4(0u, 0u, 0u, 0u);
+  if (live) {
+    p = b.src_item[t];
+    pi = b.pair_info[p];
+    i = t - b.src_off[p];
+    base = b.trans_off[p];
+    KB = (pi.z >> 8) & 0xffu;
   }
-  const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
-  __shared__ uint32_t s_res[kMaxCand][256];
-  uint32_t* res = &s_res[0][threadIdx.x];
-  const uint64_t brow = p * kMaxCand * 2;
-  for (uint32_t j0 = 0; j0 < KB; j0 += kBallBatch) {
-    uint4 t0[kBallBatch], t1[kBallBatch];
-#pragma unroll
-    for (int x = 0; x < kBallBatch; ++x) {
-      const uint32_t jc = min(j0 + x, KB - 1u);
-      t0[x] = b.cand_desc[brow + 2 * jc];
-      t1[x] = b.cand_desc[brow + 2 * jc + 1];
-    }
-    uint4 e1[kBallBatch], e0[kBallBatch];   // first probes of the target road in both exits' tables
-#pragma unroll
-    for (int x = 0; x < kBallBatch; ++x) {
-      const bool any = t0[x].w != 0u;   // some direction of the target road is usable
-      e1[x] = ball_first(ent, h1, t0[x].x, u1 && any);
-      e0[x] = ball_first(ent, h0, t0[x].x, u0 && any);
-    }
-#pragma unroll
-    for (int x = 0; x < kBallBatch; ++x) {
-      const uint4 r1 = ball_resolve(ent, h1, t0[x].x, e1[x]);
-      const uint4 r0 = ball_resolve(ent, h0, t0[x].x, e0[x]);
-      const unsigned long long lab0 = ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
-      const unsigned long long lab1 = ball_label(rk1, row_key1(r1), rk0, row_key1(r0));
-      const unsigned long long key = route_key_vals(a0, t0[x], t1[x], lab0, lab1, nullptr);
-      uint32_t rt = kRouteInvalid;
-      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = key_dist(key);
-      res[((j0 + x) & (kMaxCand - 1)) * 256] = rt;
+  const uint32_t ob = base + i * KB;
+  if (t == tb) s_lo = ob;
+  if (t == tl) s_hi = ob + KB;
+  __syncthreads();
+  if (live) {
+    uint32_t* res = s_out + (ob - s_lo);
+    const uint32_t bound = pi.x, tmax = pi.y;
+    const int mode = (int)(pi.z >> 16);
+    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+    unsigned long long rk1, rk0;
+    exit_keys(a0, bound, rk1, rk0);
+    const uint4* ent = g.ball_ent[mode];
+    const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
+    const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+    if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {   // search tiers take it (they run later)
+      for (uint32_t j = 0; j < KB; ++j) res[j] = kRouteInvalid;
+      b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+    } else {
+      const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
+      const uint64_t brow = p * kMaxCand * 2;
+      for (uint32_t j = 0; j < KB; ++j) {
+        const uint4 t0 = b.cand_desc[brow + 2 * j], t1 = b.cand_desc[brow + 2 * j + 1];
+        const bool any = t0.w != 0u;   // some direction of the target road is usable
+        // first probes of the target road in both exits' tables, then their chains
+        const uint4 e1 = ball_first(ent, h1, t0.x, u1 && any);
+        const uint4 e0 = ball_first(ent, h0, t0.x, u0 && any);
+        const uint4 r1 = ball_resolve(ent, h1, t0.x, e1);
+        const uint4 r0 = ball_resolve(ent, h0, t0.x, e0);
+        const unsigned long long lab0 = ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
+        const unsigned long long lab1 = ball_label(rk1, row_key1(r1), rk0, row_key1(r0));
+        const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, nullptr);
+        uint32_t rt = kRouteInvalid;
+        if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = key_dist(key);
+        res[j] = rt;
+      }
     }
   }
-  const uint64_t ob = (uint64_t)base + i * KB;
-  for (uint32_t j = 0; j < KB; ++j) b.route[ob + j] = res[j * 256];
+  __syncthreads();
+  const uint32_t lo = s_lo, n = s_hi - s_lo;
+  for (uint32_t q = threadIdx.x; q < n; q += blockDim.x) b.route[lo + q] = s_out[q];
 }
 
 // K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
