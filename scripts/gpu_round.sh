@@ -19,4 +19,6 @@ cd $R
 python scripts/pmc_summary.py $O $O/summary --config C2 --traces 10000 > $O/summary.log 2>&1 || { echo "summary failed"; exit 1; }
 timeout -k 10 300 python -u bench.py --traffic-json $O/summary/pmc_routes_c2.json > $O/bench.json 2> $O/bench.err || { echo "bench failed"; exit 1; }
 cat $O/bench.json
+timeout -k 10 600 python -u bench.py --config C3 --traces 125000 --steps 5 --warmup 1 > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench C3 failed"; exit 1; }
+timeout -k 10 900 python -u bench.py --config C4 --traces 125000 --steps 3 --warmup 1 > $O/bench_c4.json 2> $O/bench_c4.err || { echo "bench C4 failed"; exit 1; }
 echo ALLDONE
