@@ -72,3 +72,22 @@ def test_traces_deterministic_and_noisy(small_world):
         dx = np.sign(a["lon"][k * 100:(k + 1) * 100] - c["lon"][k * 100:(k + 1) * 100])
         dy = np.sign(a["lat"][k * 100:(k + 1) * 100] - c["lat"][k * 100:(k + 1) * 100])
         assert (np.mean(dx == dx[0]) > 0.9) and (np.mean(dy == dy[0]) > 0.9)
+
+
+def test_traces_on_a_graph_wider_than_their_reach(built_lib, tmp_path):
+    """Country-scale worlds (C4): uniform destination draws miss the trace's reach, so the
+    generator draws from the ring around the vehicle (world.cpp pick_destination) —
+    generation stays fast and the vehicles still drive routed (far-travelling) paths."""
+    import time
+    path = str(tmp_path / "wide.rmg")
+    world.build_world(path, 40, 1200, 250.0, seed=4, cell_m=250.0)   # 10 km x 300 km
+    t = time.time()
+    tr = world.generate_traces(path, 100, 120, rate_s=5.0, noise_m=1e-9, seed=8)
+    assert time.time() - t < 30.0
+    lon = tr["lon"].reshape(100, 120)
+    lat = tr["lat"].reshape(100, 120)
+    mx = 111320.0 * np.cos(np.radians(lat.mean()))
+    step = np.hypot(np.diff(lon, axis=1) * mx, np.diff(lat, axis=1) * 110567.0)
+    assert step.max() < 5.0 * 90 / 3.6 + 1.0                       # never faster than 90 km/h
+    net = np.hypot((lon[:, -1] - lon[:, 0]) * mx, (lat[:, -1] - lat[:, 0]) * 110567.0)
+    assert np.median(net) > 0.3 * np.median(step.sum(axis=1))       # routed, not a random walk
