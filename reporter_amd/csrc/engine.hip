@@ -926,9 +926,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
 // one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A search
 // that outgrows the registers is queued (as its item) for the LDS lane tier.
 // With `listed`, thread q takes the q-th item the ball tier handed over (rl_routes_0, ctl[1]).
+constexpr uint64_t kListedGrid = 4096;   // blocks of a grid-stride launch over hand-over lists
+
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items, int listed) {
-  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= (listed ? b.ctl[1] : n_items)) return;
+  // grid-stride: a listed launch is sized for every item but usually finds few hand-overs
+  const uint32_t n = listed ? b.ctl[1] : n_items;
+  __shared__ uint32_t s_res[kMaxCand][256];
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
   const uint32_t t = listed ? b.rl_routes_0[q] : q;
   const uint32_t p = b.src_item[t];
   const uint4 pi = b.pair_info[p];
@@ -943,10 +947,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
   lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
   if (S.ovf) {
     b.rl_routes_a[atomicAdd(&b.ctl[3], 1u)] = t;
-    return;
+    continue;
   }
-  __shared__ uint32_t s_res[kMaxCand][256];
   route_targets(b, StoreLabel<RegLabels>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256);
+  }
 }
 
 #ifdef RM_ALL_LDS
@@ -1185,9 +1189,13 @@ __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_paths_lane(DevGraph g, DevBatch b, int listed) {
   const uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t p = q0;
-  if (listed) {
-    if (q0 >= b.ctl[8]) return;
-    p = b.rl_routes_0[q0];
+  if (listed) {   // grid-stride over the ball tier's hand-overs
+    const uint32_t n = b.ctl[8];
+    for (uint64_t q = q0; q < n; q += (uint64_t)gridDim.x * blockDim.x) {
+      RegLabels S;
+      if (!lane_path(g, b, b.rl_routes_0[q], S, kLaneCap)) b.rl_paths_a[atomicAdd(&b.ctl[4], 1u)] = b.rl_routes_0[q];
+    }
+    return;
   } else {
     if (p >= b.P) return;
     const uint32_t k = b.slot_trace[p];
@@ -2355,7 +2363,8 @@ void Matcher::run_device(const RunParams& rp) {
 #else
   if (n_src && balls) {
     hipLaunchKernelGGL(k_routes_ball, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
-    hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, 0u, 1);
+    hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)), dim3(256), 0,
+                       st, g, v, 0u, 1);
   } else if (n_src) {
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
   }
@@ -2375,7 +2384,8 @@ void Matcher::run_device(const RunParams& rp) {
     if (balls) {
       RM_HIP(hipMemsetAsync(w.ctl + 8, 0, sizeof(uint32_t), st));
       hipLaunchKernelGGL(k_paths_ball, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
-      hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 1);
+      hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>((P + 255) / 256, kListedGrid)), dim3(256), 0,
+                         st, g, v, 1);
     } else {
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 0);
     }
