@@ -1672,9 +1672,13 @@ __device__ __forceinline__ double interp_time(double ta, double tb, uint64_t x, 
   return ta + (tb - ta) * ((double)x / (double)D);
 }
 
-__global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
-  const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= b.P) return;
+// The records of a block's 256 slots are one contiguous range of trav (trav_off is a scan in
+// slot order): the first kTravStage of them are staged in LDS and written by the whole block
+// with coalesced 16-byte stores; records past the stage (long paths) are stored by their lane.
+constexpr uint32_t kTravStage = 512;
+
+__device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch& b, uint64_t l, uint32_t base,
+                                               uint4* s_rec) {
   const uint32_t ns = b.path_cnt[l];
   if (ns == 0) return;  // not a chosen transition
   const uint32_t k = b.slot_trace[l];
@@ -1685,7 +1689,8 @@ __global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
   const double ta = b.time[o + oa], tb = b.time[o + ob];
   const uint32_t D = b.route_dist[l];
   const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
-  TravRec* out = b.trav + b.trav_off[l];
+  const uint32_t r0 = b.trav_off[l];
+  TravRec* out = b.trav + r0;
   uint64_t x = 0;
   // four path edges per group: every graph load of a group is issued before its record
   // stores (loads after a pending store wait for it: shared vmcnt)
@@ -1727,9 +1732,30 @@ __global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
       t.way = way[y];
       t.internal = (rec[y].z & kFlagInternal) ? 1u : 0u;
       t.seg_len = sd[y] != kNone ? sl[y] : 0u;
-      out[q] = t;
+      const uint32_t si = r0 + q - base;
+      if (si < kTravStage) {
+        const uint4* tv = reinterpret_cast<const uint4*>(&t);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s_rec[si * 4 + c] = tv[c];
+      } else {
+        out[q] = t;
+      }
     }
   }
+}
+
+__global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
+  __shared__ uint4 s_rec[kTravStage * 4];
+  const uint64_t l0 = (uint64_t)blockIdx.x * blockDim.x;
+  const uint64_t l = l0 + threadIdx.x;
+  const uint64_t last = (l0 + blockDim.x < b.P ? l0 + blockDim.x : b.P) - 1;
+  const uint32_t base = b.trav_off[l0];
+  const uint32_t n_rec = b.trav_off[last] + b.path_cnt[last] - base;
+  if (l < b.P) traversal_lane(g, b, l, base, s_rec);
+  __syncthreads();
+  const uint32_t n_stage = n_rec < kTravStage ? n_rec : kTravStage;
+  uint4* dst = reinterpret_cast<uint4*>(b.trav + base);
+  for (uint32_t v = threadIdx.x; v < n_stage * 4; v += blockDim.x) dst[v] = s_rec[v];
 }
 
 // The meili merge / run rules only ever compare a record with the previous kept record
