@@ -1672,6 +1672,59 @@ __device__ __forceinline__ double interp_time(double ta, double tb, uint64_t x, 
   return ta + (tb - ta) * ((double)x / (double)D);
 }
 
+// The meili merge / run rules only ever compare a record with the previous kept record
+// of its chain, so run boundaries are local and K4 needs no per-trace serial loop:
+//   k_run_flags   one lane per record: kind (skip / new traversal / merged piece) and
+//                 run-head flag
+//   (scan)        exclusive sum of the head flags = each run's output index
+//   k_runs        one lane per run head: walks its run (a few records) and writes the
+//                 segment; one lane per trace records seg_base / seg_cnt
+enum : uint8_t { kRecSkip = 0, kRecNew = 1, kRecMerged = 2 };
+
+__device__ __forceinline__ bool same_chain(uint32_t slot_prev, uint32_t slot_next) {
+  // traversal records of a chain come from consecutive transition slots; traces are
+  // at least two slots apart, so this also separates traces
+  return slot_next == slot_prev || slot_next == slot_prev + 1;
+}
+
+// kind / head flag of record r (index into recs; the lookback stops at index 0)
+__device__ __forceinline__ void run_flag(const TravRec* recs, int64_t r, uint8_t& kind, uint32_t& head) {
+  const TravRec& t = recs[r];
+  const uint32_t tb = t.b, ten = t.en, tslot = t.slot;
+  kind = kRecSkip;
+  head = 0;
+  if (ten == tb) return;
+  // previous kept record of the same chain
+  int64_t p = r - 1;
+  uint32_t nslot = tslot;
+  bool has = false;
+  while (p >= 0) {
+    const uint32_t ps = recs[p].slot;
+    if (!same_chain(ps, nslot)) break;
+    if (recs[p].en != recs[p].b) { has = true; break; }
+    nslot = ps;
+    --p;
+  }
+  if (has) {
+    const TravRec& u = recs[p];
+    if (u.e == t.e && u.en == tb) {
+      kind = kRecMerged;
+    } else {
+      kind = kRecNew;
+      bool cont = u.sd == t.sd;
+      if (cont && t.sd == kNone && u.internal != t.internal) cont = false;
+      if (cont) {
+        if (u.en != u.len || tb != 0) cont = false;
+        else if (t.sd != kNone && t.soff != u.soff + u.len) cont = false;
+      }
+      head = cont ? 0u : 1u;
+    }
+  } else {
+    kind = kRecNew;
+    head = 1;
+  }
+}
+
 // The records of a block's 256 slots are one contiguous range of trav (trav_off is a scan in
 // slot order): the first kTravStage of them are staged in LDS and written by the whole block
 // with coalesced 16-byte stores; records past the stage (long paths) are stored by their lane.
@@ -1756,64 +1809,49 @@ __global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
   const uint32_t n_stage = n_rec < kTravStage ? n_rec : kTravStage;
   uint4* dst = reinterpret_cast<uint4*>(b.trav + base);
   for (uint32_t v = threadIdx.x; v < n_stage * 4; v += blockDim.x) dst[v] = s_rec[v];
-}
-
-// The meili merge / run rules only ever compare a record with the previous kept record
-// of its chain, so run boundaries are local and K4 needs no per-trace serial loop:
-//   k_run_flags   one lane per record: kind (skip / new traversal / merged piece) and
-//                 run-head flag
-//   (scan)        exclusive sum of the head flags = each run's output index
-//   k_runs        one lane per run head: walks its run (a few records) and writes the
-//                 segment; one lane per trace records seg_base / seg_cnt
-enum : uint8_t { kRecSkip = 0, kRecNew = 1, kRecMerged = 2 };
-
-__device__ __forceinline__ bool same_chain(uint32_t slot_prev, uint32_t slot_next) {
-  // traversal records of a chain come from consecutive transition slots; traces are
-  // at least two slots apart, so this also separates traces
-  return slot_next == slot_prev || slot_next == slot_prev + 1;
-}
-
-__global__ void __launch_bounds__(256) k_run_flags(DevBatch b, uint32_t total) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > total) return;
-  if (r == total) { b.run_head[r] = 0; return; }
-  const TravRec& t = b.trav[r];
-  const uint32_t tb = t.b, ten = t.en, tslot = t.slot;
-  uint8_t kind = kRecSkip;
-  uint32_t head = 0;
-  if (ten != tb) {
-    // previous kept record of the same chain
-    int64_t p = (int64_t)r - 1;
-    uint32_t nslot = tslot;
-    bool has = false;
-    while (p >= 0) {
-      const uint32_t ps = b.trav[p].slot;
-      if (!same_chain(ps, nslot)) break;
-      if (b.trav[p].en != b.trav[p].b) { has = true; break; }
-      nslot = ps;
-      --p;
-    }
-    if (has) {
-      const TravRec& u = b.trav[p];
-      if (u.e == t.e && u.en == tb) {
-        kind = kRecMerged;
-      } else {
-        kind = kRecNew;
-        bool cont = u.sd == t.sd;
-        if (cont && t.sd == kNone && u.internal != t.internal) cont = false;
-        if (cont) {
-          if (u.en != u.len || tb != 0) cont = false;
-          else if (t.sd != kNone && t.soff != u.soff + u.len) cont = false;
-        }
-        head = cont ? 0u : 1u;
-      }
-    } else {
-      kind = kRecNew;
-      head = 1;
+  // run flags of the staged block, looking back within the stage only (k_run_flags_fix
+  // redoes the prefix whose lookback crosses into the previous block)
+  if (n_rec <= kTravStage) {
+    const TravRec* st = reinterpret_cast<const TravRec*>(s_rec);
+    for (uint32_t r = threadIdx.x; r < n_rec; r += blockDim.x) {
+      uint8_t kind;
+      uint32_t head;
+      run_flag(st, r, kind, head);
+      b.run_kind[base + r] = kind;
+      b.run_head[base + r] = head;
     }
   }
-  b.run_kind[r] = kind;
-  b.run_head[r] = head;
+}
+
+// Flags of the records k_traversals could not decide from its LDS stage: the leading records
+// of a staged block whose lookback leaves the block (a prefix: kept record, or skipped
+// records continuing one chain), and every record of a block whose range outgrew the stage.
+// Runs after k_traversals, so it overwrites that kernel's block-local guesses.
+__global__ void __launch_bounds__(256) k_run_flags_fix(DevBatch b, uint32_t total) {
+  const uint64_t l0 = (uint64_t)blockIdx.x * blockDim.x;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) b.run_head[total] = 0;
+  const uint64_t last = (l0 + blockDim.x < b.P ? l0 + blockDim.x : b.P) - 1;
+  const uint32_t base = b.trav_off[l0];
+  const uint32_t end = b.trav_off[last] + b.path_cnt[last];
+  if (end - base > kTravStage) {
+    for (uint32_t r = base + threadIdx.x; r < end; r += blockDim.x) {
+      uint8_t kind;
+      uint32_t head;
+      run_flag(b.trav, r, kind, head);
+      b.run_kind[r] = kind;
+      b.run_head[r] = head;
+    }
+  } else if (threadIdx.x == 0 && base > 0) {
+    for (uint32_t r = base; r < end; ++r) {
+      uint8_t kind;
+      uint32_t head;
+      run_flag(b.trav, r, kind, head);
+      b.run_kind[r] = kind;
+      b.run_head[r] = head;
+      if (kind != kRecSkip) break;
+      if (r + 1 < end && !same_chain(b.trav[r].slot, b.trav[r + 1].slot)) break;
+    }
+  }
 }
 
 // scatter: run head record of every run, in run order (runs are contiguous in record order)
@@ -2452,7 +2490,7 @@ void Matcher::run_device(const RunParams& rp) {
   v.run_kind = w.run_kind; v.run_head = w.run_head; v.run_idx = w.run_idx; v.run_pos = w.run_pos;
   tic(kKSegments);
   hipLaunchKernelGGL(k_traversals, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_run_flags, dim3((uint32_t)((seg_total + 1 + 255) / 256)), dim3(256), 0, st, v, (uint32_t)seg_total);
+  hipLaunchKernelGGL(k_run_flags_fix, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v, (uint32_t)seg_total);
   tmp = w.seg_scan_tmp_bytes;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.seg_scan_tmp, tmp, w.run_head, w.run_idx, (int)(seg_total + 1), st));
   hipLaunchKernelGGL(k_run_heads, dim3((uint32_t)((seg_total + 255) / 256)), dim3(256), 0, st, v, (uint32_t)seg_total);
