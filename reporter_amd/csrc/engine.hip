@@ -1690,7 +1690,7 @@ __device__ __forceinline__ bool same_chain(uint32_t slot_prev, uint32_t slot_nex
 // kind / head flag of record r (index into recs; the lookback stops at index 0)
 __device__ __forceinline__ void run_flag(const TravRec* recs, int64_t r, uint8_t& kind, uint32_t& head) {
   const TravRec& t = recs[r];
-  const uint32_t tb = t.b, ten = t.en, tslot = t.slot;
+  const uint32_t tb = t.b, ten = t.en, tslot = t.slot & kTravSlotMask;
   kind = kRecSkip;
   head = 0;
   if (ten == tb) return;
@@ -1699,7 +1699,7 @@ __device__ __forceinline__ void run_flag(const TravRec* recs, int64_t r, uint8_t
   uint32_t nslot = tslot;
   bool has = false;
   while (p >= 0) {
-    const uint32_t ps = recs[p].slot;
+    const uint32_t ps = recs[p].slot & kTravSlotMask;
     if (!same_chain(ps, nslot)) break;
     if (recs[p].en != recs[p].b) { has = true; break; }
     nslot = ps;
@@ -1712,7 +1712,7 @@ __device__ __forceinline__ void run_flag(const TravRec* recs, int64_t r, uint8_t
     } else {
       kind = kRecNew;
       bool cont = u.sd == t.sd;
-      if (cont && t.sd == kNone && u.internal != t.internal) cont = false;
+      if (cont && t.sd == kNone && ((u.slot ^ t.slot) & kTravInternal)) cont = false;
       if (cont) {
         if (u.en != u.len || tb != 0) cont = false;
         else if (t.sd != kNone && t.soff != u.soff + u.len) cont = false;
@@ -1748,7 +1748,7 @@ __device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch
   // four path edges per group: every graph load of a group is issued before its record
   // stores (loads after a pending store wait for it: shared vmcnt)
   for (uint32_t q0 = 0; q0 < ns; q0 += 4) {
-    uint32_t e[4], sd[4], soff[4], way[4], sl[4];
+    uint32_t e[4], sd[4], soff[4], way[4];
     uint4 rec[4];
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
@@ -1762,8 +1762,6 @@ __device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch
       way[y] = g.edge_way[e[y]];
     }
 #pragma unroll
-    for (int y = 0; y < 4; ++y) sl[y] = g.seg_len[sd[y] != kNone ? sd[y] : 0u];
-#pragma unroll
     for (int y = 0; y < 4; ++y) {
       const uint32_t q = q0 + y;
       if (q >= ns) break;
@@ -1773,23 +1771,20 @@ __device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch
       if (q == 0) b0 = rev ? L - sa : sa;
       if (q + 1 == ns) b1 = rev ? L - sb : sb;
       TravRec t;
-      t.e = e[y]; t.b = b0; t.en = b1; t.slot = (uint32_t)l;
+      t.e = e[y]; t.b = b0; t.en = b1;
+      t.slot = (uint32_t)l | (q + 1 == ns ? kTravLast : 0u) | ((rec[y].z & kFlagInternal) ? kTravInternal : 0u);
       t.tb = interp_time(ta, tb, x, D);
       x += (uint64_t)(b1 - b0);
       t.te = interp_time(ta, tb, x, D);
-      t.sb = oa;
-      t.se = (q + 1 == ns) ? ob : oa;
       t.sd = sd[y];
       t.soff = soff[y];
       t.len = L;
       t.way = way[y];
-      t.internal = (rec[y].z & kFlagInternal) ? 1u : 0u;
-      t.seg_len = sd[y] != kNone ? sl[y] : 0u;
       const uint32_t si = r0 + q - base;
       if (si < kTravStage) {
         const uint4* tv = reinterpret_cast<const uint4*>(&t);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) s_rec[si * 4 + c] = tv[c];
+        for (int c = 0; c < 3; ++c) s_rec[si * 3 + c] = tv[c];
       } else {
         out[q] = t;
       }
@@ -1798,7 +1793,7 @@ __device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch
 }
 
 __global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
-  __shared__ uint4 s_rec[kTravStage * 4];
+  __shared__ uint4 s_rec[kTravStage * 3];
   const uint64_t l0 = (uint64_t)blockIdx.x * blockDim.x;
   const uint64_t l = l0 + threadIdx.x;
   const uint64_t last = (l0 + blockDim.x < b.P ? l0 + blockDim.x : b.P) - 1;
@@ -1808,7 +1803,7 @@ __global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
   __syncthreads();
   const uint32_t n_stage = n_rec < kTravStage ? n_rec : kTravStage;
   uint4* dst = reinterpret_cast<uint4*>(b.trav + base);
-  for (uint32_t v = threadIdx.x; v < n_stage * 4; v += blockDim.x) dst[v] = s_rec[v];
+  for (uint32_t v = threadIdx.x; v < n_stage * 3; v += blockDim.x) dst[v] = s_rec[v];
   // run flags of the staged block, looking back within the stage only (k_run_flags_fix
   // redoes the prefix whose lookback crosses into the previous block)
   if (n_rec <= kTravStage) {
@@ -1849,7 +1844,7 @@ __global__ void __launch_bounds__(256) k_run_flags_fix(DevBatch b, uint32_t tota
       b.run_kind[r] = kind;
       b.run_head[r] = head;
       if (kind != kRecSkip) break;
-      if (r + 1 < end && !same_chain(b.trav[r].slot, b.trav[r + 1].slot)) break;
+      if (r + 1 < end && !same_chain(b.trav[r].slot & kTravSlotMask, b.trav[r + 1].slot & kTravSlotMask)) break;
     }
   }
 }
@@ -1873,7 +1868,7 @@ __device__ __forceinline__ void run_piece(RunState& R, const TravRec& t, uint8_t
     md = t.en - t.b; mtb = t.tb; mte = t.te;
     if (t.way != R.way_first) R.way_last = t.way;
   }
-  R.l_en = t.en; R.l_len = t.len; R.l_soff = t.soff; R.te = t.te; R.se = t.se;
+  R.l_en = t.en; R.l_len = t.len; R.l_soff = t.soff; R.te = t.te; R.se = t.slot;  // raw slot, resolved at close
 }
 
 // one lane per run: records [run_pos[i], run_pos[i+1]) (skips and merged pieces inside)
@@ -1893,12 +1888,13 @@ __global__ void __launch_bounds__(256) k_runs(DevGraph g, DevBatch b, uint32_t t
   const uint32_t end = (i + 1 < n_runs) ? b.run_pos[i + 1] : total;
   const TravRec f = b.trav[r];
   RunState R;
-  R.open = true; R.sd = f.sd; R.internal = f.internal != 0u; R.seg_len = f.seg_len;
-  R.f_b = f.b; R.f_soff = f.soff; R.tb = f.tb; R.sb = f.sb;
+  R.open = true; R.sd = f.sd; R.internal = (f.slot & kTravInternal) != 0u;
+  R.seg_len = f.sd != kNone ? g.seg_len[f.sd] : 0u;
+  R.f_b = f.b; R.f_soff = f.soff; R.tb = f.tb; R.sb = b.state_orig[(f.slot & kTravSlotMask) - 1u];
   R.tot = 0; R.q = 0; R.way_first = f.way; R.way_last = f.way;
   uint32_t md = f.en - f.b;
   double mtb = f.tb, mte = f.te;
-  R.l_en = f.en; R.l_len = f.len; R.l_soff = f.soff; R.te = f.te; R.se = f.se;
+  R.l_en = f.en; R.l_len = f.len; R.l_soff = f.soff; R.te = f.te; R.se = f.slot;
   // records are consumed four at a time so their loads overlap
   uint32_t q = r + 1;
   for (; q + 4 <= end; q += 4) {
@@ -1919,6 +1915,12 @@ __global__ void __launch_bounds__(256) k_runs(DevGraph g, DevBatch b, uint32_t t
     const bool slow = dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
     R.tot += md;
     R.q = slow ? R.q + md : 0;
+  }
+  {
+    // end state of the run's last piece: its transition's target state if it is the last
+    // record of that transition, else the transition's source state
+    const uint32_t sl = R.se & kTravSlotMask;
+    R.se = b.state_orig[(R.se & kTravLast) ? sl : sl - 1u];
   }
   uint32_t n = 0;
   run_close(g, R, b.segs + i, n);

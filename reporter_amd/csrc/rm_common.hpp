@@ -195,12 +195,14 @@ static_assert(sizeof(ReportRec) == 48, "ReportRec layout is shared with oracle/m
 
 // ---- traversal record: one piece of a chosen path with its times and OSMLR tags ----
 struct TravRec {
-  uint32_t e, b, en, slot;          // directed edge, [b, en] cm along it, transition slot
+  uint32_t e, b, en, slot;          // directed edge, [b, en] cm along it, transition slot | flags below
   double tb, te;                    // interpolated epoch times at b and en
-  uint32_t sb, se, sd, soff;        // state indices at/before b and en, dense segment, edge offset in segment
-  uint32_t len, way, internal, seg_len;
+  uint32_t sd, soff, len, way;      // dense segment, edge offset in segment, edge length, way id
 };
-static_assert(sizeof(TravRec) == 64, "TravRec is four dwordx4");
+static_assert(sizeof(TravRec) == 48, "TravRec is three dwordx4");
+// TravRec::slot flags: the edge is internal; the record is the last of its transition (its end
+// state is the transition's target state, otherwise its source state)
+constexpr uint32_t kTravInternal = 1u << 31, kTravLast = 1u << 30, kTravSlotMask = kTravLast - 1u;
 
 struct ReportStats {        // per trace (reporter_service.py:164-177)
   int32_t successful_count, unreported_count;
