@@ -2486,6 +2486,7 @@ void Matcher::run_device(const RunParams& rp) {
   }
   const uint64_t seg_total = (uint64_t)hctl_[10] + hctl_[11];
   if (seg_total >= 0xffffffffull) throw std::runtime_error("batch too large (path edges >= 2^32); split it");
+  if (P >= (uint64_t)kTravLast) throw std::runtime_error("batch too large (slots >= 2^30); split it");  // TravRec::slot flags
   n_path_ = seg_total;  // one traversal record (and at most one segment) per chosen path edge
   ensure_segs(seg_total);
   v.segs = w.segs; v.reps = w.reps; v.trav = w.trav;
