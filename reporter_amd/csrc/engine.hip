@@ -1728,7 +1728,10 @@ __device__ __forceinline__ void run_flag(const TravRec* recs, int64_t r, uint8_t
 // The records of a block's 256 slots are one contiguous range of trav (trav_off is a scan in
 // slot order): the first kTravStage of them are staged in LDS and written by the whole block
 // with coalesced 16-byte stores; records past the stage (long paths) are stored by their lane.
-constexpr uint32_t kTravStage = 512;
+#ifndef RM_TRAV_STAGE
+#define RM_TRAV_STAGE 1024
+#endif
+constexpr uint32_t kTravStage = RM_TRAV_STAGE;
 
 __device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch& b, uint64_t l, uint32_t base,
                                                uint4* s_rec) {
