@@ -3,11 +3,16 @@
 
 One step = the whole hot path over one resident batch: state selection,
 candidate search (K1), bounded route search (K2), Viterbi (K3), path recovery
-and OSMLR segment forming (K4), the reference's report() epilogue and the
-per-segment speed histogram — i.e. what valhalla.SegmentMatcher().Match +
-reporter_service.report() do for every trace (reference py/reporter_service.py:
-240-242), batched.  With N>1 ranks each GPU matches its own uuid shard (weak
-scaling) and the histograms are all-reduced over RCCL every step.
+and OSMLR segment forming (K4), the reference's report() epilogue, the
+per-segment speed histogram and its RCCL all-reduce — i.e. what
+valhalla.SegmentMatcher().Match + reporter_service.report() do for every trace
+(reference py/reporter_service.py:240-242), batched, plus the exchange that
+replaces the keyed "id next_id" repartition (BatchingProcessor.java:126).
+
+Workload: ONE seeded set of N x 10,000 C2 trajectories (uuids "C2-veh-0000000"...),
+sharded over the N ranks by dist.shard_by_uuid (hash(uuid) buckets balanced by point
+count, py/simple_reporter.py:116); each rank generates exactly its shard.  Weak
+scaling: 10k trajectories per GPU.
 
     python bench.py                       # N=1, C2 (configs[1]): 10k x 600 pts @1 Hz
     python bench.py --gpus 8              # self-launches 8 ranks (or run under torch.distributed.run)
@@ -16,6 +21,7 @@ Prints ONE JSON line (rank 0).  No PyTorch is loaded: RCCL is bound natively
 by libreporter_match.so and ranks rendezvous through a node-local file.
 """
 import argparse
+import hashlib
 import json
 import multiprocessing as mp
 import os
@@ -29,6 +35,7 @@ sys.path.insert(0, ROOT)
 METRIC = "GPS points map-matched/sec (node) at 1/2/4/8 MI355X; % of HBM peak"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0      # float4 copy ceiling from the same guide
+ENGINE_SRC = os.path.join(ROOT, "reporter_amd", "csrc", "engine.hip")
 
 
 def parse():
@@ -40,11 +47,19 @@ def parse():
     ap.add_argument("--traces", type=int, default=0, help="override traces per rank")
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (default min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the C1 latency and JSON-boundary lines")
+    ap.add_argument("--json-traces", type=int, default=10000, help="traces sent through rm_match_batch as JSON")
     ap.add_argument("--ball-radius", type=float, default=None,
                     help="route-ball radius in m (default: the config's, else the engine's automatic radius)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_routes_c2.json"),
-                    help="rocprofv3 PMC summary giving HBM bytes per routes launch (optional)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_routes_c2.json"),
+                    help="rocprofv3 PMC summary giving HBM bytes per routes launch (optional; used only when it "
+                         "was measured on this engine.hip)")
     return ap.parse_args()
+
+
+def engine_sha():
+    with open(ENGINE_SRC, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 # ---------------------------------------------------------------- CPU baseline leg (oracle)
@@ -91,8 +106,8 @@ def cpu_baseline_leg(graph_path, tr, search_radius, procs):
     for r in res:
         for k, v in r[3].items():
             counts[k] = counts.get(k, 0) + v
-    return dict(value=pts / wall, seconds=wall, points=pts, reports=sum(r[2] for r in res), cores=len(blocks),
-                counts=counts)
+    return dict(value=pts / wall, seconds=wall, cpu_seconds=sum(r[0] for r in res), points=pts,
+                reports=sum(r[2] for r in res), cores=len(blocks), counts=counts)
 
 
 # ---------------------------------------------------------------- launcher for --gpus N without torchrun
@@ -109,6 +124,110 @@ def self_launch(n):
     return rc
 
 
+def shard_ids(config, n_per_rank, n_points, world, rank):
+    """Trace indices of this rank's uuid shard of the ONE seeded workload of world x n_per_rank
+    trajectories (dist.shard_by_uuid: hash(uuid) buckets balanced by point count)."""
+    import numpy as np
+    from reporter_amd import dist
+    total = n_per_rank * world
+    uuids = ["%s-veh-%07d" % (config, k) for k in range(total)]
+    return dist.shard_by_uuid(uuids, np.full(total, n_points), world)[rank].astype(np.uint32)
+
+
+def roofline(name, kernels, abytes, ms, formulation):
+    if not abytes or not ms:
+        return {"kernel": kernels, "formulation": formulation, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": None, "traffic": None, "algorithmic_bytes_per_launch": abytes,
+                "avg_launch_ms": ms}
+    achieved = abytes / (ms * 1e-3) / 1e9
+    return {"kernel": kernels, "formulation": formulation, "bound": "hbm", "achieved": achieved,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "frac_vs_measured_copy": achieved / HBM_MEASURED_GBS, "traffic": None,
+            "algorithmic_bytes_per_launch": abytes, "avg_launch_ms": ms}
+
+
+def timed(fn, steps, comm, sync):
+    """barrier + sync, `steps` calls, sync + barrier; max over ranks."""
+    sync()
+    if comm is not None:
+        comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    if comm is not None:
+        comm.barrier()
+    dt = time.perf_counter() - t0
+    if comm is not None:
+        dt = comm.allreduce_host(dt, 1)
+    return dt
+
+
+def request_jsons(tr, n):
+    """/report requests (reporter_service.py:184-235 contract) of the first n traces."""
+    import numpy as np
+    off = tr["trace_off"].tolist()
+    n = min(n, len(off) - 1)
+    P = off[n]
+    f = '{"lat":%.6f,"lon":%.6f,"time":%d,"accuracy":%g}'
+    pts = [f % q for q in zip(tr["lat"][:P].tolist(), tr["lon"][:P].tolist(), tr["time"][:P].astype(np.int64).tolist(),
+                              tr["accuracy"][:P].tolist())]
+    mo = '"match_options":{"mode":"auto","report_levels":[0,1],"transition_levels":[0,1]}'
+    return ['{"uuid":"%d","trace":[%s],%s}' % (k, ",".join(pts[off[k]:off[k + 1]]), mo) for k in range(n)], P
+
+
+def extras(gpath, tr, json_traces, tmpdir):
+    """C1's defining measurement (single-trace latency through rm_match) and the JSON-boundary
+    throughput of rm_match_batch (PCIe + parse + serialize inclusive), both through the drop-in
+    valhalla module exactly as reporter_service.py calls it (:52, :240, :284)."""
+    import numpy as np
+    import valhalla
+    from reporter_amd import world as W
+    out = {}
+    c1 = W.CONFIGS["C1"]
+    c1g = os.path.join(tmpdir, "reporter_bench_C1_%d.rmg" % os.getpid())
+    W.build_world(c1g, c1["rows"], c1["cols"], c1["block_m"], seed=1, cell_m=c1["cell_m"])
+    c1tr = W.generate_traces(c1g, 1, c1["n_points"], c1["rate_s"], c1["noise_m"], seed=1)
+    req = json.dumps(W.trace_to_request(c1tr, 0), separators=(",", ":"))
+    conf = valhalla.write_config(os.path.join(tmpdir, "reporter_bench_c1_%d.json" % os.getpid()), c1g, device=0)
+    valhalla.Configure(conf)
+    sm = valhalla.SegmentMatcher()
+    for _ in range(5):
+        sm.Match(req)
+    lat = []
+    for _ in range(50):
+        t = time.perf_counter()
+        r = sm.Match(req)
+        lat.append((time.perf_counter() - t) * 1e3)
+    lat.sort()
+    out["c1_latency"] = {"what": "one 1,000-point 1 Hz trace (C1: 40x40 grid @100 m) through valhalla.SegmentMatcher()"
+                                 ".Match -> rm_match (JSON in, JSON out; request coalescing on, one request in flight)",
+                         "median_ms": lat[len(lat) // 2], "p90_ms": lat[int(len(lat) * 0.9)], "min_ms": lat[0],
+                         "segments": len(json.loads(r)["segments"]), "caller_budget_ms": 10000,
+                         "caller_budget_source": "HttpClient.java:80-87 (10 s socket timeout)"}
+    sm.close()
+    os.remove(c1g)
+    # JSON boundary: the rank's C2 traces as /report JSON through rm_match_batch
+    t = time.perf_counter()
+    reqs, P = request_jsons(tr, json_traces)
+    build_s = time.perf_counter() - t
+    conf = valhalla.write_config(os.path.join(tmpdir, "reporter_bench_c2_%d.json" % os.getpid()), gpath, device=0,
+                                 coalesce=False)
+    valhalla.Configure(conf)
+    sm = valhalla.SegmentMatcher()
+    sm.MatchMany(reqs[:64])   # warm: workspace + route balls
+    t = time.perf_counter()
+    outs = sm.MatchMany(reqs)
+    dt = time.perf_counter() - t
+    out["json_boundary"] = {"what": "%d C2 traces (%d points, %.0f MB of /report JSON) through rm_match_batch: host "
+                                    "JSON parse -> H2D -> every kernel -> D2H -> segment JSON" % (
+                                        len(reqs), P, sum(map(len, reqs)) / 1e6),
+                            "value": P / dt, "unit": "points/s", "seconds": dt, "json_build_s_untimed": build_s,
+                            "reply_mb": sum(map(len, outs)) / 1e6}
+    sm.close()
+    return out
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "RANK" not in os.environ:
@@ -120,25 +239,34 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
 
     import numpy as np
-    from reporter_amd import dist, engine, world as W
+    from reporter_amd import _lib, dist, engine, world as W
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import meili_oracle as mo  # cpu_baseline leg only (algorithmic byte counts + CPU timing)
 
     cfg = dict(W.CONFIGS[a.config])
-    n_traces = a.traces or cfg["n_traces"]
+    n_per = a.traces or cfg["n_traces"]
     gdir = os.environ.get("TMPDIR", "/tmp")
     gpath = os.path.join(gdir, "reporter_bench_%s_%d_%d.rmg" % (a.config, os.getpid(), rank))
     W.build_world(gpath, cfg["rows"], cfg["cols"], cfg["block_m"], seed=1, cell_m=cfg["cell_m"])
-    tr = W.generate_traces(gpath, n_traces, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=1000 + rank)
+    ids = shard_ids(a.config, n_per, cfg["n_points"], world, rank)
+    tr = W.generate_traces(gpath, 0, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=1000, ids=ids)
     P = int(tr["trace_off"][-1])
+    T = len(ids)
 
     # CPU leg first, before this process touches the GPU (forked workers never inherit a HIP context)
     cpu = None
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
         procs = a.cpu_procs or min(16, os.cpu_count() or 1)
         cpu = cpu_baseline_leg(gpath, tr, cfg["search_radius"], procs)
 
-    comm = dist.Comm(rank, world, local, token=os.environ.get("RM_RDZV_TOKEN")) if world > 1 else None
+    comm, comm_note = None, None
+    try:
+        comm = dist.Comm(rank, world, local, token=os.environ.get("RM_RDZV_TOKEN"))
+    except Exception as e:  # noqa: BLE001 -- one rank without RCCL still measures the matcher
+        if world > 1:
+            raise
+        comm_note = "RCCL unavailable at N=1 (%s): histogram not all-reduced" % e
+    t_up = time.perf_counter()
     eng = engine.Engine(gpath, local)
     radius = a.ball_radius if a.ball_radius is not None else cfg.get("ball_radius_m")
     if radius is not None:
@@ -149,41 +277,39 @@ def main():
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
     rp = dict(hist_dev=hist.ptr, zero_hist=True)
     bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, None, **rp)
+    cold_s = time.perf_counter() - t_up
 
-    def step():
-        bm.rerun(**rp)
+    def sync():
+        _lib.check(_lib.lib().rm_device_synchronize())
+
+    def allreduce():
         if comm is not None:
             comm.allreduce(hist.ptr, nseg * 16, dist.U32, dist.SUM)
 
+    def step():
+        bm.rerun(**rp)
+        allreduce()
+
     for _ in range(a.warmup):
         step()
-    _lib_sync()
-    if comm is not None:
-        comm.barrier()
     bm.set_timing(True)
     bm.reset_times()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    _lib_sync()
-    if comm is not None:
-        comm.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(step, a.steps, comm, sync)               # the official step: match + all-reduce
     kt = bm.kernel_times()
-    if comm is not None:
-        elapsed = comm.allreduce_host(elapsed, dist.MAX)
-        total_points = comm.allreduce_host(P, dist.SUM)
-    else:
-        total_points = P
+    bm.set_timing(False)
+    t_ar = timed(allreduce, a.steps, comm, sync)             # the all-reduce alone, reported alongside
+    t_match = timed(lambda: bm.rerun(**rp), a.steps, comm, sync)   # matching alone
+    total_points = comm.allreduce_host(P, dist.SUM) if comm is not None else P
     sizes = bm.sizes()
     hist_sum = int(hist.download().sum())
+    balls = eng.ball_stats(0)
+    tiers = bm.route_tiers()
 
+    out = None
     if rank == 0:
         steps = max(a.steps, 1)
-        routes_ms = kt["routes"][0] / steps
+        ms = {k: v[0] / steps for k, v in kt.items()}
         counts = cpu["counts"] if cpu else {}
-        balls = eng.ball_stats(0)
-        tiers = bm.route_tiers()
         ball_tier = balls["radius_m"] > 0 and balls["keys"] > 0
         # bytes of the formulation the launch runs: route-ball probes (every item answered by
         # the tables when nothing was handed over), else the bounded searches
@@ -193,16 +319,36 @@ def main():
             abytes, formulation = mo.routes_algorithmic_bytes(counts), "bounded searches"
         else:
             abytes, formulation = None, None
-        achieved = abytes / (routes_ms * 1e-3) / 1e9 if abytes else None
-        traffic = None
+        k2 = roofline("K2", "K2 route stage: k_src_items + k_routes_ball + search tiers for hand-overs", abytes,
+                      ms["routes"], formulation)
+        traffic, traffic_note = None, "no PMC summary of this engine.hip (sha %s)" % engine_sha()
         if os.path.exists(a.traffic_json):
             try:
                 with open(a.traffic_json) as f:
                     tj = json.load(f)
-                if tj.get("config") == a.config and tj.get("traces") == n_traces:
+                if tj.get("config") == a.config and tj.get("traces") == n_per and tj.get("engine_sha") == engine_sha():
                     traffic = tj.get("hbm_bytes_per_launch")
+                    traffic_note = ("%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this engine.hip (sha %s), "
+                                    "read side x%s per MI355X_MICROARCH.md" % (
+                                        os.path.relpath(a.traffic_json, ROOT), engine_sha(), tj.get("read_factor", 2)))
             except (OSError, ValueError):
                 traffic = None
+        k2["traffic"] = traffic
+        k2["traffic_source"] = traffic_note
+        k2.update({"search_equivalent_bytes_per_launch": mo.routes_algorithmic_bytes(counts) if counts else None,
+                   "counts": counts, "route_tiers": tiers, "route_balls": balls})
+        rooflines = {
+            "K1": roofline("K1", "k_candidates_lane + k_candidates_wave", mo.candidates_algorithmic_bytes(counts)
+                           if counts else None, ms["candidates"], "cell-major 32 B records, per-road minima in registers"),
+            "K2": {k: k2[k] for k in ("kernel", "achieved", "frac", "algorithmic_bytes_per_launch", "avg_launch_ms")},
+            "K3": roofline("K3", "k_viterbi", mo.viterbi_algorithmic_bytes(counts) if counts else None, ms["viterbi"],
+                           "u32 routes + f32 emissions, fp64 costs in registers"),
+            "K4": roofline("K4", "segments stage: trav_off scan + k_traversals + run flags + k_runs",
+                           mo.segments_algorithmic_bytes(counts) if counts else None, ms["segments"],
+                           "path edges -> traversal records -> OSMLR runs"),
+        }
+        step_ms = elapsed / steps * 1e3
+        build_ms = balls["build_ms"]
         out = {
             "metric": METRIC,
             "value": total_points * a.steps / elapsed,
@@ -210,68 +356,61 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": elapsed / steps * 1e3,
+            "ms_per_step": step_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 geometry / f64 Viterbi + times / u64 (dist,time) route keys",
             "data": "synthetic (seeded perturbed-grid world + generate_test_trace.py-style noisy traces)",
             "config": {
-                "workload": "%s: %d traces x %d pts @%gs per GPU, %dx%d grid @%gm, radius %gm" % (
-                    a.config, n_traces, cfg["n_points"], cfg["rate_s"], cfg["rows"], cfg["cols"], cfg["block_m"],
-                    cfg["search_radius"]),
-                "points_per_gpu": P,
-                "traces_per_gpu": n_traces,
+                "workload": "%s: %d traces x %d pts @%gs per GPU (uuid shard of one %d-trace seeded set), %dx%d grid "
+                            "@%gm, radius %gm" % (a.config, n_per, cfg["n_points"], cfg["rate_s"], n_per * world,
+                                                 cfg["rows"], cfg["cols"], cfg["block_m"], cfg["search_radius"]),
+                "points_rank0": P,
+                "traces_rank0": T,
+                "points_all_ranks": int(total_points),
                 "graph": W.graph_info(gpath),
-                "parallelism": "uuid shard x%d, graph replicated, RCCL all-reduce of %d x 16 u32 speed histogram"
-                               % (world, nseg),
+                "parallelism": "uuid shard x%d (dist.shard_by_uuid), graph replicated, RCCL all-reduce of %d x 16 u32 "
+                               "speed histogram every step" % (world, nseg),
             },
-            "roofline": {
-                "kernel": "K2 route stage: k_src_items + k_routes_ball + search tiers for hand-overs (one launch "
-                          "each per step)",
-                "formulation": formulation,
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "frac_vs_measured_copy": (achieved / HBM_MEASURED_GBS) if achieved else None,
-                "traffic": traffic,
-                "traffic_source": (os.path.relpath(a.traffic_json, ROOT) + " (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE "
-                                   "passes of this bench, read side x2 per MI355X_MICROARCH.md)") if traffic else None,
-                "algorithmic_bytes_per_launch": abytes,
-                "search_equivalent_bytes_per_launch": mo.routes_algorithmic_bytes(counts) if counts else None,
-                "avg_launch_ms": routes_ms,
-                "counts": counts,
-                "route_tiers": tiers,
-                "route_balls": balls,
-            },
-            "kernels_ms_per_step": {k: v[0] / steps for k, v in kt.items()},
-            "sizes_per_gpu": sizes,
+            "ms_allreduce": t_ar / steps * 1e3,
+            "allreduce_bytes": nseg * 16 * 4,
+            "ms_matching_only": t_match / steps * 1e3,
+            "value_matching_only": total_points * a.steps / t_match,
+            "roofline": k2,
+            "rooflines": rooflines,
+            "cold_start": {"graph_upload_and_first_run_s": cold_s, "route_ball_build_ms": build_ms,
+                           "ball_build_in_steps": build_ms / step_ms,
+                           "value_over_first_hour_incl_ball_build": total_points / (step_ms * 1e-3) *
+                           max(0.0, 3600.0 - build_ms * 1e-3) / 3600.0,
+                           "note": "the route balls are built once per graph and travel mode (host, at rm_configure); "
+                                   "they are outside the timed step"},
+            "kernels_ms_per_step": ms,
+            "sizes_rank0": sizes,
             "histogram_total": hist_sum,
         }
-        if cpu and world == 1:
+        if comm_note:
+            out["comm_note"] = comm_note
+        if cpu:
             out["cpu_baseline"] = {
                 "value": cpu["value"], "unit": "points/s", "cores": cpu["cores"], "kind": "port",
-                "sample": "full %s workload (%d pts, %d traces) split into %d contiguous blocks, one "
-                          "single-threaded oracle process each (match + report() + histogram); %.2fs wall"
-                          % (a.config, cpu["points"], n_traces, cpu["cores"], cpu["seconds"]),
+                "sample": "full %s rank-0 workload (%d pts, %d traces) split into %d contiguous blocks, one "
+                          "single-threaded oracle process each (match + report() + histogram); %.2fs wall, %.1f "
+                          "CPU-s" % (a.config, cpu["points"], T, cpu["cores"], cpu["seconds"], cpu["cpu_seconds"]),
             }
-        print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()
     hist.close()
     bm.close()
     eng.close()
+    if rank == 0 and world == 1 and not a.no_extras and a.config == "C2":
+        out.update(extras(gpath, tr, a.json_traces, gdir))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     try:
         os.remove(gpath)
     except OSError:
         pass
-
-
-def _lib_sync():
-    from reporter_amd import _lib
-    _lib.check(_lib.lib().rm_device_synchronize())
 
 
 if __name__ == "__main__":

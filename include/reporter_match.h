@@ -89,6 +89,10 @@ void rm_default_trace_params(rm_trace_params* p);
 /* Arrays sized n_traces*n_points; truth_* may be NULL. */
 int rm_traces_generate(const char* graph_path, const rm_trace_params* p, double* lon, double* lat, double* time,
                        float* accuracy, uint32_t* truth_edge, uint32_t* truth_off_cm);
+/* p->n_traces traces; slot k holds trace ids[k] of the seeded set (identical to what
+ * rm_traces_generate puts at index ids[k]): one rank generates just its uuid shard. */
+int rm_traces_generate_ids(const char* graph_path, const rm_trace_params* p, const uint32_t* ids, double* lon,
+                           double* lat, double* time, float* accuracy, uint32_t* truth_edge, uint32_t* truth_off_cm);
 
 /* ---------------- batched array API (bench / batch pipeline / parity tests) ---------------- */
 typedef struct rm_engine rm_engine;
@@ -153,8 +157,9 @@ int rm_runner_rerun(rm_runner* r, const rm_run_params* p);
 int rm_runner_sizes(rm_runner* r, uint64_t out[10]);
 /* K2 tier hand-overs of the last run: [0] items the ball tier passed to the search tiers,
  * [1] items the register search tier passed on, [2] items the second register tier passed on,
- * [3] chosen transitions the path ball tier passed to the path search tiers */
-int rm_runner_route_tiers(rm_runner* r, uint64_t out[4]);
+ * [3] chosen transitions the path ball tier passed to the path search tiers,
+ * [4] route items the LDS wave tier passed to the global-memory tier, [5] likewise for paths */
+int rm_runner_route_tiers(rm_runner* r, uint64_t out[6]);
 int rm_runner_get_states(rm_runner* r, uint32_t* n_states, uint32_t* state_orig);
 int rm_runner_get_candidates(rm_runner* r, uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
 int rm_runner_get_routes(rm_runner* r, uint32_t* trans_off, double* gc, uint32_t* route_cm);
@@ -164,12 +169,39 @@ int rm_runner_get_paths(rm_runner* r, uint32_t* path_off, uint32_t* path_cnt, ui
 int rm_runner_get_segments(rm_runner* r, uint32_t* seg_off, void* segs);
 /* reports: 48-byte records (rm::ReportRec); stats: 40-byte rm::ReportStats per trace */
 int rm_runner_get_reports(rm_runner* r, uint32_t* rep_off, void* reps, void* stats);
+/* Failure isolation (default off: a trace that fails makes rm_runner_run return non-zero).
+ * On: a trace that fails on its own — more than 192 roads inside its search radius, a route
+ * search beyond every tier's capacity, a path that cannot be rebuilt — gets no segments and no
+ * reports, the run succeeds for every other trace, and rm_runner_trace_errors gives the bits
+ * (1 candidates, 2 route search, 8 path reconstruction) per trace.  The reference fails just
+ * that request (py/reporter_service.py:244-245) or skips just that window
+ * (py/simple_reporter.py:169-173). */
+int rm_runner_set_isolation(rm_runner* r, int on);
+int rm_runner_trace_errors(rm_runner* r, uint32_t* errs);   /* n_traces words of the last run */
 /* per-kernel HIP-event timing on the runner's stream */
 int rm_runner_set_timing(rm_runner* r, int on);
 int rm_runner_kernel_times(rm_runner* r, double* ms, uint64_t* launches, int n);
 int rm_runner_reset_times(rm_runner* r);
 const char* rm_kernel_name(int k);
 int rm_num_kernels(void);
+
+/* ---------------- report() on host-supplied segment lists ----------------
+ * The device report() epilogue (reference py/reporter_service.py:79-179) over segment lists
+ * that did not come from the matcher: trace k's segments are segs[seg_off[k] .. seg_off[k+1])
+ * (56-byte rm::SegmentRec), its last point's time trace_end_time[k] (:81), its threshold and
+ * level masks per trace.  Reports come back compacted per trace (rep_off: n_traces+1 offsets,
+ * reps: room for seg_off[n_traces] 48-byte records), stats: 40-byte rm::ReportStats per trace.
+ * Uses the device of rm_set_device. */
+typedef struct {
+  uint32_t n_traces;
+  const uint32_t* seg_off;
+  const void* segs;
+  const double* trace_end_time;
+  const double* threshold_sec;
+  const uint32_t* report_mask;      /* bit (level+1) per reported level */
+  const uint32_t* transition_mask;
+} rm_report_desc;
+int rm_report_segments(const rm_report_desc* d, uint32_t* rep_off, void* reps, void* stats);
 
 /* ---------------- batch-pipeline stages around the matcher (reference py/simple_reporter.py) ----------------
  * rm_runner_run_points replaces the per-vehicle grouping, time sort and inactivity
@@ -227,6 +259,7 @@ int rm_device_alloc(size_t bytes, void** dev_ptr);
 int rm_device_free(void* dev_ptr);
 int rm_device_memset(void* dev_ptr, int value, size_t bytes);
 int rm_device_download(void* host_dst, const void* dev_src, size_t bytes);
+int rm_device_upload(void* dev_dst, const void* host_src, size_t bytes);
 int rm_device_synchronize(void);
 
 #ifdef __cplusplus

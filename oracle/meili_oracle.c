@@ -78,13 +78,15 @@ static int e_ok(const og_graph* g, uint32_t e, uint32_t acc) {
 static uint32_t e_speed(const og_graph* g, uint32_t e, int mode) { return mode_speed(mode, e_info(g, e) & 0xffffu); }
 static uint64_t mk(uint32_t d, uint32_t t) { return ((uint64_t)d << 32) | t; }
 
-/* ---------------- algorithmic work counters (roofline of K1/K2) ----------------
+/* ---------------- algorithmic work counters (rooflines of K1..K4) ----------------
  * [0] searches [1] settled nodes [2] scanned edges [3] label writes
  * [4] target label lookups [5] route writes [6] candidate items tested [7] states
  * [8] route-ball rows a table formulation of K2 reads: per (source, target with a usable
  *     direction), one per usable exit of the source [9] candidate descriptors read by K2
- *     (KA sources + KB targets per layer pair) */
-#define OG_NCNT 10
+ *     (KA sources + KB targets per layer pair) [10] candidates kept (sum of K over states)
+ * [11] grid rows visited by the candidate search (one item range per row) [12] chained
+ * transitions (a path is built) [13] path edges [14] segments formed */
+#define OG_NCNT 15
 static uint64_t og_cnt[OG_NCNT];
 static uint32_t og_roots;   /* usable exits of the last search_from */
 static int og_counting = 0;
@@ -302,6 +304,7 @@ static uint32_t find_candidates(const og_graph* g, float lon, float lat, float r
   const uint32_t x1 = fx1 > (double)(g->ncx - 1) ? g->ncx - 1 : (uint32_t)fx1;
   const uint32_t y1 = fy1 > (double)(g->ncy - 1) ? g->ncy - 1 : (uint32_t)fy1;
   uint32_t n = 0;
+  og_cnt[11] += y1 - y0 + 1;
   for (uint32_t cy = y0; cy <= y1; ++cy)
     for (uint32_t cx = x0; cx <= x1; ++cx) {
       const uint32_t c = cy * g->ncx + cx;
@@ -483,6 +486,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
       const float r = point_radius(op, b->accuracy[p]);
       const uint32_t m = find_candidates(g, b->lon[p], b->lat[p], r, op->mode, &cbuf, &cap, top);
       R->cand_n[o + s] = (uint8_t)m;
+      og_cnt[10] += m;
       for (uint32_t j = 0; j < m; ++j) {
         R->cand_road[(o + s) * (uint64_t)OG_K + j] = top[j].road;
         R->cand_s[(o + s) * (uint64_t)OG_K + j] = top[j].s;
@@ -665,6 +669,8 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
       }
       R->path_off[l] = (uint32_t)pn;
       R->path_cnt[l] = ns;
+      og_cnt[12]++;
+      og_cnt[13] += ns;
       if (pn + ns > pcap) { while (pn + ns > pcap) pcap *= 2; pool = (uint32_t*)realloc(pool, sizeof(uint32_t) * pcap); }
       memcpy(pool + pn, stack, sizeof(uint32_t) * ns);
       pn += ns;
@@ -695,6 +701,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
     form_runs(g, &tv, &sv);
   }
   R->seg_off[T] = (uint32_t)sv.n;
+  og_cnt[14] += sv.n;
   R->path_edges = pool; R->n_path = pn;
   R->segs = sv.v; R->n_seg = sv.n;
   free(tv.v); free(stack); free(cbuf);

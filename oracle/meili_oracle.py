@@ -64,7 +64,8 @@ def lib():
 
 
 COUNTER_NAMES = ("searches", "settled", "scanned", "label_writes", "target_lookups", "route_writes",
-                 "cand_items", "states", "ball_rows", "desc_reads")
+                 "cand_items", "states", "ball_rows", "desc_reads", "cands", "grid_rows", "chained", "path_edges",
+                 "segments")
 
 
 def reset_counters():
@@ -93,9 +94,27 @@ def routes_ball_algorithmic_bytes(c):
 
 
 def candidates_algorithmic_bytes(c):
-    """K1 algorithmic bytes: 16 B point per state + 36 B per tested cell item (item id +
-    two 16 B vertex records) + 24 B per state for up to 16 candidates written at 12 B each (avg)."""
-    return 16 * c["states"] + 36 * c["cand_items"]
+    """K1 algorithmic bytes of the formulation k_candidates_lane runs: per state
+    16 B (point lon/lat, slot, options index) + 1 B candidate count; 8 B item range per grid
+    row visited; 32 B self-contained cell record per cell item tested (both shape vertices,
+    road, access); per candidate kept 32 B road record read + 32 B descriptor + 4 B sq written."""
+    return 17 * c["states"] + 8 * c["grid_rows"] + 32 * c["cand_items"] + 68 * c["cands"]
+
+
+def viterbi_algorithmic_bytes(c):
+    """K3 algorithmic bytes (in the layout k_viterbi reads): 4 B route per
+    transition, 4 B emission (sq) per candidate, per layer 8 B gc + 12 B layer descriptor
+    (cand count, route offset, state) + 16 B back-pointer row written and read back + 2 B
+    choice / chain flag."""
+    return 4 * c["route_writes"] + 4 * c["cands"] + (8 + 12 + 32 + 2) * c["states"]
+
+
+def segments_algorithmic_bytes(c):
+    """K4 algorithmic bytes (matched edges x 16 B + segments x 48 B, in this
+    build's layout): per path edge 4 B edge id + 16 B edge record + 12 B OSMLR association
+    (segment, offset, way); per chained transition 64 B (two candidate offsets, two state
+    indices, two times, route length, path header); per segment 56 B written."""
+    return 32 * c["path_edges"] + 64 * c["chained"] + 56 * c["segments"]
 
 
 def make_graph(g):

@@ -53,6 +53,12 @@ class RmPointsDesc(C.Structure):
                 ("n_uuids", C.c_uint32), ("n_opts", C.c_uint32), ("opts", C.c_void_p), ("uuid_opt", C.c_void_p)]
 
 
+class RmReportDesc(C.Structure):
+    _fields_ = [("n_traces", C.c_uint32), ("seg_off", C.c_void_p), ("segs", C.c_void_p),
+                ("trace_end_time", C.c_void_p), ("threshold_sec", C.c_void_p), ("report_mask", C.c_void_p),
+                ("transition_mask", C.c_void_p)]
+
+
 class RmTileParams(C.Structure):
     _fields_ = [("quantisation", C.c_uint32), ("privacy", C.c_uint32), ("source", C.c_char_p), ("mode", C.c_char_p)]
 
@@ -79,6 +85,7 @@ PROTOTYPES = [
     ("rm_graph_info", C.c_int, [C.c_char_p, C.POINTER(C.c_uint64)]),
     ("rm_default_trace_params", None, [C.POINTER(RmTraceParams)]),
     ("rm_traces_generate", C.c_int, [C.c_char_p, C.POINTER(RmTraceParams), P, P, P, P, P, P]),
+    ("rm_traces_generate_ids", C.c_int, [C.c_char_p, C.POINTER(RmTraceParams), P, P, P, P, P, P, P]),
     ("rm_engine_create", P, [C.c_char_p, C.c_int]),
     ("rm_engine_destroy", None, [P]),
     ("rm_engine_n_segments", C.c_uint32, [P]),
@@ -102,6 +109,9 @@ PROTOTYPES = [
     ("rm_runner_get_segments", C.c_int, [P, P, P]),
     ("rm_runner_get_reports", C.c_int, [P, P, P, P]),
     ("rm_runner_set_timing", C.c_int, [P, C.c_int]),
+    ("rm_runner_set_isolation", C.c_int, [P, C.c_int]),
+    ("rm_runner_trace_errors", C.c_int, [P, P]),
+    ("rm_report_segments", C.c_int, [C.POINTER(RmReportDesc), P, P, P]),
     ("rm_runner_kernel_times", C.c_int, [P, P, P, C.c_int]),
     ("rm_runner_reset_times", C.c_int, [P]),
     ("rm_kernel_name", C.c_char_p, [C.c_int]),
@@ -121,6 +131,7 @@ PROTOTYPES = [
     ("rm_device_free", C.c_int, [P]),
     ("rm_device_memset", C.c_int, [P, C.c_int, C.c_size_t]),
     ("rm_device_download", C.c_int, [P, P, C.c_size_t]),
+    ("rm_device_upload", C.c_int, [P, P, C.c_size_t]),
     ("rm_device_synchronize", C.c_int, []),
 ]
 

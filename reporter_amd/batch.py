@@ -21,6 +21,7 @@ writes the tile files it owns.  There is no CPU path: the library raises without
 """
 import argparse
 import json
+import logging
 import os
 import sys
 
@@ -99,9 +100,15 @@ def run(trace_files, conf, dest_dir, mode="auto", report_levels=(0, 1), transiti
     if radius is not None:
         eng.set_ball_radius(float(radius))
     bm = engine.BatchMatcher(eng)
+    bm.set_isolation(True)   # a failing window is logged and skipped (py/simple_reporter.py:169-173)
     try:
         bm.run_points(idx, pts["time"], pts["lon"], pts["lat"], pts["accuracy"], inactivity=inactivity, opts=opts,
                       n_uuids=len(names), report_levels=report_levels, transition_levels=transition_levels)
+        errs = bm.trace_errors()
+        if errs.any():
+            owner = bm.trace_uuid()
+            for k in np.nonzero(errs)[0]:
+                logging.error("%s window %d failed to match (error bits %d); skipped", names[owner[k]], k, int(errs[k]))
         files = bm.tiles(quantisation=quantisation, privacy=privacy, source=source, mode=mode, comm=comm)
         write_tiles(files, dest_dir)
         return files

@@ -258,8 +258,9 @@ char* dup_string(const std::string& s) {
   return p;
 }
 
-// run a list of parsed traces as one batch on matcher m; per-trace JSON replies
-std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*>& pt) {
+// run a list of parsed traces as one batch on matcher m; per-trace JSON replies, and per-trace
+// error messages (non-empty = that trace failed alone; its reply is empty)
+std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*>& pt, std::vector<std::string>* errs) {
   const size_t n = pt.size();
   std::vector<uint32_t> off(n + 1, 0), topt(n);
   std::vector<MatchOptions> opts(n);
@@ -279,13 +280,51 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
   hb.trace_opt = topt.data();
   RunParams rp;
   rp.do_report = 0;
+  m.set_isolation(true);
   m.run(hb, rp);
+  std::vector<uint32_t> terr(n, 0u);
+  if (m.error_bits()) m.get_trace_errors(terr.data());
   std::vector<uint32_t> soff(n + 1);
   std::vector<SegmentRec> segs(m.count_segments());
   m.get_segments(soff.data(), segs.data());
   std::vector<std::string> out(n);
-  for (size_t i = 0; i < n; ++i) out[i] = segments_json(segs.data() + soff[i], soff[i + 1] - soff[i]);
+  if (errs) errs->assign(n, std::string());
+  for (size_t i = 0; i < n; ++i) {
+    if (terr[i]) {
+      if (!errs) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
+      (*errs)[i] = error_text(terr[i]);
+      continue;
+    }
+    out[i] = segments_json(segs.data() + soff[i], soff[i + 1] - soff[i]);
+  }
   return out;
+}
+
+// Run `batch` and fill each request's reply or error.  A failure that belongs to one trace is
+// reported per trace by the engine; anything that still fails a whole batch (a device or
+// capacity error) is retried by halves, so only the requests that fail on their own get an error.
+void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch) {
+  std::vector<std::string> outs, errs;
+  try {
+    if (!m) m = std::make_unique<Matcher>(eng);
+    std::vector<ParsedTrace*> pt;
+    for (MatchRequest* r : batch) pt.push_back(r->trace);
+    outs = match_parsed(*m, pt, &errs);
+  } catch (const std::exception& e) {
+    m.reset();   // a fresh workspace for what follows
+    if (batch.size() > 1) {
+      const size_t h = batch.size() / 2;
+      serve_batch(m, eng, std::vector<MatchRequest*>(batch.begin(), batch.begin() + h));
+      serve_batch(m, eng, std::vector<MatchRequest*>(batch.begin() + h, batch.end()));
+      return;
+    }
+    batch[0]->err = e.what();
+    return;
+  }
+  for (size_t i = 0; i < batch.size(); ++i) {
+    if (!errs[i].empty()) batch[i]->err = errs[i];
+    else batch[i]->out = std::move(outs[i]);
+  }
 }
 
 void Coalescer::loop() {
@@ -305,24 +344,10 @@ void Coalescer::loop() {
       requests_ += batch.size();
       max_seen_ = std::max<uint64_t>(max_seen_, batch.size());
     }
-    std::vector<std::string> outs;
-    std::string err;
-    try {
-      if (!m) m = std::make_unique<Matcher>(eng_.get());
-      std::vector<ParsedTrace*> pt;
-      for (MatchRequest* r : batch) pt.push_back(r->trace);
-      outs = match_parsed(*m, pt);
-    } catch (const std::exception& e) {
-      err = e.what();
-      m.reset();   // a fresh workspace for the next batch
-    }
+    serve_batch(m, eng_.get(), batch);   // fills out / err of each request (not under the lock)
     {
       std::lock_guard<std::mutex> lk(mu_);
-      for (size_t i = 0; i < batch.size(); ++i) {
-        if (err.empty()) batch[i]->out = std::move(outs[i]);
-        else batch[i]->err = err;
-        batch[i]->done = true;
-      }
+      for (MatchRequest* r : batch) r->done = true;
     }
     cv_done_.notify_all();
   }
@@ -449,7 +474,7 @@ int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** ou
       if (!m->m) m->m = std::make_unique<Matcher>(m->conf->engine.get());
       std::vector<ParsedTrace*> pp;
       for (auto& t : pt) pp.push_back(&t);
-      js = match_parsed(*m->m, pp);
+      js = match_parsed(*m->m, pp, nullptr);   // any failing trace fails the call, naming the trace
     }
     try {
       for (size_t i = 0; i < n; ++i) outs[i] = dup_string(js[i]);
@@ -518,12 +543,17 @@ void rm_default_trace_params(rm_trace_params* p) {
 
 int rm_traces_generate(const char* graph_path, const rm_trace_params* p, double* lon, double* lat, double* time,
                        float* accuracy, uint32_t* truth_edge, uint32_t* truth_off_cm) {
+  return rm_traces_generate_ids(graph_path, p, nullptr, lon, lat, time, accuracy, truth_edge, truth_off_cm);
+}
+
+int rm_traces_generate_ids(const char* graph_path, const rm_trace_params* p, const uint32_t* ids, double* lon,
+                           double* lat, double* time, float* accuracy, uint32_t* truth_edge, uint32_t* truth_off_cm) {
   return guarded([&] {
     Graph g = Graph::load(graph_path);
     TraceParams t;
     t.n_traces = p->n_traces; t.n_points = p->n_points; t.rate_s = p->rate_s; t.noise_m = p->noise_m;
     t.seed = p->seed; t.mode = p->mode; t.start_epoch = p->start_epoch; t.threads = p->threads;
-    TraceSet ts = generate_traces(g, t);
+    TraceSet ts = generate_traces(g, t, ids);
     const size_t P = ts.lon.size();
     std::memcpy(lon, ts.lon.data(), P * 8); std::memcpy(lat, ts.lat.data(), P * 8);
     std::memcpy(time, ts.time.data(), P * 8); std::memcpy(accuracy, ts.accuracy.data(), P * 4);
@@ -644,11 +674,11 @@ int rm_runner_sizes(rm_runner* r, uint64_t out[10]) {
     for (int i = 0; i < 4; ++i) out[6 + i] = t[i];
   });
 }
-int rm_runner_route_tiers(rm_runner* r, uint64_t out[3]) {
+int rm_runner_route_tiers(rm_runner* r, uint64_t out[6]) {
   return guarded([&] {
     uint32_t c[kCtlWords];
     r->m->ctl_words(c);
-    out[0] = c[1]; out[1] = c[3]; out[2] = c[5]; out[3] = c[8];
+    out[0] = c[1]; out[1] = c[3]; out[2] = c[5]; out[3] = c[8]; out[4] = c[9]; out[5] = c[10];
   });
 }
 int rm_runner_get_states(rm_runner* r, uint32_t* a, uint32_t* b) { return guarded([&] { r->m->get_states(a, b); }); }
@@ -667,6 +697,17 @@ int rm_runner_get_reports(rm_runner* r, uint32_t* off, void* reps, void* stats) 
   return guarded([&] { r->m->get_reports(off, (ReportRec*)reps, (ReportStats*)stats); });
 }
 int rm_runner_set_timing(rm_runner* r, int on) { return guarded([&] { r->m->set_timing(on != 0); }); }
+int rm_runner_set_isolation(rm_runner* r, int on) { return guarded([&] { r->m->set_isolation(on != 0); }); }
+int rm_runner_trace_errors(rm_runner* r, uint32_t* errs) { return guarded([&] { r->m->get_trace_errors(errs); }); }
+int rm_report_segments(const rm_report_desc* d, uint32_t* rep_off, void* reps, void* stats) {
+  return guarded([&] {
+    if (!d || !rep_off || (d->n_traces && (!d->seg_off || !d->trace_end_time || !d->threshold_sec || !d->report_mask ||
+                                           !d->transition_mask || !stats)))
+      throw std::runtime_error("report descriptor or output is NULL");
+    report_segments(g_device, d->n_traces, d->seg_off, (const SegmentRec*)d->segs, d->trace_end_time, d->threshold_sec,
+                    d->report_mask, d->transition_mask, rep_off, (ReportRec*)reps, (ReportStats*)stats);
+  });
+}
 int rm_runner_kernel_times(rm_runner* r, double* ms, uint64_t* launches, int n) {
   return guarded([&] {
     double t[kNumKernels];
@@ -820,6 +861,9 @@ int rm_device_free(void* p) { return guarded([&] { RM_HIP(hipFree(p)); }); }
 int rm_device_memset(void* p, int v, size_t n) { return guarded([&] { RM_HIP(hipMemset(p, v, n)); }); }
 int rm_device_download(void* dst, const void* src, size_t n) {
   return guarded([&] { RM_HIP(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost)); });
+}
+int rm_device_upload(void* dst, const void* src, size_t n) {
+  return guarded([&] { RM_HIP(hipMemcpy(dst, src, n, hipMemcpyHostToDevice)); });
 }
 int rm_device_synchronize(void) { return guarded([&] { RM_HIP(hipDeviceSynchronize()); }); }
 

@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <type_traits>
 
 #include "engine.hpp"
 
@@ -67,11 +68,22 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint8_t* run_kind; uint32_t* run_head; uint32_t* run_idx; uint32_t* run_pos;
   ReportRec* reps; uint32_t* rep_cnt; ReportStats* stats;
   // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
-  // [5] routes list B [6] paths list B [7] candidates list
+  // [5] routes list B [6] paths list B [7] candidates list [8] path ball hand-overs
+  // [9] routes list C [10] paths list C (the global-memory search tier)
   uint32_t* rl_routes_0;  // items the K2 ball tier hands to the search tiers (count ctl[1])
   uint32_t* ctl; uint32_t* rl_routes_a; uint32_t* rl_routes_b; uint32_t* rl_paths_a; uint32_t* rl_paths_b;
   uint32_t* rl_cand;
+  uint32_t* rl_routes_c; uint32_t* rl_paths_c;
+  uint32_t* trace_err;    // per trace: error bits of that trace only (the rest of the batch is unaffected)
 };
+
+// A failure that belongs to one trajectory (too many roads in a radius, a search beyond every
+// tier's capacity, a path that cannot be rebuilt) marks that trace only, as the reference fails
+// one request (py/reporter_service.py:244-245) or skips one window (py/simple_reporter.py:169-173).
+__device__ __forceinline__ void trace_fail(const DevBatch& b, uint64_t p, uint32_t bit) {
+  atomicOr(&b.trace_err[b.slot_trace[p]], bit);
+  atomicOr(&b.ctl[2], bit);
+}
 
 __device__ __forceinline__ bool edge_ok(uint32_t info, uint32_t acc) { return (((info >> 16) & 7u) & acc) != 0u; }
 __device__ __forceinline__ uint64_t edge_key(const uint4& r, int mode) {
@@ -404,7 +416,7 @@ __device__ void cand_wave_one(const DevGraph& g, const DevBatch& b, CandSmem& sm
     n_found = sm.used;
   }
   if (n_found > kCandH * 3 / 4) {  // too many roads inside the radius
-    if (lane == 0) atomicOr(&b.ctl[2], kErrCandOverflow);
+    if (lane == 0) trace_fail(b, p, kErrCandOverflow);
     n_found = 0;
   }
   // rank by (sq, road); keep the first 16
@@ -524,9 +536,10 @@ __device__ __forceinline__ void exit_keys(const uint4& a0, uint32_t bound, unsig
 // Bounded search shared by the wave tiers of K2 (routes) and of the path kernel.
 template <int H, bool PATH>
 struct SearchSmem {
+  using FIdx = typename std::conditional<(H > 65536), uint32_t, uint16_t>::type;
   uint32_t key[H];                 // (source << 28) | node
   unsigned long long lab[H];       // u64 (dist cm, time ms) key
-  uint16_t fa[H], fb[H];           // frontier (slot ids), ping-pong
+  FIdx fa[H], fb[H];               // frontier (slot ids), ping-pong
   uint32_t inq[H];
   uint32_t pred[PATH ? H : 1];
   uint32_t nf, nn, used, ovf;
@@ -595,7 +608,7 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
       const int slot = h_insert(sm, (i << 28) | node);
       if (slot >= 0) {
         const unsigned long long old = atomicMin(&sm.lab[slot], kk);
-        if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[atomicAdd(&sm.nf, 1u)] = (uint16_t)slot;
+        if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[atomicAdd(&sm.nf, 1u)] = (typename SearchSmem<H, PATH>::FIdx)slot;
       }
     }
   }
@@ -604,8 +617,8 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
     const uint32_t nf = sm.nf;
     if (nf == 0 || sm.ovf) break;
     if (round > 4 * H) { if (lane == 0) sm.ovf = 2u; break; }
-    uint16_t* cur = (round & 1) ? sm.fb : sm.fa;
-    uint16_t* nxt = (round & 1) ? sm.fa : sm.fb;
+    typename SearchSmem<H, PATH>::FIdx* cur = (round & 1) ? sm.fb : sm.fa;
+    typename SearchSmem<H, PATH>::FIdx* nxt = (round & 1) ? sm.fa : sm.fb;
     for (uint32_t q = lane; q < nf; q += kWave) sm.inq[cur[q]] = 0u;
     __syncthreads();
     for (uint32_t q = lane; q < nf; q += kWave) {
@@ -622,7 +635,7 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
         const int t = h_insert(sm, srcbits | rec.x);
         if (t < 0) continue;
         const unsigned long long old = atomicMin(&sm.lab[t], nk);
-        if (nk < old && atomicExch(&sm.inq[t], 1u) == 0u) nxt[atomicAdd(&sm.nn, 1u)] = (uint16_t)t;
+        if (nk < old && atomicExch(&sm.inq[t], 1u) == 0u) nxt[atomicAdd(&sm.nn, 1u)] = (typename SearchSmem<H, PATH>::FIdx)t;
       }
     }
     __syncthreads();
@@ -1064,7 +1077,7 @@ __device__ __forceinline__ void path_walk(const DevGraph& g, const DevBatch& b, 
 #pragma unroll
   for (int q = 0; q < kInlinePath; ++q) pr[q] = entry_e;
   for (int guard = 0;; ++guard) {
-    if (lx == kKeyInf || guard > cap) { atomicOr(&b.ctl[2], kErrRounds); return; }
+    if (lx == kKeyInf || guard > cap) { trace_fail(b, p, kErrRounds); return; }
     if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
     uint32_t pe = kNone, pu = 0;
     unsigned long long plu = kKeyInf;
@@ -1077,7 +1090,7 @@ __device__ __forceinline__ void path_walk(const DevGraph& g, const DevBatch& b, 
       const unsigned long long lu = lab(u, rec.w >> 1, rec.w & 1u);
       if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { pe = e; pu = u; plu = lu; break; }
     }
-    if (pe == kNone) { atomicOr(&b.ctl[2], kErrRounds); return; }
+    if (pe == kNone) { trace_fail(b, p, kErrRounds); return; }
 #pragma unroll
     for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
     pr[0] = pe;
@@ -1242,37 +1255,62 @@ __global__ void __launch_bounds__(64) k_paths_lds(DevGraph g, DevBatch b) {
 
 // ------------------------------------------------------------------------------------------
 // K2 wave tier: one wave per (pair, source) item that outgrew both lane tiers; the
-// source is searched alone in a 4096-slot LDS hash.
-__global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
-  constexpr int H = kBigH;
-  __shared__ SearchSmem<H, false> sm;
-  __shared__ uint4 s_src[2];
+// source is searched alone in a hash of H (source, node) labels.  Returns false when the
+// search outgrew the hash (the caller hands the item to the next tier).
+template <int H>
+__device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const DevGraph& g, const DevBatch& b,
+                                   uint32_t t) {
   const int lane = threadIdx.x;
+  const uint64_t p = b.src_item[t];
+  const uint4 pi = b.pair_info[p];
+  const uint32_t i = t - b.src_off[p];
+  const uint32_t KB = (pi.z >> 8) & 0xffu;
+  const int mode = (int)(pi.z >> 16);
+  const uint32_t bound = pi.x, tmax = pi.y;
+  const uint32_t base = b.trans_off[p];
+  if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
+  __syncthreads();
+  bounded_search<H, false>(sm, g, mode, bound, s_src, 1);
+  const bool ok = !sm.ovf;
+  if (ok) {
+    for (uint32_t j = lane; j < KB; j += kWave) {
+      const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+      const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, nullptr);
+      uint32_t out = kRouteInvalid;
+      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
+      b.route[base + i * KB + j] = out;
+    }
+  }
+  __syncthreads();
+  return ok;
+}
+
+__global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
+  __shared__ SearchSmem<kBigH, false> sm;
+  __shared__ uint4 s_src[2];
   const uint32_t n_items = b.ctl[5];
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const uint32_t t = b.rl_routes_b[item];
-    const uint64_t p = b.src_item[t];
-    const uint4 pi = b.pair_info[p];
-    const uint32_t i = t - b.src_off[p];
-    const uint32_t KB = (pi.z >> 8) & 0xffu;
-    const int mode = (int)(pi.z >> 16);
-    const uint32_t bound = pi.x, tmax = pi.y;
-    const uint32_t base = b.trans_off[p];
-    if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
-    __syncthreads();
-    bounded_search<H, false>(sm, g, mode, bound, s_src, 1);
-    if (sm.ovf) {
-      if (lane == 0) atomicOr(&b.ctl[2], kErrSearchOverflow);
-    } else {
-      for (uint32_t j = lane; j < KB; j += kWave) {
-        const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-        const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, nullptr);
-        uint32_t out = kRouteInvalid;
-        if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
-        b.route[base + i * KB + j] = out;
-      }
-    }
-    __syncthreads();
+    if (!routes_search_item<kBigH>(sm, s_src, g, b, t) && threadIdx.x == 0) b.rl_routes_c[atomicAdd(&b.ctl[9], 1u)] = t;
+  }
+}
+
+// Global-memory tier (routes and paths): searches that outgrew the 4096-slot LDS hash (route
+// bounds of many kilometres: sparse sampling with a large breakage_distance) run here with a
+// kGlobalH-slot hash in a per-block global scratch.  What outgrows even this fails ITS trace
+// only (trace_err), never the batch.
+constexpr int kGlobalH = 1 << 17;
+constexpr int kGlobalGrid = 32;
+using GlobalRouteSmem = SearchSmem<kGlobalH, false>;
+using GlobalPathSmem = SearchSmem<kGlobalH, true>;
+
+__global__ void __launch_bounds__(64) k_routes_global(DevGraph g, DevBatch b, GlobalPathSmem* scratch) {
+  __shared__ uint4 s_src[2];
+  GlobalRouteSmem& sm = *reinterpret_cast<GlobalRouteSmem*>(scratch + blockIdx.x);
+  const uint32_t n_items = b.ctl[9];
+  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const uint32_t t = b.rl_routes_c[item];
+    if (!routes_search_item<kGlobalH>(sm, s_src, g, b, t) && threadIdx.x == 0) trace_fail(b, b.src_item[t], kErrSearchOverflow);
   }
 }
 
@@ -1529,104 +1567,112 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
 // ------------------------------------------------------------------------------------------
 // k_paths wave tiers: one wave per chosen transition whose search outgrew the lane tier;
 // re-run the search for (i*, j*), compute canonical predecessors and write the
-// directed-edge path.
-template <bool BIG>
-__global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
-  constexpr int H = BIG ? kBigH : kSmallH;
-  __shared__ SearchSmem<H, true> sm;
-  __shared__ uint4 s_src[2];
+// directed-edge path.  Returns false when the search outgrew the hash (next tier).
+template <int H>
+__device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const DevGraph& g, const DevBatch& b,
+                                  uint64_t p) {
   const int lane = threadIdx.x;
-  static_assert(BIG, "the small path wave tier was replaced by the LDS lane tier");
+  const uint4 pi = b.pair_info[p];
+  const int mode = (int)(pi.z >> 16);
+  const uint32_t acc = mode_access(mode);
+  const uint32_t bound = pi.x;
+  const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+  const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+  if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
+  __syncthreads();
+  const uint4 a0 = s_src[0], a1 = s_src[1];
+  bounded_search<H, true>(sm, g, mode, bound, s_src, 1);
+  if (sm.ovf) {
+    __syncthreads();
+    return false;
+  }
+  int combo = -1;
+  const unsigned long long key = route_key(HashLabel<H, true>{sm, 0u}, a0, b0, b1, &combo);
+  unsigned long long rk1, rk0;
+  exit_keys(a0, bound, rk1, rk0);   // root keys of the source exits (only roots within the bound exist)
+  const uint32_t n1a = a1.y, n0a = a1.x;
+  if (combo >= 2) {
+    // canonical predecessors: min edge id among tight in-edges of non-root nodes
+    for (int h = lane; h < H; h += kWave) {
+      const uint32_t ku = sm.key[h];
+      if (ku == kEmpty) continue;
+      const unsigned long long lu = sm.lab[h];
+      if (lu == kKeyInf) continue;
+      const uint32_t u = ku & 0x0fffffffu;
+      for (uint32_t e = g.node_off[u]; e < g.node_off[u + 1]; ++e) {
+        const uint4 rec = g.edges[e];
+        if (!edge_ok(rec.z, acc)) continue;
+        const int hv = h_find(sm, rec.x);
+        if (hv < 0) continue;
+        const unsigned long long lv = sm.lab[hv];
+        if (lv == kKeyInf) continue;
+        if ((rec.x == n1a && lv == rk1) || (rec.x == n0a && lv == rk0)) continue;
+        if (lu + edge_key(rec, mode) == lv) atomicMin(&sm.pred[hv], e);
+      }
+    }
+    __syncthreads();
+  }
+  // walk the canonical predecessors once (lane 0) into an LDS buffer that reuses the
+  // frontier arrays (H u32), then copy in travel order: inline slot when short, pool else
+  uint32_t* pbuf = reinterpret_cast<uint32_t*>(sm.fa);
+  if (lane == 0) {
+    uint32_t n = 0;
+    if (combo <= 1) {
+      pbuf[n++] = combo == 0 ? g.road_fwd[a0.x] : g.road_rev[a0.x];
+    } else {
+      pbuf[n++] = combo == 2 ? g.road_fwd[b0.x] : g.road_rev[b0.x];   // entry edge (reversed order)
+      uint32_t x = combo == 2 ? b1.x : b1.y;
+      for (;;) {
+        const int hx = h_find(sm, x);
+        if (hx < 0 || n + 2 > (uint32_t)H) { trace_fail(b, p, kErrRounds); n = 0; break; }
+        const unsigned long long lx = sm.lab[hx];
+        if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
+        const uint32_t e = sm.pred[hx];
+        if (e == kNone) { trace_fail(b, p, kErrRounds); n = 0; break; }
+        pbuf[n++] = e;
+        x = g.edge_src[e];
+      }
+      if (n) pbuf[n++] = (x == n1a) ? g.road_fwd[a0.x] : g.road_rev[a0.x];  // exit edge
+    }
+    uint32_t at = 0;
+    if (n > (uint32_t)kInlinePath) {
+      at = atomicAdd(&b.ctl[0], n);
+      if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); at = kNone; }
+    }
+    b.path_cnt[p] = n;
+    b.path_off[p] = at;
+    b.route_dist[p] = key_dist(key);
+    sm.nf = n;
+    sm.nn = at;
+  }
+  __syncthreads();
+  {
+    const uint32_t n = sm.nf, at = sm.nn;
+    uint32_t* dst = n <= (uint32_t)kInlinePath ? b.path_inline + p * kInlinePath : (at == kNone ? nullptr : b.path_pool + at);
+    if (dst)
+      for (uint32_t q = lane; q < n; q += kWave) dst[q] = pbuf[n - 1 - q];
+  }
+  __syncthreads();
+  return true;
+}
+
+__global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
+  __shared__ SearchSmem<kBigH, true> sm;
+  __shared__ uint4 s_src[2];
   const uint32_t n_items = b.ctl[6];
-  const uint32_t* list = b.rl_paths_b;
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const uint64_t p = list[item];
-    const uint4 pi = b.pair_info[p];
-    const int mode = (int)(pi.z >> 16);
-    const uint32_t acc = mode_access(mode);
-    const uint32_t bound = pi.x;
-    const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
-    const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-    if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
-    __syncthreads();
-    const uint4 a0 = s_src[0], a1 = s_src[1];
-    bounded_search<H, true>(sm, g, mode, bound, s_src, 1);
-    if (sm.ovf) {
-      if (!BIG) {
-        if (lane == 0) { const uint32_t q = atomicAdd(&b.ctl[6], 1u); b.rl_paths_b[q] = (uint32_t)p; }
-      } else if (lane == 0) {
-        atomicOr(&b.ctl[2], kErrSearchOverflow);
-      }
-      __syncthreads();
-      continue;
-    }
-    int combo = -1;
-    const unsigned long long key = route_key(HashLabel<H, true>{sm, 0u}, a0, b0, b1, &combo);
-    unsigned long long rk1, rk0;
-    exit_keys(a0, bound, rk1, rk0);   // root keys of the source exits (only roots within the bound exist)
-    const uint32_t n1a = a1.y, n0a = a1.x;
-    if (combo >= 2) {
-      // canonical predecessors: min edge id among tight in-edges of non-root nodes
-      for (int h = lane; h < H; h += kWave) {
-        const uint32_t ku = sm.key[h];
-        if (ku == kEmpty) continue;
-        const unsigned long long lu = sm.lab[h];
-        if (lu == kKeyInf) continue;
-        const uint32_t u = ku & 0x0fffffffu;
-        for (uint32_t e = g.node_off[u]; e < g.node_off[u + 1]; ++e) {
-          const uint4 rec = g.edges[e];
-          if (!edge_ok(rec.z, acc)) continue;
-          const int hv = h_find(sm, rec.x);
-          if (hv < 0) continue;
-          const unsigned long long lv = sm.lab[hv];
-          if (lv == kKeyInf) continue;
-          if ((rec.x == n1a && lv == rk1) || (rec.x == n0a && lv == rk0)) continue;
-          if (lu + edge_key(rec, mode) == lv) atomicMin(&sm.pred[hv], e);
-        }
-      }
-      __syncthreads();
-    }
-    // walk the canonical predecessors once (lane 0) into an LDS buffer that reuses the
-    // frontier arrays (H u32), then copy in travel order: inline slot when short, pool else
-    uint32_t* pbuf = reinterpret_cast<uint32_t*>(sm.fa);
-    if (lane == 0) {
-      uint32_t n = 0;
-      if (combo <= 1) {
-        pbuf[n++] = combo == 0 ? g.road_fwd[a0.x] : g.road_rev[a0.x];
-      } else {
-        pbuf[n++] = combo == 2 ? g.road_fwd[b0.x] : g.road_rev[b0.x];   // entry edge (reversed order)
-        uint32_t x = combo == 2 ? b1.x : b1.y;
-        for (;;) {
-          const int hx = h_find(sm, x);
-          if (hx < 0 || n + 2 > (uint32_t)H) { atomicOr(&b.ctl[2], kErrRounds); n = 0; break; }
-          const unsigned long long lx = sm.lab[hx];
-          if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
-          const uint32_t e = sm.pred[hx];
-          if (e == kNone) { atomicOr(&b.ctl[2], kErrRounds); n = 0; break; }
-          pbuf[n++] = e;
-          x = g.edge_src[e];
-        }
-        if (n) pbuf[n++] = (x == n1a) ? g.road_fwd[a0.x] : g.road_rev[a0.x];  // exit edge
-      }
-      uint32_t at = 0;
-      if (n > (uint32_t)kInlinePath) {
-        at = atomicAdd(&b.ctl[0], n);
-        if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); at = kNone; }
-      }
-      b.path_cnt[p] = n;
-      b.path_off[p] = at;
-      b.route_dist[p] = key_dist(key);
-      sm.nf = n;
-      sm.nn = at;
-    }
-    __syncthreads();
-    {
-      const uint32_t n = sm.nf, at = sm.nn;
-      uint32_t* dst = n <= (uint32_t)kInlinePath ? b.path_inline + p * kInlinePath : (at == kNone ? nullptr : b.path_pool + at);
-      if (dst)
-        for (uint32_t q = lane; q < n; q += kWave) dst[q] = pbuf[n - 1 - q];
-    }
-    __syncthreads();
+    const uint32_t p = b.rl_paths_b[item];
+    if (!paths_search_item<kBigH>(sm, s_src, g, b, p) && threadIdx.x == 0) b.rl_paths_c[atomicAdd(&b.ctl[10], 1u)] = p;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_paths_global(DevGraph g, DevBatch b, GlobalPathSmem* scratch) {
+  __shared__ uint4 s_src[2];
+  GlobalPathSmem& sm = scratch[blockIdx.x];
+  const uint32_t n_items = b.ctl[10];
+  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const uint32_t p = b.rl_paths_c[item];
+    if (!paths_search_item<kGlobalH>(sm, s_src, g, b, p) && threadIdx.x == 0) trace_fail(b, p, kErrSearchOverflow);
   }
 }
 
@@ -1747,6 +1793,8 @@ __device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch
   const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
   const uint32_t r0 = b.trav_off[l];
   TravRec* out = b.trav + r0;
+  // a trace that failed (trace_err) forms no segments: its records become empty pieces
+  const bool bad = b.trace_err[k] != 0u;
   uint64_t x = 0;
   // four path edges per group: every graph load of a group is issued before its record
   // stores (loads after a pending store wait for it: shared vmcnt)
@@ -1773,6 +1821,7 @@ __device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch
       uint32_t b0 = 0, b1 = L;
       if (q == 0) b0 = rev ? L - sa : sa;
       if (q + 1 == ns) b1 = rev ? L - sb : sb;
+      if (bad) b0 = b1 = 0;
       TravRec t;
       t.e = e[y]; t.b = b0; t.en = b1;
       t.slot = (uint32_t)l | (q + 1 == ns ? kTravLast : 0u) | ((rec[y].z & kFlagInternal) ? kTravInternal : 0u);
@@ -1932,22 +1981,17 @@ __global__ void __launch_bounds__(256) k_runs(DevGraph g, DevBatch b, uint32_t t
 // ------------------------------------------------------------------------------------------
 // A8 k_report: reference report() per trace (py/reporter_service.py:79-179) + the batch
 // filter (py/simple_reporter.py:177) + per-segment 10 km/h speed histogram.
-__global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uint32_t rmask, uint32_t tmask,
-                                               uint32_t* hist) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= b.T) return;
-  const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
-  const SegmentRec* segs = b.segs + b.seg_base[k];
-  const uint32_t n = b.seg_cnt[k];
-  ReportRec* out = b.reps + b.seg_base[k];
+// report() of one trace over its segments: reports written to out, stats returned
+__device__ __forceinline__ ReportStats report_trace(const SegmentRec* segs, uint32_t n, bool has_pts, double end_time,
+                                                   double threshold, uint32_t rmask, uint32_t tmask, ReportRec* out,
+                                                   uint32_t* hist) {
   ReportStats st;
   st.successful_count = st.unreported_count = 0;
   st.successful_length_m = st.unreported_length_m = -1;
   st.discontinuities = st.invalid_speeds = st.invalid_times = st.unassociated = 0;
   st.shape_used = -1;
   int nrep = 0;
-  if (npts > 0) {
-    const double end_time = b.time[o + npts - 1];
+  if (has_pts) {
     int last = (int)n - 1;
     while (last >= 0 && end_time - segs[last].start_time < threshold) --last;
     if (last >= 0 && segs[last].begin_shape_index != 0) st.shape_used = (int32_t)segs[last].begin_shape_index;
@@ -1991,8 +2035,54 @@ __global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uin
     }
   }
   st.n_reports = nrep;
-  b.rep_cnt[k] = (uint32_t)nrep;
+  return st;
+}
+
+__global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uint32_t rmask, uint32_t tmask,
+                                               uint32_t* hist) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= b.T) return;
+  const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
+  const ReportStats st = report_trace(b.segs + b.seg_base[k], b.seg_cnt[k], npts > 0, npts ? b.time[o + npts - 1] : 0.0,
+                                      threshold, rmask, tmask, b.reps + b.seg_base[k], hist);
+  b.rep_cnt[k] = (uint32_t)st.n_reports;
   b.stats[k] = st;
+}
+
+// report() over host-supplied segment lists (rm_report_segments): per-trace end time,
+// threshold and level masks; reports of trace k start at seg_off[k]
+__global__ void __launch_bounds__(64) k_report_lists(uint32_t T, const uint32_t* seg_off, const SegmentRec* segs,
+                                                     const double* end_time, const double* threshold,
+                                                     const uint32_t* rmask, const uint32_t* tmask, ReportRec* reps,
+                                                     ReportStats* stats) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= T) return;
+  const uint32_t o = seg_off[k];
+  stats[k] = report_trace(segs + o, seg_off[k + 1] - o, true, end_time[k], threshold[k], rmask[k], tmask[k], reps + o,
+                          nullptr);
+}
+
+// u64 totals of one or two u32 count arrays: the u32 exclusive scans that lay out routes and
+// records would wrap silently past 2^32, so the host checks these totals instead of off+cnt
+__global__ void __launch_bounds__(256) k_sum_u64(const uint32_t* a, const uint32_t* c, uint64_t n,
+                                                 unsigned long long* out) {
+  __shared__ unsigned long long sa[256], sc[256];
+  unsigned long long va = 0, vc = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
+    va += a[i];
+    if (c) vc += c[i];
+  }
+  sa[threadIdx.x] = va;
+  sc[threadIdx.x] = vc;
+  __syncthreads();
+  for (int d = 128; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d) { sa[threadIdx.x] += sa[threadIdx.x + d]; sc[threadIdx.x] += sc[threadIdx.x + d]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(out, sa[0]);
+    if (c) atomicAdd(out + 1, sc[0]);
+  }
 }
 
 __global__ void k_fill_edge_src(const uint32_t* node_off, uint32_t n_nodes, uint32_t* edge_src) {
@@ -2215,12 +2305,16 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.ctl = dalloc<uint32_t>(L, kCtlWords);
   w.rl_paths_a = dalloc<uint32_t>(L, cp); w.rl_paths_b = dalloc<uint32_t>(L, cp);
   w.rl_cand = dalloc<uint32_t>(L, cp);
+  w.rl_paths_c = dalloc<uint32_t>(L, cp);
+  w.trace_err = dalloc<uint32_t>(L, ct);
+  w.tot64 = dalloc<unsigned long long>(L, 4);
   size_t tmp = 0;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, w.trans_cnt, w.trans_off, (int)cp, stream_));
   w.scan_tmp_bytes = tmp;
   w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
-  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
+  w.gsearch = nullptr;
+  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
   w.run_kind = nullptr; w.run_head = nullptr; w.run_idx = nullptr; w.run_pos = nullptr; w.seg_scan_tmp = nullptr;
   w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
   ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
@@ -2241,11 +2335,13 @@ void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
     if (w.rl_routes_a) { (void)hipFree(w.rl_routes_a); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_a)); }
     if (w.rl_routes_b) { (void)hipFree(w.rl_routes_b); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_b)); }
     if (w.rl_routes_0) { (void)hipFree(w.rl_routes_0); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_0)); }
+    if (w.rl_routes_c) { (void)hipFree(w.rl_routes_c); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_c)); }
     const uint64_t c = n_src + n_src / 4 + 1024;
     w.src_item = dalloc<uint32_t>(w.allocs, c);
     w.rl_routes_a = dalloc<uint32_t>(w.allocs, c);   // overflow lists hold (pair, source) items
     w.rl_routes_b = dalloc<uint32_t>(w.allocs, c);
     w.rl_routes_0 = dalloc<uint32_t>(w.allocs, c);
+    w.rl_routes_c = dalloc<uint32_t>(w.allocs, c);
     w.cap_src = c;
   }
 }
@@ -2345,6 +2441,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.reps = w.reps; v.rep_cnt = w.rep_cnt; v.stats = w.stats;
   v.ctl = w.ctl; v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
   v.rl_paths_a = w.rl_paths_a; v.rl_paths_b = w.rl_paths_b; v.rl_cand = w.rl_cand;
+  v.rl_routes_c = w.rl_routes_c; v.rl_paths_c = w.rl_paths_c; v.trace_err = w.trace_err;
   return v;
 }
 
@@ -2378,20 +2475,51 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
   run_device(rp);
 }
 
+// global-memory search scratch (kGlobalGrid blocks), allocated the first time a search
+// outgrows the LDS wave tier
+void Matcher::ensure_global_search() {
+  if (ws_.gsearch) return;
+  ws_.gsearch = dalloc<char>(ws_.allocs, (uint64_t)kGlobalGrid * sizeof(GlobalPathSmem));
+}
+
+// read the control words (and nothing else) into hctl_[0..kCtlWords)
+void Matcher::read_ctl() {
+  RM_HIP(hipMemcpyAsync(hctl_, ws_.ctl, kCtlWords * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  RM_HIP(hipStreamSynchronize(stream_));
+}
+
+const char* error_text(uint32_t bits) {
+  if (bits & kErrCandOverflow) return "too many candidate roads inside the search radius (limit 192)";
+  if (bits & kErrSearchOverflow) return "route search exceeded its label capacity (bound too large for this graph)";
+  if (bits & kErrRounds) return "route search did not converge / path reconstruction failed";
+  return "";
+}
+
+// limits of the u32 layouts: route / record offsets are u32 and the record scans take int counts
+// that the workspace pads by 1/4 (ensure_segs), so totals must stay below INT32_MAX / 1.25
+constexpr uint64_t kMaxTransitions = 0xF0000000ull;
+constexpr uint64_t kMaxRecords = 1700000000ull;
+
 void Matcher::run_device(const RunParams& rp) {
   RM_HIP(hipSetDevice(eng_->device()));
   const uint32_t T = n_traces_;
   const uint64_t P = n_points_;
+  err_bits_ = 0;
   if (T == 0) return;
+  if (P >= (uint64_t)kTravLast) throw std::runtime_error("batch too large (slots >= 2^30); split it");  // TravRec::slot flags
   Workspace& w = ws_;
   hipStream_t st = stream_;
   eng_->ensure_balls(mode_mask_);
   const DevGraph g = eng_->dev_snapshot();
-  if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 16 * sizeof(uint32_t), hipHostMallocDefault));
+  if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 32 * sizeof(uint32_t), hipHostMallocDefault));
+  unsigned long long* htot = reinterpret_cast<unsigned long long*>(hctl_ + 16);
   RM_HIP(hipMemsetAsync(w.ctl, 0, kCtlWords * sizeof(uint32_t), st));
   RM_HIP(hipMemsetAsync(w.choice, 0xff, P, st));
   RM_HIP(hipMemsetAsync(w.path_cnt, 0, P * sizeof(uint32_t), st));
+  RM_HIP(hipMemsetAsync(w.trace_err, 0, T * sizeof(uint32_t), st));
+  RM_HIP(hipMemsetAsync(w.tot64, 0, 4 * sizeof(unsigned long long), st));
   DevBatch v = make_view(w, T, P);
+  const uint32_t sum_grid = (uint32_t)std::min<uint64_t>((P + 255) / 256, 1024);
 
   tic(kKStates);
   hipLaunchKernelGGL(k_states, dim3((T + 63) / 64), dim3(64), 0, st, v);
@@ -2406,15 +2534,13 @@ void Matcher::run_device(const RunParams& rp) {
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.trans_cnt, w.trans_off, (int)P, st));
   tmp = w.scan_tmp_bytes;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.src_cnt, w.src_off, (int)P, st));
+  hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.trans_cnt, w.src_cnt, P, w.tot64);
   toc(kKScan);
-  RM_HIP(hipMemcpyAsync(hctl_ + 8, w.trans_off + (P - 1), 4, hipMemcpyDeviceToHost, st));
-  RM_HIP(hipMemcpyAsync(hctl_ + 9, w.trans_cnt + (P - 1), 4, hipMemcpyDeviceToHost, st));
-  RM_HIP(hipMemcpyAsync(hctl_ + 12, w.src_off + (P - 1), 4, hipMemcpyDeviceToHost, st));
-  RM_HIP(hipMemcpyAsync(hctl_ + 13, w.src_cnt + (P - 1), 4, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipMemcpyAsync(htot, w.tot64, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   RM_HIP(hipStreamSynchronize(st));
-  const uint64_t total = (uint64_t)hctl_[8] + hctl_[9];
-  const uint64_t n_src = (uint64_t)hctl_[12] + hctl_[13];
-  if (total >= 0xffffffffull) throw std::runtime_error("batch too large (transitions >= 2^32); split it");
+  const uint64_t total = htot[0];
+  const uint64_t n_src = htot[1];
+  if (total >= kMaxTransitions) throw std::runtime_error("batch too large (transitions >= 0xF0000000); split it");
   n_trans_ = total;
   ensure_trans(total, n_src);
   v.route = w.route;
@@ -2422,6 +2548,7 @@ void Matcher::run_device(const RunParams& rp) {
   v.rl_routes_a = w.rl_routes_a;
   v.rl_routes_b = w.rl_routes_b;
   v.rl_routes_0 = w.rl_routes_0;
+  v.rl_routes_c = w.rl_routes_c;
 
   const bool balls = (mode_mask_ & ~g.ball_mask) == 0u;   // every mode of the batch has its route balls
   tic(kKRoutes);
@@ -2444,14 +2571,20 @@ void Matcher::run_device(const RunParams& rp) {
   hipLaunchKernelGGL(k_routes_reg2, dim3(kLdsGrid / 4), dim3(256), 0, st, g, v);
 #endif
   hipLaunchKernelGGL(k_routes_wave, dim3(1024), dim3(64), 0, st, g, v);
+  // the global tier runs in line once its scratch exists; before that, a hand-over seen at the
+  // path-stage read-back allocates it and re-runs K3 (rare: bounds of many kilometres)
+  bool routes_global_done = w.gsearch != nullptr;
+  if (routes_global_done)
+    hipLaunchKernelGGL(k_routes_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
   toc(kKRoutes);
   tic(kKViterbi);
   hipLaunchKernelGGL(k_viterbi, dim3((T + 3) / 4), dim3(64), 0, st, v);
   toc(kKViterbi);
   for (int attempt = 0;; ++attempt) {
     tic(kKPaths);
+    RM_HIP(hipMemsetAsync(w.ctl + 8, 0, sizeof(uint32_t), st));    // path ball hand-overs
+    RM_HIP(hipMemsetAsync(w.ctl + 10, 0, sizeof(uint32_t), st));   // paths list C
     if (balls) {
-      RM_HIP(hipMemsetAsync(w.ctl + 8, 0, sizeof(uint32_t), st));
       hipLaunchKernelGGL(k_paths_ball, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>((P + 255) / 256, kListedGrid)), dim3(256), 0,
                          st, g, v, 1);
@@ -2463,23 +2596,46 @@ void Matcher::run_device(const RunParams& rp) {
 #else
     hipLaunchKernelGGL(k_paths_reg2, dim3(kLdsGrid / 4), dim3(256), 0, st, g, v);
 #endif
-    hipLaunchKernelGGL(k_paths_wave<true>, dim3(1024), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_wave, dim3(1024), dim3(64), 0, st, g, v);
+    if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
     toc(kKPaths);
     // traversal records are laid out by a scan of path_cnt (0 for slots without a chosen transition)
     tic(kKSegments);
     tmp = w.scan_tmp_bytes;
     RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
+    RM_HIP(hipMemsetAsync(w.tot64 + 2, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, (const uint32_t*)nullptr, P, w.tot64 + 2);
     toc(kKSegments);
-    RM_HIP(hipMemcpyAsync(hctl_ + 10, w.trav_off + (P - 1), 4, hipMemcpyDeviceToHost, st));
-    RM_HIP(hipMemcpyAsync(hctl_ + 11, w.path_cnt + (P - 1), 4, hipMemcpyDeviceToHost, st));
-    RM_HIP(hipMemcpyAsync(hctl_, w.ctl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    RM_HIP(hipStreamSynchronize(st));
+    RM_HIP(hipMemcpyAsync(htot + 2, w.tot64 + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    read_ctl();
+    if (!routes_global_done && hctl_[9]) {
+      // routes outgrew the LDS wave tier: run them in the global tier, then K3 and paths again
+      ensure_global_search();
+      routes_global_done = true;
+      hipLaunchKernelGGL(k_routes_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
+      hipLaunchKernelGGL(k_viterbi, dim3((T + 3) / 4), dim3(64), 0, st, v);
+      RM_HIP(hipMemsetAsync(w.path_cnt, 0, P * sizeof(uint32_t), st));
+      for (int c : {0, 4, 6}) RM_HIP(hipMemsetAsync(w.ctl + c, 0, sizeof(uint32_t), st));
+      uint32_t flags = hctl_[2] & ~kErrPathOverflow;
+      RM_HIP(hipMemcpyAsync(w.ctl + 2, &flags, sizeof(uint32_t), hipMemcpyHostToDevice, st));
+      RM_HIP(hipStreamSynchronize(st));
+      continue;
+    }
+    if (!w.gsearch && hctl_[10]) {
+      // chosen transitions whose path search outgrew the LDS wave tier
+      ensure_global_search();
+      hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
+      tmp = w.scan_tmp_bytes;
+      RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
+      RM_HIP(hipMemsetAsync(w.tot64 + 2, 0, sizeof(unsigned long long), st));
+      hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, (const uint32_t*)nullptr, P, w.tot64 + 2);
+      RM_HIP(hipMemcpyAsync(htot + 2, w.tot64 + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+      read_ctl();
+    }
     if (!(hctl_[2] & kErrPathOverflow)) break;
     if (attempt > 3) throw std::runtime_error("path pool overflow persists");
     ensure_path((uint64_t)hctl_[0]);
     v.path_pool = w.path_pool; v.path_cap = w.cap_path;
-    const uint32_t clear_bits = ~kErrPathOverflow;
-    (void)clear_bits;
     RM_HIP(hipMemsetAsync(w.ctl, 0, sizeof(uint32_t), st));          // path_used
     RM_HIP(hipMemsetAsync(w.ctl + 4, 0, sizeof(uint32_t), st));      // paths list A
     RM_HIP(hipMemsetAsync(w.ctl + 6, 0, sizeof(uint32_t), st));      // paths list B
@@ -2487,9 +2643,8 @@ void Matcher::run_device(const RunParams& rp) {
     RM_HIP(hipMemcpyAsync(w.ctl + 2, &flags, sizeof(uint32_t), hipMemcpyHostToDevice, st));
     RM_HIP(hipStreamSynchronize(st));
   }
-  const uint64_t seg_total = (uint64_t)hctl_[10] + hctl_[11];
-  if (seg_total >= 0xffffffffull) throw std::runtime_error("batch too large (path edges >= 2^32); split it");
-  if (P >= (uint64_t)kTravLast) throw std::runtime_error("batch too large (slots >= 2^30); split it");  // TravRec::slot flags
+  const uint64_t seg_total = htot[2];
+  if (seg_total >= kMaxRecords) throw std::runtime_error("batch too large (path edges >= 1.7e9); split it");
   n_path_ = seg_total;  // one traversal record (and at most one segment) per chosen path edge
   ensure_segs(seg_total);
   v.segs = w.segs; v.reps = w.reps; v.trav = w.trav;
@@ -2513,14 +2668,58 @@ void Matcher::run_device(const RunParams& rp) {
     toc(kKReport);
   }
   RM_HIP(hipGetLastError());
-  RM_HIP(hipMemcpyAsync(hctl_, w.ctl, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  RM_HIP(hipMemcpyAsync(hctl_, w.ctl, kCtlWords * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   sync();
   seg_used_ = seg_total;
-  const uint32_t err = hctl_[2];
-  if (err & kErrCandOverflow) throw std::runtime_error("too many candidate roads inside the search radius (limit 192)");
-  if (err & kErrSearchOverflow) throw std::runtime_error("route search exceeded its label capacity (bound too large for this graph)");
-  if (err & kErrRounds) throw std::runtime_error("route search did not converge / path reconstruction failed");
   has_report_ = rp.do_report != 0;
+  err_bits_ = hctl_[2] & (kErrCandOverflow | kErrSearchOverflow | kErrRounds);
+  if (err_bits_ && !isolate_) throw std::runtime_error(error_text(err_bits_));
+}
+
+void Matcher::get_trace_errors(uint32_t* out) {
+  sync();
+  if (n_traces_) RM_HIP(hipMemcpy(out, ws_.trace_err, n_traces_ * 4ull, hipMemcpyDeviceToHost));
+}
+
+// report() on host-supplied segment lists, one thread per trace (rm_report_segments)
+void report_segments(int device, uint32_t T, const uint32_t* seg_off, const SegmentRec* segs, const double* end_time,
+                     const double* threshold, const uint32_t* rmask, const uint32_t* tmask, uint32_t* rep_off,
+                     ReportRec* reps, ReportStats* stats) {
+  RM_HIP(hipSetDevice(device));
+  if (T == 0) { rep_off[0] = 0; return; }
+  for (uint32_t k = 0; k < T; ++k)
+    if (seg_off[k + 1] < seg_off[k]) throw std::runtime_error("segment offsets not monotone");
+  const uint64_t S = seg_off[T];
+  std::vector<void*> L;
+  struct Free { std::vector<void*>& l; ~Free() { for (void* p : l) (void)hipFree(p); } } fr{L};
+  uint32_t* d_off = dalloc<uint32_t>(L, T + 1);
+  SegmentRec* d_segs = dalloc<SegmentRec>(L, S);
+  double* d_end = dalloc<double>(L, T);
+  double* d_thr = dalloc<double>(L, T);
+  uint32_t* d_rm = dalloc<uint32_t>(L, T);
+  uint32_t* d_tm = dalloc<uint32_t>(L, T);
+  ReportRec* d_reps = dalloc<ReportRec>(L, S);
+  ReportStats* d_st = dalloc<ReportStats>(L, T);
+  RM_HIP(hipMemcpy(d_off, seg_off, (T + 1) * 4ull, hipMemcpyHostToDevice));
+  if (S) RM_HIP(hipMemcpy(d_segs, segs, S * sizeof(SegmentRec), hipMemcpyHostToDevice));
+  RM_HIP(hipMemcpy(d_end, end_time, T * 8ull, hipMemcpyHostToDevice));
+  RM_HIP(hipMemcpy(d_thr, threshold, T * 8ull, hipMemcpyHostToDevice));
+  RM_HIP(hipMemcpy(d_rm, rmask, T * 4ull, hipMemcpyHostToDevice));
+  RM_HIP(hipMemcpy(d_tm, tmask, T * 4ull, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_report_lists, dim3((T + 63) / 64), dim3(64), 0, 0, T, d_off, d_segs, d_end, d_thr, d_rm, d_tm,
+                     d_reps, d_st);
+  RM_HIP(hipGetLastError());
+  std::vector<ReportRec> all(S);
+  if (S) RM_HIP(hipMemcpy(all.data(), d_reps, S * sizeof(ReportRec), hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(stats, d_st, T * sizeof(ReportStats), hipMemcpyDeviceToHost));
+  uint64_t at = 0;
+  for (uint32_t k = 0; k < T; ++k) {
+    rep_off[k] = (uint32_t)at;
+    const uint32_t c = (uint32_t)stats[k].n_reports;
+    if (c) std::memcpy(reps + at, all.data() + seg_off[k], c * sizeof(ReportRec));
+    at += c;
+  }
+  rep_off[T] = (uint32_t)at;
 }
 
 // ---- downloads ----

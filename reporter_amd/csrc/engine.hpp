@@ -116,9 +116,14 @@ struct Workspace {
   ReportRec* reps = nullptr; uint32_t* rep_cnt = nullptr; ReportStats* stats = nullptr;
   // control words (kCtlWords): [0] path pool used [1] K2 ball-tier hand-over list [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list (overflow lists of the lane tiers)
+  // [8] path ball-tier hand-overs [9] routes list C [10] paths list C (global-memory tier)
   uint32_t* ctl = nullptr;
   uint32_t* rl_routes_a = nullptr; uint32_t* rl_routes_b = nullptr; uint32_t* rl_routes_0 = nullptr;
   uint32_t* rl_paths_a = nullptr; uint32_t* rl_paths_b = nullptr; uint32_t* rl_cand = nullptr;
+  // global-memory search tier: its hand-over lists (ctl[9] routes, ctl[10] paths) and scratch
+  uint32_t* rl_routes_c = nullptr; uint32_t* rl_paths_c = nullptr; void* gsearch = nullptr;
+  uint32_t* trace_err = nullptr;            // per trace: error bits (kErr*) of that trace alone
+  unsigned long long* tot64 = nullptr;      // u64 totals: [0] transitions [1] sources [2] path edges
   void* scan_tmp = nullptr; size_t scan_tmp_bytes = 0;
   std::vector<void*> allocs;
   ~Workspace();
@@ -181,10 +186,19 @@ struct StageBufs {  // grow-only device buffers of the windowing and tile stages
   ~StageBufs();
 };
 
-// error bits in ctl[2]
+// error bits in ctl[2] (and, except the path pool, per trace in Workspace::trace_err)
 constexpr uint32_t kErrCandOverflow = 1u, kErrSearchOverflow = 2u, kErrPathOverflow = 4u, kErrRounds = 8u;
+// message of the first error bit set in `bits` ("" for none)
+const char* error_text(uint32_t bits);
 
 class Engine;
+
+// report() (reference py/reporter_service.py:79-179) on the device over host-supplied segment
+// lists: trace k's segments are segs[seg_off[k] .. seg_off[k+1]); reports come back compacted
+// (rep_off, T+1) with per-trace stats.  reps must hold seg_off[T] records.
+void report_segments(int device, uint32_t T, const uint32_t* seg_off, const SegmentRec* segs, const double* end_time,
+                     const double* threshold, const uint32_t* rmask, const uint32_t* tmask, uint32_t* rep_off,
+                     ReportRec* reps, ReportStats* stats);
 
 // RCCL communicator handed to the tile stage (one process per GPU)
 struct TileComm {
@@ -230,6 +244,13 @@ class Matcher {
   void ctl_words(uint32_t* out);
   void reset_kernel_times();
   void set_timing(bool on) { timing_ = on; }
+  // Failure isolation: off (default), a trace that fails (kErrCandOverflow / kErrSearchOverflow /
+  // kErrRounds) makes run() throw; on, run() returns, the failed traces carry no segments or
+  // reports and their bits are in get_trace_errors().  The reference fails one request
+  // (py/reporter_service.py:244-245) or skips one window (py/simple_reporter.py:169-173).
+  void set_isolation(bool on) { isolate_ = on; }
+  uint32_t error_bits() const { return err_bits_; }   // OR of the last run's per-trace errors
+  void get_trace_errors(uint32_t* out);                // n_traces() words
   hipStream_t stream() const { return stream_; }
 
   // Raw point stream -> per-vehicle time sort and inactivity windows of >= 2 points on the
@@ -249,6 +270,8 @@ class Matcher {
   void ensure_trans(uint64_t n, uint64_t n_src);
   void ensure_path(uint64_t n);
   void ensure_segs(uint64_t n);
+  void ensure_global_search();
+  void read_ctl();
   void tic(int k);
   void toc(int k);
   void harvest_times();
@@ -260,6 +283,8 @@ class Matcher {
   uint64_t n_points_ = 0, n_trans_ = 0, n_path_ = 0, seg_used_ = 0;
   bool timing_ = false;
   bool has_report_ = false;
+  bool isolate_ = false;
+  uint32_t err_bits_ = 0;
   uint32_t* hctl_ = nullptr;  // pinned host mirror of the control words
   StageBufs sb_;
   bool from_points_ = false;

@@ -90,6 +90,8 @@ struct TraceSet {
   std::vector<uint32_t> truth_off_cm;   // offset along that edge
 };
 
-TraceSet generate_traces(const Graph& g, const TraceParams& p);
+// p.n_traces traces; with ids, slot k holds trace ids[k] of the seeded set (the same trace
+// the full set has at index ids[k]): a rank generates exactly its uuid shard
+TraceSet generate_traces(const Graph& g, const TraceParams& p, const uint32_t* ids = nullptr);
 
 }  // namespace rm

@@ -473,8 +473,9 @@ std::string Matcher::tiles(const TileParams& tp, TileComm* comm) {
     ensure_rows(R, T);
     if (R) hipLaunchKernelGGL(k_tile_emit, dim3(grid(T, 64)), dim3(64), 0, st, a, ofs, s.rows);
   }
-  // ---- RCCL: all-gather every rank's rows, keep the files this rank owns
-  if (comm && comm->nranks > 1) {
+  // ---- RCCL: all-gather every rank's rows, keep the files this rank owns (a one-rank
+  // communicator runs the same collectives, so the path is exercised on a single GPU)
+  if (comm) {
     ncclComm_t nc = (ncclComm_t)comm->nccl;
     double* scratch = nullptr;
     RM_HIP(hipMalloc(&scratch, 8));

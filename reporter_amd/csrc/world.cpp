@@ -473,11 +473,12 @@ uint32_t pick_destination(const Graph& g, Rng& r, uint32_t from, double remainin
   return ring != kNone ? ring : best;
 }
 
-void gen_one(const Graph& g, const TraceParams& p, uint32_t k, TraceSet& ts, const std::vector<uint32_t>& starts,
-             RoutePlanner& planner) {
+// trace number k of the seeded set (its own RNG stream), written to output slot `slot`
+void gen_one(const Graph& g, const TraceParams& p, uint32_t k, uint32_t slot, TraceSet& ts,
+             const std::vector<uint32_t>& starts, RoutePlanner& planner) {
   Rng r(mix(p.seed, 0x7472616365ull + k));
   const uint32_t acc = mode_access(p.mode);
-  const uint32_t base = ts.trace_off[k];
+  const uint32_t base = ts.trace_off[slot];
   // start edge
   uint32_t e = starts[r.below((uint32_t)starts.size())];
   double off_m = r.uniform() * g.edges[e].len_cm * 0.01;
@@ -560,7 +561,7 @@ void gen_one(const Graph& g, const TraceParams& p, uint32_t k, TraceSet& ts, con
 
 }  // namespace
 
-TraceSet generate_traces(const Graph& g, const TraceParams& p) {
+TraceSet generate_traces(const Graph& g, const TraceParams& p, const uint32_t* ids) {
   TraceSet ts;
   const uint64_t P = (uint64_t)p.n_traces * p.n_points;
   if (P > 0xffffffffull) throw std::runtime_error("too many points for one trace set");
@@ -583,7 +584,7 @@ TraceSet generate_traces(const Graph& g, const TraceParams& p) {
   for (unsigned t = 0; t < nt; ++t)
     th.emplace_back([&, t] {
       RoutePlanner planner(g, p.mode);
-      for (uint32_t k = t; k < p.n_traces; k += nt) gen_one(g, p, k, ts, starts, planner);
+      for (uint32_t k = t; k < p.n_traces; k += nt) gen_one(g, p, ids ? ids[k] : k, k, ts, starts, planner);
     });
   for (auto& x : th) x.join();
   return ts;

@@ -135,6 +135,12 @@ class DeviceBuffer:
         _lib.check(_lib.lib().rm_device_download(out.ctypes.data, self.ptr, self.nbytes))
         return out
 
+    def upload(self, arr):
+        arr = np.ascontiguousarray(arr)
+        if arr.nbytes > self.nbytes:
+            raise ValueError("array larger than the buffer")
+        _lib.check(_lib.lib().rm_device_upload(self.ptr, arr.ctypes.data, arr.nbytes))
+
     def close(self):
         if getattr(self, "ptr", None):
             _lib.lib().rm_device_free(self.ptr)

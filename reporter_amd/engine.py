@@ -224,10 +224,10 @@ class BatchMatcher:
     def route_tiers(self):
         """Hand-overs of the last run: K2 ball tier -> search, register tier -> tier 2, tier 2 -> wave;
         path ball tier -> path search tiers."""
-        out = (C.c_uint64 * 4)()
+        out = (C.c_uint64 * 6)()
         _lib.check(_lib.lib().rm_runner_route_tiers(self._h, out))
-        return dict(zip(("ball_to_search", "lane_to_tier2", "tier2_to_wave", "paths_ball_to_search"),
-                        [int(x) for x in out]))
+        return dict(zip(("ball_to_search", "lane_to_tier2", "tier2_to_wave", "paths_ball_to_search",
+                         "wave_to_global", "paths_wave_to_global"), [int(x) for x in out]))
 
     # ---- stage outputs (parity tests) ----
     def states(self):
@@ -287,6 +287,17 @@ class BatchMatcher:
         _lib.check(_lib.lib().rm_runner_get_reports(self._h, off.ctypes.data, reps.ctypes.data, stats.ctypes.data))
         return off, reps[: sz["reports"]], stats
 
+    def set_isolation(self, on=True):
+        """Per-trace failure isolation (rm_runner_set_isolation): a failing trace gets no output
+        instead of failing the run; see trace_errors()."""
+        _lib.check(_lib.lib().rm_runner_set_isolation(self._h, 1 if on else 0))
+
+    def trace_errors(self):
+        """Error bits per trace of the last run (1 candidates, 2 route search, 8 path rebuild)."""
+        out = np.zeros(self.sizes()["traces"], np.uint32)
+        _lib.check(_lib.lib().rm_runner_trace_errors(self._h, out.ctypes.data))
+        return out
+
     # ---- timing ----
     def set_timing(self, on=True):
         _lib.check(_lib.lib().rm_runner_set_timing(self._h, 1 if on else 0))
@@ -301,6 +312,25 @@ class BatchMatcher:
         _lib.check(_lib.lib().rm_runner_kernel_times(self._h, ms.ctypes.data, la.ctypes.data, n))
         names = [_lib.lib().rm_kernel_name(i).decode() for i in range(n)]
         return {names[i]: (float(ms[i]), int(la[i])) for i in range(n)}
+
+
+def report_segments(seg_off, segs, trace_end_time, threshold_sec, report_mask, transition_mask):
+    """The device report() epilogue (rm_report_segments) over host segment lists.
+    seg_off: n+1 offsets into segs (SEGMENT_DTYPE); per-trace end time, threshold and level
+    masks (scalars broadcast).  Returns (rep_off, reports REPORT_DTYPE, stats STATS_DTYPE)."""
+    seg_off = _c(seg_off, np.uint32)
+    n = len(seg_off) - 1
+    segs = np.ascontiguousarray(segs, SEGMENT_DTYPE)
+    bc = lambda x, dt: _c(np.broadcast_to(np.asarray(x, dt), (n,)), dt)
+    end, thr = bc(trace_end_time, np.float64), bc(threshold_sec, np.float64)
+    rm, tm = bc(report_mask, np.uint32), bc(transition_mask, np.uint32)
+    d = _lib.RmReportDesc(n, seg_off.ctypes.data, segs.ctypes.data if len(segs) else None, end.ctypes.data,
+                          thr.ctypes.data, rm.ctypes.data, tm.ctypes.data)
+    rep_off = np.zeros(n + 1, np.uint32)
+    reps = np.empty(max(int(seg_off[-1]) if n else 0, 1), REPORT_DTYPE)
+    stats = np.empty(max(n, 1), STATS_DTYPE)
+    _lib.check(_lib.lib().rm_report_segments(C.byref(d), rep_off.ctypes.data, reps.ctypes.data, stats.ctypes.data))
+    return rep_off, reps[: rep_off[-1]], stats[:n]
 
 
 def segment_dicts(segs):

@@ -59,10 +59,14 @@ def graph_info(path):
 
 
 def generate_traces(graph_path, n_traces, n_points, rate_s=1.0, noise_m=5.0, seed=1, mode="auto",
-                    start_epoch=1483228800, threads=0):
+                    start_epoch=1483228800, threads=0, ids=None):
     """Seeded GPS traces on the graph.  Returns a dict of numpy arrays:
     lon/lat (6-dp degrees, f64), time (epoch s, f64), accuracy (f32),
-    trace_off (u32, n_traces+1), truth_edge / truth_off_cm (u32)."""
+    trace_off (u32, n_traces+1), truth_edge / truth_off_cm (u32).
+    With ``ids``, trace k is trace ids[k] of the seeded set (n_traces = len(ids))."""
+    if ids is not None:
+        ids = np.ascontiguousarray(ids, np.uint32)
+        n_traces = len(ids)
     p = _lib.RmTraceParams()
     _lib.lib().rm_default_trace_params(C.byref(p))
     p.n_traces, p.n_points, p.rate_s, p.noise_m = n_traces, n_points, rate_s, noise_m
@@ -72,8 +76,9 @@ def generate_traces(graph_path, n_traces, n_points, rate_s=1.0, noise_m=5.0, see
     out["accuracy"] = np.empty(n, np.float32)
     out["truth_edge"] = np.empty(n, np.uint32)
     out["truth_off_cm"] = np.empty(n, np.uint32)
-    _lib.check(_lib.lib().rm_traces_generate(
-        os.fsencode(graph_path), C.byref(p), out["lon"].ctypes.data, out["lat"].ctypes.data,
+    _lib.check(_lib.lib().rm_traces_generate_ids(
+        os.fsencode(graph_path), C.byref(p), ids.ctypes.data if ids is not None else None,
+        out["lon"].ctypes.data, out["lat"].ctypes.data,
         out["time"].ctypes.data, out["accuracy"].ctypes.data, out["truth_edge"].ctypes.data,
         out["truth_off_cm"].ctypes.data))
     out["trace_off"] = (np.arange(n_traces + 1, dtype=np.uint64) * n_points).astype(np.uint32)

@@ -75,7 +75,10 @@ def main():
                                          "k_routes_wave")]
     tot = lambda key: sum(summary[k].get(key, 0) for k in stage)
     hits, miss = tot("TCC_HIT_sum"), tot("TCC_MISS_sum")
-    rt = {"config": a.config, "traces": a.traces, "kernels": sorted(stage),
+    import hashlib
+    src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reporter_amd", "csrc", "engine.hip")
+    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+    rt = {"config": a.config, "traces": a.traces, "kernels": sorted(stage), "engine_sha": sha, "read_factor": 2,
           "hbm_bytes_per_launch": (tot("hbm_read_bytes_corrected") + tot("hbm_write_bytes")) or None,
           "hbm_read_bytes_raw": tot("hbm_read_bytes_raw"), "hbm_write_bytes": tot("hbm_write_bytes"),
           "l2_hit_rate": hits / (hits + miss) if hits + miss else None,

@@ -108,3 +108,23 @@ def check_reports(bm, ref, tr, rl=(0, 1), tl=(0, 1), threshold=15.0):
         np.testing.assert_array_equal(stats[f][:T].astype(np.int64), np.array([w[f] for w in wsts], np.int64),
                                       "stat " + f)
     return len(got)
+
+
+def truth_recovery(trace_off, n_states, state_orig, cand_road, choice, truth_edge, edges):
+    """Fraction of matched states (choice >= 0) whose chosen road is the road the generator
+    drove at that point (world.generate_traces truth_edge): an independent check of the
+    matcher's spec that the GPU/oracle bit-parity cannot give (a rule both sides get wrong
+    the same way still loses the truth).  Returns (fraction, matched states, all states)."""
+    E = np.asarray(edges).reshape(-1, 4)
+    truth_road = E[np.asarray(truth_edge, np.int64), 3] >> 1
+    trace_off = np.asarray(trace_off, np.int64)
+    T = len(trace_off) - 1
+    ns = np.asarray(n_states, np.int64)
+    slots = _ranges(trace_off[:-1], ns)
+    owner = np.repeat(np.arange(T), ns)
+    pts = trace_off[owner] + np.asarray(state_orig, np.int64)[slots]
+    ch = np.asarray(choice)[slots].astype(np.int64)
+    ok = ch >= 0
+    chosen = np.asarray(cand_road).reshape(-1, 16)[slots[ok], ch[ok]]
+    hit = int((chosen == truth_road[pts[ok]]).sum())
+    return hit / max(int(ok.sum()), 1), int(ok.sum()), len(slots)

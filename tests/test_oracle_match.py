@@ -68,3 +68,27 @@ def test_sparse_routes_use_long_searches(built_lib, tmp_path):
     c = mo.counters()
     assert c["settled"] / max(c["searches"], 1) > 20   # long bounded searches (C3 regime)
     assert (out["choice"] >= 0).sum() > 300
+
+
+def test_truth_recovery_sparse_and_sigma_sweep(built_lib, tmp_path):
+    """The oracle's spec recovers the driven road in the C3 regime (30 s sampling, 100 m
+    radius) and across C5's modes x sigma_z (CPU, small samples; the GPU test
+    tests/test_gpu_pinned.py asserts the same on the GPU's own choices at full size)."""
+    from parity_util import truth_recovery
+    p = str(tmp_path / "c3like.rmg")
+    world.build_world(p, 60, 60, 200.0, seed=3, cell_m=200.0)
+    tr = world.generate_traces(p, 200, 40, rate_s=30.0, noise_m=5.0, seed=9)
+    g, out = _run(p, tr, search_radius=100.0)
+    frac, n, _ = truth_recovery(tr["trace_off"], out["n_states"], out["state_orig"], out["cand_road"], out["choice"],
+                                tr["truth_edge"], g["edges"])
+    assert n > 5000 and frac > 0.93, (frac, n)
+    p2 = str(tmp_path / "c5like.rmg")
+    world.build_world(p2, 60, 60, 100.0, seed=1)
+    floors = {2.0: 0.95, 8.0: 0.87, 16.0: 0.72}
+    for mode in ("auto", "bicycle", "pedestrian"):
+        for sz, floor in floors.items():
+            tr = world.generate_traces(p2, 12, 300, rate_s=1.0, noise_m=sz, seed=11, mode=mode)
+            g, out = _run(p2, tr, mode=world.MODES[mode], sigma_z=sz, search_radius=max(50.0, 3 * sz))
+            frac, n, _ = truth_recovery(tr["trace_off"], out["n_states"], out["state_orig"], out["cand_road"],
+                                        out["choice"], tr["truth_edge"], g["edges"])
+            assert n > 300 and frac > floor, (mode, sz, frac, n)

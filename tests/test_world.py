@@ -91,3 +91,21 @@ def test_traces_on_a_graph_wider_than_their_reach(built_lib, tmp_path):
     assert step.max() < 5.0 * 90 / 3.6 + 1.0                       # never faster than 90 km/h
     net = np.hypot((lon[:, -1] - lon[:, 0]) * mx, (lat[:, -1] - lat[:, 0]) * 110567.0)
     assert np.median(net) > 0.3 * np.median(step.sum(axis=1))       # routed, not a random walk
+
+
+def test_generate_ids_equals_full_set_and_uuid_shard(built_lib, tmp_path):
+    """bench.py's multi-GPU workload: each rank generates exactly its uuid shard of ONE seeded
+    set; the shards partition the set and trace ids[k] equals the full set's trace ids[k]."""
+    import numpy as np
+    import bench
+    p = str(tmp_path / "ids.rmg")
+    world.build_world(p, 20, 20, 100.0, seed=1)
+    full = world.generate_traces(p, 64, 30, seed=1000)
+    shards = [bench.shard_ids("C2", 16, 30, 4, r) for r in range(4)]
+    assert sorted(np.concatenate(shards).tolist()) == list(range(64))
+    assert max(len(s) for s in shards) - min(len(s) for s in shards) <= 16
+    for ids in shards:
+        sub = world.generate_traces(p, 0, 30, seed=1000, ids=ids)
+        for i, k in enumerate(ids):
+            for f in ("lon", "lat", "time", "truth_edge"):
+                assert np.array_equal(sub[f][i * 30:(i + 1) * 30], full[f][k * 30:(k + 1) * 30])
