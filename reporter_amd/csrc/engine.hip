@@ -15,8 +15,8 @@
 //   k_viterbi     K3, one 16-lane group per trace: fp64 costs in registers,
 //                 shuffle broadcast of the previous layer, back-pointers, backtrace
 //   k_paths       one wave per chosen transition: re-search + canonical predecessors
-//   k_traversals / k_run_flags / k_runs   K4: traversal records, time interpolation,
-//                 OSMLR runs (parallel over records and runs)
+//   k_seg_blocks / k_segments   K4: traversal records, time interpolation and OSMLR
+//                 runs in one kernel, records staged in LDS (parallel over slots, records, runs)
 //   k_report      A8 epilogue, one lane per trace: report() + speed histogram
 //
 // All arithmetic follows rm_common.hpp; compiled with -ffp-contract=off so the
@@ -64,8 +64,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
   SegmentRec* segs; uint32_t* seg_base; uint32_t* seg_cnt;
-  TravRec* trav; uint32_t* trav_off;
-  uint8_t* run_kind; uint32_t* run_head; uint32_t* run_idx; uint32_t* run_pos;
+  uint32_t* trav_off;
   ReportRec* reps; uint32_t* rep_cnt; ReportStats* stats;
   // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list [8] path ball hand-overs
@@ -1677,12 +1676,20 @@ __global__ void __launch_bounds__(64) k_paths_global(DevGraph g, DevBatch b, Glo
 }
 
 // ------------------------------------------------------------------------------------------
-// K4 (segments), in two passes:
-//   k_traversals  one lane per chosen transition: expands its path into 64-byte traversal
-//                 records (edge, [b,en] cm, interpolated times, state indices, OSMLR tags);
-//                 all dependent graph lookups happen here, in parallel
-//   k_run_flags / k_runs  merge pieces that continue through a state point and form
-//                 OSMLR runs (meili form_segments analogue), parallel over records
+// K4 (segments): traversal records -> OSMLR runs -> segments, fused in one kernel whose
+// traversal records never leave LDS.
+//   k_seg_blocks  block -> trace range: block b takes the traces whose first record lies in
+//                 [b * kSegSpan, (b+1) * kSegSpan) (records never cross traces, so neither do runs)
+//   k_segments    per block, the block's record range in chunks of kSegChunk records:
+//                 build    one lane per transition slot expands its path into traversal
+//                          records (edge, [b,en] cm, interpolated times, OSMLR tags) in LDS
+//                 flags    one lane per record: skip / new traversal / merged piece and the
+//                          run-head flag (meili form_segments' merge + run rules compare a
+//                          record with the previous kept record of its chain only)
+//                 runs     one lane per run head walks its run in LDS and writes the segment;
+//                          the run still open at a chunk's end carries its state into the next
+// Segments of trace k are compacted at seg_base[k] = its block's first record + the runs of
+// the block before it (a per-block layout: no global scan of runs, gaps between blocks).
 struct RunState {
   bool open, internal;
   uint32_t sd, f_b, f_soff, l_en, l_len, l_soff, seg_len, sb, se, way_first, way_last;
@@ -1712,19 +1719,11 @@ __device__ __forceinline__ void run_close(const DevGraph& g, RunState& R, Segmen
   R.open = false;
 }
 
-
 __device__ __forceinline__ double interp_time(double ta, double tb, uint64_t x, uint64_t D) {
   if (D == 0) return ta;
   return ta + (tb - ta) * ((double)x / (double)D);
 }
 
-// The meili merge / run rules only ever compare a record with the previous kept record
-// of its chain, so run boundaries are local and K4 needs no per-trace serial loop:
-//   k_run_flags   one lane per record: kind (skip / new traversal / merged piece) and
-//                 run-head flag
-//   (scan)        exclusive sum of the head flags = each run's output index
-//   k_runs        one lane per run head: walks its run (a few records) and writes the
-//                 segment; one lane per trace records seg_base / seg_cnt
 enum : uint8_t { kRecSkip = 0, kRecNew = 1, kRecMerged = 2 };
 
 __device__ __forceinline__ bool same_chain(uint32_t slot_prev, uint32_t slot_next) {
@@ -1733,178 +1732,18 @@ __device__ __forceinline__ bool same_chain(uint32_t slot_prev, uint32_t slot_nex
   return slot_next == slot_prev || slot_next == slot_prev + 1;
 }
 
-// kind / head flag of record r (index into recs; the lookback stops at index 0)
-__device__ __forceinline__ void run_flag(const TravRec* recs, int64_t r, uint8_t& kind, uint32_t& head) {
-  const TravRec& t = recs[r];
-  const uint32_t tb = t.b, ten = t.en, tslot = t.slot & kTravSlotMask;
-  kind = kRecSkip;
-  head = 0;
-  if (ten == tb) return;
-  // previous kept record of the same chain
-  int64_t p = r - 1;
-  uint32_t nslot = tslot;
-  bool has = false;
-  while (p >= 0) {
-    const uint32_t ps = recs[p].slot & kTravSlotMask;
-    if (!same_chain(ps, nslot)) break;
-    if (recs[p].en != recs[p].b) { has = true; break; }
-    nslot = ps;
-    --p;
+// kind / head flag of t given the previous kept record u of its chain (has_u)
+__device__ __forceinline__ void flag_vs(const TravRec& t, bool has_u, const TravRec& u, uint8_t& kind, uint32_t& head) {
+  if (!has_u) { kind = kRecNew; head = 1; return; }
+  if (u.e == t.e && u.en == t.b) { kind = kRecMerged; head = 0; return; }
+  kind = kRecNew;
+  bool cont = u.sd == t.sd;
+  if (cont && t.sd == kNone && ((u.slot ^ t.slot) & kTravInternal)) cont = false;
+  if (cont) {
+    if (u.en != u.len || t.b != 0) cont = false;
+    else if (t.sd != kNone && t.soff != u.soff + u.len) cont = false;
   }
-  if (has) {
-    const TravRec& u = recs[p];
-    if (u.e == t.e && u.en == tb) {
-      kind = kRecMerged;
-    } else {
-      kind = kRecNew;
-      bool cont = u.sd == t.sd;
-      if (cont && t.sd == kNone && ((u.slot ^ t.slot) & kTravInternal)) cont = false;
-      if (cont) {
-        if (u.en != u.len || tb != 0) cont = false;
-        else if (t.sd != kNone && t.soff != u.soff + u.len) cont = false;
-      }
-      head = cont ? 0u : 1u;
-    }
-  } else {
-    kind = kRecNew;
-    head = 1;
-  }
-}
-
-// The records of a block's 256 slots are one contiguous range of trav (trav_off is a scan in
-// slot order): the first kTravStage of them are staged in LDS and written by the whole block
-// with coalesced 16-byte stores; records past the stage (long paths) are stored by their lane.
-#ifndef RM_TRAV_STAGE
-#define RM_TRAV_STAGE 1024
-#endif
-constexpr uint32_t kTravStage = RM_TRAV_STAGE;
-
-__device__ __forceinline__ void traversal_lane(const DevGraph& g, const DevBatch& b, uint64_t l, uint32_t base,
-                                               uint4* s_rec) {
-  const uint32_t ns = b.path_cnt[l];
-  if (ns == 0) return;  // not a chosen transition
-  const uint32_t k = b.slot_trace[l];
-  const uint32_t o = b.trace_off[k];
-  const uint32_t i = (uint32_t)b.choice[l - 1], j = (uint32_t)b.choice[l];
-  const uint32_t sa = b.cand_desc[((l - 1) * kMaxCand + i) * 2].y, sb = b.cand_desc[(l * kMaxCand + j) * 2].y;
-  const uint32_t oa = b.state_orig[l - 1], ob = b.state_orig[l];
-  const double ta = b.time[o + oa], tb = b.time[o + ob];
-  const uint32_t D = b.route_dist[l];
-  const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
-  const uint32_t r0 = b.trav_off[l];
-  TravRec* out = b.trav + r0;
-  // a trace that failed (trace_err) forms no segments: its records become empty pieces
-  const bool bad = b.trace_err[k] != 0u;
-  uint64_t x = 0;
-  // four path edges per group: every graph load of a group is issued before its record
-  // stores (loads after a pending store wait for it: shared vmcnt)
-  for (uint32_t q0 = 0; q0 < ns; q0 += 4) {
-    uint32_t e[4], sd[4], soff[4], way[4];
-    uint4 rec[4];
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      e[y] = pe[min(q0 + y, ns - 1u)];
-    }
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      rec[y] = g.edges[e[y]];
-      sd[y] = g.edge_seg[e[y]];
-      soff[y] = g.edge_seg_off[e[y]];
-      way[y] = g.edge_way[e[y]];
-    }
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const uint32_t q = q0 + y;
-      if (q >= ns) break;
-      const uint32_t L = rec[y].y;
-      const bool rev = (rec[y].w & 1u) != 0u;
-      uint32_t b0 = 0, b1 = L;
-      if (q == 0) b0 = rev ? L - sa : sa;
-      if (q + 1 == ns) b1 = rev ? L - sb : sb;
-      if (bad) b0 = b1 = 0;
-      TravRec t;
-      t.e = e[y]; t.b = b0; t.en = b1;
-      t.slot = (uint32_t)l | (q + 1 == ns ? kTravLast : 0u) | ((rec[y].z & kFlagInternal) ? kTravInternal : 0u);
-      t.tb = interp_time(ta, tb, x, D);
-      x += (uint64_t)(b1 - b0);
-      t.te = interp_time(ta, tb, x, D);
-      t.sd = sd[y];
-      t.soff = soff[y];
-      t.len = L;
-      t.way = way[y];
-      const uint32_t si = r0 + q - base;
-      if (si < kTravStage) {
-        const uint4* tv = reinterpret_cast<const uint4*>(&t);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) s_rec[si * 3 + c] = tv[c];
-      } else {
-        out[q] = t;
-      }
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256) k_traversals(DevGraph g, DevBatch b) {
-  __shared__ uint4 s_rec[kTravStage * 3];
-  const uint64_t l0 = (uint64_t)blockIdx.x * blockDim.x;
-  const uint64_t l = l0 + threadIdx.x;
-  const uint64_t last = (l0 + blockDim.x < b.P ? l0 + blockDim.x : b.P) - 1;
-  const uint32_t base = b.trav_off[l0];
-  const uint32_t n_rec = b.trav_off[last] + b.path_cnt[last] - base;
-  if (l < b.P) traversal_lane(g, b, l, base, s_rec);
-  __syncthreads();
-  const uint32_t n_stage = n_rec < kTravStage ? n_rec : kTravStage;
-  uint4* dst = reinterpret_cast<uint4*>(b.trav + base);
-  for (uint32_t v = threadIdx.x; v < n_stage * 3; v += blockDim.x) dst[v] = s_rec[v];
-  // run flags of the staged block, looking back within the stage only (k_run_flags_fix
-  // redoes the prefix whose lookback crosses into the previous block)
-  if (n_rec <= kTravStage) {
-    const TravRec* st = reinterpret_cast<const TravRec*>(s_rec);
-    for (uint32_t r = threadIdx.x; r < n_rec; r += blockDim.x) {
-      uint8_t kind;
-      uint32_t head;
-      run_flag(st, r, kind, head);
-      b.run_kind[base + r] = kind;
-      b.run_head[base + r] = head;
-    }
-  }
-}
-
-// Flags of the records k_traversals could not decide from its LDS stage: the leading records
-// of a staged block whose lookback leaves the block (a prefix: kept record, or skipped
-// records continuing one chain), and every record of a block whose range outgrew the stage.
-// Runs after k_traversals, so it overwrites that kernel's block-local guesses.
-__global__ void __launch_bounds__(256) k_run_flags_fix(DevBatch b, uint32_t total) {
-  const uint64_t l0 = (uint64_t)blockIdx.x * blockDim.x;
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) b.run_head[total] = 0;
-  const uint64_t last = (l0 + blockDim.x < b.P ? l0 + blockDim.x : b.P) - 1;
-  const uint32_t base = b.trav_off[l0];
-  const uint32_t end = b.trav_off[last] + b.path_cnt[last];
-  if (end - base > kTravStage) {
-    for (uint32_t r = base + threadIdx.x; r < end; r += blockDim.x) {
-      uint8_t kind;
-      uint32_t head;
-      run_flag(b.trav, r, kind, head);
-      b.run_kind[r] = kind;
-      b.run_head[r] = head;
-    }
-  } else if (threadIdx.x == 0 && base > 0) {
-    for (uint32_t r = base; r < end; ++r) {
-      uint8_t kind;
-      uint32_t head;
-      run_flag(b.trav, r, kind, head);
-      b.run_kind[r] = kind;
-      b.run_head[r] = head;
-      if (kind != kRecSkip) break;
-      if (r + 1 < end && !same_chain(b.trav[r].slot & kTravSlotMask, b.trav[r + 1].slot & kTravSlotMask)) break;
-    }
-  }
-}
-
-// scatter: run head record of every run, in run order (runs are contiguous in record order)
-__global__ void __launch_bounds__(256) k_run_heads(DevBatch b, uint32_t total) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < total && b.run_head[r]) b.run_pos[b.run_idx[r]] = r;
+  head = cont ? 0u : 1u;
 }
 
 __device__ __forceinline__ void run_piece(RunState& R, const TravRec& t, uint8_t kind, uint32_t& md, double& mtb,
@@ -1923,59 +1762,282 @@ __device__ __forceinline__ void run_piece(RunState& R, const TravRec& t, uint8_t
   R.l_en = t.en; R.l_len = t.len; R.l_soff = t.soff; R.te = t.te; R.se = t.slot;  // raw slot, resolved at close
 }
 
-// one lane per run: records [run_pos[i], run_pos[i+1]) (skips and merged pieces inside)
-__global__ void __launch_bounds__(256) k_runs(DevGraph g, DevBatch b, uint32_t total) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t n_runs = b.run_idx[total];
-  if (i < b.T) {  // per-trace range of the compacted segments
-    const uint32_t p0 = b.trace_off[i], p1 = b.trace_off[i + 1];
-    const uint32_t r0 = p0 < b.P ? b.trav_off[p0] : total;   // empty trailing traces start at P
-    const uint32_t r1 = p1 < b.P ? b.trav_off[p1] : total;
-    const uint32_t i0 = b.run_idx[r0];
-    b.seg_base[i] = i0;
-    b.seg_cnt[i] = b.run_idx[r1] - i0;
-  }
-  if (i >= n_runs) return;
-  const uint32_t r = b.run_pos[i];
-  const uint32_t end = (i + 1 < n_runs) ? b.run_pos[i + 1] : total;
-  const TravRec f = b.trav[r];
+#ifndef RM_SEG_CHUNK
+#define RM_SEG_CHUNK 512
+#endif
+constexpr uint32_t kSegChunk = RM_SEG_CHUNK;   // traversal records staged per chunk
+constexpr uint32_t kSegSpan = RM_SEG_CHUNK;    // first-record span of the traces a block takes
+constexpr uint32_t kSegThreads = 256;
+
+// a run open at a chunk's end (its records continue in the next chunk)
+struct RunCarry {
   RunState R;
+  double mtb, mte;
+  uint32_t md, idx, open, pad;
+};
+
+struct SegSmem {
+  TravRec rec[kSegChunk];
+  uint32_t scan[kSegChunk];         // exclusive scan of the head flags (chunk-local)
+  uint16_t pos[kSegChunk];          // chunk position of the i-th head
+  uint8_t kind[kSegChunk];
+  uint32_t wsum[kSegThreads / 64];
+  TravRec carry_rec;                // last kept record before the chunk (valid when carry_has)
+  uint32_t carry_slot, carry_has;   // slot of the record just before the chunk; chain has a kept record
+  RunCarry rc[2];                   // open run into / out of the chunk (double-buffered)
+  uint32_t next_lo, n_heads;
+};
+
+// record position of trace k's first traversal record (records of trace k are contiguous)
+__device__ __forceinline__ uint32_t trace_first_rec(const DevBatch& b, uint32_t k, uint32_t total) {
+  if (k >= b.T) return total;
+  const uint32_t o = b.trace_off[k];
+  return o < b.P ? b.trav_off[o] : total;
+}
+
+// blk_first[blk] = first trace of block blk, for blk in [0, nb]; trace k belongs to block
+// first_rec(k) / kSegSpan
+__global__ void __launch_bounds__(256) k_seg_blocks(DevBatch b, uint32_t total, uint32_t nb, uint32_t* blk_first) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > b.T) return;
+  const uint32_t bk = k < b.T ? trace_first_rec(b, k, total) / kSegSpan : nb;
+  const int32_t bp = k > 0 ? (int32_t)(trace_first_rec(b, k - 1, total) / kSegSpan) : -1;
+  for (int32_t x = bp + 1; x <= (int32_t)bk; ++x) blk_first[x] = k;
+}
+
+// one transition slot l: its traversal records that fall in [c0, c1) into st
+__device__ __forceinline__ void seg_build_slot(const DevGraph& g, const DevBatch& b, uint64_t l, uint32_t c0, uint32_t c1,
+                                               TravRec* st) {
+  const uint32_t ns = b.path_cnt[l];
+  if (ns == 0) return;
+  const uint32_t r0 = b.trav_off[l];
+  if (r0 >= c1 || r0 + ns <= c0) return;
+  const uint32_t k = b.slot_trace[l];
+  const uint32_t o = b.trace_off[k];
+  const uint32_t i = (uint32_t)b.choice[l - 1], j = (uint32_t)b.choice[l];
+  const uint32_t sa = b.cand_desc[((l - 1) * kMaxCand + i) * 2].y, sb = b.cand_desc[(l * kMaxCand + j) * 2].y;
+  const uint32_t oa = b.state_orig[l - 1], ob = b.state_orig[l];
+  const double ta = b.time[o + oa], tb = b.time[o + ob];
+  const uint32_t D = b.route_dist[l];
+  const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
+  // a trace that failed (trace_err) forms no segments: its records become empty pieces
+  const bool bad = b.trace_err[k] != 0u;
+  uint64_t x = 0;
+  // four path edges per group: every graph load of a group is issued before its LDS stores
+  for (uint32_t q0 = 0; q0 < ns; q0 += 4) {
+    uint32_t e[4], sd[4], soff[4], way[4];
+    uint4 rec[4];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) e[y] = pe[min(q0 + y, ns - 1u)];
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      rec[y] = g.edges[e[y]];
+      sd[y] = g.edge_seg[e[y]];
+      soff[y] = g.edge_seg_off[e[y]];
+      way[y] = g.edge_way[e[y]];
+    }
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const uint32_t q = q0 + y;
+      if (q >= ns) break;
+      const uint32_t L = rec[y].y;
+      const bool rev = (rec[y].w & 1u) != 0u;
+      uint32_t b0 = 0, b1 = L;
+      if (q == 0) b0 = rev ? L - sa : sa;
+      if (q + 1 == ns) b1 = rev ? L - sb : sb;
+      if (bad) b0 = b1 = 0;
+      const double t_b = interp_time(ta, tb, x, D);
+      x += (uint64_t)(b1 - b0);
+      const uint32_t r = r0 + q;
+      if (r < c0 || r >= c1) continue;
+      TravRec& t = st[r - c0];
+      t.e = e[y]; t.b = b0; t.en = b1;
+      t.slot = (uint32_t)l | (q + 1 == ns ? kTravLast : 0u) | ((rec[y].z & kFlagInternal) ? kTravInternal : 0u);
+      t.tb = t_b;
+      t.te = interp_time(ta, tb, x, D);
+      t.sd = sd[y];
+      t.soff = soff[y];
+      t.len = L;
+      t.way = way[y];
+    }
+  }
+}
+
+// run state opened by head record f
+__device__ __forceinline__ void run_open(const DevGraph& g, const DevBatch& b, const TravRec& f, RunState& R, uint32_t& md,
+                                         double& mtb, double& mte) {
   R.open = true; R.sd = f.sd; R.internal = (f.slot & kTravInternal) != 0u;
   R.seg_len = f.sd != kNone ? g.seg_len[f.sd] : 0u;
   R.f_b = f.b; R.f_soff = f.soff; R.tb = f.tb; R.sb = b.state_orig[(f.slot & kTravSlotMask) - 1u];
   R.tot = 0; R.q = 0; R.way_first = f.way; R.way_last = f.way;
-  uint32_t md = f.en - f.b;
-  double mtb = f.tb, mte = f.te;
+  md = f.en - f.b;
+  mtb = f.tb; mte = f.te;
   R.l_en = f.en; R.l_len = f.len; R.l_soff = f.soff; R.te = f.te; R.se = f.slot;
-  // records are consumed four at a time so their loads overlap
-  uint32_t q = r + 1;
-  for (; q + 4 <= end; q += 4) {
-    uint8_t kd[4];
-    TravRec t[4];
-#pragma unroll
-    for (int x = 0; x < 4; ++x) { kd[x] = b.run_kind[q + x]; t[x] = b.trav[q + x]; }
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
-      if (kd[x] != kRecSkip) run_piece(R, t[x], kd[x], md, mtb, mte);
-  }
-  for (; q < end; ++q) {
-    const uint8_t kd = b.run_kind[q];
-    if (kd != kRecSkip) run_piece(R, b.trav[q], kd, md, mtb, mte);
-  }
-  {
-    const double dt = mte - mtb;
-    const bool slow = dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
-    R.tot += md;
-    R.q = slow ? R.q + md : 0;
-  }
-  {
-    // end state of the run's last piece: its transition's target state if it is the last
-    // record of that transition, else the transition's source state
-    const uint32_t sl = R.se & kTravSlotMask;
-    R.se = b.state_orig[(R.se & kTravLast) ? sl : sl - 1u];
-  }
+}
+
+// fold the last piece, resolve the end state and write the run's segment
+__device__ __forceinline__ void run_finish(const DevGraph& g, const DevBatch& b, RunState& R, uint32_t md, double mtb,
+                                           double mte, SegmentRec* out) {
+  const double dt = mte - mtb;
+  const bool slow = dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
+  R.tot += md;
+  R.q = slow ? R.q + md : 0;
+  // end state of the run's last piece: its transition's target state if it is the last
+  // record of that transition, else the transition's source state
+  const uint32_t sl = R.se & kTravSlotMask;
+  R.se = b.state_orig[(R.se & kTravLast) ? sl : sl - 1u];
   uint32_t n = 0;
-  run_close(g, R, b.segs + i, n);
+  run_close(g, R, out, n);
+}
+
+__global__ void __launch_bounds__(kSegThreads) k_segments(DevGraph g, DevBatch b, uint32_t total,
+                                                          const uint32_t* blk_first) {
+  __shared__ SegSmem sm;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
+  const uint32_t k0 = blk_first[blk], k1 = blk_first[blk + 1];
+  if (k0 >= k1) return;
+  const uint32_t R0 = trace_first_rec(b, k0, total), R1 = trace_first_rec(b, k1, total);
+  const uint32_t L1 = k1 < b.T ? b.trace_off[k1] : (uint32_t)b.P;
+  if (tid == 0) { sm.carry_has = 0; sm.carry_slot = kNone; sm.rc[0].open = 0; sm.rc[1].open = 0; sm.next_lo = b.trace_off[k0]; }
+  __syncthreads();
+  uint32_t runs = 0;     // runs of the block before the current chunk
+  int cur = 0;           // rc[cur]: the run open into this chunk
+  for (uint32_t c0 = R0; c0 < R1; c0 += kSegChunk) {
+    const uint32_t c1 = min(c0 + kSegChunk, R1), n = c1 - c0;
+    const bool last_chunk = c1 == R1;
+    // ---- build: the slots whose records reach into [c0, c1)
+    const uint32_t l_lo = sm.next_lo;
+    __syncthreads();
+    if (tid == 0) sm.next_lo = L1;
+    __syncthreads();
+    for (uint32_t l = l_lo + tid; l < L1; l += kSegThreads) {
+      const uint32_t r0 = b.trav_off[l];
+      if (r0 >= c1) { atomicMin(&sm.next_lo, l); break; }
+      if (r0 + b.path_cnt[l] > c1) atomicMin(&sm.next_lo, l);   // straddles into the next chunk
+      seg_build_slot(g, b, l, c0, c1, sm.rec);
+    }
+    __syncthreads();
+    // ---- flags: previous kept record of the chain, in LDS or carried from before the chunk
+    uint32_t hsum = 0;
+    uint32_t hv[2];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const uint32_t r = tid * 2 + y;
+      hv[y] = 0;
+      if (r >= n) continue;
+      const TravRec& t = sm.rec[r];
+      uint8_t kind = kRecSkip;
+      uint32_t head = 0;
+      if (t.en != t.b) {
+        int32_t p = (int32_t)r - 1;
+        uint32_t nslot = t.slot & kTravSlotMask;
+        bool has = false, chain = true;
+        while (p >= 0) {
+          const uint32_t ps = sm.rec[p].slot & kTravSlotMask;
+          if (!same_chain(ps, nslot)) { chain = false; break; }
+          if (sm.rec[p].en != sm.rec[p].b) { has = true; break; }
+          nslot = ps;
+          --p;
+        }
+        if (has) flag_vs(t, true, sm.rec[p], kind, head);
+        else if (chain && sm.carry_has && same_chain(sm.carry_slot, nslot)) flag_vs(t, true, sm.carry_rec, kind, head);
+        else flag_vs(t, false, t, kind, head);
+      }
+      sm.kind[r] = kind;
+      hv[y] = head;
+      hsum += head;
+    }
+    // ---- exclusive scan of the head flags (two records per lane)
+    uint32_t incl = hsum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t u = __shfl_up(incl, d, 64);
+      if ((tid & 63) >= (uint32_t)d) incl += u;
+    }
+    if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) wbase += sm.wsum[w];
+    const uint32_t nh = sm.wsum[0] + sm.wsum[1] + sm.wsum[2] + sm.wsum[3];
+    uint32_t ex = wbase + incl - hsum;
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const uint32_t r = tid * 2 + y;
+      if (r < n) {
+        sm.scan[r] = ex;
+        if (hv[y]) sm.pos[ex] = (uint16_t)r;
+      }
+      ex += hv[y];
+    }
+    __syncthreads();
+    // ---- runs
+    const int nxt = cur ^ 1;
+    if (tid == 0) {
+      // the run carried in from the previous chunk continues up to the first head
+      RunCarry& c = sm.rc[cur];
+      if (c.open) {
+        const uint32_t end = nh ? sm.pos[0] : n;
+        for (uint32_t q = 0; q < end; ++q)
+          if (sm.kind[q] != kRecSkip) run_piece(c.R, sm.rec[q], sm.kind[q], c.md, c.mtb, c.mte);
+        if (nh || last_chunk) {
+          run_finish(g, b, c.R, c.md, c.mtb, c.mte, b.segs + R0 + c.idx);
+          c.open = 0;
+        } else {
+          sm.rc[nxt] = c;   // still open: it spans this whole chunk
+        }
+      }
+    }
+    if (tid == kSegThreads - 1 && nh == 0 && !sm.rc[cur].open) sm.rc[nxt].open = 0;
+    for (uint32_t i = tid; i < nh; i += kSegThreads) {
+      const uint32_t r = sm.pos[i];
+      const uint32_t end = i + 1 < nh ? sm.pos[i + 1] : n;
+      RunState R;
+      uint32_t md;
+      double mtb, mte;
+      run_open(g, b, sm.rec[r], R, md, mtb, mte);
+      for (uint32_t q = r + 1; q < end; ++q)
+        if (sm.kind[q] != kRecSkip) run_piece(R, sm.rec[q], sm.kind[q], md, mtb, mte);
+      if (i + 1 == nh && !last_chunk) {   // open into the next chunk
+        RunCarry& c = sm.rc[nxt];
+        c.R = R; c.md = md; c.mtb = mtb; c.mte = mte; c.idx = runs + i; c.open = 1;
+      } else {
+        run_finish(g, b, R, md, mtb, mte, b.segs + R0 + runs + i);
+      }
+    }
+    // first segment of each trace starting in this chunk
+    for (uint32_t k = k0 + tid; k < k1; k += kSegThreads) {
+      const uint32_t rk = trace_first_rec(b, k, total);
+      if (rk >= c0 && rk < c1) b.seg_base[k] = R0 + runs + sm.scan[rk - c0];
+    }
+    // chain state at the end of the chunk for the next chunk's lookback
+    if (tid == kSegThreads - 2) {
+      uint32_t nslot = sm.rec[n - 1].slot & kTravSlotMask;
+      const uint32_t end_slot = nslot;
+      bool found = false, chain = true;
+      for (int32_t r = (int32_t)n - 1; r >= 0; --r) {
+        const uint32_t rs = sm.rec[r].slot & kTravSlotMask;
+        if (r < (int32_t)n - 1 && !same_chain(rs, nslot)) { chain = false; break; }
+        if (sm.rec[r].en != sm.rec[r].b) { found = true; sm.carry_rec = sm.rec[r]; break; }
+        nslot = rs;
+      }
+      if (!found) sm.carry_has = (chain && sm.carry_has && same_chain(sm.carry_slot, nslot)) ? 1u : 0u;
+      else sm.carry_has = 1u;
+      sm.carry_slot = end_slot;
+    }
+    __syncthreads();
+    runs += nh;
+    cur = nxt;
+  }
+  // traces whose records start at the block's end (none left) and per-trace counts
+  for (uint32_t k = k0 + tid; k < k1; k += kSegThreads)
+    if (trace_first_rec(b, k, total) >= R1) b.seg_base[k] = R0 + runs;
+  __threadfence_block();
+  __syncthreads();
+  for (uint32_t k = k0 + tid; k < k1; k += kSegThreads) {
+    const uint32_t nb = k + 1 < k1 ? b.seg_base[k + 1] : R0 + runs;
+    b.seg_cnt[k] = nb - b.seg_base[k];
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2314,8 +2376,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
   w.gsearch = nullptr;
-  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.trav = nullptr;
-  w.run_kind = nullptr; w.run_head = nullptr; w.run_idx = nullptr; w.run_pos = nullptr; w.seg_scan_tmp = nullptr;
+  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.blk_first = nullptr;
   w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
   ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
   ensure_path(std::max<uint64_t>(keep_path, cp / 8 + 1024));
@@ -2366,24 +2427,11 @@ void Matcher::ensure_segs(uint64_t n) {
   if (n <= w.cap_segs && w.segs) return;
   free_one(w, w.segs);
   free_one(w, w.reps);
-  free_one(w, w.trav);
-  free_one(w, w.run_kind);
-  free_one(w, w.run_head);
-  free_one(w, w.run_idx);
-  free_one(w, w.run_pos);
-  free_one(w, w.seg_scan_tmp);
+  free_one(w, w.blk_first);
   const uint64_t c = n + n / 4 + 1024;
   w.segs = dalloc<SegmentRec>(w.allocs, c);
   w.reps = dalloc<ReportRec>(w.allocs, c);
-  w.trav = dalloc<TravRec>(w.allocs, c);
-  w.run_kind = dalloc<uint8_t>(w.allocs, c + 1);
-  w.run_head = dalloc<uint32_t>(w.allocs, c + 1);
-  w.run_idx = dalloc<uint32_t>(w.allocs, c + 1);
-  w.run_pos = dalloc<uint32_t>(w.allocs, c + 1);
-  size_t tmp = 0;
-  RM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, w.run_head, w.run_idx, (int)(c + 1), stream_));
-  w.seg_scan_tmp_bytes = tmp;
-  w.seg_scan_tmp = dalloc<char>(w.allocs, tmp);
+  w.blk_first = dalloc<uint32_t>(w.allocs, c / kSegSpan + 3);
   w.cap_segs = c;
 }
 
@@ -2437,7 +2485,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.path_pool = w.path_pool; v.path_cap = w.cap_path;
   v.route_dist = w.route_dist;
   v.segs = w.segs; v.seg_base = w.seg_base; v.seg_cnt = w.seg_cnt;
-  v.trav = w.trav; v.trav_off = w.trav_off;
+  v.trav_off = w.trav_off;
   v.reps = w.reps; v.rep_cnt = w.rep_cnt; v.stats = w.stats;
   v.ctl = w.ctl; v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
   v.rl_paths_a = w.rl_paths_a; v.rl_paths_b = w.rl_paths_b; v.rl_cand = w.rl_cand;
@@ -2647,17 +2695,14 @@ void Matcher::run_device(const RunParams& rp) {
   if (seg_total >= kMaxRecords) throw std::runtime_error("batch too large (path edges >= 1.7e9); split it");
   n_path_ = seg_total;  // one traversal record (and at most one segment) per chosen path edge
   ensure_segs(seg_total);
-  v.segs = w.segs; v.reps = w.reps; v.trav = w.trav;
-  v.run_kind = w.run_kind; v.run_head = w.run_head; v.run_idx = w.run_idx; v.run_pos = w.run_pos;
+  v.segs = w.segs; v.reps = w.reps;
   tic(kKSegments);
-  hipLaunchKernelGGL(k_traversals, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_run_flags_fix, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v, (uint32_t)seg_total);
-  tmp = w.seg_scan_tmp_bytes;
-  RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.seg_scan_tmp, tmp, w.run_head, w.run_idx, (int)(seg_total + 1), st));
-  hipLaunchKernelGGL(k_run_heads, dim3((uint32_t)((seg_total + 255) / 256)), dim3(256), 0, st, v, (uint32_t)seg_total);
-  // runs <= records: the grid covers both bounds, n_runs is read on the device
-  hipLaunchKernelGGL(k_runs, dim3((uint32_t)((std::max<uint64_t>(seg_total, T) + 255) / 256)), dim3(256), 0, st, g, v,
-                     (uint32_t)seg_total);
+  {
+    const uint32_t nb = (uint32_t)(seg_total / kSegSpan) + 1;   // a block per kSegSpan first-record span
+    hipLaunchKernelGGL(k_seg_blocks, dim3((T + 1 + 255) / 256), dim3(256), 0, st, v, (uint32_t)seg_total, nb, w.blk_first);
+    hipLaunchKernelGGL(k_segments, dim3(nb), dim3(kSegThreads), 0, st, g, v, (uint32_t)seg_total,
+                       (const uint32_t*)w.blk_first);
+  }
   toc(kKSegments);
   if (rp.do_report) {
     if (rp.hist && rp.zero_hist)

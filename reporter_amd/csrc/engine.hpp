@@ -110,9 +110,8 @@ struct Workspace {
   uint32_t* path_inline = nullptr;  // kInlinePath edges per slot
   // per trace outputs
   SegmentRec* segs = nullptr; uint32_t* seg_base = nullptr; uint32_t* seg_cnt = nullptr;
-  TravRec* trav = nullptr; uint32_t* trav_off = nullptr;  // traversal records (K4 pass 1)
-  uint8_t* run_kind = nullptr; uint32_t* run_head = nullptr; uint32_t* run_idx = nullptr; uint32_t* run_pos = nullptr;  // K4 run flags
-  void* seg_scan_tmp = nullptr; size_t seg_scan_tmp_bytes = 0;
+  uint32_t* trav_off = nullptr;     // first traversal record of each slot (scan of path_cnt)
+  uint32_t* blk_first = nullptr;    // K4: first trace of each segments block (k_seg_blocks)
   ReportRec* reps = nullptr; uint32_t* rep_cnt = nullptr; ReportStats* stats = nullptr;
   // control words (kCtlWords): [0] path pool used [1] K2 ball-tier hand-over list [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list (overflow lists of the lane tiers)

