@@ -76,6 +76,16 @@ void rm_default_world_params(rm_world_params* p);
 int rm_world_build(const rm_world_params* p, const char* out_path);
 /* counts of a graph file: nodes, edges, roads, verts, segments, cells, cell items */
 int rm_graph_info(const char* graph_path, uint64_t out[7]);
+/* OpenStreetMap exchange (graph_osm.cpp; the reference builds its Valhalla tiles from OSM,
+ * py/get_tiles.py:30-102, py/simple_reporter.py:36-49).  rm_graph_export_osm writes an .rmg
+ * graph as OSM XML: routing tags (highway, maxspeed, oneway, access) on one way per road,
+ * exact reporter:* tags, one type=osmlr relation per OSMLR segment, the grid geometry in a
+ * type=reporter_grid relation.  rm_graph_import_osm reads OSM XML into an .rmg: an exported
+ * file comes back bit-identical; any other OSM XML is split into roads at intersections with
+ * speeds / access from its tags and a grid index of cell_m metres (OSMLR segments only where
+ * osmlr relations give them). */
+int rm_graph_export_osm(const char* graph_path, const char* osm_path);
+int rm_graph_import_osm(const char* osm_path, const char* graph_path, double cell_m);
 
 typedef struct {
   uint32_t n_traces, n_points;

@@ -535,6 +535,20 @@ int rm_graph_info(const char* graph_path, uint64_t out[7]) {
   });
 }
 
+int rm_graph_export_osm(const char* graph_path, const char* osm_path) {
+  return guarded([&] {
+    if (!graph_path || !osm_path) throw std::runtime_error("path is NULL");
+    export_osm(Graph::load(graph_path), osm_path);
+  });
+}
+
+int rm_graph_import_osm(const char* osm_path, const char* graph_path, double cell_m) {
+  return guarded([&] {
+    if (!graph_path || !osm_path) throw std::runtime_error("path is NULL");
+    import_osm(osm_path, cell_m).save(graph_path);
+  });
+}
+
 void rm_default_trace_params(rm_trace_params* p) {
   TraceParams d;
   p->n_traces = d.n_traces; p->n_points = d.n_points; p->rate_s = d.rate_s; p->noise_m = d.noise_m;

@@ -57,7 +57,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint64_t P;
   const uint32_t* trace_off; const float* lon; const float* lat; const double* time; const float* acc;
   const MatchOptions* opts; const uint32_t* trace_opt;
-  uint32_t* slot_trace; uint32_t* n_states; uint32_t* state_orig;
+  uint32_t* slot_trace; uint32_t* n_states; uint32_t* state_orig; double* state_time;
   uint8_t* cand_n; uint4* cand_desc; float* cand_sq;
   uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route; uint4* pair_info;
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
@@ -451,28 +451,52 @@ __global__ void __launch_bounds__(64) k_candidates_wave(DevGraph g, DevBatch b) 
 }
 
 // ------------------------------------------------------------------------------------------
-// transition counts for the exclusive scan that lays out route[] compactly, plus the
-// per-pair constants K2 needs (bounds, candidate counts, mode) in one dwordx4
-__global__ void k_trans_count(DevBatch b) {
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= b.P) return;
-  const uint32_t k = b.slot_trace[p];
-  const uint32_t o = b.trace_off[k];
-  const uint32_t s = (uint32_t)(p - o);
-  uint32_t c = 0, ns = 0;
-  if (s >= 1 && s < b.n_states[k]) {
-    const uint32_t KA = b.cand_n[p - 1], KB = b.cand_n[p];
-    c = KA * KB;
-    ns = KB ? KA : 0u;
-    const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
-    const double gc = gc_distance(b.lon[pa], b.lat[pa], b.lon[pb], b.lat[pb]);
-    b.gc[p] = gc;
-    const MatchOptions op = b.opts[b.trace_opt[k]];
-    b.pair_info[p] = make_uint4(route_bound(gc, op), time_bound(b.time[pb] - b.time[pa], op),
-                                KA | (KB << 8) | ((uint32_t)op.mode << 16), 0u);
+// u64 sums of two per-lane values over a 256-thread block, added to out[0], out[1] by one
+// atomic each: the u32 exclusive scans that lay out routes and records would wrap silently
+// past 2^32, so the host checks these totals instead of off + cnt
+__device__ __forceinline__ void block_sum2_u64(unsigned long long a, unsigned long long c, unsigned long long* out) {
+  __shared__ unsigned long long sa[4], sc[4];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    a += __shfl_down(a, d, 64);
+    c += __shfl_down(c, d, 64);
   }
-  b.trans_cnt[p] = c;
-  b.src_cnt[p] = ns;
+  if ((threadIdx.x & 63) == 0) { sa[threadIdx.x >> 6] = a; sc[threadIdx.x >> 6] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long ta = sa[0] + sa[1] + sa[2] + sa[3], tc = sc[0] + sc[1] + sc[2] + sc[3];
+    if (ta) atomicAdd(out, ta);
+    if (tc) atomicAdd(out + 1, tc);
+  }
+}
+
+// transition counts for the exclusive scan that lays out route[] compactly, plus the
+// per-pair constants K2 needs (bounds, candidate counts, mode) in one dwordx4; the u64
+// totals of transitions and (pair, source) items go to tot[0], tot[1]
+__global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long long* tot) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t c = 0, ns = 0;
+  if (p < b.P) {   // every lane reaches the block sum below (it holds a barrier)
+    const uint32_t k = b.slot_trace[p];
+    const uint32_t o = b.trace_off[k];
+    const uint32_t s = (uint32_t)(p - o);
+    const uint32_t S = b.n_states[k];
+    if (s < S) b.state_time[p] = b.time[o + b.state_orig[p]];   // K4 reads the state times by slot
+    if (s >= 1 && s < S) {
+      const uint32_t KA = b.cand_n[p - 1], KB = b.cand_n[p];
+      c = KA * KB;
+      ns = KB ? KA : 0u;
+      const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
+      const double gc = gc_distance(b.lon[pa], b.lat[pa], b.lon[pb], b.lat[pb]);
+      b.gc[p] = gc;
+      const MatchOptions op = b.opts[b.trace_opt[k]];
+      b.pair_info[p] = make_uint4(route_bound(gc, op), time_bound(b.time[pb] - b.time[pa], op),
+                                  KA | (KB << 8) | ((uint32_t)op.mode << 16), 0u);
+    }
+    b.trans_cnt[p] = c;
+    b.src_cnt[p] = ns;
+  }
+  block_sum2_u64(c, ns, tot);
 }
 
 // one work item per (layer pair, source candidate): item -> pair slot
@@ -1378,13 +1402,15 @@ __device__ void backtrace_chain(const DevBatch& b, VitGroup& gs, uint32_t o, uin
   __threadfence_block();  // this wave's bp stores are visible to its loads
   int t = (int)end;
   for (;;) {
+    uint4 row[kVitBt / 16];
 #pragma unroll
-    for (int x = 0; x < kVitBt / 16; ++x) {
+    for (int x = 0; x < kVitBt / 16; ++x) {   // every row load in flight before the LDS stores
       const int lay = t - (j + 16 * x);
-      uint4 row = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-      if (lay >= 0) row = *reinterpret_cast<const uint4*>(b.bp + (uint64_t)(o + lay) * kMaxCand);
-      gs.bst[j + 16 * x] = row;
+      row[x] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+      if (lay >= 0) row[x] = *reinterpret_cast<const uint4*>(b.bp + (uint64_t)(o + lay) * kMaxCand);
     }
+#pragma unroll
+    for (int x = 0; x < kVitBt / 16; ++x) gs.bst[j + 16 * x] = row[x];
     wave_sync();
     if (j == 0) {
       uint32_t l = 0, done = 0;
@@ -1510,15 +1536,18 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
       int arg = -1;
       if (KB && !start) {
         const uint32_t jj = min((uint32_t)j, KB - 1u);
+        // row i of the layer's K_A x K_B routes starts at rel + i * KB; sources past prevK
+        // read slots that are never selected (i0 + x < prevK), so no index is clamped
+        const uint32_t* rp = gs.route + rel + jj;
         for (uint32_t i0 = 0; i0 < prevK; i0 += 4) {
           double ci[4];
           uint32_t rr[4];
 #pragma unroll
           for (int x = 0; x < 4; ++x) {
-            const uint32_t i = min(i0 + x, prevK - 1u);
-            ci[x] = gs.cost[i];
-            rr[x] = gs.route[rel + i * KB + jj];
+            ci[x] = gs.cost[i0 + x];
+            rr[x] = rp[x * KB];
           }
+          rp += 4 * KB;
           // an invalid route or an unreachable source gives +inf, which never wins
 #pragma unroll
           for (int x = 0; x < 4; ++x) {
@@ -1767,7 +1796,12 @@ __device__ __forceinline__ void run_piece(RunState& R, const TravRec& t, uint8_t
 #endif
 constexpr uint32_t kSegChunk = RM_SEG_CHUNK;   // traversal records staged per chunk
 constexpr uint32_t kSegSpan = RM_SEG_CHUNK;    // first-record span of the traces a block takes
-constexpr uint32_t kSegThreads = 256;
+#ifndef RM_SEG_THREADS
+#define RM_SEG_THREADS 256
+#endif
+constexpr uint32_t kSegThreads = RM_SEG_THREADS;
+constexpr uint32_t kSegRpl = kSegChunk / kSegThreads;   // records per lane in the flag / scan phases
+static_assert(kSegRpl * kSegThreads == kSegChunk && kSegRpl >= 1 && kSegThreads % 64 == 0, "k_segments shape");
 
 // a run open at a chunk's end (its records continue in the next chunk)
 struct RunCarry {
@@ -1813,11 +1847,9 @@ __device__ __forceinline__ void seg_build_slot(const DevGraph& g, const DevBatch
   const uint32_t r0 = b.trav_off[l];
   if (r0 >= c1 || r0 + ns <= c0) return;
   const uint32_t k = b.slot_trace[l];
-  const uint32_t o = b.trace_off[k];
   const uint32_t i = (uint32_t)b.choice[l - 1], j = (uint32_t)b.choice[l];
   const uint32_t sa = b.cand_desc[((l - 1) * kMaxCand + i) * 2].y, sb = b.cand_desc[(l * kMaxCand + j) * 2].y;
-  const uint32_t oa = b.state_orig[l - 1], ob = b.state_orig[l];
-  const double ta = b.time[o + oa], tb = b.time[o + ob];
+  const double ta = b.state_time[l - 1], tb = b.state_time[l];
   const uint32_t D = b.route_dist[l];
   const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
   // a trace that failed (trace_err) forms no segments: its records become empty pieces
@@ -1919,11 +1951,11 @@ __global__ void __launch_bounds__(kSegThreads) k_segments(DevGraph g, DevBatch b
     }
     __syncthreads();
     // ---- flags: previous kept record of the chain, in LDS or carried from before the chunk
+    uint32_t hv[kSegRpl];
     uint32_t hsum = 0;
-    uint32_t hv[2];
 #pragma unroll
-    for (int y = 0; y < 2; ++y) {
-      const uint32_t r = tid * 2 + y;
+    for (uint32_t y = 0; y < kSegRpl; ++y) {
+      const uint32_t r = tid * kSegRpl + y;
       hv[y] = 0;
       if (r >= n) continue;
       const TravRec& t = sm.rec[r];
@@ -1948,7 +1980,7 @@ __global__ void __launch_bounds__(kSegThreads) k_segments(DevGraph g, DevBatch b
       hv[y] = head;
       hsum += head;
     }
-    // ---- exclusive scan of the head flags (two records per lane)
+    // ---- exclusive scan of the head flags over the chunk
     uint32_t incl = hsum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1957,13 +1989,17 @@ __global__ void __launch_bounds__(kSegThreads) k_segments(DevGraph g, DevBatch b
     }
     if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
     __syncthreads();
-    uint32_t wbase = 0;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) wbase += sm.wsum[w];
-    const uint32_t nh = sm.wsum[0] + sm.wsum[1] + sm.wsum[2] + sm.wsum[3];
+    uint32_t wbase = 0, nh = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kSegThreads / 64; ++w) {
+      const uint32_t ws = sm.wsum[w];
+      wbase += w < (tid >> 6) ? ws : 0u;
+      nh += ws;
+    }
     uint32_t ex = wbase + incl - hsum;
 #pragma unroll
-    for (int y = 0; y < 2; ++y) {
-      const uint32_t r = tid * 2 + y;
+    for (uint32_t y = 0; y < kSegRpl; ++y) {
+      const uint32_t r = tid * kSegRpl + y;
       if (r < n) {
         sm.scan[r] = ex;
         if (hv[y]) sm.pos[ex] = (uint16_t)r;
@@ -2126,25 +2162,17 @@ __global__ void __launch_bounds__(64) k_report_lists(uint32_t T, const uint32_t*
 
 // u64 totals of one or two u32 count arrays: the u32 exclusive scans that lay out routes and
 // records would wrap silently past 2^32, so the host checks these totals instead of off+cnt
-__global__ void __launch_bounds__(256) k_sum_u64(const uint32_t* a, const uint32_t* c, uint64_t n,
-                                                 unsigned long long* out) {
-  __shared__ unsigned long long sa[256], sc[256];
-  unsigned long long va = 0, vc = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u) {
-    va += a[i];
-    if (c) vc += c[i];
+// u64 total of a u32 count array (four per lane, one atomic per block)
+__global__ void __launch_bounds__(256) k_sum_u64(const uint32_t* a, uint64_t n, unsigned long long* out) {
+  const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+  unsigned long long v = 0;
+  if (i + 4 <= n) {
+    const uint4 q = *reinterpret_cast<const uint4*>(a + i);
+    v = (unsigned long long)q.x + q.y + q.z + q.w;
+  } else {
+    for (uint64_t x = i; x < n; ++x) v += a[x];
   }
-  sa[threadIdx.x] = va;
-  sc[threadIdx.x] = vc;
-  __syncthreads();
-  for (int d = 128; d > 0; d >>= 1) {
-    if ((int)threadIdx.x < d) { sa[threadIdx.x] += sa[threadIdx.x + d]; sc[threadIdx.x] += sc[threadIdx.x + d]; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    atomicAdd(out, sa[0]);
-    if (c) atomicAdd(out + 1, sc[0]);
-  }
+  block_sum2_u64(v, 0, out);
 }
 
 __global__ void k_fill_edge_src(const uint32_t* node_off, uint32_t n_nodes, uint32_t* edge_src) {
@@ -2354,6 +2382,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.lon = dalloc<float>(L, cp); w.lat = dalloc<float>(L, cp); w.time = dalloc<double>(L, cp);
   w.acc = dalloc<float>(L, cp); w.opts = dalloc<MatchOptions>(L, co); w.trace_opt = dalloc<uint32_t>(L, ct);
   w.slot_trace = dalloc<uint32_t>(L, cp); w.n_states = dalloc<uint32_t>(L, ct); w.state_orig = dalloc<uint32_t>(L, cp);
+  w.state_time = dalloc<double>(L, cp);
   w.cand_n = dalloc<uint8_t>(L, cp); w.cand_desc = dalloc<uint4>(L, cp * kMaxCand * 2);
   w.cand_sq = dalloc<float>(L, cp * kMaxCand); w.pair_info = dalloc<uint4>(L, cp);
   w.trans_cnt = dalloc<uint32_t>(L, cp); w.trans_off = dalloc<uint32_t>(L, cp); w.gc = dalloc<double>(L, cp);
@@ -2476,7 +2505,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.T = T; v.P = P;
   v.trace_off = w.trace_off; v.lon = w.lon; v.lat = w.lat; v.time = w.time; v.acc = w.acc;
   v.opts = w.opts; v.trace_opt = w.trace_opt;
-  v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig;
+  v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig; v.state_time = w.state_time;
   v.cand_n = w.cand_n; v.cand_desc = w.cand_desc; v.cand_sq = w.cand_sq;
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
@@ -2567,7 +2596,7 @@ void Matcher::run_device(const RunParams& rp) {
   RM_HIP(hipMemsetAsync(w.trace_err, 0, T * sizeof(uint32_t), st));
   RM_HIP(hipMemsetAsync(w.tot64, 0, 4 * sizeof(unsigned long long), st));
   DevBatch v = make_view(w, T, P);
-  const uint32_t sum_grid = (uint32_t)std::min<uint64_t>((P + 255) / 256, 1024);
+  const uint32_t sum_grid = (uint32_t)((P + 1023) / 1024);   // k_sum_u64: four counts per lane
 
   tic(kKStates);
   hipLaunchKernelGGL(k_states, dim3((T + 63) / 64), dim3(64), 0, st, v);
@@ -2577,12 +2606,11 @@ void Matcher::run_device(const RunParams& rp) {
   hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, g, v);
   toc(kKCandidates);
   tic(kKScan);
-  hipLaunchKernelGGL(k_trans_count, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
+  hipLaunchKernelGGL(k_trans_count, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v, w.tot64);
   size_t tmp = w.scan_tmp_bytes;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.trans_cnt, w.trans_off, (int)P, st));
   tmp = w.scan_tmp_bytes;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.src_cnt, w.src_off, (int)P, st));
-  hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.trans_cnt, w.src_cnt, P, w.tot64);
   toc(kKScan);
   RM_HIP(hipMemcpyAsync(htot, w.tot64, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   RM_HIP(hipStreamSynchronize(st));
@@ -2652,7 +2680,7 @@ void Matcher::run_device(const RunParams& rp) {
     tmp = w.scan_tmp_bytes;
     RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
     RM_HIP(hipMemsetAsync(w.tot64 + 2, 0, sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, (const uint32_t*)nullptr, P, w.tot64 + 2);
+    hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot64 + 2);
     toc(kKSegments);
     RM_HIP(hipMemcpyAsync(htot + 2, w.tot64 + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     read_ctl();
@@ -2676,7 +2704,7 @@ void Matcher::run_device(const RunParams& rp) {
       tmp = w.scan_tmp_bytes;
       RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
       RM_HIP(hipMemsetAsync(w.tot64 + 2, 0, sizeof(unsigned long long), st));
-      hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, (const uint32_t*)nullptr, P, w.tot64 + 2);
+      hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot64 + 2);
       RM_HIP(hipMemcpyAsync(htot + 2, w.tot64 + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
       read_ctl();
     }

@@ -98,6 +98,7 @@ struct Workspace {
   float* acc = nullptr; MatchOptions* opts = nullptr; uint32_t* trace_opt = nullptr;
   // per slot
   uint32_t* slot_trace = nullptr; uint32_t* n_states = nullptr; uint32_t* state_orig = nullptr;
+  double* state_time = nullptr;     // epoch time of the state at each slot (K4 interpolation)
   // candidate descriptors, 2 x uint4 per (slot, rank): {road, s_cm, len_cm, spf | spr << 16},
   // {node0, node1, time_ms(s_cm) forward from node0, time_ms(len_cm - s_cm) reverse from node1}
   // (sp* = mode-capped speed of the directed edge in 0.1 km/h, 0 when the mode cannot use it)

@@ -9,6 +9,7 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 #include "rm_common.hpp"
 
@@ -67,6 +68,31 @@ struct WorldParams {
 };
 
 Graph build_world(const WorldParams& p);
+
+// Graph assembly shared by the world builder and the OSM importer (graph_osm.cpp).
+// A road: its two graph nodes, its shape (lon, lat incl. both endpoints), the info words
+// and way ids of its forward (n0 -> n1) and reverse directed edges.
+struct RoadInput {
+  uint32_t n0, n1;
+  std::vector<std::pair<float, float>> shape;
+  uint32_t info_fwd, info_rev, way_fwd, way_rev;
+};
+// shape vertices (cumulative cm), road lengths, CSR of directed edges (stable by source
+// node, forward before reverse per road), road -> edge maps; node arrays must be set.
+// edge_seg / edge_seg_off are reset to "no OSMLR segment".
+void assemble_roads(Graph& g, const std::vector<RoadInput>& roads);
+// cell_off / cell_item of g.grid from its origin, cell size and dimensions
+void build_grid_index(Graph& g);
+// length of a straight shape piece, metres (equirectangular at its mean latitude)
+double piece_m(float lon0, float lat0, float lon1, float lat1);
+
+// OpenStreetMap exchange of a graph (graph_osm.cpp).  export_osm writes OSM XML (".osm")
+// whose ways, tags and relations carry everything an .rmg holds; import_osm reads it back
+// bit-identically, or builds a graph from a generic OSM XML file (intersections split ways,
+// highway / maxspeed / oneway / access tags give speeds and access, no OSMLR segments
+// unless osmlr relations are present; cell_m sizes the grid index then).
+void export_osm(const Graph& g, const std::string& path);
+Graph import_osm(const std::string& path, double cell_m = 100.0);
 
 // Synthetic GPS traces (restating reference py/generate_test_trace.py:35-104,120-164):
 // fastest routes (A* on travel time) to random destinations, driven at edge speed and

@@ -49,14 +49,6 @@ uint64_t mix(uint64_t a, uint64_t b) { uint64_t x = a * 0x9e3779b97f4a7c15ull ^ 
 
 double round6(double x) { return std::round(x * 1e6) / 1e6; }
 
-// length of a straight shape piece, metres (equirectangular at its mean latitude)
-double piece_m(float lon0, float lat0, float lon1, float lat1) {
-  const double ml = 0.5 * ((double)lat0 + (double)lat1);
-  const double dy = ((double)lat1 - (double)lat0) * kMetersPerDegLat;
-  const double dx = ((double)lon1 - (double)lon0) * (kMetersPerDegLonEq * std::cos(ml * kDegToRad));
-  return std::sqrt(dx * dx + dy * dy);
-}
-
 int line_level(uint32_t idx, const WorldParams& p) {
   if (p.highway_every && idx % p.highway_every == 0) return 0;
   if (p.arterial_every && idx % p.arterial_every == 0) return 1;
@@ -75,6 +67,100 @@ struct RoadSpec {
 };
 
 }  // namespace
+
+// length of a straight shape piece, metres (equirectangular at its mean latitude)
+double piece_m(float lon0, float lat0, float lon1, float lat1) {
+  const double ml = 0.5 * ((double)lat0 + (double)lat1);
+  const double dy = ((double)lat1 - (double)lat0) * kMetersPerDegLat;
+  const double dx = ((double)lon1 - (double)lon0) * (kMetersPerDegLonEq * std::cos(ml * kDegToRad));
+  return std::sqrt(dx * dx + dy * dy);
+}
+
+void assemble_roads(Graph& g, const std::vector<RoadInput>& roads) {
+  // roads -> shapes, lengths
+  const uint32_t R = (uint32_t)roads.size();
+  g.road_node0.resize(R); g.road_node1.resize(R); g.road_len_cm.resize(R);
+  g.road_vert_off.resize(R + 1);
+  g.road_fwd.assign(R, kNone); g.road_rev.assign(R, kNone);
+  g.verts.clear();
+  for (uint32_t r = 0; r < R; ++r) {
+    const RoadInput& rs = roads[r];
+    g.road_node0[r] = rs.n0; g.road_node1[r] = rs.n1;
+    g.road_vert_off[r] = (uint32_t)g.verts.size();
+    double cum = 0;
+    uint32_t last_cm = 0;
+    for (size_t k = 0; k < rs.shape.size(); ++k) {
+      if (k) cum += piece_m(rs.shape[k - 1].first, rs.shape[k - 1].second, rs.shape[k].first, rs.shape[k].second);
+      uint32_t cm = (uint32_t)std::llround(cum * 100.0);
+      if (k && cm <= last_cm) cm = last_cm + 1;  // strictly increasing
+      last_cm = cm;
+      VertRec v;
+      v.lon = rs.shape[k].first; v.lat = rs.shape[k].second; v.cum_cm = cm;
+      v.road = (k + 1 < rs.shape.size()) ? r : kNone;
+      g.verts.push_back(v);
+    }
+    g.road_len_cm[r] = last_cm;
+  }
+  g.road_vert_off[R] = (uint32_t)g.verts.size();
+
+  // directed edges -> CSR (stable by source node)
+  const uint32_t N = (uint32_t)g.node_lon.size();
+  struct DE { uint32_t from; EdgeRec rec; uint32_t way; };
+  std::vector<DE> des;
+  des.reserve(2 * (size_t)R);
+  for (uint32_t r = 0; r < R; ++r) {
+    des.push_back({roads[r].n0, {roads[r].n1, g.road_len_cm[r], roads[r].info_fwd, r << 1}, roads[r].way_fwd});
+    des.push_back({roads[r].n1, {roads[r].n0, g.road_len_cm[r], roads[r].info_rev, (r << 1) | 1u}, roads[r].way_rev});
+  }
+  std::stable_sort(des.begin(), des.end(), [](const DE& a, const DE& b) { return a.from < b.from; });
+  const uint32_t E = (uint32_t)des.size();
+  g.node_off.assign(N + 1, 0);
+  g.edges.resize(E);
+  g.edge_way.resize(E);
+  for (uint32_t e = 0; e < E; ++e) {
+    g.node_off[des[e].from + 1]++;
+    g.edges[e] = des[e].rec;
+    g.edge_way[e] = des[e].way;
+    const uint32_t road = des[e].rec.road >> 1;
+    if (des[e].rec.road & 1u) g.road_rev[road] = e; else g.road_fwd[road] = e;
+  }
+  for (uint32_t n = 0; n < N; ++n) g.node_off[n + 1] += g.node_off[n];
+  g.edge_seg.assign(E, kNone);
+  g.edge_seg_off.assign(E, 0);
+}
+
+void build_grid_index(Graph& g) {
+  GridIndex& gi = g.grid;
+  const size_t ncell = (size_t)gi.ncx * gi.ncy;
+  if (ncell > 400000000ull) throw std::runtime_error("grid index too large; raise cell_m");
+  std::vector<uint32_t> cnt(ncell + 1, 0);
+  auto cell_range = [&](const VertRec& a, const VertRec& b, uint32_t& x0, uint32_t& x1, uint32_t& y0, uint32_t& y1) {
+    const double lo0 = std::min(a.lon, b.lon), lo1 = std::max(a.lon, b.lon);
+    const double la0 = std::min(a.lat, b.lat), la1 = std::max(a.lat, b.lat);
+    x0 = (uint32_t)std::floor((lo0 - gi.lon0) / gi.dlon); x1 = (uint32_t)std::floor((lo1 - gi.lon0) / gi.dlon);
+    y0 = (uint32_t)std::floor((la0 - gi.lat0) / gi.dlat); y1 = (uint32_t)std::floor((la1 - gi.lat0) / gi.dlat);
+    x1 = std::min(x1, gi.ncx - 1); y1 = std::min(y1, gi.ncy - 1);
+  };
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      gi.cell_off.assign(ncell + 1, 0);
+      for (size_t c = 0; c < ncell; ++c) gi.cell_off[c + 1] = gi.cell_off[c] + cnt[c];
+      gi.cell_item.resize(gi.cell_off[ncell]);
+      std::fill(cnt.begin(), cnt.end(), 0);
+    }
+    for (uint32_t v = 0; v + 1 < (uint32_t)g.verts.size(); ++v) {
+      if (g.verts[v].road == kNone) continue;
+      uint32_t x0, x1, y0, y1;
+      cell_range(g.verts[v], g.verts[v + 1], x0, x1, y0, y1);
+      for (uint32_t y = y0; y <= y1; ++y)
+        for (uint32_t x = x0; x <= x1; ++x) {
+          const size_t c = (size_t)y * gi.ncx + x;
+          if (pass == 1) gi.cell_item[gi.cell_off[c] + cnt[c]] = v;
+          cnt[c]++;
+        }
+    }
+  }
+}
 
 Graph build_world(const WorldParams& p) {
   if (p.rows < 2 || p.cols < 2) throw std::runtime_error("world needs at least 2x2 nodes");
@@ -180,55 +266,13 @@ Graph build_world(const WorldParams& p) {
       make_piece(i * p.cols + j, (i + 1) * p.cols + j, major(i, j), major(i + 1, j), line_level(j, p),
                  1000u + p.rows + j, p.rows + j, (1ull << 62) | ((uint64_t)j << 32) | i);
 
-  // roads -> shapes, lengths
-  const uint32_t R = (uint32_t)roads.size();
-  g.road_node0.resize(R); g.road_node1.resize(R); g.road_len_cm.resize(R);
-  g.road_vert_off.resize(R + 1);
-  g.road_fwd.assign(R, kNone); g.road_rev.assign(R, kNone);
-  for (uint32_t r = 0; r < R; ++r) {
-    const RoadSpec& rs = roads[r];
-    g.road_node0[r] = rs.n0; g.road_node1[r] = rs.n1;
-    g.road_vert_off[r] = (uint32_t)g.verts.size();
-    double cum = 0;
-    uint32_t last_cm = 0;
-    for (size_t k = 0; k < rs.shape.size(); ++k) {
-      if (k) cum += piece_m(rs.shape[k - 1].first, rs.shape[k - 1].second, rs.shape[k].first, rs.shape[k].second);
-      uint32_t cm = (uint32_t)std::llround(cum * 100.0);
-      if (k && cm <= last_cm) cm = last_cm + 1;  // strictly increasing
-      last_cm = cm;
-      VertRec v;
-      v.lon = rs.shape[k].first; v.lat = rs.shape[k].second; v.cum_cm = cm;
-      v.road = (k + 1 < rs.shape.size()) ? r : kNone;
-      g.verts.push_back(v);
-    }
-    g.road_len_cm[r] = last_cm;
+  {
+    std::vector<RoadInput> in(roads.size());
+    for (size_t r = 0; r < roads.size(); ++r)
+      in[r] = {roads[r].n0, roads[r].n1, roads[r].shape, roads[r].info_fwd, roads[r].info_rev, roads[r].way, roads[r].way};
+    assemble_roads(g, in);
   }
-  g.road_vert_off[R] = (uint32_t)g.verts.size();
-
-  // directed edges -> CSR (stable by source node)
   const uint32_t N = (uint32_t)g.node_lon.size();
-  struct DE { uint32_t from; EdgeRec rec; };
-  std::vector<DE> des;
-  des.reserve(2 * (size_t)R);
-  for (uint32_t r = 0; r < R; ++r) {
-    des.push_back({roads[r].n0, {roads[r].n1, g.road_len_cm[r], roads[r].info_fwd, r << 1}});
-    des.push_back({roads[r].n1, {roads[r].n0, g.road_len_cm[r], roads[r].info_rev, (r << 1) | 1u}});
-  }
-  std::stable_sort(des.begin(), des.end(), [](const DE& a, const DE& b) { return a.from < b.from; });
-  const uint32_t E = (uint32_t)des.size();
-  g.node_off.assign(N + 1, 0);
-  g.edges.resize(E);
-  for (uint32_t e = 0; e < E; ++e) {
-    g.node_off[des[e].from + 1]++;
-    g.edges[e] = des[e].rec;
-    const uint32_t road = des[e].rec.road >> 1;
-    if (des[e].rec.road & 1u) g.road_rev[road] = e; else g.road_fwd[road] = e;
-  }
-  for (uint32_t n = 0; n < N; ++n) g.node_off[n + 1] += g.node_off[n];
-  g.edge_seg.assign(E, kNone);
-  g.edge_seg_off.assign(E, 0);
-  g.edge_way.resize(E);
-  for (uint32_t e = 0; e < E; ++e) g.edge_way[e] = roads[g.edges[e].road >> 1].way;
 
   // OSMLR chaining along each line and direction
   const double tile_size[3] = {4.0, 1.0, 0.25};
@@ -294,35 +338,7 @@ Graph build_world(const WorldParams& p) {
   gi.lat0 = (double)min_lat - gi.dlat;
   gi.ncx = (uint32_t)std::ceil(((double)max_lon - gi.lon0) / gi.dlon) + 2;
   gi.ncy = (uint32_t)std::ceil(((double)max_lat - gi.lat0) / gi.dlat) + 2;
-  const size_t ncell = (size_t)gi.ncx * gi.ncy;
-  if (ncell > 400000000ull) throw std::runtime_error("grid index too large; raise cell_m");
-  std::vector<uint32_t> cnt(ncell + 1, 0);
-  auto cell_range = [&](const VertRec& a, const VertRec& b, uint32_t& x0, uint32_t& x1, uint32_t& y0, uint32_t& y1) {
-    const double lo0 = std::min(a.lon, b.lon), lo1 = std::max(a.lon, b.lon);
-    const double la0 = std::min(a.lat, b.lat), la1 = std::max(a.lat, b.lat);
-    x0 = (uint32_t)std::floor((lo0 - gi.lon0) / gi.dlon); x1 = (uint32_t)std::floor((lo1 - gi.lon0) / gi.dlon);
-    y0 = (uint32_t)std::floor((la0 - gi.lat0) / gi.dlat); y1 = (uint32_t)std::floor((la1 - gi.lat0) / gi.dlat);
-    x1 = std::min(x1, gi.ncx - 1); y1 = std::min(y1, gi.ncy - 1);
-  };
-  for (int pass = 0; pass < 2; ++pass) {
-    if (pass == 1) {
-      gi.cell_off.assign(ncell + 1, 0);
-      for (size_t c = 0; c < ncell; ++c) gi.cell_off[c + 1] = gi.cell_off[c] + cnt[c];
-      gi.cell_item.resize(gi.cell_off[ncell]);
-      std::fill(cnt.begin(), cnt.end(), 0);
-    }
-    for (uint32_t v = 0; v + 1 < (uint32_t)g.verts.size(); ++v) {
-      if (g.verts[v].road == kNone) continue;
-      uint32_t x0, x1, y0, y1;
-      cell_range(g.verts[v], g.verts[v + 1], x0, x1, y0, y1);
-      for (uint32_t y = y0; y <= y1; ++y)
-        for (uint32_t x = x0; x <= x1; ++x) {
-          const size_t c = (size_t)y * gi.ncx + x;
-          if (pass == 1) gi.cell_item[gi.cell_off[c] + cnt[c]] = v;
-          cnt[c]++;
-        }
-    }
-  }
+  build_grid_index(g);
   g.validate();
   return g;
 }

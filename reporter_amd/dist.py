@@ -59,6 +59,20 @@ def shard_by_uuid(uuids, points, world_size, buckets_per_rank=16):
     return [np.nonzero(owner[b] == r)[0] for r in range(world_size)]
 
 
+def _stdout_to_stderr(fn):
+    """Run fn with file descriptor 1 pointed at stderr: RCCL prints a version banner on
+    stdout at communicator init, and bench.py's stdout must hold exactly one JSON line."""
+    import sys
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        return fn()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class Comm:
     """RCCL communicator for one rank (one process per GPU, single node)."""
 
@@ -89,7 +103,7 @@ class Comm:
                     raise TimeoutError("rank %d: no RCCL id at %s" % (rank, path))
                 time.sleep(0.05)
             C.memmove(uid, data, 128)
-        self._h = L.rm_comm_init(world_size, rank, uid, device)
+        self._h = _stdout_to_stderr(lambda: L.rm_comm_init(world_size, rank, uid, device))
         if not self._h:
             raise _lib.RmError(_lib.last_error())
         self._path = path

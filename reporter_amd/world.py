@@ -51,6 +51,18 @@ def build_world(path, rows, cols, block_m=100.0, seed=1, cell_m=None, **kw):
     return path
 
 
+def export_osm(graph_path, osm_path):
+    """The .rmg graph as OSM XML (routing tags + exact reporter:* tags + osmlr relations)."""
+    _lib.check(_lib.lib().rm_graph_export_osm(os.fsencode(graph_path), os.fsencode(osm_path)))
+    return osm_path
+
+
+def import_osm(osm_path, graph_path, cell_m=100.0):
+    """OSM XML -> .rmg (bit-identical for an export_osm file; generic OSM split at intersections)."""
+    _lib.check(_lib.lib().rm_graph_import_osm(os.fsencode(osm_path), os.fsencode(graph_path), float(cell_m)))
+    return graph_path
+
+
 def graph_info(path):
     out = (C.c_uint64 * 7)()
     _lib.check(_lib.lib().rm_graph_info(os.fsencode(path), out))

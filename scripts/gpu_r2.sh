@@ -9,9 +9,9 @@ mkdir -p $O
 export TMPDIR=/tmp
 cd $R
 K=${1:-}
-ARGS="-m gpu -v -s --maxfail 6 --timeout 900 --timeout-method thread"
-if [ -n "$K" ]; then ARGS="$ARGS -k $K"; fi
-timeout -k 10 1500 python -u -m pytest tests $ARGS > $O/pytest_gpu.log 2>&1
+ARGS=(-m gpu -v -s --maxfail 6 --timeout 900 --timeout-method thread)
+if [ -n "$K" ]; then ARGS+=(-k "$K"); fi
+timeout -k 10 1500 python -u -m pytest tests "${ARGS[@]}" > $O/pytest_gpu.log 2>&1
 rc=$?
 grep -E "PASSED|FAILED|ERROR|passed|failed" $O/pytest_gpu.log | tail -60
 case $rc in 124|134|137|139) echo "pytest fatal rc=$rc"; exit $rc;; esac
