@@ -121,10 +121,16 @@ int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids); /* n_segments ids 
 int rm_engine_set_ball_radius(rm_engine* e, double radius_m);
 /* Host-only: the engine's automatic radius for a graph file — the largest of 2000 m (meili's
  * default breakage distance, so every default-bounded transition is a table probe), 1500,
- * 1000, 700, 500 m whose estimated tables stay within 16 GiB per mode; else 400 m. */
+ * 1000, 700, 500 m whose estimated tables stay within 72 GiB per mode (of 288 GB); else 400 m. */
 int rm_graph_auto_ball_radius(const char* graph_path, double* radius_m);
-/* out[5]: radius m, keys stored, table entries (16 B each), nodes without a table, build ms */
-int rm_engine_ball_stats(const rm_engine* e, int mode, double out[5]);
+/* out[6]: radius m, keys stored, table entries (16 B each), nodes without a table, build ms,
+ * 1 when the tables were built on the GPU (small balls on large graphs; env RM_BALL_BUILD=host|gpu) */
+int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]);
+/* The engine's own tables of `mode` (built by a run that used the mode), probed on the device as
+ * K2 probes them: keys[2i], keys[2i+1] from node from[i] to road[i]'s node0 / node1, all-ones
+ * outside the ball or for a node without a table.  Compare with rm_balls_lookup (host build). */
+int rm_engine_ball_lookup(rm_engine* e, int mode, uint64_t n, const uint32_t* from, const uint32_t* road,
+                          uint64_t* keys);
 /* Host-only check of the ball tables (no GPU): builds the balls of `mode` for the graph
  * file and looks up n (from node, road) pairs the way the K2 kernel probes them;
  * keys[2i], keys[2i+1] = dist_cm << 32 | time_ms from `from` to the road's node0 / node1,

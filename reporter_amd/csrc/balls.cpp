@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <chrono>
+#include <cstdlib>
 #include <functional>
 #include <queue>
 #include <stdexcept>
@@ -105,9 +106,9 @@ void parallel_nodes(uint32_t n, int threads, F&& f) {
 
 }  // namespace
 
-uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes) {
+namespace {
+double node_density(const Graph& g) {   // nodes per m^2 over the graph's bounding box
   const uint32_t N = g.num_nodes();
-  if (N < 2) return 40000u;
   float lo0 = g.node_lon[0], lo1 = lo0, la0 = g.node_lat[0], la1 = la0;
   for (uint32_t n = 1; n < N; ++n) {
     lo0 = std::min(lo0, g.node_lon[n]); lo1 = std::max(lo1, g.node_lon[n]);
@@ -116,7 +117,44 @@ uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes) {
   const double mid = 0.5 * ((double)la0 + (double)la1) * 3.14159265358979323846 / 180.0;
   const double w = std::max(1.0, ((double)lo1 - lo0) * 111320.0 * std::cos(mid));
   const double h = std::max(1.0, ((double)la1 - la0) * 110567.0);
-  const double rho = (double)N / (w * h);                                 // nodes per m^2
+  return (double)N / (w * h);
+}
+}  // namespace
+
+double est_ball_nodes(const Graph& g, uint32_t radius_cm) {
+  const uint32_t N = g.num_nodes();
+  if (N < 2) return (double)N;
+  const double rm = radius_cm / 100.0;
+  return std::min((double)N, node_density(g) * 3.14159265358979323846 * rm * rm);
+}
+
+void road_incidence(const Graph& g, std::vector<uint32_t>& inc_off, std::vector<uint32_t>& inc) {
+  const uint32_t N = g.num_nodes(), R = g.num_roads();
+  inc_off.assign(N + 1, 0);
+  for (uint32_t r = 0; r < R; ++r) {
+    inc_off[g.road_node0[r] + 1]++;
+    if (g.road_node1[r] != g.road_node0[r]) inc_off[g.road_node1[r] + 1]++;
+  }
+  for (uint32_t n = 0; n < N; ++n) inc_off[n + 1] += inc_off[n];
+  inc.resize(inc_off[N]);
+  std::vector<uint32_t> fill(inc_off.begin(), inc_off.end() - 1);
+  for (uint32_t r = 0; r < R; ++r) {
+    inc[fill[g.road_node0[r]]++] = r;
+    if (g.road_node1[r] != g.road_node0[r]) inc[fill[g.road_node1[r]]++] = r;
+  }
+}
+
+uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes) {
+  if (budget_bytes == 0) {
+    budget_bytes = kBallAutoBudget;
+    if (const char* s = std::getenv("RM_BALL_BUDGET_GB")) {
+      const double gb = std::atof(s);
+      if (gb > 0.0) budget_bytes = (uint64_t)(gb * (double)(1ull << 30));
+    }
+  }
+  const uint32_t N = g.num_nodes();
+  if (N < 2) return 40000u;
+  const double rho = node_density(g);                                     // nodes per m^2
   const double roads_per_node = 1.3 * (double)g.num_roads() / (double)N;  // + roads crossing the rim
   for (const uint32_t r : {200000u, 150000u, 100000u, 70000u, 50000u}) {
     const double rm = r / 100.0;
@@ -141,20 +179,8 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
   if (radius_cm > kBallMaxRadiusCm) throw std::runtime_error("ball radius above 10 km");
   // node -> incident roads
   const uint32_t R = g.num_roads();
-  std::vector<uint32_t> inc_off(N + 1, 0), inc;
-  for (uint32_t r = 0; r < R; ++r) {
-    inc_off[g.road_node0[r] + 1]++;
-    if (g.road_node1[r] != g.road_node0[r]) inc_off[g.road_node1[r] + 1]++;
-  }
-  for (uint32_t n = 0; n < N; ++n) inc_off[n + 1] += inc_off[n];
-  inc.resize(inc_off[N]);
-  {
-    std::vector<uint32_t> fill(inc_off.begin(), inc_off.end() - 1);
-    for (uint32_t r = 0; r < R; ++r) {
-      inc[fill[g.road_node0[r]]++] = r;
-      if (g.road_node1[r] != g.road_node0[r]) inc[fill[g.road_node1[r]]++] = r;
-    }
-  }
+  std::vector<uint32_t> inc_off, inc;
+  road_incidence(g, inc_off, inc);
   threads = std::max(1, threads);
   std::vector<Scratch> scr;
   std::vector<RoadAcc> acc_r;

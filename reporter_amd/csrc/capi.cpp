@@ -602,11 +602,21 @@ int rm_engine_set_ball_radius(rm_engine* e, double radius_m) {
     e->e->set_ball_radius((uint32_t)(radius_m * 100.0));
   });
 }
-int rm_engine_ball_stats(const rm_engine* e, int mode, double out[5]) {
+int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]) {
   return guarded([&] {
     if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
     out[0] = e->e->ball_radius() / 100.0;
     e->e->ball_stats(mode, out + 1);
+    out[5] = ((e->e->ball_gpu_mask() >> mode) & 1u) ? 1.0 : 0.0;
+  });
+}
+
+int rm_engine_ball_lookup(rm_engine* e, int mode, uint64_t n, const uint32_t* from, const uint32_t* road,
+                          uint64_t* keys) {
+  return guarded([&] {
+    if (!e) throw std::runtime_error("engine is NULL");
+    if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    e->e->ball_lookup(mode, n, from, road, keys);
   });
 }
 

@@ -25,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -63,6 +64,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
+  uint2* path_sab;   // per chosen transition: offsets (cm) of its source and target candidates on their roads
   SegmentRec* segs; uint32_t* seg_base; uint32_t* seg_cnt;
   uint32_t* trav_off;
   ReportRec* reps; uint32_t* rep_cnt; ReportStats* stats;
@@ -451,10 +453,12 @@ __global__ void __launch_bounds__(64) k_candidates_wave(DevGraph g, DevBatch b) 
 }
 
 // ------------------------------------------------------------------------------------------
-// u64 sums of two per-lane values over a 256-thread block, added to out[0], out[1] by one
-// atomic each: the u32 exclusive scans that lay out routes and records would wrap silently
-// past 2^32, so the host checks these totals instead of off + cnt
-__device__ __forceinline__ void block_sum2_u64(unsigned long long a, unsigned long long c, unsigned long long* out) {
+// u64 sums of two per-lane values: the u32 exclusive scans that lay out routes and records
+// would wrap silently past 2^32, so the host checks these totals instead of off + cnt.
+// Each 256-thread block writes its pair of partials to part[2 * block]; k_sum_parts folds
+// them.  (One same-address u64 atomic per block serialises at ~12 ns across the 8 XCDs:
+// 23 k blocks of C2 cost 0.57 ms that way.)
+__device__ __forceinline__ void block_sum2_u64(unsigned long long a, unsigned long long c, unsigned long long* part) {
   __shared__ unsigned long long sa[4], sc[4];
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) {
@@ -463,17 +467,40 @@ __device__ __forceinline__ void block_sum2_u64(unsigned long long a, unsigned lo
   }
   if ((threadIdx.x & 63) == 0) { sa[threadIdx.x >> 6] = a; sc[threadIdx.x >> 6] = c; }
   __syncthreads();
+  if (threadIdx.x == 0)
+    reinterpret_cast<ulonglong2*>(part)[blockIdx.x] =
+        make_ulonglong2(sa[0] + sa[1] + sa[2] + sa[3], sc[0] + sc[1] + sc[2] + sc[3]);
+}
+
+// out[0], out[1] = sums of the nb partial pairs (one block of 1024 threads)
+__global__ void __launch_bounds__(1024) k_sum_parts(const unsigned long long* part, uint32_t nb,
+                                                    unsigned long long* out) {
+  __shared__ unsigned long long sa[16], sc[16];
+  unsigned long long a = 0, c = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += 1024) {
+    const ulonglong2 q = reinterpret_cast<const ulonglong2*>(part)[i];
+    a += q.x;
+    c += q.y;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    a += __shfl_down(a, d, 64);
+    c += __shfl_down(c, d, 64);
+  }
+  if ((threadIdx.x & 63) == 0) { sa[threadIdx.x >> 6] = a; sc[threadIdx.x >> 6] = c; }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned long long ta = sa[0] + sa[1] + sa[2] + sa[3], tc = sc[0] + sc[1] + sc[2] + sc[3];
-    if (ta) atomicAdd(out, ta);
-    if (tc) atomicAdd(out + 1, tc);
+    unsigned long long ta = 0, tc = 0;
+    for (int k = 0; k < 16; ++k) { ta += sa[k]; tc += sc[k]; }
+    out[0] = ta;
+    out[1] = tc;
   }
 }
 
 // transition counts for the exclusive scan that lays out route[] compactly, plus the
-// per-pair constants K2 needs (bounds, candidate counts, mode) in one dwordx4; the u64
-// totals of transitions and (pair, source) items go to tot[0], tot[1]
-__global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long long* tot) {
+// per-pair constants K2 needs (bounds, candidate counts, mode) in one dwordx4; the block
+// partials of the u64 totals of transitions and (pair, source) items go to part[]
+__global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long long* part) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t c = 0, ns = 0;
   if (p < b.P) {   // every lane reaches the block sum below (it holds a barrier)
@@ -496,7 +523,7 @@ __global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long l
     b.trans_cnt[p] = c;
     b.src_cnt[p] = ns;
   }
-  block_sum2_u64(c, ns, tot);
+  block_sum2_u64(c, ns, part);
 }
 
 // one work item per (layer pair, source candidate): item -> pair slot
@@ -609,9 +636,10 @@ __device__ __forceinline__ unsigned long long h_label(const SearchSmem<H, PATH>&
 // Exact lexicographic shortest (dist, time) keys from the exits of n_src source
 // candidates (descriptors src[0..n_src), source ids 0..n_src-1) to every node within
 // `bound` cm, by synchronous label-correcting rounds over an LDS frontier.  All 64 lanes call it.
+// With src == nullptr the single root is node `root` at key 0 (route-ball build).
 template <int H, bool PATH>
 __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int mode, uint32_t bound,
-                               const uint4* src, uint32_t n_src) {
+                               const uint4* src, uint32_t n_src, uint32_t root = 0) {
   const int lane = threadIdx.x;
   const uint32_t acc = mode_access(mode);
   for (int h = lane; h < H; h += kWave) {
@@ -620,7 +648,14 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
   }
   if (lane == 0) { sm.nf = 0; sm.nn = 0; sm.used = 0; sm.ovf = 0; }
   __syncthreads();
-  if ((uint32_t)lane < 2u * n_src) {  // roots: two exits per source
+  if (!src) {
+    if (lane == 0) {
+      const int slot = h_insert(sm, root);
+      sm.lab[slot] = 0ull;
+      sm.inq[slot] = 1u;
+      sm.fa[sm.nf++] = (typename SearchSmem<H, PATH>::FIdx)slot;
+    }
+  } else if ((uint32_t)lane < 2u * n_src) {  // roots: two exits per source
     const uint32_t i = lane >> 1;
     const uint4 a0 = src[2 * i], a1 = src[2 * i + 1];
     unsigned long long rk1, rk0;
@@ -1084,6 +1119,7 @@ __device__ __forceinline__ void path_walk(const DevGraph& g, const DevBatch& b, 
   uint32_t* inl = b.path_inline + p * kInlinePath;
   if (combo <= 1) {
     b.route_dist[p] = key_dist(key);
+    b.path_sab[p] = make_uint2(a0.y, b0.y);
     inl[0] = combo == 0 ? g.road_fwd[a0.x] : g.road_rev[a0.x];
     b.path_cnt[p] = 1;
     b.path_off[p] = 0;
@@ -1127,6 +1163,7 @@ __device__ __forceinline__ void path_walk(const DevGraph& g, const DevBatch& b, 
   pr[0] = exit_e;
   ++n;
   b.route_dist[p] = key_dist(key);
+  b.path_sab[p] = make_uint2(a0.y, b0.y);
   b.path_cnt[p] = n;
   if (n <= (uint32_t)kInlinePath) {
 #pragma unroll
@@ -1670,6 +1707,7 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
     b.path_cnt[p] = n;
     b.path_off[p] = at;
     b.route_dist[p] = key_dist(key);
+    b.path_sab[p] = make_uint2(a0.y, b0.y);
     sm.nf = n;
     sm.nn = at;
   }
@@ -1847,8 +1885,8 @@ __device__ __forceinline__ void seg_build_slot(const DevGraph& g, const DevBatch
   const uint32_t r0 = b.trav_off[l];
   if (r0 >= c1 || r0 + ns <= c0) return;
   const uint32_t k = b.slot_trace[l];
-  const uint32_t i = (uint32_t)b.choice[l - 1], j = (uint32_t)b.choice[l];
-  const uint32_t sa = b.cand_desc[((l - 1) * kMaxCand + i) * 2].y, sb = b.cand_desc[(l * kMaxCand + j) * 2].y;
+  const uint2 sab = b.path_sab[l];
+  const uint32_t sa = sab.x, sb = sab.y;
   const double ta = b.state_time[l - 1], tb = b.state_time[l];
   const uint32_t D = b.route_dist[l];
   const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
@@ -1857,23 +1895,18 @@ __device__ __forceinline__ void seg_build_slot(const DevGraph& g, const DevBatch
   uint64_t x = 0;
   // four path edges per group: every graph load of a group is issued before its LDS stores
   for (uint32_t q0 = 0; q0 < ns; q0 += 4) {
-    uint32_t e[4], sd[4], soff[4], way[4];
-    uint4 rec[4];
+    uint32_t e[4];
+    uint4 sr[4];   // packed K4 edge records (DevGraph::seg_rec)
 #pragma unroll
     for (int y = 0; y < 4; ++y) e[y] = pe[min(q0 + y, ns - 1u)];
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      rec[y] = g.edges[e[y]];
-      sd[y] = g.edge_seg[e[y]];
-      soff[y] = g.edge_seg_off[e[y]];
-      way[y] = g.edge_way[e[y]];
-    }
+    for (int y = 0; y < 4; ++y) sr[y] = g.seg_rec[e[y]];
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
       const uint32_t q = q0 + y;
       if (q >= ns) break;
-      const uint32_t L = rec[y].y;
-      const bool rev = (rec[y].w & 1u) != 0u;
+      const uint32_t L = sr[y].x & 0x3fffffffu;
+      const bool rev = (sr[y].x >> 31) != 0u;
       uint32_t b0 = 0, b1 = L;
       if (q == 0) b0 = rev ? L - sa : sa;
       if (q + 1 == ns) b1 = rev ? L - sb : sb;
@@ -1884,13 +1917,13 @@ __device__ __forceinline__ void seg_build_slot(const DevGraph& g, const DevBatch
       if (r < c0 || r >= c1) continue;
       TravRec& t = st[r - c0];
       t.e = e[y]; t.b = b0; t.en = b1;
-      t.slot = (uint32_t)l | (q + 1 == ns ? kTravLast : 0u) | ((rec[y].z & kFlagInternal) ? kTravInternal : 0u);
+      t.slot = (uint32_t)l | (q + 1 == ns ? kTravLast : 0u) | (((sr[y].x >> 30) & 1u) ? kTravInternal : 0u);
       t.tb = t_b;
       t.te = interp_time(ta, tb, x, D);
-      t.sd = sd[y];
-      t.soff = soff[y];
+      t.sd = sr[y].y;
+      t.soff = sr[y].z;
       t.len = L;
-      t.way = way[y];
+      t.way = sr[y].w;
     }
   }
 }
@@ -2163,7 +2196,8 @@ __global__ void __launch_bounds__(64) k_report_lists(uint32_t T, const uint32_t*
 // u64 totals of one or two u32 count arrays: the u32 exclusive scans that lay out routes and
 // records would wrap silently past 2^32, so the host checks these totals instead of off+cnt
 // u64 total of a u32 count array (four per lane, one atomic per block)
-__global__ void __launch_bounds__(256) k_sum_u64(const uint32_t* a, uint64_t n, unsigned long long* out) {
+// block partials of the sum of a[0, n) (four u32 per lane), folded by k_sum_parts
+__global__ void __launch_bounds__(256) k_sum_u64(const uint32_t* a, uint64_t n, unsigned long long* part) {
   const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
   unsigned long long v = 0;
   if (i + 4 <= n) {
@@ -2172,7 +2206,134 @@ __global__ void __launch_bounds__(256) k_sum_u64(const uint32_t* a, uint64_t n, 
   } else {
     for (uint64_t x = i; x < n; ++x) v += a[x];
   }
-  block_sum2_u64(v, 0, out);
+  block_sum2_u64(v, 0, part);
+}
+
+// ------------------------------------------------------------------------------------------
+// Route-ball build on the GPU (balls.hpp; the host build is balls.cpp): one wave per node
+// runs the bounded search from the node (key 0) in an LDS hash, folds the settled nodes
+// into one row per incident road, and (pass 1) sizes the node's table or (pass 2) inserts
+// the rows into it by linear probing.  Keys are the exact ones the host Dijkstra settles, so
+// every lookup agrees with the host tables (row order inside a table may differ).  A node
+// whose ball outgrows the LDS hash is reported (stats[1]) and the caller builds on the host.
+constexpr int kBallSearchH = 256;
+constexpr int kBallRowH = 256;
+struct BallSmem {
+  SearchSmem<kBallSearchH, false> s;
+  uint32_t road[kBallRowH];
+  unsigned long long k0[kBallRowH], k1[kBallRowH];
+  uint32_t used, bad;
+};
+
+__device__ __forceinline__ uint32_t table_bits_dev(uint32_t rows) {
+  uint32_t bits = 1;
+  while ((1ull << bits) < 2ull * rows) ++bits;
+  return bits;
+}
+
+// stats: [0] rows stored [1] nodes whose ball outgrew the LDS hashes [2] nodes without a table
+template <bool FILL>
+__global__ void __launch_bounds__(64) k_ball_build(DevGraph g, int mode, uint32_t radius, uint32_t max_keys,
+                                                   const uint32_t* inc_off, const uint32_t* inc, uint32_t* bits_out,
+                                                   const uint2* hdr, uint4* ent, unsigned long long* stats) {
+  __shared__ BallSmem sm;
+  const int lane = threadIdx.x;
+  unsigned long long n_rows = 0, n_ovf = 0, n_none = 0;   // stats of this block's nodes (lane 0)
+  for (uint32_t u = blockIdx.x; u < g.n_nodes; u += gridDim.x) {
+    if (FILL && hdr[u].y == 0u) continue;
+    bounded_search<kBallSearchH, false>(sm.s, g, mode, radius, nullptr, 0u, u);
+    for (int h = lane; h < kBallRowH; h += kWave) { sm.road[h] = kEmpty; sm.k0[h] = kKeyInf; sm.k1[h] = kKeyInf; }
+    if (lane == 0) { sm.used = 0; sm.bad = sm.s.ovf ? 2u : 0u; }
+    __syncthreads();
+    if (!sm.bad) {
+      for (int h = lane; h < kBallSearchH; h += kWave) {
+        const uint32_t v = sm.s.key[h];
+        if (v == kEmpty) continue;
+        const unsigned long long lab = sm.s.lab[h];
+        if (!ball_key_fits(lab)) { atomicOr(&sm.bad, 1u); continue; }
+        for (uint32_t q = inc_off[v]; q < inc_off[v + 1]; ++q) {
+          const uint32_t r = inc[q];
+          uint32_t x = (r * 2654435761u) & (kBallRowH - 1);
+          int probe = 0;
+          for (; probe < kBallRowH; ++probe, x = (x + 1) & (kBallRowH - 1)) {
+            uint32_t cur = sm.road[x];
+            if (cur == kEmpty) {
+              cur = atomicCAS(&sm.road[x], kEmpty, r);
+              if (cur == kEmpty && atomicAdd(&sm.used, 1u) >= (uint32_t)(kBallRowH * 3 / 4)) atomicOr(&sm.bad, 2u);
+              if (cur == kEmpty) cur = r;
+            }
+            if (cur == r) break;
+          }
+          if (probe == kBallRowH) { atomicOr(&sm.bad, 2u); break; }
+          if (g.road_node0[r] == v) sm.k0[x] = lab;
+          if (g.road_node1[r] == v) sm.k1[x] = lab;
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t bad = sm.bad, rows = sm.used, settled = sm.s.used;
+    if (!FILL) {
+      // as the host build: no table for a ball of more than max_keys nodes, rows of more than
+      // 2 * max_keys roads, or a key beyond the 24-bit row fields
+      uint32_t bits = 0;
+      if (!bad && settled <= max_keys && rows <= 2u * max_keys) bits = table_bits_dev(rows);
+      if (lane == 0) {
+        bits_out[u] = bits;
+        n_ovf += (bad & 2u) ? 1u : 0u;
+        n_none += bits ? 0u : 1u;
+        n_rows += bits ? rows : 0u;
+      }
+    } else {
+      const uint2 hh = hdr[u];
+      const uint32_t mask = (1u << hh.y) - 1u;
+      for (int h = lane; h < kBallRowH; h += kWave) {
+        const uint32_t r = sm.road[h];
+        if (r == kEmpty) continue;
+        uint32_t x = ball_slot(r, hh.y);
+        while (atomicCAS(reinterpret_cast<unsigned int*>(&ent[(uint64_t)hh.x + x]), kNone, r) != kNone) x = (x + 1) & mask;
+        uint32_t y, z, w;
+        ball_pack(sm.k0[h], sm.k1[h], y, z, w);
+        uint4* e = &ent[(uint64_t)hh.x + x];
+        e->y = y; e->z = z; e->w = w;
+      }
+    }
+    __syncthreads();
+  }
+  // one atomic per block and counter (same-address atomics serialise across the XCDs)
+  if (!FILL && lane == 0) {
+    if (n_rows) atomicAdd(&stats[0], n_rows);
+    if (n_ovf) atomicAdd(&stats[1], n_ovf);
+    if (n_none) atomicAdd(&stats[2], n_none);
+  }
+}
+
+__global__ void k_ball_entries(const uint32_t* bits, uint32_t n, unsigned long long* cnt) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < n) cnt[u] = bits[u] ? (1ull << bits[u]) : 0ull;
+}
+
+__global__ void k_ball_hdr(const uint32_t* bits, const unsigned long long* off, uint32_t n, uint2* hdr) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < n) hdr[u] = make_uint2((uint32_t)off[u], bits[u]);
+}
+
+// keys from node `from` to both endpoints of `road` through the mode's tables, as K2 probes
+// them (rm_engine_ball_lookup; all-ones when outside the ball or the node has no table)
+__global__ void k_ball_lookup(DevGraph g, int mode, uint64_t n, const uint32_t* from, const uint32_t* road,
+                              unsigned long long* keys) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint2 h = g.ball_hdr[mode][from[i]];
+  unsigned long long k0 = kKeyInf, k1 = kKeyInf;
+  if (h.y) {
+    const uint4* ent = g.ball_ent[mode];
+    const uint4 e = ball_resolve(ent, h, road[i], ent[h.x + ball_slot(road[i], h.y)]);
+    k0 = row_key0(e);
+    k1 = row_key1(e);
+    if (e.x != road[i]) k0 = k1 = kKeyInf;
+  }
+  keys[2 * i] = k0;
+  keys[2 * i + 1] = k1;
 }
 
 __global__ void k_fill_edge_src(const uint32_t* node_off, uint32_t n_nodes, uint32_t* edge_src) {
@@ -2223,6 +2384,20 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
     dg_.in_edge = upload(allocs_, in_edge);
   }
   dg_.edge_seg = upload(allocs_, g.edge_seg);
+  {
+    // K4 reads one 16-byte record per path edge: {len_cm | reversed << 31 | internal << 30,
+    // OSMLR segment, offset in segment, way id}
+    std::vector<uint32_t> sr(4 * (size_t)g.num_edges());
+    for (uint32_t e = 0; e < g.num_edges(); ++e) {
+      const EdgeRec& r = g.edges[e];
+      if (r.len_cm >= (1u << 30)) throw std::runtime_error("edge longer than 2^30 cm");
+      sr[4 * (size_t)e] = r.len_cm | ((r.road & 1u) << 31) | ((r.info & kFlagInternal) ? 1u << 30 : 0u);
+      sr[4 * (size_t)e + 1] = g.edge_seg[e];
+      sr[4 * (size_t)e + 2] = g.edge_seg_off[e];
+      sr[4 * (size_t)e + 3] = g.edge_way[e];
+    }
+    dg_.seg_rec = (const uint4*)upload(allocs_, sr);
+  }
   dg_.edge_seg_off = upload(allocs_, g.edge_seg_off);
   dg_.edge_way = upload(allocs_, g.edge_way);
   dg_.road_node0 = upload(allocs_, g.road_node0);
@@ -2324,11 +2499,17 @@ void Engine::ensure_balls(uint32_t mode_mask) {
   if (!todo) return;
   RM_HIP(hipSetDevice(device_));
   const int threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  // small balls (country graphs at moderate radii: millions of nodes, tens of nodes per ball)
+  // are built on the GPU; env RM_BALL_BUILD=host|gpu forces one
+  const char* how = std::getenv("RM_BALL_BUILD");
+  const bool try_gpu = how ? std::strcmp(how, "gpu") == 0
+                           : est_ball_nodes(host_, ball_radius_cm_) <= 48.0 && host_.num_nodes() >= 100000;
   for (int mode = 0; mode <= kModePedestrian; ++mode) {
     if (!((todo >> mode) & 1u)) continue;
-    BallTables bt;
     uint32_t max_keys = kBallMaxKeys;   // env RM_BALL_MAX_KEYS: tuning / tests of the no-table path
     if (const char* e = std::getenv("RM_BALL_MAX_KEYS")) max_keys = (uint32_t)std::max(1, std::atoi(e));
+    if (try_gpu && build_balls_gpu(mode, max_keys)) continue;
+    BallTables bt;
     build_balls(host_, mode, ball_radius_cm_, max_keys, threads, bt);
     dg_.ball_hdr[mode] = (const uint2*)upload(allocs_, bt.hdr);
     dg_.ball_ent[mode] = (const uint4*)upload(allocs_, bt.ent);
@@ -2341,6 +2522,80 @@ void Engine::ensure_balls(uint32_t mode_mask) {
     ball_info_[mode][3] = bt.build_ms;
   }
   RM_HIP(hipDeviceSynchronize());
+}
+
+// GPU route-ball build of one mode (k_ball_build); false (nothing changed) when some ball
+// outgrew the kernel's LDS hashes, and the caller builds on the host.  Called under ball_mu_.
+bool Engine::build_balls_gpu(int mode, uint32_t max_keys) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const uint32_t N = host_.num_nodes();
+  std::vector<uint32_t> inc_off, inc;
+  road_incidence(host_, inc_off, inc);
+  std::vector<void*> tmp;
+  struct Free { std::vector<void*>& l; ~Free() { for (void* p : l) (void)hipFree(p); } } fr{tmp};
+  const uint32_t* d_inc_off = upload(tmp, inc_off);
+  const uint32_t* d_inc = upload(tmp, inc);
+  uint32_t* d_bits = dalloc<uint32_t>(tmp, N);
+  unsigned long long* d_cnt = dalloc<unsigned long long>(tmp, N);
+  unsigned long long* d_off = dalloc<unsigned long long>(tmp, N);
+  unsigned long long* d_stats = dalloc<unsigned long long>(tmp, 4);
+  RM_HIP(hipMemset(d_stats, 0, 4 * sizeof(unsigned long long)));
+  DevGraph g = dg_;
+  const uint32_t grid = std::min<uint32_t>(N, 16384);
+  hipLaunchKernelGGL(k_ball_build<false>, dim3(grid), dim3(64), 0, 0, g, mode, ball_radius_cm_, max_keys, d_inc_off,
+                     d_inc, d_bits, (const uint2*)nullptr, (uint4*)nullptr, d_stats);
+  hipLaunchKernelGGL(k_ball_entries, dim3((N + 255) / 256), dim3(256), 0, 0, d_bits, N, d_cnt);
+  size_t tb = 0;
+  RM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, d_cnt, d_off, (int)N, (hipStream_t)0));
+  void* d_tmp = dalloc<char>(tmp, tb);
+  RM_HIP(hipcub::DeviceScan::ExclusiveSum(d_tmp, tb, d_cnt, d_off, (int)N, (hipStream_t)0));
+  unsigned long long st[4], last[2];
+  RM_HIP(hipMemcpy(st, d_stats, sizeof st, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(&last[0], d_off + (N - 1), 8, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(&last[1], d_cnt + (N - 1), 8, hipMemcpyDeviceToHost));
+  if (st[1]) return false;   // a ball outgrew the LDS hashes: the host build takes the mode
+  const uint64_t total = last[0] + last[1];
+  if (total >= 0xffffffffull) throw std::runtime_error("route balls too large (entries >= 2^32); lower the radius");
+  uint2* d_hdr = dalloc<uint2>(allocs_, N);
+  uint4* d_ent = dalloc<uint4>(allocs_, total);
+  hipLaunchKernelGGL(k_ball_hdr, dim3((N + 255) / 256), dim3(256), 0, 0, d_bits, d_off, N, d_hdr);
+  RM_HIP(hipMemset(d_ent, 0xff, total * sizeof(uint4)));
+  hipLaunchKernelGGL(k_ball_build<true>, dim3(grid), dim3(64), 0, 0, g, mode, ball_radius_cm_, max_keys, d_inc_off,
+                     d_inc, d_bits, (const uint2*)d_hdr, d_ent, d_stats);
+  RM_HIP(hipGetLastError());
+  RM_HIP(hipDeviceSynchronize());
+  dg_.ball_hdr[mode] = d_hdr;
+  dg_.ball_ent[mode] = d_ent;
+  dg_.ball_radius[mode] = ball_radius_cm_;
+  dg_.ball_mask |= 1u << mode;
+  ball_built_ |= 1u << mode;
+  ball_info_[mode][0] = (double)st[0];
+  ball_info_[mode][1] = (double)total;
+  ball_info_[mode][2] = (double)st[2];
+  ball_info_[mode][3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ball_gpu_ |= 1u << mode;
+  return true;
+}
+
+void Engine::ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys) {
+  std::lock_guard<std::mutex> lk(ball_mu_);
+  RM_HIP(hipSetDevice(device_));
+  for (uint64_t i = 0; i < n; ++i) {
+    keys[2 * i] = keys[2 * i + 1] = kKeyInf;
+    if (from[i] >= host_.num_nodes() || road[i] >= host_.num_roads()) throw std::runtime_error("node or road out of range");
+  }
+  if (!((ball_built_ >> mode) & 1u) || n == 0) return;
+  std::vector<void*> tmp;
+  struct Free { std::vector<void*>& l; ~Free() { for (void* p : l) (void)hipFree(p); } } fr{tmp};
+  uint32_t* d_from = dalloc<uint32_t>(tmp, n);
+  uint32_t* d_road = dalloc<uint32_t>(tmp, n);
+  unsigned long long* d_keys = dalloc<unsigned long long>(tmp, 2 * n);
+  RM_HIP(hipMemcpy(d_from, from, n * 4, hipMemcpyHostToDevice));
+  RM_HIP(hipMemcpy(d_road, road, n * 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_ball_lookup, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, dg_, mode, n, d_from, d_road,
+                     d_keys);
+  RM_HIP(hipGetLastError());
+  RM_HIP(hipMemcpy(keys, d_keys, 2 * n * 8, hipMemcpyDeviceToHost));
 }
 
 // ==========================================================================================
@@ -2389,6 +2644,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.src_cnt = dalloc<uint32_t>(L, cp); w.src_off = dalloc<uint32_t>(L, cp);
   w.choice = dalloc<int8_t>(L, cp); w.chain_start = dalloc<uint8_t>(L, cp); w.bp = dalloc<uint8_t>(L, cp * kMaxCand);
   w.path_off = dalloc<uint32_t>(L, cp); w.path_cnt = dalloc<uint32_t>(L, cp); w.route_dist = dalloc<uint32_t>(L, cp);
+  w.path_sab = dalloc<uint2>(L, cp);
   w.path_inline = dalloc<uint32_t>(L, cp * kInlinePath);
   w.trav_off = dalloc<uint32_t>(L, cp);
   w.seg_base = dalloc<uint32_t>(L, ct); w.seg_cnt = dalloc<uint32_t>(L, ct);
@@ -2399,6 +2655,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.rl_paths_c = dalloc<uint32_t>(L, cp);
   w.trace_err = dalloc<uint32_t>(L, ct);
   w.tot64 = dalloc<unsigned long long>(L, 4);
+  w.tot_part = dalloc<unsigned long long>(L, 2 * ((cp + 255) / 256) + 2);
   size_t tmp = 0;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, w.trans_cnt, w.trans_off, (int)cp, stream_));
   w.scan_tmp_bytes = tmp;
@@ -2512,7 +2769,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
   v.path_pool = w.path_pool; v.path_cap = w.cap_path;
-  v.route_dist = w.route_dist;
+  v.route_dist = w.route_dist; v.path_sab = w.path_sab;
   v.segs = w.segs; v.seg_base = w.seg_base; v.seg_cnt = w.seg_cnt;
   v.trav_off = w.trav_off;
   v.reps = w.reps; v.rep_cnt = w.rep_cnt; v.stats = w.stats;
@@ -2594,8 +2851,8 @@ void Matcher::run_device(const RunParams& rp) {
   RM_HIP(hipMemsetAsync(w.choice, 0xff, P, st));
   RM_HIP(hipMemsetAsync(w.path_cnt, 0, P * sizeof(uint32_t), st));
   RM_HIP(hipMemsetAsync(w.trace_err, 0, T * sizeof(uint32_t), st));
-  RM_HIP(hipMemsetAsync(w.tot64, 0, 4 * sizeof(unsigned long long), st));
   DevBatch v = make_view(w, T, P);
+  const uint32_t count_grid = (uint32_t)((P + 255) / 256);
   const uint32_t sum_grid = (uint32_t)((P + 1023) / 1024);   // k_sum_u64: four counts per lane
 
   tic(kKStates);
@@ -2606,7 +2863,8 @@ void Matcher::run_device(const RunParams& rp) {
   hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, g, v);
   toc(kKCandidates);
   tic(kKScan);
-  hipLaunchKernelGGL(k_trans_count, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v, w.tot64);
+  hipLaunchKernelGGL(k_trans_count, dim3(count_grid), dim3(256), 0, st, v, w.tot_part);
+  hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(1024), 0, st, (const unsigned long long*)w.tot_part, count_grid, w.tot64);
   size_t tmp = w.scan_tmp_bytes;
   RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.trans_cnt, w.trans_off, (int)P, st));
   tmp = w.scan_tmp_bytes;
@@ -2679,8 +2937,8 @@ void Matcher::run_device(const RunParams& rp) {
     tic(kKSegments);
     tmp = w.scan_tmp_bytes;
     RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
-    RM_HIP(hipMemsetAsync(w.tot64 + 2, 0, sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot64 + 2);
+    hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot_part);
+    hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(1024), 0, st, (const unsigned long long*)w.tot_part, sum_grid, w.tot64 + 2);
     toc(kKSegments);
     RM_HIP(hipMemcpyAsync(htot + 2, w.tot64 + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     read_ctl();
@@ -2703,8 +2961,8 @@ void Matcher::run_device(const RunParams& rp) {
       hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
       tmp = w.scan_tmp_bytes;
       RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
-      RM_HIP(hipMemsetAsync(w.tot64 + 2, 0, sizeof(unsigned long long), st));
-      hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot64 + 2);
+      hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot_part);
+      hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(1024), 0, st, (const unsigned long long*)w.tot_part, sum_grid, w.tot64 + 2);
       RM_HIP(hipMemcpyAsync(htot + 2, w.tot64 + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
       read_ctl();
     }

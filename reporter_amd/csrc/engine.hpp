@@ -51,6 +51,7 @@ struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   const uint4* relax[5];         // per travel mode, per directed edge: {target, len_cm | 0xffffffff if the mode
                                  // cannot use it, time_ms at the mode's speed, CSR range of the target}
   const uint32_t* node_rng;      // per node: first out-edge << 5 | out-degree
+  const uint4* seg_rec;          // per directed edge, for K4: {len_cm | reversed << 31 | internal << 30, segment, offset, way}
   // route balls per travel mode (balls.hpp): per node {first entry, log2 table size or 0},
   // entries {node | kNone, dist cm, time ms, 0}; radius 0 = not built (K2 searches instead)
   const uint2* ball_hdr[5];
@@ -108,6 +109,7 @@ struct Workspace {
   uint32_t* src_cnt = nullptr; uint32_t* src_off = nullptr; uint32_t* src_item = nullptr;
   int8_t* choice = nullptr; uint8_t* chain_start = nullptr; uint8_t* bp = nullptr;
   uint32_t* path_off = nullptr; uint32_t* path_cnt = nullptr; uint32_t* path_pool = nullptr; uint32_t* route_dist = nullptr;
+  uint2* path_sab = nullptr;        // per chosen transition: source / target candidate offsets on their roads (cm)
   uint32_t* path_inline = nullptr;  // kInlinePath edges per slot
   // per trace outputs
   SegmentRec* segs = nullptr; uint32_t* seg_base = nullptr; uint32_t* seg_cnt = nullptr;
@@ -124,6 +126,7 @@ struct Workspace {
   uint32_t* rl_routes_c = nullptr; uint32_t* rl_paths_c = nullptr; void* gsearch = nullptr;
   uint32_t* trace_err = nullptr;            // per trace: error bits (kErr*) of that trace alone
   unsigned long long* tot64 = nullptr;      // u64 totals: [0] transitions [1] sources [2] path edges
+  unsigned long long* tot_part = nullptr;   // per-block partial pairs of those totals (k_sum_parts folds them)
   void* scan_tmp = nullptr; size_t scan_tmp_bytes = 0;
   std::vector<void*> allocs;
   ~Workspace();
@@ -316,6 +319,11 @@ class Engine {
   uint32_t ball_radius() const { return ball_radius_cm_; }
   // stats of one mode's tables: {keys, table entries, nodes without a table, build ms}
   void ball_stats(int mode, double* out4) const;
+  // modes whose tables were built on the GPU (bit per Mode)
+  uint32_t ball_gpu_mask() const { return ball_gpu_; }
+  // keys[2i], keys[2i+1] from node from[i] to road[i]'s node0 / node1 through the built tables
+  // of `mode`, probed on the device as K2 does (all-ones: outside the ball / no table)
+  void ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys);
 
  private:
   int device_;
@@ -325,6 +333,8 @@ class Engine {
   mutable std::mutex ball_mu_;
   uint32_t ball_radius_cm_ = 40000;   // set from auto_ball_radius_cm(graph) at construction
   uint32_t ball_built_ = 0;             // mode bits
+  uint32_t ball_gpu_ = 0;               // mode bits built on the GPU
+  bool build_balls_gpu(int mode, uint32_t max_keys);
   double ball_info_[5][4] = {};
 };
 

@@ -82,9 +82,21 @@ class Engine:
         _lib.check(_lib.lib().rm_engine_set_ball_radius(self._h, float(meters)))
 
     def ball_stats(self, mode=0):
-        out = np.zeros(5, np.float64)
+        out = np.zeros(6, np.float64)
         _lib.check(_lib.lib().rm_engine_ball_stats(self._h, int(mode), out.ctypes.data))
-        return dict(zip(("radius_m", "keys", "entries", "nodes_without_table", "build_ms"), out.tolist()))
+        d = dict(zip(("radius_m", "keys", "entries", "nodes_without_table", "build_ms"), out[:5].tolist()))
+        d["built_on_gpu"] = bool(out[5])
+        return d
+
+    def ball_lookup(self, mode, from_nodes, roads):
+        """Keys (n, 2) from each node to the two endpoints of each road through the engine's
+        device tables of `mode` (all-ones outside the ball / without a table)."""
+        f = _c(from_nodes, np.uint32)
+        r = _c(roads, np.uint32)
+        keys = np.empty((len(f), 2), np.uint64)
+        _lib.check(_lib.lib().rm_engine_ball_lookup(self._h, int(mode), len(f), f.ctypes.data, r.ctypes.data,
+                                                    keys.ctypes.data))
+        return keys
 
     def close(self):
         if getattr(self, "_h", None):

@@ -26,7 +26,7 @@ CONFIGS = {
     "C3": dict(rows=500, cols=500, block_m=200.0, n_traces=1000000, n_points=40, rate_s=30.0, noise_m=5.0,
                search_radius=100.0, cell_m=200.0, ball_radius_m=None),
     "C4": dict(rows=4000, cols=4000, block_m=250.0, n_traces=1000000, n_points=120, rate_s=5.0, noise_m=5.0,
-               search_radius=50.0, cell_m=250.0, ball_radius_m=700.0),
+               search_radius=50.0, cell_m=250.0, ball_radius_m=None),
     "C5": dict(rows=200, cols=200, block_m=100.0, n_traces=10000, n_points=600, rate_s=1.0, noise_m=5.0,
                search_radius=50.0, cell_m=100.0, ball_radius_m=None),
 }

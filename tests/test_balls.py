@@ -91,9 +91,10 @@ def test_ball_radius_zero_keeps_only_self(small_world):
     assert list(got[0]) == [0, KEY_INF] and list(got[1]) == [KEY_INF, 0]
 
 
-def test_auto_radius_covers_default_breakage(small_world, tmpdir_session):
+def test_auto_radius_covers_default_breakage(small_world, tmpdir_session, monkeypatch):
     """A city graph gets 2000 m balls (meili's default breakage distance: every default
-    bound is a probe); a graph too large for 16 GiB tables per mode gets a smaller radius."""
+    bound is a probe); a graph too large for the table budget per mode (72 GiB, or
+    RM_BALL_BUDGET_GB) gets a smaller radius."""
     import ctypes
     r = ctypes.c_double()
     _lib.check(_lib.lib().rm_graph_auto_ball_radius(os.fsencode(small_world), ctypes.byref(r)))
@@ -101,6 +102,9 @@ def test_auto_radius_covers_default_breakage(small_world, tmpdir_session):
     from reporter_amd import world
     big = str(tmpdir_session / "auto_r_big.rmg")
     world.build_world(big, 1400, 1400, 250.0, seed=2, cell_m=250.0)   # 2 M nodes
+    _lib.check(_lib.lib().rm_graph_auto_ball_radius(os.fsencode(big), ctypes.byref(r)))
+    assert r.value == 2000.0
+    monkeypatch.setenv("RM_BALL_BUDGET_GB", "16")
     _lib.check(_lib.lib().rm_graph_auto_ball_radius(os.fsencode(big), ctypes.byref(r)))
     assert 400.0 <= r.value < 2000.0
     assert _lib.lib().rm_graph_auto_ball_radius(b"/nonexistent.rmg", ctypes.byref(r)) != 0
