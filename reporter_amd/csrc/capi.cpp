@@ -92,8 +92,8 @@ void apply_options(const json::Value* o, MatchOptions& m) {
   num("max_route_distance_factor", m.max_route_distance_factor);
   num("max_route_time_factor", m.max_route_time_factor);
   num("turn_penalty_factor", m.turn_penalty_factor);
-  if (!(m.sigma_z > 0.f)) throw std::runtime_error("sigma_z must be positive");
-  if (!(m.beta > 0.f)) throw std::runtime_error("beta must be positive");
+  if (!(m.sigma_z > 0.f) || !std::isfinite(m.sigma_z)) throw std::runtime_error("sigma_z must be positive");
+  if (!(m.beta > 0.f) || !std::isfinite(m.beta)) throw std::runtime_error("beta must be positive");
   if (!(m.search_radius >= 0.f)) throw std::runtime_error("search_radius must be non-negative");
 }
 

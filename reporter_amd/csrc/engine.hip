@@ -1378,30 +1378,84 @@ __global__ void __launch_bounds__(64) k_routes_global(DevGraph g, DevBatch b, Gl
 // K3 k_viterbi: 16 lanes per trace, 4 traces per wave; lane j owns candidate j of the
 // current layer.  A wave64 VALU instruction costs a SIMD four cycles, so the layer
 // recurrence is packed four traces to an instruction (one trace per wave would spend
-// ~4x the issue slots on the same work).  Each group streams its trace through LDS in
+// ~4x the issue slots on the same work), and the recurrence is issue-bound, so the layer
+// body is cut to the fewest instructions: a group is a DPP row, the previous layer's costs
+// stay in registers (lane i holds cost i) and reach every lane of the row by row_newbcast
+// moves (no LDS round trip, no barrier), and routes are staged as fp64 metres (+inf when
+// invalid) so a source costs three fp64 operations and a compare.  Each group streams its trace through LDS in
 // chunks of <= 16 layers / <= kVitRoutes routes: one lane describes one layer, a 16-lane
 // scan lays the chunk out, and routes / emission rows arrive with coalesced loads while
 // the next chunk's descriptor is already in flight.  No global store is issued inside a
 // chunk (gfx9 loads and stores share vmcnt): back-pointer rows and chain flags are
 // buffered in LDS and flushed once per chunk.
 constexpr int kVitChunk = 16;     // layers per staged chunk (one per lane of the group)
+#ifndef RM_VIT_WPE
+#define RM_VIT_WPE 3   // 2,500 C2 waves over 1,024 SIMDs must be resident at once (also LDS: VitGroup)
+#endif
 #ifndef RM_VIT_ROUTES
 #define RM_VIT_ROUTES 256
 #endif
 constexpr int kVitRoutes = RM_VIT_ROUTES;  // routes per staged chunk and group
 constexpr int kVitBt = 64;        // layers per backtrace staging block
 struct VitGroup {
-  uint32_t route[kVitRoutes];
+  // LDS per wave bounds K3's residency (C2: 2,500 waves over 256 CUs need <= 14.5 KB per
+  // wave for one round), so the backtrace staging aliases the chunk's routes; a backtrace
+  // inside a chunk re-stages them from HBM afterwards (chain breaks are rare)
+  union {
+    double route_m[kVitRoutes];   // route length in metres ((double)cm * 0.01), +inf when invalid
+    uint4 bst[kVitBt];            // backtrace staging
+  };
   float sq[kVitChunk][16];
   double gc[kVitChunk];
-  double cost[16];                // costs of the previous layer
   uint32_t kb[kVitChunk], rel[kVitChunk];
   uint4 bpo[kVitChunk];           // this chunk's back-pointer rows (16 x u8)
-  uint4 bst[kVitBt];              // backtrace staging
   uint8_t cs[kVitChunk];          // this chunk's chain-start flags
   uint8_t ch[kVitBt];             // choices of one backtrace block
   uint32_t nch, done, w, pad;
 };
+
+// lane I of this lane's 16-lane row (DPP row_newbcast; rows are the K3 groups)
+template <int I>
+__device__ __forceinline__ double row_bcast(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0x150 + I, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0x150 + I, 0xf, 0xf, false);
+  return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// best / arg over sources I.. prevK-1 of this lane's target: cost of source i (lane i's
+// cj) + |route_m - gc| / beta, the first strict minimum in source order.  Bit-identical to
+// cj + trans_cost(route_cm): route_m is the same (double)cm * 0.01 and +inf stays +inf.
+// Sources go in blocks of four under a group-uniform guard (every lane of the row is active
+// inside it): the block's four LDS loads issue together and complete under one wait, then
+// each source costs three fp64 operations, a compare and a branch-free select (sources past
+// prevK in the last block are computed and discarded).
+template <int I>
+__device__ __forceinline__ void vit_src(double& best, int& arg, double cj, double rm, uint32_t prevK, double gcl,
+                                        double inv_beta) {
+  const double c = row_bcast<I>(cj) + fabs(rm - gcl) * inv_beta;
+  const bool take = ((uint32_t)I < prevK) & (c < best);
+  best = take ? c : best;
+  arg = take ? I : arg;
+}
+template <int B>
+__device__ __forceinline__ void vit_min(double& best, int& arg, double cj, const double* dp, uint32_t KB,
+                                        uint32_t prevK, double gcl, double inv_beta) {
+  if constexpr (B < 4) {
+    if ((uint32_t)(4 * B) < prevK) {
+      double rm[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rm[x] = dp[(4 * B + x) * KB];   // past prevK: never selected
+#pragma unroll
+      for (int x = 0; x < 4; ++x) __asm__ volatile("" : "+v"(rm[x]));   // keep the loads together
+      vit_src<4 * B + 0>(best, arg, cj, rm[0], prevK, gcl, inv_beta);
+      vit_src<4 * B + 1>(best, arg, cj, rm[1], prevK, gcl, inv_beta);
+      vit_src<4 * B + 2>(best, arg, cj, rm[2], prevK, gcl, inv_beta);
+      vit_src<4 * B + 3>(best, arg, cj, rm[3], prevK, gcl, inv_beta);
+      vit_min<B + 1>(best, arg, cj, dp, KB, prevK, gcl, inv_beta);
+    }
+  }
+}
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1423,12 +1477,12 @@ __device__ __forceinline__ void vit_flush(const DevBatch& b, const VitGroup& gs,
   }
 }
 
-// Backtrace of the chain ending at layer `end` (costs of that layer in gs.cost, K
+// Backtrace of the chain ending at layer `end` (lane j holds cost j of that layer, K
 // candidates).  Winner = lowest cost, ties to the lowest j.  Rows are staged 64 layers
 // per block (four coalesced loads per lane); lane 0 of the group walks them in LDS and
 // the block's choices leave as one store per lane.
-__device__ void backtrace_chain(const DevBatch& b, VitGroup& gs, uint32_t o, uint32_t end, uint32_t K, int j) {
-  double bc = (j < (int)K) ? gs.cost[j] : __longlong_as_double(0x7ff0000000000000ll);
+__device__ void backtrace_chain(const DevBatch& b, VitGroup& gs, uint32_t o, uint32_t end, uint32_t K, int j, double cj) {
+  double bc = (j < (int)K) ? cj : __longlong_as_double(0x7ff0000000000000ll);
   int bj = (j < (int)K) ? j : 1 << 20;
   for (int m = 1; m < 16; m <<= 1) {
     const double oc = shfl_xor_d(bc, m, 16);
@@ -1495,7 +1549,7 @@ __device__ __forceinline__ VitLayerDesc vit_describe(const DevBatch& b, uint32_t
   return d;
 }
 
-__global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_WPE))) k_viterbi(DevBatch b) {
   __shared__ VitGroup smem[4];
   const int lane = threadIdx.x;
   const int j = lane & 15, gb = lane & 48;
@@ -1510,6 +1564,7 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   bool prev_ok = false;
   uint32_t prevK = 0;
+  double cj = INF;   // cost of candidate j of the previous layer
   // chunk descriptor: lane j describes layer s0 + j (clamped, branch-free loads)
   VitLayerDesc dq{0u, 0u, 0u, 0.0};
   if (S) dq = vit_describe(b, o, S, 0, j);
@@ -1548,7 +1603,7 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
     // ---- chunk -> LDS
 #pragma unroll
     for (int x = 0; x < kVitRoutes / 16; ++x)
-      if ((uint32_t)j + 16u * x < nroutes) gs.route[j + 16 * x] = rv[x];
+      if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
     {
       float4* sqdst = reinterpret_cast<float4*>(&gs.sq[0][0]);
       const uint32_t nf = C * (kMaxCand / 4);
@@ -1573,31 +1628,24 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
       int arg = -1;
       if (KB && !start) {
         const uint32_t jj = min((uint32_t)j, KB - 1u);
-        // row i of the layer's K_A x K_B routes starts at rel + i * KB; sources past prevK
-        // read slots that are never selected (i0 + x < prevK), so no index is clamped
-        const uint32_t* rp = gs.route + rel + jj;
-        for (uint32_t i0 = 0; i0 < prevK; i0 += 4) {
-          double ci[4];
-          uint32_t rr[4];
-#pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            ci[x] = gs.cost[i0 + x];
-            rr[x] = rp[x * KB];
-          }
-          rp += 4 * KB;
-          // an invalid route or an unreachable source gives +inf, which never wins
-#pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            const double c = ci[x] + trans_cost(rr[x], gcl, inv_beta);
-            if (i0 + x < prevK && c < best) { best = c; arg = (int)(i0 + x); }
-          }
-        }
+        // row i of the layer's K_A x K_B routes starts at rel + i * KB; an invalid route
+        // or an unreachable source gives +inf, which never wins
+        vit_min<0>(best, arg, cj, gs.route_m + rel + jj, KB, prevK, gcl, inv_beta);
         if (j >= (int)KB) { best = INF; arg = -1; }
         if (((__ballot(j < (int)KB && arg >= 0) >> gb) & 0xffffull) == 0ull) start = true;
       }
       if (s > 0 && prev_ok && (KB == 0 || start)) {
+        wave_sync();                      // the group's row stores precede the flush
         vit_flush(b, gs, o + s0, t, j);   // rows [s0, s) are needed by the backtrace
-        backtrace_chain(b, gs, o, s - 1, prevK, j);
+        backtrace_chain(b, gs, o, s - 1, prevK, j, cj);
+        // the backtrace staged through route_m: bring the chunk's routes back
+#pragma unroll
+        for (int x = 0; x < kVitRoutes / 16; ++x)
+          if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
+#pragma unroll
+        for (int x = 0; x < kVitRoutes / 16; ++x)
+          if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
+        wave_sync();
       }
       uint8_t* row = reinterpret_cast<uint8_t*>(&gs.bpo[t]);
       if (KB == 0) {
@@ -1605,7 +1653,7 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
         if (j == 0) gs.cs[t] = 1;
         prev_ok = false;
         prevK = 0;
-        wave_sync();
+        cj = INF;
         continue;
       }
       const double em = (j < (int)KB) ? (double)gs.sq[t][j] * inv2s2 : INF;
@@ -1613,11 +1661,9 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
       uint32_t bpj;
       if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255u; }
       else { nc = (j < (int)KB && arg >= 0) ? best + em : INF; bpj = arg >= 0 ? (uint32_t)arg : 255u; }
-      wave_sync();   // every lane's reads of gs.cost precede the overwrite
-      gs.cost[j] = nc;
+      cj = nc;
       row[j] = (uint8_t)bpj;
       if (j == 0) gs.cs[t] = start ? 1 : 0;
-      wave_sync();
       prev_ok = true;
       prevK = KB;
     }
@@ -1626,7 +1672,7 @@ __global__ void __launch_bounds__(64) k_viterbi(DevBatch b) {
     wave_sync();
     s0 += C;
   }
-  if (prev_ok) backtrace_chain(b, gs, o, S - 1, prevK, j);
+  if (prev_ok) backtrace_chain(b, gs, o, S - 1, prevK, j, cj);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2792,6 +2838,9 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
   mode_mask_ = 0;
   for (uint32_t q = 0; q < hb.n_opts; ++q) {
     if (hb.opts[q].mode < 0 || hb.opts[q].mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    // K3 divides by both (a zero 1/beta would turn an invalid route's +inf into NaN)
+    if (!(hb.opts[q].sigma_z > 0.f) || !std::isfinite(hb.opts[q].sigma_z)) throw std::runtime_error("sigma_z must be positive and finite");
+    if (!(hb.opts[q].beta > 0.f) || !std::isfinite(hb.opts[q].beta)) throw std::runtime_error("beta must be positive and finite");
     mode_mask_ |= 1u << hb.opts[q].mode;
   }
   ensure(P, T, hb.n_opts);

@@ -1,6 +1,7 @@
 """Build an experiment variant of libreporter_match.so with extra -D flags (diagnostic).
 
     python scripts/build_variant.py NAME -DRM_LANE_CAP=24 ...
+    python scripts/build_variant.py NAME --src path/to/engine_variant.hip [-D...]
 
 Output: variants/NAME.so (git-ignored, travels to the GPU box).  Load it with
 REPORTER_MATCH_LIB=variants/NAME.so (reporter_amd/_lib.py).
@@ -14,11 +15,16 @@ sys.path.insert(0, ROOT)
 from reporter_amd import build  # noqa: E402
 
 name, defs = sys.argv[1], sys.argv[2:]
+src = os.path.join(build.CSRC, "engine.hip")
+if "--src" in defs:
+    k = defs.index("--src")
+    src = os.path.abspath(defs[k + 1])
+    defs = defs[:k] + defs[k + 2:]
 out_dir = os.path.join(ROOT, "variants")
 os.makedirs(out_dir, exist_ok=True)
 build.build()  # the other objects are shared with the product build
 obj = os.path.join(out_dir, name + "_engine.o")
-cmd = [build._hipcc()] + build._flags() + defs + ["-c", os.path.join(build.CSRC, "engine.hip"), "-o", obj]
+cmd = [build._hipcc()] + build._flags() + defs + ["-I" + build.CSRC, "-c", src, "-o", obj]
 subprocess.run(cmd, check=True)
 objs = [obj] + [os.path.join(build.OBJ, s + ".o") for s in build.SOURCES if s != "engine.hip"]
 lib = os.path.join(out_dir, name + ".so")
