@@ -1417,10 +1417,7 @@ struct VitGroup {
 // lane I of this lane's 16-lane row (DPP row_newbcast; rows are the K3 groups)
 template <int I>
 __device__ __forceinline__ double row_bcast(double v) {
-  const unsigned long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0x150 + I, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0x150 + I, 0xf, 0xf, false);
-  return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + I, 0xf, 0xf, false);   // one v_mov_b64_dpp
 }
 
 // best / arg over sources I.. prevK-1 of this lane's target: cost of source i (lane i's
@@ -1428,31 +1425,36 @@ __device__ __forceinline__ double row_bcast(double v) {
 // cj + trans_cost(route_cm): route_m is the same (double)cm * 0.01 and +inf stays +inf.
 // Sources go in blocks of four under a group-uniform guard (every lane of the row is active
 // inside it): the block's four LDS loads issue together and complete under one wait, then
-// each source costs three fp64 operations, a compare and a branch-free select (sources past
-// prevK in the last block are computed and discarded).
+// each source costs three fp64 operations, a compare and a branch-free select.  Sources past
+// prevK in the last block need no guard: lanes i >= prevK hold cj = +inf (every layer sets
+// cost +inf past its KB), and +inf (or NaN from the unstaged LDS they read) never wins.
 template <int I>
-__device__ __forceinline__ void vit_src(double& best, int& arg, double cj, double rm, uint32_t prevK, double gcl,
-                                        double inv_beta) {
+__device__ __forceinline__ void vit_src(double& best, int& arg, double cj, double rm, double gcl, double inv_beta) {
   const double c = row_bcast<I>(cj) + fabs(rm - gcl) * inv_beta;
-  const bool take = ((uint32_t)I < prevK) & (c < best);
+  const bool take = c < best;
   best = take ? c : best;
   arg = take ? I : arg;
 }
 template <int B>
 __device__ __forceinline__ void vit_min(double& best, int& arg, double cj, const double* dp, uint32_t KB,
-                                        uint32_t prevK, double gcl, double inv_beta) {
+                                        uint32_t prevK, double gcl, double inv_beta, const double (&rm0)[4]) {
   if constexpr (B < 4) {
     if ((uint32_t)(4 * B) < prevK) {
       double rm[4];
+      if constexpr (B == 0) {   // block 0 was loaded at the end of the previous layer
 #pragma unroll
-      for (int x = 0; x < 4; ++x) rm[x] = dp[(4 * B + x) * KB];   // past prevK: never selected
+        for (int x = 0; x < 4; ++x) rm[x] = rm0[x];
+      } else {
 #pragma unroll
-      for (int x = 0; x < 4; ++x) __asm__ volatile("" : "+v"(rm[x]));   // keep the loads together
-      vit_src<4 * B + 0>(best, arg, cj, rm[0], prevK, gcl, inv_beta);
-      vit_src<4 * B + 1>(best, arg, cj, rm[1], prevK, gcl, inv_beta);
-      vit_src<4 * B + 2>(best, arg, cj, rm[2], prevK, gcl, inv_beta);
-      vit_src<4 * B + 3>(best, arg, cj, rm[3], prevK, gcl, inv_beta);
-      vit_min<B + 1>(best, arg, cj, dp, KB, prevK, gcl, inv_beta);
+        for (int x = 0; x < 4; ++x) rm[x] = dp[(4 * B + x) * KB];   // past prevK: never selected
+#pragma unroll
+        for (int x = 0; x < 4; ++x) __asm__ volatile("" : "+v"(rm[x]));   // keep the loads together
+      }
+      vit_src<4 * B + 0>(best, arg, cj, rm[0], gcl, inv_beta);
+      vit_src<4 * B + 1>(best, arg, cj, rm[1], gcl, inv_beta);
+      vit_src<4 * B + 2>(best, arg, cj, rm[2], gcl, inv_beta);
+      vit_src<4 * B + 3>(best, arg, cj, rm[3], gcl, inv_beta);
+      vit_min<B + 1>(best, arg, cj, dp, KB, prevK, gcl, inv_beta, rm0);
     }
   }
 }
@@ -1616,13 +1618,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     wave_sync();
     uint32_t maxC = max(C, (uint32_t)__shfl_xor((int)C, 16));
     maxC = max(maxC, (uint32_t)__shfl_xor((int)maxC, 32));
+    // layer parameters and the first four route rows run one layer ahead of their use
+    uint32_t KBn = gs.kb[0], reln = gs.rel[0];
+    double gcn = gs.gc[0];
+    float sqn = gs.sq[0][j];
+    double rmn[4];
+    {
+      const double* dp = gs.route_m + reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
+    }
     // ---- the layers of the chunk, in order, out of LDS (groups with fewer layers idle)
     for (uint32_t t = 0; t < maxC; ++t) {
       if (t >= C) continue;
       const uint32_t s = s0 + t;
-      const uint32_t KB = gs.kb[t];
-      const double gcl = gs.gc[t];
-      const uint32_t rel = gs.rel[t];
+      const uint32_t KB = KBn, rel = reln;
+      const double gcl = gcn;
+      const float sqv = sqn;
+      double rm0[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rm0[x] = rmn[x];
+      if (t + 1 < C) { KBn = gs.kb[t + 1]; reln = gs.rel[t + 1]; gcn = gs.gc[t + 1]; sqn = gs.sq[t + 1][j]; }
       bool start = !prev_ok || (s > 0 && gcl > brk);
       double best = INF;
       int arg = -1;
@@ -1630,7 +1646,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         const uint32_t jj = min((uint32_t)j, KB - 1u);
         // row i of the layer's K_A x K_B routes starts at rel + i * KB; an invalid route
         // or an unreachable source gives +inf, which never wins
-        vit_min<0>(best, arg, cj, gs.route_m + rel + jj, KB, prevK, gcl, inv_beta);
+        vit_min<0>(best, arg, cj, gs.route_m + rel + jj, KB, prevK, gcl, inv_beta, rm0);
         if (j >= (int)KB) { best = INF; arg = -1; }
         if (((__ballot(j < (int)KB && arg >= 0) >> gb) & 0xffffull) == 0ull) start = true;
       }
@@ -1647,6 +1663,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
           if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
         wave_sync();
       }
+      if (t + 1 < C) {   // next layer's first route rows (after any re-staging above)
+        const double* dp = gs.route_m + reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
+      }
       uint8_t* row = reinterpret_cast<uint8_t*>(&gs.bpo[t]);
       if (KB == 0) {
         row[j] = 255;
@@ -1656,7 +1677,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         cj = INF;
         continue;
       }
-      const double em = (j < (int)KB) ? (double)gs.sq[t][j] * inv2s2 : INF;
+      const double em = (j < (int)KB) ? (double)sqv * inv2s2 : INF;
       double nc;
       uint32_t bpj;
       if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255u; }
