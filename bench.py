@@ -343,9 +343,9 @@ def main():
             "K2": {k: k2[k] for k in ("kernel", "achieved", "frac", "algorithmic_bytes_per_launch", "avg_launch_ms")},
             "K3": roofline("K3", "k_viterbi", mo.viterbi_algorithmic_bytes(counts) if counts else None, ms["viterbi"],
                            "u32 routes + f32 emissions, fp64 costs in registers"),
-            "K4": roofline("K4", "segments stage: trav_off scan + k_traversals + run flags + k_runs",
+            "K4": roofline("K4", "segments stage: trav_off scan + k_rec_slot + k_seg_wave",
                            mo.segments_algorithmic_bytes(counts) if counts else None, ms["segments"],
-                           "path edges -> traversal records -> OSMLR runs"),
+                           "wave per trace, 64 traversal records per step in registers, runs by ballot/scan"),
         }
         step_ms = elapsed / steps * 1e3
         build_ms = balls["build_ms"]

@@ -1810,20 +1810,10 @@ __global__ void __launch_bounds__(64) k_paths_global(DevGraph g, DevBatch b, Glo
 }
 
 // ------------------------------------------------------------------------------------------
-// K4 (segments): traversal records -> OSMLR runs -> segments, fused in one kernel whose
-// traversal records never leave LDS.
-//   k_seg_blocks  block -> trace range: block b takes the traces whose first record lies in
-//                 [b * kSegSpan, (b+1) * kSegSpan) (records never cross traces, so neither do runs)
-//   k_segments    per block, the block's record range in chunks of kSegChunk records:
-//                 build    one lane per transition slot expands its path into traversal
-//                          records (edge, [b,en] cm, interpolated times, OSMLR tags) in LDS
-//                 flags    one lane per record: skip / new traversal / merged piece and the
-//                          run-head flag (meili form_segments' merge + run rules compare a
-//                          record with the previous kept record of its chain only)
-//                 runs     one lane per run head walks its run in LDS and writes the segment;
-//                          the run still open at a chunk's end carries its state into the next
-// Segments of trace k are compacted at seg_base[k] = its block's first record + the runs of
-// the block before it (a per-block layout: no global scan of runs, gaps between blocks).
+// K4 (segments): traversal records -> OSMLR runs -> segments (meili form_segments + the
+// reporter's segment fields).  Shared pieces: the run state a segment is written from, the
+// time interpolation along a transition's route, and the record-vs-previous-kept-record rule
+// (merge / continue / new run); k_seg_wave below applies them to 64 records at a time.
 struct RunState {
   bool open, internal;
   uint32_t sd, f_b, f_soff, l_en, l_len, l_soff, seg_len, sb, se, way_first, way_last;
@@ -1880,299 +1870,228 @@ __device__ __forceinline__ void flag_vs(const TravRec& t, bool has_u, const Trav
   head = cont ? 0u : 1u;
 }
 
-__device__ __forceinline__ void run_piece(RunState& R, const TravRec& t, uint8_t kind, uint32_t& md, double& mtb,
-                                          double& mte) {
-  if (kind == kRecMerged) {
-    md += t.en - t.b;
-    mte = t.te;
-  } else {
-    const double dt = mte - mtb;
-    const bool slow = dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
-    R.tot += md;
-    R.q = slow ? R.q + md : 0;
-    md = t.en - t.b; mtb = t.tb; mte = t.te;
-    if (t.way != R.way_first) R.way_last = t.way;
+// ------------------------------------------------------------------------------------------
+// K4, one wave per trace (k_seg_wave).  The trace's traversal records are taken 64 at a
+// time, one record per lane, straight into registers: rec_slot[r] names the transition a
+// record comes from (k_rec_slot), a wave scan gives its distance into the transition's route
+// (the interpolated times), and the meili form_segments rules become wave-wide mask algebra
+// over ballots: the previous kept record of the chain (lookback), merged / new / head flags,
+// piece and run extents, and the segmented sums a run folds (total length, queue length of
+// the trailing slow pieces, last differing way).  The run or piece still open at a window's
+// end is carried in wave-uniform registers.  Segments of trace k land at seg_base[k] = its
+// first record (a trace has no more runs than records).  No LDS, no block barrier: the
+// per-trace work is independent, so the launch is as wide as the trace count.
+__device__ __forceinline__ int hi_le(unsigned long long m, int i) {   // highest set bit <= i, or -1
+  if (i < 0) return -1;
+  const unsigned long long mm = m & ((2ull << i) - 1ull);
+  return mm ? 63 - __builtin_clzll(mm) : -1;
+}
+__device__ __forceinline__ int lo_gt(unsigned long long m, int i) {   // lowest set bit > i, or 64
+  const unsigned long long mm = m & ~((2ull << i) - 1ull);
+  return mm ? __builtin_ctzll(mm) : 64;
+}
+__device__ __forceinline__ unsigned long long wave_incl_sum(unsigned long long v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
   }
-  R.l_en = t.en; R.l_len = t.len; R.l_soff = t.soff; R.te = t.te; R.se = t.slot;  // raw slot, resolved at close
+  return v;
+}
+// value of v in lane src (clamped to 0).  Called with every lane active: a bpermute under a
+// divergent condition reads nothing from the lanes the condition switched off.
+template <class T>
+__device__ __forceinline__ T at_lane(T v, int src) { return __shfl(v, src < 0 ? 0 : src, 64); }
+
+__global__ void k_rec_slot(DevBatch b, uint32_t* rec_slot) {
+  const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= b.P) return;
+  const uint32_t n = b.path_cnt[l], r0 = b.trav_off[l];
+  for (uint32_t q = 0; q < n; ++q) rec_slot[r0 + q] = (uint32_t)l;
 }
 
-#ifndef RM_SEG_CHUNK
-#define RM_SEG_CHUNK 512
-#endif
-constexpr uint32_t kSegChunk = RM_SEG_CHUNK;   // traversal records staged per chunk
-constexpr uint32_t kSegSpan = RM_SEG_CHUNK;    // first-record span of the traces a block takes
-#ifndef RM_SEG_THREADS
-#define RM_SEG_THREADS 256
-#endif
-constexpr uint32_t kSegThreads = RM_SEG_THREADS;
-constexpr uint32_t kSegRpl = kSegChunk / kSegThreads;   // records per lane in the flag / scan phases
-static_assert(kSegRpl * kSegThreads == kSegChunk && kSegRpl >= 1 && kSegThreads % 64 == 0, "k_segments shape");
-
-// a run open at a chunk's end (its records continue in the next chunk)
-struct RunCarry {
+// write the segment of a run (meili form_segments' segment, run_close above)
+__device__ __forceinline__ void seg_emit(const DevGraph& g, const DevBatch& b, SegmentRec* out, uint32_t f_sd, bool f_int,
+                                         uint32_t f_b, uint32_t f_soff, double f_tb, uint32_t f_slot, uint32_t wf,
+                                         uint32_t wl, unsigned long long tot, unsigned long long q, uint32_t l_en,
+                                         uint32_t l_len, uint32_t l_soff, double l_te, uint32_t l_slot) {
   RunState R;
-  double mtb, mte;
-  uint32_t md, idx, open, pad;
-};
-
-struct SegSmem {
-  TravRec rec[kSegChunk];
-  uint32_t scan[kSegChunk];         // exclusive scan of the head flags (chunk-local)
-  uint16_t pos[kSegChunk];          // chunk position of the i-th head
-  uint8_t kind[kSegChunk];
-  uint32_t wsum[kSegThreads / 64];
-  TravRec carry_rec;                // last kept record before the chunk (valid when carry_has)
-  uint32_t carry_slot, carry_has;   // slot of the record just before the chunk; chain has a kept record
-  RunCarry rc[2];                   // open run into / out of the chunk (double-buffered)
-  uint32_t next_lo, n_heads;
-};
-
-// record position of trace k's first traversal record (records of trace k are contiguous)
-__device__ __forceinline__ uint32_t trace_first_rec(const DevBatch& b, uint32_t k, uint32_t total) {
-  if (k >= b.T) return total;
-  const uint32_t o = b.trace_off[k];
-  return o < b.P ? b.trav_off[o] : total;
-}
-
-// blk_first[blk] = first trace of block blk, for blk in [0, nb]; trace k belongs to block
-// first_rec(k) / kSegSpan
-__global__ void __launch_bounds__(256) k_seg_blocks(DevBatch b, uint32_t total, uint32_t nb, uint32_t* blk_first) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k > b.T) return;
-  const uint32_t bk = k < b.T ? trace_first_rec(b, k, total) / kSegSpan : nb;
-  const int32_t bp = k > 0 ? (int32_t)(trace_first_rec(b, k - 1, total) / kSegSpan) : -1;
-  for (int32_t x = bp + 1; x <= (int32_t)bk; ++x) blk_first[x] = k;
-}
-
-// one transition slot l: its traversal records that fall in [c0, c1) into st
-__device__ __forceinline__ void seg_build_slot(const DevGraph& g, const DevBatch& b, uint64_t l, uint32_t c0, uint32_t c1,
-                                               TravRec* st) {
-  const uint32_t ns = b.path_cnt[l];
-  if (ns == 0) return;
-  const uint32_t r0 = b.trav_off[l];
-  if (r0 >= c1 || r0 + ns <= c0) return;
-  const uint32_t k = b.slot_trace[l];
-  const uint2 sab = b.path_sab[l];
-  const uint32_t sa = sab.x, sb = sab.y;
-  const double ta = b.state_time[l - 1], tb = b.state_time[l];
-  const uint32_t D = b.route_dist[l];
-  const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + l * kInlinePath : b.path_pool + b.path_off[l];
-  // a trace that failed (trace_err) forms no segments: its records become empty pieces
-  const bool bad = b.trace_err[k] != 0u;
-  uint64_t x = 0;
-  // four path edges per group: every graph load of a group is issued before its LDS stores
-  for (uint32_t q0 = 0; q0 < ns; q0 += 4) {
-    uint32_t e[4];
-    uint4 sr[4];   // packed K4 edge records (DevGraph::seg_rec)
-#pragma unroll
-    for (int y = 0; y < 4; ++y) e[y] = pe[min(q0 + y, ns - 1u)];
-#pragma unroll
-    for (int y = 0; y < 4; ++y) sr[y] = g.seg_rec[e[y]];
-#pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const uint32_t q = q0 + y;
-      if (q >= ns) break;
-      const uint32_t L = sr[y].x & 0x3fffffffu;
-      const bool rev = (sr[y].x >> 31) != 0u;
-      uint32_t b0 = 0, b1 = L;
-      if (q == 0) b0 = rev ? L - sa : sa;
-      if (q + 1 == ns) b1 = rev ? L - sb : sb;
-      if (bad) b0 = b1 = 0;
-      const double t_b = interp_time(ta, tb, x, D);
-      x += (uint64_t)(b1 - b0);
-      const uint32_t r = r0 + q;
-      if (r < c0 || r >= c1) continue;
-      TravRec& t = st[r - c0];
-      t.e = e[y]; t.b = b0; t.en = b1;
-      t.slot = (uint32_t)l | (q + 1 == ns ? kTravLast : 0u) | (((sr[y].x >> 30) & 1u) ? kTravInternal : 0u);
-      t.tb = t_b;
-      t.te = interp_time(ta, tb, x, D);
-      t.sd = sr[y].y;
-      t.soff = sr[y].z;
-      t.len = L;
-      t.way = sr[y].w;
-    }
-  }
-}
-
-// run state opened by head record f
-__device__ __forceinline__ void run_open(const DevGraph& g, const DevBatch& b, const TravRec& f, RunState& R, uint32_t& md,
-                                         double& mtb, double& mte) {
-  R.open = true; R.sd = f.sd; R.internal = (f.slot & kTravInternal) != 0u;
-  R.seg_len = f.sd != kNone ? g.seg_len[f.sd] : 0u;
-  R.f_b = f.b; R.f_soff = f.soff; R.tb = f.tb; R.sb = b.state_orig[(f.slot & kTravSlotMask) - 1u];
-  R.tot = 0; R.q = 0; R.way_first = f.way; R.way_last = f.way;
-  md = f.en - f.b;
-  mtb = f.tb; mte = f.te;
-  R.l_en = f.en; R.l_len = f.len; R.l_soff = f.soff; R.te = f.te; R.se = f.slot;
-}
-
-// fold the last piece, resolve the end state and write the run's segment
-__device__ __forceinline__ void run_finish(const DevGraph& g, const DevBatch& b, RunState& R, uint32_t md, double mtb,
-                                           double mte, SegmentRec* out) {
-  const double dt = mte - mtb;
-  const bool slow = dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
-  R.tot += md;
-  R.q = slow ? R.q + md : 0;
-  // end state of the run's last piece: its transition's target state if it is the last
-  // record of that transition, else the transition's source state
-  const uint32_t sl = R.se & kTravSlotMask;
-  R.se = b.state_orig[(R.se & kTravLast) ? sl : sl - 1u];
+  R.open = true; R.sd = f_sd; R.internal = f_int;
+  R.seg_len = f_sd != kNone ? g.seg_len[f_sd] : 0u;
+  R.f_b = f_b; R.f_soff = f_soff; R.tb = f_tb; R.sb = b.state_orig[(f_slot & kTravSlotMask) - 1u];
+  R.tot = tot; R.q = q; R.way_first = wf; R.way_last = wl;
+  R.l_en = l_en; R.l_len = l_len; R.l_soff = l_soff; R.te = l_te;
+  const uint32_t sl = l_slot & kTravSlotMask;
+  R.se = b.state_orig[(l_slot & kTravLast) ? sl : sl - 1u];
   uint32_t n = 0;
   run_close(g, R, out, n);
 }
 
-__global__ void __launch_bounds__(kSegThreads) k_segments(DevGraph g, DevBatch b, uint32_t total,
-                                                          const uint32_t* blk_first) {
-  __shared__ SegSmem sm;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t blk = xcd_block(blockIdx.x, gridDim.x);
-  const uint32_t k0 = blk_first[blk], k1 = blk_first[blk + 1];
-  if (k0 >= k1) return;
-  const uint32_t R0 = trace_first_rec(b, k0, total), R1 = trace_first_rec(b, k1, total);
-  const uint32_t L1 = k1 < b.T ? b.trace_off[k1] : (uint32_t)b.P;
-  if (tid == 0) { sm.carry_has = 0; sm.carry_slot = kNone; sm.rc[0].open = 0; sm.rc[1].open = 0; sm.next_lo = b.trace_off[k0]; }
-  __syncthreads();
-  uint32_t runs = 0;     // runs of the block before the current chunk
-  int cur = 0;           // rc[cur]: the run open into this chunk
-  for (uint32_t c0 = R0; c0 < R1; c0 += kSegChunk) {
-    const uint32_t c1 = min(c0 + kSegChunk, R1), n = c1 - c0;
-    const bool last_chunk = c1 == R1;
-    // ---- build: the slots whose records reach into [c0, c1)
-    const uint32_t l_lo = sm.next_lo;
-    __syncthreads();
-    if (tid == 0) sm.next_lo = L1;
-    __syncthreads();
-    for (uint32_t l = l_lo + tid; l < L1; l += kSegThreads) {
-      const uint32_t r0 = b.trav_off[l];
-      if (r0 >= c1) { atomicMin(&sm.next_lo, l); break; }
-      if (r0 + b.path_cnt[l] > c1) atomicMin(&sm.next_lo, l);   // straddles into the next chunk
-      seg_build_slot(g, b, l, c0, c1, sm.rec);
+__device__ __forceinline__ bool piece_slow(unsigned long long md, double mtb, double mte) {
+  const double dt = mte - mtb;
+  return dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
+}
+
+__global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const uint32_t* rec_slot, uint32_t total) {
+  const uint32_t k = blockIdx.x;
+  if (k >= b.T) return;
+  const int lane = threadIdx.x;
+  const uint32_t o = b.trace_off[k], o1 = b.trace_off[k + 1];
+  const uint32_t Rb = o < b.P ? b.trav_off[o] : total;
+  const uint32_t Re = o1 < b.P ? b.trav_off[o1] : total;
+  const bool bad = b.trace_err[k] != 0u;   // a failed trace forms no segments (empty pieces)
+  // chain lookback carry: slot of the record before the window, and whether the last kept
+  // record (lk_*) is chain-continuous up to it
+  uint32_t c_slot = kNone;
+  bool c_has = false;
+  uint32_t lk_e = 0, lk_en = 0, lk_len = 0, lk_soff = 0, lk_sd = kNone, lk_slot = 0;
+  double lk_te = 0.0;
+  // the run open at the window start: head fields, folded totals, the open piece
+  bool r_open = false, r_int = false;
+  uint32_t r_sd = kNone, r_fb = 0, r_fsoff = 0, r_fslot = 0, r_wf = 0, r_wl = 0, r_idx = 0;
+  double r_tb = 0.0, p_mtb = 0.0;
+  unsigned long long r_tot = 0, r_q = 0, p_md = 0;
+  unsigned long long carry_x = 0;   // route distance of the transition that straddles the window start
+  uint32_t runs = 0;
+  for (uint32_t c0 = Rb; c0 < Re; c0 += 64) {
+    const uint32_t n = min(64u, Re - c0);
+    const bool last = c0 + n == Re;
+    const bool act = (uint32_t)lane < n;
+    // ---- build one traversal record per lane (seg_build_slot's arithmetic)
+    uint32_t l = 0, q = 0, e = 0, b0 = 0, b1 = 0, L = 0, sd = kNone, soff = 0, way = 0, slotf = 0;
+    double ta = 0.0, tbs = 0.0;
+    uint32_t D = 0;
+    if (act) {
+      const uint32_t r = c0 + lane;
+      l = rec_slot[r];
+      const uint32_t ns = b.path_cnt[l];
+      q = r - b.trav_off[l];
+      const uint2 sab = b.path_sab[l];
+      ta = b.state_time[l - 1];
+      tbs = b.state_time[l];
+      D = b.route_dist[l];
+      const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + (uint64_t)l * kInlinePath : b.path_pool + b.path_off[l];
+      e = pe[q];
+      const uint4 sr = g.seg_rec[e];
+      L = sr.x & 0x3fffffffu;
+      const bool rev = (sr.x >> 31) != 0u;
+      b1 = L;
+      if (q == 0) b0 = rev ? L - sab.x : sab.x;
+      if (q + 1 == ns) b1 = rev ? L - sab.y : sab.y;
+      if (bad) b0 = b1 = 0;
+      sd = sr.y; soff = sr.z; way = sr.w;
+      slotf = l | (q + 1 == ns ? kTravLast : 0u) | (((sr.x >> 30) & 1u) ? kTravInternal : 0u);
     }
-    __syncthreads();
-    // ---- flags: previous kept record of the chain, in LDS or carried from before the chunk
-    uint32_t hv[kSegRpl];
-    uint32_t hsum = 0;
-#pragma unroll
-    for (uint32_t y = 0; y < kSegRpl; ++y) {
-      const uint32_t r = tid * kSegRpl + y;
-      hv[y] = 0;
-      if (r >= n) continue;
-      const TravRec& t = sm.rec[r];
-      uint8_t kind = kRecSkip;
-      uint32_t head = 0;
-      if (t.en != t.b) {
-        int32_t p = (int32_t)r - 1;
-        uint32_t nslot = t.slot & kTravSlotMask;
-        bool has = false, chain = true;
-        while (p >= 0) {
-          const uint32_t ps = sm.rec[p].slot & kTravSlotMask;
-          if (!same_chain(ps, nslot)) { chain = false; break; }
-          if (sm.rec[p].en != sm.rec[p].b) { has = true; break; }
-          nslot = ps;
-          --p;
-        }
-        if (has) flag_vs(t, true, sm.rec[p], kind, head);
-        else if (chain && sm.carry_has && same_chain(sm.carry_slot, nslot)) flag_vs(t, true, sm.carry_rec, kind, head);
-        else flag_vs(t, false, t, kind, head);
+    const unsigned long long w = (unsigned long long)(b1 - b0);
+    const unsigned long long S = wave_incl_sum(w, lane);   // also the run / piece length prefix
+    const int st = lane - (int)q;                          // lane of the transition's first record
+    const unsigned long long S_st = at_lane(S, st - 1);
+    unsigned long long xb = S - w - (st > 0 ? S_st : 0ull);
+    if (st < 0) xb += carry_x;
+    const double tbr = interp_time(ta, tbs, xb, D);
+    const double ter = interp_time(ta, tbs, xb + w, D);
+    // ---- flags: previous kept record of the chain, kind, run head
+    const bool kept = act && b1 != b0;
+    const unsigned long long K = __ballot(kept);
+    const uint32_t lp = __shfl_up(l, 1, 64);
+    const bool brk = act && (lane == 0 ? !(c_slot != kNone && same_chain(c_slot, l)) : !same_chain(lp, l));
+    const unsigned long long BR = __ballot(brk);
+    const int j = hi_le(K, lane - 1), pb = hi_le(BR, lane);
+    const bool has = j >= 0 ? pb <= j : (pb < 0 && c_has);
+    TravRec t, u;
+    t.e = e; t.b = b0; t.en = b1; t.slot = slotf; t.sd = sd; t.soff = soff; t.len = L;
+    u.e = at_lane(e, j); u.b = 0; u.en = at_lane(b1, j); u.slot = at_lane(slotf, j);
+    u.sd = at_lane(sd, j); u.soff = at_lane(soff, j); u.len = at_lane(L, j);
+    if (j < 0) { u.e = lk_e; u.en = lk_en; u.slot = lk_slot; u.sd = lk_sd; u.soff = lk_soff; u.len = lk_len; }
+    uint8_t kind = kRecSkip;
+    uint32_t head = 0;
+    if (kept) flag_vs(t, has, u, kind, head);
+    const unsigned long long NW = __ballot(kept && kind == kRecNew);
+    const unsigned long long HD = __ballot(kept && head != 0u);
+    // ---- pieces (a new record and the merged records after it) and runs (head .. next head)
+    // a piece carried in closes before this window's first kept record when that starts a new
+    // piece of the same run (a head closes the whole run below)
+    if (r_open && K != 0ull) {
+      const int fk = __builtin_ctzll(K);
+      if (((NW >> fk) & 1ull) && !((HD >> fk) & 1ull)) r_q = piece_slow(p_md, p_mtb, lk_te) ? r_q + p_md : 0ull;
+    }
+    const int ps = hi_le(NW, lane), rs = hi_le(HD, lane);
+    const unsigned long long S_ps = at_lane(S, ps - 1), S_rs = at_lane(S, rs - 1);
+    const double tb_ps = at_lane(tbr, ps);
+    const unsigned long long md = ps >= 0 ? S - (ps > 0 ? S_ps : 0ull) : p_md + S;
+    const double mtb = ps >= 0 ? tb_ps : p_mtb;
+    const int nx = lo_gt(K, lane);
+    const bool next_new = nx < 64 && ((NW >> nx) & 1ull);
+    const bool next_head = nx < 64 && ((HD >> nx) & 1ull);
+    const bool closeP = kept && (next_new || (nx == 64 && last));
+    const bool endR = kept && (next_head || (nx == 64 && last));
+    const bool slow = closeP && piece_slow(md, mtb, ter);
+    const unsigned long long CN = __ballot(closeP && !slow);
+    const unsigned long long Qs = wave_incl_sum(closeP && slow ? md : 0ull, lane);
+    // head fields of this lane's run
+    const uint32_t h_way = at_lane(way, rs), h_sd = at_lane(sd, rs), h_slot = at_lane(slotf, rs);
+    const uint32_t h_b = at_lane(b0, rs), h_soff = at_lane(soff, rs);
+    const double h_tb = at_lane(tbr, rs);
+    const uint32_t wf = rs >= 0 ? h_way : r_wf;
+    const unsigned long long MW = __ballot(kept && kind == kRecNew && head == 0u && way != wf);
+    // folded run state through this lane (closed pieces only for the queue length)
+    const int z = hi_le(CN, lane), z2 = hi_le(MW, lane);
+    const unsigned long long Q_z = at_lane(Qs, z), Q_rs = at_lane(Qs, rs - 1);
+    const uint32_t way_z2 = at_lane(way, z2);
+    const unsigned long long qv = (z >= 0 && z >= rs) ? Qs - Q_z : (rs >= 0 ? Qs - (rs > 0 ? Q_rs : 0ull) : r_q + Qs);
+    const unsigned long long totv = rs >= 0 ? S - (rs > 0 ? S_rs : 0ull) : r_tot + S;
+    const uint32_t wlv = (z2 >= 0 && z2 > rs) ? way_z2 : (rs >= 0 ? wf : r_wl);
+    const uint32_t f_sd = rs >= 0 ? h_sd : r_sd;
+    const uint32_t f_slot = rs >= 0 ? h_slot : r_fslot;
+    const uint32_t f_b = rs >= 0 ? h_b : r_fb;
+    const uint32_t f_soff = rs >= 0 ? h_soff : r_fsoff;
+    const double f_tb = rs >= 0 ? h_tb : r_tb;
+    const bool f_int = rs >= 0 ? (f_slot & kTravInternal) != 0u : r_int;
+    // the run carried in closes before this window's first kept record when that is a head
+    // (or, at the trace's end, when the window keeps nothing)
+    if (r_open && ((K != 0ull && ((HD >> __builtin_ctzll(K)) & 1ull)) || (K == 0ull && last))) {
+      if (lane == 0) {
+        const bool s0 = piece_slow(p_md, p_mtb, lk_te);
+        seg_emit(g, b, b.segs + Rb + r_idx, r_sd, r_int, r_fb, r_fsoff, r_tb, r_fslot, r_wf, r_wl, r_tot,
+                 s0 ? r_q + p_md : 0ull, lk_en, lk_len, lk_soff, lk_te, lk_slot);
       }
-      sm.kind[r] = kind;
-      hv[y] = head;
-      hsum += head;
+      r_open = false;
     }
-    // ---- exclusive scan of the head flags over the chunk
-    uint32_t incl = hsum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t u = __shfl_up(incl, d, 64);
-      if ((tid & 63) >= (uint32_t)d) incl += u;
+    if (endR) {
+      const uint32_t idx = rs >= 0 ? runs + (uint32_t)__popcll(HD & ((2ull << lane) - 1ull)) - 1u : r_idx;
+      seg_emit(g, b, b.segs + Rb + idx, f_sd, f_int, f_b, f_soff, f_tb, f_slot, wf, wlv, totv, qv, b1, L, soff, ter, slotf);
     }
-    if ((tid & 63) == 63) sm.wsum[tid >> 6] = incl;
-    __syncthreads();
-    uint32_t wbase = 0, nh = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < kSegThreads / 64; ++w) {
-      const uint32_t ws = sm.wsum[w];
-      wbase += w < (tid >> 6) ? ws : 0u;
-      nh += ws;
-    }
-    uint32_t ex = wbase + incl - hsum;
-#pragma unroll
-    for (uint32_t y = 0; y < kSegRpl; ++y) {
-      const uint32_t r = tid * kSegRpl + y;
-      if (r < n) {
-        sm.scan[r] = ex;
-        if (hv[y]) sm.pos[ex] = (uint16_t)r;
+    runs += (uint32_t)__popcll(HD);
+    if (last) break;
+    // ---- carry into the next window
+    if (K != 0ull) {
+      const int jl = 63 - __builtin_clzll(K);
+      const int rsl = __shfl(rs, jl, 64);
+      if (rsl >= 0) {
+        r_sd = __shfl(sd, rsl, 64); r_fslot = __shfl(slotf, rsl, 64); r_fb = __shfl(b0, rsl, 64);
+        r_fsoff = __shfl(soff, rsl, 64); r_tb = __shfl(tbr, rsl, 64); r_wf = __shfl(way, rsl, 64);
+        r_int = (r_fslot & kTravInternal) != 0u;
+        r_idx = runs - 1u;   // the window's last head
       }
-      ex += hv[y];
+      r_open = true;
+      r_tot = __shfl(totv, jl, 64);
+      r_q = __shfl(qv, jl, 64);
+      r_wl = __shfl(wlv, jl, 64);
+      p_md = __shfl(md, jl, 64);
+      p_mtb = __shfl(mtb, jl, 64);
+      lk_e = __shfl(e, jl, 64); lk_en = __shfl(b1, jl, 64); lk_len = __shfl(L, jl, 64);
+      lk_soff = __shfl(soff, jl, 64); lk_sd = __shfl(sd, jl, 64); lk_slot = __shfl(slotf, jl, 64);
+      lk_te = __shfl(ter, jl, 64);
+      c_has = jl == 63 ? true : (BR >> (jl + 1)) == 0ull;
+    } else {
+      c_has = c_has && BR == 0ull;
     }
-    __syncthreads();
-    // ---- runs
-    const int nxt = cur ^ 1;
-    if (tid == 0) {
-      // the run carried in from the previous chunk continues up to the first head
-      RunCarry& c = sm.rc[cur];
-      if (c.open) {
-        const uint32_t end = nh ? sm.pos[0] : n;
-        for (uint32_t q = 0; q < end; ++q)
-          if (sm.kind[q] != kRecSkip) run_piece(c.R, sm.rec[q], sm.kind[q], c.md, c.mtb, c.mte);
-        if (nh || last_chunk) {
-          run_finish(g, b, c.R, c.md, c.mtb, c.mte, b.segs + R0 + c.idx);
-          c.open = 0;
-        } else {
-          sm.rc[nxt] = c;   // still open: it spans this whole chunk
-        }
-      }
-    }
-    if (tid == kSegThreads - 1 && nh == 0 && !sm.rc[cur].open) sm.rc[nxt].open = 0;
-    for (uint32_t i = tid; i < nh; i += kSegThreads) {
-      const uint32_t r = sm.pos[i];
-      const uint32_t end = i + 1 < nh ? sm.pos[i + 1] : n;
-      RunState R;
-      uint32_t md;
-      double mtb, mte;
-      run_open(g, b, sm.rec[r], R, md, mtb, mte);
-      for (uint32_t q = r + 1; q < end; ++q)
-        if (sm.kind[q] != kRecSkip) run_piece(R, sm.rec[q], sm.kind[q], md, mtb, mte);
-      if (i + 1 == nh && !last_chunk) {   // open into the next chunk
-        RunCarry& c = sm.rc[nxt];
-        c.R = R; c.md = md; c.mtb = mtb; c.mte = mte; c.idx = runs + i; c.open = 1;
-      } else {
-        run_finish(g, b, R, md, mtb, mte, b.segs + R0 + runs + i);
-      }
-    }
-    // first segment of each trace starting in this chunk
-    for (uint32_t k = k0 + tid; k < k1; k += kSegThreads) {
-      const uint32_t rk = trace_first_rec(b, k, total);
-      if (rk >= c0 && rk < c1) b.seg_base[k] = R0 + runs + sm.scan[rk - c0];
-    }
-    // chain state at the end of the chunk for the next chunk's lookback
-    if (tid == kSegThreads - 2) {
-      uint32_t nslot = sm.rec[n - 1].slot & kTravSlotMask;
-      const uint32_t end_slot = nslot;
-      bool found = false, chain = true;
-      for (int32_t r = (int32_t)n - 1; r >= 0; --r) {
-        const uint32_t rs = sm.rec[r].slot & kTravSlotMask;
-        if (r < (int32_t)n - 1 && !same_chain(rs, nslot)) { chain = false; break; }
-        if (sm.rec[r].en != sm.rec[r].b) { found = true; sm.carry_rec = sm.rec[r]; break; }
-        nslot = rs;
-      }
-      if (!found) sm.carry_has = (chain && sm.carry_has && same_chain(sm.carry_slot, nslot)) ? 1u : 0u;
-      else sm.carry_has = 1u;
-      sm.carry_slot = end_slot;
-    }
-    __syncthreads();
-    runs += nh;
-    cur = nxt;
+    c_slot = __shfl(l, (int)n - 1, 64);
+    carry_x = __shfl(xb + w, (int)n - 1, 64);
   }
-  // traces whose records start at the block's end (none left) and per-trace counts
-  for (uint32_t k = k0 + tid; k < k1; k += kSegThreads)
-    if (trace_first_rec(b, k, total) >= R1) b.seg_base[k] = R0 + runs;
-  __threadfence_block();
-  __syncthreads();
-  for (uint32_t k = k0 + tid; k < k1; k += kSegThreads) {
-    const uint32_t nb = k + 1 < k1 ? b.seg_base[k + 1] : R0 + runs;
-    b.seg_cnt[k] = nb - b.seg_base[k];
+  if (lane == 0) {
+    b.seg_base[k] = Rb;
+    b.seg_cnt[k] = runs;
   }
 }
 
@@ -2729,7 +2648,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
   w.gsearch = nullptr;
-  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.blk_first = nullptr;
+  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
   w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
   ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
   ensure_path(std::max<uint64_t>(keep_path, cp / 8 + 1024));
@@ -2780,11 +2699,11 @@ void Matcher::ensure_segs(uint64_t n) {
   if (n <= w.cap_segs && w.segs) return;
   free_one(w, w.segs);
   free_one(w, w.reps);
-  free_one(w, w.blk_first);
+  free_one(w, w.rec_slot);
   const uint64_t c = n + n / 4 + 1024;
   w.segs = dalloc<SegmentRec>(w.allocs, c);
   w.reps = dalloc<ReportRec>(w.allocs, c);
-  w.blk_first = dalloc<uint32_t>(w.allocs, c / kSegSpan + 3);
+  w.rec_slot = dalloc<uint32_t>(w.allocs, c);
   w.cap_segs = c;
 }
 
@@ -3053,11 +2972,9 @@ void Matcher::run_device(const RunParams& rp) {
   ensure_segs(seg_total);
   v.segs = w.segs; v.reps = w.reps;
   tic(kKSegments);
-  {
-    const uint32_t nb = (uint32_t)(seg_total / kSegSpan) + 1;   // a block per kSegSpan first-record span
-    hipLaunchKernelGGL(k_seg_blocks, dim3((T + 1 + 255) / 256), dim3(256), 0, st, v, (uint32_t)seg_total, nb, w.blk_first);
-    hipLaunchKernelGGL(k_segments, dim3(nb), dim3(kSegThreads), 0, st, g, v, (uint32_t)seg_total,
-                       (const uint32_t*)w.blk_first);
+  if (T) {
+    hipLaunchKernelGGL(k_rec_slot, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v, w.rec_slot);
+    hipLaunchKernelGGL(k_seg_wave, dim3(T), dim3(64), 0, st, g, v, (const uint32_t*)w.rec_slot, (uint32_t)seg_total);
   }
   toc(kKSegments);
   if (rp.do_report) {

@@ -114,7 +114,7 @@ struct Workspace {
   // per trace outputs
   SegmentRec* segs = nullptr; uint32_t* seg_base = nullptr; uint32_t* seg_cnt = nullptr;
   uint32_t* trav_off = nullptr;     // first traversal record of each slot (scan of path_cnt)
-  uint32_t* blk_first = nullptr;    // K4: first trace of each segments block (k_seg_blocks)
+  uint32_t* rec_slot = nullptr;     // K4: transition slot of each traversal record (k_rec_slot)
   ReportRec* reps = nullptr; uint32_t* rep_cnt = nullptr; ReportStats* stats = nullptr;
   // control words (kCtlWords): [0] path pool used [1] K2 ball-tier hand-over list [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list (overflow lists of the lane tiers)
