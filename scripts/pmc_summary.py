@@ -72,7 +72,7 @@ def main():
         json.dump(summary, f, indent=1, sort_keys=True)
     # the K2 stage = every kernel bench.py times as "routes" (each runs once per step)
     stage = [k for k in summary if k in ("k_src_items", "k_routes_ball", "k_routes_lane", "k_routes_reg2",
-                                         "k_routes_wave")]
+                                         "k_routes_wave", "k_routes_global")]
     tot = lambda key: sum(summary[k].get(key, 0) for k in stage)
     hits, miss = tot("TCC_HIT_sum"), tot("TCC_MISS_sum")
     import hashlib
@@ -83,7 +83,8 @@ def main():
           "hbm_read_bytes_raw": tot("hbm_read_bytes_raw"), "hbm_write_bytes": tot("hbm_write_bytes"),
           "l2_hit_rate": hits / (hits + miss) if hits + miss else None,
           "note": "per-step sums of per-dispatch averages from separate --pmc passes; read side doubled per "
-                  "MI355X_MICROARCH.md HBM"}
+                  "MI355X_MICROARCH.md HBM, which profiles/r02/calib confirms for 16-B random gathers "
+                  "(one 128-B line request per miss)"}
     with open(os.path.join(a.out, "pmc_routes_%s.json" % a.config.lower()), "w") as f:
         json.dump(rt, f, indent=1)
     for k in sorted(summary, key=lambda x: -summary[x].get("FETCH_SIZE", 0))[:12]:
