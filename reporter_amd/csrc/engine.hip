@@ -455,9 +455,9 @@ __global__ void __launch_bounds__(64) k_candidates_wave(DevGraph g, DevBatch b) 
 // ------------------------------------------------------------------------------------------
 // u64 sums of two per-lane values: the u32 exclusive scans that lay out routes and records
 // would wrap silently past 2^32, so the host checks these totals instead of off + cnt.
-// Each 256-thread block writes its pair of partials to part[2 * block]; k_sum_parts folds
-// them.  (One same-address u64 atomic per block serialises at ~12 ns across the 8 XCDs:
-// 23 k blocks of C2 cost 0.57 ms that way.)
+// Each 256-thread block writes its pair of partials to part[2 * block]; k_scan_parts turns
+// them into block offsets and totals.  (One same-address u64 atomic per block serialises at
+// ~12 ns across the 8 XCDs: 23 k blocks of C2 cost 0.57 ms that way.)
 __device__ __forceinline__ void block_sum2_u64(unsigned long long a, unsigned long long c, unsigned long long* part) {
   __shared__ unsigned long long sa[4], sc[4];
 #pragma unroll
@@ -472,28 +472,103 @@ __device__ __forceinline__ void block_sum2_u64(unsigned long long a, unsigned lo
         make_ulonglong2(sa[0] + sa[1] + sa[2] + sa[3], sc[0] + sc[1] + sc[2] + sc[3]);
 }
 
-// out[0], out[1] = sums of the nb partial pairs (one block of 1024 threads)
-__global__ void __launch_bounds__(1024) k_sum_parts(const unsigned long long* part, uint32_t nb,
-                                                    unsigned long long* out) {
-  __shared__ unsigned long long sa[16], sc[16];
-  unsigned long long a = 0, c = 0;
-  for (uint32_t i = threadIdx.x; i < nb; i += 1024) {
-    const ulonglong2 q = reinterpret_cast<const ulonglong2*>(part)[i];
-    a += q.x;
-    c += q.y;
-  }
+// Exclusive scans of per-slot counts from the block partials the counting kernels already
+// produce (k_trans_count: pairs per 256 slots, k_sum_u64: per 1024): k_scan_parts turns the
+// partial pairs into block offsets in place (one block) and writes the u64 totals; the apply
+// kernels scan each block locally and add its offset.  Three short passes instead of a
+// generic device scan per array.
+__device__ __forceinline__ void block_excl_scan2(unsigned long long a, unsigned long long c, unsigned long long& ea,
+                                                 unsigned long long& ec, unsigned long long* sa, unsigned long long* sc,
+                                                 int nwaves) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long ia = a, ic = c;
 #pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    a += __shfl_down(a, d, 64);
-    c += __shfl_down(c, d, 64);
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned long long ta = __shfl_up(ia, d, 64), tc = __shfl_up(ic, d, 64);
+    if (lane >= d) { ia += ta; ic += tc; }
   }
-  if ((threadIdx.x & 63) == 0) { sa[threadIdx.x >> 6] = a; sc[threadIdx.x >> 6] = c; }
+  if (lane == 63) { sa[wv] = ia; sc[wv] = ic; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long ta = 0, tc = 0;
-    for (int k = 0; k < 16; ++k) { ta += sa[k]; tc += sc[k]; }
-    out[0] = ta;
-    out[1] = tc;
+  unsigned long long ba = 0, bc = 0;
+  for (int w = 0; w < nwaves; ++w) {
+    const unsigned long long xa = sa[w], xc = sc[w];
+    ba += w < wv ? xa : 0ull;
+    bc += w < wv ? xc : 0ull;
+  }
+  ea = ba + ia - a;
+  ec = bc + ic - c;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_parts(unsigned long long* part, uint32_t nb, unsigned long long* out) {
+  __shared__ unsigned long long sa[16], sc[16];
+  const uint32_t per = (nb + 1023u) / 1024u;
+  const uint32_t b0 = min(threadIdx.x * per, nb), b1 = min(b0 + per, nb);
+  ulonglong2* pp = reinterpret_cast<ulonglong2*>(part);
+  unsigned long long a = 0, c = 0;
+#pragma unroll 8
+  for (uint32_t q = b0; q < b1; ++q) { const ulonglong2 v = pp[q]; a += v.x; c += v.y; }
+  unsigned long long ea, ec;
+  block_excl_scan2(a, c, ea, ec, sa, sc, 16);
+#pragma unroll 8
+  for (uint32_t q = b0; q < b1; ++q) {
+    const ulonglong2 v = pp[q];
+    pp[q] = make_ulonglong2(ea, ec);
+    ea += v.x;
+    ec += v.y;
+  }
+  if (threadIdx.x == 1023) { out[0] = ea; out[1] = ec; }
+}
+
+// one count of each array per thread, blocks of 256 (k_trans_count's partials); a block's
+// counts sum to < 2^32 (at most 256 x 16 x 16), so the in-block scan runs on u32 pairs
+__global__ void __launch_bounds__(256) k_scan_apply2(const uint32_t* a, const uint32_t* c, uint64_t n,
+                                                     const unsigned long long* part, uint32_t* ao, uint32_t* co) {
+  __shared__ uint32_t sa[4], sc[4];
+  const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const ulonglong2 base = reinterpret_cast<const ulonglong2*>(part)[blockIdx.x];
+  const uint32_t va = p < n ? a[p] : 0u, vc = p < n ? c[p] : 0u;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t ia = va, ic = vc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t ta = __shfl_up(ia, d, 64), tc = __shfl_up(ic, d, 64);
+    if (lane >= d) { ia += ta; ic += tc; }
+  }
+  if (lane == 63) { sa[wv] = ia; sc[wv] = ic; }
+  __syncthreads();
+  uint32_t ba = 0, bc = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    ba += w < wv ? sa[w] : 0u;
+    bc += w < wv ? sc[w] : 0u;
+  }
+  if (p < n) {
+    ao[p] = (uint32_t)base.x + ba + ia - va;
+    co[p] = (uint32_t)base.y + bc + ic - vc;
+  }
+}
+
+// four counts per thread, blocks of 256 (k_sum_u64's partials)
+__global__ void __launch_bounds__(256) k_scan_apply4(const uint32_t* a, uint64_t n, const unsigned long long* part,
+                                                     uint32_t* ao) {
+  __shared__ unsigned long long sa[4], sc[4];
+  const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  if (i + 4 <= n) {
+    const uint4 q = *reinterpret_cast<const uint4*>(a + i);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    for (uint64_t x = i; x < n; ++x) v[x - i] = a[x];
+  }
+  unsigned long long ea, ec;
+  block_excl_scan2((unsigned long long)v[0] + v[1] + v[2] + v[3], 0ull, ea, ec, sa, sc, 4);
+  const unsigned long long base = part[2 * blockIdx.x] + ea;
+  const uint32_t o0 = (uint32_t)base, o1 = o0 + v[0], o2 = o1 + v[1], o3 = o2 + v[2];
+  if (i + 4 <= n) {
+    *reinterpret_cast<uint4*>(ao + i) = make_uint4(o0, o1, o2, o3);
+  } else {
+    const uint32_t o[4] = {o0, o1, o2, o3};
+    for (uint64_t x = i; x < n; ++x) ao[x] = o[x - i];
   }
 }
 
@@ -504,6 +579,8 @@ __global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long l
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t c = 0, ns = 0;
   if (p < b.P) {   // every lane reaches the block sum below (it holds a barrier)
+    b.choice[p] = -1;      // K3 sets the chosen candidates; the path stage counts chosen transitions
+    b.path_cnt[p] = 0u;
     const uint32_t k = b.slot_trace[p];
     const uint32_t o = b.trace_off[k];
     const uint32_t s = (uint32_t)(p - o);
@@ -2182,7 +2259,7 @@ __global__ void __launch_bounds__(64) k_report_lists(uint32_t T, const uint32_t*
 // u64 totals of one or two u32 count arrays: the u32 exclusive scans that lay out routes and
 // records would wrap silently past 2^32, so the host checks these totals instead of off+cnt
 // u64 total of a u32 count array (four per lane, one atomic per block)
-// block partials of the sum of a[0, n) (four u32 per lane), folded by k_sum_parts
+// block partials of the sum of a[0, n) (four u32 per lane), scanned by k_scan_parts
 __global__ void __launch_bounds__(256) k_sum_u64(const uint32_t* a, uint64_t n, unsigned long long* part) {
   const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
   unsigned long long v = 0;
@@ -2642,10 +2719,6 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.trace_err = dalloc<uint32_t>(L, ct);
   w.tot64 = dalloc<unsigned long long>(L, 4);
   w.tot_part = dalloc<unsigned long long>(L, 2 * ((cp + 255) / 256) + 2);
-  size_t tmp = 0;
-  RM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, w.trans_cnt, w.trans_off, (int)cp, stream_));
-  w.scan_tmp_bytes = tmp;
-  w.scan_tmp = dalloc<char>(L, tmp);
   w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
   w.gsearch = nullptr;
   w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
@@ -2837,8 +2910,6 @@ void Matcher::run_device(const RunParams& rp) {
   if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 32 * sizeof(uint32_t), hipHostMallocDefault));
   unsigned long long* htot = reinterpret_cast<unsigned long long*>(hctl_ + 16);
   RM_HIP(hipMemsetAsync(w.ctl, 0, kCtlWords * sizeof(uint32_t), st));
-  RM_HIP(hipMemsetAsync(w.choice, 0xff, P, st));
-  RM_HIP(hipMemsetAsync(w.path_cnt, 0, P * sizeof(uint32_t), st));
   RM_HIP(hipMemsetAsync(w.trace_err, 0, T * sizeof(uint32_t), st));
   DevBatch v = make_view(w, T, P);
   const uint32_t count_grid = (uint32_t)((P + 255) / 256);
@@ -2853,11 +2924,9 @@ void Matcher::run_device(const RunParams& rp) {
   toc(kKCandidates);
   tic(kKScan);
   hipLaunchKernelGGL(k_trans_count, dim3(count_grid), dim3(256), 0, st, v, w.tot_part);
-  hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(1024), 0, st, (const unsigned long long*)w.tot_part, count_grid, w.tot64);
-  size_t tmp = w.scan_tmp_bytes;
-  RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.trans_cnt, w.trans_off, (int)P, st));
-  tmp = w.scan_tmp_bytes;
-  RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.src_cnt, w.src_off, (int)P, st));
+  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.tot_part, count_grid, w.tot64);
+  hipLaunchKernelGGL(k_scan_apply2, dim3(count_grid), dim3(256), 0, st, (const uint32_t*)w.trans_cnt,
+                     (const uint32_t*)w.src_cnt, P, (const unsigned long long*)w.tot_part, w.trans_off, w.src_off);
   toc(kKScan);
   RM_HIP(hipMemcpyAsync(htot, w.tot64, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   RM_HIP(hipStreamSynchronize(st));
@@ -2905,8 +2974,10 @@ void Matcher::run_device(const RunParams& rp) {
   toc(kKViterbi);
   for (int attempt = 0;; ++attempt) {
     tic(kKPaths);
-    RM_HIP(hipMemsetAsync(w.ctl + 8, 0, sizeof(uint32_t), st));    // path ball hand-overs
-    RM_HIP(hipMemsetAsync(w.ctl + 10, 0, sizeof(uint32_t), st));   // paths list C
+    if (attempt) {   // the first attempt starts from the zeroed control words
+      RM_HIP(hipMemsetAsync(w.ctl + 8, 0, sizeof(uint32_t), st));    // path ball hand-overs
+      RM_HIP(hipMemsetAsync(w.ctl + 10, 0, sizeof(uint32_t), st));   // paths list C
+    }
     if (balls) {
       hipLaunchKernelGGL(k_paths_ball, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>((P + 255) / 256, kListedGrid)), dim3(256), 0,
@@ -2924,10 +2995,10 @@ void Matcher::run_device(const RunParams& rp) {
     toc(kKPaths);
     // traversal records are laid out by a scan of path_cnt (0 for slots without a chosen transition)
     tic(kKSegments);
-    tmp = w.scan_tmp_bytes;
-    RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
     hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot_part);
-    hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(1024), 0, st, (const unsigned long long*)w.tot_part, sum_grid, w.tot64 + 2);
+    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.tot_part, sum_grid, w.tot64 + 2);
+    hipLaunchKernelGGL(k_scan_apply4, dim3(sum_grid), dim3(256), 0, st, (const uint32_t*)w.path_cnt, P,
+                       (const unsigned long long*)w.tot_part, w.trav_off);
     toc(kKSegments);
     RM_HIP(hipMemcpyAsync(htot + 2, w.tot64 + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     read_ctl();
@@ -2948,10 +3019,10 @@ void Matcher::run_device(const RunParams& rp) {
       // chosen transitions whose path search outgrew the LDS wave tier
       ensure_global_search();
       hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
-      tmp = w.scan_tmp_bytes;
-      RM_HIP(hipcub::DeviceScan::ExclusiveSum(w.scan_tmp, tmp, w.path_cnt, w.trav_off, (int)P, st));
       hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot_part);
-      hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(1024), 0, st, (const unsigned long long*)w.tot_part, sum_grid, w.tot64 + 2);
+      hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.tot_part, sum_grid, w.tot64 + 2);
+      hipLaunchKernelGGL(k_scan_apply4, dim3(sum_grid), dim3(256), 0, st, (const uint32_t*)w.path_cnt, P,
+                         (const unsigned long long*)w.tot_part, w.trav_off);
       RM_HIP(hipMemcpyAsync(htot + 2, w.tot64 + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
       read_ctl();
     }

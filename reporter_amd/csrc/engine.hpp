@@ -127,7 +127,6 @@ struct Workspace {
   uint32_t* trace_err = nullptr;            // per trace: error bits (kErr*) of that trace alone
   unsigned long long* tot64 = nullptr;      // u64 totals: [0] transitions [1] sources [2] path edges
   unsigned long long* tot_part = nullptr;   // per-block partial pairs of those totals (k_sum_parts folds them)
-  void* scan_tmp = nullptr; size_t scan_tmp_bytes = 0;
   std::vector<void*> allocs;
   ~Workspace();
   void release();
