@@ -32,6 +32,8 @@
 static const double MPD_LAT = 110567.0;
 static const double MPD_LON_EQ = 111320.0;
 static const double DEG2RAD = 0.017453292519943295;
+static const double OG_PI = 3.141592653589793;
+static const double RAD_EARTH_M = 6378160.187; /* Valhalla midgard kRadEarthMeters */
 static const double QUEUE_SPEED_MPS = 2.7777777777777777; /* 10 km/h */
 
 /* ---------------- deterministic math (identical op order on the GPU) ---------------- */
@@ -50,12 +52,84 @@ static double og_cos(double x) {
   p = p * z + 1.0;
   return p;
 }
+/* sin(x), |x| <= pi/2: odd Taylor series to x^21 in Horner form (exact hex coefficients) */
+static double og_sin(double x) {
+  const double z = x * x;
+  double p = 0x1.71b8ef6dcf572p-66;
+  p = p * z + -0x1.2f49b46814157p-57;
+  p = p * z + 0x1.952c77030ad4ap-49;
+  p = p * z + -0x1.ae7f3e733b81fp-41;
+  p = p * z + 0x1.6124613a86d09p-33;
+  p = p * z + -0x1.ae64567f544e4p-26;
+  p = p * z + 0x1.71de3a556c734p-19;
+  p = p * z + -0x1.a01a01a01a01ap-13;
+  p = p * z + 0x1.1111111111111p-7;
+  p = p * z + -0x1.5555555555555p-3;
+  p = p * z + 0x1.0000000000000p+0;
+  return x * p;
+}
+
+// cos(x) for |x| <= 2 pi (differences of longitudes), reduced onto det_cos's range.
+static double og_cos_wide(double x) {
+  double a = x < 0.0 ? -x : x;
+  if (a > OG_PI) a = 2.0 * OG_PI - a;
+  if (a > 0.5 * OG_PI) return -og_cos(OG_PI - a);
+  return og_cos(a);
+}
+
+// asin(y) for |y| <= 1/2: Taylor series to y^55 (coefficients (2n)!/(4^n n!^2 (2n+1)) as exact
+// hex literals), Horner in y^2.
+static double og_asin_half(double y) {
+  const double z = y * y;
+  double p = 0x1.018f963c229bfp-9;
+  p = p * z + 0x1.1052bc5fa960ap-9;
+  p = p * z + 0x1.208d3570ae5a6p-9;
+  p = p * z + 0x1.3275586c5f2f0p-9;
+  p = p * z + 0x1.464c0950f7d47p-9;
+  p = p * z + 0x1.5c5f56efaaaabp-9;
+  p = p * z + 0x1.750de64d7d05fp-9;
+  p = p * z + 0x1.90cb77f60c7cep-9;
+  p = p * z + 0x1.b026f57b13b14p-9;
+  p = p * z + 0x1.d3d2a8e0dd67dp-9;
+  p = p * z + 0x1.fcaf8fb6db6dbp-9;
+  p = p * z + 0x1.15ee9d45d1746p-8;
+  p = p * z + 0x1.31683bdef7bdfp-8;
+  p = p * z + 0x1.51ba308d3dcb1p-8;
+  p = p * z + 0x1.782dda12f684cp-8;
+  p = p * z + 0x1.a6863d70a3d71p-8;
+  p = p * z + 0x1.df3bd37a6f4dfp-8;
+  p = p * z + 0x1.12ef3cf3cf3cfp-7;
+  p = p * z + 0x1.3fde50d79435ep-7;
+  p = p * z + 0x1.7a87878787878p-7;
+  p = p * z + 0x1.c99999999999ap-7;
+  p = p * z + 0x1.1c4ec4ec4ec4fp-6;
+  p = p * z + 0x1.6e8ba2e8ba2e9p-6;
+  p = p * z + 0x1.f1c71c71c71c7p-6;
+  p = p * z + 0x1.6db6db6db6db7p-5;
+  p = p * z + 0x1.3333333333333p-4;
+  p = p * z + 0x1.5555555555555p-3;
+  p = p * z + 0x1.0000000000000p+0;
+  return y * p;
+}
+
+// acos(c) for -1 < c < 1 from det_asin_half: 2 asin(sqrt((1-c)/2)) near 1, pi/2 - asin(c) in the
+// middle, pi - 2 asin(sqrt((1+c)/2)) near -1 (IEEE sqrt: correctly rounded on both sides).
+static double og_acos(double c) {
+  if (c > 0.5) return 2.0 * og_asin_half(sqrt((1.0 - c) * 0.5));
+  if (c < -0.5) return OG_PI - 2.0 * og_asin_half(sqrt((1.0 + c) * 0.5));
+  return 0.5 * OG_PI - og_asin_half(c);
+}
 static float og_mlon(float lat) { return (float)(MPD_LON_EQ * og_cos((double)lat * DEG2RAD)); }
+/* measurement distance: Valhalla PointLL::Distance (meili GreatCircleDistance), spherical law of
+   cosines on the float coordinates, radius RAD_EARTH_M, rounded to float */
 static double og_gc(float lon_a, float lat_a, float lon_b, float lat_b) {
-  const double mlat = 0.5 * ((double)lat_a + (double)lat_b);
-  const double dy = ((double)lat_b - (double)lat_a) * MPD_LAT;
-  const double dx = ((double)lon_b - (double)lon_a) * (MPD_LON_EQ * og_cos(mlat * DEG2RAD));
-  return sqrt(dx * dx + dy * dy);
+  if (lon_a == lon_b && lat_a == lat_b) return 0.0;
+  const double a = (double)lat_a * DEG2RAD, c = (double)lat_b * DEG2RAD;
+  const double dl = ((double)lon_b - (double)lon_a) * DEG2RAD;
+  const double cosb = og_sin(a) * og_sin(c) + og_cos(a) * og_cos(c) * og_cos_wide(dl);
+  if (cosb >= 1.0) return 0.0;
+  if (cosb <= -1.0) return (double)(float)(OG_PI * RAD_EARTH_M);
+  return (double)(float)(og_acos(cosb) * RAD_EARTH_M);
 }
 static float f32_of(uint32_t bits) { float f; memcpy(&f, &bits, 4); return f; }
 

@@ -116,41 +116,81 @@ __device__ __forceinline__ uint32_t time_bound(double dt, const MatchOptions& o)
 
 // ------------------------------------------------------------------------------------------
 // k_states: interpolation rule (points closer than interpolation_distance to the last
-// state are not states; meili MapMatcher::OfflineMatch)
-// One lane per trace (the last-state chain is sequential); coordinates are prefetched
-// eight points ahead so the fp64 distance chain does not wait on memory.
+// state are not states; meili MapMatcher::OfflineMatch).  One wave per trace, 64 points per
+// step: every lane computes, speculatively and in parallel, the distance from the point
+// before it (d1) and from two points back (d2) — the two the sequential rule needs unless two
+// points in a row are skipped.  The rule itself then walks the chunk with mask arithmetic:
+// runs of d1 >= interp extend a run of states in one step, after a skipped point d2 decides,
+// and only a second skip in a row computes a distance from the last state (wave-uniform).
+__device__ __forceinline__ float lane_f(float v, uint32_t q) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)q));
+}
+
 __global__ void __launch_bounds__(64) k_states(DevBatch b) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = blockIdx.x;
   if (k >= b.T) return;
+  const int lane = threadIdx.x;
   const uint32_t o = b.trace_off[k], n = b.trace_off[k + 1] - o;
   const MatchOptions op = b.opts[b.trace_opt[k]];
   const double interp = (double)op.interpolation_distance;
-  uint32_t ns = 0;
-  float llon = 0.f, llat = 0.f;
-  float clo[8], cla[8], nlo[8], nla[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) { clo[q] = q < (int)n ? b.lon[o + q] : 0.f; cla[q] = q < (int)n ? b.lat[o + q] : 0.f; }
-  for (uint32_t i0 = 0; i0 < n; i0 += 8) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint32_t i = i0 + 8 + q;
-      nlo[q] = i < n ? b.lon[o + i] : 0.f;
-      nla[q] = i < n ? b.lat[o + i] : 0.f;
+  uint32_t ns = 0, last = 0;              // states so far, index of the last state
+  float llon = 0.f, llat = 0.f;           // coordinates of the last state
+  float c1lo = 0.f, c1la = 0.f, c2lo = 0.f, c2la = 0.f;   // points c0-1, c0-2
+  for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+    const uint32_t i = c0 + lane, m = min(64u, n - c0);
+    const bool act = i < n;
+    const float lo = act ? b.lon[o + i] : 0.f, la = act ? b.lat[o + i] : 0.f;
+    if (act) b.slot_trace[o + i] = k;
+    float lo1 = __shfl_up(lo, 1, 64), la1 = __shfl_up(la, 1, 64);
+    float lo2 = __shfl_up(lo, 2, 64), la2 = __shfl_up(la, 2, 64);
+    if (lane == 0) { lo1 = c1lo; la1 = c1la; lo2 = c2lo; la2 = c2la; }
+    if (lane == 1) { lo2 = c1lo; la2 = c1la; }
+    // sin / cos of each latitude once per lane, neighbours' by shuffle (the carried points
+    // recompute theirs)
+    const double s0 = lat_sin(la), k0 = lat_cos(la);
+    double s1 = __shfl_up(s0, 1, 64), k1 = __shfl_up(k0, 1, 64), s2 = __shfl_up(s0, 2, 64), k2 = __shfl_up(k0, 2, 64);
+    if (lane <= 1) {
+      const float cl = lane == 0 ? c2la : c1la;
+      s2 = lat_sin(cl); k2 = lat_cos(cl);
+      if (lane == 0) { s1 = lat_sin(c1la); k1 = lat_cos(c1la); }
     }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint32_t i = i0 + q;
-      if (i >= n) break;
-      b.slot_trace[o + i] = k;
-      const float lo = clo[q], la = cla[q];
-      if (i > 0 && gc_distance(llon, llat, lo, la) < interp) continue;
-      b.state_orig[o + ns++] = i;
-      llon = lo; llat = la;
+    const bool a1 = act && (i == 0 || !(gc_trig(lo1, la1, s1, k1, lo, la, s0, k0) < interp));
+    const bool a2 = act && i >= 2 && !(gc_trig(lo2, la2, s2, k2, lo, la, s0, k0) < interp);
+    const unsigned long long A = __ballot(a1), B = __ballot(a2);
+    unsigned long long st = 0;
+    for (uint32_t q = 0; q < m;) {
+      const uint32_t ii = c0 + q;
+      if (ii == 0 || last + 1 == ii) {
+        // a state right before: d1 decides; a run of d1 passes is a run of states
+        const unsigned long long rest = ~(A >> q);
+        const uint32_t run = min(rest ? (uint32_t)__builtin_ctzll(rest) : 64u, m - q);
+        if (run) {
+          st |= (run == 64u ? ~0ull : ((1ull << run) - 1ull)) << q;
+          q += run;
+          last = c0 + q - 1;
+        } else {
+          ++q;   // skipped: the next point is measured from two back
+        }
+        continue;
+      }
+      bool s;
+      if (last + 2 == ii) {
+        s = (B >> q) & 1ull;
+      } else {   // two or more skipped in a row: measure from the last state itself
+        float plo = llon, pla = llat;
+        if (last >= c0) { plo = lane_f(lo, last - c0); pla = lane_f(la, last - c0); }
+        s = !(gc_distance(plo, pla, lane_f(lo, q), lane_f(la, q)) < interp);
+      }
+      if (s) { st |= 1ull << q; last = ii; }
+      ++q;
     }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { clo[q] = nlo[q]; cla[q] = nla[q]; }
+    if ((st >> lane) & 1ull) b.state_orig[o + ns + (uint32_t)__popcll(st & ((1ull << lane) - 1ull))] = i;
+    ns += (uint32_t)__popcll(st);
+    if (last >= c0) { llon = lane_f(lo, last - c0); llat = lane_f(la, last - c0); }
+    c1lo = lane_f(lo, 63); c1la = lane_f(la, 63);
+    c2lo = lane_f(lo, 62); c2la = lane_f(la, 62);
   }
-  b.n_states[k] = ns;
+  if (lane == 0) b.n_states[k] = ns;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2916,7 +2956,7 @@ void Matcher::run_device(const RunParams& rp) {
   const uint32_t sum_grid = (uint32_t)((P + 1023) / 1024);   // k_sum_u64: four counts per lane
 
   tic(kKStates);
-  hipLaunchKernelGGL(k_states, dim3((T + 63) / 64), dim3(64), 0, st, v);
+  hipLaunchKernelGGL(k_states, dim3(T), dim3(64), 0, st, v);
   toc(kKStates);
   tic(kKCandidates);
   hipLaunchKernelGGL(k_candidates_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);

@@ -32,6 +32,8 @@ constexpr uint32_t kNone = 0xffffffffu;
 constexpr double kMetersPerDegLat = 110567.0;  // meters per degree latitude
 constexpr double kMetersPerDegLonEq = 111320.0;  // meters per degree longitude at the equator
 constexpr double kDegToRad = 0.017453292519943295;
+constexpr double kPi = 3.141592653589793;
+constexpr double kRadEarthMeters = 6378160.187;   // Valhalla midgard kRadEarthMeters
 
 // cos(x) for |x| <= pi/2 by a fixed Horner polynomial in x^2 (Taylor to x^20).
 // Pure IEEE add/mul in a fixed order: identical bits on host and device.
@@ -51,18 +53,97 @@ RM_HD double det_cos(double x) {
   return p;
 }
 
+// sin(x) for |x| <= pi/2: odd Taylor series to x^21, Horner in x^2 (coefficients as exact
+// hex literals of (-1)^k/(2k+1)!); same contract as det_cos.
+RM_HD double det_sin(double x) {
+  const double z = x * x;
+  double p = 0x1.71b8ef6dcf572p-66;
+  p = p * z + -0x1.2f49b46814157p-57;
+  p = p * z + 0x1.952c77030ad4ap-49;
+  p = p * z + -0x1.ae7f3e733b81fp-41;
+  p = p * z + 0x1.6124613a86d09p-33;
+  p = p * z + -0x1.ae64567f544e4p-26;
+  p = p * z + 0x1.71de3a556c734p-19;
+  p = p * z + -0x1.a01a01a01a01ap-13;
+  p = p * z + 0x1.1111111111111p-7;
+  p = p * z + -0x1.5555555555555p-3;
+  p = p * z + 0x1.0000000000000p+0;
+  return x * p;
+}
+
+// cos(x) for |x| <= 2 pi (differences of longitudes), reduced onto det_cos's range.
+RM_HD double det_cos_wide(double x) {
+  double a = x < 0.0 ? -x : x;
+  if (a > kPi) a = 2.0 * kPi - a;
+  if (a > 0.5 * kPi) return -det_cos(kPi - a);
+  return det_cos(a);
+}
+
+// asin(y) for |y| <= 1/2: Taylor series to y^55 (coefficients (2n)!/(4^n n!^2 (2n+1)) as exact
+// hex literals), Horner in y^2.
+RM_HD double det_asin_half(double y) {
+  const double z = y * y;
+  double p = 0x1.018f963c229bfp-9;
+  p = p * z + 0x1.1052bc5fa960ap-9;
+  p = p * z + 0x1.208d3570ae5a6p-9;
+  p = p * z + 0x1.3275586c5f2f0p-9;
+  p = p * z + 0x1.464c0950f7d47p-9;
+  p = p * z + 0x1.5c5f56efaaaabp-9;
+  p = p * z + 0x1.750de64d7d05fp-9;
+  p = p * z + 0x1.90cb77f60c7cep-9;
+  p = p * z + 0x1.b026f57b13b14p-9;
+  p = p * z + 0x1.d3d2a8e0dd67dp-9;
+  p = p * z + 0x1.fcaf8fb6db6dbp-9;
+  p = p * z + 0x1.15ee9d45d1746p-8;
+  p = p * z + 0x1.31683bdef7bdfp-8;
+  p = p * z + 0x1.51ba308d3dcb1p-8;
+  p = p * z + 0x1.782dda12f684cp-8;
+  p = p * z + 0x1.a6863d70a3d71p-8;
+  p = p * z + 0x1.df3bd37a6f4dfp-8;
+  p = p * z + 0x1.12ef3cf3cf3cfp-7;
+  p = p * z + 0x1.3fde50d79435ep-7;
+  p = p * z + 0x1.7a87878787878p-7;
+  p = p * z + 0x1.c99999999999ap-7;
+  p = p * z + 0x1.1c4ec4ec4ec4fp-6;
+  p = p * z + 0x1.6e8ba2e8ba2e9p-6;
+  p = p * z + 0x1.f1c71c71c71c7p-6;
+  p = p * z + 0x1.6db6db6db6db7p-5;
+  p = p * z + 0x1.3333333333333p-4;
+  p = p * z + 0x1.5555555555555p-3;
+  p = p * z + 0x1.0000000000000p+0;
+  return y * p;
+}
+
+// acos(c) for -1 < c < 1 from det_asin_half: 2 asin(sqrt((1-c)/2)) near 1, pi/2 - asin(c) in the
+// middle, pi - 2 asin(sqrt((1+c)/2)) near -1 (IEEE sqrt: correctly rounded on both sides).
+RM_HD double det_acos(double c) {
+  if (c > 0.5) return 2.0 * det_asin_half(__builtin_sqrt((1.0 - c) * 0.5));
+  if (c < -0.5) return kPi - 2.0 * det_asin_half(__builtin_sqrt((1.0 + c) * 0.5));
+  return 0.5 * kPi - det_asin_half(c);
+}
+
 // meters per degree of longitude at latitude lat (degrees), as float.
 RM_HD float meters_per_lon(float lat) {
   return (float)(kMetersPerDegLonEq * det_cos((double)lat * kDegToRad));
 }
 
-// "great-circle" distance between two measurements: equirectangular at the
-// mean latitude, fp64.
+// Great-circle distance between two measurements, as Valhalla's PointLL::Distance (meili's
+// GreatCircleDistance): spherical law of cosines on the float lon/lat, Earth radius
+// kRadEarthMeters, the result rounded to float; deterministic sin/cos/acos so both sides agree.
+// gc_trig takes sin/cos of both latitudes (lat_sin / lat_cos below), so kernels that measure a
+// point against several others evaluate them once per point; same operations, same bits.
+RM_HD double lat_sin(float lat) { return det_sin((double)lat * kDegToRad); }
+RM_HD double lat_cos(float lat) { return det_cos((double)lat * kDegToRad); }
+RM_HD double gc_trig(float lon_a, float lat_a, double sa, double ca, float lon_b, float lat_b, double sb, double cb) {
+  if (lon_a == lon_b && lat_a == lat_b) return 0.0;
+  const double dl = ((double)lon_b - (double)lon_a) * kDegToRad;
+  const double cosb = sa * sb + ca * cb * det_cos_wide(dl);
+  if (cosb >= 1.0) return 0.0;
+  if (cosb <= -1.0) return (double)(float)(kPi * kRadEarthMeters);
+  return (double)(float)(det_acos(cosb) * kRadEarthMeters);
+}
 RM_HD double gc_distance(float lon_a, float lat_a, float lon_b, float lat_b) {
-  const double mlat = 0.5 * ((double)lat_a + (double)lat_b);
-  const double dy = ((double)lat_b - (double)lat_a) * kMetersPerDegLat;
-  const double dx = ((double)lon_b - (double)lon_a) * (kMetersPerDegLonEq * det_cos(mlat * kDegToRad));
-  return __builtin_sqrt(dx * dx + dy * dy);
+  return gc_trig(lon_a, lat_a, lat_sin(lat_a), lat_cos(lat_a), lon_b, lat_b, lat_sin(lat_b), lat_cos(lat_b));
 }
 
 // ---- directed-edge record (16 B, one dwordx4 load in the route kernel) ----
@@ -119,10 +200,17 @@ RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) { return (v * 2654435761u) >
 // are spread by a Fibonacci hash.  Small tables hash every road (few groups would collide into
 // long probe chains: C4's 700 m tables ran K2 2x slower grouped).  C2 K2 1.10 -> 1.04 ms,
 // C3 4.11 -> 3.58 ms on 200 k traces.
-constexpr uint32_t kBallGroupBits = 10;
+#ifndef RM_BALL_GROUP_LOG
+#define RM_BALL_GROUP_LOG 3
+#endif
+#ifndef RM_BALL_GROUP_BITS
+#define RM_BALL_GROUP_BITS 10
+#endif
+constexpr uint32_t kBallGroupBits = RM_BALL_GROUP_BITS, kBallGroupLog = RM_BALL_GROUP_LOG;
 RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) {
   if (bits < kBallGroupBits) return (v * 2654435761u) >> (32u - bits);
-  return ((((v >> 3) * 2654435761u) >> (35u - bits)) << 3) | (v & 7u);
+  return ((((v >> kBallGroupLog) * 2654435761u) >> (32u + kBallGroupLog - bits)) << kBallGroupLog) |
+         (v & ((1u << kBallGroupLog) - 1u));
 }
 #endif
 

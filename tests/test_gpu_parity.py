@@ -261,3 +261,32 @@ def test_coalesced_match_from_threads(c1, tmpdir_session):
     assert served == n
     assert st["batches"] - before["batches"] < served and st["max_batch"] > 1
     print("coalescing", st)
+
+
+def test_randomised_options_per_trace(c1):
+    """Every MatchOptions field varied per trace (one option row per trace), with mixed sampling
+    rates and noise: the GPU against the oracle at every stage, and report() on top."""
+    path, g, eng = c1
+    rng = np.random.default_rng(2024)
+    parts, opts = [], []
+    modes = list(world.MODES)
+    for q in range(48):
+        mode = modes[q % len(modes)]
+        rate = float(rng.choice([1.0, 2.0, 5.0, 15.0, 30.0, 60.0]))
+        noise = float(rng.uniform(2.0, 20.0))
+        n_pts = int(rng.integers(2, 400))
+        parts.append(world.generate_traces(path, 1, n_pts, rate, noise, seed=int(rng.integers(1 << 30)), mode=mode))
+        opts.append(engine.default_options(
+            1, mode=world.MODES[mode], sigma_z=float(rng.uniform(1.0, 25.0)), beta=float(rng.uniform(0.3, 12.0)),
+            search_radius=float(rng.uniform(5.0, 220.0)), gps_accuracy=float(rng.uniform(1.0, 60.0)),
+            breakage_distance=float(rng.uniform(150.0, 4000.0)),
+            interpolation_distance=float(rng.uniform(0.0, 40.0)),
+            max_route_distance_factor=float(rng.uniform(1.0, 8.0)),
+            max_route_time_factor=float(rng.uniform(1.0, 6.0)))[0])
+    tr = {k: np.concatenate([p[k] for p in parts]) for k in ("lon", "lat", "time", "accuracy")}
+    tr["trace_off"] = np.concatenate([[0], np.cumsum([len(p["lon"]) for p in parts])]).astype(np.uint32)
+    trace_opt = np.arange(len(parts), dtype=np.uint32)
+    bm, ref = _run_both(path, g, eng, tr, np.array(opts, engine.OPTIONS_DTYPE), trace_opt)
+    c = compare_all(bm, ref, tr["trace_off"])
+    assert c["segments"] > 50 and c["chained"] > 1000, c
+    bm.close()
