@@ -645,7 +645,8 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
             const double ci = cost[(l - 1) * (uint64_t)OG_K + i];
             const uint32_t rc = R->route[R->trans_off[l] + i * KB + j];
             if (ci == INFINITY || rc == OG_ROUTE_INVALID) continue;
-            const double c = ci + fabs((double)rc * 0.01 - R->gc[l]) * inv_beta;
+            /* one fused multiply-add: cost_i + |route_m - gc| / beta, rounded once */
+            const double c = fma(fabs((double)rc * 0.01 - R->gc[l]), inv_beta, ci);
             if (c < best) { best = c; arg = (int)i; }
           }
           const double em = (double)R->cand_sq[l * (uint64_t)OG_K + j] * inv2s2;

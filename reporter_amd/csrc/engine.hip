@@ -651,14 +651,6 @@ __global__ void k_src_items(DevBatch b) {
   for (uint32_t i = 0; i < n; ++i) b.src_item[at + i] = (uint32_t)p;
 }
 
-// transition cost |route_m - gc| * (1/beta) (meili TransitionCostModel restatement, fp64),
-// +inf for an invalid route.  K2 stores only the route length (4 B per transition);
-// K3 evaluates this where it consumes the route.
-__device__ __forceinline__ double trans_cost(uint32_t r, double gc, double inv_beta) {
-  if (r == kRouteInvalid) return __longlong_as_double(0x7ff0000000000000ll);
-  return fabs((double)r * 0.01 - gc) * inv_beta;
-}
-
 // descriptor field access (see Workspace::cand_desc)
 __device__ __forceinline__ uint32_t d_spf(const uint4& d0) { return d0.w & 0xffffu; }
 __device__ __forceinline__ uint32_t d_spr(const uint4& d0) { return d0.w >> 16; }
@@ -1537,19 +1529,20 @@ __device__ __forceinline__ double row_bcast(double v) {
   return __builtin_amdgcn_mov_dpp(v, 0x150 + I, 0xf, 0xf, false);   // one v_mov_b64_dpp
 }
 
-// best / arg over sources I.. prevK-1 of this lane's target: cost of source i (lane i's
-// cj) + |route_m - gc| / beta, the first strict minimum in source order.  Bit-identical to
-// cj + trans_cost(route_cm): route_m is the same (double)cm * 0.01 and +inf stays +inf.
+// best / arg over sources I.. prevK-1 of this lane's target: cost of source i (lane i's cj)
+// plus |route_m - gc| / beta, the first strict minimum in source order.
 // Sources go in blocks of four under a group-uniform guard (every lane of the row is active
 // inside it): the block's four LDS loads issue together and complete under one wait, then
-// each source costs three fp64 operations, a compare and a branch-free select.  Sources past
+// each source costs a subtract, a fused multiply-add, a compare, a min and one select.  Sources past
 // prevK in the last block need no guard: lanes i >= prevK hold cj = +inf (every layer sets
 // cost +inf past its KB), and +inf (or NaN from the unstaged LDS they read) never wins.
 template <int I>
 __device__ __forceinline__ void vit_src(double& best, int& arg, double cj, double rm, double gcl, double inv_beta) {
-  const double c = row_bcast<I>(cj) + fabs(rm - gcl) * inv_beta;
+  // fma(|route_m - gc|, 1/beta, cost of source i): one rounding, as the oracle's fma; an
+  // invalid route is +inf and stays +inf
+  const double c = __builtin_fma(fabs(rm - gcl), inv_beta, row_bcast<I>(cj));
   const bool take = c < best;
-  best = take ? c : best;
+  best = __builtin_fmin(best, c);   // = c exactly when take (no NaN reaches here, costs >= 0)
   arg = take ? I : arg;
 }
 template <int B>
