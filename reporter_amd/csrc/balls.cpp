@@ -89,7 +89,7 @@ struct RoadAcc {
 
 uint32_t table_bits(uint64_t keys) {
   uint32_t bits = 1;
-  while ((1ull << bits) < 2 * keys) ++bits;
+  while ((1ull << bits) < kBallSlotsPerRow * keys) ++bits;
   return bits;
 }
 

@@ -2323,7 +2323,7 @@ struct BallSmem {
 
 __device__ __forceinline__ uint32_t table_bits_dev(uint32_t rows) {
   uint32_t bits = 1;
-  while ((1ull << bits) < 2ull * rows) ++bits;
+  while ((1ull << bits) < (unsigned long long)kBallSlotsPerRow * rows) ++bits;
   return bits;
 }
 

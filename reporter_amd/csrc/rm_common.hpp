@@ -207,6 +207,10 @@ RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) { return (v * 2654435761u) >
 #define RM_BALL_GROUP_BITS 10
 #endif
 constexpr uint32_t kBallGroupBits = RM_BALL_GROUP_BITS, kBallGroupLog = RM_BALL_GROUP_LOG;
+#ifndef RM_BALL_SLOTS_PER_ROW
+#define RM_BALL_SLOTS_PER_ROW 2
+#endif
+constexpr uint32_t kBallSlotsPerRow = RM_BALL_SLOTS_PER_ROW;   // table size >= this x rows (load <= 1/this)
 RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) {
   if (bits < kBallGroupBits) return (v * 2654435761u) >> (32u - bits);
   return ((((v >> kBallGroupLog) * 2654435761u) >> (32u + kBallGroupLog - bits)) << kBallGroupLog) |
