@@ -9,7 +9,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("REPORTER_MATCH_LIB", os.path.join(_HERE, "libreporter_match.so"))
+LIB_PATH = os.environ.get("REPORTER_MATCH_LIB") or os.path.join(_HERE, "libreporter_match.so")
 
 _lock = threading.Lock()
 _lib = None
