@@ -93,7 +93,9 @@ def cpu_baseline_leg(graph_path, tr, search_radius, procs):
     import meili_oracle as mo
     from reporter_amd import graphfile
     from reporter_amd.dist import split
-    _CPU.update(graph=graphfile.load(graph_path), traces=tr, radius=search_radius)
+    # the engine's K1 grid (each file cell split f x f): same results, the item counts it reads
+    g = graphfile.split_grid(graphfile.load(graph_path), graphfile.engine_grid_split(graph_path))
+    _CPU.update(graph=g, traces=tr, radius=search_radius)
     mo.lib()  # load once in the parent; children inherit it
     T = len(tr["trace_off"]) - 1
     blocks = [(b[0], b[-1] + 1) for b in split(list(range(T)), procs) if len(b)]
@@ -336,10 +338,12 @@ def main():
         k2["traffic"] = traffic
         k2["traffic_source"] = traffic_note
         k2.update({"search_equivalent_bytes_per_launch": mo.routes_algorithmic_bytes(counts) if counts else None,
-                   "counts": counts, "route_tiers": tiers, "route_balls": balls})
+                   "counts": counts, "route_tiers": tiers, "route_balls": balls, "k1_grid_split": eng.grid_split()})
         rooflines = {
             "K1": roofline("K1", "k_candidates_lane + k_candidates_wave", mo.candidates_algorithmic_bytes(counts)
-                           if counts else None, ms["candidates"], "cell-major 32 B records, per-road minima in registers"),
+                           if counts else None, ms["candidates"], "cell-major 32 B records on the engine grid (file cells split "
+                           "%dx%d; items counted by the oracle on that grid), per-road minima in registers"
+                           % (eng.grid_split(), eng.grid_split())),
             "K2": {k: k2[k] for k in ("kernel", "achieved", "frac", "algorithmic_bytes_per_launch", "avg_launch_ms")},
             "K3": roofline("K3", "k_viterbi", mo.viterbi_algorithmic_bytes(counts) if counts else None, ms["viterbi"],
                            "u32 routes + f32 emissions, fp64 costs in registers"),

@@ -126,6 +126,12 @@ int rm_graph_auto_ball_radius(const char* graph_path, double* radius_m);
 /* out[6]: radius m, keys stored, table entries (16 B each), nodes without a table, build ms,
  * 1 when the tables were built on the GPU (small balls on large graphs; env RM_BALL_BUILD=host|gpu) */
 int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]);
+/* K1's spatial index: the graph file's grid with each cell split f x f (*f = 1: the file's grid),
+ * chosen at upload to minimise the items a default-radius query reads (RM_GRID_SPLIT overrides).
+ * It changes which grid items are read, never which roads are found. */
+int rm_engine_grid_split(const rm_engine* e, uint32_t* f);
+/* Host-only: the grid refinement an engine would choose for a graph file. */
+int rm_graph_grid_split(const char* graph_path, uint32_t* f);
 /* The engine's own tables of `mode` (built by a run that used the mode), probed on the device as
  * K2 probes them: keys[2i], keys[2i+1] from node from[i] to road[i]'s node0 / node1, all-ones
  * outside the ball or for a node without a table.  Compare with rm_balls_lookup (host build). */

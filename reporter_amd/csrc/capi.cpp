@@ -611,12 +611,23 @@ int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]) {
   });
 }
 
+int rm_engine_grid_split(const rm_engine* e, uint32_t* f) {
+  return guarded([&] { *f = e->e->grid_split(); });
+}
+
 int rm_engine_ball_lookup(rm_engine* e, int mode, uint64_t n, const uint32_t* from, const uint32_t* road,
                           uint64_t* keys) {
   return guarded([&] {
     if (!e) throw std::runtime_error("engine is NULL");
     if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
     e->e->ball_lookup(mode, n, from, road, keys);
+  });
+}
+
+int rm_graph_grid_split(const char* graph_path, uint32_t* f) {
+  return guarded([&] {
+    if (!f) throw std::runtime_error("f is NULL");
+    *f = choose_grid_split(Graph::load(graph_path));
   });
 }
 

@@ -269,6 +269,10 @@ __device__ __forceinline__ void put_cand(const DevGraph& g, const DevBatch& b, u
 // (both shape vertices + road + access bits), so a test is two dwordx4 loads with no
 // dependent lookup.  Per-road minima live in 16 registers; a state with more roads
 // inside its radius is queued for the wave tier (k_candidates_wave).
+#ifndef RM_K1_ROWS
+#define RM_K1_ROWS 4
+#endif
+constexpr int kK1Rows = RM_K1_ROWS;   // grid rows whose items K1 walks as one sequence
 __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
@@ -298,22 +302,43 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
     const uint32_t x0 = fx0 < 0 ? 0u : (uint32_t)fx0, y0 = fy0 < 0 ? 0u : (uint32_t)fy0;
     const uint32_t x1 = fx1 > (double)(g.ncx - 1) ? g.ncx - 1 : (uint32_t)fx1;
     const uint32_t y1 = fy1 > (double)(g.ncy - 1) ? g.ncy - 1 : (uint32_t)fy1;
-    // the items of cells x0..x1 of one grid row are one contiguous range (cell-major CSR);
-    // they are read four records at a time with clamped, branch-free loads so the loads
-    // of a batch overlap instead of paying one round trip per item
-    for (uint32_t cy = y0; cy <= y1 && !ovf; ++cy) {
-      const uint32_t lo = g.cell_off[cy * g.ncx + x0], hi = g.cell_off[cy * g.ncx + x1 + 1];
-      for (uint32_t it0 = lo; it0 < hi && !ovf; it0 += 4) {
+    // the items of cells x0..x1 of one grid row are one contiguous range (cell-major CSR).
+    // Rows go kK1Rows at a time: the window's row ranges are read at once and its rows' items
+    // are walked as ONE sequence, four records per batch across row boundaries (clamped,
+    // branch-free loads, so the loads of a batch overlap instead of paying one round trip per
+    // item or per row)
+    for (uint32_t w0 = y0; w0 <= y1 && !ovf; w0 += kK1Rows) {
+      const uint32_t nrow = min(y1 - w0 + 1u, (uint32_t)kK1Rows);
+      uint32_t ra[kK1Rows], re[kK1Rows], base[kK1Rows], end[kK1Rows];
+#pragma unroll
+      for (int r = 0; r < kK1Rows; ++r) {
+        const uint32_t cy = w0 + min((uint32_t)r, nrow - 1u);
+        ra[r] = g.cell_off[cy * g.ncx + x0];
+        re[r] = g.cell_off[cy * g.ncx + x1 + 1];
+      }
+      uint32_t tot = 0;
+#pragma unroll
+      for (int r = 0; r < kK1Rows; ++r) {
+        base[r] = ra[r] - tot;   // item of sequence index q in row r: base[r] + q
+        tot += (uint32_t)r < nrow ? re[r] - ra[r] : 0u;
+        end[r] = tot;
+      }
+      for (uint32_t q0 = 0; q0 < tot && !ovf; q0 += 4) {
         uint4 r0[4], r1[4];
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
-          const uint64_t it = min(it0 + y, hi - 1u);
+          const uint32_t q = min(q0 + (uint32_t)y, tot - 1u);
+          uint32_t bq = base[0];
+#pragma unroll
+          for (int r = 1; r < kK1Rows; ++r)
+            if (q >= end[r - 1]) bq = base[r];
+          const uint64_t it = bq + q;
           r0[y] = g.cell_rec[2 * it];
           r1[y] = g.cell_rec[2 * it + 1];
         }
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
-          if (it0 + y >= hi || ovf) break;
+          if (q0 + y >= tot || ovf) break;
           if (!((r1[y].z >> 29) & acc)) continue;
           float sq; uint32_t sc;
           project(as_f(r0[y].x), as_f(r0[y].y), r1[y].x, as_f(r0[y].z), as_f(r0[y].w), r1[y].y, lon, lat, mlon, mlat,
@@ -2759,6 +2784,64 @@ T* upload(std::vector<void*>& list, const std::vector<T>& v) {
 // ==========================================================================================
 // Engine
 
+// K1 reads every item listed in every grid cell its query box touches, so the engine may index
+// the shape pieces on a finer grid than the graph file's: each cell split f x f.  Which roads
+// a query finds never depends on it (a piece within the radius overlaps the box, so it is
+// listed in a touched cell at any resolution); only how many items it reads does.  f in 1..4
+// minimises, over 2,048 default-radius (50 m) queries centred on sampled shape pieces, the
+// items read + 2 per touched cell row (a row costs two dependent offset loads).
+// RM_GRID_SPLIT=f overrides.  C2/C3/C4 worlds: f = 2 (C2 19.4 -> 13.2 items per state, C4-like
+// 11.9 -> 6.1; 3 and 4 list long pieces in too many cells).
+uint32_t choose_grid_split(const Graph& g) {
+  if (const char* e = std::getenv("RM_GRID_SPLIT")) return (uint32_t)std::min(8, std::max(1, std::atoi(e)));
+  const GridIndex& gi = g.grid;
+  const size_t n = gi.cell_item.size();
+  if (n == 0) return 1;
+  constexpr int kQ = 2048, kMaxF = 4;
+  double cost[kMaxF + 1] = {};
+  auto cell = [](double x, double x0, double d) { return (int64_t)std::floor((x - x0) / d); };
+  std::vector<uint32_t> items;
+  for (int q = 0; q < kQ; ++q) {
+    const uint32_t v = gi.cell_item[(size_t)((double)q * (double)n / kQ)];
+    const VertRec& A = g.verts[v];
+    const VertRec& B = g.verts[v + 1];
+    const float lon = 0.5f * (A.lon + B.lon), lat = 0.5f * (A.lat + B.lat);
+    const float pad = 50.f * 1.01f + 0.5f;   // K1's padded box for the default radius
+    const float qlon = pad / meters_per_lon(lat), qlat = pad / (float)kMetersPerDegLat;
+    const double b0 = (double)(lon - qlon), b1 = (double)(lon + qlon), c0 = (double)(lat - qlat), c1 = (double)(lat + qlat);
+    // distinct items of the graph-grid cells the box touches: a superset of any finer grid's
+    const int64_t x0 = std::max<int64_t>(0, cell(b0, gi.lon0, gi.dlon)), x1 = std::min<int64_t>(gi.ncx - 1, cell(b1, gi.lon0, gi.dlon));
+    const int64_t y0 = std::max<int64_t>(0, cell(c0, gi.lat0, gi.dlat)), y1 = std::min<int64_t>(gi.ncy - 1, cell(c1, gi.lat0, gi.dlat));
+    if (x0 > x1 || y0 > y1) continue;
+    items.clear();
+    for (int64_t y = y0; y <= y1; ++y)
+      for (uint32_t it = gi.cell_off[y * gi.ncx + x0]; it < gi.cell_off[y * gi.ncx + x1 + 1]; ++it) items.push_back(gi.cell_item[it]);
+    std::sort(items.begin(), items.end());
+    items.erase(std::unique(items.begin(), items.end()), items.end());
+    for (int f = 1; f <= kMaxF; ++f) {
+      if ((uint64_t)gi.ncx * f * gi.ncy * f > 400000000ull) break;
+      const double dl = gi.dlon / f, dt = gi.dlat / f;
+      const int64_t X = (int64_t)gi.ncx * f, Y = (int64_t)gi.ncy * f;
+      const int64_t qx0 = std::max<int64_t>(0, cell(b0, gi.lon0, dl)), qx1 = std::min<int64_t>(X - 1, cell(b1, gi.lon0, dl));
+      const int64_t qy0 = std::max<int64_t>(0, cell(c0, gi.lat0, dt)), qy1 = std::min<int64_t>(Y - 1, cell(c1, gi.lat0, dt));
+      double cnt = 0;
+      for (uint32_t u : items) {
+        const VertRec& P = g.verts[u];
+        const VertRec& Q = g.verts[u + 1];
+        const int64_t ix0 = cell(std::min(P.lon, Q.lon), gi.lon0, dl), ix1 = std::min(X - 1, cell(std::max(P.lon, Q.lon), gi.lon0, dl));
+        const int64_t iy0 = cell(std::min(P.lat, Q.lat), gi.lat0, dt), iy1 = std::min(Y - 1, cell(std::max(P.lat, Q.lat), gi.lat0, dt));
+        const int64_t ox = std::min(ix1, qx1) - std::max(ix0, qx0) + 1, oy = std::min(iy1, qy1) - std::max(iy0, qy0) + 1;
+        if (ox > 0 && oy > 0) cnt += (double)(ox * oy);
+      }
+      cost[f] += cnt + 2.0 * (double)(qy1 - qy0 + 1);
+    }
+  }
+  uint32_t best = 1;
+  for (int f = 2; f <= kMaxF; ++f)
+    if (cost[f] > 0 && cost[f] < 0.97 * cost[best]) best = (uint32_t)f;
+  return best;
+}
+
 Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   RM_HIP(hipSetDevice(device));
   ball_radius_cm_ = auto_ball_radius_cm(g);
@@ -2804,15 +2887,25 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   dg_.verts = (const uint4*)upload(allocs_, g.verts);
   dg_.seg_id = (const unsigned long long*)upload(allocs_, g.seg_id);
   dg_.seg_len = upload(allocs_, g.seg_len_cm);
-  dg_.cell_off = upload(allocs_, g.grid.cell_off);
-  dg_.cell_item = upload(allocs_, g.grid.cell_item);
+  // K1's grid: the graph's own, or each of its cells split f x f (choose_grid_split)
+  GridIndex split;
+  grid_split_ = choose_grid_split(g);
+  if (grid_split_ > 1) {
+    split.lon0 = g.grid.lon0; split.lat0 = g.grid.lat0;
+    split.dlon = g.grid.dlon / grid_split_; split.dlat = g.grid.dlat / grid_split_;
+    split.ncx = g.grid.ncx * grid_split_; split.ncy = g.grid.ncy * grid_split_;
+    build_grid_index(g.verts, split);
+  }
+  const GridIndex& gk = grid_split_ > 1 ? split : g.grid;
+  dg_.cell_off = upload(allocs_, gk.cell_off);
+  dg_.cell_item = nullptr;   // K1 reads the self-contained records below
   {
     // K1 reads cell items as self-contained records (no item -> vertex -> road chain)
     if (g.num_roads() >= (1u << 29)) throw std::runtime_error("graph has too many roads (limit 2^29)");
     auto acc_of = [&](uint32_t e) { return e == kNone ? 0u : edge_access(g.edges[e].info); };
-    std::vector<uint32_t> rec(8 * (size_t)g.grid.cell_item.size());
-    for (size_t it = 0; it < g.grid.cell_item.size(); ++it) {
-      const uint32_t v = g.grid.cell_item[it];
+    std::vector<uint32_t> rec(8 * (size_t)gk.cell_item.size());
+    for (size_t it = 0; it < gk.cell_item.size(); ++it) {
+      const uint32_t v = gk.cell_item[it];
       const VertRec& A = g.verts[v];
       const VertRec& B = g.verts[v + 1];
       const uint32_t road = A.road;
@@ -2857,8 +2950,8 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
       dg_.relax[mode] = (const uint4*)upload(allocs_, rel);
     }
   }
-  dg_.lon0 = g.grid.lon0; dg_.lat0 = g.grid.lat0; dg_.dlon = g.grid.dlon; dg_.dlat = g.grid.dlat;
-  dg_.ncx = g.grid.ncx; dg_.ncy = g.grid.ncy;
+  dg_.lon0 = gk.lon0; dg_.lat0 = gk.lat0; dg_.dlon = gk.dlon; dg_.dlat = gk.dlat;
+  dg_.ncx = gk.ncx; dg_.ncy = gk.ncy;
   dg_.n_nodes = g.num_nodes(); dg_.n_edges = g.num_edges(); dg_.n_segments = g.num_segments();
   if (g.num_nodes()) {
     hipLaunchKernelGGL(k_fill_edge_src, dim3((g.num_nodes() + 255) / 256), dim3(256), 0, 0, dg_.node_off,

@@ -299,6 +299,9 @@ class Matcher {
   uint64_t klaunch_[kNumKernels] = {0};
 };
 
+// K1's grid refinement for a graph (host only; engine.hip): each graph-file cell split f x f
+uint32_t choose_grid_split(const Graph& g);
+
 class Engine {
  public:
   Engine(const Graph& g, int device);
@@ -323,6 +326,8 @@ class Engine {
   // keys[2i], keys[2i+1] from node from[i] to road[i]'s node0 / node1 through the built tables
   // of `mode`, probed on the device as K2 does (all-ones: outside the ball / no table)
   void ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys);
+  // K1's grid: each cell of the graph's grid split f x f (1 = the graph's grid)
+  uint32_t grid_split() const { return grid_split_; }
 
  private:
   int device_;
@@ -333,6 +338,7 @@ class Engine {
   uint32_t ball_radius_cm_ = 40000;   // set from auto_ball_radius_cm(graph) at construction
   uint32_t ball_built_ = 0;             // mode bits
   uint32_t ball_gpu_ = 0;               // mode bits built on the GPU
+  uint32_t grid_split_ = 1;
   bool build_balls_gpu(int mode, uint32_t max_keys);
   double ball_info_[5][4] = {};
 };

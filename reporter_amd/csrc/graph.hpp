@@ -83,6 +83,9 @@ struct RoadInput {
 void assemble_roads(Graph& g, const std::vector<RoadInput>& roads);
 // cell_off / cell_item of g.grid from its origin, cell size and dimensions
 void build_grid_index(Graph& g);
+// (re)build the cell -> shape piece CSR of `gi` (origin, cell size and extent already set):
+// every piece is listed in each cell its lon/lat bounding box overlaps
+void build_grid_index(const std::vector<VertRec>& verts, GridIndex& gi);
 // length of a straight shape piece, metres (equirectangular at its mean latitude)
 double piece_m(float lon0, float lat0, float lon1, float lat1);
 

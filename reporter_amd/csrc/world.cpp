@@ -129,8 +129,9 @@ void assemble_roads(Graph& g, const std::vector<RoadInput>& roads) {
   g.edge_seg_off.assign(E, 0);
 }
 
-void build_grid_index(Graph& g) {
-  GridIndex& gi = g.grid;
+void build_grid_index(Graph& g) { build_grid_index(g.verts, g.grid); }
+
+void build_grid_index(const std::vector<VertRec>& verts, GridIndex& gi) {
   const size_t ncell = (size_t)gi.ncx * gi.ncy;
   if (ncell > 400000000ull) throw std::runtime_error("grid index too large; raise cell_m");
   std::vector<uint32_t> cnt(ncell + 1, 0);
@@ -148,10 +149,10 @@ void build_grid_index(Graph& g) {
       gi.cell_item.resize(gi.cell_off[ncell]);
       std::fill(cnt.begin(), cnt.end(), 0);
     }
-    for (uint32_t v = 0; v + 1 < (uint32_t)g.verts.size(); ++v) {
-      if (g.verts[v].road == kNone) continue;
+    for (uint32_t v = 0; v + 1 < (uint32_t)verts.size(); ++v) {
+      if (verts[v].road == kNone) continue;
       uint32_t x0, x1, y0, y1;
-      cell_range(g.verts[v], g.verts[v + 1], x0, x1, y0, y1);
+      cell_range(verts[v], verts[v + 1], x0, x1, y0, y1);
       for (uint32_t y = y0; y <= y1; ++y)
         for (uint32_t x = x0; x <= x1; ++x) {
           const size_t c = (size_t)y * gi.ncx + x;

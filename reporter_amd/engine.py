@@ -88,6 +88,12 @@ class Engine:
         d["built_on_gpu"] = bool(out[5])
         return d
 
+    def grid_split(self):
+        """K1 grid refinement f (each graph-file cell split f x f)."""
+        out = np.zeros(1, np.uint32)
+        _lib.check(_lib.lib().rm_engine_grid_split(self._h, out.ctypes.data))
+        return int(out[0])
+
     def ball_lookup(self, mode, from_nodes, roads):
         """Keys (n, 2) from each node to the two endpoints of each road through the engine's
         device tables of `mode` (all-ones outside the ball / without a table)."""

@@ -1,0 +1,43 @@
+"""K1's split grid (engine.hip choose_grid_split / Engine::Engine; numpy mirror
+graphfile.split_grid): the same bounding-box rule as the graph builder, and the oracle finds
+exactly the same candidates (and everything downstream) on it while reading fewer items.
+CPU only."""
+import sys
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def test_split_rule_matches_builder(built_lib, tmp_path):
+    from reporter_amd import graphfile, world
+    gp = str(tmp_path / "g.rmg")
+    world.build_world(gp, 30, 30, 100.0, seed=4)
+    g = graphfile.load(gp)
+    r = graphfile.split_grid(g, 1, rebuild=True)
+    assert np.array_equal(r["cell_off"], g["cell_off"])
+    assert np.array_equal(r["cell_item"], g["cell_item"])
+
+
+def test_oracle_identical_on_split_grid(built_lib, tmp_path):
+    import meili_oracle as mo
+    from reporter_amd import engine, graphfile, world
+    gp = str(tmp_path / "g.rmg")
+    world.build_world(gp, 40, 40, 100.0, seed=1)
+    g = graphfile.load(gp)
+    tr = world.generate_traces(gp, 40, 300, 1.0, 5.0, seed=3)
+    T = len(tr["trace_off"]) - 1
+    opts = engine.default_options(1)
+    out = []
+    for f in (1, 2, 3):
+        mo.reset_counters()
+        res = mo.match(graphfile.split_grid(g, f), mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"],
+                                                          tr["accuracy"], opts, np.zeros(T, np.uint32)))
+        out.append((res, mo.counters()["cand_items"]))
+    for res, _ in out[1:]:
+        for k, v in out[0][0].items():
+            if isinstance(v, np.ndarray):
+                assert np.array_equal(v, res[k]), k
+    assert out[1][1] < 0.8 * out[0][1]   # f = 2 reads fewer grid items on a 100 m-block grid
