@@ -767,9 +767,23 @@ __device__ __forceinline__ unsigned long long h_label(const SearchSmem<H, PATH>&
   return h < 0 ? kKeyInf : sm.lab[h];
 }
 
+// Frontier compaction: the active lanes of one wave instruction reserve their slots with ONE
+// atomic by the lowest active lane (ballot -> popcount), which broadcasts the base by shuffle;
+// each lane's slot is base + the number of active lanes below it.  Callable in divergent code.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter) {
+  const unsigned long long m = __ballot(1);
+  const int lane = (int)(threadIdx.x & (kWave - 1));
+  const int leader = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = (uint32_t)__shfl((int)base, leader, kWave);
+  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
 // Exact lexicographic shortest (dist, time) keys from the exits of n_src source
 // candidates (descriptors src[0..n_src), source ids 0..n_src-1) to every node within
-// `bound` cm, by synchronous label-correcting rounds over an LDS frontier.  All 64 lanes call it.
+// `bound` cm, by synchronous label-correcting rounds over an LDS frontier compacted by ballot
+// (wave_append).  All 64 lanes call it.
 // With src == nullptr the single root is node `root` at key 0 (route-ball build).
 template <int H, bool PATH>
 __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int mode, uint32_t bound,
@@ -800,7 +814,7 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
       const int slot = h_insert(sm, (i << 28) | node);
       if (slot >= 0) {
         const unsigned long long old = atomicMin(&sm.lab[slot], kk);
-        if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[atomicAdd(&sm.nf, 1u)] = (typename SearchSmem<H, PATH>::FIdx)slot;
+        if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[wave_append(&sm.nf)] = (typename SearchSmem<H, PATH>::FIdx)slot;
       }
     }
   }
@@ -827,7 +841,7 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
         const int t = h_insert(sm, srcbits | rec.x);
         if (t < 0) continue;
         const unsigned long long old = atomicMin(&sm.lab[t], nk);
-        if (nk < old && atomicExch(&sm.inq[t], 1u) == 0u) nxt[atomicAdd(&sm.nn, 1u)] = (typename SearchSmem<H, PATH>::FIdx)t;
+        if (nk < old && atomicExch(&sm.inq[t], 1u) == 0u) nxt[wave_append(&sm.nn)] = (typename SearchSmem<H, PATH>::FIdx)t;
       }
     }
     __syncthreads();
