@@ -46,6 +46,11 @@ def parse():
     ap.add_argument("--config", default="C2", help="C1..C5 (BASELINE.json configs); C2 is the metric's workload")
     ap.add_argument("--traces", type=int, default=0, help="override traces per rank")
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (default min(16, cpus))")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="the batch runs as this many concurrent parts, one HIP stream each (1 = one stream)")
+    ap.add_argument("--parts-extra", type=int, default=2,
+                    help="also time the batch as this many concurrent parts (engine.MultiMatcher), reported "
+                         "beside the value as concurrent_parts (0 = skip; batches <= 20 M points)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C1 latency and JSON-boundary lines")
     ap.add_argument("--json-traces", type=int, default=10000, help="traces sent through rm_match_batch as JSON")
@@ -136,16 +141,23 @@ def shard_ids(config, n_per_rank, n_points, world, rank):
     return dist.shard_by_uuid(uuids, np.full(total, n_points), world)[rank].astype(np.uint32)
 
 
+LAUNCHES = 1   # launches of each stage per step (one per concurrent part of the batch)
+
+
 def roofline(name, kernels, abytes, ms, formulation):
+    """abytes / ms: the step's algorithmic bytes and summed launch time of the stage; reported
+    per launch (each part's launch does its share of the bytes, timed on its own stream)."""
+    abytes = abytes / LAUNCHES if abytes else abytes
+    ms = ms / LAUNCHES if ms else ms
     if not abytes or not ms:
         return {"kernel": kernels, "formulation": formulation, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": None, "traffic": None, "algorithmic_bytes_per_launch": abytes,
-                "avg_launch_ms": ms}
+                "avg_launch_ms": ms, "launches_per_step": LAUNCHES}
     achieved = abytes / (ms * 1e-3) / 1e9
     return {"kernel": kernels, "formulation": formulation, "bound": "hbm", "achieved": achieved,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "frac_vs_measured_copy": achieved / HBM_MEASURED_GBS, "traffic": None,
-            "algorithmic_bytes_per_launch": abytes, "avg_launch_ms": ms}
+            "algorithmic_bytes_per_launch": abytes, "avg_launch_ms": ms, "launches_per_step": LAUNCHES}
 
 
 def timed(fn, steps, comm, sync):
@@ -273,7 +285,10 @@ def main():
     radius = a.ball_radius if a.ball_radius is not None else cfg.get("ball_radius_m")
     if radius is not None:
         eng.set_ball_radius(radius)   # else the engine's automatic radius (balls.hpp auto_ball_radius_cm)
-    bm = engine.BatchMatcher(eng)
+    global LAUNCHES
+    LAUNCHES = max(1, a.streams)
+    # the batch as `streams` concurrent parts (engine.MultiMatcher: one HIP stream each), or one
+    bm = engine.MultiMatcher(eng, a.streams) if a.streams > 1 else engine.BatchMatcher(eng)
     nseg = eng.n_segments
     hist = dist.DeviceBuffer(nseg * 16 * 4)
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
@@ -294,13 +309,39 @@ def main():
 
     for _ in range(a.warmup):
         step()
-    bm.set_timing(True)
+    # the official step (match + all-reduce), with the roofline kernel's stage (K2) timed live by
+    # HIP events on each part's stream; an event record per stage would perturb the concurrent parts
+    bm.set_timing_stages(("routes",))
     bm.reset_times()
-    elapsed = timed(step, a.steps, comm, sync)               # the official step: match + all-reduce
-    kt = bm.kernel_times()
+    elapsed = timed(step, a.steps, comm, sync)
+    kt_live = bm.kernel_times()
     bm.set_timing(False)
     t_ar = timed(allreduce, a.steps, comm, sync)             # the all-reduce alone, reported alongside
     t_match = timed(lambda: bm.rerun(**rp), a.steps, comm, sync)   # matching alone
+    # the same batch as concurrent parts, one HIP stream each (rm_runners_rerun): gather-bound
+    # stages of one part overlap issue-bound stages of another; reported beside the value (the
+    # parts share the GPU, so their per-launch K2 roofline is not the kernel's)
+    conc = None
+    if a.parts_extra > 1 and a.streams == 1 and P <= 20_000_000:
+        mm = engine.MultiMatcher(eng, a.parts_extra)
+        mm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, None, **rp)
+        for _ in range(a.warmup):
+            mm.rerun(**rp)
+            allreduce()
+        t_conc = timed(lambda: (mm.rerun(**rp), allreduce()), a.steps, comm, sync)
+        conc = {"parts": len(mm.bms), "streams": len(mm.bms), "ms_per_step": t_conc / max(a.steps, 1) * 1e3,
+                "value_points_per_s": (comm.allreduce_host(P, dist.SUM) if comm is not None else P) * a.steps / t_conc,
+                "what": "the same step (match + all-reduce) with the batch split into contiguous trace ranges "
+                        "balanced by points, run concurrently on their own HIP streams (engine.MultiMatcher / "
+                        "rm_runners_rerun); bit-identical results (tests/test_gpu_multistream.py)"}
+        mm.close()
+    # per-stage breakdown (the other rooflines): a separate pass with every stage timed
+    bm.set_timing(True)
+    bm.reset_times()
+    t_staged = timed(lambda: bm.rerun(**rp), a.steps, comm, sync)
+    kt = bm.kernel_times()
+    bm.set_timing(False)
+    kt["routes"] = kt_live["routes"]
     total_points = comm.allreduce_host(P, dist.SUM) if comm is not None else P
     sizes = bm.sizes()
     hist_sum = int(hist.download().sum())
@@ -328,7 +369,8 @@ def main():
             try:
                 with open(a.traffic_json) as f:
                     tj = json.load(f)
-                if tj.get("config") == a.config and tj.get("traces") == n_per and tj.get("engine_sha") == engine_sha():
+                if (tj.get("config") == a.config and tj.get("traces") == n_per and tj.get("engine_sha") == engine_sha()
+                        and tj.get("streams", 1) == max(1, a.streams)):
                     traffic = tj.get("hbm_bytes_per_launch")
                     traffic_note = ("%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this engine.hip (sha %s), "
                                     "read side x%s per MI355X_MICROARCH.md" % (
@@ -375,7 +417,8 @@ def main():
                 "points_all_ranks": int(total_points),
                 "graph": W.graph_info(gpath),
                 "parallelism": "uuid shard x%d (dist.shard_by_uuid), graph replicated, RCCL all-reduce of %d x 16 u32 "
-                               "speed histogram every step" % (world, nseg),
+                               "speed histogram every step; per GPU the batch runs as %d concurrent part(s), one HIP "
+                               "stream each" % (world, nseg, max(1, a.streams)),
             },
             "ms_allreduce": t_ar / steps * 1e3,
             "allreduce_bytes": nseg * 16 * 4,
@@ -389,7 +432,11 @@ def main():
                            max(0.0, 3600.0 - build_ms * 1e-3) / 3600.0,
                            "note": "the route balls are built once per graph and travel mode (host, at rm_configure); "
                                    "they are outside the timed step"},
+            "concurrent_parts": conc,
             "kernels_ms_per_step": ms,
+            "kernels_ms_note": ("summed launch ms of each stage per step over the %d part(s); routes timed live in the "
+                                "official step, the other stages in a separate pass with every stage timed (%.3f ms "
+                                "per step)" % (max(1, a.streams), t_staged / steps * 1e3)),
             "sizes_rank0": sizes,
             "histogram_total": hist_sum,
         }

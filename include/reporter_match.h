@@ -173,6 +173,10 @@ void rm_default_run_params(rm_run_params* p);
 int rm_runner_run(rm_runner* r, const rm_batch_desc* b, const rm_run_params* p);
 /* run again over the batch already resident in HBM (bench steps) */
 int rm_runner_rerun(rm_runner* r, const rm_run_params* p);
+/* rerun n runners (contiguous parts of one batch, same engine) concurrently, one host thread
+ * per part, so their kernels overlap on their streams; with zero_hist the shared histogram is
+ * zeroed once before any part reports.  Returns the first part's error. */
+int rm_runners_rerun(rm_runner* const* rs, uint32_t n, const rm_run_params* p);
 /* out: [0] points [1] traces [2] transitions [3] path edges [4] segments [5] reports
  *      [6] route pairs sent to the wave tier [7] ... to the single-source tier
  *      [8] transitions sent to the path wave tier [9] states sent to the candidate wave tier */
@@ -202,6 +206,8 @@ int rm_runner_set_isolation(rm_runner* r, int on);
 int rm_runner_trace_errors(rm_runner* r, uint32_t* errs);   /* n_traces words of the last run */
 /* per-kernel HIP-event timing on the runner's stream */
 int rm_runner_set_timing(rm_runner* r, int on);
+/* time only the stages whose bit is set (bit k = rm_kernel_name(k)): fewer event records in a timed region */
+int rm_runner_set_timing_mask(rm_runner* r, uint32_t mask);
 int rm_runner_kernel_times(rm_runner* r, double* ms, uint64_t* launches, int n);
 int rm_runner_reset_times(rm_runner* r);
 const char* rm_kernel_name(int k);

@@ -105,6 +105,7 @@ PROTOTYPES = [
     ("rm_default_run_params", None, [C.POINTER(RmRunParams)]),
     ("rm_runner_run", C.c_int, [P, C.POINTER(RmBatchDesc), C.POINTER(RmRunParams)]),
     ("rm_runner_rerun", C.c_int, [P, C.POINTER(RmRunParams)]),
+    ("rm_runners_rerun", C.c_int, [P, C.c_uint32, C.POINTER(RmRunParams)]),
     ("rm_runner_sizes", C.c_int, [P, C.POINTER(C.c_uint64)]),
     ("rm_runner_get_states", C.c_int, [P, P, P]),
     ("rm_runner_get_candidates", C.c_int, [P, P, P, P, P]),
@@ -114,6 +115,7 @@ PROTOTYPES = [
     ("rm_runner_get_segments", C.c_int, [P, P, P]),
     ("rm_runner_get_reports", C.c_int, [P, P, P, P]),
     ("rm_runner_set_timing", C.c_int, [P, C.c_int]),
+    ("rm_runner_set_timing_mask", C.c_int, [P, C.c_uint32]),
     ("rm_runner_set_isolation", C.c_int, [P, C.c_int]),
     ("rm_runner_trace_errors", C.c_int, [P, P]),
     ("rm_report_segments", C.c_int, [C.POINTER(RmReportDesc), P, P, P]),

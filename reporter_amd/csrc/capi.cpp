@@ -700,6 +700,35 @@ int rm_runner_run(rm_runner* r, const rm_batch_desc* b, const rm_run_params* p) 
   });
 }
 int rm_runner_rerun(rm_runner* r, const rm_run_params* p) { return guarded([&] { r->m->run_device(to_rp(p)); }); }
+
+int rm_runners_rerun(rm_runner* const* rs, uint32_t n, const rm_run_params* p) {
+  return guarded([&] {
+    if (!rs || n == 0) throw std::runtime_error("no runners");
+    for (uint32_t i = 0; i < n; ++i)
+      if (!rs[i]) throw std::runtime_error("runner is NULL");
+    RunParams rp = to_rp(p);
+    if (rp.hist && rp.zero_hist && rp.do_report) {
+      // the parts add into one histogram: zero it once before any part reports
+      hipStream_t st = rs[0]->m->stream();
+      RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)rs[0]->m->engine().n_segments() * kHistBins * sizeof(uint32_t), st));
+      RM_HIP(hipStreamSynchronize(st));
+    }
+    rp.zero_hist = false;
+    // one host thread per part: each part's read-backs block only its own thread, so the parts'
+    // kernels run concurrently on their streams
+    std::vector<std::exception_ptr> err(n);
+    std::vector<std::thread> th;
+    th.reserve(n - 1);
+    for (uint32_t i = 1; i < n; ++i)
+      th.emplace_back([&, i] {
+        try { rs[i]->m->run_device(rp); } catch (...) { err[i] = std::current_exception(); }
+      });
+    try { rs[0]->m->run_device(rp); } catch (...) { err[0] = std::current_exception(); }
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+      if (e) std::rethrow_exception(e);
+  });
+}
 int rm_runner_sizes(rm_runner* r, uint64_t out[10]) {
   return guarded([&] {
     out[0] = r->m->n_points(); out[1] = r->m->n_traces(); out[2] = r->m->n_trans(); out[3] = r->m->n_path_edges();
@@ -732,6 +761,7 @@ int rm_runner_get_reports(rm_runner* r, uint32_t* off, void* reps, void* stats) 
   return guarded([&] { r->m->get_reports(off, (ReportRec*)reps, (ReportStats*)stats); });
 }
 int rm_runner_set_timing(rm_runner* r, int on) { return guarded([&] { r->m->set_timing(on != 0); }); }
+int rm_runner_set_timing_mask(rm_runner* r, uint32_t mask) { return guarded([&] { r->m->set_timing_mask(mask); }); }
 int rm_runner_set_isolation(rm_runner* r, int on) { return guarded([&] { r->m->set_isolation(on != 0); }); }
 int rm_runner_trace_errors(rm_runner* r, uint32_t* errs) { return guarded([&] { r->m->get_trace_errors(errs); }); }
 int rm_report_segments(const rm_report_desc* d, uint32_t* rep_off, void* reps, void* stats) {

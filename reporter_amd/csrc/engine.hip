@@ -3221,7 +3221,7 @@ void Matcher::ensure_segs(uint64_t n) {
 }
 
 void Matcher::tic(int k) {
-  if (!timing_) return;
+  if (!((timing_mask_ >> k) & 1u)) return;
   Ev ev;
   if (!free_ev_.empty()) { ev = free_ev_.back(); free_ev_.pop_back(); }
   else { RM_HIP(hipEventCreate(&ev.a)); RM_HIP(hipEventCreate(&ev.b)); }
@@ -3230,8 +3230,7 @@ void Matcher::tic(int k) {
   pending_.push_back(ev);
 }
 void Matcher::toc(int k) {
-  if (!timing_ || pending_.empty()) return;
-  (void)k;
+  if (!((timing_mask_ >> k) & 1u) || pending_.empty()) return;
   RM_HIP(hipEventRecord(pending_.back().b, stream_));
 }
 void Matcher::harvest_times() {

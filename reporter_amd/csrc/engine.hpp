@@ -245,7 +245,8 @@ class Matcher {
   // the kCtlWords control words of the last run (zeros before any run)
   void ctl_words(uint32_t* out);
   void reset_kernel_times();
-  void set_timing(bool on) { timing_ = on; }
+  void set_timing(bool on) { timing_mask_ = on ? ~0u : 0u; }
+  void set_timing_mask(uint32_t mask) { timing_mask_ = mask; }   // bit k: stage k (kernel_name)
   // Failure isolation: off (default), a trace that fails (kErrCandOverflow / kErrSearchOverflow /
   // kErrRounds) makes run() throw; on, run() returns, the failed traces carry no segments or
   // reports and their bits are in get_trace_errors().  The reference fails one request
@@ -254,6 +255,7 @@ class Matcher {
   uint32_t error_bits() const { return err_bits_; }   // OR of the last run's per-trace errors
   void get_trace_errors(uint32_t* out);                // n_traces() words
   hipStream_t stream() const { return stream_; }
+  const Engine& engine() const { return *eng_; }
 
   // Raw point stream -> per-vehicle time sort and inactivity windows of >= 2 points on the
   // GPU (simple_reporter.py:137-164), then every matching stage over the windows.
@@ -283,7 +285,7 @@ class Matcher {
   Workspace ws_;
   uint32_t n_traces_ = 0;
   uint64_t n_points_ = 0, n_trans_ = 0, n_path_ = 0, seg_used_ = 0;
-  bool timing_ = false;
+  uint32_t timing_mask_ = 0;   // stages timed by HIP events
   bool has_report_ = false;
   bool isolate_ = false;
   uint32_t err_bits_ = 0;

@@ -320,6 +320,15 @@ class BatchMatcher:
     def set_timing(self, on=True):
         _lib.check(_lib.lib().rm_runner_set_timing(self._h, 1 if on else 0))
 
+    def set_timing_stages(self, names):
+        """Time only the named stages (rm_kernel_name), e.g. ("routes",)."""
+        n = _lib.lib().rm_num_kernels()
+        idx = {_lib.lib().rm_kernel_name(i).decode(): i for i in range(n)}
+        mask = 0
+        for nm in names:
+            mask |= 1 << idx[nm]
+        _lib.check(_lib.lib().rm_runner_set_timing_mask(self._h, mask))
+
     def reset_times(self):
         _lib.check(_lib.lib().rm_runner_reset_times(self._h))
 
@@ -330,6 +339,90 @@ class BatchMatcher:
         _lib.check(_lib.lib().rm_runner_kernel_times(self._h, ms.ctypes.data, la.ctypes.data, n))
         names = [_lib.lib().rm_kernel_name(i).decode() for i in range(n)]
         return {names[i]: (float(ms[i]), int(la[i])) for i in range(n)}
+
+
+class MultiMatcher:
+    """One batch as `parts` contiguous trace ranges (balanced by points), each on its own
+    BatchMatcher (HIP stream + workspace).  rerun() runs every part at once
+    (rm_runners_rerun: one host thread per part), so one part's gather-latency-bound stages
+    (K2 route probes, the path walk) overlap another part's issue-bound ones (K1, K3).  Every
+    point of the batch is matched once per rerun; a shared histogram is zeroed once."""
+
+    def __init__(self, engine, parts=2):
+        self.engine = engine
+        self.parts = max(1, int(parts))
+        self.bms = []
+
+    def run(self, trace_off, lon, lat, time, accuracy=None, opts=None, trace_opt=None, **rp_kw):
+        trace_off = np.asarray(trace_off, np.uint64)
+        T = len(trace_off) - 1
+        P = int(trace_off[-1])
+        accuracy = np.full(P, -1.0, np.float32) if accuracy is None else np.asarray(accuracy, np.float32)
+        trace_opt = np.zeros(T, np.uint32) if trace_opt is None else np.asarray(trace_opt, np.uint32)
+        # cut where the running point count crosses k * P / parts
+        cuts = [0] + [int(np.searchsorted(trace_off, P * k / self.parts)) for k in range(1, self.parts)] + [T]
+        cuts = sorted(set(min(max(c, 0), T) for c in cuts))
+        for bm in self.bms:
+            bm.close()
+        self.bms = []
+        zero = rp_kw.pop("zero_hist", False)
+        if zero and rp_kw.get("hist_dev"):
+            _lib.check(_lib.lib().rm_device_memset(rp_kw["hist_dev"], 0, self.engine.n_segments * 16 * 4))
+        for t0, t1 in zip(cuts[:-1], cuts[1:]):
+            if t1 <= t0:
+                continue
+            o0, o1 = int(trace_off[t0]), int(trace_off[t1])
+            bm = BatchMatcher(self.engine)
+            bm.run(trace_off[t0:t1 + 1] - o0, lon[o0:o1], lat[o0:o1], time[o0:o1], accuracy[o0:o1], opts,
+                   trace_opt[t0:t1], **rp_kw)
+            self.bms.append(bm)
+        return self
+
+    def rerun(self, **rp_kw):
+        rp = BatchMatcher.run_params(**rp_kw)
+        hs = (C.c_void_p * len(self.bms))(*[bm._h for bm in self.bms])
+        _lib.check(_lib.lib().rm_runners_rerun(hs, len(self.bms), C.byref(rp)))
+
+    def set_timing(self, on=True):
+        for bm in self.bms:
+            bm.set_timing(on)
+
+    def set_timing_stages(self, names):
+        for bm in self.bms:
+            bm.set_timing_stages(names)
+
+    def reset_times(self):
+        for bm in self.bms:
+            bm.reset_times()
+
+    def kernel_times(self):
+        """Per stage: (ms summed over the parts' launches, launches) — each launch timed by HIP
+        events on its own stream while the other parts run."""
+        out = {}
+        for bm in self.bms:
+            for k, (ms, n) in bm.kernel_times().items():
+                a, b = out.get(k, (0.0, 0))
+                out[k] = (a + ms, b + n)
+        return out
+
+    def sizes(self):
+        out = {}
+        for bm in self.bms:
+            for k, v in bm.sizes().items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def route_tiers(self):
+        out = {}
+        for bm in self.bms:
+            for k, v in bm.route_tiers().items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def close(self):
+        for bm in self.bms:
+            bm.close()
+        self.bms = []
 
 
 def report_segments(seg_off, segs, trace_end_time, threshold_sec, report_mask, transition_mask):

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--config", default="C2")
     ap.add_argument("--traces", type=int, default=10000)
+    ap.add_argument("--streams", type=int, default=2, help="concurrent parts the profiled bench ran (bench --streams)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     ks = os.path.join(a.src, "prof_kt", "run_kernel_stats.csv")
@@ -78,7 +79,8 @@ def main():
     import hashlib
     src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reporter_amd", "csrc", "engine.hip")
     sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
-    rt = {"config": a.config, "traces": a.traces, "kernels": sorted(stage), "engine_sha": sha, "read_factor": 2,
+    rt = {"config": a.config, "traces": a.traces, "streams": a.streams, "kernels": sorted(stage), "engine_sha": sha,
+          "read_factor": 2,
           "hbm_bytes_per_launch": (tot("hbm_read_bytes_corrected") + tot("hbm_write_bytes")) or None,
           "hbm_read_bytes_raw": tot("hbm_read_bytes_raw"), "hbm_write_bytes": tot("hbm_write_bytes"),
           "l2_hit_rate": hits / (hits + miss) if hits + miss else None,
