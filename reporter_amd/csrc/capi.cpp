@@ -260,6 +260,34 @@ char* dup_string(const std::string& s) {
 
 // run a list of parsed traces as one batch on matcher m; per-trace JSON replies, and per-trace
 // error messages (non-empty = that trace failed alone; its reply is empty)
+// fn(i) for i in [0, n) over up to 16 host threads in contiguous chunks (the JSON parse and
+// formatting around a batch are host work that a single thread makes the boundary's limit);
+// an exception is rethrown for the lowest failing index's chunk, as a serial loop would
+template <class F>
+void parallel_for(size_t n, F&& fn) {
+  const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t nt = std::min<size_t>(std::min<size_t>(hw, 16), (n + 127) / 128);
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::vector<std::exception_ptr> err(nt);
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      const size_t a = n * t / nt, b = n * (t + 1) / nt;
+      try {
+        for (size_t i = a; i < b; ++i) fn(i);
+      } catch (...) {
+        err[t] = std::current_exception();
+      }
+    });
+  for (auto& x : th) x.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
 std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*>& pt, std::vector<std::string>* errs) {
   const size_t n = pt.size();
   std::vector<uint32_t> off(n + 1, 0), topt(n);
@@ -268,12 +296,12 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
   const uint64_t P = off[n];
   std::vector<float> lon(P), lat(P), acc(P);
   std::vector<double> tm(P);
-  for (size_t i = 0; i < n; ++i) {
+  parallel_for(n, [&](size_t i) {
     std::copy(pt[i]->lon.begin(), pt[i]->lon.end(), lon.begin() + off[i]);
     std::copy(pt[i]->lat.begin(), pt[i]->lat.end(), lat.begin() + off[i]);
     std::copy(pt[i]->acc.begin(), pt[i]->acc.end(), acc.begin() + off[i]);
     std::copy(pt[i]->time.begin(), pt[i]->time.end(), tm.begin() + off[i]);
-  }
+  });
   HostBatch hb;
   hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = lon.data(); hb.lat = lat.data();
   hb.time = tm.data(); hb.accuracy = acc.data(); hb.n_opts = (uint32_t)n; hb.opts = opts.data();
@@ -290,13 +318,13 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
   std::vector<std::string> out(n);
   if (errs) errs->assign(n, std::string());
   for (size_t i = 0; i < n; ++i) {
-    if (terr[i]) {
-      if (!errs) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
-      (*errs)[i] = error_text(terr[i]);
-      continue;
-    }
-    out[i] = segments_json(segs.data() + soff[i], soff[i + 1] - soff[i]);
+    if (!terr[i]) continue;
+    if (!errs) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
+    (*errs)[i] = error_text(terr[i]);
   }
+  parallel_for(n, [&](size_t i) {
+    if (!terr[i]) out[i] = segments_json(segs.data() + soff[i], soff[i + 1] - soff[i]);
+  });
   return out;
 }
 
@@ -461,12 +489,10 @@ int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** ou
     if (!m) throw std::runtime_error("matcher is NULL");
     for (size_t i = 0; i < n; ++i) outs[i] = nullptr;
     if (n == 0) return;
-    std::vector<ParsedTrace> pt;
-    pt.reserve(n);
-    for (size_t i = 0; i < n; ++i) {
+    for (size_t i = 0; i < n; ++i)
       if (!traces[i]) throw std::runtime_error("trace string is NULL");
-      pt.push_back(parse_trace(traces[i], *m->conf));
-    }
+    std::vector<ParsedTrace> pt(n);
+    parallel_for(n, [&](size_t i) { pt[i] = parse_trace(traces[i], *m->conf); });
     std::vector<std::string> js;
     if (n == 1 && m->conf->coalescer) {
       js.push_back(m->conf->coalescer->submit(&pt[0]));
