@@ -227,6 +227,15 @@ __device__ __forceinline__ void project(float alon, float alat, uint32_t acum, f
   s = v;
 }
 
+// time_ms on the device: below 2^32 cm*360 the IEEE double quotient truncates to the exact
+// floor (a non-integer quotient lies >= 1/dkph >= 2^-16 below the next integer, far above half
+// an ulp, 2^-21); about half the instructions of the integer division
+__device__ __forceinline__ uint32_t time_ms_dev(uint32_t d_cm, uint32_t dkph) {
+  if (d_cm > 11930464u) return time_ms(d_cm, dkph);   // d_cm * 360 >= 2^32
+  const uint32_t D = dkph ? dkph : 1u;
+  return (uint32_t)((double)(d_cm * 360u) / (double)D);
+}
+
 // candidate descriptor of (road, s) for a travel mode: everything the route and path
 // kernels need about a candidate in two dwordx4 (no dependent graph loads there)
 __device__ __forceinline__ void desc_from_rec(const uint4& a, const uint4& c, uint32_t road, uint32_t s, int mode,
@@ -238,7 +247,7 @@ __device__ __forceinline__ void desc_from_rec(const uint4& a, const uint4& c, ui
   if (c.x != kNone && edge_ok(c.z, acc) && spr == 0u) spr = 1u;
   d0 = make_uint4(road, s, a.z, spf | (spr << 16));
   // d1 = {node0, node1, time_ms(s) entering forward from node0, time_ms(L - s) entering reverse from node1}
-  d1 = make_uint4(a.x, a.y, spf ? time_ms(s, spf) : 0xffffffffu, spr ? time_ms(a.z - s, spr) : 0xffffffffu);
+  d1 = make_uint4(a.x, a.y, spf ? time_ms_dev(s, spf) : 0xffffffffu, spr ? time_ms_dev(a.z - s, spr) : 0xffffffffu);
 }
 
 __device__ __forceinline__ void make_desc(const DevGraph& g, uint32_t road, uint32_t s, int mode, uint4& d0,
@@ -391,13 +400,14 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
       const int x = x0 + y;
       if (x >= (int)n) break;
       const uint32_t sqb = (uint32_t)(rbest[x] >> 32);
+      // rank by (sq, road): both fit one u64 key (sq >= 0, so its bits order as the value)
+      const unsigned long long kx = ((unsigned long long)sqb << 32) | rroad[x];
       uint32_t rank = 0;
 #pragma unroll
       for (int z = 0; z < kMaxCand; ++z) {
         if (K1_UNIFORM_STOP(z < (int)n)) break;
         if (z >= (int)n) continue;
-        const uint32_t sqb2 = (uint32_t)(rbest[z] >> 32);
-        rank += (sqb2 < sqb || (sqb2 == sqb && rroad[z] < rroad[x])) ? 1u : 0u;
+        rank += ((((rbest[z] >> 32) << 32) | rroad[z]) < kx) ? 1u : 0u;
       }
       uint4 d0, d1;
       desc_from_rec(ra[y], rc[y], rroad[x], rs[x], op.mode, cacc, d0, d1);

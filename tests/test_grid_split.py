@@ -41,3 +41,19 @@ def test_oracle_identical_on_split_grid(built_lib, tmp_path):
             if isinstance(v, np.ndarray):
                 assert np.array_equal(v, res[k]), k
     assert out[1][1] < 0.8 * out[0][1]   # f = 2 reads fewer grid items on a 100 m-block grid
+
+
+def test_double_quotient_time_is_exact():
+    """engine.hip time_ms_dev: trunc((double)(d*360) / (double)D) == floor for d*360 < 2^32 and
+    every 16-bit speed D (exact multiples, their neighbours and random distances)."""
+    rng = np.random.default_rng(5)
+    D = np.arange(1, 65536, dtype=np.uint64)
+    for _ in range(4):
+        k = (rng.integers(0, 2**32, len(D), dtype=np.uint64) // D)
+        for dd in (-1, 0, 1):
+            N = (k * D).astype(np.int64) + dd
+            d = np.clip(N // 360, 0, 11930464).astype(np.uint64)
+            num = d * 360
+            ref = num // D
+            got = np.trunc(num.astype(np.float64) / D.astype(np.float64)).astype(np.uint64)
+            assert np.array_equal(ref, got)
