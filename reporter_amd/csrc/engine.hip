@@ -701,8 +701,8 @@ __device__ __forceinline__ unsigned long long route_key_vals(const uint4& a0, co
   unsigned long long best = kKeyInf;
   int bc = -1;
   if (a0.x == rb) {
-    if (spf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
-    if (spr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
+    if (spf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms_dev(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
+    if (spr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms_dev(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
   }
   if (spf && lab0 != kKeyInf) { const unsigned long long k = lab0 + make_key(sb, b1.z); if (k < best) { best = k; bc = 2; } }
   if (spr && lab1 != kKeyInf) { const unsigned long long k = lab1 + make_key(L - sb, b1.w); if (k < best) { best = k; bc = 3; } }
@@ -722,8 +722,8 @@ __device__ __forceinline__ unsigned long long route_key(const Label& label, cons
 __device__ __forceinline__ void exit_keys(const uint4& a0, uint32_t bound, unsigned long long& rk1,
                                           unsigned long long& rk0) {
   const uint32_t s = a0.y, L = a0.z, spf = d_spf(a0), spr = d_spr(a0);
-  rk1 = (spf && L - s <= bound) ? make_key(L - s, time_ms(L - s, spf)) : kKeyInf;
-  rk0 = (spr && s <= bound) ? make_key(s, time_ms(s, spr)) : kKeyInf;
+  rk1 = (spf && L - s <= bound) ? make_key(L - s, time_ms_dev(L - s, spf)) : kKeyInf;
+  rk0 = (spr && s <= bound) ? make_key(s, time_ms_dev(s, spr)) : kKeyInf;
 }
 
 // ------------------------------------------------------------------------------------------
