@@ -1263,6 +1263,29 @@ struct SearchPathLabels {
   __device__ unsigned long long operator()(uint32_t x, uint32_t, uint32_t) const { return s.label(x); }
 };
 
+// Canonical predecessor of node x (label lx): the smallest-id usable in-edge (u -> x) with
+// label(u) + key(edge) == lx, in ascending edge id.  Each in-edge is one self-contained record
+// (edge, source node, road|rev, length; info word): one round trip before its label probe
+// instead of three dependent loads (in_edge -> edges -> edge_src).  Probing several in-edges
+// at once was slower: most nodes find the tight edge first, and the extra probes and
+// registers cost more than the overlap (C2 paths 0.32 -> 0.39 ms).
+template <class PL>
+__device__ __forceinline__ bool find_pred(const DevGraph& g, const PL& lab, uint32_t acc, int mode, uint32_t x,
+                                          unsigned long long lx, uint32_t& pe, uint32_t& pu, unsigned long long& plu) {
+  for (uint32_t q = g.in_off[x], q1 = g.in_off[x + 1]; q < q1; ++q) {
+    const uint4 r = g.in_rec[q];
+    const uint32_t inf = g.in_info[q];
+    if (!edge_ok(inf, acc)) continue;
+    // r.y is the edge's start: node0 of its road when the edge runs forward
+    const unsigned long long lu = lab(r.y, r.z >> 1, r.z & 1u);
+    if (lu != kKeyInf && lu + make_key(r.w, time_ms_dev(r.w, mode_speed_dkph(mode, inf & 0xffffu))) == lx) {
+      pe = r.x; pu = r.y; plu = lu;
+      return true;
+    }
+  }
+  return false;
+}
+
 // Walk the chosen transition's route back from its entry node by canonical predecessors
 // (smallest-id usable in-edge from a labelled node whose label + edge key equals the
 // node's label) and write its edges.  `key`/`combo` are the transition's route key and
@@ -1298,16 +1321,7 @@ __device__ __forceinline__ void path_walk(const DevGraph& g, const DevBatch& b, 
     if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
     uint32_t pe = kNone, pu = 0;
     unsigned long long plu = kKeyInf;
-    for (uint32_t q = g.in_off[x]; q < g.in_off[x + 1]; ++q) {
-      const uint32_t e = g.in_edge[q];
-      const uint4 rec = g.edges[e];
-      if (!edge_ok(rec.z, acc)) continue;
-      const uint32_t u = g.edge_src[e];
-      // u is the edge's start: node0 of its road when the edge runs forward
-      const unsigned long long lu = lab(u, rec.w >> 1, rec.w & 1u);
-      if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { pe = e; pu = u; plu = lu; break; }
-    }
-    if (pe == kNone) { trace_fail(b, p, kErrRounds); return; }
+    if (!find_pred(g, lab, acc, mode, x, lx, pe, pu, plu)) { trace_fail(b, p, kErrRounds); return; }
 #pragma unroll
     for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
     pr[0] = pe;
@@ -1340,14 +1354,10 @@ __device__ __forceinline__ void path_walk(const DevGraph& g, const DevBatch& b, 
   x = v0;
   lx = lab(v0, b0.x, combo == 2 ? 0u : 1u);
   for (uint32_t q = n - 2; q >= 1; --q) {
-    for (uint32_t r = g.in_off[x]; r < g.in_off[x + 1]; ++r) {
-      const uint32_t e = g.in_edge[r];
-      const uint4 rec = g.edges[e];
-      if (!edge_ok(rec.z, acc)) continue;
-      const uint32_t u = g.edge_src[e];
-      const unsigned long long lu = lab(u, rec.w >> 1, rec.w & 1u);
-      if (lu != kKeyInf && lu + edge_key(rec, mode) == lx) { dst[q] = e; x = u; lx = lu; break; }
-    }
+    uint32_t pe = kNone, pu = 0;
+    unsigned long long plu = kKeyInf;
+    if (!find_pred(g, lab, acc, mode, x, lx, pe, pu, plu)) break;   // found on the first walk
+    dst[q] = pe; x = pu; lx = plu;
   }
 }
 
@@ -2885,6 +2895,20 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
     for (uint32_t e = 0; e < g.num_edges(); ++e) in_edge[fill[g.edges[e].target]++] = e;
     dg_.in_off = upload(allocs_, in_off);
     dg_.in_edge = upload(allocs_, in_edge);
+    // path walks read one self-contained record per in-edge: {edge, source node, road << 1 | rev,
+    // length cm} + its info word (access, speed)
+    std::vector<uint32_t> src(g.num_edges());
+    for (uint32_t n = 0; n < g.num_nodes(); ++n)
+      for (uint32_t e = g.node_off[n]; e < g.node_off[n + 1]; ++e) src[e] = n;
+    std::vector<uint32_t> irec(4 * (size_t)g.num_edges()), iinf(g.num_edges());
+    for (size_t q = 0; q < in_edge.size(); ++q) {
+      const uint32_t e = in_edge[q];
+      const EdgeRec& er = g.edges[e];
+      irec[4 * q] = e; irec[4 * q + 1] = src[e]; irec[4 * q + 2] = er.road; irec[4 * q + 3] = er.len_cm;
+      iinf[q] = er.info;
+    }
+    dg_.in_rec = (const uint4*)upload(allocs_, irec);
+    dg_.in_info = upload(allocs_, iinf);
   }
   dg_.edge_seg = upload(allocs_, g.edge_seg);
   {

@@ -33,6 +33,8 @@ struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   const uint32_t* edge_src;      // source node of each directed edge
   const uint32_t* in_off;        // in-edge CSR offsets (N+1)
   const uint32_t* in_edge;       // edge ids by target node, ascending
+  const uint4* in_rec;           // per in-edge: {edge, source node, road << 1 | rev, len_cm}
+  const uint32_t* in_info;       // per in-edge: the edge's info word
   const uint32_t* edge_seg;
   const uint32_t* edge_seg_off;
   const uint32_t* edge_way;
