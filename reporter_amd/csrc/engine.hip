@@ -154,10 +154,14 @@ __global__ void __launch_bounds__(64) k_states(DevBatch b) {
       s2 = lat_sin(cl); k2 = lat_cos(cl);
       if (lane == 0) { s1 = lat_sin(c1la); k1 = lat_cos(c1la); }
     }
-    const bool a1 = act && (i == 0 || !(gc_trig(lo1, la1, s1, k1, lo, la, s0, k0) < interp));
-    const bool a2 = act && i >= 2 && !(gc_trig(lo2, la2, s2, k2, lo, la, s0, k0) < interp);
+    const double d1 = gc_trig(lo1, la1, s1, k1, lo, la, s0, k0);
+    const double d2 = gc_trig(lo2, la2, s2, k2, lo, la, s0, k0);
+    const bool a1 = act && (i == 0 || !(d1 < interp));
+    const bool a2 = act && i >= 2 && !(d2 < interp);
     const unsigned long long A = __ballot(a1), B = __ballot(a2);
     unsigned long long st = 0;
+    const uint32_t last0 = last;   // last state before this chunk
+    double dx = 0.0;               // distance from the last state when two or more were skipped
     for (uint32_t q = 0; q < m;) {
       const uint32_t ii = c0 + q;
       if (ii == 0 || last + 1 == ii) {
@@ -179,12 +183,24 @@ __global__ void __launch_bounds__(64) k_states(DevBatch b) {
       } else {   // two or more skipped in a row: measure from the last state itself
         float plo = llon, pla = llat;
         if (last >= c0) { plo = lane_f(lo, last - c0); pla = lane_f(la, last - c0); }
-        s = !(gc_distance(plo, pla, lane_f(lo, q), lane_f(la, q)) < interp);
+        const double dq = gc_distance(plo, pla, lane_f(lo, q), lane_f(la, q));
+        s = !(dq < interp);
+        if (lane == (int)q) dx = dq;
       }
       if (s) { st |= 1ull << q; last = ii; }
       ++q;
     }
-    if ((st >> lane) & 1ull) b.state_orig[o + ns + (uint32_t)__popcll(st & ((1ull << lane) - 1ull))] = i;
+    if ((st >> lane) & 1ull) {
+      const unsigned long long below = st & ((1ull << lane) - 1ull);
+      const uint32_t si = ns + (uint32_t)__popcll(below);
+      b.state_orig[o + si] = i;
+      // gc from the previous state (the distance the rule just tested: d1, d2 or the explicit
+      // one); k_trans_count and K3 read it instead of measuring it again
+      if (si > 0) {
+        const uint32_t prev = below ? c0 + 63u - (uint32_t)__builtin_clzll(below) : last0;
+        b.gc[o + si] = i - prev == 1u ? d1 : (i - prev == 2u ? d2 : dx);
+      }
+    }
     ns += (uint32_t)__popcll(st);
     if (last >= c0) { llon = lane_f(lo, last - c0); llat = lane_f(la, last - c0); }
     c1lo = lane_f(lo, 63); c1la = lane_f(la, 63);
@@ -666,8 +682,7 @@ __global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long l
       c = KA * KB;
       ns = KB ? KA : 0u;
       const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
-      const double gc = gc_distance(b.lon[pa], b.lat[pa], b.lon[pb], b.lat[pb]);
-      b.gc[p] = gc;
+      const double gc = b.gc[p];   // written by k_states (the rule's own measurement)
       const MatchOptions op = b.opts[b.trace_opt[k]];
       b.pair_info[p] = make_uint4(route_bound(gc, op), time_bound(b.time[pb] - b.time[pa], op),
                                   KA | (KB << 8) | ((uint32_t)op.mode << 16), 0u);
