@@ -239,6 +239,35 @@ def extras(gpath, tr, json_traces, tmpdir):
                             "value": P / dt, "unit": "points/s", "seconds": dt, "json_build_s_untimed": build_s,
                             "reply_mb": sum(map(len, outs)) / 1e6}
     sm.close()
+    # the service under concurrent load: one SegmentMatcher per client thread (as
+    # reporter_service.py's threaded server), every Match coalesced into shared batches
+    n_cli, n_req = 64, min(len(reqs), 4096)
+    for workers in (1,):
+        conf = valhalla.write_config(os.path.join(tmpdir, "reporter_bench_svc_%d.json" % os.getpid()), gpath, device=0,
+                                     coalesce=True, coalesce_workers=workers)
+        valhalla.Configure(conf)
+        done = [0] * n_cli
+
+        def client(c):
+            m = valhalla.SegmentMatcher()
+            for q in range(c, n_req, n_cli):
+                m.Match(reqs[q])
+                done[c] += 1
+            m.close()
+
+        import threading
+        ths = [threading.Thread(target=client, args=(c,)) for c in range(n_cli)]
+        t = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        dt = time.perf_counter() - t
+        pts = int(tr["trace_off"][min(n_req, len(tr["trace_off"]) - 1)])
+        out["service_throughput"] = {
+            "what": "%d C2 /report requests (600 points each) from %d client threads through valhalla.SegmentMatcher()"
+                    ".Match with request coalescing, %d dispatcher(s)" % (sum(done), n_cli, workers),
+            "requests_per_s": sum(done) / dt, "points_per_s": pts / dt, "seconds": dt}
     return out
 
 

@@ -87,7 +87,7 @@ def coalesce_stats():
 
 
 def write_config(path, graph_path, device=0, coalesce=True, coalesce_window_ms=0.0, ball_radius=None,
-                 **meili_default):
+                 coalesce_workers=None, **meili_default):
     """Write a Valhalla-style config naming the engine's graph file (ball_radius: route-ball radius
     in metres, 0..10000, None = engine default)."""
     conf = {"meili": {"default": dict(meili_default)},
@@ -95,6 +95,8 @@ def write_config(path, graph_path, device=0, coalesce=True, coalesce_window_ms=0
                              "coalesce_window_ms": float(coalesce_window_ms)}}
     if ball_radius is not None:
         conf["reporter_amd"]["ball_radius"] = float(ball_radius)
+    if coalesce_workers is not None:
+        conf["reporter_amd"]["coalesce_workers"] = int(coalesce_workers)
     with open(path, "w") as f:
         _json.dump(conf, f, indent=1)
     return path
