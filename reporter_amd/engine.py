@@ -341,6 +341,16 @@ class BatchMatcher:
         return {names[i]: (float(ms[i]), int(la[i])) for i in range(n)}
 
 
+def split_by_points(trace_off, parts):
+    """Trace index cuts [0, ..., T] of `parts` contiguous ranges with about equal point counts
+    (a cut where the running point count crosses k * P / parts); empty ranges are dropped."""
+    trace_off = np.asarray(trace_off, np.uint64)
+    T = len(trace_off) - 1
+    P = int(trace_off[-1]) if T >= 0 else 0
+    cuts = [0] + [int(np.searchsorted(trace_off, P * k / parts)) for k in range(1, max(1, int(parts)))] + [T]
+    return sorted(set(min(max(c, 0), T) for c in cuts))
+
+
 class MultiMatcher:
     """One batch as `parts` contiguous trace ranges (balanced by points), each on its own
     BatchMatcher (HIP stream + workspace).  rerun() runs every part at once
@@ -359,9 +369,7 @@ class MultiMatcher:
         P = int(trace_off[-1])
         accuracy = np.full(P, -1.0, np.float32) if accuracy is None else np.asarray(accuracy, np.float32)
         trace_opt = np.zeros(T, np.uint32) if trace_opt is None else np.asarray(trace_opt, np.uint32)
-        # cut where the running point count crosses k * P / parts
-        cuts = [0] + [int(np.searchsorted(trace_off, P * k / self.parts)) for k in range(1, self.parts)] + [T]
-        cuts = sorted(set(min(max(c, 0), T) for c in cuts))
+        cuts = split_by_points(trace_off, self.parts)
         for bm in self.bms:
             bm.close()
         self.bms = []

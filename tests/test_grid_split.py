@@ -57,3 +57,18 @@ def test_double_quotient_time_is_exact():
             ref = num // D
             got = np.trunc(num.astype(np.float64) / D.astype(np.float64)).astype(np.uint64)
             assert np.array_equal(ref, got)
+
+
+def test_split_by_points_balances_and_covers():
+    """engine.split_by_points (MultiMatcher's parts): contiguous, covering, balanced by points."""
+    from reporter_amd import engine
+    rng = np.random.default_rng(2)
+    for parts in (1, 2, 3, 7):
+        lens = rng.integers(1, 400, 500)
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint32)
+        cuts = engine.split_by_points(off, parts)
+        assert cuts[0] == 0 and cuts[-1] == 500 and cuts == sorted(set(cuts))
+        pts = [int(off[b] - off[a]) for a, b in zip(cuts[:-1], cuts[1:])]
+        assert sum(pts) == int(off[-1])
+        assert max(pts) - min(pts) <= 2 * 400   # within two traces of even
+    assert engine.split_by_points(np.array([0, 5], np.uint32), 4) == [0, 1]
