@@ -13,6 +13,8 @@
 #include <cstdlib>
 #include <functional>
 #include <queue>
+#include <unordered_map>
+#include <unordered_set>
 #include <stdexcept>
 #include <thread>
 #include <utility>
@@ -106,26 +108,73 @@ void parallel_nodes(uint32_t n, int threads, F&& f) {
 
 }  // namespace
 
-namespace {
-double node_density(const Graph& g) {   // nodes per m^2 over the graph's bounding box
-  const uint32_t N = g.num_nodes();
-  float lo0 = g.node_lon[0], lo1 = lo0, la0 = g.node_lat[0], la1 = la0;
-  for (uint32_t n = 1; n < N; ++n) {
-    lo0 = std::min(lo0, g.node_lon[n]); lo1 = std::max(lo1, g.node_lon[n]);
-    la0 = std::min(la0, g.node_lat[n]); la1 = std::max(la1, g.node_lat[n]);
+
+// Ball size by sampling: the bounded search (auto mode) from 256 nodes spread over the node
+// ids, with sparse labels (no per-graph arrays: cheap on a 16.6 M-node graph).  Rows are the
+// roads of the settled nodes' out-edges (a one-way road entering the ball from outside is the
+// only row it misses).  A density-times-disc estimate overshoots route-distance balls (a grid's
+// network ball is a diamond) and power-of-two tables amplify that: it put C4's 1000 m tables
+// at 136 GB (they are 68 GB) and picked 700 m.
+struct BallSampler {
+  const Graph& g;
+  explicit BallSampler(const Graph& gr) : g(gr) {}
+  BallSample at(uint32_t radius_cm, uint32_t max_keys) const {
+    BallSample out;
+    const uint32_t N = g.num_nodes();
+    const uint32_t S = std::min<uint32_t>(N, 256u);
+    const uint32_t acc = mode_access(kModeAuto);
+    double nodes = 0, slots = 0;
+    uint32_t skipped = 0;
+    std::unordered_map<uint32_t, uint64_t> lab;
+    std::unordered_set<uint32_t> roads;
+    using Item = std::pair<uint64_t, uint32_t>;
+    for (uint32_t i = 0; i < S; ++i) {
+      const uint32_t u = (uint32_t)(((uint64_t)i * N) / S);
+      lab.clear();
+      roads.clear();
+      std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
+      lab[u] = 0;
+      pq.push({0ull, u});
+      uint32_t settled = 0;
+      bool ok = true;
+      while (!pq.empty()) {
+        const Item it = pq.top();
+        pq.pop();
+        if (it.first != lab[it.second]) continue;
+        if (++settled > max_keys) { ok = false; break; }
+        for (uint32_t e = g.node_off[it.second]; e < g.node_off[it.second + 1]; ++e) {
+          const EdgeRec& r = g.edges[e];
+          roads.insert(r.road >> 1);
+          if (!(edge_access(r.info) & acc)) continue;
+          const uint64_t nk = it.first + make_key(r.len_cm, time_ms(r.len_cm, mode_speed_dkph(kModeAuto, edge_speed_dkph(r.info))));
+          if (key_dist(nk) > radius_cm) continue;
+          auto f = lab.find(r.target);
+          if (f == lab.end() || nk < f->second) {
+            lab[r.target] = nk;
+            pq.push({nk, r.target});
+          }
+        }
+      }
+      if (!ok) { ++skipped; nodes += max_keys; continue; }
+      nodes += settled;
+      slots += (double)(1ull << table_bits(std::max<size_t>(1, roads.size())));
+    }
+    out.nodes = S ? nodes / S : 0.0;
+    out.table_bytes = S ? slots / S * (double)N * 16.0 : 0.0;
+    out.skipped_frac = S ? (double)skipped / S : 0.0;
+    return out;
   }
-  const double mid = 0.5 * ((double)la0 + (double)la1) * 3.14159265358979323846 / 180.0;
-  const double w = std::max(1.0, ((double)lo1 - lo0) * 111320.0 * std::cos(mid));
-  const double h = std::max(1.0, ((double)la1 - la0) * 110567.0);
-  return (double)N / (w * h);
+};
+
+BallSample sample_balls(const Graph& g, uint32_t radius_cm, uint32_t max_keys) {
+  if (g.num_nodes() == 0) return BallSample{};
+  BallSampler bs(g);
+  return bs.at(radius_cm, max_keys);
 }
-}  // namespace
 
 double est_ball_nodes(const Graph& g, uint32_t radius_cm) {
-  const uint32_t N = g.num_nodes();
-  if (N < 2) return (double)N;
-  const double rm = radius_cm / 100.0;
-  return std::min((double)N, node_density(g) * 3.14159265358979323846 * rm * rm);
+  if (g.num_nodes() < 2) return (double)g.num_nodes();
+  return sample_balls(g, radius_cm, kBallMaxKeysHost).nodes;
 }
 
 void road_incidence(const Graph& g, std::vector<uint32_t>& inc_off, std::vector<uint32_t>& inc) {
@@ -154,14 +203,11 @@ uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes) {
   }
   const uint32_t N = g.num_nodes();
   if (N < 2) return 40000u;
-  const double rho = node_density(g);                                     // nodes per m^2
-  const double roads_per_node = 1.3 * (double)g.num_roads() / (double)N;  // + roads crossing the rim
+  BallSampler sampler(g);
   for (const uint32_t r : {200000u, 150000u, 100000u, 70000u, 50000u}) {
-    const double rm = r / 100.0;
-    const double nodes = std::min((double)N, rho * 3.14159265358979323846 * rm * rm);
-    const double rows = std::max(1.0, nodes * roads_per_node);
-    const double table = (double)(1ull << table_bits((uint64_t)rows));
-    if (nodes <= kBallMaxKeysHost && (double)N * table * 16.0 <= (double)budget_bytes) return r;
+    const BallSample bs = sampler.at(r, kBallMaxKeysHost);
+    // most balls must get a table, and the tables must fit the budget (sampled sizes, +10 %)
+    if (bs.skipped_frac <= 0.05 && bs.table_bytes * 1.1 <= (double)budget_bytes) return r;
   }
   return 40000u;
 }

@@ -38,10 +38,10 @@ constexpr uint32_t kBallMaxKeysHost = 4096;   // ball nodes above which a node g
 constexpr uint32_t kBallMaxRadiusCm = 1000000;   // 10 km knob cap (rows hold 24-bit distances)
 
 // Default radius for a graph: the largest of {2000 (meili's default breakage distance, so
-// every default-bounded transition is a table probe), 1500, 1000, 700, 500} m whose
-// estimated tables (from the graph's node density) stay within `budget_bytes` per mode;
-// 400 m when none does.
-constexpr uint64_t kBallAutoBudget = 72ull << 30;   // estimate (power-of-two tables); C4 at 700 m: 68 GB estimated, 33 GB built
+// every default-bounded transition is a table probe), 1500, 1000, 700, 500} m whose tables
+// (sampled: sample_balls, +10 %) stay within `budget_bytes` per mode and whose balls mostly
+// fit kBallMaxKeysHost; 400 m when none does.
+constexpr uint64_t kBallAutoBudget = 72ull << 30;   // per mode; C4: 1000 m (68 GB built)
 // budget 0: kBallAutoBudget, or RM_BALL_BUDGET_GB when set (the HBM a deployment grants the tables)
 uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes = 0);
 
@@ -50,8 +50,14 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
 // node -> incident roads CSR (every road listed at node0 and at node1)
 void road_incidence(const Graph& g, std::vector<uint32_t>& inc_off, std::vector<uint32_t>& inc);
 
-// nodes an average ball of radius_cm holds, from the graph's node density (the estimate
-// auto_ball_radius_cm uses); the engine builds small balls on the GPU
+// sampled ball statistics at a radius (exact bounded searches from 256 nodes, auto mode)
+struct BallSample {
+  double nodes = 0;          // mean nodes per ball
+  double table_bytes = 0;    // estimated bytes of all nodes' power-of-two tables
+  double skipped_frac = 0;   // sampled balls above max_keys (no table)
+};
+BallSample sample_balls(const Graph& g, uint32_t radius_cm, uint32_t max_keys);
+// nodes an average ball of radius_cm holds (sampled); the engine builds small balls on the GPU
 double est_ball_nodes(const Graph& g, uint32_t radius_cm);
 
 }  // namespace rm

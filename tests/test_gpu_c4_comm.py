@@ -2,7 +2,7 @@
 
 C4 (BASELINE.json configs[3]): the 4000 x 4000 @250 m country graph — 16.6 M nodes,
 65 M directed edges, 19.4 M OSMLR segments — replicated in HBM, traces at 5 s.  Sampled
-traces are matched at the product default (automatic ball radius, 700 m on this graph,
+traces are matched at the product default (automatic ball radius, 1000 m on this graph,
 tables built on the GPU) and at 400 m (5 s bounds beyond the radius go to the search tiers), every stage compared bit for bit with the oracle, and the full
 19.4 M x 16 speed histogram compared with the CPU pipeline's.
 
@@ -42,7 +42,7 @@ def test_c4_full_graph(c4_graph, ball_radius):
     path, cfg = c4_graph
     auto = ctypes.c_double()
     _lib.check(_lib.lib().rm_graph_auto_ball_radius(os.fsencode(path), ctypes.byref(auto)))
-    assert auto.value == 700.0
+    assert auto.value == 1000.0
     tr = world.generate_traces(path, 3000, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=4000)
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
     t = time.time()
