@@ -733,6 +733,15 @@ __device__ __forceinline__ unsigned long long route_key(const Label& label, cons
   return route_key_vals(a0, b0, b1, lab0, lab1, combo);
 }
 
+// route[] word of a valid route: distance cm (<= kMaxBoundCm < 2^30) plus, when the best
+// combination runs along the source's own road (combo 0 / 1), a flag bit telling the path
+// stage the route is that one edge, so it skips the labels and the walk (most chosen
+// transitions at 1-5 s sampling).  kRouteInvalid (all ones) stays distinct.
+constexpr uint32_t kRouteDirF = 1u << 31, kRouteDirR = 1u << 30, kRouteDistMask = kRouteDirR - 1u;
+__device__ __forceinline__ uint32_t route_word(unsigned long long key, int combo) {
+  return key_dist(key) | (combo == 0 ? kRouteDirF : 0u) | (combo == 1 ? kRouteDirR : 0u);
+}
+
 // root keys of a source candidate's two exits (forward to node1, reverse to node0)
 __device__ __forceinline__ void exit_keys(const uint4& a0, uint32_t bound, unsigned long long& rk1,
                                           unsigned long long& rk0) {
@@ -1044,9 +1053,10 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
     }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
-      const unsigned long long key = route_key(lab, a0, t0[x], t1[x], nullptr);
+      int cb = -1;
+      const unsigned long long key = route_key(lab, a0, t0[x], t1[x], &cb);
       uint32_t r = kRouteInvalid;
-      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
+      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = route_word(key, cb);
       res[((j0 + x) & (kMaxCand - 1)) * stride] = r;
     }
   }
@@ -1154,9 +1164,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
         const uint4 r0 = ball_resolve(ent, h0, t0.x, e0);
         const unsigned long long lab0 = ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
         const unsigned long long lab1 = ball_label(rk1, row_key1(r1), rk0, row_key1(r0));
-        const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, nullptr);
+        int cb = -1;
+        const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, &cb);
         uint32_t rt = kRouteInvalid;
-        if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = key_dist(key);
+        if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = route_word(key, cb);
         res[j] = rt;
       }
     }
@@ -1422,7 +1433,18 @@ __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
   const int mode = (int)(pi.z >> 16);
   const uint32_t bound = pi.x;
   const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
-  const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
+  const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2];
+  const uint32_t rw = b.route[b.trans_off[p] + i * ((pi.z >> 8) & 0xffu) + j];
+  if (rw & (kRouteDirF | kRouteDirR)) {   // K2 found the route along the source's road: one edge
+    const uint32_t sb = b.cand_desc[(p * kMaxCand + j) * 2].y;
+    b.route_dist[p] = rw & kRouteDistMask;
+    b.path_sab[p] = make_uint2(a0.y, sb);
+    b.path_inline[p * kInlinePath] = (rw & kRouteDirF) ? g.road_fwd[a0.x] : g.road_rev[a0.x];
+    b.path_cnt[p] = 1;
+    b.path_off[p] = 0;
+    return;
+  }
+  const uint4 a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
   const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
   unsigned long long rk1, rk0;
   exit_keys(a0, bound, rk1, rk0);
@@ -1518,9 +1540,10 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
   if (ok) {
     for (uint32_t j = lane; j < KB; j += kWave) {
       const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-      const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, nullptr);
+      int cb = -1;
+      const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, &cb);
       uint32_t out = kRouteInvalid;
-      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
+      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = route_word(key, cb);
       b.route[base + i * KB + j] = out;
     }
   }
@@ -1789,7 +1812,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     // ---- chunk -> LDS
 #pragma unroll
     for (int x = 0; x < kVitRoutes / 16; ++x)
-      if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
+      if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)(rv[x] & kRouteDistMask) * 0.01;
     {
       float4* sqdst = reinterpret_cast<float4*>(&gs.sq[0][0]);
       const uint32_t nf = C * (kMaxCand / 4);
@@ -1844,7 +1867,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
           if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
 #pragma unroll
         for (int x = 0; x < kVitRoutes / 16; ++x)
-          if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
+          if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)(rv[x] & kRouteDistMask) * 0.01;
         wave_sync();
       }
       if (t + 1 < C) {   // next layer's first route rows (after any re-staging above)
@@ -3324,7 +3347,11 @@ void Matcher::get_routes(uint32_t* trans_off, double* gc, uint32_t* route) {
   sync();
   RM_HIP(hipMemcpy(trans_off, ws_.trans_off, n_points_ * 4, hipMemcpyDeviceToHost));
   RM_HIP(hipMemcpy(gc, ws_.gc, n_points_ * 8, hipMemcpyDeviceToHost));
-  if (n_trans_) RM_HIP(hipMemcpy(route, ws_.route, n_trans_ * 4, hipMemcpyDeviceToHost));
+  if (n_trans_) {
+    RM_HIP(hipMemcpy(route, ws_.route, n_trans_ * 4, hipMemcpyDeviceToHost));
+    for (uint64_t q = 0; q < n_trans_; ++q)   // drop the direct-route flags (route_word)
+      if (route[q] != kRouteInvalid) route[q] &= 0x3fffffffu;
+  }
 }
 void Matcher::get_viterbi(int8_t* choice, uint8_t* chain_start) {
   sync();
