@@ -63,6 +63,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route; uint4* pair_info;
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
+  uint32_t* path_list; uint32_t* path_list_n;   // k_paths_direct -> k_paths_ball, per 256-slot block
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
   uint2* path_sab;   // per chosen transition: offsets (cm) of its source and target candidates on their roads
   SegmentRec* segs; uint32_t* seg_base; uint32_t* seg_cnt;
@@ -1419,47 +1420,74 @@ struct BallPathLabels {
   }
 };
 
-// path ball tier: one lane per chosen transition whose bound fits the ball radius; the
-// others go to the search tiers (rl_routes_0 reused after K2, count ctl[8])
-__global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
+// path direct tier: one lane per slot.  A chosen transition whose route K2 found along the
+// source's own road (route_word's flags: most of them at 1-5 s sampling) is one edge and is
+// written here; the others are compacted within the block (path_list, count path_list_n per
+// block; no global atomics) for the ball tier, so its waves hold only transitions that probe
+// tables and walk.
+__global__ void __launch_bounds__(256) k_paths_direct(DevGraph g, DevBatch b) {
+  __shared__ uint32_t s_wn[4];
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= b.P) return;
-  const uint32_t k = b.slot_trace[p];
-  const uint32_t o = b.trace_off[k];
-  const uint32_t s = (uint32_t)(p - o);
-  if (s < 1 || s >= b.n_states[k]) return;
-  if (b.chain_start[p] || b.choice[p] < 0) return;
-  const uint4 pi = b.pair_info[p];
-  const int mode = (int)(pi.z >> 16);
-  const uint32_t bound = pi.x;
-  const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
-  const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2];
-  const uint32_t rw = b.route[b.trans_off[p] + i * ((pi.z >> 8) & 0xffu) + j];
-  if (rw & (kRouteDirF | kRouteDirR)) {   // K2 found the route along the source's road: one edge
-    const uint32_t sb = b.cand_desc[(p * kMaxCand + j) * 2].y;
-    b.route_dist[p] = rw & kRouteDistMask;
-    b.path_sab[p] = make_uint2(a0.y, sb);
-    b.path_inline[p * kInlinePath] = (rw & kRouteDirF) ? g.road_fwd[a0.x] : g.road_rev[a0.x];
-    b.path_cnt[p] = 1;
-    b.path_off[p] = 0;
-    return;
+  bool walk = false;
+  if (p < b.P) {
+    const uint32_t k = b.slot_trace[p];
+    const uint32_t o = b.trace_off[k];
+    const uint32_t s = (uint32_t)(p - o);
+    if (s >= 1 && s < b.n_states[k] && !b.chain_start[p] && b.choice[p] >= 0) {
+      const uint32_t KB = (b.pair_info[p].z >> 8) & 0xffu;
+      const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+      const uint32_t rw = b.route[b.trans_off[p] + i * KB + j];
+      if (rw & (kRouteDirF | kRouteDirR)) {
+        const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2];
+        const uint32_t sb = b.cand_desc[(p * kMaxCand + j) * 2].y;
+        b.route_dist[p] = rw & kRouteDistMask;
+        b.path_sab[p] = make_uint2(a0.y, sb);
+        b.path_inline[p * kInlinePath] = (rw & kRouteDirF) ? g.road_fwd[a0.x] : g.road_rev[a0.x];
+        b.path_cnt[p] = 1;
+        b.path_off[p] = 0;
+      } else {
+        walk = true;
+      }
+    }
   }
-  const uint4 a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
-  const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-  unsigned long long rk1, rk0;
-  exit_keys(a0, bound, rk1, rk0);
-  const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
-  const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
-  if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {
-    b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
-    return;
+  const unsigned long long m = __ballot(walk);
+  const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
+  if (lane == 0) s_wn[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t at = 0;
+  for (int x = 0; x < w; ++x) at += s_wn[x];
+  if (walk) b.path_list[(uint64_t)blockIdx.x * 256u + at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)p;
+  if (threadIdx.x == 0) b.path_list_n[blockIdx.x] = s_wn[0] + s_wn[1] + s_wn[2] + s_wn[3];
+}
+
+// path ball tier: block B takes block B's list of k_paths_direct, one lane per transition whose
+// bound fits the ball radius; the others go to the search tiers (rl_routes_0 reused after K2,
+// count ctl[8])
+__global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
+  if (threadIdx.x >= b.path_list_n[blockIdx.x]) return;
+  {
+    const uint64_t p = b.path_list[(uint64_t)blockIdx.x * 256u + threadIdx.x];
+    const uint4 pi = b.pair_info[p];
+    const int mode = (int)(pi.z >> 16);
+    const uint32_t bound = pi.x;
+    const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+    const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
+    const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+    unsigned long long rk1, rk0;
+    exit_keys(a0, bound, rk1, rk0);
+    const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
+    const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+    if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {
+      b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
+      return;
+    }
+    const BallPathLabels lab{g.ball_ent[mode], h1, h0, rk1, rk0};
+    const unsigned long long lab0 = d_spf(b0) ? lab(b1.x, b0.x, 0u) : kKeyInf;
+    const unsigned long long lab1 = d_spr(b0) ? lab(b1.y, b0.x, 1u) : kKeyInf;
+    int combo = -1;
+    const unsigned long long key = route_key_vals(a0, b0, b1, lab0, lab1, &combo);
+    path_walk(g, b, p, lab, mode, a0, a1, b0, b1, rk1, rk0, key, combo, (int)kBallMaxKeys);
   }
-  const BallPathLabels lab{g.ball_ent[mode], h1, h0, rk1, rk0};
-  const unsigned long long lab0 = d_spf(b0) ? lab(b1.x, b0.x, 0u) : kKeyInf;
-  const unsigned long long lab1 = d_spr(b0) ? lab(b1.y, b0.x, 1u) : kKeyInf;
-  int combo = -1;
-  const unsigned long long key = route_key_vals(a0, b0, b1, lab0, lab1, &combo);
-  path_walk(g, b, p, lab, mode, a0, a1, b0, b1, rk1, rk0, key, combo, (int)kBallMaxKeys);
 }
 
 // path lane tier: one lane per chosen transition, labels in registers.  With `listed`,
@@ -2420,9 +2448,12 @@ struct BallSmem {
   SearchSmem<kBallSearchH, false> s;
   uint32_t road[kBallRowH];
   unsigned long long k0[kBallRowH], k1[kBallRowH];
+  uint16_t dense[kBallRowH], order[kBallRowH];   // fill pass: occupied row slots, rows by rank
+  uint16_t tslot[2 * kBallRowH];                 // fill pass: the node's table (row slot per table slot)
   uint32_t used, bad;
 };
 
+static_assert(kBallSlotsPerRow * (kBallRowH * 3 / 4) <= 2 * kBallRowH, "BallSmem::tslot holds the largest table");
 __device__ __forceinline__ uint32_t table_bits_dev(uint32_t rows) {
   uint32_t bits = 1;
   while ((1ull << bits) < (unsigned long long)kBallSlotsPerRow * rows) ++bits;
@@ -2482,17 +2513,49 @@ __global__ void __launch_bounds__(64) k_ball_build(DevGraph g, int mode, uint32_
         n_rows += bits ? rows : 0u;
       }
     } else {
+      // Rows go in in order of their nearer endpoint's key, as the host build inserts them
+      // (Dijkstra settle order): linear probing leaves the first-inserted rows at their home
+      // slots, and K2 / the path walk probe near roads far more often than far ones (C4 at
+      // 1000 m: K2 23.2 -> 19.8 ms against tables filled in LDS-hash order).  The table is
+      // laid out in LDS by one lane, then written with coalesced stores.
       const uint2 hh = hdr[u];
-      const uint32_t mask = (1u << hh.y) - 1u;
-      for (int h = lane; h < kBallRowH; h += kWave) {
-        const uint32_t r = sm.road[h];
-        if (r == kEmpty) continue;
-        uint32_t x = ball_slot(r, hh.y);
-        while (atomicCAS(reinterpret_cast<unsigned int*>(&ent[(uint64_t)hh.x + x]), kNone, r) != kNone) x = (x + 1) & mask;
+      const uint32_t nslot = 1u << hh.y, mask = nslot - 1u;
+      uint32_t n = 0;
+      for (int h0 = 0; h0 < kBallRowH; h0 += kWave) {
+        const bool has = sm.road[h0 + lane] != kEmpty;
+        const unsigned long long m = __ballot(has);
+        if (has) sm.dense[n + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(h0 + lane);
+        n += (uint32_t)__popcll(m);
+      }
+      for (uint32_t s = lane; s < nslot; s += kWave) sm.tslot[s] = 0xffffu;
+      __syncthreads();
+      for (uint32_t a = lane; a < n; a += kWave) {
+        const uint32_t h = sm.dense[a], r = sm.road[h];
+        const unsigned long long kh = min(sm.k0[h], sm.k1[h]);
+        uint32_t rank = 0;
+        for (uint32_t c = 0; c < n; ++c) {
+          const uint32_t hq = sm.dense[c], rq = sm.road[hq];
+          const unsigned long long kq = min(sm.k0[hq], sm.k1[hq]);
+          rank += (kq < kh || (kq == kh && rq < r)) ? 1u : 0u;
+        }
+        sm.order[rank] = (uint16_t)h;
+      }
+      __syncthreads();
+      if (lane == 0) {
+        for (uint32_t q = 0; q < n; ++q) {
+          const uint32_t h = sm.order[q];
+          uint32_t x = ball_slot(sm.road[h], hh.y);
+          while (sm.tslot[x] != 0xffffu) x = (x + 1) & mask;
+          sm.tslot[x] = (uint16_t)h;
+        }
+      }
+      __syncthreads();
+      for (uint32_t s = lane; s < nslot; s += kWave) {
+        const uint32_t h = sm.tslot[s];
+        if (h == 0xffffu) continue;
         uint32_t y, z, w;
         ball_pack(sm.k0[h], sm.k1[h], y, z, w);
-        uint4* e = &ent[(uint64_t)hh.x + x];
-        e->y = y; e->z = z; e->w = w;
+        ent[(uint64_t)hh.x + s] = make_uint4(sm.road[h], y, z, w);
       }
     }
     __syncthreads();
@@ -2923,6 +2986,7 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.trans_cnt = dalloc<uint32_t>(L, cp); w.trans_off = dalloc<uint32_t>(L, cp); w.gc = dalloc<double>(L, cp);
   w.src_cnt = dalloc<uint32_t>(L, cp); w.src_off = dalloc<uint32_t>(L, cp);
   w.choice = dalloc<int8_t>(L, cp); w.chain_start = dalloc<uint8_t>(L, cp); w.bp = dalloc<uint8_t>(L, cp * kMaxCand);
+  w.path_list = dalloc<uint32_t>(L, cp + 256); w.path_list_n = dalloc<uint32_t>(L, cp / 256 + 2);
   w.path_off = dalloc<uint32_t>(L, cp); w.path_cnt = dalloc<uint32_t>(L, cp); w.route_dist = dalloc<uint32_t>(L, cp);
   w.path_sab = dalloc<uint2>(L, cp);
   w.path_inline = dalloc<uint32_t>(L, cp * kInlinePath);
@@ -3042,6 +3106,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
+  v.path_list = w.path_list; v.path_list_n = w.path_list_n;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
   v.path_pool = w.path_pool; v.path_cap = w.cap_path;
   v.route_dist = w.route_dist; v.path_sab = w.path_sab;
@@ -3195,6 +3260,7 @@ void Matcher::run_device(const RunParams& rp) {
       RM_HIP(hipMemsetAsync(w.ctl + 10, 0, sizeof(uint32_t), st));   // paths list C
     }
     if (balls) {
+      hipLaunchKernelGGL(k_paths_direct, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
       hipLaunchKernelGGL(k_paths_ball, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>((P + 255) / 256, kListedGrid)), dim3(256), 0,
                          st, g, v, 1);
