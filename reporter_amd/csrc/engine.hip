@@ -63,7 +63,6 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route; uint4* pair_info;
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
-  uint32_t* path_list; uint32_t* path_list_n;   // k_paths_direct -> k_paths_ball, per 256-slot block
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
   uint2* path_sab;   // per chosen transition: offsets (cm) of its source and target candidates on their roads
   SegmentRec* segs; uint32_t* seg_base; uint32_t* seg_cnt;
@@ -734,15 +733,6 @@ __device__ __forceinline__ unsigned long long route_key(const Label& label, cons
   return route_key_vals(a0, b0, b1, lab0, lab1, combo);
 }
 
-// route[] word of a valid route: distance cm (<= kMaxBoundCm < 2^30) plus, when the best
-// combination runs along the source's own road (combo 0 / 1), a flag bit telling the path
-// stage the route is that one edge, so it skips the labels and the walk (most chosen
-// transitions at 1-5 s sampling).  kRouteInvalid (all ones) stays distinct.
-constexpr uint32_t kRouteDirF = 1u << 31, kRouteDirR = 1u << 30, kRouteDistMask = kRouteDirR - 1u;
-__device__ __forceinline__ uint32_t route_word(unsigned long long key, int combo) {
-  return key_dist(key) | (combo == 0 ? kRouteDirF : 0u) | (combo == 1 ? kRouteDirR : 0u);
-}
-
 // root keys of a source candidate's two exits (forward to node1, reverse to node0)
 __device__ __forceinline__ void exit_keys(const uint4& a0, uint32_t bound, unsigned long long& rk1,
                                           unsigned long long& rk0) {
@@ -1054,10 +1044,9 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
     }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
-      int cb = -1;
-      const unsigned long long key = route_key(lab, a0, t0[x], t1[x], &cb);
+      const unsigned long long key = route_key(lab, a0, t0[x], t1[x], nullptr);
       uint32_t r = kRouteInvalid;
-      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = route_word(key, cb);
+      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
       res[((j0 + x) & (kMaxCand - 1)) * stride] = r;
     }
   }
@@ -1165,10 +1154,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
         const uint4 r0 = ball_resolve(ent, h0, t0.x, e0);
         const unsigned long long lab0 = ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
         const unsigned long long lab1 = ball_label(rk1, row_key1(r1), rk0, row_key1(r0));
-        int cb = -1;
-        const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, &cb);
+        const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, nullptr);
         uint32_t rt = kRouteInvalid;
-        if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = route_word(key, cb);
+        if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = key_dist(key);
         res[j] = rt;
       }
     }
@@ -1420,74 +1408,36 @@ struct BallPathLabels {
   }
 };
 
-// path direct tier: one lane per slot.  A chosen transition whose route K2 found along the
-// source's own road (route_word's flags: most of them at 1-5 s sampling) is one edge and is
-// written here; the others are compacted within the block (path_list, count path_list_n per
-// block; no global atomics) for the ball tier, so its waves hold only transitions that probe
-// tables and walk.
-__global__ void __launch_bounds__(256) k_paths_direct(DevGraph g, DevBatch b) {
-  __shared__ uint32_t s_wn[4];
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool walk = false;
-  if (p < b.P) {
-    const uint32_t k = b.slot_trace[p];
-    const uint32_t o = b.trace_off[k];
-    const uint32_t s = (uint32_t)(p - o);
-    if (s >= 1 && s < b.n_states[k] && !b.chain_start[p] && b.choice[p] >= 0) {
-      const uint32_t KB = (b.pair_info[p].z >> 8) & 0xffu;
-      const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
-      const uint32_t rw = b.route[b.trans_off[p] + i * KB + j];
-      if (rw & (kRouteDirF | kRouteDirR)) {
-        const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2];
-        const uint32_t sb = b.cand_desc[(p * kMaxCand + j) * 2].y;
-        b.route_dist[p] = rw & kRouteDistMask;
-        b.path_sab[p] = make_uint2(a0.y, sb);
-        b.path_inline[p * kInlinePath] = (rw & kRouteDirF) ? g.road_fwd[a0.x] : g.road_rev[a0.x];
-        b.path_cnt[p] = 1;
-        b.path_off[p] = 0;
-      } else {
-        walk = true;
-      }
-    }
-  }
-  const unsigned long long m = __ballot(walk);
-  const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63u);
-  if (lane == 0) s_wn[w] = (uint32_t)__popcll(m);
-  __syncthreads();
-  uint32_t at = 0;
-  for (int x = 0; x < w; ++x) at += s_wn[x];
-  if (walk) b.path_list[(uint64_t)blockIdx.x * 256u + at + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)p;
-  if (threadIdx.x == 0) b.path_list_n[blockIdx.x] = s_wn[0] + s_wn[1] + s_wn[2] + s_wn[3];
-}
-
-// path ball tier: block B takes block B's list of k_paths_direct, one lane per transition whose
-// bound fits the ball radius; the others go to the search tiers (rl_routes_0 reused after K2,
-// count ctl[8])
+// path ball tier: one lane per chosen transition whose bound fits the ball radius; the
+// others go to the search tiers (rl_routes_0 reused after K2, count ctl[8])
 __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
-  if (threadIdx.x >= b.path_list_n[blockIdx.x]) return;
-  {
-    const uint64_t p = b.path_list[(uint64_t)blockIdx.x * 256u + threadIdx.x];
-    const uint4 pi = b.pair_info[p];
-    const int mode = (int)(pi.z >> 16);
-    const uint32_t bound = pi.x;
-    const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
-    const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
-    const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-    unsigned long long rk1, rk0;
-    exit_keys(a0, bound, rk1, rk0);
-    const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
-    const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
-    if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {
-      b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
-      return;
-    }
-    const BallPathLabels lab{g.ball_ent[mode], h1, h0, rk1, rk0};
-    const unsigned long long lab0 = d_spf(b0) ? lab(b1.x, b0.x, 0u) : kKeyInf;
-    const unsigned long long lab1 = d_spr(b0) ? lab(b1.y, b0.x, 1u) : kKeyInf;
-    int combo = -1;
-    const unsigned long long key = route_key_vals(a0, b0, b1, lab0, lab1, &combo);
-    path_walk(g, b, p, lab, mode, a0, a1, b0, b1, rk1, rk0, key, combo, (int)kBallMaxKeys);
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= b.P) return;
+  const uint32_t k = b.slot_trace[p];
+  const uint32_t o = b.trace_off[k];
+  const uint32_t s = (uint32_t)(p - o);
+  if (s < 1 || s >= b.n_states[k]) return;
+  if (b.chain_start[p] || b.choice[p] < 0) return;
+  const uint4 pi = b.pair_info[p];
+  const int mode = (int)(pi.z >> 16);
+  const uint32_t bound = pi.x;
+  const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+  const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
+  const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
+  unsigned long long rk1, rk0;
+  exit_keys(a0, bound, rk1, rk0);
+  const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
+  const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+  if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {
+    b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
+    return;
   }
+  const BallPathLabels lab{g.ball_ent[mode], h1, h0, rk1, rk0};
+  const unsigned long long lab0 = d_spf(b0) ? lab(b1.x, b0.x, 0u) : kKeyInf;
+  const unsigned long long lab1 = d_spr(b0) ? lab(b1.y, b0.x, 1u) : kKeyInf;
+  int combo = -1;
+  const unsigned long long key = route_key_vals(a0, b0, b1, lab0, lab1, &combo);
+  path_walk(g, b, p, lab, mode, a0, a1, b0, b1, rk1, rk0, key, combo, (int)kBallMaxKeys);
 }
 
 // path lane tier: one lane per chosen transition, labels in registers.  With `listed`,
@@ -1568,10 +1518,9 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
   if (ok) {
     for (uint32_t j = lane; j < KB; j += kWave) {
       const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-      int cb = -1;
-      const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, &cb);
+      const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, nullptr);
       uint32_t out = kRouteInvalid;
-      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = route_word(key, cb);
+      if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
       b.route[base + i * KB + j] = out;
     }
   }
@@ -1840,7 +1789,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     // ---- chunk -> LDS
 #pragma unroll
     for (int x = 0; x < kVitRoutes / 16; ++x)
-      if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)(rv[x] & kRouteDistMask) * 0.01;
+      if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
     {
       float4* sqdst = reinterpret_cast<float4*>(&gs.sq[0][0]);
       const uint32_t nf = C * (kMaxCand / 4);
@@ -1895,7 +1844,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
           if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
 #pragma unroll
         for (int x = 0; x < kVitRoutes / 16; ++x)
-          if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)(rv[x] & kRouteDistMask) * 0.01;
+          if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
         wave_sync();
       }
       if (t + 1 < C) {   // next layer's first route rows (after any re-staging above)
@@ -2986,7 +2935,6 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
   w.trans_cnt = dalloc<uint32_t>(L, cp); w.trans_off = dalloc<uint32_t>(L, cp); w.gc = dalloc<double>(L, cp);
   w.src_cnt = dalloc<uint32_t>(L, cp); w.src_off = dalloc<uint32_t>(L, cp);
   w.choice = dalloc<int8_t>(L, cp); w.chain_start = dalloc<uint8_t>(L, cp); w.bp = dalloc<uint8_t>(L, cp * kMaxCand);
-  w.path_list = dalloc<uint32_t>(L, cp + 256); w.path_list_n = dalloc<uint32_t>(L, cp / 256 + 2);
   w.path_off = dalloc<uint32_t>(L, cp); w.path_cnt = dalloc<uint32_t>(L, cp); w.route_dist = dalloc<uint32_t>(L, cp);
   w.path_sab = dalloc<uint2>(L, cp);
   w.path_inline = dalloc<uint32_t>(L, cp * kInlinePath);
@@ -3106,7 +3054,6 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
-  v.path_list = w.path_list; v.path_list_n = w.path_list_n;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
   v.path_pool = w.path_pool; v.path_cap = w.cap_path;
   v.route_dist = w.route_dist; v.path_sab = w.path_sab;
@@ -3260,7 +3207,6 @@ void Matcher::run_device(const RunParams& rp) {
       RM_HIP(hipMemsetAsync(w.ctl + 10, 0, sizeof(uint32_t), st));   // paths list C
     }
     if (balls) {
-      hipLaunchKernelGGL(k_paths_direct, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
       hipLaunchKernelGGL(k_paths_ball, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>((P + 255) / 256, kListedGrid)), dim3(256), 0,
                          st, g, v, 1);
@@ -3413,11 +3359,7 @@ void Matcher::get_routes(uint32_t* trans_off, double* gc, uint32_t* route) {
   sync();
   RM_HIP(hipMemcpy(trans_off, ws_.trans_off, n_points_ * 4, hipMemcpyDeviceToHost));
   RM_HIP(hipMemcpy(gc, ws_.gc, n_points_ * 8, hipMemcpyDeviceToHost));
-  if (n_trans_) {
-    RM_HIP(hipMemcpy(route, ws_.route, n_trans_ * 4, hipMemcpyDeviceToHost));
-    for (uint64_t q = 0; q < n_trans_; ++q)   // drop the direct-route flags (route_word)
-      if (route[q] != kRouteInvalid) route[q] &= 0x3fffffffu;
-  }
+  if (n_trans_) RM_HIP(hipMemcpy(route, ws_.route, n_trans_ * 4, hipMemcpyDeviceToHost));
 }
 void Matcher::get_viterbi(int8_t* choice, uint8_t* chain_start) {
   sync();

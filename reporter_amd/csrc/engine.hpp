@@ -110,7 +110,6 @@ struct Workspace {
   uint4* pair_info = nullptr;  // per layer pair slot: {route bound cm, time bound ms, KA | KB << 8 | mode << 16, 0}
   uint32_t* src_cnt = nullptr; uint32_t* src_off = nullptr; uint32_t* src_item = nullptr;
   int8_t* choice = nullptr; uint8_t* chain_start = nullptr; uint8_t* bp = nullptr;
-  uint32_t* path_list = nullptr; uint32_t* path_list_n = nullptr;   // path stage: transitions to walk, per block
   uint32_t* path_off = nullptr; uint32_t* path_cnt = nullptr; uint32_t* path_pool = nullptr; uint32_t* route_dist = nullptr;
   uint2* path_sab = nullptr;        // per chosen transition: source / target candidate offsets on their roads (cm)
   uint32_t* path_inline = nullptr;  // kInlinePath edges per slot
