@@ -121,8 +121,20 @@ int rm_engine_segment_ids(const rm_engine* e, uint64_t* ids); /* n_segments ids 
 int rm_engine_set_ball_radius(rm_engine* e, double radius_m);
 /* Host-only: the engine's automatic radius for a graph file — the largest of 2000 m (meili's
  * default breakage distance, so every default-bounded transition is a table probe), 1500,
- * 1000, 700, 500 m whose estimated tables stay within 72 GiB per mode (of 288 GB); else 400 m. */
+ * 1000, 700, 500 m whose estimated tables stay within 72 GiB per mode (RM_BALL_BUDGET_GB) and
+ * 2^33 rows; else 400 m. */
 int rm_graph_auto_ball_radius(const char* graph_path, double* radius_m);
+/* Host-only: the radius a travel mode's tables are built at when avail_gb GiB of HBM are left
+ * for them — the largest of start_m and the radii below it (2000, 1500, 1000, 700, 500, 400,
+ * 300, 200 m) whose sampled tables for that mode (+10 %) fit avail_gb and 2^33 rows; 0 when none
+ * does (the mode's transitions then run in the search tiers).  The engine applies it per mode
+ * with avail = min(per-mode budget, half the device's HBM less earlier modes' tables, free HBM
+ * less 4 GiB); auto and bus share one build. */
+int rm_graph_fit_ball_radius(const char* graph_path, int mode, double start_m, double avail_gb, double* radius_m);
+/* Host-only: sampled ball statistics of `mode` at radius_m (bounded searches from 256 nodes):
+ * out[3] = mean nodes per ball, estimated table bytes of all nodes, fraction of balls above
+ * 4096 nodes. */
+int rm_graph_ball_sample(const char* graph_path, int mode, double radius_m, double out[3]);
 /* out[6]: radius m, keys stored, table entries (16 B each), nodes without a table, build ms,
  * 1 when the tables were built on the GPU (small balls on large graphs; env RM_BALL_BUILD=host|gpu) */
 int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]);

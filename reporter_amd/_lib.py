@@ -99,6 +99,8 @@ PROTOTYPES = [
     ("rm_runner_route_tiers", C.c_int, [P, P]),
     ("rm_balls_lookup", C.c_int, [C.c_char_p, C.c_int, C.c_double, C.c_uint64, P, P, P]),
     ("rm_graph_auto_ball_radius", C.c_int, [C.c_char_p, P]),
+    ("rm_graph_fit_ball_radius", C.c_int, [C.c_char_p, C.c_int, C.c_double, C.c_double, P]),
+    ("rm_graph_ball_sample", C.c_int, [C.c_char_p, C.c_int, C.c_double, P]),
     ("rm_graph_grid_split", C.c_int, [C.c_char_p, P]),
     ("rm_runner_create", P, [P]),
     ("rm_runner_destroy", None, [P]),

@@ -117,12 +117,13 @@ void parallel_nodes(uint32_t n, int threads, F&& f) {
 // at 136 GB (they are 68 GB) and picked 700 m.
 struct BallSampler {
   const Graph& g;
-  explicit BallSampler(const Graph& gr) : g(gr) {}
+  int mode;
+  BallSampler(const Graph& gr, int m) : g(gr), mode(m) {}
   BallSample at(uint32_t radius_cm, uint32_t max_keys) const {
     BallSample out;
     const uint32_t N = g.num_nodes();
     const uint32_t S = std::min<uint32_t>(N, 256u);
-    const uint32_t acc = mode_access(kModeAuto);
+    const uint32_t acc = mode_access(mode);
     double nodes = 0, slots = 0;
     uint32_t skipped = 0;
     std::unordered_map<uint32_t, uint64_t> lab;
@@ -146,7 +147,7 @@ struct BallSampler {
           const EdgeRec& r = g.edges[e];
           roads.insert(r.road >> 1);
           if (!(edge_access(r.info) & acc)) continue;
-          const uint64_t nk = it.first + make_key(r.len_cm, time_ms(r.len_cm, mode_speed_dkph(kModeAuto, edge_speed_dkph(r.info))));
+          const uint64_t nk = it.first + make_key(r.len_cm, time_ms(r.len_cm, mode_speed_dkph(mode, edge_speed_dkph(r.info))));
           if (key_dist(nk) > radius_cm) continue;
           auto f = lab.find(r.target);
           if (f == lab.end() || nk < f->second) {
@@ -166,10 +167,57 @@ struct BallSampler {
   }
 };
 
-BallSample sample_balls(const Graph& g, uint32_t radius_cm, uint32_t max_keys) {
+BallSample sample_balls(const Graph& g, uint32_t radius_cm, uint32_t max_keys, int mode) {
   if (g.num_nodes() == 0) return BallSample{};
-  BallSampler bs(g);
+  BallSampler bs(g, mode);
   return bs.at(radius_cm, max_keys);
+}
+
+namespace {
+// sampled tables of one mode fit `avail` bytes (+10 %) and the row cap, and most balls fit
+bool sample_fits(const BallSample& bs, uint64_t avail_bytes) {
+  const double bytes = bs.table_bytes * 1.1;
+  return bs.skipped_frac <= 0.05 && bytes <= (double)avail_bytes && bytes <= (double)kBallMaxRows * 16.0;
+}
+double env_gb(const char* name) {
+  const char* s = std::getenv(name);
+  return s ? std::atof(s) : 0.0;
+}
+}  // namespace
+
+uint64_t ball_mode_budget() {
+  const double gb = env_gb("RM_BALL_BUDGET_GB");
+  return gb > 0.0 ? (uint64_t)(gb * (double)(1ull << 30)) : kBallAutoBudget;
+}
+
+uint64_t ball_total_budget(uint64_t hbm_total) {
+  const double gb = env_gb("RM_BALL_TOTAL_GB");
+  return gb > 0.0 ? (uint64_t)(gb * (double)(1ull << 30)) : hbm_total / 2;
+}
+
+uint32_t next_ball_radius_cm(uint32_t r_cm) {
+  for (const uint32_t r : kBallRadii)
+    if (r < r_cm) return r;
+  return 0u;
+}
+
+uint32_t fit_ball_radius_cm(const Graph& g, int mode, uint32_t start_cm, uint64_t avail_bytes, BallSample* sample) {
+  if (g.num_nodes() < 2 || start_cm == 0) return start_cm;
+  BallSampler sampler(g, mode);
+  for (uint32_t r = start_cm; r; r = next_ball_radius_cm(r)) {
+    const BallSample bs = sampler.at(r, kBallMaxKeysHost);
+    if (!sample_fits(bs, avail_bytes)) continue;
+    if (sample) *sample = bs;
+    return r;
+  }
+  return 0u;
+}
+
+int ball_twin_mode(int mode) {
+  // bus routes exactly as auto: same access bit, no speed cap (rm_common.hpp mode_speed_dkph)
+  if (mode == kModeBus) return kModeAuto;
+  if (mode == kModeAuto) return kModeBus;
+  return -1;
 }
 
 double est_ball_nodes(const Graph& g, uint32_t radius_cm) {
@@ -194,25 +242,17 @@ void road_incidence(const Graph& g, std::vector<uint32_t>& inc_off, std::vector<
 }
 
 uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes) {
-  if (budget_bytes == 0) {
-    budget_bytes = kBallAutoBudget;
-    if (const char* s = std::getenv("RM_BALL_BUDGET_GB")) {
-      const double gb = std::atof(s);
-      if (gb > 0.0) budget_bytes = (uint64_t)(gb * (double)(1ull << 30));
-    }
-  }
+  if (budget_bytes == 0) budget_bytes = ball_mode_budget();
   const uint32_t N = g.num_nodes();
   if (N < 2) return 40000u;
-  BallSampler sampler(g);
-  for (const uint32_t r : {200000u, 150000u, 100000u, 70000u, 50000u}) {
-    const BallSample bs = sampler.at(r, kBallMaxKeysHost);
-    // most balls must get a table, and the tables must fit the budget (sampled sizes, +10 %)
-    if (bs.skipped_frac <= 0.05 && bs.table_bytes * 1.1 <= (double)budget_bytes) return r;
-  }
+  BallSampler sampler(g, kModeAuto);
+  for (const uint32_t r : {200000u, 150000u, 100000u, 70000u, 50000u})
+    if (sample_fits(sampler.at(r, kBallMaxKeysHost), budget_bytes)) return r;
   return 40000u;
 }
 
-void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys, int threads, BallTables& out) {
+void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys, int threads, BallTables& out,
+                 uint64_t max_rows) {
   const auto t0 = std::chrono::steady_clock::now();
   const uint32_t N = g.num_nodes(), E = g.num_edges();
   const uint32_t acc = mode_access(mode);
@@ -246,11 +286,11 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
   uint64_t total = 0;
   out.n_skipped = 0;
   for (uint32_t u = 0; u < N; ++u) {
-    out.hdr[2 * (size_t)u] = (uint32_t)total;
+    out.hdr[2 * (size_t)u] = (uint32_t)(total >> 1);   // first row / 2 (rm_common.hpp ball_row0)
     out.hdr[2 * (size_t)u + 1] = bits[u];
     if (bits[u]) total += 1ull << bits[u];
     else out.n_skipped++;
-    if (total >= 0xffffffffull) throw std::runtime_error("route balls too large (entries >= 2^32); lower the radius");
+    if (total > std::min(kBallMaxRows, max_rows)) throw BallsTooLarge("route balls too large for their budget; lower the radius");
   }
   out.ent.assign(4 * total, 0);
   for (uint64_t i = 0; i < total; ++i) out.ent[4 * i] = kNone;
@@ -262,7 +302,7 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
     RoadAcc& ra = acc_r[t];
     ra.collect(g, inc_off, inc, scr[t].out);
     const uint32_t b = bits[u], mask = (1u << b) - 1u;
-    uint32_t* tab = out.ent.data() + 4 * (size_t)out.hdr[2 * (size_t)u];
+    uint32_t* tab = out.ent.data() + 4 * ball_row0(out.hdr[2 * (size_t)u]);
     for (size_t q = 0; q < ra.roads.size(); ++q) {
       uint32_t s = ball_slot(ra.roads[q], b);
       while (tab[4 * s] != kNone) s = (s + 1) & mask;

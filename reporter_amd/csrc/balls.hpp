@@ -15,6 +15,7 @@
 // (the engine's graph-load step); the tables live in HBM next to the graph.
 #pragma once
 #include <cstdint>
+#include <stdexcept>
 #include <vector>
 
 #include "graph.hpp"
@@ -37,26 +38,53 @@ struct BallTables {
 constexpr uint32_t kBallMaxKeysHost = 4096;   // ball nodes above which a node gets no table
 constexpr uint32_t kBallMaxRadiusCm = 1000000;   // 10 km knob cap (rows hold 24-bit distances)
 
+// Tables that would exceed kBallMaxRows (rm_common.hpp) or the memory granted to them: the
+// caller steps the radius down instead of failing.
+struct BallsTooLarge : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
 // Default radius for a graph: the largest of {2000 (meili's default breakage distance, so
 // every default-bounded transition is a table probe), 1500, 1000, 700, 500} m whose tables
 // (sampled: sample_balls, +10 %) stay within `budget_bytes` per mode and whose balls mostly
 // fit kBallMaxKeysHost; 400 m when none does.
 constexpr uint64_t kBallAutoBudget = 72ull << 30;   // per mode; C4: 1000 m (68 GB built)
-// budget 0: kBallAutoBudget, or RM_BALL_BUDGET_GB when set (the HBM a deployment grants the tables)
+// budget 0: ball_mode_budget() (kBallAutoBudget, or RM_BALL_BUDGET_GB when set)
 uint32_t auto_ball_radius_cm(const Graph& g, uint64_t budget_bytes = 0);
+uint64_t ball_mode_budget();
+// bytes all modes' tables together may take on a device with `hbm_total` bytes: half of it
+// (the other half holds the graph and the batch workspaces: ~0.75 KB per point), or
+// RM_BALL_TOTAL_GB when set
+uint64_t ball_total_budget(uint64_t hbm_total);
 
-void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys, int threads, BallTables& out);
+// Radii (cm) the per-mode choice steps down through, largest first.
+constexpr uint32_t kBallRadii[] = {200000u, 150000u, 100000u, 70000u, 50000u, 40000u, 30000u, 20000u};
+// The radius a mode's tables are built at: the largest of kBallRadii at or below start_cm
+// (start_cm itself first when it is not on the ladder) whose sampled tables for THIS mode
+// (+10 %) fit both `avail_bytes` and kBallMaxRows, and whose balls mostly fit
+// kBallMaxKeysHost; 0 when none does (the mode's transitions use the search tiers).
+uint32_t fit_ball_radius_cm(const Graph& g, int mode, uint32_t start_cm, uint64_t avail_bytes,
+                            struct BallSample* sample = nullptr);
+// next radius below r_cm on the ladder (0 when none)
+uint32_t next_ball_radius_cm(uint32_t r_cm);
+// Travel modes whose tables are identical (same access mask and routing speeds: auto and
+// bus) share one build: the mode whose tables `mode` can reuse, or -1.
+int ball_twin_mode(int mode);
+
+// throws BallsTooLarge (before allocating the rows) when the tables need more than max_rows rows
+void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys, int threads, BallTables& out,
+                 uint64_t max_rows = kBallMaxRows);
 
 // node -> incident roads CSR (every road listed at node0 and at node1)
 void road_incidence(const Graph& g, std::vector<uint32_t>& inc_off, std::vector<uint32_t>& inc);
 
-// sampled ball statistics at a radius (exact bounded searches from 256 nodes, auto mode)
+// sampled ball statistics at a radius (exact bounded searches of `mode` from 256 nodes)
 struct BallSample {
   double nodes = 0;          // mean nodes per ball
   double table_bytes = 0;    // estimated bytes of all nodes' power-of-two tables
   double skipped_frac = 0;   // sampled balls above max_keys (no table)
 };
-BallSample sample_balls(const Graph& g, uint32_t radius_cm, uint32_t max_keys);
+BallSample sample_balls(const Graph& g, uint32_t radius_cm, uint32_t max_keys, int mode = 0);
 // nodes an average ball of radius_cm holds (sampled); the engine builds small balls on the GPU
 double est_ball_nodes(const Graph& g, uint32_t radius_cm);
 

@@ -26,6 +26,7 @@
 #include "engine.hpp"
 #include "graph.hpp"
 #include "json.hpp"
+#include "serve_policy.hpp"
 
 using namespace rm;
 
@@ -331,30 +332,29 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
 }
 
 // Run `batch` and fill each request's reply or error.  A failure that belongs to one trace is
-// reported per trace by the engine; anything that still fails a whole batch (a device or
-// capacity error) is retried by halves, so only the requests that fail on their own get an error.
+// reported per trace by the engine; a whole-batch failure follows serve_policy.hpp: a batch too
+// large for the device is retried by halves (bounded), any other error fails every request in
+// it at once.  A failed run drops the matcher, so what follows starts on a fresh workspace.
 void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch) {
-  std::vector<std::string> outs, errs;
-  try {
-    if (!m) m = std::make_unique<Matcher>(eng);
-    std::vector<ParsedTrace*> pt;
-    for (MatchRequest* r : batch) pt.push_back(r->trace);
-    outs = match_parsed(*m, pt, &errs);
-  } catch (const std::exception& e) {
-    m.reset();   // a fresh workspace for what follows
-    if (batch.size() > 1) {
-      const size_t h = batch.size() / 2;
-      serve_batch(m, eng, std::vector<MatchRequest*>(batch.begin(), batch.begin() + h));
-      serve_batch(m, eng, std::vector<MatchRequest*>(batch.begin() + h, batch.end()));
-      return;
+  int budget = kServeRetryBudget;
+  auto run = [&](MatchRequest* const* reqs, size_t n) {
+    try {
+      if (!m) m = std::make_unique<Matcher>(eng);
+      std::vector<ParsedTrace*> pt(n);
+      for (size_t i = 0; i < n; ++i) pt[i] = reqs[i]->trace;
+      std::vector<std::string> errs;
+      std::vector<std::string> outs = match_parsed(*m, pt, &errs);
+      for (size_t i = 0; i < n; ++i) {
+        if (!errs[i].empty()) reqs[i]->err = errs[i];
+        else reqs[i]->out = std::move(outs[i]);
+      }
+    } catch (...) {
+      m.reset();
+      throw;
     }
-    batch[0]->err = e.what();
-    return;
-  }
-  for (size_t i = 0; i < batch.size(); ++i) {
-    if (!errs[i].empty()) batch[i]->err = errs[i];
-    else batch[i]->out = std::move(outs[i]);
-  }
+  };
+  auto fail = [](MatchRequest* r, const char* msg) { r->err = msg; };
+  serve_split(batch.data(), batch.size(), run, fail, budget);
 }
 
 void Coalescer::loop() {
@@ -454,10 +454,25 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
       if (const json::Value* mx = ra->get("coalesce_max_traces"); mx && mx->is_num()) max_traces = (size_t)mx->num;
       if (const json::Value* wk = ra->get("coalesce_workers"); wk && wk->is_num()) workers = (int)wk->num;
     }
+    // travel modes whose route tables are built now, so no request waits for a build (the Java
+    // caller gives up after 10 s, HttpClient.java:80-87): auto (the default mode), every mode
+    // with its own meili section, and reporter_amd.modes
+    uint32_t modes = 1u << kModeAuto;
+    for (int m = 0; m < 5; ++m)
+      if (meili && meili->get(kModeNames[m])) modes |= 1u << m;
+    if (const json::Value* ra = v.get("reporter_amd")) {
+      if (const json::Value* ml = ra->get("modes")) {
+        if (ml->type != json::Value::Array) throw std::runtime_error("reporter_amd.modes must be a list of mode names");
+        for (const json::Value& x : ml->arr) {
+          if (x.type != json::Value::String) throw std::runtime_error("reporter_amd.modes must be a list of mode names");
+          modes |= 1u << mode_from_name(x.str);
+        }
+      }
+    }
     Graph g = Graph::load(graph);
     conf->engine = std::make_shared<Engine>(g, device);
     if (ball_radius_m >= 0.0) conf->engine->set_ball_radius((uint32_t)(ball_radius_m * 100.0));
-    conf->engine->ensure_balls(1u << kModeAuto);   // the service's default mode: no build on the first request
+    conf->engine->ensure_balls(modes);
     if (coalesce) conf->coalescer = std::make_unique<Coalescer>(conf->engine, window_ms, max_traces, workers);
     std::lock_guard<std::mutex> lk(g_mu);
     g_conf = conf;
@@ -635,7 +650,7 @@ int rm_engine_set_ball_radius(rm_engine* e, double radius_m) {
 int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]) {
   return guarded([&] {
     if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
-    out[0] = e->e->ball_radius() / 100.0;
+    out[0] = e->e->mode_ball_radius(mode) / 100.0;
     e->e->ball_stats(mode, out + 1);
     out[5] = ((e->e->ball_gpu_mask() >> mode) & 1u) ? 1.0 : 0.0;
   });
@@ -668,6 +683,27 @@ int rm_graph_auto_ball_radius(const char* graph_path, double* radius_m) {
   });
 }
 
+int rm_graph_fit_ball_radius(const char* graph_path, int mode, double start_m, double avail_gb, double* radius_m) {
+  return guarded([&] {
+    if (!graph_path || !radius_m) throw std::runtime_error("path or radius_m is NULL");
+    if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    if (!(start_m >= 0.0) || start_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..10000 m)");
+    if (!(avail_gb >= 0.0)) throw std::runtime_error("avail_gb must be non-negative");
+    const uint64_t avail = (uint64_t)std::min(avail_gb * (double)(1ull << 30), 1.8e19);
+    *radius_m = fit_ball_radius_cm(Graph::load(graph_path), mode, (uint32_t)(start_m * 100.0), avail) / 100.0;
+  });
+}
+
+int rm_graph_ball_sample(const char* graph_path, int mode, double radius_m, double out[3]) {
+  return guarded([&] {
+    if (!graph_path || !out) throw std::runtime_error("path or out is NULL");
+    if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    if (!(radius_m >= 0.0) || radius_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..10000 m)");
+    const BallSample bs = sample_balls(Graph::load(graph_path), (uint32_t)(radius_m * 100.0), kBallMaxKeysHost, mode);
+    out[0] = bs.nodes; out[1] = bs.table_bytes; out[2] = bs.skipped_frac;
+  });
+}
+
 int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t n, const uint32_t* from,
                     const uint32_t* road, uint64_t* keys) {
   return guarded([&] {
@@ -683,7 +719,7 @@ int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t 
       if (!bits) continue;
       const uint32_t mask = (1u << bits) - 1u;
       for (uint32_t s = ball_slot(road[i], bits);; s = (s + 1) & mask) {
-        const uint32_t* e = bt.ent.data() + 4 * ((size_t)off + s);
+        const uint32_t* e = bt.ent.data() + 4 * (ball_row0(off) + s);
         if (e[0] == kNone) break;
         if (e[0] != road[i]) continue;
         keys[2 * i] = ball_key0(e[0], e[1], e[3]);

@@ -46,10 +46,7 @@ constexpr int kSmallH = 256;    // LDS hash slots, fast tier
 constexpr int kBigH = 4096;     // LDS hash slots, retry tier (one source at a time)
 constexpr int kCandH = 256;     // road hash slots in the candidate kernel
 constexpr int kInlinePath = 8;  // path edges stored inline per slot (no allocation)
-#ifndef RM_LDS_GRID
-#define RM_LDS_GRID 2048
-#endif
-constexpr int kLdsGrid = RM_LDS_GRID;  // blocks of the LDS lane tiers (grid-stride over their work lists)
+constexpr int kReg2Grid = 512;  // blocks of the second register tiers (grid-stride over their work lists)
 constexpr uint32_t kMaxBoundCm = 100000000u;
 constexpr double kQueueSpeedMps = 2.7777777777777777;  // 10 km/h
 
@@ -889,8 +886,8 @@ struct HashLabel {
 // Edges are read as per-mode relax records {target, len_cm | kNoLen, time_ms, target's
 // CSR range}: a settled node's label already holds its out-edge range, so each settle is
 // ONE dependent round trip (the node's edge records), not two (offsets, then edges).
-// Labels live in registers (kLaneCap slots, the common case) or, for searches that
-// outgrow them, in LDS (kLdsCap slots per lane); keys are exact, so every store agrees.
+// Labels live in registers (kLaneCap slots, the common case; kTier2Cap in the second tier);
+// keys are exact, so every store agrees.
 #ifndef RM_LANE_CAP
 #define RM_LANE_CAP 7
 #endif
@@ -898,10 +895,6 @@ constexpr int kLaneCap = RM_LANE_CAP;
 #ifndef RM_LANE_WPE
 #define RM_LANE_WPE 4   // waves per SIMD the register lane tiers are compiled for
 #endif
-#ifndef RM_LDS_CAP
-#define RM_LDS_CAP 16
-#endif
-constexpr int kLdsCap = RM_LDS_CAP;
 constexpr uint32_t kNoLen = 0xffffffffu;
 
 template <int CAP>
@@ -948,46 +941,6 @@ struct RegLabelsT {
   }
 };
 using RegLabels = RegLabelsT<kLaneCap>;
-
-// labels in LDS, lane-minor ([slot][64]) so a wave's accesses to one slot are conflict-free
-struct LdsLabels {
-  uint32_t* node;
-  uint32_t* rng;
-  unsigned long long* key;
-  uint32_t n;
-  unsigned long long settled;
-  bool ovf;
-  __device__ __forceinline__ void init() { n = 0; settled = 0; ovf = false; }
-  __device__ __forceinline__ unsigned long long label(uint32_t v) const {
-    for (uint32_t x = 0; x < n; ++x)
-      if (node[x * kWave] == v) return key[x * kWave];
-    return kKeyInf;
-  }
-  __device__ __forceinline__ void relax(uint32_t v, unsigned long long k, uint32_t r, uint32_t) {
-    for (uint32_t x = 0; x < n; ++x)
-      if (node[x * kWave] == v) {
-        if (k < key[x * kWave]) key[x * kWave] = k;
-        return;
-      }
-    if (n >= (uint32_t)kLdsCap) { ovf = true; return; }
-    node[n * kWave] = v; key[n * kWave] = k; rng[n * kWave] = r;
-    n++;
-  }
-  __device__ __forceinline__ bool pick(unsigned long long& bk, uint32_t& r, uint32_t& u, uint32_t& from) {
-    int bi = -1;
-    bk = kKeyInf;
-    for (uint32_t x = 0; x < n; ++x) {
-      const unsigned long long kx = key[x * kWave];
-      if (!((settled >> x) & 1ull) && kx < bk) { bk = kx; bi = (int)x; }
-    }
-    if (bi < 0) return false;
-    settled |= 1ull << bi;
-    r = rng[bi * kWave];
-    u = node[bi * kWave];
-    from = kNone;   // no parent kept here: every out-edge is relaxed
-    return true;
-  }
-};
 
 template <class L>
 struct StoreLabel {
@@ -1068,7 +1021,7 @@ __device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, 
   uint32_t s = ball_slot(road, h.y);
   for (;;) {
     s = (s + 1u) & mask;
-    e = ent[h.x + s];
+    e = ent[ball_row0(h.x) + s];
     if (e.x == road || e.x == kNone) return e;
   }
 }
@@ -1077,16 +1030,12 @@ __device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, 
 // (block i runs on XCD i % 8), so consecutive work (the pairs of one trace) would land
 // in 8 different L2s.  Renumber so each XCD gets one contiguous range of logical blocks.
 __device__ __forceinline__ uint32_t xcd_block(uint32_t i, uint32_t n) {
-#ifdef RM_NO_XCD_REMAP
-  return i;
-#else
   const uint32_t x = i & 7u, idx = i >> 3, q = n >> 3, r = n & 7u;
   return x < r ? x * (q + 1u) + idx : r * (q + 1u) + (x - r) * q + idx;
-#endif
 }
 
 __device__ __forceinline__ uint4 ball_first(const uint4* ent, const uint2& h, uint32_t road, bool use) {
-  return use ? ent[h.x + ball_slot(road, h.y)] : make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+  return use ? ent[ball_row0(h.x) + ball_slot(road, h.y)] : make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
 }
 
 // keys from a row (kKeyInf for an endpoint outside the ball or a road not in the table)
@@ -1136,9 +1085,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     unsigned long long rk1, rk0;
     exit_keys(a0, bound, rk1, rk0);
     const uint4* ent = g.ball_ent[mode];
-    const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
-    const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
-    if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {   // search tiers take it (they run later)
+    // a mode without tables has radius 0 (and no header array): every bound > 0 hands over
+    const bool fits = bound <= g.ball_radius[mode] && ((g.ball_mask >> mode) & 1u);
+    const uint2 h1 = fits && rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
+    const uint2 h0 = fits && rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+    if (!fits || h1.y == 0u || h0.y == 0u) {   // search tiers take it (they run later)
       for (uint32_t j = 0; j < KB; ++j) res[j] = kRouteInvalid;
       b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
     } else {
@@ -1197,14 +1148,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
   }
 }
 
-#ifdef RM_ALL_LDS
-__global__ void k_all_items(DevBatch b, uint32_t n) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n) b.rl_routes_a[t] = t;
-  if (t == 0) b.ctl[3] = n;
-}
-#endif
-
 // K2 second register tier: the items the first tier queued, RM_TIER2_CAP labels per lane
 // (compiled for fewer waves per SIMD); what still overflows goes to the wave tier.
 #ifndef RM_TIER2_CAP
@@ -1234,36 +1177,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
     }
     route_targets(b, StoreLabel<RegLabelsT<kTier2Cap>>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB,
                   &s_res[0][threadIdx.x], 256);
-  }
-}
-
-// K2 LDS lane tier: the items the register tier queued, kLdsCap labels per lane in LDS.
-// Grid-stride over the device-side list; what still overflows goes to the wave tier.
-__global__ void __launch_bounds__(64) k_routes_lds(DevGraph g, DevBatch b) {
-  __shared__ uint32_t s_node[kLdsCap][kWave], s_rng[kLdsCap][kWave];
-  __shared__ unsigned long long s_key[kLdsCap][kWave];
-  __shared__ uint32_t s_res[kMaxCand][kWave];
-  const int lane = threadIdx.x;
-  const uint32_t n_items = b.ctl[3];
-  for (uint32_t q = blockIdx.x * kWave + lane; q < n_items; q += gridDim.x * kWave) {
-    const uint32_t t = b.rl_routes_a[q];
-    const uint32_t p = b.src_item[t];
-    const uint4 pi = b.pair_info[p];
-    const uint32_t i = t - b.src_off[p];
-    const uint32_t base = b.trans_off[p];
-    const uint32_t bound = pi.x, tmax = pi.y, KB = (pi.z >> 8) & 0xffu;
-    const int mode = (int)(pi.z >> 16);
-    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
-    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
-    LdsLabels S{&s_node[0][lane], &s_rng[0][lane], &s_key[0][lane], 0, 0, false};
-    unsigned long long rk1, rk0;
-    lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
-    if (S.ovf) {
-      const uint32_t x = atomicAdd(&b.ctl[5], 1u);
-      b.rl_routes_b[x] = t;
-      continue;
-    }
-    route_targets(b, StoreLabel<LdsLabels>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB, &s_res[0][lane], kWave);
   }
 }
 
@@ -1426,9 +1339,10 @@ __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
   const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
   unsigned long long rk1, rk0;
   exit_keys(a0, bound, rk1, rk0);
-  const uint2 h1 = rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
-  const uint2 h0 = rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
-  if (bound > g.ball_radius[mode] || h1.y == 0u || h0.y == 0u) {
+  const bool fits = bound <= g.ball_radius[mode] && ((g.ball_mask >> mode) & 1u);
+  const uint2 h1 = fits && rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
+  const uint2 h0 = fits && rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+  if (!fits || h1.y == 0u || h0.y == 0u) {
     b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
     return;
   }
@@ -1474,22 +1388,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
     const uint32_t p = b.rl_paths_a[q];
     RegLabelsT<kTier2Cap> S;
     if (!lane_path(g, b, p, S, kTier2Cap)) {
-      const uint32_t x = atomicAdd(&b.ctl[6], 1u);
-      b.rl_paths_b[x] = p;
-    }
-  }
-}
-
-// path LDS lane tier: the transitions the register tier queued
-__global__ void __launch_bounds__(64) k_paths_lds(DevGraph g, DevBatch b) {
-  __shared__ uint32_t s_node[kLdsCap][kWave], s_rng[kLdsCap][kWave];
-  __shared__ unsigned long long s_key[kLdsCap][kWave];
-  const int lane = threadIdx.x;
-  const uint32_t n_items = b.ctl[4];
-  for (uint32_t q = blockIdx.x * kWave + lane; q < n_items; q += gridDim.x * kWave) {
-    const uint32_t p = b.rl_paths_a[q];
-    LdsLabels S{&s_node[0][lane], &s_rng[0][lane], &s_key[0][lane], 0, 0, false};
-    if (!lane_path(g, b, p, S, kLdsCap)) {
       const uint32_t x = atomicAdd(&b.ctl[6], 1u);
       b.rl_paths_b[x] = p;
     }
@@ -2393,16 +2291,18 @@ __global__ void __launch_bounds__(256) k_sum_u64(const uint32_t* a, uint64_t n, 
 // whose ball outgrows the LDS hash is reported (stats[1]) and the caller builds on the host.
 constexpr int kBallSearchH = 256;
 constexpr int kBallRowH = 256;
+// largest table a node gets here: a power of two >= kBallSlotsPerRow x the 3/4-full row hash
+constexpr uint32_t pow2_at_least(uint32_t x) { return x <= 1u ? 1u : 2u * pow2_at_least((x + 1u) / 2u); }
+constexpr uint32_t kBallMaxTable = pow2_at_least(kBallSlotsPerRow * (kBallRowH * 3 / 4));
 struct BallSmem {
   SearchSmem<kBallSearchH, false> s;
   uint32_t road[kBallRowH];
   unsigned long long k0[kBallRowH], k1[kBallRowH];
   uint16_t dense[kBallRowH], order[kBallRowH];   // fill pass: occupied row slots, rows by rank
-  uint16_t tslot[2 * kBallRowH];                 // fill pass: the node's table (row slot per table slot)
+  uint16_t tslot[kBallMaxTable];                 // fill pass: the node's table (row slot per table slot)
   uint32_t used, bad;
 };
 
-static_assert(kBallSlotsPerRow * (kBallRowH * 3 / 4) <= 2 * kBallRowH, "BallSmem::tslot holds the largest table");
 __device__ __forceinline__ uint32_t table_bits_dev(uint32_t rows) {
   uint32_t bits = 1;
   while ((1ull << bits) < (unsigned long long)kBallSlotsPerRow * rows) ++bits;
@@ -2504,7 +2404,7 @@ __global__ void __launch_bounds__(64) k_ball_build(DevGraph g, int mode, uint32_
         if (h == 0xffffu) continue;
         uint32_t y, z, w;
         ball_pack(sm.k0[h], sm.k1[h], y, z, w);
-        ent[(uint64_t)hh.x + s] = make_uint4(sm.road[h], y, z, w);
+        ent[ball_row0(hh.x) + s] = make_uint4(sm.road[h], y, z, w);
       }
     }
     __syncthreads();
@@ -2524,7 +2424,7 @@ __global__ void k_ball_entries(const uint32_t* bits, uint32_t n, unsigned long l
 
 __global__ void k_ball_hdr(const uint32_t* bits, const unsigned long long* off, uint32_t n, uint2* hdr) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u < n) hdr[u] = make_uint2((uint32_t)off[u], bits[u]);
+  if (u < n) hdr[u] = make_uint2((uint32_t)(off[u] >> 1), bits[u]);   // first rows are even (rm_common.hpp)
 }
 
 // keys from node `from` to both endpoints of `road` through the mode's tables, as K2 probes
@@ -2537,7 +2437,7 @@ __global__ void k_ball_lookup(DevGraph g, int mode, uint64_t n, const uint32_t* 
   unsigned long long k0 = kKeyInf, k1 = kKeyInf;
   if (h.y) {
     const uint4* ent = g.ball_ent[mode];
-    const uint4 e = ball_resolve(ent, h, road[i], ent[h.x + ball_slot(road[i], h.y)]);
+    const uint4 e = ball_resolve(ent, h, road[i], ent[ball_row0(h.x) + ball_slot(road[i], h.y)]);
     k0 = row_key0(e);
     k1 = row_key1(e);
     if (e.x != road[i]) k0 = k1 = kKeyInf;
@@ -2556,9 +2456,24 @@ template <class T>
 T* dalloc(std::vector<void*>& list, uint64_t n) {
   void* p = nullptr;
   if (n == 0) n = 1;
-  RM_HIP(hipMalloc(&p, n * sizeof(T)));
+  const hipError_t e = hipMalloc(&p, n * sizeof(T));
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();   // not sticky: clear it for the caller's next call
+    throw OutOfDeviceMemory("out of device memory allocating " + std::to_string(n * sizeof(T)) + " bytes");
+  }
+  RM_HIP(e);
   list.push_back(p);
   return (T*)p;
+}
+
+// a workspace that does not fit in HBM is a batch too large for the device (serve_policy.hpp)
+template <class F>
+void grow_workspace(F&& f) {
+  try {
+    f();
+  } catch (const OutOfDeviceMemory& e) {
+    throw BatchTooLarge(std::string("batch workspace does not fit in HBM: ") + e.what());
+  }
 }
 
 template <class T>
@@ -2779,11 +2694,22 @@ void Engine::set_ball_radius(uint32_t radius_cm) {
   ball_radius_cm_ = radius_cm;
 }
 
+uint32_t Engine::mode_ball_radius(int mode) const {
+  std::lock_guard<std::mutex> lk(ball_mu_);
+  return (mode >= 0 && mode <= kModePedestrian && ((dg_.ball_mask >> mode) & 1u)) ? dg_.ball_radius[mode] : 0u;
+}
+
 void Engine::ball_stats(int mode, double* out4) const {
   std::lock_guard<std::mutex> lk(ball_mu_);
   for (int i = 0; i < 4; ++i) out4[i] = (mode >= 0 && mode <= kModePedestrian) ? ball_info_[mode][i] : 0.0;
 }
 
+// Route balls of every mode in mode_mask that has none yet.  Each mode gets the largest radius
+// at or below the engine's (ladder: balls.hpp kBallRadii) whose sampled tables fit what is left
+// of the memory granted to tables (ball_total_budget of the device's HBM, less what earlier modes
+// took, and the free HBM less a reserve) and the per-mode budget; a build that still comes out
+// too large steps down again; a mode nothing fits runs its transitions in the search tiers.
+// auto and bus route identically and share one build (ball_twin_mode).
 void Engine::ensure_balls(uint32_t mode_mask) {
   std::lock_guard<std::mutex> lk(ball_mu_);
   if (ball_radius_cm_ == 0 || host_.num_nodes() == 0) return;
@@ -2794,31 +2720,74 @@ void Engine::ensure_balls(uint32_t mode_mask) {
   // small balls (country graphs at moderate radii: millions of nodes, tens of nodes per ball)
   // are built on the GPU; env RM_BALL_BUILD=host|gpu forces one
   const char* how = std::getenv("RM_BALL_BUILD");
-  const bool try_gpu = how ? std::strcmp(how, "gpu") == 0
-                           : est_ball_nodes(host_, ball_radius_cm_) <= 48.0 && host_.num_nodes() >= 100000;
+  uint32_t max_keys = kBallMaxKeys;   // env RM_BALL_MAX_KEYS: tuning / tests of the no-table path
+  if (const char* e = std::getenv("RM_BALL_MAX_KEYS")) max_keys = (uint32_t)std::max(1, std::atoi(e));
+  constexpr uint64_t kReserve = 4ull << 30;   // HBM kept free for the first workspaces
   for (int mode = 0; mode <= kModePedestrian; ++mode) {
     if (!((todo >> mode) & 1u)) continue;
-    uint32_t max_keys = kBallMaxKeys;   // env RM_BALL_MAX_KEYS: tuning / tests of the no-table path
-    if (const char* e = std::getenv("RM_BALL_MAX_KEYS")) max_keys = (uint32_t)std::max(1, std::atoi(e));
-    if (try_gpu && build_balls_gpu(mode, max_keys)) continue;
-    BallTables bt;
-    build_balls(host_, mode, ball_radius_cm_, max_keys, threads, bt);
-    dg_.ball_hdr[mode] = (const uint2*)upload(allocs_, bt.hdr);
-    dg_.ball_ent[mode] = (const uint4*)upload(allocs_, bt.ent);
-    dg_.ball_radius[mode] = bt.radius_cm;
-    dg_.ball_mask |= 1u << mode;
-    ball_built_ |= 1u << mode;
-    ball_info_[mode][0] = (double)bt.n_keys;
-    ball_info_[mode][1] = (double)(bt.ent.size() / 4);
-    ball_info_[mode][2] = (double)bt.n_skipped;
-    ball_info_[mode][3] = bt.build_ms;
+    const uint32_t bit = 1u << mode;
+    const int tw = ball_twin_mode(mode);
+    if (tw >= 0 && ((ball_built_ >> tw) & 1u)) {   // identical tables: share them
+      dg_.ball_hdr[mode] = dg_.ball_hdr[tw];
+      dg_.ball_ent[mode] = dg_.ball_ent[tw];
+      dg_.ball_radius[mode] = dg_.ball_radius[tw];
+      if ((dg_.ball_mask >> tw) & 1u) dg_.ball_mask |= bit;
+      for (int i = 0; i < 4; ++i) ball_info_[mode][i] = ball_info_[tw][i];
+      ball_gpu_ |= ((ball_gpu_ >> tw) & 1u) << mode;
+      ball_built_ |= bit;
+      continue;
+    }
+    size_t hbm_free = 0, hbm_total = 0;
+    RM_HIP(hipMemGetInfo(&hbm_free, &hbm_total));
+    const uint64_t total_cap = ball_total_budget(hbm_total);
+    uint64_t avail = std::min<uint64_t>(ball_mode_budget(), total_cap > ball_bytes_ ? total_cap - ball_bytes_ : 0);
+    avail = std::min<uint64_t>(avail, hbm_free > kReserve ? hbm_free - kReserve : 0);
+    BallSample bs;
+    uint32_t r = fit_ball_radius_cm(host_, mode, ball_radius_cm_, avail, &bs);
+    bool built = false;
+    for (; r && !built; r = next_ball_radius_cm(r)) {
+      const double nodes = sample_balls(host_, r, kBallMaxKeysHost, mode).nodes;
+      const bool try_gpu = how ? std::strcmp(how, "gpu") == 0 : nodes <= 48.0 && host_.num_nodes() >= 100000;
+      try {
+        if (try_gpu && build_balls_gpu(mode, r, max_keys, avail)) { built = true; break; }
+        BallTables bt;
+        build_balls(host_, mode, r, max_keys, threads, bt, avail / 16);
+        std::vector<void*> tmp;   // both arrays or neither
+        struct Free { std::vector<void*>& l; ~Free() { for (void* p : l) (void)hipFree(p); } } fr{tmp};
+        const uint2* hdr = (const uint2*)upload(tmp, bt.hdr);
+        const uint4* ent = (const uint4*)upload(tmp, bt.ent);
+        allocs_.insert(allocs_.end(), tmp.begin(), tmp.end());
+        tmp.clear();
+        dg_.ball_hdr[mode] = hdr;
+        dg_.ball_ent[mode] = ent;
+        dg_.ball_radius[mode] = bt.radius_cm;
+        dg_.ball_mask |= bit;
+        ball_bytes_ += (uint64_t)bt.ent.size() * 4;
+        ball_info_[mode][0] = (double)bt.n_keys;
+        ball_info_[mode][1] = (double)(bt.ent.size() / 4);
+        ball_info_[mode][2] = (double)bt.n_skipped;
+        ball_info_[mode][3] = bt.build_ms;
+        built = true;
+      } catch (const BallsTooLarge&) {
+        // the tables came out larger than sampled: the next radius down
+      } catch (const OutOfDeviceMemory&) {
+        // the free HBM moved under us (another matcher's workspace): the next radius down
+      }
+    }
+    if (!built) {   // no tables for this mode: every transition of it runs in the search tiers
+      dg_.ball_radius[mode] = 0;
+      for (int i = 0; i < 4; ++i) ball_info_[mode][i] = 0.0;
+    }
+    ball_built_ |= bit;
   }
   RM_HIP(hipDeviceSynchronize());
 }
 
-// GPU route-ball build of one mode (k_ball_build); false (nothing changed) when some ball
-// outgrew the kernel's LDS hashes, and the caller builds on the host.  Called under ball_mu_.
-bool Engine::build_balls_gpu(int mode, uint32_t max_keys) {
+// GPU route-ball build of one mode at radius_cm (k_ball_build); false (nothing changed) when
+// some ball outgrew the kernel's LDS hashes, and the caller builds on the host.  Throws
+// BallsTooLarge, allocating nothing, when the tables need more than avail_bytes (or rows
+// beyond kBallMaxRows).  Called under ball_mu_.
+bool Engine::build_balls_gpu(int mode, uint32_t radius_cm, uint32_t max_keys, uint64_t avail_bytes) {
   const auto t0 = std::chrono::steady_clock::now();
   const uint32_t N = host_.num_nodes();
   std::vector<uint32_t> inc_off, inc;
@@ -2834,7 +2803,7 @@ bool Engine::build_balls_gpu(int mode, uint32_t max_keys) {
   RM_HIP(hipMemset(d_stats, 0, 4 * sizeof(unsigned long long)));
   DevGraph g = dg_;
   const uint32_t grid = std::min<uint32_t>(N, 16384);
-  hipLaunchKernelGGL(k_ball_build<false>, dim3(grid), dim3(64), 0, 0, g, mode, ball_radius_cm_, max_keys, d_inc_off,
+  hipLaunchKernelGGL(k_ball_build<false>, dim3(grid), dim3(64), 0, 0, g, mode, radius_cm, max_keys, d_inc_off,
                      d_inc, d_bits, (const uint2*)nullptr, (uint4*)nullptr, d_stats);
   hipLaunchKernelGGL(k_ball_entries, dim3((N + 255) / 256), dim3(256), 0, 0, d_bits, N, d_cnt);
   size_t tb = 0;
@@ -2847,20 +2816,26 @@ bool Engine::build_balls_gpu(int mode, uint32_t max_keys) {
   RM_HIP(hipMemcpy(&last[1], d_cnt + (N - 1), 8, hipMemcpyDeviceToHost));
   if (st[1]) return false;   // a ball outgrew the LDS hashes: the host build takes the mode
   const uint64_t total = last[0] + last[1];
-  if (total >= 0xffffffffull) throw std::runtime_error("route balls too large (entries >= 2^32); lower the radius");
-  uint2* d_hdr = dalloc<uint2>(allocs_, N);
-  uint4* d_ent = dalloc<uint4>(allocs_, total);
+  if (total > kBallMaxRows || total * 16 > avail_bytes)
+    throw BallsTooLarge("route balls too large for their budget; lower the radius");
+  // header and rows join the engine's allocations only once both are filled
+  uint2* d_hdr = dalloc<uint2>(tmp, N);
+  uint4* d_ent = dalloc<uint4>(tmp, total);
   hipLaunchKernelGGL(k_ball_hdr, dim3((N + 255) / 256), dim3(256), 0, 0, d_bits, d_off, N, d_hdr);
   RM_HIP(hipMemset(d_ent, 0xff, total * sizeof(uint4)));
-  hipLaunchKernelGGL(k_ball_build<true>, dim3(grid), dim3(64), 0, 0, g, mode, ball_radius_cm_, max_keys, d_inc_off,
+  hipLaunchKernelGGL(k_ball_build<true>, dim3(grid), dim3(64), 0, 0, g, mode, radius_cm, max_keys, d_inc_off,
                      d_inc, d_bits, (const uint2*)d_hdr, d_ent, d_stats);
   RM_HIP(hipGetLastError());
   RM_HIP(hipDeviceSynchronize());
+  tmp.erase(std::remove(tmp.begin(), tmp.end(), (void*)d_hdr), tmp.end());
+  tmp.erase(std::remove(tmp.begin(), tmp.end(), (void*)d_ent), tmp.end());
+  allocs_.push_back(d_hdr);
+  allocs_.push_back(d_ent);
   dg_.ball_hdr[mode] = d_hdr;
   dg_.ball_ent[mode] = d_ent;
-  dg_.ball_radius[mode] = ball_radius_cm_;
+  dg_.ball_radius[mode] = radius_cm;
   dg_.ball_mask |= 1u << mode;
-  ball_built_ |= 1u << mode;
+  ball_bytes_ += total * 16;
   ball_info_[mode][0] = (double)st[0];
   ball_info_[mode][1] = (double)total;
   ball_info_[mode][2] = (double)st[2];
@@ -2916,69 +2891,47 @@ Matcher::~Matcher() {
 }
 
 void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
-  Workspace& w = ws_;
-  if (points <= w.cap_points && traces <= w.cap_traces && nopts <= w.cap_opts && w.ctl) return;
-  // grow everything sized by points/traces (trans/path pools are grown separately)
-  const uint64_t cp = std::max<uint64_t>(points, w.cap_points) + 64;
-  const uint64_t ct = std::max<uint64_t>(traces, w.cap_traces) + 16;
-  const uint64_t co = std::max<uint64_t>(nopts, w.cap_opts) + 4;
-  const uint64_t keep_trans = w.cap_trans, keep_path = w.cap_path, keep_segs = w.cap_segs, keep_src = w.cap_src;
-  w.release();
-  std::vector<void*>& L = w.allocs;
-  w.trace_off = dalloc<uint32_t>(L, ct + 1);
-  w.lon = dalloc<float>(L, cp); w.lat = dalloc<float>(L, cp); w.time = dalloc<double>(L, cp);
-  w.acc = dalloc<float>(L, cp); w.opts = dalloc<MatchOptions>(L, co); w.trace_opt = dalloc<uint32_t>(L, ct);
-  w.slot_trace = dalloc<uint32_t>(L, cp); w.n_states = dalloc<uint32_t>(L, ct); w.state_orig = dalloc<uint32_t>(L, cp);
-  w.state_time = dalloc<double>(L, cp);
-  w.cand_n = dalloc<uint8_t>(L, cp); w.cand_desc = dalloc<uint4>(L, cp * kMaxCand * 2);
-  w.cand_sq = dalloc<float>(L, cp * kMaxCand); w.pair_info = dalloc<uint4>(L, cp);
-  w.trans_cnt = dalloc<uint32_t>(L, cp); w.trans_off = dalloc<uint32_t>(L, cp); w.gc = dalloc<double>(L, cp);
-  w.src_cnt = dalloc<uint32_t>(L, cp); w.src_off = dalloc<uint32_t>(L, cp);
-  w.choice = dalloc<int8_t>(L, cp); w.chain_start = dalloc<uint8_t>(L, cp); w.bp = dalloc<uint8_t>(L, cp * kMaxCand);
-  w.path_off = dalloc<uint32_t>(L, cp); w.path_cnt = dalloc<uint32_t>(L, cp); w.route_dist = dalloc<uint32_t>(L, cp);
-  w.path_sab = dalloc<uint2>(L, cp);
-  w.path_inline = dalloc<uint32_t>(L, cp * kInlinePath);
-  w.trav_off = dalloc<uint32_t>(L, cp);
-  w.seg_base = dalloc<uint32_t>(L, ct); w.seg_cnt = dalloc<uint32_t>(L, ct);
-  w.rep_cnt = dalloc<uint32_t>(L, ct); w.stats = dalloc<ReportStats>(L, ct);
-  w.ctl = dalloc<uint32_t>(L, kCtlWords);
-  w.rl_paths_a = dalloc<uint32_t>(L, cp); w.rl_paths_b = dalloc<uint32_t>(L, cp);
-  w.rl_cand = dalloc<uint32_t>(L, cp);
-  w.rl_paths_c = dalloc<uint32_t>(L, cp);
-  w.trace_err = dalloc<uint32_t>(L, ct);
-  w.tot64 = dalloc<unsigned long long>(L, 4);
-  w.tot_part = dalloc<unsigned long long>(L, 2 * ((cp + 255) / 256) + 2);
-  w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
-  w.gsearch = nullptr;
-  w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
-  w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
-  ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
-  ensure_path(std::max<uint64_t>(keep_path, cp / 8 + 1024));
-  ensure_segs(std::max<uint64_t>(keep_segs, cp / 2 + 1024));
-}
-
-void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
-  Workspace& w = ws_;
-  if (!(n <= w.cap_trans && w.route)) {
-    if (w.route) { (void)hipFree(w.route); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.route)); }
-    const uint64_t c = n + n / 4 + 1024;
-    w.route = dalloc<uint32_t>(w.allocs, c);
-    w.cap_trans = c;
-  }
-  if (!(n_src <= w.cap_src && w.src_item)) {
-    if (w.src_item) { (void)hipFree(w.src_item); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.src_item)); }
-    if (w.rl_routes_a) { (void)hipFree(w.rl_routes_a); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_a)); }
-    if (w.rl_routes_b) { (void)hipFree(w.rl_routes_b); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_b)); }
-    if (w.rl_routes_0) { (void)hipFree(w.rl_routes_0); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_0)); }
-    if (w.rl_routes_c) { (void)hipFree(w.rl_routes_c); w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), (void*)w.rl_routes_c)); }
-    const uint64_t c = n_src + n_src / 4 + 1024;
-    w.src_item = dalloc<uint32_t>(w.allocs, c);
-    w.rl_routes_a = dalloc<uint32_t>(w.allocs, c);   // overflow lists hold (pair, source) items
-    w.rl_routes_b = dalloc<uint32_t>(w.allocs, c);
-    w.rl_routes_0 = dalloc<uint32_t>(w.allocs, c);
-    w.rl_routes_c = dalloc<uint32_t>(w.allocs, c);
-    w.cap_src = c;
-  }
+  grow_workspace([&] {
+    Workspace& w = ws_;
+    if (points <= w.cap_points && traces <= w.cap_traces && nopts <= w.cap_opts && w.ctl) return;
+    // grow everything sized by points/traces (trans/path pools are grown separately)
+    const uint64_t cp = std::max<uint64_t>(points, w.cap_points) + 64;
+    const uint64_t ct = std::max<uint64_t>(traces, w.cap_traces) + 16;
+    const uint64_t co = std::max<uint64_t>(nopts, w.cap_opts) + 4;
+    const uint64_t keep_trans = w.cap_trans, keep_path = w.cap_path, keep_segs = w.cap_segs, keep_src = w.cap_src;
+    w.release();
+    std::vector<void*>& L = w.allocs;
+    w.trace_off = dalloc<uint32_t>(L, ct + 1);
+    w.lon = dalloc<float>(L, cp); w.lat = dalloc<float>(L, cp); w.time = dalloc<double>(L, cp);
+    w.acc = dalloc<float>(L, cp); w.opts = dalloc<MatchOptions>(L, co); w.trace_opt = dalloc<uint32_t>(L, ct);
+    w.slot_trace = dalloc<uint32_t>(L, cp); w.n_states = dalloc<uint32_t>(L, ct); w.state_orig = dalloc<uint32_t>(L, cp);
+    w.state_time = dalloc<double>(L, cp);
+    w.cand_n = dalloc<uint8_t>(L, cp); w.cand_desc = dalloc<uint4>(L, cp * kMaxCand * 2);
+    w.cand_sq = dalloc<float>(L, cp * kMaxCand); w.pair_info = dalloc<uint4>(L, cp);
+    w.trans_cnt = dalloc<uint32_t>(L, cp); w.trans_off = dalloc<uint32_t>(L, cp); w.gc = dalloc<double>(L, cp);
+    w.src_cnt = dalloc<uint32_t>(L, cp); w.src_off = dalloc<uint32_t>(L, cp);
+    w.choice = dalloc<int8_t>(L, cp); w.chain_start = dalloc<uint8_t>(L, cp); w.bp = dalloc<uint8_t>(L, cp * kMaxCand);
+    w.path_off = dalloc<uint32_t>(L, cp); w.path_cnt = dalloc<uint32_t>(L, cp); w.route_dist = dalloc<uint32_t>(L, cp);
+    w.path_sab = dalloc<uint2>(L, cp);
+    w.path_inline = dalloc<uint32_t>(L, cp * kInlinePath);
+    w.trav_off = dalloc<uint32_t>(L, cp);
+    w.seg_base = dalloc<uint32_t>(L, ct); w.seg_cnt = dalloc<uint32_t>(L, ct);
+    w.rep_cnt = dalloc<uint32_t>(L, ct); w.stats = dalloc<ReportStats>(L, ct);
+    w.ctl = dalloc<uint32_t>(L, kCtlWords);
+    w.rl_paths_a = dalloc<uint32_t>(L, cp); w.rl_paths_b = dalloc<uint32_t>(L, cp);
+    w.rl_cand = dalloc<uint32_t>(L, cp);
+    w.rl_paths_c = dalloc<uint32_t>(L, cp);
+    w.trace_err = dalloc<uint32_t>(L, ct);
+    w.tot64 = dalloc<unsigned long long>(L, 4);
+    w.tot_part = dalloc<unsigned long long>(L, 2 * ((cp + 255) / 256) + 2);
+    w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
+    w.gsearch = nullptr;
+    w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
+    w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
+    ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
+    ensure_path(std::max<uint64_t>(keep_path, cp / 8 + 1024));
+    ensure_segs(std::max<uint64_t>(keep_segs, cp / 2 + 1024));
+  });
 }
 
 static void free_one(Workspace& w, void* q) {
@@ -2987,26 +2940,62 @@ static void free_one(Workspace& w, void* q) {
   w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), q));
 }
 
+void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
+  grow_workspace([&] {
+    Workspace& w = ws_;
+    if (!(n <= w.cap_trans && w.route)) {
+      free_one(w, w.route);
+      w.route = nullptr;
+      w.cap_trans = 0;
+      const uint64_t c = n + n / 4 + 1024;
+      w.route = dalloc<uint32_t>(w.allocs, c);
+      w.cap_trans = c;
+    }
+    if (!(n_src <= w.cap_src && w.src_item)) {
+      for (uint32_t** q : {&w.src_item, &w.rl_routes_a, &w.rl_routes_b, &w.rl_routes_0, &w.rl_routes_c}) {
+        free_one(w, *q);
+        *q = nullptr;
+      }
+      w.cap_src = 0;
+      const uint64_t c = n_src + n_src / 4 + 1024;
+      w.src_item = dalloc<uint32_t>(w.allocs, c);
+      w.rl_routes_a = dalloc<uint32_t>(w.allocs, c);   // overflow lists hold (pair, source) items
+      w.rl_routes_b = dalloc<uint32_t>(w.allocs, c);
+      w.rl_routes_0 = dalloc<uint32_t>(w.allocs, c);
+      w.rl_routes_c = dalloc<uint32_t>(w.allocs, c);
+      w.cap_src = c;
+    }
+  });
+}
+
 void Matcher::ensure_path(uint64_t n) {
-  Workspace& w = ws_;
-  if (n <= w.cap_path && w.path_pool) return;
-  free_one(w, w.path_pool);
-  const uint64_t c = n + n / 4 + 1024;
-  w.path_pool = dalloc<uint32_t>(w.allocs, c);
-  w.cap_path = c;
+  grow_workspace([&] {
+    Workspace& w = ws_;
+    if (n <= w.cap_path && w.path_pool) return;
+    free_one(w, w.path_pool);
+    w.path_pool = nullptr;
+    w.cap_path = 0;
+    const uint64_t c = n + n / 4 + 1024;
+    w.path_pool = dalloc<uint32_t>(w.allocs, c);
+    w.cap_path = c;
+  });
 }
 
 void Matcher::ensure_segs(uint64_t n) {
-  Workspace& w = ws_;
-  if (n <= w.cap_segs && w.segs) return;
-  free_one(w, w.segs);
-  free_one(w, w.reps);
-  free_one(w, w.rec_slot);
-  const uint64_t c = n + n / 4 + 1024;
-  w.segs = dalloc<SegmentRec>(w.allocs, c);
-  w.reps = dalloc<ReportRec>(w.allocs, c);
-  w.rec_slot = dalloc<uint32_t>(w.allocs, c);
-  w.cap_segs = c;
+  grow_workspace([&] {
+    Workspace& w = ws_;
+    if (n <= w.cap_segs && w.segs) return;
+    for (void** q : {(void**)&w.segs, (void**)&w.reps, (void**)&w.rec_slot}) {
+      free_one(w, *q);
+      *q = nullptr;
+    }
+    w.cap_segs = 0;
+    const uint64_t c = n + n / 4 + 1024;
+    w.segs = dalloc<SegmentRec>(w.allocs, c);
+    w.reps = dalloc<ReportRec>(w.allocs, c);
+    w.rec_slot = dalloc<uint32_t>(w.allocs, c);
+    w.cap_segs = c;
+  });
 }
 
 void Matcher::tic(int k) {
@@ -3071,7 +3060,7 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
   const uint32_t T = hb.n_traces;
   if (T == 0) { n_traces_ = 0; n_points_ = 0; n_trans_ = 0; n_path_ = 0; seg_used_ = 0; return; }
   const uint64_t P = hb.trace_off[T];
-  if (P >= 0xffffffffull) throw std::runtime_error("batch too large (points >= 2^32)");
+  if (P >= 0xffffffffull) throw BatchTooLarge("batch too large (points >= 2^32)");
   for (uint32_t k = 0; k < T; ++k) {
     if (hb.trace_off[k + 1] < hb.trace_off[k]) throw std::runtime_error("trace offsets not monotone");
     if (hb.trace_opt[k] >= hb.n_opts) throw std::runtime_error("trace option index out of range");
@@ -3130,7 +3119,7 @@ void Matcher::run_device(const RunParams& rp) {
   const uint64_t P = n_points_;
   err_bits_ = 0;
   if (T == 0) return;
-  if (P >= (uint64_t)kTravLast) throw std::runtime_error("batch too large (slots >= 2^30); split it");  // TravRec::slot flags
+  if (P >= (uint64_t)kTravLast) throw BatchTooLarge("batch too large (slots >= 2^30); split it");  // TravRec::slot flags
   Workspace& w = ws_;
   hipStream_t st = stream_;
   eng_->ensure_balls(mode_mask_);
@@ -3160,7 +3149,7 @@ void Matcher::run_device(const RunParams& rp) {
   RM_HIP(hipStreamSynchronize(st));
   const uint64_t total = htot[0];
   const uint64_t n_src = htot[1];
-  if (total >= kMaxTransitions) throw std::runtime_error("batch too large (transitions >= 0xF0000000); split it");
+  if (total >= kMaxTransitions) throw BatchTooLarge("batch too large (transitions >= 0xF0000000); split it");
   n_trans_ = total;
   ensure_trans(total, n_src);
   v.route = w.route;
@@ -3170,13 +3159,11 @@ void Matcher::run_device(const RunParams& rp) {
   v.rl_routes_0 = w.rl_routes_0;
   v.rl_routes_c = w.rl_routes_c;
 
-  const bool balls = (mode_mask_ & ~g.ball_mask) == 0u;   // every mode of the batch has its route balls
+  // the ball tiers run when some mode of the batch has route balls; items of a mode without
+  // them (or bounds above its radius) are handed to the search tiers
+  const bool balls = (mode_mask_ & g.ball_mask) != 0u;
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
-#ifdef RM_ALL_LDS
-  if (n_src)
-    hipLaunchKernelGGL(k_all_items, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, v, (uint32_t)n_src);
-#else
   if (n_src && balls) {
     hipLaunchKernelGGL(k_routes_ball, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)), dim3(256), 0,
@@ -3184,12 +3171,7 @@ void Matcher::run_device(const RunParams& rp) {
   } else if (n_src) {
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
   }
-#endif
-#ifdef RM_TIER2_LDS
-  hipLaunchKernelGGL(k_routes_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
-#else
-  hipLaunchKernelGGL(k_routes_reg2, dim3(kLdsGrid / 4), dim3(256), 0, st, g, v);
-#endif
+  hipLaunchKernelGGL(k_routes_reg2, dim3(kReg2Grid), dim3(256), 0, st, g, v);
   hipLaunchKernelGGL(k_routes_wave, dim3(1024), dim3(64), 0, st, g, v);
   // the global tier runs in line once its scratch exists; before that, a hand-over seen at the
   // path-stage read-back allocates it and re-runs K3 (rare: bounds of many kilometres)
@@ -3213,11 +3195,7 @@ void Matcher::run_device(const RunParams& rp) {
     } else {
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 0);
     }
-#ifdef RM_TIER2_LDS
-    hipLaunchKernelGGL(k_paths_lds, dim3(kLdsGrid), dim3(64), 0, st, g, v);
-#else
-    hipLaunchKernelGGL(k_paths_reg2, dim3(kLdsGrid / 4), dim3(256), 0, st, g, v);
-#endif
+    hipLaunchKernelGGL(k_paths_reg2, dim3(kReg2Grid), dim3(256), 0, st, g, v);
     hipLaunchKernelGGL(k_paths_wave, dim3(1024), dim3(64), 0, st, g, v);
     if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
     toc(kKPaths);
@@ -3255,7 +3233,7 @@ void Matcher::run_device(const RunParams& rp) {
       read_ctl();
     }
     if (!(hctl_[2] & kErrPathOverflow)) break;
-    if (attempt > 3) throw std::runtime_error("path pool overflow persists");
+    if (attempt > 3) throw BatchTooLarge("path pool overflow persists");
     ensure_path((uint64_t)hctl_[0]);
     v.path_pool = w.path_pool; v.path_cap = w.cap_path;
     RM_HIP(hipMemsetAsync(w.ctl, 0, sizeof(uint32_t), st));          // path_used
@@ -3266,7 +3244,7 @@ void Matcher::run_device(const RunParams& rp) {
     RM_HIP(hipStreamSynchronize(st));
   }
   const uint64_t seg_total = htot[2];
-  if (seg_total >= kMaxRecords) throw std::runtime_error("batch too large (path edges >= 1.7e9); split it");
+  if (seg_total >= kMaxRecords) throw BatchTooLarge("batch too large (path edges >= 1.7e9); split it");
   n_path_ = seg_total;  // one traversal record (and at most one segment) per chosen path edge
   ensure_segs(seg_total);
   v.segs = w.segs; v.reps = w.reps;

@@ -17,6 +17,7 @@
 #include "balls.hpp"
 #include "graph.hpp"
 #include "rm_common.hpp"
+#include "serve_policy.hpp"
 
 namespace rm {
 
@@ -26,6 +27,12 @@ namespace rm {
     if (_e != hipSuccess)                                                                        \
       throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " #x);   \
   } while (0)
+
+// hipMalloc found too little free HBM (the engine's allocator; callers decide whether a smaller
+// request can succeed: workspaces turn it into BatchTooLarge, the route-ball build steps down)
+struct OutOfDeviceMemory : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 
 struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   const uint32_t* node_off;
@@ -325,6 +332,8 @@ class Engine {
   uint32_t ball_radius() const { return ball_radius_cm_; }
   // stats of one mode's tables: {keys, table entries, nodes without a table, build ms}
   void ball_stats(int mode, double* out4) const;
+  // radius (cm) the mode's tables were built at (0: none; its transitions use the search tiers)
+  uint32_t mode_ball_radius(int mode) const;
   // modes whose tables were built on the GPU (bit per Mode)
   uint32_t ball_gpu_mask() const { return ball_gpu_; }
   // keys[2i], keys[2i+1] from node from[i] to road[i]'s node0 / node1 through the built tables
@@ -343,7 +352,8 @@ class Engine {
   uint32_t ball_built_ = 0;             // mode bits
   uint32_t ball_gpu_ = 0;               // mode bits built on the GPU
   uint32_t grid_split_ = 1;
-  bool build_balls_gpu(int mode, uint32_t max_keys);
+  uint64_t ball_bytes_ = 0;             // bytes of the tables built so far (all modes)
+  bool build_balls_gpu(int mode, uint32_t radius_cm, uint32_t max_keys, uint64_t avail_bytes);
   double ball_info_[5][4] = {};
 };
 

@@ -218,6 +218,12 @@ RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) {
 }
 #endif
 
+// A node's table starts at row 2 * hdr.x of its mode's entry array (hdr = {first row / 2,
+// log2 size}): every table has a power-of-two size >= 2 and the tables are laid out back to
+// back, so every first row is even, and a u32 hdr.x addresses 2^33 rows (128 GiB) per mode.
+constexpr uint64_t kBallMaxRows = 1ull << 33;
+RM_HD uint64_t ball_row0(uint32_t hx) { return (uint64_t)hx << 1; }
+
 // Route-ball row (balls.hpp), 16 bytes: the keys from the table's node to both endpoints
 // of road x, as 24-bit cm distances and 24-bit ms times split over the words:
 //   x = road (kNone: free slot)

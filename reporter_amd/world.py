@@ -105,3 +105,14 @@ def trace_to_request(tr, k, uuid=None, mode="auto", report_levels=(0, 1), transi
     mo = {"mode": mode, "report_levels": list(report_levels), "transition_levels": list(transition_levels)}
     mo.update(opts)
     return {"uuid": uuid or str(k), "trace": pts, "match_options": mo}
+
+
+def concat_traces(*sets):
+    """One trace set of several (each a generate_traces dict), in order."""
+    out = {k: np.concatenate([s[k] for s in sets]) for k in ("lon", "lat", "time", "accuracy", "truth_edge", "truth_off_cm")}
+    off, base = [np.zeros(1, np.uint64)], 0
+    for s in sets:
+        off.append(s["trace_off"][1:].astype(np.uint64) + base)
+        base += int(s["trace_off"][-1])
+    out["trace_off"] = np.concatenate(off).astype(np.uint32)
+    return out

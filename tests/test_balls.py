@@ -118,3 +118,46 @@ def test_ball_lookup_errors(small_world):
     assert L.rm_balls_lookup(os.fsencode(small_world), 0, 20000.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
     big = np.array([10 ** 9], np.uint32)
     assert L.rm_balls_lookup(os.fsencode(small_world), 0, 100.0, 1, big.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
+
+
+def _sample(path, mode, radius_m):
+    import ctypes
+    out = (ctypes.c_double * 3)()
+    _lib.check(_lib.lib().rm_graph_ball_sample(os.fsencode(path), mode, radius_m, out))
+    return {"nodes": out[0], "table_bytes": out[1], "skipped_frac": out[2]}
+
+
+def _fit(path, mode, start_m, avail_gb):
+    import ctypes
+    r = ctypes.c_double()
+    _lib.check(_lib.lib().rm_graph_fit_ball_radius(os.fsencode(path), mode, start_m, avail_gb, ctypes.byref(r)))
+    return r.value
+
+
+def test_fit_ball_radius_steps_down_at_the_budget(tmpdir_session, built_lib):
+    """VERDICT r02 (route-ball memory): a mode's tables are built at the largest radius whose
+    sampled tables (+10 %) fit the memory left for them; a budget just below the 2000 m tables
+    steps down instead of failing, and a budget nothing fits leaves the mode to the search tiers."""
+    from reporter_amd import world
+    path = str(tmpdir_session / "fit_c2.rmg")
+    cfg = world.CONFIGS["C2"]
+    world.build_world(path, cfg["rows"], cfg["cols"], cfg["block_m"], seed=1, cell_m=cfg["cell_m"])
+    gib = float(1 << 30)
+    for mode in (0, 3, 4):
+        s2000 = _sample(path, mode, 2000.0)
+        need = s2000["table_bytes"] * 1.1 / gib
+        assert _fit(path, mode, 2000.0, need * 1.01) == 2000.0
+        below = _fit(path, mode, 2000.0, need * 0.99)   # just above the cap: the next radius down
+        assert 0.0 < below < 2000.0
+        assert _sample(path, mode, below)["table_bytes"] * 1.1 / gib <= need * 0.99
+        assert _fit(path, mode, 2000.0, 1e-6) == 0.0    # nothing fits: no tables for the mode
+        assert _fit(path, mode, 0.0, 1.0) == 0.0        # radius 0: the search tiers by choice
+    # a start radius off the ladder is tried first, then the ladder below it
+    assert _fit(path, 0, 650.0, 64.0) == 650.0
+    # each mode is sampled over its own edges (pedestrians: no highways, no one-way limits)
+    assert _sample(path, 4, 1000.0)["table_bytes"] != _sample(path, 0, 1000.0)["table_bytes"]
+    L = _lib.lib()
+    import ctypes
+    r = ctypes.c_double()
+    assert L.rm_graph_fit_ball_radius(os.fsencode(path), 7, 100.0, 1.0, ctypes.byref(r)) != 0
+    assert L.rm_graph_fit_ball_radius(os.fsencode(path), 0, 20000.0, 1.0, ctypes.byref(r)) != 0

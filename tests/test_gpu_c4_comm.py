@@ -53,6 +53,41 @@ def test_c4_full_graph(c4_graph, ball_radius):
 
 
 @pytest.mark.timeout(900)
+def test_c4_three_modes_fit_hbm(c4_graph):
+    """VERDICT r02 (route-ball memory): auto, bicycle and pedestrian on the full C4 graph in one
+    batch.  Their tables come out of one budget (half of the HBM): auto keeps its 1000 m tables
+    (68 GB), the others step down as far as the remaining budget needs, nothing runs out of
+    memory, and every stage equals the oracle's."""
+    import meili_oracle as mo
+    from parity_util import compare_all
+    from reporter_amd import graphfile
+    path, cfg = c4_graph
+    eng = engine.Engine(path, 0)
+    names = [("auto", 0), ("bicycle", 3), ("pedestrian", 4)]
+    sets = [world.generate_traces(path, 400, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=4200 + m, mode=nm)
+            for nm, m in names]
+    tr = world.concat_traces(*sets)
+    opts = engine.default_options(3, search_radius=cfg["search_radius"])
+    for q, (_, m) in enumerate(names):
+        opts[q]["mode"] = m
+    trace_opt = np.repeat(np.arange(3, dtype=np.uint32), 400)
+    bm = engine.BatchMatcher(eng)
+    t = time.time()
+    bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt)
+    st = {m: eng.ball_stats(m) for _, m in names}
+    print("C4 three modes: first run %.1fs" % (time.time() - t), st, flush=True)
+    assert st[0]["radius_m"] == 1000.0
+    total = sum(s["entries"] for s in st.values()) * 16
+    assert total <= 0.5 * 288e9 * 1.05, total
+    ref = mo.match(graphfile.load(path), mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"],
+                                                  opts, trace_opt))
+    c = compare_all(bm, ref, tr["trace_off"])
+    assert c["chained"] > 100_000, c
+    bm.close()
+    eng.close()
+
+
+@pytest.mark.timeout(900)
 def test_rccl_comm_on_c4_histogram(c4_graph, tmpdir_session):
     path, cfg = c4_graph
     eng = engine.Engine(path, 0)

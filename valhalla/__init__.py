@@ -87,9 +87,10 @@ def coalesce_stats():
 
 
 def write_config(path, graph_path, device=0, coalesce=True, coalesce_window_ms=0.0, ball_radius=None,
-                 coalesce_workers=None, **meili_default):
+                 coalesce_workers=None, modes=None, **meili_default):
     """Write a Valhalla-style config naming the engine's graph file (ball_radius: route-ball radius
-    in metres, 0..10000, None = engine default)."""
+    in metres, 0..10000, None = engine default; modes: travel modes whose route tables Configure
+    builds besides auto)."""
     conf = {"meili": {"default": dict(meili_default)},
             "reporter_amd": {"graph": _os.path.abspath(graph_path), "device": int(device), "coalesce": bool(coalesce),
                              "coalesce_window_ms": float(coalesce_window_ms)}}
@@ -97,6 +98,8 @@ def write_config(path, graph_path, device=0, coalesce=True, coalesce_window_ms=0
         conf["reporter_amd"]["ball_radius"] = float(ball_radius)
     if coalesce_workers is not None:
         conf["reporter_amd"]["coalesce_workers"] = int(coalesce_workers)
+    if modes is not None:
+        conf["reporter_amd"]["modes"] = list(modes)
     with open(path, "w") as f:
         _json.dump(conf, f, indent=1)
     return path
