@@ -187,7 +187,9 @@ def request_jsons(tr, n):
     pts = [f % q for q in zip(tr["lat"][:P].tolist(), tr["lon"][:P].tolist(), tr["time"][:P].astype(np.int64).tolist(),
                               tr["accuracy"][:P].tolist())]
     mo = '"match_options":{"mode":"auto","report_levels":[0,1],"transition_levels":[0,1]}'
-    return ['{"uuid":"%d","trace":[%s],%s}' % (k, ",".join(pts[off[k]:off[k + 1]]), mo) for k in range(n)], P
+    # bytes, as the reference's Python 2 service hands Match a str (= bytes) from json.dumps
+    return [('{"uuid":"%d","trace":[%s],%s}' % (k, ",".join(pts[off[k]:off[k + 1]]), mo)).encode()
+            for k in range(n)], P
 
 
 def extras(gpath, tr, json_traces, tmpdir):
@@ -237,7 +239,8 @@ def extras(gpath, tr, json_traces, tmpdir):
                                     "JSON parse -> H2D -> every kernel -> D2H -> segment JSON" % (
                                         len(reqs), P, sum(map(len, reqs)) / 1e6),
                             "value": P / dt, "unit": "points/s", "seconds": dt, "json_build_s_untimed": build_s,
-                            "reply_mb": sum(map(len, outs)) / 1e6}
+                            "reply_mb": sum(map(len, outs)) / 1e6, "host_threads": os.cpu_count() and min(16, os.cpu_count()),
+                            "library_ms": sm.last_timing()}
     sm.close()
     # the service under concurrent load: one SegmentMatcher per client thread (as
     # reporter_service.py's threaded server), every Match coalesced into shared batches

@@ -48,6 +48,11 @@ int rm_match(rm_matcher* m, const char* trace_json, char** out_json);
 /* n traces at once (one GPU launch sequence); outs[i] must each be freed with rm_free. */
 int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs);
 void rm_free(char* p);
+/* Host wall times (ms) of the matcher's last uncoalesced rm_match_batch: out[0] JSON parse
+ * (single pass, up to 16 host threads), [1] staging into pinned host arrays, [2] engine run
+ * (H2D of the batch + every kernel + its size read-backs), [3] segment download (D2H),
+ * [4] reply formatting, [5] total. */
+int rm_matcher_timing(const rm_matcher* m, double out[6]);
 /* Request coalescing (on unless the config sets "reporter_amd": {"coalesce": false}):
  * concurrent rm_match calls from many threads are queued and run as one GPU batch by a
  * dispatcher thread; "coalesce_window_ms" (default 0: take whatever queued while the

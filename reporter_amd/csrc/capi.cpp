@@ -25,8 +25,10 @@
 #include "../../include/reporter_match.h"
 #include "engine.hpp"
 #include "graph.hpp"
+#include "host_pool.hpp"
 #include "json.hpp"
 #include "serve_policy.hpp"
+#include "trace_json.hpp"
 
 using namespace rm;
 
@@ -114,80 +116,17 @@ std::string read_file(const std::string& path) {
   return s;
 }
 
-// parsed trace ready for the engine
+// parsed trace ready for the engine (one request of the coalesced path)
 struct ParsedTrace {
-  std::vector<float> lon, lat, acc;
-  std::vector<double> time;
+  tj::PointSink pts;
   MatchOptions opt;
 };
 
+// one /report Match request (trace_json.hpp: single validating pass, the DOM reader's contract)
 ParsedTrace parse_trace(const char* text, const Config& conf) {
-  json::Value v = json::parse(text);
-  if (v.type != json::Value::Object) throw std::runtime_error("trace request must be a JSON object");
   ParsedTrace t;
-  const json::Value* mo = v.get("match_options");
-  int mode = kModeAuto;
-  if (mo && mo->type == json::Value::Object) {
-    const json::Value* mv = mo->get("mode");
-    if (mv && mv->type == json::Value::String) mode = mode_from_name(mv->str);
-  }
-  t.opt = conf.mode_defaults[mode];
-  t.opt.mode = mode;
-  apply_options(mo, t.opt);
-  const json::Value* tr = v.get("trace");
-  if (!tr || tr->type != json::Value::Array) throw std::runtime_error("trace must be an array of points");
-  if (tr->arr.empty()) throw std::runtime_error("trace must contain at least one point");
-  const size_t n = tr->arr.size();
-  t.lon.resize(n); t.lat.resize(n); t.acc.resize(n); t.time.resize(n);
-  for (size_t i = 0; i < n; ++i) {
-    const json::Value& p = tr->arr[i];
-    const json::Value* la = p.get("lat");
-    const json::Value* lo = p.get("lon");
-    if (!la || !lo || !la->is_num() || !lo->is_num()) throw std::runtime_error("each trace point needs numeric lat and lon");
-    if (!(la->num >= -90.0 && la->num <= 90.0 && lo->num >= -180.0 && lo->num <= 180.0))
-      throw std::runtime_error("trace point out of range");
-    t.lat[i] = (float)la->num;   // Valhalla PointLL is float
-    t.lon[i] = (float)lo->num;
-    const json::Value* tm = p.get("time");
-    t.time[i] = (tm && tm->is_num()) ? tm->num : -1.0;
-    const json::Value* ac = p.get("accuracy");
-    t.acc[i] = (ac && ac->is_num()) ? (float)ac->num : -1.0f;
-  }
+  t.opt = tj::parse_request(text, conf.mode_defaults, t.pts);
   return t;
-}
-
-void append_num(std::string& o, double x) {
-  char buf[40];
-  if (x == -1.0) { o += "-1"; return; }
-  std::snprintf(buf, sizeof buf, "%.17g", x);
-  o += buf;
-}
-void append_u(std::string& o, uint64_t x) { o += std::to_string(x); }
-void append_i(std::string& o, int64_t x) { o += std::to_string(x); }
-
-std::string segments_json(const SegmentRec* s, uint32_t n) {
-  std::string o;
-  o.reserve(64 + n * 200);
-  o += "{\"segments\":[";
-  for (uint32_t k = 0; k < n; ++k) {
-    const SegmentRec& r = s[k];
-    if (k) o += ',';
-    o += '{';
-    if (r.flags & 2u) { o += "\"segment_id\":"; append_u(o, r.segment_id); o += ','; }
-    o += "\"way_ids\":[";
-    append_u(o, r.way_first);
-    if (r.way_last != r.way_first) { o += ','; append_u(o, r.way_last); }
-    o += "],\"start_time\":"; append_num(o, r.start_time);
-    o += ",\"end_time\":"; append_num(o, r.end_time);
-    o += ",\"queue_length\":"; append_i(o, r.queue_length);
-    o += ",\"length\":"; append_i(o, r.length);
-    o += ",\"internal\":"; o += (r.flags & 1u) ? "true" : "false";
-    o += ",\"begin_shape_index\":"; append_u(o, r.begin_shape_index);
-    o += ",\"end_shape_index\":"; append_u(o, r.end_shape_index);
-    o += '}';
-  }
-  o += "]}";
-  return o;
 }
 
 // Request coalescing (HTTP front end): the reference's service answers
@@ -263,47 +202,37 @@ char* dup_string(const std::string& s) {
 
 // run a list of parsed traces as one batch on matcher m; per-trace JSON replies, and per-trace
 // error messages (non-empty = that trace failed alone; its reply is empty)
-// fn(i) for i in [0, n) over up to 16 host threads in contiguous chunks (the JSON parse and
-// formatting around a batch are host work that a single thread makes the boundary's limit);
-// an exception is rethrown for the lowest failing index's chunk, as a serial loop would
+// fn(i) for i in [0, n) over the host pool (up to 16 threads) in contiguous chunks (the JSON
+// parse and formatting around a batch are host work that a single thread makes the boundary's
+// limit); an exception is rethrown for the lowest failing index's chunk, as a serial loop would
 template <class F>
 void parallel_for(size_t n, F&& fn) {
-  const size_t hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t nt = std::min<size_t>(std::min<size_t>(hw, 16), (n + 127) / 128);
+  HostPool& pool = HostPool::get();
+  const size_t nt = std::min<size_t>(pool.size(), (n + 31) / 32);
   if (nt <= 1) {
     for (size_t i = 0; i < n; ++i) fn(i);
     return;
   }
-  std::vector<std::exception_ptr> err(nt);
-  std::vector<std::thread> th;
-  th.reserve(nt);
-  for (size_t t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
-      const size_t a = n * t / nt, b = n * (t + 1) / nt;
-      try {
-        for (size_t i = a; i < b; ++i) fn(i);
-      } catch (...) {
-        err[t] = std::current_exception();
-      }
-    });
-  for (auto& x : th) x.join();
-  for (auto& e : err)
-    if (e) std::rethrow_exception(e);
+  pool.run(nt, [&](size_t t) {
+    const size_t a = n * t / nt, b = n * (t + 1) / nt;
+    for (size_t i = a; i < b; ++i) fn(i);
+  });
 }
 
 std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*>& pt, std::vector<std::string>* errs) {
   const size_t n = pt.size();
   std::vector<uint32_t> off(n + 1, 0), topt(n);
   std::vector<MatchOptions> opts(n);
-  for (size_t i = 0; i < n; ++i) { off[i + 1] = off[i] + (uint32_t)pt[i]->lon.size(); opts[i] = pt[i]->opt; topt[i] = (uint32_t)i; }
+  for (size_t i = 0; i < n; ++i) { off[i + 1] = off[i] + (uint32_t)pt[i]->pts.size(); opts[i] = pt[i]->opt; topt[i] = (uint32_t)i; }
   const uint64_t P = off[n];
   std::vector<float> lon(P), lat(P), acc(P);
   std::vector<double> tm(P);
   parallel_for(n, [&](size_t i) {
-    std::copy(pt[i]->lon.begin(), pt[i]->lon.end(), lon.begin() + off[i]);
-    std::copy(pt[i]->lat.begin(), pt[i]->lat.end(), lat.begin() + off[i]);
-    std::copy(pt[i]->acc.begin(), pt[i]->acc.end(), acc.begin() + off[i]);
-    std::copy(pt[i]->time.begin(), pt[i]->time.end(), tm.begin() + off[i]);
+    const tj::PointSink& q = pt[i]->pts;
+    std::copy(q.lon.begin(), q.lon.end(), lon.begin() + off[i]);
+    std::copy(q.lat.begin(), q.lat.end(), lat.begin() + off[i]);
+    std::copy(q.acc.begin(), q.acc.end(), acc.begin() + off[i]);
+    std::copy(q.time.begin(), q.time.end(), tm.begin() + off[i]);
   });
   HostBatch hb;
   hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = lon.data(); hb.lat = lat.data();
@@ -326,7 +255,7 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
     (*errs)[i] = error_text(terr[i]);
   }
   parallel_for(n, [&](size_t i) {
-    if (!terr[i]) out[i] = segments_json(segs.data() + soff[i], soff[i + 1] - soff[i]);
+    if (!terr[i]) tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], out[i]);
   });
   return out;
 }
@@ -385,10 +314,123 @@ void Coalescer::loop() {
 
 }  // namespace
 
+// pinned host staging of one matcher's batch arrays (grow-only): the parse threads copy their
+// points here and the engine's uploads run at full PCIe rate
+struct HostStaging {
+  float* lon = nullptr; float* lat = nullptr; float* acc = nullptr; double* time = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    release();
+    const size_t c = n + n / 4 + 4096;
+    RM_HIP(hipHostMalloc((void**)&lon, c * 4, hipHostMallocDefault));
+    RM_HIP(hipHostMalloc((void**)&lat, c * 4, hipHostMallocDefault));
+    RM_HIP(hipHostMalloc((void**)&acc, c * 4, hipHostMallocDefault));
+    RM_HIP(hipHostMalloc((void**)&time, c * 8, hipHostMallocDefault));
+    cap = c;
+  }
+  void release() {
+    for (void* q : {(void*)lon, (void*)lat, (void*)acc, (void*)time})
+      if (q) (void)hipHostFree(q);
+    lon = lat = acc = nullptr;
+    time = nullptr;
+    cap = 0;
+  }
+  ~HostStaging() { release(); }
+};
+
 struct rm_matcher {
   std::shared_ptr<Config> conf;
   std::unique_ptr<Matcher> m;
+  HostStaging stage;
+  double ms[6] = {};   // the last rm_match_batch: parse, stage, engine, download, format, total
 };
+
+namespace {
+
+// rm_match_batch without the coalescer: each pool thread parses a contiguous range of the
+// requests into its own point arrays, copies them into the matcher's pinned staging at their
+// batch offsets, and after the engine's run formats its range's replies straight into the
+// caller's output strings.  Any failing trace fails the call, naming the trace.
+void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  const auto t0 = clk::now();
+  HostPool& pool = HostPool::get();
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(pool.size(), (n + 15) / 16));
+  std::vector<tj::PointSink> sink(nt);
+  std::vector<uint32_t> cnt(n), topt(n);
+  std::vector<MatchOptions> opts(n);
+  const Config& conf = *m->conf;
+  pool.run(nt, [&](size_t t) {
+    const size_t a = n * t / nt, b = n * (t + 1) / nt;
+    size_t bytes = 0;
+    for (size_t i = a; i < b; ++i) bytes += std::strlen(traces[i]);
+    tj::PointSink& sk = sink[t];
+    const size_t guess = bytes / 48 + 16;   // a /report point is ~60-90 bytes of JSON
+    sk.lon.reserve(guess); sk.lat.reserve(guess); sk.acc.reserve(guess); sk.time.reserve(guess);
+    for (size_t i = a; i < b; ++i) {
+      const size_t before = sk.size();
+      opts[i] = tj::parse_request(traces[i], conf.mode_defaults, sk);
+      cnt[i] = (uint32_t)(sk.size() - before);
+      topt[i] = (uint32_t)i;
+    }
+  });
+  std::vector<uint32_t> off(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    if ((uint64_t)off[i] + cnt[i] >= 0xffffffffull) throw BatchTooLarge("batch too large (points >= 2^32)");
+    off[i + 1] = off[i] + cnt[i];
+  }
+  const uint64_t P = off[n];
+  m->ms[0] = ms_since(t0);
+  const auto t1 = clk::now();
+  m->stage.ensure(P);
+  HostStaging& hs = m->stage;
+  pool.run(nt, [&](size_t t) {
+    const size_t a = n * t / nt;
+    const tj::PointSink& sk = sink[t];
+    const size_t o = off[a], k = sk.size();
+    std::memcpy(hs.lon + o, sk.lon.data(), k * 4);
+    std::memcpy(hs.lat + o, sk.lat.data(), k * 4);
+    std::memcpy(hs.acc + o, sk.acc.data(), k * 4);
+    std::memcpy(hs.time + o, sk.time.data(), k * 8);
+  });
+  m->ms[1] = ms_since(t1);
+  const auto t2 = clk::now();
+  if (!m->m) m->m = std::make_unique<Matcher>(conf.engine.get());
+  Matcher& mt = *m->m;
+  HostBatch hb;
+  hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = hs.lon; hb.lat = hs.lat;
+  hb.time = hs.time; hb.accuracy = hs.acc; hb.n_opts = (uint32_t)n; hb.opts = opts.data();
+  hb.trace_opt = topt.data();
+  RunParams rp;
+  rp.do_report = 0;
+  mt.set_isolation(true);
+  mt.run(hb, rp);
+  std::vector<uint32_t> terr(n, 0u);
+  if (mt.error_bits()) mt.get_trace_errors(terr.data());
+  for (size_t i = 0; i < n; ++i)
+    if (terr[i]) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
+  m->ms[2] = ms_since(t2);
+  const auto t3 = clk::now();
+  std::vector<uint32_t> soff(n + 1);
+  std::vector<SegmentRec> segs(mt.count_segments());
+  mt.get_segments(soff.data(), segs.data());
+  m->ms[3] = ms_since(t3);
+  const auto t4 = clk::now();
+  pool.run(nt, [&](size_t t) {
+    const size_t a = n * t / nt, b = n * (t + 1) / nt;
+    std::string js;
+    for (size_t i = a; i < b; ++i) {
+      tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], js);
+      outs[i] = dup_string(js);
+    }
+  });
+  m->ms[4] = ms_since(t4);
+  m->ms[5] = ms_since(t0);
+}
+
+}  // namespace
 struct rm_engine {
   std::shared_ptr<Engine> e;
 };
@@ -510,19 +552,14 @@ int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** ou
     if (n == 0) return;
     for (size_t i = 0; i < n; ++i)
       if (!traces[i]) throw std::runtime_error("trace string is NULL");
-    std::vector<ParsedTrace> pt(n);
-    parallel_for(n, [&](size_t i) { pt[i] = parse_trace(traces[i], *m->conf); });
-    std::vector<std::string> js;
     if (n == 1 && m->conf->coalescer) {
-      js.push_back(m->conf->coalescer->submit(&pt[0]));
-    } else {
-      if (!m->m) m->m = std::make_unique<Matcher>(m->conf->engine.get());
-      std::vector<ParsedTrace*> pp;
-      for (auto& t : pt) pp.push_back(&t);
-      js = match_parsed(*m->m, pp, nullptr);   // any failing trace fails the call, naming the trace
+      ParsedTrace pt = parse_trace(traces[0], *m->conf);
+      const std::string js = m->conf->coalescer->submit(&pt);
+      outs[0] = dup_string(js);
+      return;
     }
     try {
-      for (size_t i = 0; i < n; ++i) outs[i] = dup_string(js[i]);
+      match_json_batch(m, traces, n, outs);   // any failing trace fails the call, naming the trace
     } catch (...) {
       for (size_t i = 0; i < n; ++i) { std::free(outs[i]); outs[i] = nullptr; }
       throw;
@@ -537,6 +574,13 @@ int rm_match(rm_matcher* m, const char* trace_json, char** out_json) {
 }
 
 void rm_free(char* p) { std::free(p); }
+
+int rm_matcher_timing(const rm_matcher* m, double out[6]) {
+  return guarded([&] {
+    if (!m || !out) throw std::runtime_error("matcher or out is NULL");
+    for (int i = 0; i < 6; ++i) out[i] = m->ms[i];
+  });
+}
 
 int rm_coalesce_stats(uint64_t out[4]) {
   return guarded([&] {

@@ -66,6 +66,13 @@ class SegmentMatcher(object):
             for o in outs:
                 _lib.lib().rm_free(o)
 
+    def last_timing(self):
+        """Host wall ms of the last uncoalesced MatchMany: parse, stage, engine, download, format, total."""
+        out = (C.c_double * 6)()
+        if _lib.lib().rm_matcher_timing(self._h, out) != 0:
+            raise RuntimeError(_lib.last_error())
+        return dict(zip(("parse_ms", "stage_ms", "engine_ms", "download_ms", "format_ms", "total_ms"), list(out)))
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.lib().rm_matcher_destroy(self._h)
