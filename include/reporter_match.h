@@ -90,6 +90,12 @@ int rm_graph_info(const char* graph_path, uint64_t out[7]);
  * speeds / access from its tags and a grid index of cell_m metres (OSMLR segments only where
  * osmlr relations give them). */
 int rm_graph_export_osm(const char* graph_path, const char* osm_path);
+/* The same OSM elements as OSM PBF (the input valhalla_build_tiles reads, reference
+ * Dockerfile:42-49): zlib-deflated blobs, an OSMHeader (OsmSchema-V0.6, DenseNodes), dense
+ * nodes at nanodegree granularity (exact float coordinates; a reporter:ll tag where nanodegrees
+ * would not bring a float back), ways and relations with packed delta-coded refs. */
+int rm_graph_export_pbf(const char* graph_path, const char* pbf_path);
+/* OSM XML or PBF (told apart by content) -> .rmg. */
 int rm_graph_import_osm(const char* osm_path, const char* graph_path, double cell_m);
 
 typedef struct {

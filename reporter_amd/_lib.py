@@ -85,6 +85,7 @@ PROTOTYPES = [
     ("rm_world_build", C.c_int, [C.POINTER(RmWorldParams), C.c_char_p]),
     ("rm_graph_info", C.c_int, [C.c_char_p, C.POINTER(C.c_uint64)]),
     ("rm_graph_export_osm", C.c_int, [C.c_char_p, C.c_char_p]),
+    ("rm_graph_export_pbf", C.c_int, [C.c_char_p, C.c_char_p]),
     ("rm_graph_import_osm", C.c_int, [C.c_char_p, C.c_char_p, C.c_double]),
     ("rm_default_trace_params", None, [C.POINTER(RmTraceParams)]),
     ("rm_traces_generate", C.c_int, [C.c_char_p, C.POINTER(RmTraceParams), P, P, P, P, P, P]),

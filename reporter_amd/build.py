@@ -19,8 +19,9 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libreporter_match.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-SOURCES = ["engine.hip", "stages.hip", "capi.cpp", "graph.cpp", "graph_osm.cpp", "world.cpp", "balls.cpp"]
-HEADERS = ["engine.hpp", "graph.hpp", "json.hpp", "rm_common.hpp", "balls.hpp"]
+SOURCES = ["engine.hip", "stages.hip", "capi.cpp", "graph.cpp", "graph_osm.cpp", "osm_pbf.cpp", "world.cpp", "balls.cpp"]
+HEADERS = ["engine.hpp", "graph.hpp", "json.hpp", "rm_common.hpp", "balls.hpp", "serve_policy.hpp", "trace_json.hpp",
+           "host_pool.hpp", "osm_model.hpp"]
 
 
 def _hipcc():
@@ -64,7 +65,7 @@ def build(force=False, verbose=False):
     with cf.ThreadPoolExecutor(max_workers=min(4, os.cpu_count() or 1)) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if force or _newer(LIB, objs):
-        cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-o", LIB] + objs + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
+        cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-o", LIB] + objs + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread", "-lz"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))

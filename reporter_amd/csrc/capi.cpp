@@ -631,6 +631,13 @@ int rm_graph_export_osm(const char* graph_path, const char* osm_path) {
   });
 }
 
+int rm_graph_export_pbf(const char* graph_path, const char* pbf_path) {
+  return guarded([&] {
+    if (!graph_path || !pbf_path) throw std::runtime_error("path is NULL");
+    export_osm_pbf(Graph::load(graph_path), pbf_path);
+  });
+}
+
 int rm_graph_import_osm(const char* osm_path, const char* graph_path, double cell_m) {
   return guarded([&] {
     if (!graph_path || !osm_path) throw std::runtime_error("path is NULL");

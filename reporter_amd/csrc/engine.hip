@@ -1117,6 +1117,112 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
   for (uint32_t q = threadIdx.x; q < n; q += blockDim.x) b.route[lo + q] = s_out[q];
 }
 
+// K2 ball tier, block-expanded (round 3).  A block takes 256 consecutive (pair, source) items,
+// whose routes form one contiguous range of b.route.  Phase 1, one lane per item: the pair's
+// constants, the source's exit keys and both exits' table headers go to LDS, and the item's
+// lanes of the range are marked in an owner map.  Phase 2 deals the range over the lanes, one
+// (source, target) transition per lane and step: the target's descriptor, both exits' probes of
+// the target road, the label, the key, one coalesced store.  No lane walks a target loop of its
+// own (the round-2 kernel's lanes ran to their wave's largest K_B, each target two dependent
+// round trips after the last), and two transitions per lane are in flight at once.
+constexpr int kK2Items = 256;
+struct K2Src {
+  unsigned long long rk1, rk0;   // exit root keys (kKeyInf: that exit is unusable)
+  uint2 h1, h0;                  // table headers of the exits (bits 0: no table)
+  const uint4* ent;              // the item's mode's table rows
+  uint32_t road, s;              // source road and offset on it (direct combinations)
+  uint32_t tdesc;                // the pair's first target descriptor (p * kMaxCand)
+  uint32_t rel;                  // the item's first route, relative to the block's range
+  uint32_t bound, tmax;          // pair bounds; bound = kNone: handed to the search tiers
+};
+struct K2Smem {
+  K2Src src[kK2Items];
+  uint8_t owner[kK2Items * kMaxCand];   // route (relative to the range) -> item of the block
+  uint32_t lo, hi;
+};
+
+// route of item S to the target described by (t0, t1), from the target road's rows (r1, r0)
+// in the tables of S's two exits (kRouteInvalid when there is none within the bounds)
+__device__ __forceinline__ uint32_t k2_route(const K2Src& S, const uint4& t0, const uint4& t1, const uint4& r1,
+                                             const uint4& r0) {
+  const unsigned long long lab0 = ball_label(S.rk1, row_key0(r1), S.rk0, row_key0(r0));
+  const unsigned long long lab1 = ball_label(S.rk1, row_key1(r1), S.rk0, row_key1(r0));
+  const uint4 a0 = make_uint4(S.road, S.s, 0u, 0u);   // route_key_vals reads the source's road and offset
+  const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, nullptr);
+  return (key != kKeyInf && key_dist(key) <= S.bound && key_time(key) <= S.tmax) ? key_dist(key) : kRouteInvalid;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_items) {
+  __shared__ K2Smem sm;
+  const uint32_t t0i = xcd_block(blockIdx.x, gridDim.x) * kK2Items;   // first item of the block
+  const uint32_t t = t0i + threadIdx.x;
+  const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;              // last item of the block
+  const bool live = t <= tl;
+  // ---- phase 1: one lane per item
+  uint32_t KB = 0, ob = 0;
+  if (live) {
+    const uint32_t p = b.src_item[t];
+    const uint4 pi = b.pair_info[p];
+    const uint32_t i = t - b.src_off[p];
+    KB = (pi.z >> 8) & 0xffu;
+    ob = b.trans_off[p] + i * KB;
+    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+    const int mode = (int)(pi.z >> 16);
+    K2Src S;
+    exit_keys(a0, pi.x, S.rk1, S.rk0);
+    const bool fits = pi.x <= g.ball_radius[mode] && ((g.ball_mask >> mode) & 1u);
+    S.h1 = fits && S.rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
+    S.h0 = fits && S.rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+    S.ent = g.ball_ent[mode];
+    S.road = a0.x;
+    S.s = a0.y;
+    S.tdesc = p * kMaxCand;
+    S.rel = 0;
+    S.bound = pi.x;
+    S.tmax = pi.y;
+    if (!fits || S.h1.y == 0u || S.h0.y == 0u) {   // the search tiers take it (they run later)
+      S.bound = kNone;
+      b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+    }
+    sm.src[threadIdx.x] = S;
+    if (threadIdx.x == 0) sm.lo = ob;
+    if (t == tl) sm.hi = ob + KB;
+  }
+  __syncthreads();
+  const uint32_t lo = sm.lo, n = sm.hi - lo;
+  if (live) {
+    sm.src[threadIdx.x].rel = ob - lo;
+    for (uint32_t j = 0; j < KB; ++j) sm.owner[ob - lo + j] = (uint8_t)threadIdx.x;
+  }
+  __syncthreads();
+  // ---- phase 2: the block's routes, two transitions per lane and step (loads of both issued
+  // before either is used); a handed-over item's routes are written by the search tiers
+  for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
+    const uint32_t qb = q + kK2Items;
+    const bool hb = qb < n;
+    const K2Src& A = sm.src[sm.owner[q]];
+    const K2Src& B = sm.src[sm.owner[hb ? qb : q]];
+    const bool la = A.bound != kNone, lb = hb && B.bound != kNone;
+    uint4 ta0 = make_uint4(kNone, 0u, 0u, 0u), ta1 = ta0, tb0 = ta0, tb1 = ta0;
+    if (la) {
+      const uint4* d = b.cand_desc + 2 * (uint64_t)(A.tdesc + (q - A.rel));
+      ta0 = d[0]; ta1 = d[1];
+    }
+    if (lb) {
+      const uint4* d = b.cand_desc + 2 * (uint64_t)(B.tdesc + (qb - B.rel));
+      tb0 = d[0]; tb1 = d[1];
+    }
+    const bool ua = la && ta0.w != 0u, ub = lb && tb0.w != 0u;   // some direction of the target road is usable
+    const uint4 ea1 = ball_first(A.ent, A.h1, ta0.x, ua && A.rk1 != kKeyInf);
+    const uint4 ea0 = ball_first(A.ent, A.h0, ta0.x, ua && A.rk0 != kKeyInf);
+    const uint4 eb1 = ball_first(B.ent, B.h1, tb0.x, ub && B.rk1 != kKeyInf);
+    const uint4 eb0 = ball_first(B.ent, B.h0, tb0.x, ub && B.rk0 != kKeyInf);
+    if (la) b.route[lo + q] = k2_route(A, ta0, ta1, ball_resolve(A.ent, A.h1, ta0.x, ea1), ball_resolve(A.ent, A.h0, ta0.x, ea0));
+    if (lb) b.route[lo + qb] = k2_route(B, tb0, tb1, ball_resolve(B.ent, B.h1, tb0.x, eb1), ball_resolve(B.ent, B.h0, tb0.x, eb0));
+  }
+}
+
 // K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
 // one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A search
 // that outgrows the registers is queued (as its item) for the LDS lane tier.
@@ -3165,7 +3271,12 @@ void Matcher::run_device(const RunParams& rp) {
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
   if (n_src && balls) {
-    hipLaunchKernelGGL(k_routes_ball, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
+    static const int k2v = [] { const char* e = std::getenv("RM_K2"); return e ? std::atoi(e) : 2; }();
+    if (k2v == 2)
+      hipLaunchKernelGGL(k_routes_ball2, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st, g, v,
+                         (uint32_t)n_src);
+    else
+      hipLaunchKernelGGL(k_routes_ball, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)), dim3(256), 0,
                        st, g, v, 0u, 1);
   } else if (n_src) {

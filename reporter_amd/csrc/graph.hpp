@@ -95,6 +95,9 @@ double piece_m(float lon0, float lat0, float lon1, float lat1);
 // highway / maxspeed / oneway / access tags give speeds and access, no OSMLR segments
 // unless osmlr relations are present; cell_m sizes the grid index then).
 void export_osm(const Graph& g, const std::string& path);
+// the same elements as OSM PBF (osm_pbf.cpp: zlib blobs, dense nodes, nanodegree granularity)
+void export_osm_pbf(const Graph& g, const std::string& path);
+// XML or PBF, told apart by content
 Graph import_osm(const std::string& path, double cell_m = 100.0);
 
 // Synthetic GPS traces (restating reference py/generate_test_trace.py:35-104,120-164):

@@ -57,8 +57,15 @@ def export_osm(graph_path, osm_path):
     return osm_path
 
 
+def export_pbf(graph_path, pbf_path):
+    """The .rmg graph as OSM PBF (the same elements as export_osm; the tile builder's input)."""
+    _lib.check(_lib.lib().rm_graph_export_pbf(os.fsencode(graph_path), os.fsencode(pbf_path)))
+    return pbf_path
+
+
 def import_osm(osm_path, graph_path, cell_m=100.0):
-    """OSM XML -> .rmg (bit-identical for an export_osm file; generic OSM split at intersections)."""
+    """OSM XML or PBF -> .rmg (bit-identical for an export_osm / export_pbf file; generic OSM split
+    at intersections)."""
     _lib.check(_lib.lib().rm_graph_import_osm(os.fsencode(osm_path), os.fsencode(graph_path), float(cell_m)))
     return graph_path
 
@@ -115,4 +122,36 @@ def concat_traces(*sets):
         off.append(s["trace_off"][1:].astype(np.uint64) + base)
         base += int(s["trace_off"][-1])
     out["trace_off"] = np.concatenate(off).astype(np.uint32)
+    return out
+
+
+# Valhalla's tile hierarchy (reference py/get_tiles.py:30-39: world bbox, tile sizes 4 / 1 /
+# 0.25 degrees for levels 0 / 1 / 2) and its tile file naming (GetFile, :79-102)
+_TILE_SIZE = {0: 4.0, 1: 1.0, 2: 0.25}
+
+
+def valhalla_tile_file(level, tile_id, suffix="gph"):
+    """Path of a Valhalla tile file, as get_tiles.py:79-102 GetFile forms it: the id (with the
+    level in front) zero-padded to a multiple of three digits, split into 3-digit directories."""
+    size = _TILE_SIZE[level]
+    ncols, nrows = int(np.ceil(360.0 / size)), int(np.ceil(180.0 / size))
+    max_id = ncols * nrows - 1
+    digits = len(str(max_id))
+    if digits % 3:
+        digits += 3 - digits % 3
+    s = "{:,}".format(level * 10 ** digits + tile_id if level else 10 ** digits + tile_id).replace(",", "/")
+    if level == 0:
+        s = "0" + s[1:]
+    return s + "." + suffix
+
+
+def valhalla_tiles(graph_path):
+    """{(level, tile id): tile file} of every tile the graph's OSMLR segment ids name
+    (id layout level:3 | tile:22 | index:21, reference py/simple_reporter.py:37-49) — the tiles a
+    Valhalla build of the exported OSM would have to produce for the two paths to agree."""
+    from . import graphfile
+    ids = graphfile.load(graph_path)["seg_id"].astype(np.uint64)
+    out = {}
+    for lv, tl in set(zip((ids & np.uint64(7)).tolist(), ((ids >> np.uint64(3)) & np.uint64(0x3FFFFF)).tolist())):
+        out[(int(lv), int(tl))] = valhalla_tile_file(int(lv), int(tl))
     return out

@@ -46,7 +46,7 @@ for s in build.SOURCES:
     objs.append(o)
 lib = os.path.join(out_dir, name + ".so")
 subprocess.run([build._hipcc(), "--offload-arch=" + build.ARCH, "-shared", "-o", lib] + objs +
-               ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"], check=True)
+               ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread", "-lz"], check=True)
 for o in objs:
     if o.startswith(out_dir):
         os.remove(o)
