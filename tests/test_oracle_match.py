@@ -92,3 +92,15 @@ def test_truth_recovery_sparse_and_sigma_sweep(built_lib, tmp_path):
             frac, n, _ = truth_recovery(tr["trace_off"], out["n_states"], out["state_orig"], out["cand_road"],
                                         out["choice"], tr["truth_edge"], g["edges"])
             assert n > 300 and frac > floor, (mode, sz, frac, n)
+
+
+def test_oracle_on_the_readme_manila_trace(tmp_path, built_lib):
+    """The README.md:269 trace (no accuracy, 7-29 s sampling) on a world centred on it: the
+    oracle's segments follow the reply schema README.md:270-301 (the GPU test compares the
+    engine against these)."""
+    from test_gpu_manila import check_schema, manila_world, oracle_segments
+    path = str(tmp_path / "manila.rmg")
+    req = manila_world(path)
+    segs = oracle_segments(path, req)
+    assert len(segs) >= 3 and any("segment_id" in s for s in segs)
+    check_schema(segs, len(req["trace"]))
