@@ -56,9 +56,10 @@ def parse():
     ap.add_argument("--json-traces", type=int, default=10000, help="traces sent through rm_match_batch as JSON")
     ap.add_argument("--ball-radius", type=float, default=None,
                     help="route-ball radius in m (default: the config's, else the engine's automatic radius)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_routes_c2.json"),
-                    help="rocprofv3 PMC summary giving HBM bytes per routes launch (optional; used only when it "
-                         "was measured on this engine.hip)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="rocprofv3 PMC summary giving HBM bytes per stage launch (scripts/pmc_summary.py; default "
+                         "profiles/r03/pmc_routes_<config>.json; used only when it was measured on this engine.hip "
+                         "with the same config and trace count)")
     return ap.parse_args()
 
 
@@ -84,9 +85,11 @@ def _cpu_worker(block):
     b = mo.Batch(sub_off, tr["lon"][o0:o1], tr["lat"][o0:o1], tr["time"][o0:o1], tr["accuracy"][o0:o1], opts,
                  np.zeros(hi - lo, np.uint32))
     hist = np.zeros(len(g["seg_id"]) * 16, np.uint32)
+    dur = np.zeros(len(g["seg_id"]), np.uint64)
+    mo.prepare_path_counters(g)   # in-edge index of the path-walk counters, outside the timed region
     mo.reset_counters()
     t = time.perf_counter()
-    nrep = mo.pipeline(g, b, 15.0, 0x6, 0x6, hist)
+    nrep = mo.pipeline(g, b, 15.0, 0x6, 0x6, hist, dur)
     dt = time.perf_counter() - t
     return dt, int(o1 - o0), nrep, mo.counters()
 
@@ -144,20 +147,45 @@ def shard_ids(config, n_per_rank, n_points, world, rank):
 LAUNCHES = 1   # launches of each stage per step (one per concurrent part of the batch)
 
 
-def roofline(name, kernels, abytes, ms, formulation):
+def roofline(name, kernels, abytes, ms, formulation, traffic=None):
     """abytes / ms: the step's algorithmic bytes and summed launch time of the stage; reported
-    per launch (each part's launch does its share of the bytes, timed on its own stream)."""
+    per launch (each part's launch does its share of the bytes, timed on its own stream).
+    traffic: HBM bytes per launch from the PMC passes of this build (or None); dram_frac is what
+    the HBM pins saw (traffic / time / peak) beside the algorithmic fraction."""
     abytes = abytes / LAUNCHES if abytes else abytes
     ms = ms / LAUNCHES if ms else ms
     if not abytes or not ms:
         return {"kernel": kernels, "formulation": formulation, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": None, "traffic": None, "algorithmic_bytes_per_launch": abytes,
-                "avg_launch_ms": ms, "launches_per_step": LAUNCHES}
+                "unit": "GB/s", "frac": None, "traffic": traffic, "dram_frac": None,
+                "algorithmic_bytes_per_launch": abytes, "avg_launch_ms": ms, "launches_per_step": LAUNCHES}
     achieved = abytes / (ms * 1e-3) / 1e9
+    dram = traffic / (ms * 1e-3) / 1e9 if traffic else None
     return {"kernel": kernels, "formulation": formulation, "bound": "hbm", "achieved": achieved,
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "frac_vs_measured_copy": achieved / HBM_MEASURED_GBS, "traffic": None,
+            "frac_vs_measured_copy": achieved / HBM_MEASURED_GBS, "traffic": traffic,
+            "dram_achieved": dram, "dram_frac": dram / HBM_PEAK_GBS if dram else None,
             "algorithmic_bytes_per_launch": abytes, "avg_launch_ms": ms, "launches_per_step": LAUNCHES}
+
+
+def load_traffic(path, config, traces, streams):
+    """Per-stage HBM bytes per launch from scripts/pmc_summary.py output, when it was measured on
+    this engine.hip with the same workload; else ({}, reason)."""
+    if not path or not os.path.exists(path):
+        return {}, "no PMC summary at %s (engine.hip sha %s)" % (path, engine_sha())
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError) as e:
+        return {}, "unreadable PMC summary %s: %s" % (path, e)
+    if not (tj.get("config") == config and tj.get("traces") == traces and tj.get("engine_sha") == engine_sha()
+            and tj.get("streams", 1) == streams):
+        return {}, "PMC summary %s is of another build or workload (sha %s vs %s)" % (
+            os.path.relpath(path, ROOT), tj.get("engine_sha"), engine_sha())
+    stages = tj.get("stages") or {"routes": {"hbm_bytes_per_launch": tj.get("hbm_bytes_per_launch"),
+                                             "l2_hit_rate": tj.get("l2_hit_rate")}}
+    note = ("%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this engine.hip (sha %s), read side x%s per "
+            "MI355X_MICROARCH.md" % (os.path.relpath(path, ROOT), engine_sha(), tj.get("read_factor", 2)))
+    return {k: v for k, v in stages.items() if v.get("hbm_bytes_per_launch")}, note
 
 
 def timed(fn, steps, comm, sync):
@@ -323,8 +351,9 @@ def main():
     bm = engine.MultiMatcher(eng, a.streams) if a.streams > 1 else engine.BatchMatcher(eng)
     nseg = eng.n_segments
     hist = dist.DeviceBuffer(nseg * 16 * 4)
+    dur = dist.DeviceBuffer(nseg * 8)   # per-segment duration sums, reduced with the counts
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
-    rp = dict(hist_dev=hist.ptr, zero_hist=True)
+    rp = dict(hist_dev=hist.ptr, dur_dev=dur.ptr, zero_hist=True)
     bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, None, **rp)
     cold_s = time.perf_counter() - t_up
 
@@ -334,6 +363,7 @@ def main():
     def allreduce():
         if comm is not None:
             comm.allreduce(hist.ptr, nseg * 16, dist.U32, dist.SUM)
+            comm.allreduce(dur.ptr, nseg, dist.U64, dist.SUM)
 
     def step():
         bm.rerun(**rp)
@@ -377,6 +407,7 @@ def main():
     total_points = comm.allreduce_host(P, dist.SUM) if comm is not None else P
     sizes = bm.sizes()
     hist_sum = int(hist.download().sum())
+    dur_sum = int(dur.download(np.uint64).sum())
     balls = eng.ball_stats(0)
     tiers = bm.route_tiers()
 
@@ -394,22 +425,12 @@ def main():
             abytes, formulation = mo.routes_algorithmic_bytes(counts), "bounded searches"
         else:
             abytes, formulation = None, None
-        k2 = roofline("K2", "K2 route stage: k_src_items + k_routes_ball + search tiers for hand-overs", abytes,
-                      ms["routes"], formulation)
-        traffic, traffic_note = None, "no PMC summary of this engine.hip (sha %s)" % engine_sha()
-        if os.path.exists(a.traffic_json):
-            try:
-                with open(a.traffic_json) as f:
-                    tj = json.load(f)
-                if (tj.get("config") == a.config and tj.get("traces") == n_per and tj.get("engine_sha") == engine_sha()
-                        and tj.get("streams", 1) == max(1, a.streams)):
-                    traffic = tj.get("hbm_bytes_per_launch")
-                    traffic_note = ("%s: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this engine.hip (sha %s), "
-                                    "read side x%s per MI355X_MICROARCH.md" % (
-                                        os.path.relpath(a.traffic_json, ROOT), engine_sha(), tj.get("read_factor", 2)))
-            except (OSError, ValueError):
-                traffic = None
-        k2["traffic"] = traffic
+        tpath = a.traffic_json or os.path.join(ROOT, "profiles", "r03", "pmc_routes_%s.json" % a.config.lower())
+        traffic, traffic_note = load_traffic(tpath, a.config, n_per, max(1, a.streams))
+        tr_of = lambda st: (traffic.get(st) or {}).get("hbm_bytes_per_launch")
+        k2 = roofline("K2", "K2 route stage: k_src_items + k_routes_ball2 + search tiers for hand-overs", abytes,
+                      ms["routes"], formulation, tr_of("routes"))
+        k2["l2_hit_rate"] = (traffic.get("routes") or {}).get("l2_hit_rate")
         k2["traffic_source"] = traffic_note
         k2.update({"search_equivalent_bytes_per_launch": mo.routes_algorithmic_bytes(counts) if counts else None,
                    "counts": counts, "route_tiers": tiers, "route_balls": balls, "k1_grid_split": eng.grid_split()})
@@ -417,13 +438,19 @@ def main():
             "K1": roofline("K1", "k_candidates_lane + k_candidates_wave", mo.candidates_algorithmic_bytes(counts)
                            if counts else None, ms["candidates"], "cell-major 32 B records on the engine grid (file cells split "
                            "%dx%d; items counted by the oracle on that grid), per-road minima in registers"
-                           % (eng.grid_split(), eng.grid_split())),
-            "K2": {k: k2[k] for k in ("kernel", "achieved", "frac", "algorithmic_bytes_per_launch", "avg_launch_ms")},
+                           % (eng.grid_split(), eng.grid_split()), tr_of("candidates")),
+            "K2": {k: k2[k] for k in ("kernel", "achieved", "frac", "algorithmic_bytes_per_launch", "avg_launch_ms",
+                                      "traffic", "dram_frac")},
             "K3": roofline("K3", "k_viterbi", mo.viterbi_algorithmic_bytes(counts) if counts else None, ms["viterbi"],
-                           "u32 routes + f32 emissions, fp64 costs in registers"),
+                           "u32 routes + f32 emissions, fp64 costs in registers", tr_of("viterbi")),
+            "paths": roofline("paths", "path stage: k_paths_ball + search tiers for hand-overs",
+                              mo.paths_algorithmic_bytes(counts) if counts and "path_rows" in counts else None,
+                              ms["paths"], "route-ball labels, walk back by canonical predecessors over "
+                              "self-contained in-edge records", tr_of("paths")),
             "K4": roofline("K4", "segments stage: trav_off scan + k_rec_slot + k_seg_wave",
                            mo.segments_algorithmic_bytes(counts) if counts else None, ms["segments"],
-                           "wave per trace, 64 traversal records per step in registers, runs by ballot/scan"),
+                           "wave per trace, 64 traversal records per step in registers, runs by ballot/scan",
+                           tr_of("segments")),
         }
         step_ms = elapsed / steps * 1e3
         build_ms = balls["build_ms"]
@@ -448,12 +475,12 @@ def main():
                 "traces_rank0": T,
                 "points_all_ranks": int(total_points),
                 "graph": W.graph_info(gpath),
-                "parallelism": "uuid shard x%d (dist.shard_by_uuid), graph replicated, RCCL all-reduce of %d x 16 u32 "
-                               "speed histogram every step; per GPU the batch runs as %d concurrent part(s), one HIP "
+                "parallelism": "uuid shard x%d (dist.shard_by_uuid), graph replicated, RCCL all-reduce of the %d x 16 "
+                               "u32 speed histogram and the per-segment u64 duration sums every step; per GPU the batch runs as %d concurrent part(s), one HIP "
                                "stream each" % (world, nseg, max(1, a.streams)),
             },
             "ms_allreduce": t_ar / steps * 1e3,
-            "allreduce_bytes": nseg * 16 * 4,
+            "allreduce_bytes": nseg * 16 * 4 + nseg * 8,
             "ms_matching_only": t_match / steps * 1e3,
             "value_matching_only": total_points * a.steps / t_match,
             "roofline": k2,
@@ -471,6 +498,7 @@ def main():
                                 "per step)" % (max(1, a.streams), t_staged / steps * 1e3)),
             "sizes_rank0": sizes,
             "histogram_total": hist_sum,
+            "duration_sum_total_s": dur_sum,
         }
         if comm_note:
             out["comm_note"] = comm_note
@@ -484,6 +512,7 @@ def main():
     if comm is not None:
         comm.close()
     hist.close()
+    dur.close()
     bm.close()
     eng.close()
     if rank == 0 and world == 1 and not a.no_extras and a.config == "C2":

@@ -188,7 +188,11 @@ typedef struct {
   uint32_t transition_mask;
   uint32_t* hist_dev;         /* device pointer, n_segments*16 u32 speed histogram, may be NULL */
   int32_t do_report;          /* run the report() epilogue */
-  int32_t zero_hist;          /* zero hist_dev on the runner's stream before the epilogue */
+  int32_t zero_hist;          /* zero hist_dev (and dur_dev) on the runner's stream before the epilogue */
+  uint64_t* dur_dev;          /* device pointer, n_segments u64: per OSMLR segment the sum of the reports'
+                                 whole-second durations int(round(t1 - t0)) (the tile rows' duration
+                                 column, py/simple_reporter.py:179) over the reports the histogram counts;
+                                 may be NULL.  Integer sums, so the multi-GPU all-reduce is exact */
 } rm_run_params;
 void rm_default_run_params(rm_run_params* p);
 
@@ -304,6 +308,16 @@ int rm_comm_allreduce(rm_comm* c, void* dev_buf, size_t count, int dtype, int op
 /* all-reduce of one host double (op as above) */
 int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op);
 int rm_comm_barrier(rm_comm* c);
+/* A communicator over a host transport the caller supplies (e.g. the gloo backend of an
+ * existing job, or a test harness): fn must be a blocking all-gather across the nranks callers,
+ * placing every rank's `bytes` bytes of send at recv + rank * bytes, and return 0.  Every rm_comm
+ * operation then runs over it (device buffers staged through host memory); device -1 makes a
+ * host-only communicator (rm_comm_allreduce_host_f64 and rm_comm_barrier work without a GPU). */
+typedef int (*rm_host_allgather_fn)(void* ctx, const void* send, size_t bytes, void* recv);
+rm_comm* rm_comm_init_host(int nranks, int rank, rm_host_allgather_fn fn, void* ctx, int device);
+/* Host-only: the rank that culls and writes time-tile file (bucket, level | tile index << 3) when
+ * rm_runner_tiles runs with an nranks communicator (the device filter uses the same function). */
+int rm_tile_file_owner(uint64_t bucket, uint32_t tile, int nranks);
 
 /* ---------------- device memory helpers (histograms without a framework) ---------------- */
 int rm_device_alloc(size_t bytes, void** dev_ptr);

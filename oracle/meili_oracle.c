@@ -159,13 +159,24 @@ static uint64_t mk(uint32_t d, uint32_t t) { return ((uint64_t)d << 32) | t; }
  *     direction), one per usable exit of the source [9] candidate descriptors read by K2
  *     (KA sources + KB targets per layer pair) [10] candidates kept (sum of K over states)
  * [11] grid rows visited by the candidate search (one item range per row) [12] chained
- * transitions (a path is built) [13] path edges [14] segments formed */
-#define OG_NCNT 15
+ * transitions (a path is built) [13] path edges [14] segments formed
+ * [15] in-edge records the path walk visits (a walked node's in-edges in edge-id order up to
+ *      its canonical predecessor) [16] route-ball rows the path stage reads: per chained
+ *      transition one per usable exit for each usable direction of the target road, and per
+ *      usable in-edge visited one per usable exit (counted only after og_prepare_path_counters) */
+#define OG_NCNT 17
 static uint64_t og_cnt[OG_NCNT];
 static uint32_t og_roots;   /* usable exits of the last search_from */
 static int og_counting = 0;
 void og_reset_counters(void) { memset(og_cnt, 0, sizeof og_cnt); }
 void og_get_counters(uint64_t* out) { memcpy(out, og_cnt, sizeof og_cnt); }
+
+/* in-edge index of one graph for counters [15]/[16] (in-edges of a node in edge-id order, the
+ * order the GPU path walk visits them); built outside any timed region */
+static const uint32_t* pc_node_off = NULL;
+static uint32_t pc_nodes = 0;
+static uint32_t* pc_in_off = NULL;
+static uint32_t* pc_in_edge = NULL;
 
 /* ---------------- result container ---------------- */
 struct og_result {
@@ -721,6 +732,10 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
       R->route_dist[l] = D;
       /* directed edge sequence: exit edge, graph edges, entry edge */
       uint32_t ns = 0;
+      const int pcount = pc_node_off == g->node_off && pc_nodes == g->n_nodes;
+      if (pcount) {   /* entry labels: both exits' rows of the target road per usable direction */
+        og_cnt[16] += (uint64_t)og_roots * ((uint32_t)e_ok(g, g->road_fwd[rb], acc) + (uint32_t)e_ok(g, g->road_rev[rb], acc));
+      }
       if (combo <= 1) {
         stack[ns++] = combo == 0 ? g->road_fwd[ra] : g->road_rev[ra];
       } else {
@@ -730,6 +745,14 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
         stack[ns++] = entry_e;
         while (ws.label[v] != ws.rootkey[v]) {
           const uint32_t e = ws.pred[v];
+          if (pcount) {   /* in-edges of v visited in edge-id order up to the canonical one */
+            for (uint32_t q = pc_in_off[v]; q < pc_in_off[v + 1]; ++q) {
+              const uint32_t f = pc_in_edge[q];
+              og_cnt[15]++;
+              if (e_ok(g, f, acc)) og_cnt[16] += og_roots;
+              if (f == e) break;
+            }
+          }
           if (ns == scap) { scap *= 2; stack = (uint32_t*)realloc(stack, sizeof(uint32_t) * scap); }
           stack[ns++] = e;
           /* source node of e: binary search in CSR */
@@ -859,8 +882,28 @@ int og_report_trace(const og_segment* segs, uint32_t n, double end_time, double 
   return nrep;
 }
 
+void og_prepare_path_counters(const og_graph* g) {
+  free(pc_in_off); free(pc_in_edge);
+  pc_nodes = g->n_nodes;
+  pc_in_off = (uint32_t*)calloc((size_t)g->n_nodes + 1, sizeof(uint32_t));
+  pc_in_edge = (uint32_t*)malloc(sizeof(uint32_t) * (g->n_edges ? g->n_edges : 1));
+  uint32_t* fill = (uint32_t*)malloc(sizeof(uint32_t) * (g->n_nodes ? g->n_nodes : 1));
+  if (!pc_in_off || !pc_in_edge || !fill) { free(fill); pc_node_off = NULL; return; }
+  for (uint32_t e = 0; e < g->n_edges; ++e) pc_in_off[e_target(g, e) + 1]++;
+  for (uint32_t n = 0; n < g->n_nodes; ++n) pc_in_off[n + 1] += pc_in_off[n];
+  memcpy(fill, pc_in_off, sizeof(uint32_t) * g->n_nodes);
+  for (uint32_t e = 0; e < g->n_edges; ++e) pc_in_edge[fill[e_target(g, e)]++] = e;
+  free(fill);
+  pc_node_off = g->node_off;
+}
+
 uint64_t og_pipeline(const og_graph* g, const og_batch* b, double threshold, uint32_t rmask, uint32_t tmask,
                      uint32_t* hist) {
+  return og_pipeline2(g, b, threshold, rmask, tmask, hist, NULL);
+}
+
+uint64_t og_pipeline2(const og_graph* g, const og_batch* b, double threshold, uint32_t rmask, uint32_t tmask,
+                      uint32_t* hist, uint64_t* dur) {
   og_result* r = og_match(g, b);
   if (!r) return 0;
   uint64_t total = 0;
@@ -881,6 +924,9 @@ uint64_t og_pipeline(const og_graph* g, const og_batch* b, double threshold, uin
         if (bin < 0) bin = 0;
         hist[(uint64_t)x->seg_dense * 16u + (uint32_t)bin] += 1u;
       }
+      /* duration column of the tile row, int(round(t1 - t0)) (simple_reporter.py:179):
+       * Python 2 round() is half away from zero, as C round() */
+      if (dur && x->seg_dense != OG_NONE) dur[x->seg_dense] += (uint64_t)round(dt);
       total++;
     }
   }

@@ -108,9 +108,16 @@ int og_report_trace(const og_segment* segs, uint32_t n_segs, double trace_end_ti
 uint64_t og_pipeline(const og_graph* g, const og_batch* b, double threshold_sec, uint32_t report_mask,
                      uint32_t transition_mask, uint32_t* hist);
 
-/* Algorithmic work of the searches/candidate scans since the last reset:
+/* as og_pipeline; dur (may be NULL): n_segments u64 sums of the whole-second durations
+ * int(round(t1 - t0)) of the reports the histogram counts */
+uint64_t og_pipeline2(const og_graph* g, const og_batch* b, double threshold_sec, uint32_t report_mask,
+                      uint32_t transition_mask, uint32_t* hist, uint64_t* dur);
+/* build the in-edge index that the path-walk counters [15]/[16] need (once per graph) */
+void og_prepare_path_counters(const og_graph* g);
+
+/* Algorithmic work of the stages since the last reset (meili_oracle.c lists all 17):
  * [0] searches [1] settled nodes [2] scanned edges [3] label writes
- * [4] target label lookups [5] route writes [6] candidate items tested [7] states */
+ * [4] target label lookups [5] route writes [6] candidate items tested [7] states ... */
 void og_reset_counters(void);
 void og_get_counters(uint64_t* out8);
 

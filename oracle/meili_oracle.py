@@ -57,6 +57,10 @@ def lib():
         h.og_pipeline.restype = C.c_uint64
         h.og_pipeline.argtypes = [C.POINTER(OgGraph), C.POINTER(OgBatch), C.c_double, C.c_uint32, C.c_uint32,
                                   C.c_void_p]
+        h.og_pipeline2.restype = C.c_uint64
+        h.og_pipeline2.argtypes = [C.POINTER(OgGraph), C.POINTER(OgBatch), C.c_double, C.c_uint32, C.c_uint32,
+                                   C.c_void_p, C.c_void_p]
+        h.og_prepare_path_counters.argtypes = [C.POINTER(OgGraph)]
         h.og_reset_counters.argtypes = []
         h.og_get_counters.argtypes = [C.c_void_p]
         _lib = h
@@ -65,7 +69,13 @@ def lib():
 
 COUNTER_NAMES = ("searches", "settled", "scanned", "label_writes", "target_lookups", "route_writes",
                  "cand_items", "states", "ball_rows", "desc_reads", "cands", "grid_rows", "chained", "path_edges",
-                 "segments")
+                 "segments", "path_in_edges", "path_rows")
+
+
+def prepare_path_counters(graph):
+    """Build the in-edge index the path-walk counters need (call outside timed regions; the
+    graph's arrays must stay alive while matching on it)."""
+    lib().og_prepare_path_counters(C.byref(make_graph(graph)))
 
 
 def reset_counters():
@@ -115,6 +125,16 @@ def segments_algorithmic_bytes(c):
     (segment, offset, way); per chained transition 64 B (two candidate offsets, two state
     indices, two times, route length, path header); per segment 56 B written."""
     return 32 * c["path_edges"] + 64 * c["chained"] + 56 * c["segments"]
+
+
+def paths_algorithmic_bytes(c):
+    """Path stage (k_paths_ball) algorithmic bytes: per chained transition 64 B of the chosen
+    candidates' descriptors + 16 B pair constants + 16 B of exit table headers + 20 B written
+    (route length, both offsets, path count and offset); 16 B per route-ball row read (entry
+    labels and the labels of visited in-edges' sources); 20 B per in-edge visited by the walk
+    (self-contained record + access word); 4 B per path edge written.  Needs the counters of
+    prepare_path_counters."""
+    return 116 * c["chained"] + 16 * c["path_rows"] + 20 * c["path_in_edges"] + 4 * c["path_edges"]
 
 
 def make_graph(g):
@@ -204,8 +224,10 @@ def report_trace(segs, trace_end_time, threshold_sec, report_mask, transition_ma
     return out[:n], {f: getattr(st, f) for f, _ in OgStats._fields_}
 
 
-def pipeline(graph, batch, threshold_sec=15.0, report_mask=0x6, transition_mask=0x6, hist=None):
-    """Whole CPU pipeline (match + report + histogram); returns #valid reports."""
+def pipeline(graph, batch, threshold_sec=15.0, report_mask=0x6, transition_mask=0x6, hist=None, dur=None):
+    """Whole CPU pipeline (match + report + histogram [+ per-segment u64 duration sums]);
+    returns #valid reports."""
     og = make_graph(graph)
     hp = hist.ctypes.data if hist is not None else None
-    return int(lib().og_pipeline(C.byref(og), C.byref(batch.c), threshold_sec, report_mask, transition_mask, hp))
+    dp = dur.ctypes.data if dur is not None else None
+    return int(lib().og_pipeline2(C.byref(og), C.byref(batch.c), threshold_sec, report_mask, transition_mask, hp, dp))

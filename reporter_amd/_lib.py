@@ -44,7 +44,8 @@ class RmBatchDesc(C.Structure):
 
 class RmRunParams(C.Structure):
     _fields_ = [("threshold_sec", C.c_double), ("report_mask", C.c_uint32), ("transition_mask", C.c_uint32),
-                ("hist_dev", C.c_void_p), ("do_report", C.c_int32), ("zero_hist", C.c_int32)]
+                ("hist_dev", C.c_void_p), ("do_report", C.c_int32), ("zero_hist", C.c_int32),
+                ("dur_dev", C.c_void_p)]
 
 
 class RmPointsDesc(C.Structure):
@@ -138,6 +139,8 @@ PROTOTYPES = [
     ("rm_comm_allreduce", C.c_int, [P, P, C.c_size_t, C.c_int, C.c_int]),
     ("rm_comm_allreduce_host_f64", C.c_int, [P, C.POINTER(C.c_double), C.c_int]),
     ("rm_comm_barrier", C.c_int, [P]),
+    ("rm_comm_init_host", P, [C.c_int, C.c_int, P, P, C.c_int]),
+    ("rm_tile_file_owner", C.c_int, [C.c_uint64, C.c_uint32, C.c_int]),
     ("rm_device_alloc", C.c_int, [C.c_size_t, C.POINTER(P)]),
     ("rm_device_free", C.c_int, [P]),
     ("rm_device_memset", C.c_int, [P, C.c_int, C.c_size_t]),

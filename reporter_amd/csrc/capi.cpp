@@ -796,7 +796,7 @@ void rm_runner_destroy(rm_runner* r) { delete r; }
 
 void rm_default_run_params(rm_run_params* p) {
   p->threshold_sec = 15.0; p->report_mask = 0x6; p->transition_mask = 0x6; p->hist_dev = nullptr; p->do_report = 1;
-  p->zero_hist = 0;
+  p->zero_hist = 0; p->dur_dev = nullptr;
 }
 
 static RunParams to_rp(const rm_run_params* p) {
@@ -804,6 +804,7 @@ static RunParams to_rp(const rm_run_params* p) {
   if (p) {
     rp.threshold_sec = p->threshold_sec; rp.report_mask = p->report_mask; rp.transition_mask = p->transition_mask;
     rp.hist = p->hist_dev; rp.do_report = p->do_report; rp.zero_hist = p->zero_hist;
+    rp.dur = (unsigned long long*)p->dur_dev;
   }
   return rp;
 }
@@ -824,10 +825,12 @@ int rm_runners_rerun(rm_runner* const* rs, uint32_t n, const rm_run_params* p) {
     for (uint32_t i = 0; i < n; ++i)
       if (!rs[i]) throw std::runtime_error("runner is NULL");
     RunParams rp = to_rp(p);
-    if (rp.hist && rp.zero_hist && rp.do_report) {
+    if ((rp.hist || rp.dur) && rp.zero_hist && rp.do_report) {
       // the parts add into one histogram: zero it once before any part reports
       hipStream_t st = rs[0]->m->stream();
-      RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)rs[0]->m->engine().n_segments() * kHistBins * sizeof(uint32_t), st));
+      const size_t nseg = rs[0]->m->engine().n_segments();
+      if (rp.hist) RM_HIP(hipMemsetAsync(rp.hist, 0, nseg * kHistBins * sizeof(uint32_t), st));
+      if (rp.dur) RM_HIP(hipMemsetAsync(rp.dur, 0, nseg * 8u, st));
       RM_HIP(hipStreamSynchronize(st));
     }
     rp.zero_hist = false;
@@ -909,9 +912,73 @@ struct rm_comm {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   void* scratch = nullptr;  // 8 bytes for host-value reductions and barriers
-  int device = 0;
+  int device = 0;           // -1: a host communicator without a GPU (host values and barriers only)
   int rank = 0, nranks = 1;
+  rm_host_allgather_fn host_fn = nullptr;   // set: every collective runs over this host transport
+  void* host_ctx = nullptr;
 };
+
+namespace {
+// every rank's `bytes` host bytes, in rank order (host transport)
+std::vector<uint8_t> host_gather(rm_comm* c, const void* send, size_t bytes) {
+  std::vector<uint8_t> all(bytes * (size_t)c->nranks + 1);
+  if (c->host_fn(c->host_ctx, send, bytes, all.data()) != 0) throw std::runtime_error("host all-gather failed");
+  all.resize(bytes * (size_t)c->nranks);
+  return all;
+}
+
+// element-wise reduction of every rank's buffer in rank order (host transport)
+template <class T>
+void reduce_ranks(T* dst, const uint8_t* all, size_t count, int nranks, int op) {
+  const T* a = (const T*)all;
+  for (size_t i = 0; i < count; ++i) {
+    T v = a[i];
+    for (int r = 1; r < nranks; ++r) {
+      const T x = a[(size_t)r * count + i];
+      v = op == 0 ? (T)(v + x) : (x > v ? x : v);
+    }
+    dst[i] = v;
+  }
+}
+
+// the tile stage's collectives over RCCL
+struct RcclTileComm final : TileComm {
+  ncclComm_t nc;
+  void* scratch;
+  RcclTileComm(rm_comm* c) : nc(c->comm), scratch(c->scratch) { rank = c->rank; nranks = c->nranks; }
+  uint64_t max_u64(uint64_t v, hipStream_t st) override {
+    RM_HIP(hipMemcpyAsync(scratch, &v, 8, hipMemcpyHostToDevice, st));
+    if (ncclAllReduce(scratch, scratch, 1, ncclUint64, ncclMax, nc, st) != ncclSuccess)
+      throw std::runtime_error("ncclAllReduce failed");
+    RM_HIP(hipMemcpyAsync(&v, scratch, 8, hipMemcpyDeviceToHost, st));
+    RM_HIP(hipStreamSynchronize(st));
+    return v;
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    if (ncclAllGather(send, recv, bytes, ncclUint8, nc, st) != ncclSuccess) throw std::runtime_error("ncclAllGather failed");
+  }
+};
+
+// ... and over an injected host transport (staged through host memory)
+struct HostTileComm final : TileComm {
+  rm_comm* c;
+  explicit HostTileComm(rm_comm* cc) : c(cc) { rank = cc->rank; nranks = cc->nranks; }
+  uint64_t max_u64(uint64_t v, hipStream_t) override {
+    const std::vector<uint8_t> all = host_gather(c, &v, 8);
+    uint64_t m = 0;
+    for (int r = 0; r < nranks; ++r) { uint64_t x; std::memcpy(&x, all.data() + 8 * (size_t)r, 8); m = std::max(m, x); }
+    return m;
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
+    std::vector<uint8_t> mine(bytes);
+    RM_HIP(hipMemcpyAsync(mine.data(), send, bytes, hipMemcpyDeviceToHost, st));
+    RM_HIP(hipStreamSynchronize(st));
+    const std::vector<uint8_t> all = host_gather(c, mine.data(), bytes);
+    RM_HIP(hipMemcpyAsync(recv, all.data(), all.size(), hipMemcpyHostToDevice, st));
+    RM_HIP(hipStreamSynchronize(st));
+  }
+};
+}  // namespace
 
 extern "C" {
 
@@ -949,9 +1016,13 @@ int rm_runner_tiles(rm_runner* r, const rm_tile_params* p, rm_comm* comm, char**
     std::string mode = p->mode ? p->mode : "auto";
     for (char& ch : mode) ch = (char)std::toupper((unsigned char)ch);   // mode.upper() (:194)
     tp.mode = mode;
-    TileComm tc;
-    if (comm) { tc.nccl = comm->comm; tc.rank = comm->rank; tc.nranks = comm->nranks; }
-    const std::string out = r->m->tiles(tp, comm ? &tc : nullptr);
+    std::unique_ptr<TileComm> tc;
+    if (comm) {
+      if (comm->device < 0) throw std::runtime_error("the communicator has no GPU");
+      if (comm->host_fn) tc = std::make_unique<HostTileComm>(comm);
+      else tc = std::make_unique<RcclTileComm>(comm);
+    }
+    const std::string out = r->m->tiles(tp, tc.get());
     char* b = (char*)std::malloc(out.size() + 1);
     if (!b) throw std::bad_alloc();
     std::memcpy(b, out.data(), out.size());
@@ -997,9 +1068,32 @@ rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device) {
   return out;
 }
 
+rm_comm* rm_comm_init_host(int nranks, int rank, rm_host_allgather_fn fn, void* ctx, int device) {
+  rm_comm* out = nullptr;
+  guarded([&] {
+    if (!fn) throw std::runtime_error("host all-gather function is NULL");
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw std::runtime_error("bad rank / nranks");
+    auto c = std::make_unique<rm_comm>();
+    c->device = device;
+    c->rank = rank;
+    c->nranks = nranks;
+    c->host_fn = fn;
+    c->host_ctx = ctx;
+    if (device >= 0) {
+      RM_HIP(hipSetDevice(device));
+      RM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      RM_HIP(hipMalloc(&c->scratch, 8));
+    }
+    out = c.release();
+  });
+  return out;
+}
+
+int rm_tile_file_owner(uint64_t bucket, uint32_t tile, int nranks) { return tile_file_owner(bucket, tile, nranks); }
+
 void rm_comm_destroy(rm_comm* c) {
   if (!c) return;
-  (void)hipSetDevice(c->device);
+  if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->scratch) (void)hipFree(c->scratch);
@@ -1009,6 +1103,20 @@ void rm_comm_destroy(rm_comm* c) {
 int rm_comm_allreduce(rm_comm* c, void* buf, size_t count, int dtype, int op) {
   return guarded([&] {
     if (!c) throw std::runtime_error("comm is NULL");
+    if (dtype < 0 || dtype > 2 || op < 0 || op > 1) throw std::runtime_error("bad dtype / op");
+    if (c->host_fn) {
+      if (c->device < 0) throw std::runtime_error("the communicator has no GPU");
+      const size_t es = dtype == 0 ? 4 : 8, bytes = es * count;
+      std::vector<uint8_t> mine(bytes);
+      RM_HIP(hipSetDevice(c->device));
+      RM_HIP(hipMemcpy(mine.data(), buf, bytes, hipMemcpyDeviceToHost));
+      const std::vector<uint8_t> all = host_gather(c, mine.data(), bytes);
+      if (dtype == 0) reduce_ranks((uint32_t*)mine.data(), all.data(), count, c->nranks, op);
+      else if (dtype == 1) reduce_ranks((uint64_t*)mine.data(), all.data(), count, c->nranks, op);
+      else reduce_ranks((double*)mine.data(), all.data(), count, c->nranks, op);
+      RM_HIP(hipMemcpy(buf, mine.data(), bytes, hipMemcpyHostToDevice));
+      return;
+    }
     const ncclDataType_t dt = dtype == 0 ? ncclUint32 : (dtype == 1 ? ncclUint64 : ncclFloat64);
     const ncclRedOp_t ro = op == 0 ? ncclSum : ncclMax;
     RM_HIP(hipSetDevice(c->device));
@@ -1020,6 +1128,11 @@ int rm_comm_allreduce(rm_comm* c, void* buf, size_t count, int dtype, int op) {
 int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op) {
   return guarded([&] {
     if (!c) throw std::runtime_error("comm is NULL");
+    if (c->host_fn) {
+      const std::vector<uint8_t> all = host_gather(c, value, 8);
+      reduce_ranks(value, all.data(), 1, c->nranks, op);
+      return;
+    }
     RM_HIP(hipSetDevice(c->device));
     RM_HIP(hipMemcpyAsync(c->scratch, value, 8, hipMemcpyHostToDevice, c->stream));
     nccl_check(ncclAllReduce(c->scratch, c->scratch, 1, ncclFloat64, op == 0 ? ncclSum : ncclMax, c->comm, c->stream),
@@ -1032,7 +1145,7 @@ int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op) {
 int rm_comm_barrier(rm_comm* c) {
   double one = 1.0;
   const int rc = rm_comm_allreduce_host_f64(c, &one, 0);
-  if (rc == 0) {
+  if (rc == 0 && c->device >= 0) {
     return guarded([&] { RM_HIP(hipDeviceSynchronize()); });
   }
   return rc;

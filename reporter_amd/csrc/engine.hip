@@ -1053,70 +1053,6 @@ __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1,
 #ifndef RM_BALL_WPE
 #define RM_BALL_WPE 4
 #endif
-// The items of a block are consecutive, so their routes form ONE contiguous range of
-// b.route: results are staged in LDS at their final offsets and the block writes the range
-// with coalesced stores (a lane-per-item store loop would touch ~10 lines per instruction).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball(DevGraph g, DevBatch b, uint32_t n_items) {
-  const uint32_t tb = xcd_block(blockIdx.x, gridDim.x) * blockDim.x;
-  const uint32_t t = tb + threadIdx.x;
-  const uint32_t tl = min(n_items, tb + blockDim.x) - 1u;   // last item of this block
-  __shared__ uint32_t s_out[256 * kMaxCand];
-  __shared__ uint32_t s_lo, s_hi;
-  const bool live = t <= tl;
-  uint32_t p = 0, i = 0, KB = 0, base = 0;
-  uint4 pi = make_uint4(0u, 0u, 0u, 0u);
-  if (live) {
-    p = b.src_item[t];
-    pi = b.pair_info[p];
-    i = t - b.src_off[p];
-    base = b.trans_off[p];
-    KB = (pi.z >> 8) & 0xffu;
-  }
-  const uint32_t ob = base + i * KB;
-  if (t == tb) s_lo = ob;
-  if (t == tl) s_hi = ob + KB;
-  __syncthreads();
-  if (live) {
-    uint32_t* res = s_out + (ob - s_lo);
-    const uint32_t bound = pi.x, tmax = pi.y;
-    const int mode = (int)(pi.z >> 16);
-    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
-    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
-    unsigned long long rk1, rk0;
-    exit_keys(a0, bound, rk1, rk0);
-    const uint4* ent = g.ball_ent[mode];
-    // a mode without tables has radius 0 (and no header array): every bound > 0 hands over
-    const bool fits = bound <= g.ball_radius[mode] && ((g.ball_mask >> mode) & 1u);
-    const uint2 h1 = fits && rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
-    const uint2 h0 = fits && rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
-    if (!fits || h1.y == 0u || h0.y == 0u) {   // search tiers take it (they run later)
-      for (uint32_t j = 0; j < KB; ++j) res[j] = kRouteInvalid;
-      b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
-    } else {
-      const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
-      const uint64_t brow = p * kMaxCand * 2;
-      for (uint32_t j = 0; j < KB; ++j) {
-        const uint4 t0 = b.cand_desc[brow + 2 * j], t1 = b.cand_desc[brow + 2 * j + 1];
-        const bool any = t0.w != 0u;   // some direction of the target road is usable
-        // first probes of the target road in both exits' tables, then their chains
-        const uint4 e1 = ball_first(ent, h1, t0.x, u1 && any);
-        const uint4 e0 = ball_first(ent, h0, t0.x, u0 && any);
-        const uint4 r1 = ball_resolve(ent, h1, t0.x, e1);
-        const uint4 r0 = ball_resolve(ent, h0, t0.x, e0);
-        const unsigned long long lab0 = ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
-        const unsigned long long lab1 = ball_label(rk1, row_key1(r1), rk0, row_key1(r0));
-        const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, nullptr);
-        uint32_t rt = kRouteInvalid;
-        if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) rt = key_dist(key);
-        res[j] = rt;
-      }
-    }
-  }
-  __syncthreads();
-  const uint32_t lo = s_lo, n = s_hi - s_lo;
-  for (uint32_t q = threadIdx.x; q < n; q += blockDim.x) b.route[lo + q] = s_out[q];
-}
-
 // K2 ball tier, block-expanded (round 3).  A block takes 256 consecutive (pair, source) items,
 // whose routes form one contiguous range of b.route.  Phase 1, one lane per item: the pair's
 // constants, the source's exit keys and both exits' table headers go to LDS, and the item's
@@ -1414,7 +1350,7 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
   return true;
 }
 
-// labels from the route balls of the two exits (see k_routes_ball)
+// labels from the route balls of the two exits (see k_routes_ball2)
 struct BallPathLabels {
   const uint4* ent;
   uint2 h1, h0;
@@ -2294,7 +2230,7 @@ __global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const u
 // report() of one trace over its segments: reports written to out, stats returned
 __device__ __forceinline__ ReportStats report_trace(const SegmentRec* segs, uint32_t n, bool has_pts, double end_time,
                                                    double threshold, uint32_t rmask, uint32_t tmask, ReportRec* out,
-                                                   uint32_t* hist) {
+                                                   uint32_t* hist, unsigned long long* dur) {
   ReportStats st;
   st.successful_count = st.unreported_count = 0;
   st.successful_length_m = st.unreported_length_m = -1;
@@ -2326,10 +2262,14 @@ __device__ __forceinline__ ReportStats report_trace(const SegmentRec* segs, uint
             out[nrep++] = r;
             st.successful_count++;
             st.successful_length_m = p_len;
-            if (hist && r.t0 > 0 && r.t1 > 0 && dt > 0.5 && r.length > 0 && r.queue_length >= 0 && p_dense != kNone) {
+            if ((hist || dur) && r.t0 > 0 && r.t1 > 0 && dt > 0.5 && r.length > 0 && r.queue_length >= 0 &&
+                p_dense != kNone) {
               int bin = (int)(((double)r.length / dt) * 3.6 / 10.0);
               bin = bin > kHistBins - 1 ? kHistBins - 1 : (bin < 0 ? 0 : bin);
-              atomicAdd(&hist[(uint64_t)p_dense * kHistBins + (uint32_t)bin], 1u);
+              if (hist) atomicAdd(&hist[(uint64_t)p_dense * kHistBins + (uint32_t)bin], 1u);
+              // the tile row's duration column, int(round(t1 - t0)) (py/simple_reporter.py:179;
+              // Python 2 round() is half away from zero, as round()), summed per segment
+              if (dur) atomicAdd(&dur[p_dense], (unsigned long long)round(dt));
             }
           }
         } else {
@@ -2349,12 +2289,12 @@ __device__ __forceinline__ ReportStats report_trace(const SegmentRec* segs, uint
 }
 
 __global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uint32_t rmask, uint32_t tmask,
-                                               uint32_t* hist) {
+                                               uint32_t* hist, unsigned long long* dur) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= b.T) return;
   const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
   const ReportStats st = report_trace(b.segs + b.seg_base[k], b.seg_cnt[k], npts > 0, npts ? b.time[o + npts - 1] : 0.0,
-                                      threshold, rmask, tmask, b.reps + b.seg_base[k], hist);
+                                      threshold, rmask, tmask, b.reps + b.seg_base[k], hist, dur);
   b.rep_cnt[k] = (uint32_t)st.n_reports;
   b.stats[k] = st;
 }
@@ -2369,7 +2309,7 @@ __global__ void __launch_bounds__(64) k_report_lists(uint32_t T, const uint32_t*
   if (k >= T) return;
   const uint32_t o = seg_off[k];
   stats[k] = report_trace(segs + o, seg_off[k + 1] - o, true, end_time[k], threshold[k], rmask[k], tmask[k], reps + o,
-                          nullptr);
+                          nullptr, nullptr);
 }
 
 // u64 totals of one or two u32 count arrays: the u32 exclusive scans that lay out routes and
@@ -3271,12 +3211,8 @@ void Matcher::run_device(const RunParams& rp) {
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
   if (n_src && balls) {
-    static const int k2v = [] { const char* e = std::getenv("RM_K2"); return e ? std::atoi(e) : 2; }();
-    if (k2v == 2)
-      hipLaunchKernelGGL(k_routes_ball2, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st, g, v,
-                         (uint32_t)n_src);
-    else
-      hipLaunchKernelGGL(k_routes_ball, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src);
+    hipLaunchKernelGGL(k_routes_ball2, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st, g, v,
+                       (uint32_t)n_src);
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)), dim3(256), 0,
                        st, g, v, 0u, 1);
   } else if (n_src) {
@@ -3368,9 +3304,10 @@ void Matcher::run_device(const RunParams& rp) {
   if (rp.do_report) {
     if (rp.hist && rp.zero_hist)
       RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)eng_->n_segments() * kHistBins * sizeof(uint32_t), st));
+    if (rp.dur && rp.zero_hist) RM_HIP(hipMemsetAsync(rp.dur, 0, (size_t)eng_->n_segments() * 8u, st));
     tic(kKReport);
     hipLaunchKernelGGL(k_report, dim3((T + 63) / 64), dim3(64), 0, st, v, rp.threshold_sec, rp.report_mask,
-                       rp.transition_mask, rp.hist);
+                       rp.transition_mask, rp.hist, rp.dur);
     toc(kKReport);
   }
   RM_HIP(hipGetLastError());

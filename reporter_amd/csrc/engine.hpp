@@ -90,7 +90,8 @@ struct RunParams {
   uint32_t transition_mask = 0b0110;
   uint32_t* hist = nullptr;             // device, n_segments * 16 u32 (may be null)
   int do_report = 1;
-  int zero_hist = 0;                    // memset hist on the stream before the epilogue
+  int zero_hist = 0;                    // memset hist (and dur) on the stream before the epilogue
+  unsigned long long* dur = nullptr;    // device, n_segments u64 duration sums in whole seconds (may be null)
 };
 
 // Kernel ids for per-kernel HIP-event timing.
@@ -211,10 +212,14 @@ void report_segments(int device, uint32_t T, const uint32_t* seg_off, const Segm
                      const double* threshold, const uint32_t* rmask, const uint32_t* tmask, uint32_t* rep_off,
                      ReportRec* reps, ReportStats* stats);
 
-// RCCL communicator handed to the tile stage (one process per GPU)
+// The tile stage's collectives (one process per GPU): RCCL over xGMI, or a host transport the
+// caller injects (capi.cpp rm_comm_init_host).  Both are blocking on `st`.
 struct TileComm {
-  void* nccl;          // ncclComm_t
-  int rank, nranks;
+  int rank = 0, nranks = 1;
+  virtual ~TileComm() = default;
+  virtual uint64_t max_u64(uint64_t v, hipStream_t st) = 0;
+  // every rank's `bytes` device bytes at send, in rank order, into recv (nranks * bytes)
+  virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) = 0;
 };
 
 class Matcher {

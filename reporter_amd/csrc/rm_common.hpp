@@ -216,6 +216,15 @@ RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) {
   return ((((v >> kBallGroupLog) * 2654435761u) >> (32u + kBallGroupLog - bits)) << kBallGroupLog) |
          (v & ((1u << kBallGroupLog) - 1u));
 }
+// Rank that writes a time-tile file (bucket, level | tile index << 3) in the multi-rank batch
+// reporter: the rows of every rank are all-gathered and each file is culled and written by one
+// rank (Fibonacci hash of the file key), so the privacy count sees every vehicle.  Shared by the
+// device filter (stages.hip k_tile_own) and the host export rm_tile_file_owner.
+RM_HD int tile_file_owner(uint64_t bucket, uint32_t tile, int nranks) {
+  const unsigned long long h = (((unsigned long long)bucket << 25) | tile) * 0x9e3779b97f4a7c15ull;
+  return (int)((h >> 33) % (unsigned long long)(nranks > 0 ? nranks : 1));
+}
+
 #endif
 
 // A node's table starts at row 2 * hdr.x of its mode's entry array (hdr = {first row / 2,

@@ -13,7 +13,6 @@
 // reference's stable Python sorts do.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -181,13 +180,12 @@ __device__ __forceinline__ unsigned long long file_key(const TileRow& t) {
   return ((unsigned long long)t.bucket << 25) | t.tile;
 }
 
-// RCCL: keep the gathered rows this rank owns (files hashed over ranks)
+// keep the gathered rows this rank owns (files hashed over ranks, rm_common.hpp tile_file_owner)
 __global__ void k_tile_own(uint64_t n, const TileRow* rows, int rank, int nranks, uint32_t* flag) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const TileRow& t = rows[k];
-  unsigned long long h = file_key(t) * 0x9e3779b97f4a7c15ull;
-  flag[k] = (t.pad[0] == 1u && (int)((h >> 33) % (unsigned long long)nranks) == rank) ? 1u : 0u;
+  flag[k] = (t.pad[0] == 1u && tile_file_owner(t.bucket, t.tile, nranks) == rank) ? 1u : 0u;
 }
 
 __global__ void k_tile_compact(uint64_t n, const TileRow* src, const uint32_t* flag, const uint32_t* ofs, TileRow* dst) {
@@ -476,22 +474,12 @@ std::string Matcher::tiles(const TileParams& tp, TileComm* comm) {
   // ---- RCCL: all-gather every rank's rows, keep the files this rank owns (a one-rank
   // communicator runs the same collectives, so the path is exercised on a single GPU)
   if (comm) {
-    ncclComm_t nc = (ncclComm_t)comm->nccl;
-    double* scratch = nullptr;
-    RM_HIP(hipMalloc(&scratch, 8));
-    double rmax = (double)R;
-    RM_HIP(hipMemcpyAsync(scratch, &rmax, 8, hipMemcpyHostToDevice, st));
-    if (ncclAllReduce(scratch, scratch, 1, ncclFloat64, ncclMax, nc, st) != ncclSuccess) throw std::runtime_error("ncclAllReduce failed");
-    RM_HIP(hipMemcpyAsync(&rmax, scratch, 8, hipMemcpyDeviceToHost, st));
-    RM_HIP(hipStreamSynchronize(st));
-    RM_HIP(hipFree(scratch));
-    const uint64_t Rm = (uint64_t)rmax;
+    const uint64_t Rm = comm->max_u64(R, st);
     const uint64_t all = Rm * (uint64_t)comm->nranks;
     ensure_rows(std::max<uint64_t>(all, 1), T);
     if (all) {
       if (Rm > R) RM_HIP(hipMemsetAsync(s.rows + R, 0, (Rm - R) * sizeof(TileRow), st));   // padding rows: pad[0] = 0
-      if (ncclAllGather(s.rows, s.rows2, Rm * sizeof(TileRow), ncclUint8, nc, st) != ncclSuccess)
-        throw std::runtime_error("ncclAllGather failed");
+      comm->allgather(s.rows, s.rows2, Rm * sizeof(TileRow), st);
       hipLaunchKernelGGL(k_tile_own, dim3(grid(all)), dim3(256), 0, st, all, s.rows2, comm->rank, comm->nranks, s.rflag);
       size_t tmp = s.tmp_bytes;
       RM_HIP(hipcub::DeviceScan::ExclusiveSum(s.tmp, tmp, s.rflag, s.ridx, (int)all, st));

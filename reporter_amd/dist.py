@@ -8,7 +8,10 @@ repartition of ``"id next_id"`` reports (BatchingProcessor.java:126) into
 time-tile histograms.  Here: traces shard by uuid across ranks with no
 data-path collective; the per-OSMLR-segment speed histogram is combined with
 one RCCL all-reduce over xGMI (``Comm``), bound natively in
-libreporter_match.so (no PyTorch in the process).
+libreporter_match.so (no PyTorch in the process).  The same collectives can run
+over a host transport the caller injects (``Comm(..., allgather=fn)``,
+rm_comm_init_host): a multi-rank job that already has one (e.g. gloo), several
+ranks sharing one GPU, or a CPU-only test of the exchange logic.
 """
 import ctypes as C
 import hashlib
@@ -73,40 +76,77 @@ def _stdout_to_stderr(fn):
         os.close(saved)
 
 
-class Comm:
-    """RCCL communicator for one rank (one process per GPU, single node)."""
+def rendezvous_path(rdzv_dir=None, token=None):
+    """Node-local file through which rank 0 hands its RCCL unique id to the other ranks."""
+    rdzv_dir = rdzv_dir or os.environ.get("RM_RDZV_DIR", "/tmp")
+    token = token or "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+    return os.path.join(rdzv_dir, "rm_rdzv_%s.id" % token)
 
-    def __init__(self, rank, world_size, device, rdzv_dir=None, token=None, timeout_s=300.0):
+
+def rendezvous(rank, path, make_id, size=128, timeout_s=300.0):
+    """Rank 0 writes make_id() (`size` bytes) atomically to `path`; every other rank polls
+    until the complete id is there.  Returns the id on every rank."""
+    if rank == 0:
+        data = bytes(make_id())
+        if len(data) != size:
+            raise ValueError("rendezvous id must be %d bytes" % size)
+        tmp = "%s.%d.tmp" % (path, os.getpid())
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, path)
+        return data
+    t0 = time.time()
+    while True:
+        try:
+            with open(path, "rb") as f:
+                data = f.read()
+            if len(data) == size:
+                return data
+        except FileNotFoundError:
+            pass
+        if time.time() - t0 > timeout_s:
+            raise TimeoutError("rank %d: no rendezvous id at %s" % (rank, path))
+        time.sleep(0.05)
+
+
+HOST_ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
+class Comm:
+    """Communicator for one rank (one process per GPU, single node): RCCL over xGMI, or, with
+    `allgather`, a host transport — a callable taking this rank's bytes and returning every
+    rank's bytes in rank order (rm_comm_init_host).  device -1 (host transport only): host
+    values and barriers without a GPU."""
+
+    def __init__(self, rank, world_size, device, rdzv_dir=None, token=None, timeout_s=300.0, allgather=None):
         self.rank, self.world_size, self.device = rank, world_size, device
         L = _lib.lib()
-        rdzv_dir = rdzv_dir or os.environ.get("RM_RDZV_DIR", "/tmp")
-        token = token or "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
-        path = os.path.join(rdzv_dir, "rm_rdzv_%s.id" % token)
-        uid = (C.c_uint8 * 128)()
-        if rank == 0:
-            _lib.check(L.rm_comm_unique_id(uid))
-            tmp = path + ".tmp"
-            with open(tmp, "wb") as f:
-                f.write(bytes(uid))
-            os.replace(tmp, path)
-        else:
-            t0 = time.time()
-            while True:
+        self._path = None
+        if allgather is not None:
+            def gather(_ctx, send, nbytes, recv):
                 try:
-                    with open(path, "rb") as f:
-                        data = f.read()
-                    if len(data) == 128:
-                        break
-                except FileNotFoundError:
-                    pass
-                if time.time() - t0 > timeout_s:
-                    raise TimeoutError("rank %d: no RCCL id at %s" % (rank, path))
-                time.sleep(0.05)
-            C.memmove(uid, data, 128)
-        self._h = _stdout_to_stderr(lambda: L.rm_comm_init(world_size, rank, uid, device))
+                    parts = allgather(C.string_at(send, nbytes) if nbytes else b"")
+                    if len(parts) != world_size or any(len(p) != nbytes for p in parts):
+                        return 1
+                    if nbytes:
+                        C.memmove(recv, b"".join(parts), nbytes * world_size)
+                    return 0
+                except Exception:  # noqa: BLE001 -- reported to the library as a failed collective
+                    return 1
+            self._cb = HOST_ALLGATHER(gather)   # kept alive as long as the communicator
+            self._h = L.rm_comm_init_host(world_size, rank, self._cb, None, device)
+        else:
+            path = rendezvous_path(rdzv_dir, token)
+
+            def make_id():
+                uid = (C.c_uint8 * 128)()
+                _lib.check(L.rm_comm_unique_id(uid))
+                return bytes(uid)
+            uid = (C.c_uint8 * 128).from_buffer_copy(rendezvous(rank, path, make_id, 128, timeout_s))
+            self._h = _stdout_to_stderr(lambda: L.rm_comm_init(world_size, rank, uid, device))
+            self._path = path
         if not self._h:
             raise _lib.RmError(_lib.last_error())
-        self._path = path
 
     def allreduce(self, dev_ptr, count, dtype=U32, op=SUM):
         _lib.check(_lib.lib().rm_comm_allreduce(self._h, dev_ptr, count, dtype, op))
@@ -124,7 +164,7 @@ class Comm:
             self.barrier()
             _lib.lib().rm_comm_destroy(self._h)
             self._h = None
-            if self.rank == 0:
+            if self.rank == 0 and self._path:
                 try:
                     os.remove(self._path)
                 except OSError:

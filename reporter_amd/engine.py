@@ -137,7 +137,7 @@ class BatchMatcher:
 
     @staticmethod
     def run_params(threshold_sec=15.0, report_levels=(0, 1), transition_levels=(0, 1), hist_dev=None,
-                   do_report=True, zero_hist=False):
+                   do_report=True, zero_hist=False, dur_dev=None):
         rp = _lib.RmRunParams()
         rp.threshold_sec = threshold_sec
         rp.report_mask = levels_mask(report_levels)
@@ -145,6 +145,7 @@ class BatchMatcher:
         rp.hist_dev = hist_dev or None
         rp.do_report = 1 if do_report else 0
         rp.zero_hist = 1 if zero_hist else 0
+        rp.dur_dev = dur_dev or None
         return rp
 
     def run(self, trace_off, lon, lat, time, accuracy=None, opts=None, trace_opt=None, **rp_kw):
@@ -376,6 +377,8 @@ class MultiMatcher:
         zero = rp_kw.pop("zero_hist", False)
         if zero and rp_kw.get("hist_dev"):
             _lib.check(_lib.lib().rm_device_memset(rp_kw["hist_dev"], 0, self.engine.n_segments * 16 * 4))
+        if zero and rp_kw.get("dur_dev"):
+            _lib.check(_lib.lib().rm_device_memset(rp_kw["dur_dev"], 0, self.engine.n_segments * 8))
         for t0, t1 in zip(cuts[:-1], cuts[1:]):
             if t1 <= t0:
                 continue

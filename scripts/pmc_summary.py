@@ -71,22 +71,31 @@ def main():
         summary[k] = e
     with open(os.path.join(a.out, "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
-    # the K2 stage = every kernel bench.py times as "routes" (each runs once per step)
-    stage = [k for k in summary if k in ("k_src_items", "k_routes_ball", "k_routes_lane", "k_routes_reg2",
-                                         "k_routes_wave", "k_routes_global")]
-    tot = lambda key: sum(summary[k].get(key, 0) for k in stage)
-    hits, miss = tot("TCC_HIT_sum"), tot("TCC_MISS_sum")
+    # bench.py's stages (the kernels each stage's HIP-event pair brackets; each runs once per step)
+    stage_of = {"candidates": lambda k: k.startswith("k_candidates_"),
+                "routes": lambda k: k == "k_src_items" or k.startswith("k_routes_"),
+                "viterbi": lambda k: k.startswith("k_viterbi"),
+                "paths": lambda k: k.startswith("k_paths_"),
+                "segments": lambda k: k in ("k_rec_slot", "k_seg_wave")}
+
+    def stage_entry(kernels):
+        tot = lambda key: sum(summary[k].get(key, 0) for k in kernels)
+        hits, miss = tot("TCC_HIT_sum"), tot("TCC_MISS_sum")
+        return {"kernels": sorted(kernels),
+                "hbm_bytes_per_launch": (tot("hbm_read_bytes_corrected") + tot("hbm_write_bytes")) or None,
+                "hbm_read_bytes_raw": tot("hbm_read_bytes_raw"), "hbm_write_bytes": tot("hbm_write_bytes"),
+                "l2_hit_rate": hits / (hits + miss) if hits + miss else None}
+
+    stages = {n: stage_entry([k for k in summary if f(k)]) for n, f in stage_of.items()}
     import hashlib
     src = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "reporter_amd", "csrc", "engine.hip")
     sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
-    rt = {"config": a.config, "traces": a.traces, "streams": a.streams, "kernels": sorted(stage), "engine_sha": sha,
-          "read_factor": 2,
-          "hbm_bytes_per_launch": (tot("hbm_read_bytes_corrected") + tot("hbm_write_bytes")) or None,
-          "hbm_read_bytes_raw": tot("hbm_read_bytes_raw"), "hbm_write_bytes": tot("hbm_write_bytes"),
-          "l2_hit_rate": hits / (hits + miss) if hits + miss else None,
-          "note": "per-step sums of per-dispatch averages from separate --pmc passes; read side doubled per "
-                  "MI355X_MICROARCH.md HBM, which profiles/r02/calib confirms for 16-B random gathers "
-                  "(one 128-B line request per miss)"}
+    rt = dict(stages["routes"])
+    rt.update({"config": a.config, "traces": a.traces, "streams": a.streams, "engine_sha": sha, "read_factor": 2,
+               "stages": stages,
+               "note": "per-step sums of per-dispatch averages from separate --pmc passes; read side doubled per "
+                       "MI355X_MICROARCH.md HBM, which profiles/r02/calib confirms for 16-B random gathers "
+                       "(one 128-B line request per miss); top-level fields = the routes (K2) stage"})
     with open(os.path.join(a.out, "pmc_routes_%s.json" % a.config.lower()), "w") as f:
         json.dump(rt, f, indent=1)
     for k in sorted(summary, key=lambda x: -summary[x].get("FETCH_SIZE", 0))[:12]:

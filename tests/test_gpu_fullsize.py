@@ -6,7 +6,8 @@ cheap; here the graphs are the configs' own (C2/C5: 200x200 @100 m, C3:
 the full one takes a minute to generate on the host), and the C2 batch is the
 bench's exact rank-0 workload (10,000 traces x 600 points, seed 1000): every
 stage of every trajectory must equal the oracle bit for bit, and the speed
-histogram must equal the CPU pipeline's.  C3/C4/C5 check bounded trace
+histogram and the per-segment duration sums must equal the
+CPU pipeline's.  C3/C4/C5 check bounded trace
 samples (the oracle's long 30 s searches run ~8k points/s on one core).
 """
 import ctypes
@@ -37,29 +38,35 @@ def _match_and_compare(path, tr, opts, trace_opt, rl=(0, 1), tl=(0, 1), hist=Fal
     if trace_opt is None:
         trace_opt = np.zeros(T, np.uint32)
     nseg = eng.n_segments
-    dptr = ctypes.c_void_p()
+    dptr, uptr = ctypes.c_void_p(), ctypes.c_void_p()
     rp = dict(report_levels=rl, transition_levels=tl)
     if hist:
         _lib.check(_lib.lib().rm_device_alloc(nseg * 16 * 4, ctypes.byref(dptr)))
-        _lib.check(_lib.lib().rm_device_memset(dptr, 0, nseg * 16 * 4))
-        rp["hist_dev"] = dptr.value
+        _lib.check(_lib.lib().rm_device_alloc(nseg * 8, ctypes.byref(uptr)))
+        rp.update(hist_dev=dptr.value, dur_dev=uptr.value, zero_hist=True)
     try:
         bm = engine.BatchMatcher(eng)
         bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt, **rp)
         if hist:
             got_hist = np.empty(nseg * 16, np.uint32)
             _lib.check(_lib.lib().rm_device_download(got_hist.ctypes.data, dptr, got_hist.nbytes))
+            got_dur = np.empty(nseg, np.uint64)
+            _lib.check(_lib.lib().rm_device_download(got_dur.ctypes.data, uptr, got_dur.nbytes))
     finally:
         if hist:
             _lib.lib().rm_device_free(dptr)
+            _lib.lib().rm_device_free(uptr)
     batch = mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt)
     ref = mo.match(g, batch)
     c = compare_all(bm, ref, tr["trace_off"])
     c["reports"] = check_reports(bm, ref, tr, rl=rl, tl=tl)
     if hist:
         want = np.zeros(nseg * 16, np.uint32)
-        nvalid = mo.pipeline(g, batch, 15.0, engine.levels_mask(rl), engine.levels_mask(tl), want)
+        want_dur = np.zeros(nseg, np.uint64)
+        nvalid = mo.pipeline(g, batch, 15.0, engine.levels_mask(rl), engine.levels_mask(tl), want, want_dur)
         np.testing.assert_array_equal(got_hist, want, "speed histogram")
+        np.testing.assert_array_equal(got_dur, want_dur, "per-segment duration sums")
+        assert int(got_dur.sum()) > 0
         assert int(got_hist.sum()) == nvalid
         c["valid_reports"] = nvalid
     c["traces"] = T

@@ -104,3 +104,62 @@ def test_oracle_on_the_readme_manila_trace(tmp_path, built_lib):
     segs = oracle_segments(path, req)
     assert len(segs) >= 3 and any("segment_id" in s for s in segs)
     check_schema(segs, len(req["trace"]))
+
+
+def test_pipeline_duration_sums_and_histogram(small_world):
+    """og_pipeline2's per-segment duration sums (reduced with the histogram)
+    equal sum(int(round(t1 - t0))) of the reports the histogram counts, recomputed here from
+    the oracle's segments through report() and the batch filter of py/simple_reporter.py:177-179
+    (Python round() of a positive float > 0.5 = floor(x + 0.5) up to the exact-half ties, which
+    Python 2 rounds away from zero: np.floor(x + 0.5) matches both)."""
+    tr = world.generate_traces(small_world, 24, 300, rate_s=1.0, noise_m=5.0, seed=17)
+    g, out = _run(small_world, tr)
+    nseg = len(g["seg_id"])
+    T = len(tr["trace_off"]) - 1
+    b = mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], engine.default_options(1),
+                 np.zeros(T, np.uint32))
+    hist = np.zeros(nseg * 16, np.uint32)
+    dur = np.zeros(nseg, np.uint64)
+    nvalid = mo.pipeline(g, b, 15.0, 0x6, 0x6, hist, dur)
+    want_h = np.zeros(nseg * 16, np.uint64)
+    want_d = np.zeros(nseg, np.uint64)
+    n = 0
+    for k in range(T):
+        segs = out["segs"][out["seg_off"][k]:out["seg_off"][k + 1]]
+        end = tr["time"][tr["trace_off"][k + 1] - 1]
+        reps, _ = mo.report_trace(segs, end, 15.0, 0x6, 0x6)
+        for r in reps:
+            dt = r["t1"] - r["t0"]
+            if not (r["t0"] > 0 and r["t1"] > 0 and dt > 0.5 and r["length"] > 0 and r["queue_length"] >= 0):
+                continue
+            n += 1
+            if r["seg_dense"] == 0xFFFFFFFF:
+                continue
+            want_h[r["seg_dense"] * 16 + min(15, max(0, int(r["length"] / dt * 3.6 / 10.0)))] += 1
+            want_d[r["seg_dense"]] += int(np.floor(dt + 0.5))
+    assert nvalid == n and n > 50
+    np.testing.assert_array_equal(hist, want_h.astype(np.uint32))
+    np.testing.assert_array_equal(dur, want_d)
+
+
+def test_path_walk_counters(small_world):
+    """Counters behind bench.py's paths roofline: after prepare_path_counters, every walked
+    node visits at least its canonical in-edge, and each visited usable in-edge reads at most
+    two route-ball rows."""
+    tr = world.generate_traces(small_world, 16, 300, rate_s=1.0, noise_m=5.0, seed=18)
+    g = graphfile.load(small_world)
+    T = len(tr["trace_off"]) - 1
+    b = mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], engine.default_options(1),
+                 np.zeros(T, np.uint32))
+    mo.reset_counters()
+    mo.match(g, b)
+    assert mo.counters()["path_in_edges"] == 0          # not prepared: not counted
+    mo.prepare_path_counters(g)
+    mo.reset_counters()
+    out = mo.match(g, b)
+    c = mo.counters()
+    walked = int(np.maximum(out["path_cnt"][out["path_cnt"] > 2].astype(np.int64) - 2, 0).sum())
+    assert c["chained"] > 1000 and walked > 0
+    assert c["path_in_edges"] >= walked
+    assert c["path_rows"] <= 2 * c["path_in_edges"] + 4 * c["chained"]
+    assert mo.paths_algorithmic_bytes(c) > 116 * c["chained"]
