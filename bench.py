@@ -35,6 +35,9 @@ sys.path.insert(0, ROOT)
 METRIC = "GPS points map-matched/sec (node) at 1/2/4/8 MI355X; % of HBM peak"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0      # float4 copy ceiling from the same guide
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 4 cycles
+# (16 lanes per cycle for 32-bit and fp64 ops alike on CDNA4) at 2.4 GHz
+VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 4
 ENGINE_SRC = os.path.join(ROOT, "reporter_amd", "csrc", "engine.hip")
 
 
@@ -147,7 +150,7 @@ def shard_ids(config, n_per_rank, n_points, world, rank):
 LAUNCHES = 1   # launches of each stage per step (one per concurrent part of the batch)
 
 
-def roofline(name, kernels, abytes, ms, formulation, traffic=None):
+def roofline(name, kernels, abytes, ms, formulation, traffic=None, valu=None):
     """abytes / ms: the step's algorithmic bytes and summed launch time of the stage; reported
     per launch (each part's launch does its share of the bytes, timed on its own stream).
     traffic: HBM bytes per launch from the PMC passes of this build (or None); dram_frac is what
@@ -160,11 +163,17 @@ def roofline(name, kernels, abytes, ms, formulation, traffic=None):
                 "algorithmic_bytes_per_launch": abytes, "avg_launch_ms": ms, "launches_per_step": LAUNCHES}
     achieved = abytes / (ms * 1e-3) / 1e9
     dram = traffic / (ms * 1e-3) / 1e9 if traffic else None
-    return {"kernel": kernels, "formulation": formulation, "bound": "hbm", "achieved": achieved,
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-            "frac_vs_measured_copy": achieved / HBM_MEASURED_GBS, "traffic": traffic,
-            "dram_achieved": dram, "dram_frac": dram / HBM_PEAK_GBS if dram else None,
-            "algorithmic_bytes_per_launch": abytes, "avg_launch_ms": ms, "launches_per_step": LAUNCHES}
+    out = {"kernel": kernels, "formulation": formulation, "bound": "hbm", "achieved": achieved,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+           "frac_vs_measured_copy": achieved / HBM_MEASURED_GBS, "traffic": traffic,
+           "dram_achieved": dram, "dram_frac": dram / HBM_PEAK_GBS if dram else None,
+           "algorithmic_bytes_per_launch": abytes, "avg_launch_ms": ms, "launches_per_step": LAUNCHES}
+    if valu:   # wave64 VALU instructions per launch (PMC SQ_INSTS_VALU of this build)
+        out["valu_instrs"] = valu
+        out["valu_frac"] = valu / (ms * 1e-3) / VALU_PEAK_WAVE_INSTR_S
+        if out["valu_frac"] > out["frac"]:
+            out["bound_note"] = "VALU issue is the nearer ceiling (valu_frac > frac)"
+    return out
 
 
 def load_traffic(path, config, traces, streams):
@@ -428,8 +437,9 @@ def main():
         tpath = a.traffic_json or os.path.join(ROOT, "profiles", "r03", "pmc_routes_%s.json" % a.config.lower())
         traffic, traffic_note = load_traffic(tpath, a.config, n_per, max(1, a.streams))
         tr_of = lambda st: (traffic.get(st) or {}).get("hbm_bytes_per_launch")
+        va_of = lambda st: (traffic.get(st) or {}).get("valu_instrs")
         k2 = roofline("K2", "K2 route stage: k_src_items + k_routes_ball2 + search tiers for hand-overs", abytes,
-                      ms["routes"], formulation, tr_of("routes"))
+                      ms["routes"], formulation, tr_of("routes"), va_of("routes"))
         k2["l2_hit_rate"] = (traffic.get("routes") or {}).get("l2_hit_rate")
         k2["traffic_source"] = traffic_note
         k2.update({"search_equivalent_bytes_per_launch": mo.routes_algorithmic_bytes(counts) if counts else None,
@@ -438,19 +448,19 @@ def main():
             "K1": roofline("K1", "k_candidates_lane + k_candidates_wave", mo.candidates_algorithmic_bytes(counts)
                            if counts else None, ms["candidates"], "cell-major 32 B records on the engine grid (file cells split "
                            "%dx%d; items counted by the oracle on that grid), per-road minima in registers"
-                           % (eng.grid_split(), eng.grid_split()), tr_of("candidates")),
-            "K2": {k: k2[k] for k in ("kernel", "achieved", "frac", "algorithmic_bytes_per_launch", "avg_launch_ms",
-                                      "traffic", "dram_frac")},
+                           % (eng.grid_split(), eng.grid_split()), tr_of("candidates"), va_of("candidates")),
+            "K2": {k: k2.get(k) for k in ("kernel", "achieved", "frac", "algorithmic_bytes_per_launch", "avg_launch_ms",
+                                      "traffic", "dram_frac", "valu_frac")},
             "K3": roofline("K3", "k_viterbi", mo.viterbi_algorithmic_bytes(counts) if counts else None, ms["viterbi"],
-                           "u32 routes + f32 emissions, fp64 costs in registers", tr_of("viterbi")),
+                           "u32 routes + f32 emissions, fp64 costs in registers", tr_of("viterbi"), va_of("viterbi")),
             "paths": roofline("paths", "path stage: k_paths_ball + search tiers for hand-overs",
                               mo.paths_algorithmic_bytes(counts) if counts and "path_rows" in counts else None,
                               ms["paths"], "route-ball labels, walk back by canonical predecessors over "
-                              "self-contained in-edge records", tr_of("paths")),
+                              "self-contained in-edge records", tr_of("paths"), va_of("paths")),
             "K4": roofline("K4", "segments stage: trav_off scan + k_rec_slot + k_seg_wave",
                            mo.segments_algorithmic_bytes(counts) if counts else None, ms["segments"],
                            "wave per trace, 64 traversal records per step in registers, runs by ballot/scan",
-                           tr_of("segments")),
+                           tr_of("segments"), va_of("segments")),
         }
         step_ms = elapsed / steps * 1e3
         build_ms = balls["build_ms"]

@@ -2932,6 +2932,8 @@ Matcher::~Matcher() {
   for (auto& ev : pending_) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
   for (auto& ev : free_ev_) { (void)hipEventDestroy(ev.a); (void)hipEventDestroy(ev.b); }
   ws_.release();
+  if (dl_dev_) (void)hipFree(dl_dev_);
+  if (dl_host_) (void)hipHostFree(dl_host_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (hctl_) (void)hipHostFree(hctl_);
 }
@@ -3450,21 +3452,72 @@ uint64_t Matcher::count_segments() {
   for (uint32_t c : cnt) t += c;
   return t;
 }
+// Compaction for the downloads: trace k's records [base[k], base[k] + cnt[k]) of a per-trace
+// pool (sized by traversal records, mostly empty) to dst[off[k] ..), one wave per trace, u64
+// words.  The boundary then moves only the records (C2: 15 MB of segments, not a 362 MB pool).
+__global__ void __launch_bounds__(64) k_gather_recs(uint32_t T, const uint32_t* base, const uint32_t* cnt,
+                                                    const uint32_t* off, const unsigned long long* src, uint32_t words,
+                                                    unsigned long long* dst) {
+  for (uint32_t k = blockIdx.x; k < T; k += gridDim.x) {
+    const uint64_t n = (uint64_t)cnt[k] * words;
+    const unsigned long long* s = src + (uint64_t)base[k] * words;
+    unsigned long long* d = dst + (uint64_t)off[k] * words;
+    for (uint64_t q = threadIdx.x; q < n; q += 64) d[q] = s[q];
+  }
+}
+
+void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, const void* d_src, uint32_t words,
+                                 uint32_t* off, void* dst) {
+  const uint32_t T = n_traces_;
+  hipStream_t st = stream_;
+  RM_HIP(hipSetDevice(eng_->device()));
+  const size_t offb = ((size_t)T + 1) * 4;
+  // pinned: [0, offb) the counts then offsets, then the compacted records
+  auto grow_host = [&](size_t need) {
+    if (need <= dl_host_bytes_) return;
+    if (dl_host_) RM_HIP(hipHostFree(dl_host_));
+    dl_host_ = nullptr;
+    dl_host_bytes_ = std::max(need, dl_host_bytes_ + dl_host_bytes_ / 2);
+    RM_HIP(hipHostMalloc(&dl_host_, dl_host_bytes_, hipHostMallocDefault));
+  };
+  grow_host(offb);
+  uint32_t* hc = (uint32_t*)dl_host_;
+  RM_HIP(hipMemcpyAsync(hc, d_cnt, T * 4ull, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipStreamSynchronize(st));
+  uint64_t at = 0;
+  for (uint32_t k = 0; k < T; ++k) {
+    off[k] = (uint32_t)at;
+    at += hc[k];
+  }
+  off[T] = (uint32_t)at;
+  if (at == 0) return;
+  const size_t recb = (size_t)at * words * 8;
+  const size_t dev_need = offb + recb + 8;
+  if (dev_need > dl_dev_bytes_) {
+    if (dl_dev_) RM_HIP(hipFree(dl_dev_));
+    dl_dev_ = nullptr;
+    dl_dev_bytes_ = std::max(dev_need, dl_dev_bytes_ + dl_dev_bytes_ / 2);
+    RM_HIP(hipMalloc(&dl_dev_, dl_dev_bytes_));
+  }
+  grow_host(offb + recb + 8);
+  hc = (uint32_t*)dl_host_;
+  std::memcpy(hc, off, offb);
+  uint32_t* d_off = (uint32_t*)dl_dev_;
+  unsigned long long* d_dst = (unsigned long long*)((char*)dl_dev_ + ((offb + 7) & ~(size_t)7));
+  RM_HIP(hipMemcpyAsync(d_off, hc, offb, hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_gather_recs, dim3(std::min<uint32_t>(T, 8192u)), dim3(64), 0, st, T, d_base, d_cnt, d_off,
+                     (const unsigned long long*)d_src, words, d_dst);
+  char* h_dst = (char*)dl_host_ + ((offb + 7) & ~(size_t)7);
+  RM_HIP(hipMemcpyAsync(h_dst, d_dst, recb, hipMemcpyDeviceToHost, st));
+  RM_HIP(hipStreamSynchronize(st));
+  std::memcpy(dst, h_dst, recb);
+}
+
 void Matcher::get_segments(uint32_t* seg_off, SegmentRec* segs) {
   sync();
-  std::vector<uint32_t> base(n_traces_), cnt(n_traces_);
   if (!n_traces_) { seg_off[0] = 0; return; }
-  RM_HIP(hipMemcpy(base.data(), ws_.seg_base, n_traces_ * 4ull, hipMemcpyDeviceToHost));
-  RM_HIP(hipMemcpy(cnt.data(), ws_.seg_cnt, n_traces_ * 4ull, hipMemcpyDeviceToHost));
-  std::vector<SegmentRec> pool(seg_used_);
-  if (seg_used_) RM_HIP(hipMemcpy(pool.data(), ws_.segs, seg_used_ * sizeof(SegmentRec), hipMemcpyDeviceToHost));
-  uint64_t at = 0;
-  for (uint32_t k = 0; k < n_traces_; ++k) {
-    seg_off[k] = (uint32_t)at;
-    if (cnt[k]) std::memcpy(segs + at, pool.data() + base[k], cnt[k] * sizeof(SegmentRec));
-    at += cnt[k];
-  }
-  seg_off[n_traces_] = (uint32_t)at;
+  static_assert(sizeof(SegmentRec) % 8 == 0, "records move as u64 words");
+  download_compacted(ws_.seg_base, ws_.seg_cnt, ws_.segs, sizeof(SegmentRec) / 8, seg_off, segs);
 }
 uint64_t Matcher::count_reports() {
   sync();
@@ -3479,19 +3532,9 @@ void Matcher::get_reports(uint32_t* rep_off, ReportRec* reps, ReportStats* stats
   sync();
   if (!has_report_) throw std::runtime_error("the last run did not compute reports");
   if (!n_traces_) { rep_off[0] = 0; return; }
-  std::vector<uint32_t> base(n_traces_), cnt(n_traces_);
-  RM_HIP(hipMemcpy(base.data(), ws_.seg_base, n_traces_ * 4ull, hipMemcpyDeviceToHost));
-  RM_HIP(hipMemcpy(cnt.data(), ws_.rep_cnt, n_traces_ * 4ull, hipMemcpyDeviceToHost));
   RM_HIP(hipMemcpy(stats, ws_.stats, n_traces_ * sizeof(ReportStats), hipMemcpyDeviceToHost));
-  std::vector<ReportRec> pool(seg_used_);
-  if (seg_used_) RM_HIP(hipMemcpy(pool.data(), ws_.reps, seg_used_ * sizeof(ReportRec), hipMemcpyDeviceToHost));
-  uint64_t at = 0;
-  for (uint32_t k = 0; k < n_traces_; ++k) {
-    rep_off[k] = (uint32_t)at;
-    if (cnt[k]) std::memcpy(reps + at, pool.data() + base[k], cnt[k] * sizeof(ReportRec));
-    at += cnt[k];
-  }
-  rep_off[n_traces_] = (uint32_t)at;
+  static_assert(sizeof(ReportRec) % 8 == 0, "records move as u64 words");
+  download_compacted(ws_.seg_base, ws_.rep_cnt, ws_.reps, sizeof(ReportRec) / 8, rep_off, reps);
 }
 
 }  // namespace rm

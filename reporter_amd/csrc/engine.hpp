@@ -293,8 +293,15 @@ class Matcher {
   void tic(int k);
   void toc(int k);
   void harvest_times();
+  // per-trace record lists (base[k], cnt[k] in units of `words` u64) compacted on the device and
+  // downloaded through pinned memory into dst; off gets the T+1 offsets
+  void download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, const void* d_src, uint32_t words,
+                          uint32_t* off, void* dst);
 
   Engine* eng_;
+  void* dl_dev_ = nullptr;     // grow-only device / pinned host buffers of download_compacted
+  void* dl_host_ = nullptr;
+  size_t dl_dev_bytes_ = 0, dl_host_bytes_ = 0;
   hipStream_t stream_ = nullptr;
   Workspace ws_;
   uint32_t n_traces_ = 0;

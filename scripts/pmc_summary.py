@@ -38,6 +38,9 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--traces", type=int, default=10000)
     ap.add_argument("--streams", type=int, default=2, help="concurrent parts the profiled bench ran (bench --streams)")
+    ap.add_argument("--tag", default=None, help="output pmc_<tag>.json instead of pmc_routes_<config>.json")
+    ap.add_argument("--what", default="python bench.py --steps 10 --warmup 2 --no-cpu-baseline",
+                    help="the profiled command, for the kernel-stats title")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     ks = os.path.join(a.src, "prof_kt", "run_kernel_stats.csv")
@@ -48,8 +51,7 @@ def main():
                                                               float(r["MinNs"]) / 1e3, float(r["MaxNs"]) / 1e3,
                                                               float(r["Percentage"])))
     with open(os.path.join(a.out, "kernel_stats.md"), "w") as f:
-        f.write("rocprofv3 --kernel-trace --stats of `python bench.py --steps 10 --warmup 2 --no-cpu-baseline` "
-                "(%s, %d traces)\n\n" % (a.config, a.traces))
+        f.write("rocprofv3 --kernel-trace --stats of `%s` (%s, %d traces)\n\n" % (a.what, a.config, a.traces))
         f.write("\n".join(lines) + "\n")
     merged = defaultdict(dict)
     for d in sorted(glob.glob(os.path.join(a.src, "pmc_*"))):
@@ -84,7 +86,9 @@ def main():
         return {"kernels": sorted(kernels),
                 "hbm_bytes_per_launch": (tot("hbm_read_bytes_corrected") + tot("hbm_write_bytes")) or None,
                 "hbm_read_bytes_raw": tot("hbm_read_bytes_raw"), "hbm_write_bytes": tot("hbm_write_bytes"),
-                "l2_hit_rate": hits / (hits + miss) if hits + miss else None}
+                "l2_hit_rate": hits / (hits + miss) if hits + miss else None,
+                "valu_instrs": tot("SQ_INSTS_VALU") or None, "salu_instrs": tot("SQ_INSTS_SALU") or None,
+                "waves": tot("SQ_WAVES") or None}
 
     stages = {n: stage_entry([k for k in summary if f(k)]) for n, f in stage_of.items()}
     import hashlib
@@ -96,7 +100,7 @@ def main():
                "note": "per-step sums of per-dispatch averages from separate --pmc passes; read side doubled per "
                        "MI355X_MICROARCH.md HBM, which profiles/r02/calib confirms for 16-B random gathers "
                        "(one 128-B line request per miss); top-level fields = the routes (K2) stage"})
-    with open(os.path.join(a.out, "pmc_routes_%s.json" % a.config.lower()), "w") as f:
+    with open(os.path.join(a.out, "pmc_%s.json" % (a.tag or "routes_" + a.config.lower())), "w") as f:
         json.dump(rt, f, indent=1)
     for k in sorted(summary, key=lambda x: -summary[x].get("FETCH_SIZE", 0))[:12]:
         e = summary[k]
