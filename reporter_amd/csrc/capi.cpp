@@ -343,6 +343,7 @@ struct rm_matcher {
   std::shared_ptr<Config> conf;
   std::unique_ptr<Matcher> m;
   HostStaging stage;
+  std::vector<tj::PointSink> sinks;   // per parse thread, grow-only (no page faults on a warm matcher)
   double ms[6] = {};   // the last rm_match_batch: parse, stage, engine, download, format, total
 };
 
@@ -358,7 +359,8 @@ void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char**
   const auto t0 = clk::now();
   HostPool& pool = HostPool::get();
   const size_t nt = std::max<size_t>(1, std::min<size_t>(pool.size(), (n + 15) / 16));
-  std::vector<tj::PointSink> sink(nt);
+  if (m->sinks.size() < nt) m->sinks.resize(nt);
+  std::vector<tj::PointSink>& sink = m->sinks;
   std::vector<uint32_t> cnt(n), topt(n);
   std::vector<MatchOptions> opts(n);
   const Config& conf = *m->conf;
@@ -367,6 +369,7 @@ void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char**
     size_t bytes = 0;
     for (size_t i = a; i < b; ++i) bytes += std::strlen(traces[i]);
     tj::PointSink& sk = sink[t];
+    sk.clear();
     const size_t guess = bytes / 48 + 16;   // a /report point is ~60-90 bytes of JSON
     sk.lon.reserve(guess); sk.lat.reserve(guess); sk.acc.reserve(guess); sk.time.reserve(guess);
     for (size_t i = a; i < b; ++i) {

@@ -281,11 +281,7 @@ __device__ __forceinline__ void put_cand(const DevGraph& g, const DevBatch& b, u
 
 // Unrolled loops over the per-lane slot arrays stop as soon as no active lane needs the
 // slot (a scalar branch on a ballot) instead of always walking all kMaxCand slots.
-#ifdef RM_K1_NO_UNIFORM
-#define K1_UNIFORM_STOP(c) false
-#else
 #define K1_UNIFORM_STOP(c) (__ballot(c) == 0ull)
-#endif
 
 // K1 lane tier: one lane per state.  Cell items are read as cell-major 32-byte records
 // (both shape vertices + road + access bits), so a test is two dwordx4 loads with no
