@@ -285,9 +285,11 @@ def extras(gpath, tr, json_traces, tmpdir):
                                            "note": "the same call on a fresh matcher: buffers grow once"}}
     sm.close()
     # the service under concurrent load: one SegmentMatcher per client thread (as
-    # reporter_service.py's threaded server), every Match coalesced into shared batches
-    n_cli, n_req = 64, min(len(reqs), 4096)
-    for workers in (1,):
+    # reporter_service.py's threaded server, a thread per request), every Match coalesced into
+    # shared batches; at 64 and 256 requests in flight (a batch takes a few ms whatever its size,
+    # so the throughput follows the number of requests in flight)
+    n_req = min(len(reqs), 4096)
+    for workers, n_cli in ((1, 64), (1, 256)):
         conf = valhalla.write_config(os.path.join(tmpdir, "reporter_bench_svc_%d.json" % os.getpid()), gpath, device=0,
                                      coalesce=True, coalesce_workers=workers)
         valhalla.Configure(conf)
@@ -309,7 +311,8 @@ def extras(gpath, tr, json_traces, tmpdir):
             th.join()
         dt = time.perf_counter() - t
         pts = int(tr["trace_off"][min(n_req, len(tr["trace_off"]) - 1)])
-        out["service_throughput"] = {
+        key = "service_throughput" if n_cli == 64 else "service_throughput_%d_clients" % n_cli
+        out[key] = {
             "what": "%d C2 /report requests (600 points each) from %d client threads through valhalla.SegmentMatcher()"
                     ".Match with request coalescing, %d dispatcher(s)" % (sum(done), n_cli, workers),
             "requests_per_s": sum(done) / dt, "points_per_s": pts / dt, "seconds": dt}

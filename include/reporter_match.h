@@ -157,15 +157,20 @@ int rm_engine_grid_split(const rm_engine* e, uint32_t* f);
 int rm_graph_grid_split(const char* graph_path, uint32_t* f);
 /* The engine's own tables of `mode` (built by a run that used the mode), probed on the device as
  * K2 probes them: keys[2i], keys[2i+1] from node from[i] to road[i]'s node0 / node1, all-ones
- * outside the ball or for a node without a table.  Compare with rm_balls_lookup (host build). */
+ * outside the ball or for a node without a table; preds (may be NULL) gets the rows' canonical
+ * predecessor indices of node0 / node1 (7: none stored).  Compare with rm_balls_lookup. */
 int rm_engine_ball_lookup(rm_engine* e, int mode, uint64_t n, const uint32_t* from, const uint32_t* road,
-                          uint64_t* keys);
+                          uint64_t* keys, uint8_t* preds);
 /* Host-only check of the ball tables (no GPU): builds the balls of `mode` for the graph
  * file and looks up n (from node, road) pairs the way the K2 kernel probes them;
  * keys[2i], keys[2i+1] = dist_cm << 32 | time_ms from `from` to the road's node0 / node1,
- * all-ones for an endpoint outside the ball (or `from` without a table).  Returns 0 / -1. */
+ * all-ones for an endpoint outside the ball (or `from` without a table).  preds (may be NULL):
+ * preds[2i], preds[2i+1] = the index, among the endpoint's in-edges in edge-id order, of its
+ * canonical predecessor in the search from `from` (smallest-id usable in-edge u -> v with
+ * key(from -> u) + key(u -> v) == key(from -> v)); 7 when the endpoint is `from`, outside the
+ * ball, or the index is 7 or more.  Returns 0 / -1. */
 int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t n, const uint32_t* from,
-                    const uint32_t* road, uint64_t* keys);
+                    const uint32_t* road, uint64_t* keys, uint8_t* preds);
 
 rm_runner* rm_runner_create(rm_engine* e);
 void rm_runner_destroy(rm_runner* r);

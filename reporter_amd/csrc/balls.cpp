@@ -68,24 +68,69 @@ struct Scratch {
   }
 };
 
+// in-edges of every node in edge-id order (the engine's in_rec order) and each edge's source
+struct InEdges {
+  std::vector<uint32_t> off, edge, src;
+  explicit InEdges(const Graph& g) {
+    const uint32_t N = g.num_nodes(), E = g.num_edges();
+    off.assign(N + 1, 0);
+    edge.resize(E);
+    src.resize(E);
+    for (uint32_t u = 0; u < N; ++u)
+      for (uint32_t e = g.node_off[u]; e < g.node_off[u + 1]; ++e) src[e] = u;
+    for (uint32_t e = 0; e < E; ++e) off[g.edges[e].target + 1]++;
+    for (uint32_t n = 0; n < N; ++n) off[n + 1] += off[n];
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    for (uint32_t e = 0; e < E; ++e) edge[fill[g.edges[e].target]++] = e;
+  }
+};
+
+// canonical predecessor of settled node v (key kv) in the search from root (rm_common.hpp
+// kBallRoadBits): index among v's in-edges of the first usable tight one, kBallPredNone when
+// v is the root or the index is 7 or more
+uint32_t pred_index(const InEdges& ie, const std::vector<EdgeKey>& ek, const std::vector<uint64_t>& lab,
+                    uint32_t root, uint32_t v, uint64_t kv) {
+  if (v == root) return kBallPredNone;
+  for (uint32_t q = ie.off[v], i = 0; q < ie.off[v + 1] && i < kBallPredNone; ++q, ++i) {
+    const uint32_t e = ie.edge[q];
+    if (ek[e].key == kKeyInf) continue;
+    const uint64_t lu = lab[ie.src[e]];
+    if (lu != kKeyInf && lu + ek[e].key == kv) return i;
+  }
+  return kBallPredNone;
+}
+
 // roads touched by a ball: every road with an endpoint in it, with the keys of both
-// endpoints (kKeyInf for an endpoint outside the ball)
+// endpoints (kKeyInf for an endpoint outside the ball) and their predecessor indices
 struct RoadAcc {
   std::vector<uint32_t> pos;      // road -> index in rows (kNone when untouched)
   std::vector<uint32_t> roads;
   std::vector<uint64_t> k0, k1;
+  std::vector<uint8_t> p0, p1;
   explicit RoadAcc(uint32_t n_roads) : pos(n_roads, kNone) {}
+  // pred(i): predecessor index of settled[i] (only called when `with_pred`)
+  template <class Pred>
   void collect(const Graph& g, const std::vector<uint32_t>& inc_off, const std::vector<uint32_t>& inc,
-               const std::vector<std::pair<uint32_t, uint64_t>>& settled) {
+               const std::vector<std::pair<uint32_t, uint64_t>>& settled, bool with_pred, Pred&& pred) {
     for (uint32_t r : roads) pos[r] = kNone;
-    roads.clear(); k0.clear(); k1.clear();
-    for (const auto& kv : settled)
+    roads.clear(); k0.clear(); k1.clear(); p0.clear(); p1.clear();
+    for (size_t i = 0; i < settled.size(); ++i) {
+      const auto& kv = settled[i];
+      const uint8_t pv = with_pred ? (uint8_t)pred(i) : (uint8_t)kBallPredNone;
       for (uint32_t q = inc_off[kv.first]; q < inc_off[kv.first + 1]; ++q) {
         const uint32_t r = inc[q];
-        if (pos[r] == kNone) { pos[r] = (uint32_t)roads.size(); roads.push_back(r); k0.push_back(kKeyInf); k1.push_back(kKeyInf); }
-        if (g.road_node0[r] == kv.first) k0[pos[r]] = kv.second;
-        if (g.road_node1[r] == kv.first) k1[pos[r]] = kv.second;
+        if (pos[r] == kNone) {
+          pos[r] = (uint32_t)roads.size(); roads.push_back(r); k0.push_back(kKeyInf); k1.push_back(kKeyInf);
+          p0.push_back((uint8_t)kBallPredNone); p1.push_back((uint8_t)kBallPredNone);
+        }
+        if (g.road_node0[r] == kv.first) { k0[pos[r]] = kv.second; p0[pos[r]] = pv; }
+        if (g.road_node1[r] == kv.first) { k1[pos[r]] = kv.second; p1[pos[r]] = pv; }
       }
+    }
+  }
+  void collect(const Graph& g, const std::vector<uint32_t>& inc_off, const std::vector<uint32_t>& inc,
+               const std::vector<std::pair<uint32_t, uint64_t>>& settled) {
+    collect(g, inc_off, inc, settled, false, [](size_t) { return kBallPredNone; });
   }
 };
 
@@ -294,23 +339,30 @@ void build_balls(const Graph& g, int mode, uint32_t radius_cm, uint32_t max_keys
   }
   out.ent.assign(4 * total, 0);
   for (uint64_t i = 0; i < total; ++i) out.ent[4 * i] = kNone;
-  // pass 2: fill (tables are disjoint, so threads write without locks)
+  // pass 2: fill (tables are disjoint, so threads write without locks); rows carry the
+  // endpoints' canonical predecessors when the road ids leave room (rm_common.hpp)
+  const uint32_t rmask = ball_road_mask(R);
+  const bool with_pred = rmask != ~0u;
+  InEdges ie(g);
   std::vector<uint64_t> keys(threads, 0);
   parallel_nodes(N, threads, [&](int t, uint32_t u) {
     if (!bits[u]) return;
-    scr[t].run(g, ek, u, radius_cm, max_keys);
+    Scratch& sc = scr[t];
+    sc.run(g, ek, u, radius_cm, max_keys);
     RoadAcc& ra = acc_r[t];
-    ra.collect(g, inc_off, inc, scr[t].out);
+    ra.collect(g, inc_off, inc, sc.out, with_pred,
+               [&](size_t i) { return pred_index(ie, ek, sc.lab, u, sc.out[i].first, sc.out[i].second); });
     const uint32_t b = bits[u], mask = (1u << b) - 1u;
     uint32_t* tab = out.ent.data() + 4 * ball_row0(out.hdr[2 * (size_t)u]);
     for (size_t q = 0; q < ra.roads.size(); ++q) {
       uint32_t s = ball_slot(ra.roads[q], b);
       while (tab[4 * s] != kNone) s = (s + 1) & mask;
-      tab[4 * s] = ra.roads[q];
+      tab[4 * s] = ball_road_word(ra.roads[q], ra.p0[q], ra.p1[q], rmask);
       ball_pack(ra.k0[q], ra.k1[q], tab[4 * s + 1], tab[4 * s + 2], tab[4 * s + 3]);
     }
     keys[t] += ra.roads.size();
   });
+  out.road_mask = rmask;
   out.n_keys = 0;
   for (uint64_t k : keys) out.n_keys += k;
   out.radius_cm = radius_cm;

@@ -29,6 +29,7 @@ struct BallTables {
   uint32_t radius_cm = 0;
   uint64_t n_keys = 0;         // (node, road) rows stored
   uint32_t n_skipped = 0;      // nodes whose ball exceeded max_keys (their searches use the search tiers)
+  uint32_t road_mask = ~0u;    // road-id bits of a row's first word (rm_common.hpp ball_road_mask)
   double build_ms = 0;
 };
 

@@ -715,11 +715,11 @@ int rm_engine_grid_split(const rm_engine* e, uint32_t* f) {
 }
 
 int rm_engine_ball_lookup(rm_engine* e, int mode, uint64_t n, const uint32_t* from, const uint32_t* road,
-                          uint64_t* keys) {
+                          uint64_t* keys, uint8_t* preds) {
   return guarded([&] {
     if (!e) throw std::runtime_error("engine is NULL");
     if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
-    e->e->ball_lookup(mode, n, from, road, keys);
+    e->e->ball_lookup(mode, n, from, road, keys, preds);
   });
 }
 
@@ -759,7 +759,7 @@ int rm_graph_ball_sample(const char* graph_path, int mode, double radius_m, doub
 }
 
 int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t n, const uint32_t* from,
-                    const uint32_t* road, uint64_t* keys) {
+                    const uint32_t* road, uint64_t* keys, uint8_t* preds) {
   return guarded([&] {
     if (mode < 0 || mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
     if (!(radius_m >= 0.0) || radius_m * 100.0 > kBallMaxRadiusCm) throw std::runtime_error("ball radius out of range (0..10000 m)");
@@ -768,6 +768,7 @@ int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t 
     build_balls(g, mode, (uint32_t)(radius_m * 100.0), kBallMaxKeysHost, 4, bt);
     for (uint64_t i = 0; i < n; ++i) {
       keys[2 * i] = keys[2 * i + 1] = kKeyInf;
+      if (preds) preds[2 * i] = preds[2 * i + 1] = (uint8_t)kBallPredNone;
       if (from[i] >= g.num_nodes() || road[i] >= g.num_roads()) throw std::runtime_error("node or road out of range");
       const uint32_t off = bt.hdr[2 * (size_t)from[i]], bits = bt.hdr[2 * (size_t)from[i] + 1];
       if (!bits) continue;
@@ -775,9 +776,13 @@ int rm_balls_lookup(const char* graph_path, int mode, double radius_m, uint64_t 
       for (uint32_t s = ball_slot(road[i], bits);; s = (s + 1) & mask) {
         const uint32_t* e = bt.ent.data() + 4 * (ball_row0(off) + s);
         if (e[0] == kNone) break;
-        if (e[0] != road[i]) continue;
+        if ((e[0] & bt.road_mask) != road[i]) continue;
         keys[2 * i] = ball_key0(e[0], e[1], e[3]);
         keys[2 * i + 1] = ball_key1(e[0], e[2], e[3]);
+        if (preds) {
+          preds[2 * i] = (uint8_t)ball_pred(e[0], 0, bt.road_mask);
+          preds[2 * i + 1] = (uint8_t)ball_pred(e[0], 1, bt.road_mask);
+        }
         break;
       }
     }

@@ -1011,14 +1011,15 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
 constexpr uint32_t kBallMaxKeys = kBallMaxKeysHost;
 
 // row of `road` in a node's table (balls.hpp), continuing the probe from first-probe row e
-__device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, uint32_t road, uint4 e) {
-  if (e.x == road || e.x == kNone) return e;
+// (rmask: the road-id bits of the row's first word, rm_common.hpp ball_road_mask)
+__device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, uint32_t road, uint4 e, uint32_t rmask) {
+  if ((e.x & rmask) == road || e.x == kNone) return e;
   const uint32_t mask = (1u << h.y) - 1u;
   uint32_t s = ball_slot(road, h.y);
   for (;;) {
     s = (s + 1u) & mask;
     e = ent[ball_row0(h.x) + s];
-    if (e.x == road || e.x == kNone) return e;
+    if ((e.x & rmask) == road || e.x == kNone) return e;
   }
 }
 
@@ -1150,8 +1151,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     const uint4 ea0 = ball_first(A.ent, A.h0, ta0.x, ua && A.rk0 != kKeyInf);
     const uint4 eb1 = ball_first(B.ent, B.h1, tb0.x, ub && B.rk1 != kKeyInf);
     const uint4 eb0 = ball_first(B.ent, B.h0, tb0.x, ub && B.rk0 != kKeyInf);
-    if (la) b.route[lo + q] = k2_route(A, ta0, ta1, ball_resolve(A.ent, A.h1, ta0.x, ea1), ball_resolve(A.ent, A.h0, ta0.x, ea0));
-    if (lb) b.route[lo + qb] = k2_route(B, tb0, tb1, ball_resolve(B.ent, B.h1, tb0.x, eb1), ball_resolve(B.ent, B.h0, tb0.x, eb0));
+    const uint32_t rm = g.ball_road_mask;
+    if (la) b.route[lo + q] = k2_route(A, ta0, ta1, ball_resolve(A.ent, A.h1, ta0.x, ea1, rm), ball_resolve(A.ent, A.h0, ta0.x, ea0, rm));
+    if (lb) b.route[lo + qb] = k2_route(B, tb0, tb1, ball_resolve(B.ent, B.h1, tb0.x, eb1, rm), ball_resolve(B.ent, B.h0, tb0.x, eb0, rm));
   }
 }
 
@@ -1351,13 +1353,135 @@ struct BallPathLabels {
   const uint4* ent;
   uint2 h1, h0;
   unsigned long long rk1, rk0;
+  uint32_t rm;   // road-id bits of a row's first word
+  // both exits' rows of `road` (a dummy row for an unusable exit), first probes issued together
+  __device__ void rows(uint32_t road, uint4& r1, uint4& r0) const {
+    const uint4 e1 = ball_first(ent, h1, road, rk1 != kKeyInf);
+    const uint4 e0 = ball_first(ent, h0, road, rk0 != kKeyInf);
+    r1 = ball_resolve(ent, h1, road, e1, rm);
+    r0 = ball_resolve(ent, h0, road, e0, rm);
+  }
   __device__ unsigned long long operator()(uint32_t, uint32_t road, uint32_t side) const {
-    const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
-    const uint4 r1 = ball_resolve(ent, h1, road, ball_first(ent, h1, road, u1));
-    const uint4 r0 = ball_resolve(ent, h0, road, ball_first(ent, h0, road, u0));
+    uint4 r1, r0;
+    rows(road, r1, r0);
     return side ? ball_label(rk1, row_key1(r1), rk0, row_key1(r0)) : ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
   }
 };
+
+// One step of the ball-tier walk back from node x (label lx, rows r1/r0 of a road with x at
+// `side`): x's canonical predecessor in the two-exit search.  Where exactly one exit gives x
+// its label, the tight in-edges of the two-exit search are that exit's own and the canonical
+// one is the predecessor stored in its row; on a tie between the exits they are the union of
+// both, and the canonical one the smaller stored index (in_rec is in edge-id order).  Only
+// when that index was not stored (7 or more in-edges before it) are the in-edges scanned.
+// Returns false when no predecessor exists (not reached for a valid route).
+__device__ __forceinline__ bool ball_pred_step(const DevGraph& g, const BallPathLabels& lab, uint32_t acc, int mode,
+                                               uint32_t x, unsigned long long lx, const uint4& r1, const uint4& r0,
+                                               uint32_t side, uint4& rec, unsigned long long& plu) {
+  const uint32_t q0 = g.in_off[x];
+  const unsigned long long k1 = side ? row_key1(r1) : row_key0(r1), k0 = side ? row_key1(r0) : row_key0(r0);
+  uint32_t idx = kBallPredNone;
+  if (lab.rk1 != kKeyInf && k1 != kKeyInf && lab.rk1 + k1 == lx) idx = min(idx, ball_pred(r1.x, side, lab.rm));
+  if (lab.rk0 != kKeyInf && k0 != kKeyInf && lab.rk0 + k0 == lx) idx = min(idx, ball_pred(r0.x, side, lab.rm));
+  if (idx < kBallPredNone) {
+    rec = g.in_rec[q0 + idx];
+    plu = kKeyInf;   // the caller reads the predecessor's label from its rows
+    return true;
+  }
+  for (uint32_t q = q0, q1 = g.in_off[x + 1]; q < q1; ++q) {
+    const uint4 r = g.in_rec[q];
+    const uint32_t inf = g.in_info[q];
+    if (!edge_ok(inf, acc)) continue;
+    const unsigned long long lu = lab(r.y, r.z >> 1, r.z & 1u);
+    if (lu != kKeyInf && lu + make_key(r.w, time_ms_dev(r.w, mode_speed_dkph(mode, inf & 0xffffu))) == lx) {
+      rec = r;
+      plu = lu;
+      return true;
+    }
+  }
+  return false;
+}
+
+// path_walk for the ball tier: canonical predecessors from the rows (ball_pred_step), one
+// probe pair per walked node instead of one per examined in-edge
+// (r1_0 / r0_0: both exits' rows of the target road, already probed for the route key)
+__device__ void path_walk_ball(const DevGraph& g, const DevBatch& b, uint64_t p, const BallPathLabels& lab, int mode,
+                               const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1,
+                               unsigned long long key, int combo, int cap, const uint4& r1_0, const uint4& r0_0) {
+  const uint32_t acc = mode_access(mode);
+  const uint32_t n1a = a1.y, n0a = a1.x;
+  const unsigned long long rk1 = lab.rk1, rk0 = lab.rk0;
+  uint32_t* inl = b.path_inline + p * kInlinePath;
+  if (combo <= 1) {
+    b.route_dist[p] = key_dist(key);
+    b.path_sab[p] = make_uint2(a0.y, b0.y);
+    inl[0] = combo == 0 ? g.road_fwd[a0.x] : g.road_rev[a0.x];
+    b.path_cnt[p] = 1;
+    b.path_off[p] = 0;
+    return;
+  }
+  const uint32_t entry_e = combo == 2 ? g.road_fwd[b0.x] : g.road_rev[b0.x];
+  const uint32_t v0 = combo == 2 ? b1.x : b1.y, side0 = combo == 2 ? 0u : 1u;
+  auto label_at = [&](const uint4& r1, const uint4& r0, uint32_t side) {
+    return side ? ball_label(rk1, row_key1(r1), rk0, row_key1(r0)) : ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
+  };
+  const unsigned long long lx0 = label_at(r1_0, r0_0, side0);
+  // first walk: edges shifted into registers (front = travel order), stored after the walk
+  uint32_t n = 1, x = v0, side = side0;
+  unsigned long long lx = lx0;
+  uint4 r1 = r1_0, r0 = r0_0;
+  uint32_t pr[kInlinePath];
+#pragma unroll
+  for (int q = 0; q < kInlinePath; ++q) pr[q] = entry_e;
+  for (int guard = 0;; ++guard) {
+    if (lx == kKeyInf || guard > cap) { trace_fail(b, p, kErrRounds); return; }
+    if ((x == n1a && lx == rk1) || (x == n0a && lx == rk0)) break;
+    uint4 rec;
+    unsigned long long plu;
+    if (!ball_pred_step(g, lab, acc, mode, x, lx, r1, r0, side, rec, plu)) { trace_fail(b, p, kErrRounds); return; }
+#pragma unroll
+    for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
+    pr[0] = rec.x;
+    ++n;
+    x = rec.y;
+    side = rec.z & 1u;   // the edge's start: node0 of its road when it runs forward
+    lab.rows(rec.z >> 1, r1, r0);
+    lx = label_at(r1, r0, side);
+  }
+  const uint32_t exit_e = (x == n1a) ? g.road_fwd[a0.x] : g.road_rev[a0.x];
+#pragma unroll
+  for (int q = kInlinePath - 1; q > 0; --q) pr[q] = pr[q - 1];
+  pr[0] = exit_e;
+  ++n;
+  b.route_dist[p] = key_dist(key);
+  b.path_sab[p] = make_uint2(a0.y, b0.y);
+  b.path_cnt[p] = n;
+  if (n <= (uint32_t)kInlinePath) {
+#pragma unroll
+    for (int q = 0; q < kInlinePath; ++q)
+      if ((uint32_t)q < n) inl[q] = pr[q];
+    b.path_off[p] = 0;
+    return;
+  }
+  // long path: pool slot, second walk writing in travel order
+  const uint32_t at = atomicAdd(&b.ctl[0], n);
+  if ((uint64_t)at + n > b.path_cap) { atomicOr(&b.ctl[2], kErrPathOverflow); b.path_off[p] = kNone; return; }
+  b.path_off[p] = at;
+  uint32_t* dst = b.path_pool + at;
+  dst[n - 1] = entry_e;
+  dst[0] = exit_e;
+  x = v0; side = side0; r1 = r1_0; r0 = r0_0; lx = lx0;
+  for (uint32_t q = n - 2; q >= 1; --q) {
+    uint4 rec;
+    unsigned long long plu;
+    if (!ball_pred_step(g, lab, acc, mode, x, lx, r1, r0, side, rec, plu)) break;   // found on the first walk
+    dst[q] = rec.x;
+    x = rec.y;
+    side = rec.z & 1u;
+    lab.rows(rec.z >> 1, r1, r0);
+    lx = label_at(r1, r0, side);
+  }
+}
 
 // path ball tier: one lane per chosen transition whose bound fits the ball radius; the
 // others go to the search tiers (rl_routes_0 reused after K2, count ctl[8])
@@ -1384,12 +1508,15 @@ __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
     b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
     return;
   }
-  const BallPathLabels lab{g.ball_ent[mode], h1, h0, rk1, rk0};
-  const unsigned long long lab0 = d_spf(b0) ? lab(b1.x, b0.x, 0u) : kKeyInf;
-  const unsigned long long lab1 = d_spr(b0) ? lab(b1.y, b0.x, 1u) : kKeyInf;
+  const BallPathLabels lab{g.ball_ent[mode], h1, h0, rk1, rk0, g.ball_road_mask};
+  // the target road's rows once for both entry labels (and the walk's first node)
+  uint4 r1 = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u), r0 = r1;
+  if (d_spf(b0) || d_spr(b0)) lab.rows(b0.x, r1, r0);
+  const unsigned long long lab0 = d_spf(b0) ? ball_label(rk1, row_key0(r1), rk0, row_key0(r0)) : kKeyInf;
+  const unsigned long long lab1 = d_spr(b0) ? ball_label(rk1, row_key1(r1), rk0, row_key1(r0)) : kKeyInf;
   int combo = -1;
   const unsigned long long key = route_key_vals(a0, b0, b1, lab0, lab1, &combo);
-  path_walk(g, b, p, lab, mode, a0, a1, b0, b1, rk1, rk0, key, combo, (int)kBallMaxKeys);
+  path_walk_ball(g, b, p, lab, mode, a0, a1, b0, b1, key, combo, (int)kBallMaxKeys, r1, r0);
 }
 
 // path lane tier: one lane per chosen transition, labels in registers.  With `listed`,
@@ -2340,6 +2467,8 @@ struct BallSmem {
   SearchSmem<kBallSearchH, false> s;
   uint32_t road[kBallRowH];
   unsigned long long k0[kBallRowH], k1[kBallRowH];
+  uint8_t p0[kBallRowH], p1[kBallRowH];          // fill pass: the endpoints' canonical predecessor indices
+  uint8_t pidx[kBallSearchH];                     // fill pass: per settled slot
   uint16_t dense[kBallRowH], order[kBallRowH];   // fill pass: occupied row slots, rows by rank
   uint16_t tslot[kBallMaxTable];                 // fill pass: the node's table (row slot per table slot)
   uint32_t used, bad;
@@ -2362,8 +2491,36 @@ __global__ void __launch_bounds__(64) k_ball_build(DevGraph g, int mode, uint32_
   for (uint32_t u = blockIdx.x; u < g.n_nodes; u += gridDim.x) {
     if (FILL && hdr[u].y == 0u) continue;
     bounded_search<kBallSearchH, false>(sm.s, g, mode, radius, nullptr, 0u, u);
-    for (int h = lane; h < kBallRowH; h += kWave) { sm.road[h] = kEmpty; sm.k0[h] = kKeyInf; sm.k1[h] = kKeyInf; }
+    for (int h = lane; h < kBallRowH; h += kWave) {
+      sm.road[h] = kEmpty; sm.k0[h] = kKeyInf; sm.k1[h] = kKeyInf;
+      sm.p0[h] = (uint8_t)kBallPredNone; sm.p1[h] = (uint8_t)kBallPredNone;
+    }
     if (lane == 0) { sm.used = 0; sm.bad = sm.s.ovf ? 2u : 0u; }
+    if (FILL && g.ball_road_mask != ~0u && !sm.s.ovf) {
+      // canonical predecessor of every settled node (rm_common.hpp kBallRoadBits; the host build
+      // computes the same in balls.cpp pred_index): the first usable in-edge, in edge-id order,
+      // from a settled node whose key plus the edge's key is the node's key
+      const uint32_t acc = mode_access(mode);
+      for (int h = lane; h < kBallSearchH; h += kWave) {
+        const uint32_t v = sm.s.key[h];
+        uint32_t pv = kBallPredNone;
+        if (v != kEmpty && v != u) {
+          const unsigned long long lab = sm.s.lab[h];
+          const uint32_t q0 = g.in_off[v], q1 = g.in_off[v + 1];
+          for (uint32_t q = q0; q < q1 && q - q0 < kBallPredNone; ++q) {
+            const uint4 r = g.in_rec[q];
+            const uint32_t inf = g.in_info[q];
+            if (!edge_ok(inf, acc)) continue;
+            const unsigned long long lu = h_label(sm.s, r.y);
+            if (lu != kKeyInf && lu + make_key(r.w, time_ms_dev(r.w, mode_speed_dkph(mode, inf & 0xffffu))) == lab) {
+              pv = q - q0;
+              break;
+            }
+          }
+        }
+        sm.pidx[h] = (uint8_t)pv;
+      }
+    }
     __syncthreads();
     if (!sm.bad) {
       for (int h = lane; h < kBallSearchH; h += kWave) {
@@ -2385,8 +2542,8 @@ __global__ void __launch_bounds__(64) k_ball_build(DevGraph g, int mode, uint32_
             if (cur == r) break;
           }
           if (probe == kBallRowH) { atomicOr(&sm.bad, 2u); break; }
-          if (g.road_node0[r] == v) sm.k0[x] = lab;
-          if (g.road_node1[r] == v) sm.k1[x] = lab;
+          if (g.road_node0[r] == v) { sm.k0[x] = lab; if (FILL) sm.p0[x] = sm.pidx[h]; }
+          if (g.road_node1[r] == v) { sm.k1[x] = lab; if (FILL) sm.p1[x] = sm.pidx[h]; }
         }
       }
     }
@@ -2446,7 +2603,7 @@ __global__ void __launch_bounds__(64) k_ball_build(DevGraph g, int mode, uint32_
         if (h == 0xffffu) continue;
         uint32_t y, z, w;
         ball_pack(sm.k0[h], sm.k1[h], y, z, w);
-        ent[ball_row0(hh.x) + s] = make_uint4(sm.road[h], y, z, w);
+        ent[ball_row0(hh.x) + s] = make_uint4(ball_road_word(sm.road[h], sm.p0[h], sm.p1[h], g.ball_road_mask), y, z, w);
       }
     }
     __syncthreads();
@@ -2472,20 +2629,26 @@ __global__ void k_ball_hdr(const uint32_t* bits, const unsigned long long* off, 
 // keys from node `from` to both endpoints of `road` through the mode's tables, as K2 probes
 // them (rm_engine_ball_lookup; all-ones when outside the ball or the node has no table)
 __global__ void k_ball_lookup(DevGraph g, int mode, uint64_t n, const uint32_t* from, const uint32_t* road,
-                              unsigned long long* keys) {
+                              unsigned long long* keys, uint8_t* preds) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint2 h = g.ball_hdr[mode][from[i]];
   unsigned long long k0 = kKeyInf, k1 = kKeyInf;
+  uint32_t p0 = kBallPredNone, p1 = kBallPredNone;
   if (h.y) {
     const uint4* ent = g.ball_ent[mode];
-    const uint4 e = ball_resolve(ent, h, road[i], ent[ball_row0(h.x) + ball_slot(road[i], h.y)]);
-    k0 = row_key0(e);
-    k1 = row_key1(e);
-    if (e.x != road[i]) k0 = k1 = kKeyInf;
+    const uint32_t rm = g.ball_road_mask;
+    const uint4 e = ball_resolve(ent, h, road[i], ent[ball_row0(h.x) + ball_slot(road[i], h.y)], rm);
+    if (e.x != kNone && (e.x & rm) == road[i]) {
+      k0 = row_key0(e);
+      k1 = row_key1(e);
+      p0 = ball_pred(e.x, 0, rm);
+      p1 = ball_pred(e.x, 1, rm);
+    }
   }
   keys[2 * i] = k0;
   keys[2 * i + 1] = k1;
+  if (preds) { preds[2 * i] = (uint8_t)p0; preds[2 * i + 1] = (uint8_t)p1; }
 }
 
 __global__ void k_fill_edge_src(const uint32_t* node_off, uint32_t n_nodes, uint32_t* edge_src) {
@@ -2606,6 +2769,7 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
     std::vector<uint32_t> fill(in_off.begin(), in_off.end() - 1);
     for (uint32_t e = 0; e < g.num_edges(); ++e) in_edge[fill[g.edges[e].target]++] = e;
     dg_.in_off = upload(allocs_, in_off);
+    dg_.ball_road_mask = ball_road_mask(g.num_roads());
     dg_.in_edge = upload(allocs_, in_edge);
     // path walks read one self-contained record per in-edge: {edge, source node, road << 1 | rev,
     // length cm} + its info word (access, speed)
@@ -2886,11 +3050,13 @@ bool Engine::build_balls_gpu(int mode, uint32_t radius_cm, uint32_t max_keys, ui
   return true;
 }
 
-void Engine::ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys) {
+void Engine::ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys,
+                         uint8_t* preds) {
   std::lock_guard<std::mutex> lk(ball_mu_);
   RM_HIP(hipSetDevice(device_));
   for (uint64_t i = 0; i < n; ++i) {
     keys[2 * i] = keys[2 * i + 1] = kKeyInf;
+    if (preds) preds[2 * i] = preds[2 * i + 1] = (uint8_t)kBallPredNone;
     if (from[i] >= host_.num_nodes() || road[i] >= host_.num_roads()) throw std::runtime_error("node or road out of range");
   }
   if (!((ball_built_ >> mode) & 1u) || n == 0) return;
@@ -2899,12 +3065,14 @@ void Engine::ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint3
   uint32_t* d_from = dalloc<uint32_t>(tmp, n);
   uint32_t* d_road = dalloc<uint32_t>(tmp, n);
   unsigned long long* d_keys = dalloc<unsigned long long>(tmp, 2 * n);
+  uint8_t* d_pred = preds ? dalloc<uint8_t>(tmp, 2 * n) : nullptr;
   RM_HIP(hipMemcpy(d_from, from, n * 4, hipMemcpyHostToDevice));
   RM_HIP(hipMemcpy(d_road, road, n * 4, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(k_ball_lookup, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, dg_, mode, n, d_from, d_road,
-                     d_keys);
+                     d_keys, d_pred);
   RM_HIP(hipGetLastError());
   RM_HIP(hipMemcpy(keys, d_keys, 2 * n * 8, hipMemcpyDeviceToHost));
+  if (preds) RM_HIP(hipMemcpy(preds, d_pred, 2 * n, hipMemcpyDeviceToHost));
 }
 
 // ==========================================================================================

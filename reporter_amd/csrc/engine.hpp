@@ -67,6 +67,7 @@ struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   const uint4* ball_ent[5];
   uint32_t ball_radius[5];
   uint32_t ball_mask;            // modes whose balls are built
+  uint32_t ball_road_mask;       // road-id bits of a row's first word (rm_common.hpp ball_road_mask)
   double lon0, lat0, dlon, dlat;
   uint32_t ncx, ncy, n_nodes, n_edges, n_segments, pad;
 };
@@ -350,7 +351,7 @@ class Engine {
   uint32_t ball_gpu_mask() const { return ball_gpu_; }
   // keys[2i], keys[2i+1] from node from[i] to road[i]'s node0 / node1 through the built tables
   // of `mode`, probed on the device as K2 does (all-ones: outside the ball / no table)
-  void ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys);
+  void ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys, uint8_t* preds);
   // K1's grid: each cell of the graph's grid split f x f (1 = the graph's grid)
   uint32_t grid_split() const { return grid_split_; }
 

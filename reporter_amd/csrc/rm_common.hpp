@@ -216,6 +216,27 @@ RM_HD uint32_t ball_slot(uint32_t v, uint32_t bits) {
   return ((((v >> kBallGroupLog) * 2654435761u) >> (32u + kBallGroupLog - bits)) << kBallGroupLog) |
          (v & ((1u << kBallGroupLog) - 1u));
 }
+// Canonical predecessors in the rows (round 3).  Above a 26-bit road id, a row's road word
+// carries the canonical predecessor of each endpoint v of the road in the search from the
+// table's node x: bits 26-28 for node0, 29-31 for node1, each the index, among v's in-edges in
+// edge-id order (the engine's in_rec order), of the smallest-id edge u -> v usable by the mode
+// with key(x -> u) + key(u -> v) == key(x -> v); kBallPredNone when v is x, or that index is 7 or
+// more (the path walk then scans v's in-edges).  The path walk follows these one probe per node
+// instead of probing every in-edge (k_paths_ball).  A graph of 2^26 - 1 roads or more keeps the
+// whole word for the road: mask all-ones and no predecessors.
+constexpr uint32_t kBallRoadBits = 26;
+constexpr uint32_t kBallPredNone = 7u;
+RM_HD uint32_t ball_road_mask(uint32_t n_roads) {
+  return n_roads < (1u << kBallRoadBits) - 1u ? (1u << kBallRoadBits) - 1u : ~0u;
+}
+RM_HD uint32_t ball_road_word(uint32_t road, uint32_t p0, uint32_t p1, uint32_t mask) {
+  return mask == ~0u ? road : road | p0 << kBallRoadBits | p1 << (kBallRoadBits + 3u);
+}
+// predecessor index of endpoint `side` (0: node0, 1: node1) in a row's road word
+RM_HD uint32_t ball_pred(uint32_t word, uint32_t side, uint32_t mask) {
+  return mask == ~0u ? kBallPredNone : (word >> (kBallRoadBits + 3u * side)) & 7u;
+}
+
 // Rank that writes a time-tile file (bucket, level | tile index << 3) in the multi-rank batch
 // reporter: the rows of every rank are all-gathered and each file is culled and written by one
 // rank (Fibonacci hash of the file key), so the privacy count sees every vehicle.  Shared by the

@@ -94,15 +94,17 @@ class Engine:
         _lib.check(_lib.lib().rm_engine_grid_split(self._h, out.ctypes.data))
         return int(out[0])
 
-    def ball_lookup(self, mode, from_nodes, roads):
+    def ball_lookup(self, mode, from_nodes, roads, preds=False):
         """Keys (n, 2) from each node to the two endpoints of each road through the engine's
-        device tables of `mode` (all-ones outside the ball / without a table)."""
+        device tables of `mode` (all-ones outside the ball / without a table); with preds, also
+        the rows' canonical predecessor indices (n, 2) (7: none stored)."""
         f = _c(from_nodes, np.uint32)
         r = _c(roads, np.uint32)
         keys = np.empty((len(f), 2), np.uint64)
+        pr = np.empty((len(f), 2), np.uint8)
         _lib.check(_lib.lib().rm_engine_ball_lookup(self._h, int(mode), len(f), f.ctypes.data, r.ctypes.data,
-                                                    keys.ctypes.data))
-        return keys
+                                                    keys.ctypes.data, pr.ctypes.data if preds else None))
+        return (keys, pr) if preds else keys
 
     def close(self):
         if getattr(self, "_h", None):

@@ -53,13 +53,46 @@ def _dijkstra(g, tgt, key, u, radius_cm):
     return done
 
 
-def _lookup(path, mode, radius_m, fr, road):
+def _lookup(path, mode, radius_m, fr, road, preds=False):
     fr = np.ascontiguousarray(fr, np.uint32)
     road = np.ascontiguousarray(road, np.uint32)
     out = np.empty(2 * len(fr), np.uint64)
+    pr = np.empty(2 * len(fr), np.uint8)
     _lib.check(_lib.lib().rm_balls_lookup(os.fsencode(path), mode, radius_m, len(fr), fr.ctypes.data,
-                                          road.ctypes.data, out.ctypes.data))
-    return out.reshape(-1, 2)
+                                          road.ctypes.data, out.ctypes.data, pr.ctypes.data if preds else None))
+    return (out.reshape(-1, 2), pr.reshape(-1, 2)) if preds else out.reshape(-1, 2)
+
+
+def _pred_index(g, key, done, u, v):
+    """Canonical predecessor of v in the search from u, as the index among v's in-edges in
+    edge-id order (rm_common.hpp kBallRoadBits): the first usable edge x -> v with
+    key(u -> x) + key(x -> v) == key(u -> v); 7 for u itself, outside the ball, or index >= 7."""
+    if v == u or v not in done:
+        return 7
+    ins = _in_edges(g)[v]
+    for i, (e, x) in enumerate(ins[:7]):
+        if int(key[e]) != KEY_INF and x in done and done[x] + int(key[e]) == done[v]:
+            return i
+    return 7
+
+
+_IN = {}
+
+
+def _in_edges(g):
+    k = id(g)
+    if k not in _IN:
+        off = g["node_off"]
+        tgt = g["edges"].reshape(-1, 4)[:, 0]
+        ins = {}
+        for x in range(len(off) - 1):
+            for e in range(off[x], off[x + 1]):
+                ins.setdefault(int(tgt[e]), []).append((e, x))
+        for v in ins:
+            ins[v].sort()
+        _IN.clear()
+        _IN[k] = ins
+    return _IN[k]
 
 
 @pytest.mark.parametrize("mode,radius_m", [(0, 400.0), (0, 150.0), (3, 400.0), (4, 250.0), (0, 655.0), (0, 2000.0), (4, 2000.0)])
@@ -70,7 +103,7 @@ def test_ball_rows_match_dijkstra(small_world, mode, radius_m):
     n0, n1 = g["road_node0"], g["road_node1"]
     R = len(n0)
     rng = np.random.default_rng(mode * 7 + int(radius_m))
-    fr, roads, want = [], [], []
+    fr, roads, want, wpred = [], [], [], []
     for u in rng.choice(g.n_nodes, 50, replace=False):
         done = _dijkstra(g, tgt, key, int(u), int(radius_m * 100))
         near = np.nonzero(np.isin(n0, list(done)) | np.isin(n1, list(done)))[0]
@@ -78,9 +111,15 @@ def test_ball_rows_match_dijkstra(small_world, mode, radius_m):
             fr.append(u)
             roads.append(r)
             want.append((done.get(int(n0[r]), KEY_INF), done.get(int(n1[r]), KEY_INF)))
-    got = _lookup(small_world, mode, radius_m, fr, roads)
+            inside = any(int(x) in done for x in (n0[r], n1[r]))
+            wpred.append((_pred_index(g, key, done, int(u), int(n0[r])) if inside else 7,
+                          _pred_index(g, key, done, int(u), int(n1[r])) if inside else 7))
+    got, pred = _lookup(small_world, mode, radius_m, fr, roads, preds=True)
     np.testing.assert_array_equal(got, np.array(want, np.uint64))
     assert int(np.sum(got != np.uint64(KEY_INF))) > 200
+    # the rows' canonical predecessors (what the path walk follows)
+    np.testing.assert_array_equal(pred, np.array(wpred, np.uint8))
+    assert int(np.sum(pred < 7)) > 200
 
 
 def test_ball_radius_zero_keeps_only_self(small_world):
@@ -114,10 +153,10 @@ def test_ball_lookup_errors(small_world):
     one = np.zeros(1, np.uint32)
     out = np.zeros(2, np.uint64)
     L = _lib.lib()
-    assert L.rm_balls_lookup(os.fsencode(small_world), 9, 100.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
-    assert L.rm_balls_lookup(os.fsencode(small_world), 0, 20000.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
+    assert L.rm_balls_lookup(os.fsencode(small_world), 9, 100.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data, None) != 0
+    assert L.rm_balls_lookup(os.fsencode(small_world), 0, 20000.0, 1, one.ctypes.data, one.ctypes.data, out.ctypes.data, None) != 0
     big = np.array([10 ** 9], np.uint32)
-    assert L.rm_balls_lookup(os.fsencode(small_world), 0, 100.0, 1, big.ctypes.data, one.ctypes.data, out.ctypes.data) != 0
+    assert L.rm_balls_lookup(os.fsencode(small_world), 0, 100.0, 1, big.ctypes.data, one.ctypes.data, out.ctypes.data, None) != 0
 
 
 def _sample(path, mode, radius_m):

@@ -61,13 +61,16 @@ def test_gpu_built_balls_equal_host_build(slice_graph, mode, radius):
     print("mode", mode, "radius", radius, "first run (incl. ball build) %.2fs" % (time.time() - t), st, flush=True)
     assert st["built_on_gpu"] and st["keys"] > 0 and st["radius_m"] == radius
     f, rd = _pairs(g, 400, seed=mode)
-    got = eng.ball_lookup(mode, f, rd)
+    got, gpred = eng.ball_lookup(mode, f, rd, preds=True)
     want = np.empty((len(f), 2), np.uint64)
+    wpred = np.empty((len(f), 2), np.uint8)
     _lib.check(_lib.lib().rm_balls_lookup(os.fsencode(slice_graph), mode, radius, len(f), f.ctypes.data,
-                                          rd.ctypes.data, want.ctypes.data))
+                                          rd.ctypes.data, want.ctypes.data, wpred.ctypes.data))
     inside = (want != np.uint64(2**64 - 1)).any(axis=1)
     assert inside.sum() > 1000 and (~inside).sum() > 100, (inside.sum(), len(f))
     np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(gpred, wpred)   # the rows' canonical predecessors (path walk)
+    assert int((wpred < 7).sum()) > 1000
     bm.close()
     eng.close()
 
