@@ -160,10 +160,12 @@ static uint64_t mk(uint32_t d, uint32_t t) { return ((uint64_t)d << 32) | t; }
  *     (KA sources + KB targets per layer pair) [10] candidates kept (sum of K over states)
  * [11] grid rows visited by the candidate search (one item range per row) [12] chained
  * transitions (a path is built) [13] path edges [14] segments formed
- * [15] in-edge records the path walk visits (a walked node's in-edges in edge-id order up to
- *      its canonical predecessor) [16] route-ball rows the path stage reads: per chained
- *      transition one per usable exit for each usable direction of the target road, and per
- *      usable in-edge visited one per usable exit (counted only after og_prepare_path_counters) */
+ * [15] in-edge records the path walk reads (per walked node the canonical predecessor's record,
+ *      located by the index stored in the route-ball rows; when that index is 7 or more, the
+ *      node's in-edges in edge-id order up to it) [16] route-ball rows the path stage reads, one
+ *      per usable exit: the target road's once per chained transition, the predecessor road's
+ *      per walked node, and each usable in-edge's on a scan (counted only after
+ *      og_prepare_path_counters) */
 #define OG_NCNT 17
 static uint64_t og_cnt[OG_NCNT];
 static uint32_t og_roots;   /* usable exits of the last search_from */
@@ -733,9 +735,8 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
       /* directed edge sequence: exit edge, graph edges, entry edge */
       uint32_t ns = 0;
       const int pcount = pc_node_off == g->node_off && pc_nodes == g->n_nodes;
-      if (pcount) {   /* entry labels: both exits' rows of the target road per usable direction */
-        og_cnt[16] += (uint64_t)og_roots * ((uint32_t)e_ok(g, g->road_fwd[rb], acc) + (uint32_t)e_ok(g, g->road_rev[rb], acc));
-      }
+      if (pcount && (e_ok(g, g->road_fwd[rb], acc) || e_ok(g, g->road_rev[rb], acc)))
+        og_cnt[16] += og_roots;   /* entry labels: the exits' rows of the target road, read once */
       if (combo <= 1) {
         stack[ns++] = combo == 0 ? g->road_fwd[ra] : g->road_rev[ra];
       } else {
@@ -745,13 +746,22 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
         stack[ns++] = entry_e;
         while (ws.label[v] != ws.rootkey[v]) {
           const uint32_t e = ws.pred[v];
-          if (pcount) {   /* in-edges of v visited in edge-id order up to the canonical one */
-            for (uint32_t q = pc_in_off[v]; q < pc_in_off[v + 1]; ++q) {
-              const uint32_t f = pc_in_edge[q];
+          if (pcount) {
+            /* the GPU walk (k_paths_ball) reads the canonical predecessor's in-edge record straight
+             * from the index stored in the route-ball rows when it is below 7, else it scans the
+             * in-edges in edge-id order up to it, probing both exits' rows of each usable one; then
+             * the exits' rows of the predecessor's road give the next node's label */
+            uint32_t idx = 0;
+            while (pc_in_off[v] + idx < pc_in_off[v + 1] && pc_in_edge[pc_in_off[v] + idx] != e) ++idx;
+            if (idx < 7) {
               og_cnt[15]++;
-              if (e_ok(g, f, acc)) og_cnt[16] += og_roots;
-              if (f == e) break;
+            } else {
+              for (uint32_t q = pc_in_off[v]; q <= pc_in_off[v] + idx; ++q) {
+                og_cnt[15]++;
+                if (e_ok(g, pc_in_edge[q], acc)) og_cnt[16] += og_roots;
+              }
             }
+            og_cnt[16] += og_roots;
           }
           if (ns == scap) { scap *= 2; stack = (uint32_t*)realloc(stack, sizeof(uint32_t) * scap); }
           stack[ns++] = e;

@@ -130,10 +130,10 @@ def segments_algorithmic_bytes(c):
 def paths_algorithmic_bytes(c):
     """Path stage (k_paths_ball) algorithmic bytes: per chained transition 64 B of the chosen
     candidates' descriptors + 16 B pair constants + 16 B of exit table headers + 20 B written
-    (route length, both offsets, path count and offset); 16 B per route-ball row read (entry
-    labels and the labels of visited in-edges' sources); 20 B per in-edge visited by the walk
-    (self-contained record + access word); 4 B per path edge written.  Needs the counters of
-    prepare_path_counters."""
+    (route length, both offsets, path count and offset); 16 B per route-ball row read (the
+    target road's rows, then per walked node the rows of its predecessor's road); 20 B per
+    in-edge record read (the 16 B record + the node's 4 B in-edge offset, or its access word on
+    a scan); 4 B per path edge written.  Needs the counters of prepare_path_counters."""
     return 116 * c["chained"] + 16 * c["path_rows"] + 20 * c["path_in_edges"] + 4 * c["path_edges"]
 
 
