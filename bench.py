@@ -21,6 +21,7 @@ Prints ONE JSON line (rank 0).  No PyTorch is loaded: RCCL is bound natively
 by libreporter_match.so and ranks rendezvous through a node-local file.
 """
 import argparse
+import ctypes as C
 import hashlib
 import json
 import multiprocessing as mp
@@ -54,6 +55,10 @@ def parse():
     ap.add_argument("--parts-extra", type=int, default=2,
                     help="also time the batch as this many concurrent parts (engine.MultiMatcher), reported "
                          "beside the value as concurrent_parts (0 = skip; batches <= 20 M points)")
+    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
+                    help="rccl: one rank per GPU over xGMI (the measured configuration); host: the same "
+                         "collectives over TCP on the host (rm_comm_init_host), ranks may share a GPU -- a "
+                         "functional run of the multi-rank path on fewer GPUs, not a scaling measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the C1 latency and JSON-boundary lines")
     ap.add_argument("--json-traces", type=int, default=10000, help="traces sent through rm_match_batch as JSON")
@@ -350,13 +355,23 @@ def main():
         procs = a.cpu_procs or min(16, os.cpu_count() or 1)
         cpu = cpu_baseline_leg(gpath, tr, cfg["search_radius"], procs)
 
-    comm, comm_note = None, None
-    try:
-        comm = dist.Comm(rank, world, local, token=os.environ.get("RM_RDZV_TOKEN"))
-    except Exception as e:  # noqa: BLE001 -- one rank without RCCL still measures the matcher
-        if world > 1:
-            raise
-        comm_note = "RCCL unavailable at N=1 (%s): histogram not all-reduced" % e
+    comm, comm_note, tcp = None, None, None
+    if a.comm == "host":
+        # ranks beyond the visible GPUs share them (functional multi-rank run, not a measurement)
+        cnt = C.c_int(0)
+        _lib.check(_lib.lib().rm_device_count(C.byref(cnt)))
+        local = local % max(1, cnt.value)
+        tcp = dist.TcpAllgather(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                                int(os.environ.get("MASTER_PORT", "29500")) + 1)
+        comm = dist.Comm(rank, world, local, allgather=tcp)
+        comm_note = "host transport (TCP all-gather, rm_comm_init_host); %d rank(s) on %d GPU(s)" % (world, cnt.value)
+    else:
+        try:
+            comm = dist.Comm(rank, world, local, token=os.environ.get("RM_RDZV_TOKEN"))
+        except Exception as e:  # noqa: BLE001 -- one rank without RCCL still measures the matcher
+            if world > 1:
+                raise
+            comm_note = "RCCL unavailable at N=1 (%s): histogram not all-reduced" % e
     t_up = time.perf_counter()
     eng = engine.Engine(gpath, local)
     radius = a.ball_radius if a.ball_radius is not None else cfg.get("ball_radius_m")
@@ -529,6 +544,8 @@ def main():
             }
     if comm is not None:
         comm.close()
+    if tcp is not None:
+        tcp.close()
     hist.close()
     dur.close()
     bm.close()

@@ -112,6 +112,75 @@ def rendezvous(rank, path, make_id, size=128, timeout_s=300.0):
 HOST_ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 
 
+class TcpAllgather:
+    """A host all-gather over TCP with no framework (for rm_comm_init_host): rank 0 listens on
+    (addr, port), every other rank connects once; each call sends this rank's bytes to rank 0,
+    which returns every rank's bytes in rank order to all.  Lets several ranks share one GPU
+    (RCCL refuses two ranks on one device) with the product's exchange code unchanged."""
+
+    def __init__(self, rank, world_size, addr="127.0.0.1", port=29555, timeout_s=300.0):
+        import socket
+        self.rank, self.world = rank, world_size
+        self.peers = {}
+        if world_size == 1:
+            return
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, port))
+            srv.listen(world_size)
+            srv.settimeout(timeout_s)
+            while len(self.peers) < world_size - 1:
+                conn, _ = srv.accept()
+                conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                r = int.from_bytes(self._recv(conn, 4), "little")
+                self.peers[r] = conn
+            srv.close()
+        else:
+            t0 = time.time()
+            while True:
+                try:
+                    conn = socket.create_connection((addr, port), timeout=timeout_s)
+                    break
+                except OSError:
+                    if time.time() - t0 > timeout_s:
+                        raise
+                    time.sleep(0.05)
+            conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            conn.sendall(rank.to_bytes(4, "little"))
+            self.peers[0] = conn
+
+    @staticmethod
+    def _recv(conn, n):
+        buf = bytearray(n)
+        view, got = memoryview(buf), 0
+        while got < n:
+            k = conn.recv_into(view[got:], n - got)
+            if k == 0:
+                raise ConnectionError("peer closed")
+            got += k
+        return bytes(buf)
+
+    def __call__(self, data):
+        if self.world == 1:
+            return [data]
+        n = len(data)
+        if self.rank == 0:
+            parts = [data] + [self._recv(self.peers[r], n) for r in range(1, self.world)]
+            blob = b"".join(parts)
+            for r in range(1, self.world):
+                self.peers[r].sendall(blob)
+            return parts
+        self.peers[0].sendall(data)
+        blob = self._recv(self.peers[0], n * self.world)
+        return [blob[r * n:(r + 1) * n] for r in range(self.world)]
+
+    def close(self):
+        for c in self.peers.values():
+            c.close()
+        self.peers = {}
+
+
 class Comm:
     """Communicator for one rank (one process per GPU, single node): RCCL over xGMI, or, with
     `allgather`, a host transport — a callable taking this rank's bytes and returning every

@@ -181,3 +181,38 @@ def test_tile_owner_rule():
         owners = [L.rm_tile_file_owner(b, t, n) for b in range(412000, 412040) for t in range(0, 800, 8)]
         assert set(owners) == set(range(n))
         assert owners == [L.rm_tile_file_owner(b, t, n) for b in range(412000, 412040) for t in range(0, 800, 8)]
+
+
+def _tcp_rank(rank, world, port, out_dir):
+    sys.path.insert(0, ROOT)
+    from reporter_amd import dist
+    ag = dist.TcpAllgather(rank, world, "127.0.0.1", port, timeout_s=60)
+    res = {"parts": [p.hex() for p in ag(bytes([rank + 1]) * (3 + 0))]}
+    big = ag(bytes([rank]) * 100000)
+    res["big_ok"] = all(p == bytes([r]) * 100000 for r, p in enumerate(big))
+    comm = dist.Comm(rank, world, -1, allgather=ag)   # the product's communicator, host values only
+    res["sum"] = comm.allreduce_host(2.0 ** rank, dist.SUM)
+    res["max"] = comm.allreduce_host(float(rank), dist.MAX)
+    comm.barrier()
+    comm.close()
+    ag.close()
+    with open(os.path.join(out_dir, "tcp%d.json" % rank), "w") as f:
+        json.dump(res, f)
+
+
+@pytest.mark.timeout(120)
+def test_tcp_allgather_world3(tmp_path, built_lib):
+    """dist.TcpAllgather (bench.py --comm host: ranks sharing a GPU, no framework) at world 3."""
+    import multiprocessing as mp
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_tcp_rank, args=(r, 3, port, str(tmp_path))) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(100)
+        assert p.exitcode == 0
+    res = [json.load(open(str(tmp_path / ("tcp%d.json" % r)))) for r in range(3)]
+    for r in res:
+        assert r["parts"] == ["010101", "020202", "030303"]
+        assert r["big_ok"] and r["sum"] == 7.0 and r["max"] == 2.0
