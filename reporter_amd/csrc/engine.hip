@@ -709,8 +709,12 @@ __device__ __forceinline__ unsigned long long route_key_vals(const uint4& a0, co
   unsigned long long best = kKeyInf;
   int bc = -1;
   if (a0.x == rb) {
-    if (spf && sb >= sa) { const unsigned long long k = make_key(sb - sa, time_ms_dev(sb - sa, spf)); if (k < best) { best = k; bc = 0; } }
-    if (spr && sa >= sb) { const unsigned long long k = make_key(sa - sb, time_ms_dev(sa - sb, spr)); if (k < best) { best = k; bc = 1; } }
+    // direct along the road: forward when s_b > s_a, reverse when s_b < s_a; at s_b == s_a both
+    // give (0, 0) and forward comes first -- so one division decides it (a second, divergent
+    // fp64 division per transition cost K2 9 % on C2)
+    const bool fw = sb > sa || (sb == sa && spf);
+    const uint32_t sp = fw ? spf : spr, d = fw ? sb - sa : sa - sb;
+    if (sp) { best = make_key(d, time_ms_dev(d, sp)); bc = fw ? 0 : 1; }
   }
   if (spf && lab0 != kKeyInf) { const unsigned long long k = lab0 + make_key(sb, b1.z); if (k < best) { best = k; bc = 2; } }
   if (spr && lab1 != kKeyInf) { const unsigned long long k = lab1 + make_key(L - sb, b1.w); if (k < best) { best = k; bc = 3; } }
