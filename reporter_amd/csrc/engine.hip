@@ -1063,10 +1063,18 @@ __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1,
 // own (the round-2 kernel's lanes ran to their wave's largest K_B, each target two dependent
 // round trips after the last), and two transitions per lane are in flight at once.
 constexpr int kK2Items = 256;
+// global-address-space 16-byte pointer: loads through it are global_load_dwordx4 even when the
+// address went through LDS (a generic pointer there would become a flat load)
+typedef unsigned int k2_v4 __attribute__((ext_vector_type(4)));
+typedef const k2_v4 __attribute__((address_space(1)))* k2_gptr;
+__device__ __forceinline__ uint4 k2_ld(k2_gptr p) {
+  const k2_v4 v = *p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 struct K2Src {
   unsigned long long rk1, rk0;   // exit root keys (kKeyInf: that exit is unusable)
   uint2 h1, h0;                  // table headers of the exits (bits 0: no table)
-  const uint4* ent;              // the item's mode's table rows
+  unsigned long long ent;        // the item's mode's table rows (a global address: see k2_gptr)
   uint32_t road, s;              // source road and offset on it (direct combinations)
   uint32_t tdesc;                // the pair's first target descriptor (p * kMaxCand)
   uint32_t rel;                  // the item's first route, relative to the block's range
@@ -1109,9 +1117,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     K2Src S;
     exit_keys(a0, pi.x, S.rk1, S.rk0);
     const bool fits = pi.x <= g.ball_radius[mode] && ((g.ball_mask >> mode) & 1u);
-    S.h1 = fits && S.rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
-    S.h0 = fits && S.rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
-    S.ent = g.ball_ent[mode];
+    S.h1 = S.h0 = make_uint2(0u, 1u);
+    if (fits) {   // both headers loaded together, then kept where the exit is usable
+      const uint2* hp = g.ball_hdr[mode];
+      const uint2 x1 = hp[a1.y], x0 = hp[a1.x];
+      if (S.rk1 != kKeyInf) S.h1 = x1;
+      if (S.rk0 != kKeyInf) S.h0 = x0;
+    }
+    S.ent = (unsigned long long)(uintptr_t)g.ball_ent[mode];
     S.road = a0.x;
     S.s = a0.y;
     S.tdesc = p * kMaxCand;
@@ -1133,31 +1146,38 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     for (uint32_t j = 0; j < KB; ++j) sm.owner[ob - lo + j] = (uint8_t)threadIdx.x;
   }
   __syncthreads();
-  // ---- phase 2: the block's routes, two transitions per lane and step (loads of both issued
-  // before either is used); a handed-over item's routes are written by the search tiers
+  // ---- phase 2: the block's routes, two transitions per lane and step.  Every load of a step
+  // is issued before any is used: the descriptors unconditionally (a handed-over item's
+  // descriptor is as valid an address), the four first probes branch-free with an unused probe
+  // reading a valid dummy address, and through global-address-space pointers (a pointer that
+  // went through LDS is otherwise generic: flat loads, each waited for on its own).
+  const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
+  const uint32_t rm = g.ball_road_mask;
   for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
     const uint32_t qb = q + kK2Items;
     const bool hb = qb < n;
+    const uint32_t qB = hb ? qb : q;
     const K2Src& A = sm.src[sm.owner[q]];
-    const K2Src& B = sm.src[sm.owner[hb ? qb : q]];
+    const K2Src& B = sm.src[sm.owner[qB]];
     const bool la = A.bound != kNone, lb = hb && B.bound != kNone;
-    uint4 ta0 = make_uint4(kNone, 0u, 0u, 0u), ta1 = ta0, tb0 = ta0, tb1 = ta0;
-    if (la) {
-      const uint4* d = b.cand_desc + 2 * (uint64_t)(A.tdesc + (q - A.rel));
-      ta0 = d[0]; ta1 = d[1];
-    }
-    if (lb) {
-      const uint4* d = b.cand_desc + 2 * (uint64_t)(B.tdesc + (qb - B.rel));
-      tb0 = d[0]; tb1 = d[1];
-    }
+    const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(A.tdesc + (q - A.rel)));
+    const k2_gptr db = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(B.tdesc + (qB - B.rel)));
+    const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1), tb0 = k2_ld(db), tb1 = k2_ld(db + 1);
     const bool ua = la && ta0.w != 0u, ub = lb && tb0.w != 0u;   // some direction of the target road is usable
-    const uint4 ea1 = ball_first(A.ent, A.h1, ta0.x, ua && A.rk1 != kKeyInf);
-    const uint4 ea0 = ball_first(A.ent, A.h0, ta0.x, ua && A.rk0 != kKeyInf);
-    const uint4 eb1 = ball_first(B.ent, B.h1, tb0.x, ub && B.rk1 != kKeyInf);
-    const uint4 eb0 = ball_first(B.ent, B.h0, tb0.x, ub && B.rk0 != kKeyInf);
-    const uint32_t rm = g.ball_road_mask;
-    if (la) b.route[lo + q] = k2_route(A, ta0, ta1, ball_resolve(A.ent, A.h1, ta0.x, ea1, rm), ball_resolve(A.ent, A.h0, ta0.x, ea0, rm));
-    if (lb) b.route[lo + qb] = k2_route(B, tb0, tb1, ball_resolve(B.ent, B.h1, tb0.x, eb1, rm), ball_resolve(B.ent, B.h0, tb0.x, eb0, rm));
+    const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
+    const bool ub1 = ub && B.rk1 != kKeyInf, ub0 = ub && B.rk0 != kKeyInf;
+    const k2_gptr ea = (k2_gptr)A.ent, eb = (k2_gptr)B.ent;
+    const k2_gptr pa1 = ua1 ? ea + (ball_row0(A.h1.x) + ball_slot(ta0.x, A.h1.y)) : dummy;
+    const k2_gptr pa0 = ua0 ? ea + (ball_row0(A.h0.x) + ball_slot(ta0.x, A.h0.y)) : dummy;
+    const k2_gptr pb1 = ub1 ? eb + (ball_row0(B.h1.x) + ball_slot(tb0.x, B.h1.y)) : dummy;
+    const k2_gptr pb0 = ub0 ? eb + (ball_row0(B.h0.x) + ball_slot(tb0.x, B.h0.y)) : dummy;
+    const uint4 la1 = k2_ld(pa1), la0 = k2_ld(pa0), lb1 = k2_ld(pb1), lb0 = k2_ld(pb0);
+    const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+    const uint4 ea1 = ua1 ? la1 : none, ea0 = ua0 ? la0 : none, eb1 = ub1 ? lb1 : none, eb0 = ub0 ? lb0 : none;
+    const uint4* ga = (const uint4*)A.ent;
+    const uint4* gb = (const uint4*)B.ent;
+    if (la) b.route[lo + q] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm));
+    if (lb) b.route[lo + qb] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm));
   }
 }
 
@@ -1360,10 +1380,15 @@ struct BallPathLabels {
   uint32_t rm;   // road-id bits of a row's first word
   // both exits' rows of `road` (a dummy row for an unusable exit), first probes issued together
   __device__ void rows(uint32_t road, uint4& r1, uint4& r0) const {
-    const uint4 e1 = ball_first(ent, h1, road, rk1 != kKeyInf);
-    const uint4 e0 = ball_first(ent, h0, road, rk0 != kKeyInf);
-    r1 = ball_resolve(ent, h1, road, e1, rm);
-    r0 = ball_resolve(ent, h0, road, e0, rm);
+    // both first probes issued together: an unusable exit reads row 0 (valid: the mode has
+    // tables) and its row is replaced by the empty row afterwards
+    const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
+    const uint64_t i1 = u1 ? ball_row0(h1.x) + ball_slot(road, h1.y) : 0u;
+    const uint64_t i0 = u0 ? ball_row0(h0.x) + ball_slot(road, h0.y) : 0u;
+    const uint4 l1 = ent[i1], l0 = ent[i0];
+    const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+    r1 = ball_resolve(ent, h1, road, u1 ? l1 : none, rm);
+    r0 = ball_resolve(ent, h0, road, u0 ? l0 : none, rm);
   }
   __device__ unsigned long long operator()(uint32_t, uint32_t road, uint32_t side) const {
     uint4 r1, r0;
@@ -1492,22 +1517,30 @@ __device__ void path_walk_ball(const DevGraph& g, const DevBatch& b, uint64_t p,
 __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
+  // the slot's loads issued together (every slot < P holds a choice and a chain flag), the
+  // filters after them
   const uint32_t k = b.slot_trace[p];
-  const uint32_t o = b.trace_off[k];
+  const int8_t cj = b.choice[p], ci = b.choice[p ? p - 1 : 0];
+  const uint8_t cs = b.chain_start[p];
+  const uint32_t o = b.trace_off[k], S = b.n_states[k];
   const uint32_t s = (uint32_t)(p - o);
-  if (s < 1 || s >= b.n_states[k]) return;
-  if (b.chain_start[p] || b.choice[p] < 0) return;
+  if (s < 1 || s >= S || cs || cj < 0) return;
   const uint4 pi = b.pair_info[p];
   const int mode = (int)(pi.z >> 16);
   const uint32_t bound = pi.x;
-  const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
+  const uint32_t i = (uint32_t)ci, j = (uint32_t)cj;
   const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
   const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
   unsigned long long rk1, rk0;
   exit_keys(a0, bound, rk1, rk0);
   const bool fits = bound <= g.ball_radius[mode] && ((g.ball_mask >> mode) & 1u);
-  const uint2 h1 = fits && rk1 != kKeyInf ? g.ball_hdr[mode][a1.y] : make_uint2(0u, 1u);
-  const uint2 h0 = fits && rk0 != kKeyInf ? g.ball_hdr[mode][a1.x] : make_uint2(0u, 1u);
+  uint2 h1 = make_uint2(0u, 1u), h0 = h1;
+  if (fits) {   // both headers loaded together
+    const uint2* hp = g.ball_hdr[mode];
+    const uint2 x1 = hp[a1.y], x0 = hp[a1.x];
+    if (rk1 != kKeyInf) h1 = x1;
+    if (rk0 != kKeyInf) h0 = x0;
+  }
   if (!fits || h1.y == 0u || h0.y == 0u) {
     b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
     return;
