@@ -277,15 +277,19 @@ def extras(gpath, tr, json_traces, tmpdir):
     sm.MatchMany(reqs)        # cold: route balls, workspace, pinned staging and parse buffers grow once
     cold = time.perf_counter() - t
     cold_ms = sm.last_timing()
-    t = time.perf_counter()
-    outs = sm.MatchMany(reqs)  # steady state of a long-running service
-    dt = time.perf_counter() - t
+    runs = []
+    for _ in range(3):         # steady state of a long-running service: the median of three calls
+        t = time.perf_counter()
+        outs = sm.MatchMany(reqs)
+        runs.append((time.perf_counter() - t, sm.last_timing()))
+    runs.sort(key=lambda r: r[0])
+    dt, steady_ms = runs[1]
     out["json_boundary"] = {"what": "%d C2 traces (%d points, %.0f MB of /report JSON) through rm_match_batch: host "
                                     "JSON parse -> H2D -> every kernel -> D2H -> segment JSON" % (
                                         len(reqs), P, sum(map(len, reqs)) / 1e6),
                             "value": P / dt, "unit": "points/s", "seconds": dt, "json_build_s_untimed": build_s,
                             "reply_mb": sum(map(len, outs)) / 1e6, "host_threads": os.cpu_count() and min(16, os.cpu_count()),
-                            "library_ms": sm.last_timing(),
+                            "library_ms": steady_ms, "seconds_of_three_calls": [r[0] for r in runs],
                             "first_call": {"seconds": cold, "library_ms": cold_ms,
                                            "note": "the same call on a fresh matcher: buffers grow once"}}
     sm.close()

@@ -362,19 +362,20 @@ void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char**
   if (m->sinks.size() < nt) m->sinks.resize(nt);
   std::vector<tj::PointSink>& sink = m->sinks;
   std::vector<uint32_t> cnt(n), topt(n);
+  std::vector<size_t> len(n);
   std::vector<MatchOptions> opts(n);
   const Config& conf = *m->conf;
   pool.run(nt, [&](size_t t) {
     const size_t a = n * t / nt, b = n * (t + 1) / nt;
     size_t bytes = 0;
-    for (size_t i = a; i < b; ++i) bytes += std::strlen(traces[i]);
+    for (size_t i = a; i < b; ++i) bytes += len[i] = std::strlen(traces[i]);
     tj::PointSink& sk = sink[t];
     sk.clear();
     const size_t guess = bytes / 48 + 16;   // a /report point is ~60-90 bytes of JSON
     sk.lon.reserve(guess); sk.lat.reserve(guess); sk.acc.reserve(guess); sk.time.reserve(guess);
     for (size_t i = a; i < b; ++i) {
       const size_t before = sk.size();
-      opts[i] = tj::parse_request(traces[i], conf.mode_defaults, sk);
+      opts[i] = tj::parse_request(traces[i], len[i], conf.mode_defaults, sk);
       cnt[i] = (uint32_t)(sk.size() - before);
       topt[i] = (uint32_t)i;
     }

@@ -52,8 +52,8 @@ inline int mode_index(const char* s, size_t n) {
 
 class Reader {
  public:
-  Reader(const char* s, const MatchOptions* mode_defaults)
-      : p_(s), s0_(s), end_(s + std::strlen(s)), defaults_(mode_defaults) {}
+  Reader(const char* s, size_t len, const MatchOptions* mode_defaults)
+      : p_(s), s0_(s), end_(s + len), defaults_(mode_defaults) {}
 
   // Parse one request; its points are appended to `sink` (only when the request is valid).
   MatchOptions request(PointSink& sink) {
@@ -193,11 +193,7 @@ class Reader {
   // ---- numbers: the token is validated exactly as the DOM reader does, and converted to the
   // correctly rounded double (what strtod returns) without strtod in the common cases
   static bool digit(char c) { return (unsigned)(c - '0') < 10u; }
-  // eight ASCII digits at once (SWAR): all-digit test and their value
-  static bool eight_digits(uint64_t v) {
-    return (((v & 0xF0F0F0F0F0F0F0F0ull) | (((v + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull) >> 4)) ==
-            0x3333333333333333ull);
-  }
+  // the value of eight ASCII digits (SWAR; p_[0], the low byte, is the most significant)
   static uint32_t eight_value(uint64_t v) {
     v -= 0x3030303030303030ull;
     v = v * 10u + (v >> 8);
@@ -205,18 +201,55 @@ class Reader {
          (((v >> 16) & 0x000000FF000000FFull) * 0x0000271000000001ull)) >> 32;
     return (uint32_t)v;
   }
-  // digits at p_ into m (wrapping past 19 digits: the caller checks the count)
+  // digits at p_ into m (wrapping past 19 digits: the caller checks the count).  Eight bytes at
+  // a time: the run of digits at the front of the word is found from a per-byte non-digit mask
+  // and converted in one go (the bytes after it replaced by leading '0's), no loop per digit.
   void digits(uint64_t& m) {
+    static const uint64_t kPow10u[9] = {1u, 10u, 100u, 1000u, 10000u, 100000u, 1000000u, 10000000u, 100000000u};
     uint64_t v;
     while (end_ - p_ >= 8) {
       std::memcpy(&v, p_, 8);   // little-endian: p_[0] is the low byte
-      if (!eight_digits(v)) break;
-      m = m * 100000000u + eight_value(v);
-      p_ += 8;
+      const uint64_t a = v ^ 0x3030303030303030ull;   // a digit byte becomes 0..9
+      const uint64_t bad = (a & 0xF0F0F0F0F0F0F0F0ull) | (((a & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0x1010101010101010ull);
+      if (!bad) {
+        m = m * 100000000u + eight_value(v);
+        p_ += 8;
+        continue;
+      }
+      const unsigned n = (unsigned)__builtin_ctzll(bad) >> 3;   // digits before the first non-digit
+      if (n) {
+        m = m * kPow10u[n] + eight_value((v << (64 - 8 * n)) | (0x3030303030303030ull >> (8 * n)));
+        p_ += n;
+      }
+      return;
     }
     while (digit(*p_)) { m = m * 10u + (uint64_t)(*p_ - '0'); ++p_; }
   }
   double number() {
+    // the common token first — [-]digits[.digits], at most 15 digits, no exponent: one pass, one
+    // exact operation (Clinger); anything else (including every malformed token) is re-read by
+    // the general path below from the same start, so errors and values are the general path's
+    {
+      const char* q = p_;
+      const bool neg = *q == '-';
+      q += neg;
+      const char* d0 = q;
+      uint64_t m = 0;
+      while (digit(*q)) { m = m * 10u + (uint64_t)(*q - '0'); ++q; }
+      int nd = (int)(q - d0), fr = 0;
+      if (nd && *q == '.') {
+        const char* f0 = ++q;
+        while (digit(*q)) { m = m * 10u + (uint64_t)(*q - '0'); ++q; }
+        fr = (int)(q - f0);
+        nd = fr ? nd + fr : 99;
+      }
+      if (nd && nd <= 15 && *q != 'e' && *q != 'E') {
+        static const double kPow10s[16] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15};
+        p_ = q;
+        const double v = fr ? (double)m / kPow10s[fr] : (double)m;
+        return neg ? -v : v;
+      }
+    }
     const char* st = p_;
     const bool neg = *p_ == '-';
     p_ += neg;
@@ -434,8 +467,9 @@ class Reader {
     std::string tmp;
     for (;;) {
       ws();
-      if (*p_ == '{') point(sink, tmp);
-      else {
+      if (*p_ == '{') {
+        if (!point_compact(sink)) point(sink, tmp);
+      } else {
         skip(2);
         if (point_err_.empty()) point_err_ = "each trace point needs numeric lat and lon";
       }
@@ -444,6 +478,52 @@ class Reader {
       if (*p_ == ']') { ++p_; return; }
       fail("expected ',' or ']'");
     }
+  }
+
+  // The point layout json.dumps(separators=(',', ':')) writes, in any key order: exactly the
+  // keys lat, lon, time, accuracy, once each, unescaped, with number values and no whitespace.
+  // Anything else (another key, a repeat, a non-number, whitespace, an earlier failed point)
+  // rewinds to the '{' and takes the generic point() below, so the result, the validation and
+  // the error offsets are the generic path's: a number that fails here fails there at the same
+  // offset, since both reach it through the same bytes.
+  bool point_compact(PointSink& sink) {
+    if (!point_err_.empty()) return false;
+    const char* st = p_;
+    double v[4];
+    unsigned seen = 0;
+    ++p_;
+    auto lit = [&](const char* s, size_t n) {   // the text at p_ starts with s[0, n) (never reads past the NUL)
+      if ((size_t)(end_ - p_) < n || std::memcmp(p_, s, n) != 0) return false;
+      p_ += n;
+      return true;
+    };
+    for (;;) {
+      int k;
+      if (lit("\"lat\":", 6)) k = 0;
+      else if (lit("\"lon\":", 6)) k = 1;
+      else if (lit("\"time\":", 7)) k = 2;
+      else if (lit("\"accuracy\":", 11)) k = 3;
+      else break;
+      if (seen & (1u << k) || !(*p_ == '-' || digit(*p_))) break;
+      seen |= 1u << k;
+      v[k] = number();
+      if (*p_ == ',') { ++p_; continue; }
+      if (*p_ == '}' && seen == 15u) {
+        ++p_;
+        if (!(v[0] >= -90.0 && v[0] <= 90.0 && v[1] >= -180.0 && v[1] <= 180.0)) {
+          point_err_ = "trace point out of range";
+          return true;
+        }
+        sink.lat.push_back((float)v[0]);
+        sink.lon.push_back((float)v[1]);
+        sink.time.push_back(v[2]);
+        sink.acc.push_back((float)v[3]);
+        return true;
+      }
+      break;
+    }
+    p_ = st;
+    return false;
   }
 
   void point(PointSink& sink, std::string& tmp) {
@@ -495,7 +575,12 @@ class Reader {
 // trace's options (its mode's defaults with the request's match_options applied).  Throws with
 // the DOM reader's messages; on error nothing is appended.
 inline MatchOptions parse_request(const char* text, const MatchOptions mode_defaults[5], PointSink& sink) {
-  Reader r(text, mode_defaults);
+  Reader r(text, std::strlen(text), mode_defaults);
+  return r.request(sink);
+}
+// the same, with the text's length known (len = strlen(text): the NUL at text[len] ends it)
+inline MatchOptions parse_request(const char* text, size_t len, const MatchOptions mode_defaults[5], PointSink& sink) {
+  Reader r(text, len, mode_defaults);
   return r.request(sink);
 }
 

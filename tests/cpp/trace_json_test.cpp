@@ -263,6 +263,20 @@ int main() {
       "{\"a\":[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[[1]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]]],\"trace\":[{\"lat\":1,\"lon\":2}]}",
       "{\"s\":\"\\ud83d\\ude00\\n\\t\\\"\",\"trace\":[{\"lat\":1,\"lon\":2}]}", "{\"s\":\"\\x\"}", "{\"s\":\"ab", "",
       "{\"trace\":[{\"lat\":4.9e-324,\"lon\":123456789012345678}]}", "{\"trace\":[{\"lat\":1E+2,\"lon\":2e-0}]}",
+      // the compact point layout (trace_json.hpp point_compact) and its fall-backs
+      "{\"trace\":[{\"lat\":1.5,\"lon\":2,\"time\":3,\"accuracy\":4}]}",
+      "{\"trace\":[{\"accuracy\":4,\"time\":3.25,\"lon\":-2.125,\"lat\":-1.5}]}",
+      "{\"trace\":[{\"lat\":1,\"lon\":2,\"time\":3,\"accuracy\":4,\"lat\":5}]}",
+      "{\"trace\":[{\"lat\":1,\"lon\":2,\"time\":3,\"accuracy\":4,\"x\":5}]}",
+      "{\"trace\":[{\"lat\":1,\"lon\":2,\"time\":null,\"accuracy\":4}]}",
+      "{\"trace\":[{\"lat\":1,\"lon\":2,\"time\":3,\"accuracy\":4 }]}",
+      "{\"trace\":[{\"lat\":-,\"lon\":2,\"time\":3,\"accuracy\":4}]}",
+      "{\"trace\":[{\"lat\":1.,\"lon\":2,\"time\":3,\"accuracy\":4}]}",
+      "{\"trace\":[{\"lat\":1,\"lon\":2e1,\"time\":3,\"accuracy\":4}]}",
+      "{\"trace\":[{\"lat\":91,\"lon\":2,\"time\":3,\"accuracy\":4},{\"lat\":1,\"lon\":2,\"time\":3,\"accuracy\":4}]}",
+      "{\"trace\":[{\"lat\":1,\"lon\":2,\"time\":1234567890.12345,\"accuracy\":4}]}",
+      "{\"trace\":[{\"lat\":1,\"lon\":2,\"time\":1234567890.123456,\"accuracy\":4}]}",
+      "{\"trace\":[{\"lat\":1,\"lon\":2,\"time\":3,\"accuracy\":4}",
   };
   for (const char* c : cases) {
     const Parsed a = dom_parse(c, defaults), b = fast_parse(c, defaults, sink);
