@@ -1867,7 +1867,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     }
     const uint32_t excl = incl - dq.cnt;
     const uint32_t fit = (uint32_t)((__ballot(live && s0 + j < S && incl <= (uint32_t)kVitRoutes) >> gb) & 0xffffull);
-    const uint32_t C = live ? (uint32_t)__builtin_ctz(~fit | 0x10000u) : 0u;   // leading layers that fit
+    const uint32_t Cg = live ? (uint32_t)__builtin_ctz(~fit | 0x10000u) : 0x10000u;   // leading layers that fit
+    // every live group of the wave advances by the smallest of their chunk lengths, so no group
+    // idles through another's longer chunk (the routes staged past it are re-read next chunk)
+    uint32_t Cw = min(Cg, (uint32_t)__shfl_xor((int)Cg, 16));
+    Cw = min(Cw, (uint32_t)__shfl_xor((int)Cw, 32));
+    const uint32_t C = live ? Cw : 0u;
     const uint32_t nroutes = C ? (uint32_t)__shfl(incl, (int)C - 1, 16) : 0u;
     const uint32_t rbase = (uint32_t)__shfl(dq.off, 0, 16);                   // routes of layer s0 start here
     // ---- coalesced loads of the chunk's routes and emission rows
