@@ -512,9 +512,10 @@ def main():
                 "traces_rank0": T,
                 "points_all_ranks": int(total_points),
                 "graph": W.graph_info(gpath),
-                "parallelism": "uuid shard x%d (dist.shard_by_uuid), graph replicated, RCCL all-reduce of the %d x 16 "
+                "parallelism": "uuid shard x%d (dist.shard_by_uuid), graph replicated, %s all-reduce of the %d x 16 "
                                "u32 speed histogram and the per-segment u64 duration sums every step; per GPU the batch runs as %d concurrent part(s), one HIP "
-                               "stream each" % (world, nseg, max(1, a.streams)),
+                               "stream each" % (world, "host-transport (TCP)" if a.comm == "host" else "RCCL", nseg,
+                                                max(1, a.streams)),
             },
             "ms_allreduce": t_ar / steps * 1e3,
             "allreduce_bytes": nseg * 16 * 4 + nseg * 8,
