@@ -203,6 +203,17 @@ def test_valhalla_dropin_json(c1, tmpdir_session):
         sm.Match('{"uuid":"x","trace":[{"lat":1.0}]}')
     with pytest.raises(RuntimeError):
         sm.Match("not json")
+    # the packed batch path without coalescing: the same replies, one failing trace fails the call
+    sm.close()
+    conf = valhalla.write_config(str(tmpdir_session / "conf_nc.json"), path, device=0, coalesce=False)
+    valhalla.Configure(conf)
+    sm = valhalla.SegmentMatcher()
+    assert sm.MatchMany([json.dumps(r) for r in reqs]) == outs2
+    assert sm.MatchMany([json.dumps(reqs[0])]) == outs2[:1]
+    assert sm.MatchMany([]) == []
+    with pytest.raises(RuntimeError):
+        sm.MatchMany([json.dumps(reqs[0]), '{"uuid":"x","trace":[]}'])
+    sm.close()
 
 
 def test_rerun_is_deterministic(c1):
