@@ -200,6 +200,31 @@ char* dup_string(const std::string& s) {
   return p;
 }
 
+// pinned host staging of one matcher's batch arrays (grow-only): the parse threads copy their
+// points here and the engine's uploads run at full PCIe rate
+struct HostStaging {
+  float* lon = nullptr; float* lat = nullptr; float* acc = nullptr; double* time = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap) return;
+    release();
+    const size_t c = n + n / 4 + 4096;
+    RM_HIP(hipHostMalloc((void**)&lon, c * 4, hipHostMallocDefault));
+    RM_HIP(hipHostMalloc((void**)&lat, c * 4, hipHostMallocDefault));
+    RM_HIP(hipHostMalloc((void**)&acc, c * 4, hipHostMallocDefault));
+    RM_HIP(hipHostMalloc((void**)&time, c * 8, hipHostMallocDefault));
+    cap = c;
+  }
+  void release() {
+    for (void* q : {(void*)lon, (void*)lat, (void*)acc, (void*)time})
+      if (q) (void)hipHostFree(q);
+    lon = lat = acc = nullptr;
+    time = nullptr;
+    cap = 0;
+  }
+  ~HostStaging() { release(); }
+};
+
 // run a list of parsed traces as one batch on matcher m; per-trace JSON replies, and per-trace
 // error messages (non-empty = that trace failed alone; its reply is empty)
 // fn(i) for i in [0, n) over the host pool (up to 16 threads) in contiguous chunks (the JSON
@@ -225,18 +250,21 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
   std::vector<MatchOptions> opts(n);
   for (size_t i = 0; i < n; ++i) { off[i + 1] = off[i] + (uint32_t)pt[i]->pts.size(); opts[i] = pt[i]->opt; topt[i] = (uint32_t)i; }
   const uint64_t P = off[n];
-  std::vector<float> lon(P), lat(P), acc(P);
-  std::vector<double> tm(P);
+  // the dispatcher thread's pinned staging (grow-only): the batch's uploads run as DMA instead of
+  // staged pageable copies, which cost a small coalesced batch more than its kernels
+  static thread_local HostStaging staging;
+  HostStaging& hs = staging;   // the pool threads below must see this thread's instance
+  hs.ensure(P);
   parallel_for(n, [&](size_t i) {
     const tj::PointSink& q = pt[i]->pts;
-    std::copy(q.lon.begin(), q.lon.end(), lon.begin() + off[i]);
-    std::copy(q.lat.begin(), q.lat.end(), lat.begin() + off[i]);
-    std::copy(q.acc.begin(), q.acc.end(), acc.begin() + off[i]);
-    std::copy(q.time.begin(), q.time.end(), tm.begin() + off[i]);
+    std::copy(q.lon.begin(), q.lon.end(), hs.lon + off[i]);
+    std::copy(q.lat.begin(), q.lat.end(), hs.lat + off[i]);
+    std::copy(q.acc.begin(), q.acc.end(), hs.acc + off[i]);
+    std::copy(q.time.begin(), q.time.end(), hs.time + off[i]);
   });
   HostBatch hb;
-  hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = lon.data(); hb.lat = lat.data();
-  hb.time = tm.data(); hb.accuracy = acc.data(); hb.n_opts = (uint32_t)n; hb.opts = opts.data();
+  hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = hs.lon; hb.lat = hs.lat;
+  hb.time = hs.time; hb.accuracy = hs.acc; hb.n_opts = (uint32_t)n; hb.opts = opts.data();
   hb.trace_opt = topt.data();
   RunParams rp;
   rp.do_report = 0;
@@ -313,31 +341,6 @@ void Coalescer::loop() {
 }
 
 }  // namespace
-
-// pinned host staging of one matcher's batch arrays (grow-only): the parse threads copy their
-// points here and the engine's uploads run at full PCIe rate
-struct HostStaging {
-  float* lon = nullptr; float* lat = nullptr; float* acc = nullptr; double* time = nullptr;
-  size_t cap = 0;
-  void ensure(size_t n) {
-    if (n <= cap) return;
-    release();
-    const size_t c = n + n / 4 + 4096;
-    RM_HIP(hipHostMalloc((void**)&lon, c * 4, hipHostMallocDefault));
-    RM_HIP(hipHostMalloc((void**)&lat, c * 4, hipHostMallocDefault));
-    RM_HIP(hipHostMalloc((void**)&acc, c * 4, hipHostMallocDefault));
-    RM_HIP(hipHostMalloc((void**)&time, c * 8, hipHostMallocDefault));
-    cap = c;
-  }
-  void release() {
-    for (void* q : {(void*)lon, (void*)lat, (void*)acc, (void*)time})
-      if (q) (void)hipHostFree(q);
-    lon = lat = acc = nullptr;
-    time = nullptr;
-    cap = 0;
-  }
-  ~HostStaging() { release(); }
-};
 
 struct rm_matcher {
   std::shared_ptr<Config> conf;

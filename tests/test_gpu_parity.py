@@ -274,6 +274,46 @@ def test_coalesced_match_from_threads(c1, tmpdir_session):
     print("coalescing", st)
 
 
+def test_coalesced_large_batch(c1, tmpdir_session):
+    """80 requests released at once into a 200 ms coalescing window form batches larger than the
+    32 traces one host thread assembles, so the batch is gathered into the dispatcher's pinned
+    staging by several pool threads; every caller still gets its exact reply."""
+    import threading
+    import valhalla
+    path, g, eng = c1
+    conf = valhalla.write_config(str(tmpdir_session / "conf_coalesce_big.json"), path, device=0, coalesce=True,
+                                 coalesce_window_ms=200.0)
+    valhalla.Configure(conf)
+    n = 80
+    tr = world.generate_traces(path, n_traces=n, n_points=100, rate_s=1.0, noise_m=5.0, seed=62)
+    ref = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"],
+                               engine.default_options(1), np.zeros(n, np.uint32)))
+    reqs = [json.dumps(world.trace_to_request(tr, k), separators=(",", ":")) for k in range(n)]
+    out, errors = [None] * n, []
+    gate = threading.Barrier(n)
+
+    def worker(k):
+        try:
+            sm = valhalla.SegmentMatcher()
+            gate.wait()
+            out[k] = sm.Match(reqs[k])
+            sm.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errors, errors
+    for k in range(n):
+        want = engine.segment_dicts(ref["segs"][ref["seg_off"][k]:ref["seg_off"][k + 1]])
+        assert json.loads(out[k])["segments"] == want
+    st = valhalla.coalesce_stats()
+    assert st["max_batch"] > 32, st
+
+
 def test_randomised_options_per_trace(c1):
     """Every MatchOptions field varied per trace (one option row per trace), with mixed sampling
     rates and noise: the GPU against the oracle at every stage, and report() on top."""
