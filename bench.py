@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--parts-extra", type=int, default=2,
                     help="also time the batch as this many concurrent parts (engine.MultiMatcher), reported "
                          "beside the value as concurrent_parts (0 = skip; batches <= 20 M points)")
+    ap.add_argument("--exchange", choices=("allreduce", "reduce_scatter"), default="allreduce",
+                    help="allreduce: every rank ends with the whole histogram and duration sums; reduce_scatter: "
+                         "each rank ends with its segment-id range of them (SURVEY 8(e)'s option; half the bytes)")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="rccl: one rank per GPU over xGMI (the measured configuration); host: the same "
                          "collectives over TCP on the host (rm_comm_init_host), ranks may share a GPU -- a "
@@ -386,8 +389,11 @@ def main():
     # the batch as `streams` concurrent parts (engine.MultiMatcher: one HIP stream each), or one
     bm = engine.MultiMatcher(eng, a.streams) if a.streams > 1 else engine.BatchMatcher(eng)
     nseg = eng.n_segments
-    hist = dist.DeviceBuffer(nseg * 16 * 4)
-    dur = dist.DeviceBuffer(nseg * 8)   # per-segment duration sums, reduced with the counts
+    # reduce-scatter: buffers padded to world equal chunks of segment-id ranges (padding stays 0)
+    rs = a.exchange == "reduce_scatter"
+    ch, cd = (-(-nseg * 16 // world), -(-nseg // world)) if rs else (nseg * 16, nseg)
+    hist = dist.DeviceBuffer((ch * world if rs else nseg * 16) * 4)
+    dur = dist.DeviceBuffer((cd * world if rs else nseg) * 8)   # per-segment duration sums
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
     rp = dict(hist_dev=hist.ptr, dur_dev=dur.ptr, zero_hist=True)
     bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, None, **rp)
@@ -397,7 +403,12 @@ def main():
         _lib.check(_lib.lib().rm_device_synchronize())
 
     def allreduce():
-        if comm is not None:
+        if comm is None:
+            return
+        if rs:
+            comm.reduce_scatter(hist.ptr, ch, dist.U32, dist.SUM)
+            comm.reduce_scatter(dur.ptr, cd, dist.U64, dist.SUM)
+        else:
             comm.allreduce(hist.ptr, nseg * 16, dist.U32, dist.SUM)
             comm.allreduce(dur.ptr, nseg, dist.U64, dist.SUM)
 
@@ -442,8 +453,13 @@ def main():
     kt["routes"] = kt_live["routes"]
     total_points = comm.allreduce_host(P, dist.SUM) if comm is not None else P
     sizes = bm.sizes()
+    step()   # one more exchanged step: the totals below are of the reduced arrays
     hist_sum = int(hist.download().sum())
     dur_sum = int(dur.download(np.uint64).sum())
+    if rs and comm is not None:   # each rank holds its range: the totals are the sums of the ranges
+        hv, dv = hist.download(), dur.download(np.uint64)
+        hist_sum = int(comm.allreduce_host(float(hv[rank * ch:(rank + 1) * ch].sum()), dist.SUM))
+        dur_sum = int(comm.allreduce_host(float(dv[rank * cd:(rank + 1) * cd].sum()), dist.SUM))
     balls = eng.ball_stats(0)
     tiers = bm.route_tiers()
 
@@ -519,6 +535,7 @@ def main():
             },
             "ms_allreduce": t_ar / steps * 1e3,
             "allreduce_bytes": nseg * 16 * 4 + nseg * 8,
+            "exchange": a.exchange,
             "ms_matching_only": t_match / steps * 1e3,
             "value_matching_only": total_points * a.steps / t_match,
             "roofline": k2,

@@ -308,8 +308,14 @@ int rm_runner_tiles(rm_runner* r, const rm_tile_params* p, rm_comm* comm, char**
 int rm_comm_unique_id(uint8_t id_out[128]);
 rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device);
 void rm_comm_destroy(rm_comm* c);
-/* dtype: 0 u32, 1 u64, 2 f64; op: 0 sum, 1 max.  In place on a device buffer; blocks until done. */
+/* dtype: 0 u32, 1 u64, 2 f64; op: 0 sum, 1 max.  In place on a device buffer (a host buffer on a
+ * device -1 host-transport communicator); blocks until done. */
 int rm_comm_allreduce(rm_comm* c, void* dev_buf, size_t count, int dtype, int op);
+/* The optional exchange of SURVEY §8(e): each rank owns one segment-id range.  buf holds nranks
+ * chunks of count_per_rank elements; on return chunk `rank` holds the reduction of every rank's
+ * chunk `rank` (RCCL reduce-scatter, in place), the other chunks are unspecified.  Half the bytes
+ * per rank of an all-reduce; buffers as rm_comm_allreduce. */
+int rm_comm_reduce_scatter(rm_comm* c, void* buf, size_t count_per_rank, int dtype, int op);
 /* all-reduce of one host double (op as above) */
 int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op);
 int rm_comm_barrier(rm_comm* c);

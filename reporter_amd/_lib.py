@@ -137,6 +137,7 @@ PROTOTYPES = [
     ("rm_comm_init", P, [C.c_int, C.c_int, P, C.c_int]),
     ("rm_comm_destroy", None, [P]),
     ("rm_comm_allreduce", C.c_int, [P, P, C.c_size_t, C.c_int, C.c_int]),
+    ("rm_comm_reduce_scatter", C.c_int, [P, P, C.c_size_t, C.c_int, C.c_int]),
     ("rm_comm_allreduce_host_f64", C.c_int, [P, C.POINTER(C.c_double), C.c_int]),
     ("rm_comm_barrier", C.c_int, [P]),
     ("rm_comm_init_host", P, [C.c_int, C.c_int, P, P, C.c_int]),

@@ -1112,27 +1112,63 @@ void rm_comm_destroy(rm_comm* c) {
   delete c;
 }
 
+// host transport: reduce elements [lo, lo + count) of every rank's n-element buffer (gathered
+// whole) into dst; a device -1 communicator's buffers are host memory
+static void host_reduce_range(rm_comm* c, void* buf, size_t n, size_t lo, size_t count, int dtype, int op) {
+  const size_t es = dtype == 0 ? 4 : 8, bytes = es * n;
+  std::vector<uint8_t> mine(bytes);
+  if (c->device >= 0) {
+    RM_HIP(hipSetDevice(c->device));
+    RM_HIP(hipMemcpy(mine.data(), buf, bytes, hipMemcpyDeviceToHost));
+  } else if (bytes) {
+    std::memcpy(mine.data(), buf, bytes);
+  }
+  const std::vector<uint8_t> all = host_gather(c, mine.data(), bytes);
+  // rank r's element i sits at all[r * bytes + i * es]; reduce_ranks reads all + r * (count * es)
+  std::vector<uint8_t> part((size_t)c->nranks * count * es);
+  for (int r = 0; r < c->nranks; ++r)
+    if (count) std::memcpy(part.data() + (size_t)r * count * es, all.data() + (size_t)r * bytes + lo * es, count * es);
+  uint8_t* dst = mine.data() + lo * es;
+  if (dtype == 0) reduce_ranks((uint32_t*)dst, part.data(), count, c->nranks, op);
+  else if (dtype == 1) reduce_ranks((uint64_t*)dst, part.data(), count, c->nranks, op);
+  else reduce_ranks((double*)dst, part.data(), count, c->nranks, op);
+  if (!count) return;
+  if (c->device >= 0) RM_HIP(hipMemcpy((uint8_t*)buf + lo * es, dst, count * es, hipMemcpyHostToDevice));
+  else std::memcpy((uint8_t*)buf + lo * es, dst, count * es);
+}
+
 int rm_comm_allreduce(rm_comm* c, void* buf, size_t count, int dtype, int op) {
   return guarded([&] {
     if (!c) throw std::runtime_error("comm is NULL");
     if (dtype < 0 || dtype > 2 || op < 0 || op > 1) throw std::runtime_error("bad dtype / op");
     if (c->host_fn) {
-      if (c->device < 0) throw std::runtime_error("the communicator has no GPU");
-      const size_t es = dtype == 0 ? 4 : 8, bytes = es * count;
-      std::vector<uint8_t> mine(bytes);
-      RM_HIP(hipSetDevice(c->device));
-      RM_HIP(hipMemcpy(mine.data(), buf, bytes, hipMemcpyDeviceToHost));
-      const std::vector<uint8_t> all = host_gather(c, mine.data(), bytes);
-      if (dtype == 0) reduce_ranks((uint32_t*)mine.data(), all.data(), count, c->nranks, op);
-      else if (dtype == 1) reduce_ranks((uint64_t*)mine.data(), all.data(), count, c->nranks, op);
-      else reduce_ranks((double*)mine.data(), all.data(), count, c->nranks, op);
-      RM_HIP(hipMemcpy(buf, mine.data(), bytes, hipMemcpyHostToDevice));
+      host_reduce_range(c, buf, count, 0, count, dtype, op);
       return;
     }
     const ncclDataType_t dt = dtype == 0 ? ncclUint32 : (dtype == 1 ? ncclUint64 : ncclFloat64);
     const ncclRedOp_t ro = op == 0 ? ncclSum : ncclMax;
     RM_HIP(hipSetDevice(c->device));
     nccl_check(ncclAllReduce(buf, buf, count, dt, ro, c->comm, c->stream), "ncclAllReduce");
+    RM_HIP(hipStreamSynchronize(c->stream));
+  });
+}
+
+int rm_comm_reduce_scatter(rm_comm* c, void* buf, size_t count_per_rank, int dtype, int op) {
+  return guarded([&] {
+    if (!c) throw std::runtime_error("comm is NULL");
+    if (dtype < 0 || dtype > 2 || op < 0 || op > 1) throw std::runtime_error("bad dtype / op");
+    const size_t lo = (size_t)c->rank * count_per_rank, n = (size_t)c->nranks * count_per_rank;
+    if (c->host_fn) {
+      host_reduce_range(c, buf, n, lo, count_per_rank, dtype, op);
+      return;
+    }
+    const ncclDataType_t dt = dtype == 0 ? ncclUint32 : (dtype == 1 ? ncclUint64 : ncclFloat64);
+    const size_t es = dtype == 0 ? 4 : 8;
+    RM_HIP(hipSetDevice(c->device));
+    // in place: this rank's chunk of the nranks-chunk buffer receives the reduction
+    nccl_check(ncclReduceScatter(buf, (uint8_t*)buf + lo * es, count_per_rank, dt, op == 0 ? ncclSum : ncclMax, c->comm,
+                                 c->stream),
+               "ncclReduceScatter");
     RM_HIP(hipStreamSynchronize(c->stream));
   });
 }

@@ -218,7 +218,13 @@ class Comm:
             raise _lib.RmError(_lib.last_error())
 
     def allreduce(self, dev_ptr, count, dtype=U32, op=SUM):
+        """In place on a device buffer (host memory on a device -1 host-transport Comm)."""
         _lib.check(_lib.lib().rm_comm_allreduce(self._h, dev_ptr, count, dtype, op))
+
+    def reduce_scatter(self, ptr, count_per_rank, dtype=U32, op=SUM):
+        """ptr holds world_size chunks of count_per_rank elements; chunk `rank` receives the
+        reduction of every rank's chunk `rank` (each rank owns one segment-id range)."""
+        _lib.check(_lib.lib().rm_comm_reduce_scatter(self._h, ptr, count_per_rank, dtype, op))
 
     def allreduce_host(self, value, op=SUM):
         v = C.c_double(float(value))

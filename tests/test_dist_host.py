@@ -101,6 +101,17 @@ def _rank_main(rank, world, port, graph_path, rdzv, out_dir):
     res["sum"] = comm.allreduce_host(rank + 1.0, dist.SUM)
     res["max"] = comm.allreduce_host(10.0 * rank, dist.MAX)
     res["timed"] = bench.timed(lambda: time.sleep(0.05 * (rank + 1)), 3, comm, lambda: None)
+    # the data path of the exchange over the host transport (device -1: host buffers): the
+    # histogram all-reduce and the optional reduce-scatter by segment-id range
+    h = (np.arange(37, dtype=np.uint32) * 7 + rank * 1000).astype(np.uint32)
+    comm.allreduce(h.ctypes.data, h.size, dist.U32, dist.SUM)
+    res["ar"] = h.tolist()
+    d = (np.arange(2 * 5, dtype=np.uint64) * (rank + 3)).astype(np.uint64)
+    comm.reduce_scatter(d.ctypes.data, 5, dist.U64, dist.SUM)
+    res["rs"] = d[5 * rank:5 * rank + 5].tolist()
+    m = np.array([1.5 * rank, -2.0 * rank, 3.0], np.float64)
+    comm.allreduce(m.ctypes.data, 3, dist.F64, dist.MAX)
+    res["mx"] = m.tolist()
     # the tile exchange
     g = graphfile.load(graph_path)
     pts = _points(graph_path)
@@ -148,6 +159,11 @@ def test_world2_host_comm_timing_and_tile_exchange(small_world, tmp_path, built_
     r0, r1 = (json.load(open(str(tmp_path / ("rank%d.json" % r)))) for r in range(2))
     assert r0["rdzv"] == r1["rdzv"] and len(r0["rdzv"]) == 256
     assert r0["sum"] == r1["sum"] == 3.0 and r0["max"] == r1["max"] == 10.0
+    want_ar = (np.arange(37, dtype=np.uint64) * 14 + 1000).tolist()
+    assert r0["ar"] == r1["ar"] == want_ar
+    full = np.arange(10, dtype=np.uint64) * 3 + np.arange(10, dtype=np.uint64) * 4   # ranks 0 and 1
+    assert r0["rs"] == full[:5].tolist() and r1["rs"] == full[5:].tolist()
+    assert r0["mx"] == r1["mx"] == [1.5, 0.0, 3.0]
     # max over ranks: rank 1 sleeps 3 x 0.1 s, and both ranks report its clock
     assert r0["timed"] == r1["timed"] and 0.3 <= r0["timed"] < 2.0
     assert r0["rows_mine"] > 0 and r1["rows_mine"] > 0

@@ -40,12 +40,27 @@ def _match(path, pts, keep, comm=None):
                   inactivity=120, n_uuids=int(pts["uuid"].max()) + 1, hist_dev=hist.ptr, dur_dev=dur.ptr,
                   zero_hist=True)
     files = bm.tiles(privacy=2, comm=comm)
+    rs = None
     if comm is not None:
+        # the reduce-scatter exchange of the same counts: this rank's padded segment-id range
+        w = comm.world_size
+        ch = -(-nseg * 16 // w)
+        part = dist.DeviceBuffer(ch * w * 4)
+        part.upload(hist.download())
+        comm.reduce_scatter(part.ptr, ch, dist.U32, dist.SUM)
+        rs = part.download()[comm.rank * ch:(comm.rank + 1) * ch]
+        part.close()
         comm.allreduce(hist.ptr, nseg * 16, dist.U32, dist.SUM)
         comm.allreduce(dur.ptr, nseg, dist.U64, dist.SUM)
     h, d = hist.download(), dur.download(np.uint64)
     for x in (hist, dur, bm, eng):
         x.close()
+    if rs is not None:   # the range equals the all-reduced histogram's (zero past the last segment)
+        w = comm.world_size
+        ch = -(-nseg * 16 // w)
+        want = np.zeros(ch * w, np.uint32)
+        want[:nseg * 16] = h
+        np.testing.assert_array_equal(rs, want[comm.rank * ch:(comm.rank + 1) * ch])
     return files, h, d
 
 
