@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <cstddef>
+#include <cstdlib>
 #include <exception>
 #include <functional>
 #include <mutex>
@@ -18,9 +19,17 @@ namespace rm {
 
 class HostPool {
  public:
+  // min(16, hardware threads), or RM_HOST_THREADS (1..256) for a host with more cores to give
   static HostPool& get() {
-    static HostPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    static HostPool pool(default_size());
     return pool;
+  }
+  static unsigned default_size() {
+    if (const char* e = std::getenv("RM_HOST_THREADS")) {
+      const long v = std::strtol(e, nullptr, 10);
+      if (v >= 1 && v <= 256) return (unsigned)v;
+    }
+    return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   }
   size_t size() const { return workers_.size() + 1; }
 
