@@ -1927,7 +1927,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       double rm0[4];
 #pragma unroll
       for (int x = 0; x < 4; ++x) rm0[x] = rmn[x];
-      if (t + 1 < C) { KBn = gs.kb[t + 1]; reln = gs.rel[t + 1]; gcn = gs.gc[t + 1]; sqn = gs.sq[t + 1][j]; }
+      {   // next layer's parameters, unconditionally (past the chunk: stale entries, never used)
+        const uint32_t tn = min(t + 1u, (uint32_t)kVitChunk - 1u);
+        KBn = gs.kb[tn]; reln = gs.rel[tn]; gcn = gs.gc[tn]; sqn = gs.sq[tn][j];
+      }
       bool start = !prev_ok || (s > 0 && gcl > brk);
       double best = INF;
       int arg = -1;
@@ -1952,15 +1955,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
           if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
         wave_sync();
       }
-      if (t + 1 < C) {   // next layer's first route rows (after any re-staging above)
-        const double* dp = gs.route_m + reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
+      {   // next layer's first route rows (after any re-staging above); past the chunk the
+          // stale parameters keep the reads inside this group's LDS (never used)
+        const double* dp = gs.route_m + min(reln, (uint32_t)kVitRoutes - 1u) + min((uint32_t)j, KBn ? KBn - 1u : 0u);
+        const uint32_t kbs = min(KBn, (uint32_t)kMaxCand);
 #pragma unroll
-        for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
+        for (int x = 0; x < 4; ++x) rmn[x] = dp[x * kbs];
       }
       uint8_t* row = reinterpret_cast<uint8_t*>(&gs.bpo[t]);
       if (KB == 0) {
         row[j] = 255;
-        if (j == 0) gs.cs[t] = 1;
+        gs.cs[t] = 1;   // every lane of the group writes the same byte
         prev_ok = false;
         prevK = 0;
         cj = INF;
@@ -1973,7 +1978,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       else { nc = (j < (int)KB && arg >= 0) ? best + em : INF; bpj = arg >= 0 ? (uint32_t)arg : 255u; }
       cj = nc;
       row[j] = (uint8_t)bpj;
-      if (j == 0) gs.cs[t] = start ? 1 : 0;
+      gs.cs[t] = start ? 1 : 0;   // every lane of the group writes the same byte
       prev_ok = true;
       prevK = KB;
     }
