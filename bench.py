@@ -92,9 +92,11 @@ def _cpu_worker(block):
     off = tr["trace_off"].astype(np.int64)
     o0, o1 = off[lo], off[hi]
     sub_off = (off[lo:hi + 1] - o0).astype(np.uint32)
-    opts = default_options(1, search_radius=radius)
-    b = mo.Batch(sub_off, tr["lon"][o0:o1], tr["lat"][o0:o1], tr["time"][o0:o1], tr["accuracy"][o0:o1], opts,
-                 np.zeros(hi - lo, np.uint32))
+    if _CPU.get("opts") is not None:   # per-trace options (C5)
+        opts, topt = _CPU["opts"], np.ascontiguousarray(_CPU["trace_opt"][lo:hi], np.uint32)
+    else:
+        opts, topt = default_options(1, search_radius=radius), np.zeros(hi - lo, np.uint32)
+    b = mo.Batch(sub_off, tr["lon"][o0:o1], tr["lat"][o0:o1], tr["time"][o0:o1], tr["accuracy"][o0:o1], opts, topt)
     hist = np.zeros(len(g["seg_id"]) * 16, np.uint32)
     dur = np.zeros(len(g["seg_id"]), np.uint64)
     mo.prepare_path_counters(g)   # in-edge index of the path-walk counters, outside the timed region
@@ -105,7 +107,7 @@ def _cpu_worker(block):
     return dt, int(o1 - o0), nrep, mo.counters()
 
 
-def cpu_baseline_leg(graph_path, tr, search_radius, procs):
+def cpu_baseline_leg(graph_path, tr, search_radius, procs, opts=None, trace_opt=None):
     """The oracle (a C port of the matcher + report()) run as `procs` single-threaded
     processes over contiguous trace blocks (simple_reporter.split, py/simple_reporter.py:70-79).
     Must run before this process initialises the GPU (workers are forked)."""
@@ -114,7 +116,7 @@ def cpu_baseline_leg(graph_path, tr, search_radius, procs):
     from reporter_amd.dist import split
     # the engine's K1 grid (each file cell split f x f): same results, the item counts it reads
     g = graphfile.split_grid(graphfile.load(graph_path), graphfile.engine_grid_split(graph_path))
-    _CPU.update(graph=g, traces=tr, radius=search_radius)
+    _CPU.update(graph=g, traces=tr, radius=search_radius, opts=opts, trace_opt=trace_opt)
     mo.lib()  # load once in the parent; children inherit it
     T = len(tr["trace_off"]) - 1
     blocks = [(b[0], b[-1] + 1) for b in split(list(range(T)), procs) if len(b)]
@@ -352,7 +354,27 @@ def main():
     gpath = os.path.join(gdir, "reporter_bench_%s_%d_%d.rmg" % (a.config, os.getpid(), rank))
     W.build_world(gpath, cfg["rows"], cfg["cols"], cfg["block_m"], seed=1, cell_m=cfg["cell_m"])
     ids = shard_ids(a.config, n_per, cfg["n_points"], world, rank)
-    tr = W.generate_traces(gpath, 0, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=1000, ids=ids)
+    opts_all, trace_opt = None, None
+    if a.config == "C5":
+        # the C2 graph, traces split over auto / bicycle / pedestrian and
+        # sigma_z in {2, 4.07, 8, 16} with GPS noise sigma = sigma_z and radius max(50, 3 sigma_z);
+        # each (mode, sigma) group is a seeded set sharded by the same ids
+        from reporter_amd import engine as E
+        groups = [(m, sg) for m in ("auto", "bicycle", "pedestrian") for sg in (2.0, 4.07, 8.0, 16.0)]
+        opts_all = E.default_options(len(groups))
+        sets, tos = [], []
+        for q, (m, sg) in enumerate(groups):
+            opts_all[q]["mode"], opts_all[q]["sigma_z"] = W.MODES[m], sg
+            opts_all[q]["search_radius"] = max(50.0, 3.0 * sg)
+            gid = ids[ids % len(groups) == q]
+            if len(gid):
+                sets.append(W.generate_traces(gpath, 0, cfg["n_points"], cfg["rate_s"], sg, seed=5000 + q, mode=m,
+                                              ids=gid))
+                tos.append(np.full(len(gid), q, np.uint32))
+        tr = W.concat_traces(*sets)
+        trace_opt = np.concatenate(tos)
+    else:
+        tr = W.generate_traces(gpath, 0, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=1000, ids=ids)
     P = int(tr["trace_off"][-1])
     T = len(ids)
 
@@ -360,7 +382,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         procs = a.cpu_procs or min(16, os.cpu_count() or 1)
-        cpu = cpu_baseline_leg(gpath, tr, cfg["search_radius"], procs)
+        cpu = cpu_baseline_leg(gpath, tr, cfg["search_radius"], procs, opts_all, trace_opt)
 
     comm, comm_note, tcp = None, None, None
     if a.comm == "host":
@@ -394,9 +416,9 @@ def main():
     ch, cd = (-(-nseg * 16 // world), -(-nseg // world)) if rs else (nseg * 16, nseg)
     hist = dist.DeviceBuffer((ch * world if rs else nseg * 16) * 4)
     dur = dist.DeviceBuffer((cd * world if rs else nseg) * 8)   # per-segment duration sums
-    opts = engine.default_options(1, search_radius=cfg["search_radius"])
+    opts = opts_all if opts_all is not None else engine.default_options(1, search_radius=cfg["search_radius"])
     rp = dict(hist_dev=hist.ptr, dur_dev=dur.ptr, zero_hist=True)
-    bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, None, **rp)
+    bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt, **rp)
     cold_s = time.perf_counter() - t_up
 
     def sync():
@@ -433,7 +455,7 @@ def main():
     conc = None
     if a.parts_extra > 1 and a.streams == 1 and P <= 20_000_000:
         mm = engine.MultiMatcher(eng, a.parts_extra)
-        mm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, None, **rp)
+        mm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt, **rp)
         for _ in range(a.warmup):
             mm.rerun(**rp)
             allreduce()
@@ -523,7 +545,9 @@ def main():
             "config": {
                 "workload": "%s: %d traces x %d pts @%gs per GPU (uuid shard of one %d-trace seeded set), %dx%d grid "
                             "@%gm, radius %gm" % (a.config, n_per, cfg["n_points"], cfg["rate_s"], n_per * world,
-                                                 cfg["rows"], cfg["cols"], cfg["block_m"], cfg["search_radius"]),
+                                                 cfg["rows"], cfg["cols"], cfg["block_m"], cfg["search_radius"]) +
+                            ("; traces split over auto / bicycle / pedestrian x sigma_z {2, 4.07, 8, 16} (GPS noise "
+                             "sigma = sigma_z, radius max(50, 3 sigma_z))" if a.config == "C5" else ""),
                 "points_rank0": P,
                 "traces_rank0": T,
                 "points_all_ranks": int(total_points),
