@@ -174,18 +174,24 @@ __global__ void __launch_bounds__(64) k_states(DevBatch b) {
         }
         continue;
       }
-      bool s;
       if (last + 2 == ii) {
-        s = (B >> q) & 1ull;
-      } else {   // two or more skipped in a row: measure from the last state itself
-        float plo = llon, pla = llat;
-        if (last >= c0) { plo = lane_f(lo, last - c0); pla = lane_f(la, last - c0); }
-        const double dq = gc_distance(plo, pla, lane_f(lo, q), lane_f(la, q));
-        s = !(dq < interp);
-        if (lane == (int)q) dx = dq;
+        if ((B >> q) & 1ull) { st |= 1ull << q; last = ii; }
+        ++q;
+        continue;
       }
-      if (s) { st |= 1ull << q; last = ii; }
-      ++q;
+      // two or more skipped in a row: every remaining point of the chunk is measured from the
+      // last state at once (one vector distance, the same function the one-point test used);
+      // the first that is far enough is the next state, the ones before it are skipped
+      float plo = llon, pla = llat;
+      if (last >= c0) { plo = lane_f(lo, last - c0); pla = lane_f(la, last - c0); }
+      const double dv = gc_distance(plo, pla, lo, la);
+      const unsigned long long far = __ballot(act && !(dv < interp)) & (~0ull << q);
+      if (!far) { q = m; break; }   // the rest of the chunk is skipped
+      const uint32_t nq = (uint32_t)__builtin_ctzll(far);
+      st |= 1ull << nq;
+      last = c0 + nq;
+      if (lane == (int)nq) dx = dv;
+      q = nq + 1;
     }
     if ((st >> lane) & 1ull) {
       const unsigned long long below = st & ((1ull << lane) - 1ull);
