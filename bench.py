@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C2", help="C1..C5 (BASELINE.json configs); C2 is the metric's workload")
+    ap.add_argument("--config", default="C2", help="C1..C5 (BASELINE.json configs; C2 is the metric's workload), CITY / "
+                    "CITY30 (C2 / C3 workloads on the OSM-ingested city)")
     ap.add_argument("--traces", type=int, default=0, help="override traces per rank")
     ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (default min(16, cpus))")
     ap.add_argument("--streams", type=int, default=1,
@@ -352,7 +353,7 @@ def main():
     n_per = a.traces or cfg["n_traces"]
     gdir = os.environ.get("TMPDIR", "/tmp")
     gpath = os.path.join(gdir, "reporter_bench_%s_%d_%d.rmg" % (a.config, os.getpid(), rank))
-    W.build_world(gpath, cfg["rows"], cfg["cols"], cfg["block_m"], seed=1, cell_m=cfg["cell_m"])
+    W.build_config_graph(a.config, gpath, seed=1)
     ids = shard_ids(a.config, n_per, cfg["n_points"], world, rank)
     opts_all, trace_opt = None, None
     if a.config == "C5":
@@ -541,11 +542,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32 geometry / f64 Viterbi + times / u64 (dist,time) route keys",
-            "data": "synthetic (seeded perturbed-grid world + generate_test_trace.py-style noisy traces)",
+            "data": ("synthetic (seeded irregular city written as generic OSM PBF and ingested by rm_graph_import_osm + "
+                     "generate_test_trace.py-style noisy traces)" if cfg.get("city") else
+                     "synthetic (seeded perturbed-grid world + generate_test_trace.py-style noisy traces)"),
             "config": {
-                "workload": "%s: %d traces x %d pts @%gs per GPU (uuid shard of one %d-trace seeded set), %dx%d grid "
+                "workload": "%s: %d traces x %d pts @%gs per GPU (uuid shard of one %d-trace seeded set), %dx%d %s "
                             "@%gm, radius %gm" % (a.config, n_per, cfg["n_points"], cfg["rate_s"], n_per * world,
-                                                 cfg["rows"], cfg["cols"], cfg["block_m"], cfg["search_radius"]) +
+                                                 cfg["rows"], cfg["cols"],
+                                                 "junction OSM city" if cfg.get("city") else "grid", cfg["block_m"],
+                                                 cfg["search_radius"]) +
                             ("; traces split over auto / bicycle / pedestrian x sigma_z {2, 4.07, 8, 16} (GPS noise "
                              "sigma = sigma_z, radius max(50, 3 sigma_z))" if a.config == "C5" else ""),
                 "points_rank0": P,

@@ -97,6 +97,24 @@ int rm_graph_export_osm(const char* graph_path, const char* osm_path);
 int rm_graph_export_pbf(const char* graph_path, const char* pbf_path);
 /* OSM XML or PBF (told apart by content) -> .rmg. */
 int rm_graph_import_osm(const char* osm_path, const char* graph_path, double cell_m);
+/* A seeded irregular city written as generic OSM (osm_city.cpp), with no reporter:* tags, so
+ * rm_graph_import_osm ingests it as it would an extract: a jittered junction lattice of curved
+ * multi-vertex ways, diagonal avenues crossing at 9-road hubs, roundabouts, boulevards of one-way
+ * carriageway pairs, one-way streets, dead ends, service loops, foot / cycle paths, a trunk road
+ * on bridges joined at ramps, type=osmlr relations on part of the ways only, OSM ids in shuffled
+ * chunks.  pbf != 0 writes PBF, else XML (the same elements). */
+typedef struct {
+  uint32_t rows, cols;
+  double block_m;
+  uint64_t seed;
+  double center_lat, center_lon, jitter;
+  uint32_t primary_every, secondary_every, boulevard_every, diagonal_every;
+  double roundabout_frac, drop_frac, oneway_frac, spur_frac, service_frac, footway_frac, osmlr_local_frac,
+      way_max_m;
+  uint32_t trunk;
+} rm_city_params;
+void rm_default_city_params(rm_city_params* p);
+int rm_osm_city_write(const rm_city_params* p, const char* osm_path, int pbf);
 
 typedef struct {
   uint32_t n_traces, n_points;

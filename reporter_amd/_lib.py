@@ -30,6 +30,16 @@ class RmWorldParams(C.Structure):
                 ("curve_frac", C.c_double), ("cell_m", C.c_double)]
 
 
+class RmCityParams(C.Structure):
+    _fields_ = [("rows", C.c_uint32), ("cols", C.c_uint32), ("block_m", C.c_double), ("seed", C.c_uint64),
+                ("center_lat", C.c_double), ("center_lon", C.c_double), ("jitter", C.c_double),
+                ("primary_every", C.c_uint32), ("secondary_every", C.c_uint32), ("boulevard_every", C.c_uint32),
+                ("diagonal_every", C.c_uint32), ("roundabout_frac", C.c_double), ("drop_frac", C.c_double),
+                ("oneway_frac", C.c_double), ("spur_frac", C.c_double), ("service_frac", C.c_double),
+                ("footway_frac", C.c_double), ("osmlr_local_frac", C.c_double), ("way_max_m", C.c_double),
+                ("trunk", C.c_uint32)]
+
+
 class RmTraceParams(C.Structure):
     _fields_ = [("n_traces", C.c_uint32), ("n_points", C.c_uint32), ("rate_s", C.c_double),
                 ("noise_m", C.c_double), ("seed", C.c_uint64), ("mode", C.c_int32), ("start_epoch", C.c_int64),
@@ -88,6 +98,8 @@ PROTOTYPES = [
     ("rm_graph_export_osm", C.c_int, [C.c_char_p, C.c_char_p]),
     ("rm_graph_export_pbf", C.c_int, [C.c_char_p, C.c_char_p]),
     ("rm_graph_import_osm", C.c_int, [C.c_char_p, C.c_char_p, C.c_double]),
+    ("rm_default_city_params", None, [C.POINTER(RmCityParams)]),
+    ("rm_osm_city_write", C.c_int, [C.POINTER(RmCityParams), C.c_char_p, C.c_int]),
     ("rm_default_trace_params", None, [C.POINTER(RmTraceParams)]),
     ("rm_traces_generate", C.c_int, [C.c_char_p, C.POINTER(RmTraceParams), P, P, P, P, P, P]),
     ("rm_traces_generate_ids", C.c_int, [C.c_char_p, C.POINTER(RmTraceParams), P, P, P, P, P, P, P]),

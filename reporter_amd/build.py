@@ -19,7 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libreporter_match.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-SOURCES = ["engine.hip", "stages.hip", "capi.cpp", "graph.cpp", "graph_osm.cpp", "osm_pbf.cpp", "world.cpp", "balls.cpp"]
+SOURCES = ["engine.hip", "stages.hip", "capi.cpp", "graph.cpp", "graph_osm.cpp", "osm_pbf.cpp", "osm_city.cpp", "world.cpp", "balls.cpp"]
 HEADERS = ["engine.hpp", "graph.hpp", "json.hpp", "rm_common.hpp", "balls.hpp", "serve_policy.hpp", "trace_json.hpp",
            "host_pool.hpp", "osm_model.hpp"]
 

@@ -27,6 +27,7 @@
 #include "graph.hpp"
 #include "host_pool.hpp"
 #include "json.hpp"
+#include "osm_model.hpp"
 #include "serve_policy.hpp"
 #include "trace_json.hpp"
 
@@ -649,6 +650,33 @@ int rm_graph_import_osm(const char* osm_path, const char* graph_path, double cel
   return guarded([&] {
     if (!graph_path || !osm_path) throw std::runtime_error("path is NULL");
     import_osm(osm_path, cell_m).save(graph_path);
+  });
+}
+
+void rm_default_city_params(rm_city_params* p) {
+  const CityParams d;
+  p->rows = d.rows; p->cols = d.cols; p->block_m = d.block_m; p->seed = d.seed;
+  p->center_lat = d.center_lat; p->center_lon = d.center_lon; p->jitter = d.jitter;
+  p->primary_every = d.primary_every; p->secondary_every = d.secondary_every;
+  p->boulevard_every = d.boulevard_every; p->diagonal_every = d.diagonal_every;
+  p->roundabout_frac = d.roundabout_frac; p->drop_frac = d.drop_frac; p->oneway_frac = d.oneway_frac;
+  p->spur_frac = d.spur_frac; p->service_frac = d.service_frac; p->footway_frac = d.footway_frac;
+  p->osmlr_local_frac = d.osmlr_local_frac; p->way_max_m = d.way_max_m; p->trunk = d.trunk;
+}
+
+int rm_osm_city_write(const rm_city_params* p, const char* osm_path, int pbf) {
+  return guarded([&] {
+    if (!p || !osm_path) throw std::runtime_error("params or path is NULL");
+    CityParams c;
+    c.rows = p->rows; c.cols = p->cols; c.block_m = p->block_m; c.seed = p->seed;
+    c.center_lat = p->center_lat; c.center_lon = p->center_lon; c.jitter = p->jitter;
+    c.primary_every = p->primary_every; c.secondary_every = p->secondary_every;
+    c.boulevard_every = p->boulevard_every; c.diagonal_every = p->diagonal_every;
+    c.roundabout_frac = p->roundabout_frac; c.drop_frac = p->drop_frac; c.oneway_frac = p->oneway_frac;
+    c.spur_frac = p->spur_frac; c.service_frac = p->service_frac; c.footway_frac = p->footway_frac;
+    c.osmlr_local_frac = p->osmlr_local_frac; c.way_max_m = p->way_max_m; c.trunk = p->trunk;
+    std::unique_ptr<OsmSink> sink = pbf ? make_osm_pbf_sink(osm_path) : make_osm_xml_sink(osm_path);
+    write_osm_city(c, *sink);
   });
 }
 

@@ -250,7 +250,10 @@ void derive_info(const std::map<std::string, std::string>& t, uint32_t& info_f, 
   if (foot_only) a |= kAccessPedestrian;
   uint32_t af = a, ar = a;
   const std::string* ow = tag(t, "oneway");
-  if (ow && (*ow == "yes" || *ow == "true" || *ow == "1")) ar &= kAccessPedestrian;
+  // a roundabout is one-way in its drawing direction unless tagged otherwise (OSM convention)
+  const std::string* jc = tag(t, "junction");
+  const bool ring = jc && (*jc == "roundabout" || *jc == "circular") && !(ow && *ow == "no");
+  if (ring || (ow && (*ow == "yes" || *ow == "true" || *ow == "1"))) ar &= kAccessPedestrian;
   else if (ow && *ow == "-1") af &= kAccessPedestrian;
   uint32_t flags = 0;
   if (hw == "service") flags |= kFlagService;
@@ -347,6 +350,8 @@ void export_osm(const Graph& g, const std::string& path) {
   XmlSink x(path);
   emit_osm(g, x);
 }
+
+std::unique_ptr<OsmSink> make_osm_xml_sink(const std::string& path) { return std::make_unique<XmlSink>(path); }
 
 OsmParsed parse_osm_xml(const std::string& path) {
   std::string x;

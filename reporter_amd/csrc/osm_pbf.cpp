@@ -294,6 +294,8 @@ void export_osm_pbf(const Graph& g, const std::string& path) {
   emit_osm(g, s);
 }
 
+std::unique_ptr<OsmSink> make_osm_pbf_sink(const std::string& path) { return std::make_unique<PbfSink>(path); }
+
 // ---------------------------------------------------------------- reader
 OsmParsed parse_osm_pbf(const std::string& path) {
   FILE* f = std::fopen(path.c_str(), "rb");

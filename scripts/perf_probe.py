@@ -16,7 +16,7 @@ if a.traces:
 os.makedirs("/tmp/rmprobe", exist_ok=True)
 gp = "/tmp/rmprobe/%s.rmg" % a.config
 t = time.time()
-world.build_world(gp, c["rows"], c["cols"], c["block_m"], seed=1, cell_m=c["cell_m"])
+world.build_config_graph(a.config, gp, seed=1)
 print("world", world.graph_info(gp), "%.1fs" % (time.time() - t), flush=True)
 t = time.time()
 tr = world.generate_traces(gp, c["n_traces"], c["n_points"], c["rate_s"], c["noise_m"], seed=7)

@@ -128,3 +128,59 @@ def truth_recovery(trace_off, n_states, state_orig, cand_road, choice, truth_edg
     chosen = np.asarray(cand_road).reshape(-1, 16)[slots[ok], ch[ok]]
     hit = int((chosen == truth_road[pts[ok]]).sum())
     return hit / max(int(ok.sum()), 1), int(ok.sum()), len(slots)
+
+
+def match_and_compare(path, tr, opts, trace_opt, rl=(0, 1), tl=(0, 1), hist=False, ball_radius=None, keep_ref=False):
+    """Run the engine on a trace set and compare every stage, report() and (hist) the speed
+    histogram and duration sums with the oracle; returns compare_all's counts plus tiers."""
+    import ctypes
+
+    import meili_oracle as mo
+    from reporter_amd import _lib, engine, graphfile
+    g = graphfile.load(path)
+    eng = engine.Engine(path, 0)
+    if ball_radius is not None:
+        eng.set_ball_radius(ball_radius)
+    T = len(tr["trace_off"]) - 1
+    if trace_opt is None:
+        trace_opt = np.zeros(T, np.uint32)
+    nseg = eng.n_segments
+    dptr, uptr = ctypes.c_void_p(), ctypes.c_void_p()
+    rp = dict(report_levels=rl, transition_levels=tl)
+    if hist:
+        _lib.check(_lib.lib().rm_device_alloc(nseg * 16 * 4, ctypes.byref(dptr)))
+        _lib.check(_lib.lib().rm_device_alloc(nseg * 8, ctypes.byref(uptr)))
+        rp.update(hist_dev=dptr.value, dur_dev=uptr.value, zero_hist=True)
+    try:
+        bm = engine.BatchMatcher(eng)
+        bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt, **rp)
+        if hist:
+            got_hist = np.empty(nseg * 16, np.uint32)
+            _lib.check(_lib.lib().rm_device_download(got_hist.ctypes.data, dptr, got_hist.nbytes))
+            got_dur = np.empty(nseg, np.uint64)
+            _lib.check(_lib.lib().rm_device_download(got_dur.ctypes.data, uptr, got_dur.nbytes))
+    finally:
+        if hist:
+            _lib.lib().rm_device_free(dptr)
+            _lib.lib().rm_device_free(uptr)
+    batch = mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt)
+    ref = mo.match(g, batch)
+    c = compare_all(bm, ref, tr["trace_off"])
+    c["reports"] = check_reports(bm, ref, tr, rl=rl, tl=tl)
+    if hist:
+        want = np.zeros(nseg * 16, np.uint32)
+        want_dur = np.zeros(nseg, np.uint64)
+        nvalid = mo.pipeline(g, batch, 15.0, engine.levels_mask(rl), engine.levels_mask(tl), want, want_dur)
+        np.testing.assert_array_equal(got_hist, want, "speed histogram")
+        np.testing.assert_array_equal(got_dur, want_dur, "per-segment duration sums")
+        assert int(got_dur.sum()) > 0
+        assert int(got_hist.sum()) == nvalid
+        c["valid_reports"] = nvalid
+    c["traces"] = T
+    c["route_tiers"] = bm.route_tiers()
+    c["ball_stats"] = eng.ball_stats(0)
+    if keep_ref:
+        c["_ref"] = ref
+    bm.close()
+    eng.close()
+    return c

@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 
 from reporter_amd import _lib, dist, engine, world
-from test_gpu_fullsize import _match_and_compare
+from parity_util import match_and_compare
 
 pytestmark = pytest.mark.gpu
 
@@ -46,7 +46,7 @@ def test_c4_full_graph(c4_graph, ball_radius):
     tr = world.generate_traces(path, 3000, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=4000)
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
     t = time.time()
-    c = _match_and_compare(path, tr, opts, None, hist=True, ball_radius=ball_radius)
+    c = match_and_compare(path, tr, opts, None, hist=True, ball_radius=ball_radius)
     assert c["ball_stats"]["radius_m"] == (ball_radius or auto.value)
     assert c["segments"] > 30_000 and c["valid_reports"] > 10_000, c
     print("C4 full graph, radius", ball_radius or "auto", "%.1fs" % (time.time() - t), c, flush=True)

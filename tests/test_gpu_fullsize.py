@@ -10,14 +10,11 @@ histogram and the per-segment duration sums must equal the
 CPU pipeline's.  C3/C4/C5 check bounded trace
 samples (the oracle's long 30 s searches run ~8k points/s on one core).
 """
-import ctypes
-
 import numpy as np
 import pytest
 
-import meili_oracle as mo
-from parity_util import check_reports, compare_all
-from reporter_amd import _lib, engine, graphfile, world
+from parity_util import match_and_compare
+from reporter_amd import engine, world
 
 pytestmark = pytest.mark.gpu
 
@@ -29,61 +26,13 @@ def _world(tmpdir_session, name, rows=None, cols=None):
     return path, cfg
 
 
-def _match_and_compare(path, tr, opts, trace_opt, rl=(0, 1), tl=(0, 1), hist=False, ball_radius=None):
-    g = graphfile.load(path)
-    eng = engine.Engine(path, 0)
-    if ball_radius is not None:
-        eng.set_ball_radius(ball_radius)
-    T = len(tr["trace_off"]) - 1
-    if trace_opt is None:
-        trace_opt = np.zeros(T, np.uint32)
-    nseg = eng.n_segments
-    dptr, uptr = ctypes.c_void_p(), ctypes.c_void_p()
-    rp = dict(report_levels=rl, transition_levels=tl)
-    if hist:
-        _lib.check(_lib.lib().rm_device_alloc(nseg * 16 * 4, ctypes.byref(dptr)))
-        _lib.check(_lib.lib().rm_device_alloc(nseg * 8, ctypes.byref(uptr)))
-        rp.update(hist_dev=dptr.value, dur_dev=uptr.value, zero_hist=True)
-    try:
-        bm = engine.BatchMatcher(eng)
-        bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt, **rp)
-        if hist:
-            got_hist = np.empty(nseg * 16, np.uint32)
-            _lib.check(_lib.lib().rm_device_download(got_hist.ctypes.data, dptr, got_hist.nbytes))
-            got_dur = np.empty(nseg, np.uint64)
-            _lib.check(_lib.lib().rm_device_download(got_dur.ctypes.data, uptr, got_dur.nbytes))
-    finally:
-        if hist:
-            _lib.lib().rm_device_free(dptr)
-            _lib.lib().rm_device_free(uptr)
-    batch = mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, trace_opt)
-    ref = mo.match(g, batch)
-    c = compare_all(bm, ref, tr["trace_off"])
-    c["reports"] = check_reports(bm, ref, tr, rl=rl, tl=tl)
-    if hist:
-        want = np.zeros(nseg * 16, np.uint32)
-        want_dur = np.zeros(nseg, np.uint64)
-        nvalid = mo.pipeline(g, batch, 15.0, engine.levels_mask(rl), engine.levels_mask(tl), want, want_dur)
-        np.testing.assert_array_equal(got_hist, want, "speed histogram")
-        np.testing.assert_array_equal(got_dur, want_dur, "per-segment duration sums")
-        assert int(got_dur.sum()) > 0
-        assert int(got_hist.sum()) == nvalid
-        c["valid_reports"] = nvalid
-    c["traces"] = T
-    c["route_tiers"] = bm.route_tiers()
-    c["ball_stats"] = eng.ball_stats(0)
-    bm.close()
-    eng.close()
-    return c
-
-
 @pytest.mark.timeout(400)
 def test_c2_full_bench_workload(built_lib, tmpdir_session):
     """C2 exactly as bench.py rank 0 runs it: all 10,000 trajectories bit-exact."""
     path, cfg = _world(tmpdir_session, "C2")
     tr = world.generate_traces(path, cfg["n_traces"], cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=1000)
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
-    c = _match_and_compare(path, tr, opts, None, hist=True)
+    c = match_and_compare(path, tr, opts, None, hist=True)
     assert c["points"] == 6_000_000 and c["segments"] > 200_000 and c["valid_reports"] > 50_000, c
     print("C2 full parity", c)
 
@@ -95,7 +44,7 @@ def test_c3_full_graph_sample(built_lib, tmpdir_session, ball_radius):
     path, cfg = _world(tmpdir_session, "C3")
     tr = world.generate_traces(path, 1500, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=3000)
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
-    c = _match_and_compare(path, tr, opts, None, hist=True, ball_radius=ball_radius)
+    c = match_and_compare(path, tr, opts, None, hist=True, ball_radius=ball_radius)
     assert c["chained"] > 40_000, c
     assert (c["route_tiers"]["ball_to_search"] == 0) == (ball_radius >= 2000.0), c
     print("C3 sample parity", c)
@@ -106,7 +55,7 @@ def test_c4_country_slice_sample(built_lib, tmpdir_session):
     path, cfg = _world(tmpdir_session, "C4", rows=1000, cols=1000)
     tr = world.generate_traces(path, 2000, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=4000)
     opts = engine.default_options(1, search_radius=cfg["search_radius"])
-    c = _match_and_compare(path, tr, opts, None, hist=True, ball_radius=cfg["ball_radius_m"])
+    c = match_and_compare(path, tr, opts, None, hist=True, ball_radius=cfg["ball_radius_m"])
     assert c["segments"] > 20_000, c
     print("C4 slice parity", c)
 
@@ -126,6 +75,6 @@ def test_c5_full_graph_modes_sigma(built_lib, tmpdir_session):
     tr["trace_off"] = (np.arange(len(parts) * per + 1) * cfg["n_points"]).astype(np.uint32)
     trace_opt = np.repeat(np.arange(len(parts), dtype=np.uint32), per)
     opts = np.array(opts, engine.OPTIONS_DTYPE)
-    c = _match_and_compare(path, tr, opts, trace_opt, rl=(0, 1, 2), tl=(0, 1, 2), hist=True)
+    c = match_and_compare(path, tr, opts, trace_opt, rl=(0, 1, 2), tl=(0, 1, 2), hist=True)
     assert c["traces"] == 1200 and c["segments"] > 10_000, c
     print("C5 parity", c)
