@@ -412,9 +412,11 @@ def main():
     # the batch as `streams` concurrent parts (engine.MultiMatcher: one HIP stream each), or one
     bm = engine.MultiMatcher(eng, a.streams) if a.streams > 1 else engine.BatchMatcher(eng)
     nseg = eng.n_segments
-    # reduce-scatter: buffers padded to world equal chunks of segment-id ranges (padding stays 0)
+    # reduce-scatter: buffers padded to world equal chunks of whole segment-id ranges (padding
+    # stays 0): each rank owns cd segments, i.e. 16 * cd histogram bins (never a split segment)
     rs = a.exchange == "reduce_scatter"
-    ch, cd = (-(-nseg * 16 // world), -(-nseg // world)) if rs else (nseg * 16, nseg)
+    cd = -(-nseg // world) if rs else nseg
+    ch = 16 * cd
     hist = dist.DeviceBuffer((ch * world if rs else nseg * 16) * 4)
     dur = dist.DeviceBuffer((cd * world if rs else nseg) * 8)   # per-segment duration sums
     opts = opts_all if opts_all is not None else engine.default_options(1, search_radius=cfg["search_radius"])

@@ -332,7 +332,8 @@ int rm_comm_allreduce(rm_comm* c, void* dev_buf, size_t count, int dtype, int op
 /* The optional exchange of SURVEY §8(e): each rank owns one segment-id range.  buf holds nranks
  * chunks of count_per_rank elements; on return chunk `rank` holds the reduction of every rank's
  * chunk `rank` (RCCL reduce-scatter, in place), the other chunks are unspecified.  Half the bytes
- * per rank of an all-reduce; buffers as rm_comm_allreduce. */
+ * per rank of an all-reduce; buffers as rm_comm_allreduce.  For the speed histogram (16 bins per
+ * segment) count_per_rank must be 16 x the segments per rank, so no segment's bins are split. */
 int rm_comm_reduce_scatter(rm_comm* c, void* buf, size_t count_per_rank, int dtype, int op);
 /* all-reduce of one host double (op as above) */
 int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op);

@@ -476,6 +476,22 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
       conf->mode_defaults[m].mode = m;
       if (meili) apply_options(meili->get(kModeNames[m]), conf->mode_defaults[m]);
     }
+    // meili's turn costs are not implemented: a configured non-zero turn_penalty_factor (the stock
+    // valhalla_build_config sets 200 / 140 / 100 for auto / bicycle / pedestrian) fails Configure
+    // unless the operator accepts zero turn costs with reporter_amd.ignore_turn_penalty
+    bool ignore_turn = false;
+    if (const json::Value* ra = v.get("reporter_amd"))
+      if (const json::Value* it = ra->get("ignore_turn_penalty"); it && it->type == json::Value::Bool) ignore_turn = it->b;
+    for (int m = 0; m < 5; ++m) {
+      if (conf->mode_defaults[m].turn_penalty_factor == 0.f) continue;
+      if (!ignore_turn)
+        throw std::runtime_error(std::string("meili ") + kModeNames[m] + " turn_penalty_factor is " +
+                                 std::to_string(conf->mode_defaults[m].turn_penalty_factor) +
+                                 ": this matcher does not implement turn costs; configure 0 (valhalla_build_config "
+                                 "--meili-" + kModeNames[m] + "-turn-penalty-factor 0) or set "
+                                 "reporter_amd.ignore_turn_penalty to true to match without them");
+      conf->mode_defaults[m].turn_penalty_factor = 0.f;
+    }
     std::string graph;
     int device = g_device;
     if (const json::Value* ra = v.get("reporter_amd")) {
@@ -505,11 +521,12 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
       if (const json::Value* wk = ra->get("coalesce_workers"); wk && wk->is_num()) workers = (int)wk->num;
     }
     // travel modes whose route tables are built now, so no request waits for a build (the Java
-    // caller gives up after 10 s, HttpClient.java:80-87): auto (the default mode), every mode
-    // with its own meili section, and reporter_amd.modes
+    // caller gives up after 10 s, HttpClient.java:80-87): auto (the default mode) and the modes
+    // reporter_amd.modes lists.  Other modes build on their first request (time
+    // and HBM per mode).  The stock meili config has auto / bicycle / pedestrian sections, so
+    // building every mode with a section would cost up to half the HBM at startup for modes a
+    // deployment may never see.
     uint32_t modes = 1u << kModeAuto;
-    for (int m = 0; m < 5; ++m)
-      if (meili && meili->get(kModeNames[m])) modes |= 1u << m;
     if (const json::Value* ra = v.get("reporter_amd")) {
       if (const json::Value* ml = ra->get("modes")) {
         if (ml->type != json::Value::Array) throw std::runtime_error("reporter_amd.modes must be a list of mode names");

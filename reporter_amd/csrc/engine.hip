@@ -3336,6 +3336,7 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
     // K3 divides by both (a zero 1/beta would turn an invalid route's +inf into NaN)
     if (!(hb.opts[q].sigma_z > 0.f) || !std::isfinite(hb.opts[q].sigma_z)) throw std::runtime_error("sigma_z must be positive and finite");
     if (!(hb.opts[q].beta > 0.f) || !std::isfinite(hb.opts[q].beta)) throw std::runtime_error("beta must be positive and finite");
+    if (!(hb.opts[q].turn_penalty_factor == 0.f)) throw std::runtime_error(kTurnPenaltyError);
     mode_mask_ |= 1u << hb.opts[q].mode;
   }
   ensure(P, T, hb.n_opts);
@@ -3690,12 +3691,30 @@ void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, 
   RM_HIP(hipSetDevice(eng_->device()));
   const size_t offb = ((size_t)T + 1) * 4;
   // pinned: [0, offb) the counts then offsets, then the compacted records
+  // The buffers grow by half again (or to the need).  The old buffer is released first and the
+  // pointer / size pair only records a buffer that exists, so a failed allocation leaves (null, 0)
+  // and the next call allocates again; running out of memory here is a batch too large for the
+  // device, which the coalescer splits (serve_policy.hpp), not a generic error.
   auto grow_host = [&](size_t need) {
     if (need <= dl_host_bytes_) return;
+    const size_t want = std::max(need, dl_host_bytes_ + dl_host_bytes_ / 2);
     if (dl_host_) RM_HIP(hipHostFree(dl_host_));
     dl_host_ = nullptr;
-    dl_host_bytes_ = std::max(need, dl_host_bytes_ + dl_host_bytes_ / 2);
-    RM_HIP(hipHostMalloc(&dl_host_, dl_host_bytes_, hipHostMallocDefault));
+    dl_host_bytes_ = 0;
+    void* p = nullptr;
+    size_t got = want;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess && want > need) {
+      (void)hipGetLastError();
+      got = need;
+      e = hipHostMalloc(&p, need, hipHostMallocDefault);
+    }
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      throw BatchTooLarge("pinned download buffer of " + std::to_string(need) + " bytes: " + hipGetErrorString(e));
+    }
+    dl_host_ = p;
+    dl_host_bytes_ = got;
   };
   grow_host(offb);
   uint32_t* hc = (uint32_t*)dl_host_;
@@ -3711,10 +3730,31 @@ void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, 
   const size_t recb = (size_t)at * words * 8;
   const size_t dev_need = offb + recb + 8;
   if (dev_need > dl_dev_bytes_) {
+    const size_t want = std::max(dev_need, dl_dev_bytes_ + dl_dev_bytes_ / 2);
     if (dl_dev_) RM_HIP(hipFree(dl_dev_));
     dl_dev_ = nullptr;
-    dl_dev_bytes_ = std::max(dev_need, dl_dev_bytes_ + dl_dev_bytes_ / 2);
-    RM_HIP(hipMalloc(&dl_dev_, dl_dev_bytes_));
+    dl_dev_bytes_ = 0;
+    // test hook: allocations above RM_TEST_DOWNLOAD_ALLOC_LIMIT bytes fail as out of memory
+    // (tests/test_gpu_isolation.py drives the failure and the call after it)
+    const char* lim = std::getenv("RM_TEST_DOWNLOAD_ALLOC_LIMIT");
+    const size_t limit = lim && *lim ? (size_t)std::strtoull(lim, nullptr, 10) : ~(size_t)0;
+    void* p = nullptr;
+    size_t got = 0;
+    for (const size_t sz : {want, dev_need}) {
+      if (sz > limit) continue;
+      std::vector<void*> buf;
+      try {
+        dalloc<char>(buf, sz);
+      } catch (const OutOfDeviceMemory&) {
+        continue;
+      }
+      p = buf[0];
+      got = sz;
+      break;
+    }
+    if (!p) throw BatchTooLarge("segment download buffer of " + std::to_string(dev_need) + " bytes does not fit in HBM");
+    dl_dev_ = p;
+    dl_dev_bytes_ = got;
   }
   grow_host(offb + recb + 8);
   hc = (uint32_t*)dl_host_;

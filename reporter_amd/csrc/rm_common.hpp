@@ -297,8 +297,12 @@ struct MatchOptions {
   float interpolation_distance;     // 10 m
   float max_route_distance_factor;  // 5
   float max_route_time_factor;      // 2
-  float turn_penalty_factor;        // 0 (only 0 is supported)
+  float turn_penalty_factor;        // 0: meili's turn costs are not implemented; any other value is an error
 };
+// A request (or configured mode) asking for turn costs fails with this message instead of being
+// answered without them (the value used to be parsed and dropped).
+constexpr const char* kTurnPenaltyError =
+    "turn_penalty_factor must be 0: this matcher does not implement meili's turn costs";
 
 RM_HD MatchOptions default_options() {
   MatchOptions o;

@@ -28,8 +28,12 @@
 #include <vector>
 
 #include "rm_common.hpp"
+#include <limits>
 
 namespace rm {
+
+// the 16-19 digit number path below reads an x87 extended significand
+constexpr bool kX87LongDouble = std::numeric_limits<long double>::digits == 64 && sizeof(long double) >= 10;
 namespace tj {
 
 // points of many traces, appended in order (one sink per host thread)
@@ -79,6 +83,7 @@ class Reader {
         if (!(o.sigma_z > 0.f) || !std::isfinite(o.sigma_z)) err = "sigma_z must be positive";
         else if (!(o.beta > 0.f) || !std::isfinite(o.beta)) err = "beta must be positive";
         else if (!(o.search_radius >= 0.f)) err = "search_radius must be non-negative";
+        else if (!(o.turn_penalty_factor == 0.f)) err = kTurnPenaltyError;
       }
       if (err.empty()) {
         if (trace_state_ == 0 || trace_state_ == 2) err = "trace must be an array of points";
@@ -297,7 +302,9 @@ class Reader {
       static const long double kPow10L[28] = {
           1e0L, 1e1L, 1e2L, 1e3L, 1e4L, 1e5L, 1e6L, 1e7L, 1e8L, 1e9L, 1e10L, 1e11L, 1e12L, 1e13L,
           1e14L, 1e15L, 1e16L, 1e17L, 1e18L, 1e19L, 1e20L, 1e21L, 1e22L, 1e23L, 1e24L, 1e25L, 1e26L, 1e27L};
-      if (exp10 >= -27 && exp10 <= 27 && sizeof(long double) >= 10) {
+      // x87 80-bit extended only (64-bit significand in the low 8 bytes); IEEE quad long double
+      // (aarch64, ppc64le) lays its significand out differently and takes strtod
+      if (kX87LongDouble && exp10 >= -27 && exp10 <= 27) {
         const long double q = exp10 < 0 ? (long double)m / kPow10L[-exp10] : (long double)m * kPow10L[exp10];
         uint64_t sig;
         std::memcpy(&sig, &q, 8);   // x87 extended: the 64-bit significand is the low 8 bytes

@@ -44,7 +44,7 @@ def _match(path, pts, keep, comm=None):
     if comm is not None:
         # the reduce-scatter exchange of the same counts: this rank's padded segment-id range
         w = comm.world_size
-        ch = -(-nseg * 16 // w)
+        ch = 16 * -(-nseg // w)   # whole segments per rank
         part = dist.DeviceBuffer(ch * w * 4)
         part.upload(hist.download())
         comm.reduce_scatter(part.ptr, ch, dist.U32, dist.SUM)
@@ -57,7 +57,7 @@ def _match(path, pts, keep, comm=None):
         x.close()
     if rs is not None:   # the range equals the all-reduced histogram's (zero past the last segment)
         w = comm.world_size
-        ch = -(-nseg * 16 // w)
+        ch = 16 * -(-nseg // w)   # whole segments per rank
         want = np.zeros(ch * w, np.uint32)
         want[:nseg * 16] = h
         np.testing.assert_array_equal(rs, want[comm.rank * ch:(comm.rank + 1) * ch])

@@ -174,3 +174,26 @@ def test_coalesced_failing_request_fails_alone(built_lib, tmpdir_session):
     st = valhalla.coalesce_stats()
     assert st["batches"] - before["batches"] < n + 1   # they really shared batches
     print("isolation", st)
+
+
+def test_download_buffer_failure_then_retry(built_lib, small_world, monkeypatch):
+    """a segment download whose buffer cannot be allocated fails as a batch too
+    large for the device (the coalescer's split signal, serve_policy.hpp) and leaves the matcher
+    usable; the next call on the same matcher allocates again and returns the exact segments."""
+    tr = world.generate_traces(small_world, n_traces=16, n_points=200, rate_s=1.0, noise_m=5.0, seed=77)
+    eng = engine.Engine(small_world, 0)
+    want = engine.BatchMatcher(eng)
+    want.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"])
+    o_want, s_want = want.segments()
+    want.close()
+    bm = engine.BatchMatcher(eng)
+    bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"])
+    monkeypatch.setenv("RM_TEST_DOWNLOAD_ALLOC_LIMIT", "64")
+    with pytest.raises(RuntimeError, match="does not fit in HBM"):
+        bm.segments()
+    monkeypatch.delenv("RM_TEST_DOWNLOAD_ALLOC_LIMIT")
+    o, s = bm.segments()
+    np.testing.assert_array_equal(o, o_want)
+    assert s.tobytes() == s_want.tobytes() and len(s) > 50
+    bm.close()
+    eng.close()
