@@ -254,6 +254,16 @@ int rm_runner_get_reports(rm_runner* r, uint32_t* rep_off, void* reps, void* sta
  * (py/simple_reporter.py:169-173). */
 int rm_runner_set_isolation(rm_runner* r, int on);
 int rm_runner_trace_errors(rm_runner* r, uint32_t* errs);   /* n_traces words of the last run */
+/* Locality order of the stages that read regional graph data (K1 cell records, K2 route-ball
+ * tables, the path walk): the state slots are sorted each step into the Morton-ordered cells of a
+ * 64 x 64 grid over the graph (a counting sort) and those stages take their work in that order,
+ * XCD-contiguously, so one region's tables meet in one L2.  mode 0: slot order; 1: K1 and K2 in
+ * locality order; 2: the path stage too; -1 (default): 2 on graphs of >= 150 k nodes (env
+ * RM_LOCALITY_NODES), 1 for batches sampled every >= 10 s on average on smaller graphs, else 0.
+ * Env RM_LOCALITY sets the initial mode.  Results are identical in every mode.  *used: whether
+ * the last run used it. */
+int rm_runner_set_locality(rm_runner* r, int mode);
+int rm_runner_locality_used(rm_runner* r, int* used);
 /* per-kernel HIP-event timing on the runner's stream */
 int rm_runner_set_timing(rm_runner* r, int on);
 /* time only the stages whose bit is set (bit k = rm_kernel_name(k)): fewer event records in a timed region */

@@ -135,6 +135,8 @@ PROTOTYPES = [
     ("rm_runner_set_timing_mask", C.c_int, [P, C.c_uint32]),
     ("rm_runner_set_isolation", C.c_int, [P, C.c_int]),
     ("rm_runner_trace_errors", C.c_int, [P, P]),
+    ("rm_runner_set_locality", C.c_int, [P, C.c_int]),
+    ("rm_runner_locality_used", C.c_int, [P, C.POINTER(C.c_int)]),
     ("rm_report_segments", C.c_int, [C.POINTER(RmReportDesc), P, P, P]),
     ("rm_runner_kernel_times", C.c_int, [P, P, P, C.c_int]),
     ("rm_runner_reset_times", C.c_int, [P]),

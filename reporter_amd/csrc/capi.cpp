@@ -940,6 +940,13 @@ int rm_runner_get_reports(rm_runner* r, uint32_t* off, void* reps, void* stats) 
 int rm_runner_set_timing(rm_runner* r, int on) { return guarded([&] { r->m->set_timing(on != 0); }); }
 int rm_runner_set_timing_mask(rm_runner* r, uint32_t mask) { return guarded([&] { r->m->set_timing_mask(mask); }); }
 int rm_runner_set_isolation(rm_runner* r, int on) { return guarded([&] { r->m->set_isolation(on != 0); }); }
+int rm_runner_set_locality(rm_runner* r, int mode) {
+  return guarded([&] {
+    if (mode < -1 || mode > 2) throw std::runtime_error("locality mode must be -1, 0, 1 or 2");
+    r->m->set_locality(mode);
+  });
+}
+int rm_runner_locality_used(rm_runner* r, int* used) { return guarded([&] { *used = r->m->locality_used() ? 1 : 0; }); }
 int rm_runner_trace_errors(rm_runner* r, uint32_t* errs) { return guarded([&] { r->m->get_trace_errors(errs); }); }
 int rm_report_segments(const rm_report_desc* d, uint32_t* rep_off, void* reps, void* stats) {
   return guarded([&] {

@@ -5,19 +5,19 @@
 // search, transition routing, Viterbi and OSMLR segment forming, then the
 // reference's own post-match report() (py/reporter_service.py:79-179).
 //
-// Stage / kernel map (DESIGN.md §4 has the rooflines):
-//   k_states      one lane per trace: interpolation rule -> state layers
-//   k_candidates  K1, one wave per state: LDS-staged grid cells, point-to-polyline
-//                 projection, per-road min in an LDS hash, top-16 by rank
-//   k_routes      K2, one wave per layer pair: multi-source bounded label-correcting
-//                 search on the CSR with an LDS hash of (source, node) labels and
-//                 ballot/atomic frontier compaction; exact u64 (dist, time) keys
-//   k_viterbi     K3, one 16-lane group per trace: fp64 costs in registers,
-//                 shuffle broadcast of the previous layer, back-pointers, backtrace
-//   k_paths       one wave per chosen transition: re-search + canonical predecessors
-//   k_seg_blocks / k_segments   K4: traversal records, time interpolation and OSMLR
-//                 runs in one kernel, records staged in LDS (parallel over slots, records, runs)
-//   k_report      A8 epilogue, one lane per trace: report() + speed histogram
+// Stage / kernel map (DESIGN.md §5 has the rooflines):
+//   k_states          one wave per trace: interpolation rule -> state layers
+//   k_loc_*           locality order (large graphs): state slots counted into 64 x 64 Morton regions
+//   k_candidates_lane K1, one lane per state: cell-major 32-byte records, per-road minima in
+//                     registers, top 16 by (sq, road); k_candidates_wave takes the overflow
+//   k_trans_count     pair constants + counts; k_scan_* lay out routes and K2 items
+//   k_routes_ball2    K2, block-expanded: one lane per transition, two route-ball probes per
+//                     target; search tiers (lane / reg2 / wave LDS / global) for the hand-overs
+//   k_viterbi         K3, one 16-lane DPP row per trace: fp64 costs in registers, backtrace
+//   k_paths_ball      one lane per chosen transition: labels from the balls, walk back by the
+//                     rows' canonical predecessors (+ the search tiers)
+//   k_rec_slot / k_seg_wave   K4: one wave per trace, traversal records 64 per step, runs by ballot
+//   k_report          A8 epilogue, one wave per trace: report() + speed histogram + duration sums
 //
 // All arithmetic follows rm_common.hpp; compiled with -ffp-contract=off so the
 // results are bit-identical to oracle/meili_oracle.c.
@@ -36,7 +36,7 @@
 namespace rm {
 
 const char* const kKernelNames[kNumKernels] = {"states", "candidates", "scan", "routes",
-                                               "viterbi", "paths", "segments", "report"};
+                                               "viterbi", "paths", "segments", "report", "locality"};
 
 namespace {
 
@@ -73,6 +73,15 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint32_t* rl_cand;
   uint32_t* rl_routes_c; uint32_t* rl_paths_c;
   uint32_t* trace_err;    // per trace: error bits of that trace only (the rest of the batch is unaffected)
+  // locality order (round 4): state slots sorted by the Morton code of their point's coarse grid
+  // cell; null = slot order.  K1 takes states, K2 items and the path stage pairs in this order
+  // (a pair by its source state), so work that reads one region's cell records and route-ball
+  // tables meets in one XCD's L2 instead of arriving in trace order from everywhere.
+  const uint32_t* perm;
+  const uint32_t* perm_paths;   // perm for the path stage too (null: the path stage takes slot order)
+  const uint32_t* inv;          // rank of each slot in perm (null: slot order)
+  uint32_t* pcnt;               // K2 item count of the pair whose source has rank r
+  unsigned long long* pcnt_part;   // their partial sums per 256 ranks (.x of k_scan_parts' pairs)
 };
 
 // A failure that belongs to one trajectory (too many roads in a radius, a search beyond every
@@ -97,6 +106,14 @@ __device__ __forceinline__ float point_radius(const MatchOptions& o, float acc) 
   return r;
 }
 
+// XCD-aware block order: the dispatcher deals workgroups round-robin over the 8 XCDs
+// (block i runs on XCD i % 8), so consecutive work (the pairs of one trace) would land
+// in 8 different L2s.  Renumber so each XCD gets one contiguous range of logical blocks.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t i, uint32_t n) {
+  const uint32_t x = i & 7u, idx = i >> 3, q = n >> 3, r = n & 7u;
+  return x < r ? x * (q + 1u) + idx : r * (q + 1u) + (x - r) * q + idx;
+}
+
 // bound on route distance (cm) for a layer pair: min(factor * gc, breakage)
 __device__ __forceinline__ uint32_t route_bound(double gc, const MatchOptions& o) {
   double maxd = gc * (double)o.max_route_distance_factor;
@@ -110,6 +127,116 @@ __device__ __forceinline__ uint32_t time_bound(double dt, const MatchOptions& o)
   const double tm = floor(dt * (double)o.max_route_time_factor * 1000.0);
   return tm >= 4294967295.0 ? 0xffffffffu : (uint32_t)tm;
 }
+
+// ------------------------------------------------------------------------------------------
+// Locality order (round 4).  On graphs whose route-ball tables and cell
+// records are far larger than the L2s (C3: 4.2 GB of tables, C4: 68 GB), a step that visits
+// states in trace order probes every table from vehicles spread over the whole step and all 8
+// XCDs: each 16-byte row costs a 128-byte line from HBM (C3 K2 traffic 2.05x its algorithmic
+// bytes, L2 hit rate 0.20).  The state slots are sorted once per step by the Morton code of
+// their point's coarse grid cell; K1 reads its states, K2 its (pair, source) items and the path
+// stage its chosen transitions in that order (a pair by its source state, whose exits own the
+// tables it probes), with XCD-contiguous block ranges, and results still go to their slots.
+// Results are identical in any order; only which L2 serves the reads changes.
+__device__ __forceinline__ uint32_t morton_spread16(uint32_t v) {
+  v &= 0xffffu;
+  v = (v | (v << 8)) & 0x00ff00ffu;
+  v = (v | (v << 4)) & 0x0f0f0f0fu;
+  v = (v | (v << 2)) & 0x33333333u;
+  v = (v | (v << 1)) & 0x55555555u;
+  return v;
+}
+// The sort is a counting sort into kLocBuckets region buckets (a Morton-ordered 64 x 64 grid
+// over the graph; one more bucket, last, for the slots without a state): three short passes
+// (block histograms, one scan, block scatter) instead of a radix sort (hipcub's took 0.18 ms
+// on C3 and 0.52 ms on C4 per 125 k traces).  Order inside a bucket is unspecified.
+constexpr uint32_t kLocBucketBits = 12, kLocBuckets = 1u << kLocBucketBits;
+constexpr uint32_t kLocPerThread = 16;   // slots per thread: a block of 256 threads covers 4096 slots
+__device__ __forceinline__ uint32_t loc_bucket(const DevGraph& g, const DevBatch& b, uint64_t p, uint32_t shift) {
+  const uint32_t k = b.slot_trace[p];
+  const uint32_t o = b.trace_off[k];
+  if ((uint32_t)(p - o) >= b.n_states[k]) return kLocBuckets;   // no state at this slot: last
+  const uint32_t pt = o + b.state_orig[p];
+  const double fx = floor(((double)b.lon[pt] - g.lon0) / g.dlon), fy = floor(((double)b.lat[pt] - g.lat0) / g.dlat);
+  const uint32_t cx = fx < 0.0 ? 0u : (fx > (double)(g.ncx - 1) ? g.ncx - 1 : (uint32_t)fx);
+  const uint32_t cy = fy < 0.0 ? 0u : (fy > (double)(g.ncy - 1) ? g.ncy - 1 : (uint32_t)fy);
+  return morton_spread16(min(cx >> shift, 63u)) | (morton_spread16(min(cy >> shift, 63u)) << 1);
+}
+__global__ void __launch_bounds__(256) k_loc_count(DevGraph g, DevBatch b, uint32_t shift, uint16_t* key,
+                                                   uint32_t* hist) {
+  __shared__ uint32_t h[kLocBuckets + 1];
+  for (uint32_t q = threadIdx.x; q <= kLocBuckets; q += 256) h[q] = 0u;
+  __syncthreads();
+  const uint64_t p0 = (uint64_t)blockIdx.x * (256u * kLocPerThread) + threadIdx.x;
+#pragma unroll 4
+  for (uint32_t i = 0; i < kLocPerThread; ++i) {
+    const uint64_t p = p0 + 256u * i;
+    if (p < b.P) {
+      const uint32_t kk = loc_bucket(g, b, p, shift);
+      key[p] = (uint16_t)kk;
+      atomicAdd(&h[kk], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q <= kLocBuckets; q += 256)
+    if (h[q]) atomicAdd(&hist[q], h[q]);
+}
+// exclusive scan of the kLocBuckets + 1 bucket counts, in place (one block)
+__global__ void __launch_bounds__(1024) k_loc_scan(uint32_t* hist) {
+  __shared__ uint32_t ws[16];
+  constexpr uint32_t per = (kLocBuckets + 1 + 1023) / 1024;
+  const uint32_t q0 = threadIdx.x * per;
+  uint32_t v[per], t = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < per; ++i) { v[i] = q0 + i <= kLocBuckets ? hist[q0 + i] : 0u; t += v[i]; }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = t;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += u;
+  }
+  if (lane == 63) ws[wv] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int w = 0; w < wv; ++w) base += ws[w];
+  uint32_t at = base + incl - t;
+#pragma unroll
+  for (uint32_t i = 0; i < per; ++i) {
+    if (q0 + i <= kLocBuckets) hist[q0 + i] = at;
+    at += v[i];
+  }
+}
+__global__ void __launch_bounds__(256) k_loc_scatter(uint64_t P, const uint16_t* key, uint32_t* cursor, uint32_t* perm,
+                                                     uint32_t* inv) {
+  __shared__ uint32_t h[kLocBuckets + 1];
+  for (uint32_t q = threadIdx.x; q <= kLocBuckets; q += 256) h[q] = 0u;
+  __syncthreads();
+  const uint64_t p0 = (uint64_t)blockIdx.x * (256u * kLocPerThread) + threadIdx.x;
+  uint32_t kk[kLocPerThread], rk[kLocPerThread];
+#pragma unroll
+  for (uint32_t i = 0; i < kLocPerThread; ++i) {
+    const uint64_t p = p0 + 256u * i;
+    kk[i] = p < P ? key[p] : 0xffffu;
+    rk[i] = kk[i] != 0xffffu ? atomicAdd(&h[kk[i]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q <= kLocBuckets; q += 256)
+    if (h[q]) h[q] = atomicAdd(&cursor[q], h[q]);   // this block's range of the bucket
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < kLocPerThread; ++i)
+    if (kk[i] != 0xffffu) {
+      const uint32_t r = h[kk[i]] + rk[i];
+      perm[r] = (uint32_t)(p0 + 256u * i);
+      inv[p0 + 256u * i] = r;
+    }
+}
+// K2 items in locality order: k_trans_count puts each pair's item count at its source state's
+// rank (pcnt, with block partials of the ranks); k_scan_apply_perm scatters the scan's offsets to
+// the pairs' src_off
+__global__ void __launch_bounds__(256) k_scan_apply_perm(const uint32_t* a, uint64_t n, const unsigned long long* part,
+                                                         const uint32_t* perm, uint32_t* src_off);
 
 // ------------------------------------------------------------------------------------------
 // k_states: interpolation rule (points closer than interpolation_distance to the last
@@ -298,7 +425,12 @@ __device__ __forceinline__ void put_cand(const DevGraph& g, const DevBatch& b, u
 #endif
 constexpr int kK1Rows = RM_K1_ROWS;   // grid rows whose items K1 walks as one sequence
 __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b) {
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b.perm) {   // locality order: each XCD walks one contiguous range of the sorted states
+    const uint64_t r = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (r >= b.P) return;
+    p = b.perm[r];
+  }
   if (p >= b.P) return;
   const uint32_t k = b.slot_trace[p];
   const uint32_t o = b.trace_off[k];
@@ -662,6 +794,27 @@ __global__ void __launch_bounds__(256) k_scan_apply4(const uint32_t* a, uint64_t
   }
 }
 
+__global__ void __launch_bounds__(256) k_scan_apply_perm(const uint32_t* a, uint64_t n, const unsigned long long* part,
+                                                         const uint32_t* perm, uint32_t* src_off) {
+  __shared__ uint32_t sa[4];
+  const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint32_t base = (uint32_t)reinterpret_cast<const ulonglong2*>(part)[blockIdx.x].x;
+  const uint32_t v = r < n ? a[r] : 0u;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t iv = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(iv, d, 64);
+    if (lane >= d) iv += t;
+  }
+  if (lane == 63) sa[wv] = iv;
+  __syncthreads();
+  uint32_t bb = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) bb += w < wv ? sa[w] : 0u;
+  if (r < n && v) src_off[perm[r] + 1u] = base + bb + iv - v;
+}
+
 // transition counts for the exclusive scan that lays out route[] compactly, plus the
 // per-pair constants K2 needs (bounds, candidate counts, mode) in one dwordx4; the block
 // partials of the u64 totals of transitions and (pair, source) items go to part[]
@@ -688,6 +841,12 @@ __global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long l
     }
     b.trans_cnt[p] = c;
     b.src_cnt[p] = ns;
+    if (b.inv) {   // locality order: the count at the rank of the pair's source state (p - 1)
+      const uint32_t r = b.inv[p ? p - 1 : b.P - 1];
+      const uint32_t v = p ? ns : 0u;   // thread 0 covers the last slot, which is no pair's source
+      b.pcnt[r] = v;
+      if (v) atomicAdd(&b.pcnt_part[2 * (r >> 8)], (unsigned long long)v);
+    }
   }
   block_sum2_u64(c, ns, part);
 }
@@ -1033,14 +1192,6 @@ __device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, 
   }
 }
 
-// XCD-aware block order: the dispatcher deals workgroups round-robin over the 8 XCDs
-// (block i runs on XCD i % 8), so consecutive work (the pairs of one trace) would land
-// in 8 different L2s.  Renumber so each XCD gets one contiguous range of logical blocks.
-__device__ __forceinline__ uint32_t xcd_block(uint32_t i, uint32_t n) {
-  const uint32_t x = i & 7u, idx = i >> 3, q = n >> 3, r = n & 7u;
-  return x < r ? x * (q + 1u) + idx : r * (q + 1u) + (x - r) * q + idx;
-}
-
 __device__ __forceinline__ uint4 ball_first(const uint4* ent, const uint2& h, uint32_t road, bool use) {
   return use ? ent[ball_row0(h.x) + ball_slot(road, h.y)] : make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
 }
@@ -1069,6 +1220,10 @@ __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1,
 // own (the round-2 kernel's lanes ran to their wave's largest K_B, each target two dependent
 // round trips after the last), and two transitions per lane are in flight at once.
 constexpr int kK2Items = 256;
+// graphs from this many nodes take the locality order by default (Engine::locality_default),
+// and so do batches sampled this sparsely on average (Matcher::run)
+constexpr uint64_t kLocalityNodes = 150000;
+constexpr double kLocalitySparseS = 10.0;
 // global-address-space 16-byte pointer: loads through it are global_load_dwordx4 even when the
 // address went through LDS (a generic pointer there would become a flat load)
 typedef unsigned int k2_v4 __attribute__((ext_vector_type(4)));
@@ -1083,13 +1238,14 @@ struct K2Src {
   unsigned long long ent;        // the item's mode's table rows (a global address: see k2_gptr)
   uint32_t road, s;              // source road and offset on it (direct combinations)
   uint32_t tdesc;                // the pair's first target descriptor (p * kMaxCand)
-  uint32_t rel;                  // the item's first route, relative to the block's range
+  uint32_t rel;                  // the item's first transition among the block's (block scan of K_B)
   uint32_t bound, tmax;          // pair bounds; bound = kNone: handed to the search tiers
+  uint32_t ob;                   // the item's first route in b.route
 };
 struct K2Smem {
   K2Src src[kK2Items];
-  uint8_t owner[kK2Items * kMaxCand];   // route (relative to the range) -> item of the block
-  uint32_t lo, hi;
+  uint8_t owner[kK2Items * kMaxCand];   // transition of the block -> item of the block
+  uint32_t wsum[kK2Items / 64];
 };
 
 // route of item S to the target described by (t0, t1), from the target road's rows (r1, r0)
@@ -1137,19 +1293,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     S.rel = 0;
     S.bound = pi.x;
     S.tmax = pi.y;
+    S.ob = ob;
     if (!fits || S.h1.y == 0u || S.h0.y == 0u) {   // the search tiers take it (they run later)
       S.bound = kNone;
       b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
     }
     sm.src[threadIdx.x] = S;
-    if (threadIdx.x == 0) sm.lo = ob;
-    if (t == tl) sm.hi = ob + KB;
   }
+  // the block's transitions: an exclusive scan of the items' K_B (in slot order the items' routes
+  // are one contiguous range and this is ob - the first ob; in locality order they are not)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = KB;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += u;
+  }
+  if (lane == 63) sm.wsum[wv] = incl;
   __syncthreads();
-  const uint32_t lo = sm.lo, n = sm.hi - lo;
+  uint32_t wbase = 0, n = 0;
+#pragma unroll
+  for (int w = 0; w < kK2Items / 64; ++w) {
+    const uint32_t x = sm.wsum[w];
+    wbase += w < wv ? x : 0u;
+    n += x;
+  }
   if (live) {
-    sm.src[threadIdx.x].rel = ob - lo;
-    for (uint32_t j = 0; j < KB; ++j) sm.owner[ob - lo + j] = (uint8_t)threadIdx.x;
+    const uint32_t rel = wbase + incl - KB;
+    sm.src[threadIdx.x].rel = rel;
+    for (uint32_t j = 0; j < KB; ++j) sm.owner[rel + j] = (uint8_t)threadIdx.x;
   }
   __syncthreads();
   // ---- phase 2: the block's routes, two transitions per lane and step.  Every load of a step
@@ -1182,8 +1354,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     const uint4 ea1 = ua1 ? la1 : none, ea0 = ua0 ? la0 : none, eb1 = ub1 ? lb1 : none, eb0 = ub0 ? lb0 : none;
     const uint4* ga = (const uint4*)A.ent;
     const uint4* gb = (const uint4*)B.ent;
-    if (la) b.route[lo + q] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm));
-    if (lb) b.route[lo + qb] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm));
+    if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm));
+    if (lb) b.route[B.ob + (qb - B.rel)] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm));
   }
 }
 
@@ -1521,7 +1693,12 @@ __device__ void path_walk_ball(const DevGraph& g, const DevBatch& b, uint64_t p,
 // path ball tier: one lane per chosen transition whose bound fits the ball radius; the
 // others go to the search tiers (rl_routes_0 reused after K2, count ctl[8])
 __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b.perm_paths) {   // locality order: the pair whose source state is the r-th sorted state
+    const uint64_t r = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (r >= b.P) return;
+    p = (uint64_t)b.perm_paths[r] + 1u;
+  }
   if (p >= b.P) return;
   // the slot's loads issued together (every slot < P holds a choice and a chain flag), the
   // filters after them
@@ -1575,6 +1752,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
     }
     return;
   } else {
+    if (b.perm_paths) {
+      const uint64_t r = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+      if (r >= b.P) return;
+      p = (uint64_t)b.perm_paths[r] + 1u;
+    }
     if (p >= b.P) return;
     const uint32_t k = b.slot_trace[p];
     const uint32_t o = b.trace_off[k];
@@ -2403,62 +2585,109 @@ __global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const u
 // ------------------------------------------------------------------------------------------
 // A8 k_report: reference report() per trace (py/reporter_service.py:79-179) + the batch
 // filter (py/simple_reporter.py:177) + per-segment 10 km/h speed histogram.
-// report() of one trace over its segments: reports written to out, stats returned
-__device__ __forceinline__ ReportStats report_trace(const SegmentRec* segs, uint32_t n, bool has_pts, double end_time,
+// report() of one trace by one wave (round 4; the round-3 kernel walked a trace's segment list
+// in one lane, ~0.38 ms of a 125 k-trace C3 step): 64 segments per step, one per lane.  The
+// rule's sequential state becomes lane algebra: the tail trim is a ballot from the end, the
+// prior of segment q is the highest segment below q that may be one (q == 0 or not internal,
+// :145-147; carried across steps), each lane then decides its own report (:119-134) from the
+// prior's fields, reports are compacted in segment order by a ballot prefix count, and the
+// counters / "last assigned" lengths come from ballots.  The same function serves k_report and
+// rm_report_segments, which the reference's own report() outputs pin (tests/golden).
+__device__ __forceinline__ double shfl_d(double v, int src) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __shfl((int)(uint32_t)u, src, 64), hi = __shfl((int)(uint32_t)(u >> 32), src, 64);
+  return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ ReportStats report_wave(const SegmentRec* segs, uint32_t n, bool has_pts, double end_time,
                                                    double threshold, uint32_t rmask, uint32_t tmask, ReportRec* out,
                                                    uint32_t* hist, unsigned long long* dur) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   ReportStats st;
   st.successful_count = st.unreported_count = 0;
   st.successful_length_m = st.unreported_length_m = -1;
   st.discontinuities = st.invalid_speeds = st.invalid_times = st.unassociated = 0;
   st.shape_used = -1;
-  int nrep = 0;
+  // the tail that ends within threshold seconds of the trace's last point is not reported yet
+  // (:86-92): last = the highest segment whose start is not within it
+  int last = -1;
   if (has_pts) {
-    int last = (int)n - 1;
-    while (last >= 0 && end_time - segs[last].start_time < threshold) --last;
-    if (last >= 0 && segs[last].begin_shape_index != 0) st.shape_used = (int32_t)segs[last].begin_shape_index;
-    bool have_prior = false, p_has_id = false;
-    uint64_t p_id = 0; double p_t0 = 0, p_t1 = 0; int32_t p_len = 0, p_q = 0; int p_lvl = -1; uint32_t p_dense = kNone;
-    for (int q = 0; q <= last; ++q) {
-      const SegmentRec& s = segs[q];
-      const bool has_id = (s.flags & 2u) != 0u, internal = (s.flags & 1u) != 0u;
-      if (q != 0 && s.start_time == -1.0 && segs[q - 1].end_time == -1.0) st.discontinuities++;
-      const int lvl = has_id ? (int)(s.segment_id & 7ull) : -1;
-      if (have_prior && p_has_id && p_len > 0 && !internal) {
-        if (p_lvl >= 0 && ((rmask >> (p_lvl + 1)) & 1u)) {
+    for (int c0 = ((int)n - 1) & ~63; c0 >= 0; c0 -= 64) {
+      const int q = c0 + lane;
+      const bool keep = q < (int)n && !(end_time - segs[q].start_time < threshold);
+      const uint64_t m = __ballot(keep);
+      if (m) { last = c0 + 63 - __clzll(m); break; }
+    }
+  }
+  if (last >= 0 && segs[last].begin_shape_index != 0) st.shape_used = (int32_t)segs[last].begin_shape_index;
+  int carried = -1;          // the prior before this step's segments (index), -1: none yet
+  double prev_end = 0.0;     // end time of the segment before this step's first
+  int nrep = 0;
+  for (int c0 = 0; c0 <= last; c0 += 64) {
+    const int q = c0 + lane;
+    const bool valid = q <= last;
+    const SegmentRec& sq = segs[valid ? q : last];
+    const uint32_t flags = sq.flags;
+    const uint64_t sid = sq.segment_id;
+    const double st0 = sq.start_time, st1 = sq.end_time;
+    const bool has_id = valid && (flags & 2u) != 0u, internal = valid && (flags & 1u) != 0u;
+    const double pe = shfl_d(st1, lane ? lane - 1 : 0);
+    const double pend = lane ? pe : prev_end;
+    const bool disc = valid && q != 0 && st0 == -1.0 && pend == -1.0;
+    const bool unas = valid && !has_id && !internal;
+    const uint64_t E = __ballot(valid && (!internal || q == 0));
+    const uint64_t eb = E & below;
+    const int pj = eb ? c0 + 63 - __clzll(eb) : carried;
+    bool succ = false, unrep = false, bad_t = false, bad_v = false;
+    int32_t plen = 0;
+    ReportRec r;
+    if (valid && pj >= 0 && !internal) {
+      const SegmentRec& P = segs[pj];
+      plen = P.length;
+      if ((P.flags & 2u) && plen > 0) {
+        const int p_lvl = (int)(P.segment_id & 7ull);
+        if ((rmask >> (p_lvl + 1)) & 1u) {
+          const int lvl = has_id ? (int)(sid & 7ull) : -1;
           const bool to_next = ((tmask >> (lvl + 1)) & 1u) != 0u;
-          ReportRec r;
-          r.id = p_id; r.t0 = p_t0; r.t1 = to_next ? s.start_time : p_t1;
-          r.length = p_len; r.queue_length = p_q; r.seg_dense = p_dense; r.pad = 0;
-          r.next_id = (to_next && has_id) ? s.segment_id : kInvalidSegmentId;
+          r.id = P.segment_id; r.t0 = P.start_time; r.t1 = to_next ? st0 : P.end_time;
+          r.length = plen; r.queue_length = P.queue_length; r.seg_dense = P.seg_dense; r.pad = 0;
+          r.next_id = (to_next && has_id) ? sid : kInvalidSegmentId;
           const double dt = r.t1 - r.t0;
-          if (dt <= 0 || isinf(dt) || isnan(dt)) st.invalid_times++;
-          else if (((double)p_len / dt) * 3.6 > 160.0) st.invalid_speeds++;
-          else {
-            out[nrep++] = r;
-            st.successful_count++;
-            st.successful_length_m = p_len;
-            if ((hist || dur) && r.t0 > 0 && r.t1 > 0 && dt > 0.5 && r.length > 0 && r.queue_length >= 0 &&
-                p_dense != kNone) {
-              int bin = (int)(((double)r.length / dt) * 3.6 / 10.0);
-              bin = bin > kHistBins - 1 ? kHistBins - 1 : (bin < 0 ? 0 : bin);
-              if (hist) atomicAdd(&hist[(uint64_t)p_dense * kHistBins + (uint32_t)bin], 1u);
-              // the tile row's duration column, int(round(t1 - t0)) (py/simple_reporter.py:179;
-              // Python 2 round() is half away from zero, as round()), summed per segment
-              if (dur) atomicAdd(&dur[p_dense], (unsigned long long)round(dt));
-            }
-          }
+          if (dt <= 0 || isinf(dt) || isnan(dt)) bad_t = true;
+          else if (((double)plen / dt) * 3.6 > 160.0) bad_v = true;
+          else succ = true;
         } else {
-          st.unreported_count++;
-          st.unreported_length_m = p_len;
+          unrep = true;
         }
       }
-      if (!(internal && q != 0)) {
-        have_prior = true; p_has_id = has_id; p_id = s.segment_id; p_t0 = s.start_time; p_t1 = s.end_time;
-        p_len = s.length; p_q = s.queue_length; p_lvl = lvl; p_dense = s.seg_dense;
-      }
-      if (!has_id && !internal) st.unassociated++;
     }
+    const uint64_t ms = __ballot(succ), mu = __ballot(unrep);
+    if (succ) {
+      out[nrep + __popcll(ms & below)] = r;
+      const double dt = r.t1 - r.t0;
+      if ((hist || dur) && r.t0 > 0 && r.t1 > 0 && dt > 0.5 && r.length > 0 && r.queue_length >= 0 &&
+          r.seg_dense != kNone) {
+        int bin = (int)(((double)r.length / dt) * 3.6 / 10.0);
+        bin = bin > kHistBins - 1 ? kHistBins - 1 : (bin < 0 ? 0 : bin);
+        if (hist) atomicAdd(&hist[(uint64_t)r.seg_dense * kHistBins + (uint32_t)bin], 1u);
+        // the tile row's duration column, int(round(t1 - t0)) (py/simple_reporter.py:179;
+        // Python 2 round() is half away from zero, as round()), summed per segment
+        if (dur) atomicAdd(&dur[r.seg_dense], (unsigned long long)round(dt));
+      }
+    }
+    nrep += __popcll(ms);
+    st.successful_count += __popcll(ms);
+    st.unreported_count += __popcll(mu);
+    st.invalid_times += __popcll(__ballot(bad_t));
+    st.invalid_speeds += __popcll(__ballot(bad_v));
+    st.discontinuities += __popcll(__ballot(disc));
+    st.unassociated += __popcll(__ballot(unas));
+    const int ls = ms ? 63 - __clzll(ms) : 0, lu = mu ? 63 - __clzll(mu) : 0;
+    const int32_t len_s = __shfl(plen, ls, 64), len_u = __shfl(plen, lu, 64);
+    if (ms) st.successful_length_m = len_s;
+    if (mu) st.unreported_length_m = len_u;
+    if (E) carried = c0 + 63 - __clzll(E);
+    prev_end = shfl_d(st1, 63);
   }
   st.n_reports = nrep;
   return st;
@@ -2466,13 +2695,14 @@ __device__ __forceinline__ ReportStats report_trace(const SegmentRec* segs, uint
 
 __global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uint32_t rmask, uint32_t tmask,
                                                uint32_t* hist, unsigned long long* dur) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= b.T) return;
+  const uint32_t k = blockIdx.x;
   const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
-  const ReportStats st = report_trace(b.segs + b.seg_base[k], b.seg_cnt[k], npts > 0, npts ? b.time[o + npts - 1] : 0.0,
-                                      threshold, rmask, tmask, b.reps + b.seg_base[k], hist, dur);
-  b.rep_cnt[k] = (uint32_t)st.n_reports;
-  b.stats[k] = st;
+  const ReportStats st = report_wave(b.segs + b.seg_base[k], b.seg_cnt[k], npts > 0, npts ? b.time[o + npts - 1] : 0.0,
+                                     threshold, rmask, tmask, b.reps + b.seg_base[k], hist, dur);
+  if (threadIdx.x == 0) {
+    b.rep_cnt[k] = (uint32_t)st.n_reports;
+    b.stats[k] = st;
+  }
 }
 
 // report() over host-supplied segment lists (rm_report_segments): per-trace end time,
@@ -2481,11 +2711,11 @@ __global__ void __launch_bounds__(64) k_report_lists(uint32_t T, const uint32_t*
                                                      const double* end_time, const double* threshold,
                                                      const uint32_t* rmask, const uint32_t* tmask, ReportRec* reps,
                                                      ReportStats* stats) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= T) return;
+  const uint32_t k = blockIdx.x;
   const uint32_t o = seg_off[k];
-  stats[k] = report_trace(segs + o, seg_off[k + 1] - o, true, end_time[k], threshold[k], rmask[k], tmask[k], reps + o,
-                          nullptr, nullptr);
+  const ReportStats st = report_wave(segs + o, seg_off[k + 1] - o, true, end_time[k], threshold[k], rmask[k], tmask[k],
+                                     reps + o, nullptr, nullptr);
+  if (threadIdx.x == 0) stats[k] = st;
 }
 
 // u64 totals of one or two u32 count arrays: the u32 exclusive scans that lay out routes and
@@ -2929,6 +3159,18 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   }
   dg_.lon0 = gk.lon0; dg_.lat0 = gk.lat0; dg_.dlon = gk.dlon; dg_.dlat = gk.dlat;
   dg_.ncx = gk.ncx; dg_.ncy = gk.ncy;
+  {
+    // locality order (k_loc_count): the K1 grid coarsened 2^shift x 2^shift into at most 64 x 64
+    // region buckets (kLocBuckets), on by default on graphs of >= kLocalityNodes nodes
+    // (RM_LOCALITY_NODES overrides), where the route tables and cell records outgrow the L2s
+    uint32_t sh = 0;
+    while (((gk.ncx - 1) >> sh) >= 64u || ((gk.ncy - 1) >> sh) >= 64u) ++sh;
+    locality_shift_ = sh;
+    locality_bits_ = (gk.ncx > 1 || gk.ncy > 1) ? kLocBucketBits : 0u;
+    const char* ln = std::getenv("RM_LOCALITY_NODES");
+    const uint64_t min_nodes = ln && *ln ? std::strtoull(ln, nullptr, 10) : kLocalityNodes;
+    locality_default_ = locality_bits_ > 0 && (uint64_t)g.num_nodes() >= min_nodes;
+  }
   dg_.n_nodes = g.num_nodes(); dg_.n_edges = g.num_edges(); dg_.n_segments = g.num_segments();
   if (g.num_nodes()) {
     hipLaunchKernelGGL(k_fill_edge_src, dim3((g.num_nodes() + 255) / 256), dim3(256), 0, 0, dg_.node_off,
@@ -3135,12 +3377,42 @@ Workspace::~Workspace() { release(); }
 void Workspace::release() {
   for (void* p : allocs) (void)hipFree(p);
   allocs.clear();
-  cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = cap_src = 0;
+  cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = cap_src = cap_sort = 0;
+  perm = loc_cursor = pcnt = loc_inv = nullptr;
+  loc_key = nullptr;
+  pcnt_part = nullptr;
 }
 
 Matcher::Matcher(Engine* e) : eng_(e) {
   RM_HIP(hipSetDevice(e->device()));
   RM_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  if (const char* lv = std::getenv("RM_LOCALITY"); lv && *lv) locality_ = std::max(-1, std::min(2, std::atoi(lv)));
+}
+
+void Matcher::ensure_sort(uint64_t n) {
+  grow_workspace([&] {
+    Workspace& w = ws_;
+    if (n <= w.cap_sort && w.perm) return;
+    for (void** q : {(void**)&w.perm, (void**)&w.loc_key, (void**)&w.loc_cursor, (void**)&w.pcnt, (void**)&w.loc_inv,
+                     (void**)&w.pcnt_part}) {
+      if (*q) {
+        (void)hipFree(*q);
+        w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), *q));
+      }
+      *q = nullptr;
+    }
+    w.cap_sort = 0;
+    const uint64_t c = std::max<uint64_t>(n, w.cap_points);
+    if (c >= (uint64_t)INT32_MAX) throw BatchTooLarge("batch too large for the locality sort");
+    std::vector<void*>& L = w.allocs;
+    w.perm = dalloc<uint32_t>(L, c);
+    w.loc_key = dalloc<uint16_t>(L, c);                 // region bucket per slot
+    w.loc_cursor = dalloc<uint32_t>(L, kLocBuckets + 1);  // bucket counts -> cursors
+    w.pcnt = dalloc<uint32_t>(L, c);
+    w.loc_inv = dalloc<uint32_t>(L, c);
+    w.pcnt_part = dalloc<unsigned long long>(L, 2 * ((c + 255) / 256) + 2);
+    w.cap_sort = c;
+  });
 }
 
 Matcher::~Matcher() {
@@ -3317,6 +3589,9 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.ctl = w.ctl; v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
   v.rl_paths_a = w.rl_paths_a; v.rl_paths_b = w.rl_paths_b; v.rl_cand = w.rl_cand;
   v.rl_routes_c = w.rl_routes_c; v.rl_paths_c = w.rl_paths_c; v.trace_err = w.trace_err;
+  v.perm = nullptr;   // run_device sets it when the locality order is on
+  v.perm_paths = nullptr;
+  v.inv = nullptr; v.pcnt = nullptr; v.pcnt_part = nullptr;
   return v;
 }
 
@@ -3338,6 +3613,18 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
     if (!(hb.opts[q].beta > 0.f) || !std::isfinite(hb.opts[q].beta)) throw std::runtime_error("beta must be positive and finite");
     if (!(hb.opts[q].turn_penalty_factor == 0.f)) throw std::runtime_error(kTurnPenaltyError);
     mode_mask_ |= 1u << hb.opts[q].mode;
+  }
+  {
+    // mean sampling interval of the batch: traces sampled sparsely (C3's 30 s) have no spatial
+    // coherence from one point to the next, so the locality order pays even on small graphs;
+    // at 1 Hz consecutive points share their tables and records already (auto mode)
+    double span = 0.0;
+    uint64_t gaps = 0;
+    for (uint32_t k = 0; k < T; ++k) {
+      const uint32_t a = hb.trace_off[k], e = hb.trace_off[k + 1];
+      if (e > a + 1) { span += hb.time[e - 1] - hb.time[a]; gaps += e - a - 1; }
+    }
+    batch_sparse_ = gaps && span / (double)gaps >= kLocalitySparseS;
   }
   ensure(P, T, hb.n_opts);
   Workspace& w = ws_;
@@ -3401,6 +3688,28 @@ void Matcher::run_device(const RunParams& rp) {
   tic(kKStates);
   hipLaunchKernelGGL(k_states, dim3(T), dim3(64), 0, st, v);
   toc(kKStates);
+  // mode: 0 slot order, 1 K1 + K2 in locality order, 2 the path stage too; auto (-1): 2 on large
+  // graphs, 1 for sparsely sampled batches on small ones (measured: DESIGN.md §5 "Locality")
+  int lmode = locality_;
+  if (lmode < 0) lmode = eng_->locality_default() ? 2 : (batch_sparse_ ? 1 : 0);
+  if (eng_->locality_bits() == 0) lmode = 0;   // one region: nothing to order
+  locality_used_ = lmode > 0;
+  if (locality_used_) {
+    tic(kKLocality);
+    ensure_sort(P);
+    const uint32_t lgrid = (uint32_t)((P + 256u * kLocPerThread - 1) / (256u * kLocPerThread));
+    RM_HIP(hipMemsetAsync(w.loc_cursor, 0, (kLocBuckets + 1) * sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_loc_count, dim3(lgrid), dim3(256), 0, st, g, v, eng_->locality_shift(), w.loc_key,
+                       w.loc_cursor);
+    hipLaunchKernelGGL(k_loc_scan, dim3(1), dim3(1024), 0, st, w.loc_cursor);
+    hipLaunchKernelGGL(k_loc_scatter, dim3(lgrid), dim3(256), 0, st, P, (const uint16_t*)w.loc_key, w.loc_cursor, w.perm,
+                       w.loc_inv);
+    RM_HIP(hipMemsetAsync(w.pcnt_part, 0, 2 * sizeof(unsigned long long) * ((P + 255) / 256), st));
+    v.perm = w.perm;
+    v.inv = w.loc_inv; v.pcnt = w.pcnt; v.pcnt_part = w.pcnt_part;
+    if (lmode >= 2) v.perm_paths = w.perm;
+    toc(kKLocality);
+  }
   tic(kKCandidates);
   hipLaunchKernelGGL(k_candidates_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
   hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, g, v);
@@ -3410,6 +3719,11 @@ void Matcher::run_device(const RunParams& rp) {
   hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.tot_part, count_grid, w.tot64);
   hipLaunchKernelGGL(k_scan_apply2, dim3(count_grid), dim3(256), 0, st, (const uint32_t*)w.trans_cnt,
                      (const uint32_t*)w.src_cnt, P, (const unsigned long long*)w.tot_part, w.trans_off, w.src_off);
+  if (v.perm) {   // K2 items in locality order: src_off from a scan of the counts in perm order
+    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.pcnt_part, count_grid, w.tot64 + 2);
+    hipLaunchKernelGGL(k_scan_apply_perm, dim3(count_grid), dim3(256), 0, st, (const uint32_t*)w.pcnt, P,
+                       (const unsigned long long*)w.pcnt_part, (const uint32_t*)w.perm, w.src_off);
+  }
   toc(kKScan);
   RM_HIP(hipMemcpyAsync(htot, w.tot64, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   RM_HIP(hipStreamSynchronize(st));
@@ -3526,7 +3840,7 @@ void Matcher::run_device(const RunParams& rp) {
       RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)eng_->n_segments() * kHistBins * sizeof(uint32_t), st));
     if (rp.dur && rp.zero_hist) RM_HIP(hipMemsetAsync(rp.dur, 0, (size_t)eng_->n_segments() * 8u, st));
     tic(kKReport);
-    hipLaunchKernelGGL(k_report, dim3((T + 63) / 64), dim3(64), 0, st, v, rp.threshold_sec, rp.report_mask,
+    hipLaunchKernelGGL(k_report, dim3(T), dim3(64), 0, st, v, rp.threshold_sec, rp.report_mask,
                        rp.transition_mask, rp.hist, rp.dur);
     toc(kKReport);
   }
@@ -3569,7 +3883,7 @@ void report_segments(int device, uint32_t T, const uint32_t* seg_off, const Segm
   RM_HIP(hipMemcpy(d_thr, threshold, T * 8ull, hipMemcpyHostToDevice));
   RM_HIP(hipMemcpy(d_rm, rmask, T * 4ull, hipMemcpyHostToDevice));
   RM_HIP(hipMemcpy(d_tm, tmask, T * 4ull, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_report_lists, dim3((T + 63) / 64), dim3(64), 0, 0, T, d_off, d_segs, d_end, d_thr, d_rm, d_tm,
+  hipLaunchKernelGGL(k_report_lists, dim3(T), dim3(64), 0, 0, T, d_off, d_segs, d_end, d_thr, d_rm, d_tm,
                      d_reps, d_st);
   RM_HIP(hipGetLastError());
   std::vector<ReportRec> all(S);

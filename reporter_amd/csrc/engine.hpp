@@ -96,7 +96,8 @@ struct RunParams {
 };
 
 // Kernel ids for per-kernel HIP-event timing.
-enum KernelId { kKStates = 0, kKCandidates, kKScan, kKRoutes, kKViterbi, kKPaths, kKSegments, kKReport, kNumKernels };
+enum KernelId { kKStates = 0, kKCandidates, kKScan, kKRoutes, kKViterbi, kKPaths, kKSegments, kKReport, kKLocality,
+                kNumKernels };
 extern const char* const kKernelNames[kNumKernels];
 
 // Device workspace of one batch.  All arrays are indexed by point slot p
@@ -138,6 +139,12 @@ struct Workspace {
   uint32_t* trace_err = nullptr;            // per trace: error bits (kErr*) of that trace alone
   unsigned long long* tot64 = nullptr;      // u64 totals: [0] transitions [1] sources [2] path edges
   unsigned long long* tot_part = nullptr;   // per-block partial pairs of those totals (k_sum_parts folds them)
+  // locality order (engine.hip k_loc_count / k_loc_scatter): the sorted state slots, each slot's
+  // region bucket, the bucket cursors and the item counts in sorted order; allocated on the first
+  // run that uses it (cap_sort slots)
+  uint64_t cap_sort = 0;
+  uint32_t* perm = nullptr; uint16_t* loc_key = nullptr; uint32_t* loc_cursor = nullptr; uint32_t* pcnt = nullptr;
+  uint32_t* loc_inv = nullptr; unsigned long long* pcnt_part = nullptr;
   std::vector<void*> allocs;
   ~Workspace();
   void release();
@@ -267,6 +274,12 @@ class Matcher {
   // reports and their bits are in get_trace_errors().  The reference fails one request
   // (py/reporter_service.py:244-245) or skips one window (py/simple_reporter.py:169-173).
   void set_isolation(bool on) { isolate_ = on; }
+  // Locality order of the stages that read the graph's regional data: 0 slot order, 1 K1 and K2
+  // sorted by region, 2 the path stage too, -1 auto (2 on graphs of Engine::locality_default, 1
+  // for batches sampled every >= 10 s on smaller ones, else 0).  Results are identical in every
+  // mode.  Env RM_LOCALITY sets the initial value.
+  void set_locality(int mode) { locality_ = mode; }
+  bool locality_used() const { return locality_used_; }
   uint32_t error_bits() const { return err_bits_; }   // OR of the last run's per-trace errors
   void get_trace_errors(uint32_t* out);                // n_traces() words
   hipStream_t stream() const { return stream_; }
@@ -310,6 +323,10 @@ class Matcher {
   uint32_t timing_mask_ = 0;   // stages timed by HIP events
   bool has_report_ = false;
   bool isolate_ = false;
+  int locality_ = -1;
+  bool batch_sparse_ = false;     // the last run()'s batch is sampled sparsely (kLocalitySparseS)
+  bool locality_used_ = false;
+  void ensure_sort(uint64_t n);
   uint32_t err_bits_ = 0;
   uint32_t* hctl_ = nullptr;  // pinned host mirror of the control words
   StageBufs sb_;
@@ -354,6 +371,11 @@ class Engine {
   void ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys, uint8_t* preds);
   // K1's grid: each cell of the graph's grid split f x f (1 = the graph's grid)
   uint32_t grid_split() const { return grid_split_; }
+  // locality order by default (Matcher::set_locality -1): graphs whose route tables and cell
+  // records outgrow the L2s; and the shift from K1 grid cells to the coarse sort cells (~500 m)
+  bool locality_default() const { return locality_default_; }
+  uint32_t locality_shift() const { return locality_shift_; }
+  uint32_t locality_bits() const { return locality_bits_; }
 
  private:
   int device_;
@@ -365,6 +387,8 @@ class Engine {
   uint32_t ball_built_ = 0;             // mode bits
   uint32_t ball_gpu_ = 0;               // mode bits built on the GPU
   uint32_t grid_split_ = 1;
+  bool locality_default_ = false;
+  uint32_t locality_shift_ = 0, locality_bits_ = 0;
   uint64_t ball_bytes_ = 0;             // bytes of the tables built so far (all modes)
   bool build_balls_gpu(int mode, uint32_t radius_cm, uint32_t max_keys, uint64_t avail_bytes);
   double ball_info_[5][4] = {};

@@ -313,6 +313,16 @@ class BatchMatcher:
         instead of failing the run; see trace_errors()."""
         _lib.check(_lib.lib().rm_runner_set_isolation(self._h, 1 if on else 0))
 
+    def set_locality(self, mode):
+        """Locality order of K1 / K2 / paths (rm_runner_set_locality): -1 engine default, 0 slot
+        order, 1 sorted by region.  Results are identical either way."""
+        _lib.check(_lib.lib().rm_runner_set_locality(self._h, int(mode)))
+
+    def locality_used(self):
+        v = C.c_int(0)
+        _lib.check(_lib.lib().rm_runner_locality_used(self._h, C.byref(v)))
+        return bool(v.value)
+
     def trace_errors(self):
         """Error bits per trace of the last run (1 candidates, 2 route search, 8 path rebuild)."""
         out = np.zeros(self.sizes()["traces"], np.uint32)
@@ -424,6 +434,13 @@ class MultiMatcher:
             for k, v in bm.sizes().items():
                 out[k] = out.get(k, 0) + v
         return out
+
+    def set_locality(self, mode):
+        for bm in self.bms:
+            bm.set_locality(mode)
+
+    def locality_used(self):
+        return any(bm.locality_used() for bm in self.bms)
 
     def route_tiers(self):
         out = {}

@@ -9,6 +9,8 @@ ap.add_argument("--config", default="C2")
 ap.add_argument("--traces", type=int, default=0)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--split", type=int, default=0, help="also time M concurrent runners (streams) over sub-batches")
+ap.add_argument("--ab-locality", action="store_true", help="also time the same batch with the locality order off / on")
+ap.add_argument("--ab-modes", default="0,1,0,1", help="locality modes the A/B cycles through")
 a = ap.parse_args()
 c = dict(world.CONFIGS[a.config])
 if a.traces:
@@ -38,6 +40,18 @@ for r in range(a.reps):
     print("rerun %.4fs  %.1f Mpts/s  " % (dt, len(tr["lon"]) / dt / 1e6) +
           " ".join("%s=%.2fms" % (k, v[0]) for k, v in kt.items()), flush=True)
 
+if a.ab_locality:
+    for mode in [int(x) for x in a.ab_modes.split(",")]:
+        bm.set_locality(mode)
+        bm.rerun()
+        bm.reset_times()
+        t = time.time()
+        for r in range(a.reps):
+            bm.rerun()
+        dt = (time.time() - t) / a.reps
+        kt = bm.kernel_times()
+        print("locality=%d used=%d %.4fs  %.1f Mpts/s  " % (mode, bm.locality_used(), dt, len(tr["lon"]) / dt / 1e6) +
+              " ".join("%s=%.2fms" % (k, v[0] / a.reps) for k, v in kt.items()), flush=True)
 if a.split > 1:
     import threading
     T = len(tr["trace_off"]) - 1
