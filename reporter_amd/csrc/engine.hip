@@ -42,7 +42,6 @@ namespace {
 
 constexpr uint32_t kEmpty = 0xffffffffu;
 constexpr int kWave = 64;
-constexpr int kSmallH = 256;    // LDS hash slots, fast tier
 constexpr int kBigH = 4096;     // LDS hash slots, retry tier (one source at a time)
 constexpr int kCandH = 256;     // road hash slots in the candidate kernel
 constexpr int kInlinePath = 8;  // path edges stored inline per slot (no allocation)
@@ -79,9 +78,6 @@ struct DevBatch {  // POD view of the workspace for kernels
   // tables meets in one XCD's L2 instead of arriving in trace order from everywhere.
   const uint32_t* perm;
   const uint32_t* perm_paths;   // perm for the path stage too (null: the path stage takes slot order)
-  const uint32_t* inv;          // rank of each slot in perm (null: slot order)
-  uint32_t* pcnt;               // K2 item count of the pair whose source has rank r
-  unsigned long long* pcnt_part;   // their partial sums per 256 ranks (.x of k_scan_parts' pairs)
 };
 
 // A failure that belongs to one trajectory (too many roads in a radius, a search beyond every
@@ -207,8 +203,7 @@ __global__ void __launch_bounds__(1024) k_loc_scan(uint32_t* hist) {
     at += v[i];
   }
 }
-__global__ void __launch_bounds__(256) k_loc_scatter(uint64_t P, const uint16_t* key, uint32_t* cursor, uint32_t* perm,
-                                                     uint32_t* inv) {
+__global__ void __launch_bounds__(256) k_loc_scatter(uint64_t P, const uint16_t* key, uint32_t* cursor, uint32_t* perm) {
   __shared__ uint32_t h[kLocBuckets + 1];
   for (uint32_t q = threadIdx.x; q <= kLocBuckets; q += 256) h[q] = 0u;
   __syncthreads();
@@ -226,15 +221,13 @@ __global__ void __launch_bounds__(256) k_loc_scatter(uint64_t P, const uint16_t*
   __syncthreads();
 #pragma unroll
   for (uint32_t i = 0; i < kLocPerThread; ++i)
-    if (kk[i] != 0xffffu) {
-      const uint32_t r = h[kk[i]] + rk[i];
-      perm[r] = (uint32_t)(p0 + 256u * i);
-      inv[p0 + 256u * i] = r;
-    }
+    if (kk[i] != 0xffffu) perm[h[kk[i]] + rk[i]] = (uint32_t)(p0 + 256u * i);
 }
-// K2 items in locality order: k_trans_count puts each pair's item count at its source state's
-// rank (pcnt, with block partials of the ranks); k_scan_apply_perm scatters the scan's offsets to
-// the pairs' src_off
+// K2 items in locality order: item counts of the pairs whose source is perm[r] (their block
+// partials for the scan; k_scan_apply_perm scatters the offsets to the pairs' src_off).  (Putting
+// the counts at their ranks from k_trans_count instead, with per-256-rank atomics, measured 2-3x
+// slower: the ranks of one region's slots are adjacent, so the atomics pile onto few addresses.)
+__global__ void __launch_bounds__(256) k_perm_src_count(DevBatch b, uint32_t* pcnt, unsigned long long* part);
 __global__ void __launch_bounds__(256) k_scan_apply_perm(const uint32_t* a, uint64_t n, const unsigned long long* part,
                                                          const uint32_t* perm, uint32_t* src_off);
 
@@ -794,6 +787,16 @@ __global__ void __launch_bounds__(256) k_scan_apply4(const uint32_t* a, uint64_t
   }
 }
 
+__global__ void __launch_bounds__(256) k_perm_src_count(DevBatch b, uint32_t* pcnt, unsigned long long* part) {
+  const uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  uint32_t c = 0;
+  if (r < b.P) {   // every lane reaches the block sum (it holds a barrier)
+    const uint64_t q = (uint64_t)b.perm[r] + 1u;   // the pair whose source state is perm[r]
+    c = q < b.P ? b.src_cnt[q] : 0u;               // 0 unless q is a pair of the same trace
+    pcnt[r] = c;
+  }
+  block_sum2_u64(c, 0ull, part);
+}
 __global__ void __launch_bounds__(256) k_scan_apply_perm(const uint32_t* a, uint64_t n, const unsigned long long* part,
                                                          const uint32_t* perm, uint32_t* src_off) {
   __shared__ uint32_t sa[4];
@@ -841,12 +844,6 @@ __global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long l
     }
     b.trans_cnt[p] = c;
     b.src_cnt[p] = ns;
-    if (b.inv) {   // locality order: the count at the rank of the pair's source state (p - 1)
-      const uint32_t r = b.inv[p ? p - 1 : b.P - 1];
-      const uint32_t v = p ? ns : 0u;   // thread 0 covers the last slot, which is no pair's source
-      b.pcnt[r] = v;
-      if (v) atomicAdd(&b.pcnt_part[2 * (r >> 8)], (unsigned long long)v);
-    }
   }
   block_sum2_u64(c, ns, part);
 }
@@ -1190,10 +1187,6 @@ __device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, 
     e = ent[ball_row0(h.x) + s];
     if ((e.x & rmask) == road || e.x == kNone) return e;
   }
-}
-
-__device__ __forceinline__ uint4 ball_first(const uint4* ent, const uint2& h, uint32_t road, bool use) {
-  return use ? ent[ball_row0(h.x) + ball_slot(road, h.y)] : make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
 }
 
 // keys from a row (kKeyInf for an endpoint outside the ball or a road not in the table)
@@ -3378,9 +3371,8 @@ void Workspace::release() {
   for (void* p : allocs) (void)hipFree(p);
   allocs.clear();
   cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = cap_src = cap_sort = 0;
-  perm = loc_cursor = pcnt = loc_inv = nullptr;
+  perm = loc_cursor = pcnt = nullptr;
   loc_key = nullptr;
-  pcnt_part = nullptr;
 }
 
 Matcher::Matcher(Engine* e) : eng_(e) {
@@ -3393,8 +3385,7 @@ void Matcher::ensure_sort(uint64_t n) {
   grow_workspace([&] {
     Workspace& w = ws_;
     if (n <= w.cap_sort && w.perm) return;
-    for (void** q : {(void**)&w.perm, (void**)&w.loc_key, (void**)&w.loc_cursor, (void**)&w.pcnt, (void**)&w.loc_inv,
-                     (void**)&w.pcnt_part}) {
+    for (void** q : {(void**)&w.perm, (void**)&w.loc_key, (void**)&w.loc_cursor, (void**)&w.pcnt}) {
       if (*q) {
         (void)hipFree(*q);
         w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), *q));
@@ -3409,8 +3400,6 @@ void Matcher::ensure_sort(uint64_t n) {
     w.loc_key = dalloc<uint16_t>(L, c);                 // region bucket per slot
     w.loc_cursor = dalloc<uint32_t>(L, kLocBuckets + 1);  // bucket counts -> cursors
     w.pcnt = dalloc<uint32_t>(L, c);
-    w.loc_inv = dalloc<uint32_t>(L, c);
-    w.pcnt_part = dalloc<unsigned long long>(L, 2 * ((c + 255) / 256) + 2);
     w.cap_sort = c;
   });
 }
@@ -3591,7 +3580,6 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.rl_routes_c = w.rl_routes_c; v.rl_paths_c = w.rl_paths_c; v.trace_err = w.trace_err;
   v.perm = nullptr;   // run_device sets it when the locality order is on
   v.perm_paths = nullptr;
-  v.inv = nullptr; v.pcnt = nullptr; v.pcnt_part = nullptr;
   return v;
 }
 
@@ -3702,11 +3690,8 @@ void Matcher::run_device(const RunParams& rp) {
     hipLaunchKernelGGL(k_loc_count, dim3(lgrid), dim3(256), 0, st, g, v, eng_->locality_shift(), w.loc_key,
                        w.loc_cursor);
     hipLaunchKernelGGL(k_loc_scan, dim3(1), dim3(1024), 0, st, w.loc_cursor);
-    hipLaunchKernelGGL(k_loc_scatter, dim3(lgrid), dim3(256), 0, st, P, (const uint16_t*)w.loc_key, w.loc_cursor, w.perm,
-                       w.loc_inv);
-    RM_HIP(hipMemsetAsync(w.pcnt_part, 0, 2 * sizeof(unsigned long long) * ((P + 255) / 256), st));
+    hipLaunchKernelGGL(k_loc_scatter, dim3(lgrid), dim3(256), 0, st, P, (const uint16_t*)w.loc_key, w.loc_cursor, w.perm);
     v.perm = w.perm;
-    v.inv = w.loc_inv; v.pcnt = w.pcnt; v.pcnt_part = w.pcnt_part;
     if (lmode >= 2) v.perm_paths = w.perm;
     toc(kKLocality);
   }
@@ -3720,9 +3705,10 @@ void Matcher::run_device(const RunParams& rp) {
   hipLaunchKernelGGL(k_scan_apply2, dim3(count_grid), dim3(256), 0, st, (const uint32_t*)w.trans_cnt,
                      (const uint32_t*)w.src_cnt, P, (const unsigned long long*)w.tot_part, w.trans_off, w.src_off);
   if (v.perm) {   // K2 items in locality order: src_off from a scan of the counts in perm order
-    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.pcnt_part, count_grid, w.tot64 + 2);
+    hipLaunchKernelGGL(k_perm_src_count, dim3(count_grid), dim3(256), 0, st, v, w.pcnt, w.tot_part);
+    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.tot_part, count_grid, w.tot64 + 2);
     hipLaunchKernelGGL(k_scan_apply_perm, dim3(count_grid), dim3(256), 0, st, (const uint32_t*)w.pcnt, P,
-                       (const unsigned long long*)w.pcnt_part, (const uint32_t*)w.perm, w.src_off);
+                       (const unsigned long long*)w.tot_part, (const uint32_t*)w.perm, w.src_off);
   }
   toc(kKScan);
   RM_HIP(hipMemcpyAsync(htot, w.tot64, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));

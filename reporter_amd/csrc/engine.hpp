@@ -144,7 +144,6 @@ struct Workspace {
   // run that uses it (cap_sort slots)
   uint64_t cap_sort = 0;
   uint32_t* perm = nullptr; uint16_t* loc_key = nullptr; uint32_t* loc_cursor = nullptr; uint32_t* pcnt = nullptr;
-  uint32_t* loc_inv = nullptr; unsigned long long* pcnt_part = nullptr;
   std::vector<void*> allocs;
   ~Workspace();
   void release();
