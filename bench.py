@@ -240,6 +240,47 @@ def request_jsons(tr, n):
             for k in range(n)], P
 
 
+def window_requests(tr, n_req, n_pts):
+    """/report requests of n_pts consecutive points each, cut from the traces in order (the Java
+    batcher posts a vehicle's points once it has >= 10 points, >= 500 m and >= 60 s,
+    BatchingProcessor.java:26-29,69: ~60 points at 1 Hz)."""
+    import numpy as np
+    off = tr["trace_off"].astype(np.int64)
+    out, P = [], 0
+    f = '{"lat":%.6f,"lon":%.6f,"time":%d,"accuracy":%g}'
+    mo = '"match_options":{"mode":"auto","report_levels":[0,1],"transition_levels":[0,1]}'
+    for k in range(len(off) - 1):
+        for a in range(int(off[k]), int(off[k + 1]) - n_pts + 1, n_pts):
+            pts = ",".join(f % (tr["lat"][i], tr["lon"][i], int(tr["time"][i]), tr["accuracy"][i])
+                           for i in range(a, a + n_pts))
+            out.append('{"uuid":"%d-%d","trace":[%s],%s}' % (k, a, pts, mo))
+            P += n_pts
+            if len(out) >= n_req:
+                return out, P
+    return out, P
+
+
+def client_service(gpath, tmpdir, reqs, clients, n, warmup, workers=None):
+    """The C-ABI service client (reporter_amd/bin/rm_svc_client): `clients` threads, one
+    rm_matcher each, rm_match on `n` requests with coalescing on; no Python between calls."""
+    import valhalla
+    from reporter_amd import build as B
+    rfile = os.path.join(tmpdir, "reporter_bench_reqs_%d.txt" % os.getpid())
+    with open(rfile, "w") as f:
+        for r in reqs:
+            f.write((r.decode() if isinstance(r, bytes) else r) + "\n")
+    conf = valhalla.write_config(os.path.join(tmpdir, "reporter_bench_cli_%d.json" % os.getpid()), gpath, device=0,
+                                 coalesce=True, coalesce_workers=workers)
+    try:
+        r = subprocess.run([B.CLIENT, conf, rfile, str(clients), str(n), str(warmup)], capture_output=True, text=True,
+                           timeout=600)
+    finally:
+        os.remove(rfile)
+    if r.returncode != 0:
+        return {"error": (r.stderr or r.stdout)[-400:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def extras(gpath, tr, json_traces, tmpdir):
     """C1's defining measurement (single-trace latency through rm_match) and the JSON-boundary
     throughput of rm_match_batch (PCIe + parse + serialize inclusive), both through the drop-in
@@ -264,11 +305,30 @@ def extras(gpath, tr, json_traces, tmpdir):
         r = sm.Match(req)
         lat.append((time.perf_counter() - t) * 1e3)
     lat.sort()
+    # BASELINE configs[0] itself: the CPU path on the same trace (the oracle, one core: match +
+    # report(), the work reporter_service.py does per request; real meili cannot run here)
+    import numpy as np
+    import meili_oracle as mo
+    from reporter_amd import engine as E, graphfile
+    g1 = graphfile.load(c1g)
+    b1 = mo.Batch(c1tr["trace_off"], c1tr["lon"], c1tr["lat"], c1tr["time"], c1tr["accuracy"], E.default_options(1),
+                  np.zeros(1, np.uint32))
+    cpu_ms = []
+    for _ in range(5):
+        hist1 = np.zeros(len(g1["seg_id"]) * 16, np.uint32)
+        t = time.perf_counter()
+        mo.pipeline(g1, b1, 15.0, 0x6, 0x6, hist1)
+        cpu_ms.append((time.perf_counter() - t) * 1e3)
+    cpu_ms.sort()
     out["c1_latency"] = {"what": "one 1,000-point 1 Hz trace (C1: 40x40 grid @100 m) through valhalla.SegmentMatcher()"
                                  ".Match -> rm_match (JSON in, JSON out; request coalescing on, one request in flight)",
                          "median_ms": lat[len(lat) // 2], "p90_ms": lat[int(len(lat) * 0.9)], "min_ms": lat[0],
                          "segments": len(json.loads(r)["segments"]), "caller_budget_ms": 10000,
-                         "caller_budget_source": "HttpClient.java:80-87 (10 s socket timeout)"}
+                         "caller_budget_source": "HttpClient.java:80-87 (10 s socket timeout)",
+                         "cpu_port_ms": {"median": cpu_ms[len(cpu_ms) // 2], "min": cpu_ms[0], "cores": 1,
+                                         "what": "the oracle (C port of the matcher) + report() + histogram on the "
+                                                 "same trace, one core, arrays in memory (no JSON): BASELINE "
+                                                 "configs[0]'s CPU path"}}
     sm.close()
     os.remove(c1g)
     # JSON boundary: the rank's C2 traces as /report JSON through rm_match_batch
@@ -304,16 +364,19 @@ def extras(gpath, tr, json_traces, tmpdir):
     # shared batches; at 64 and 256 requests in flight (a batch takes a few ms whatever its size,
     # so the throughput follows the number of requests in flight)
     n_req = min(len(reqs), 4096)
-    for workers, n_cli in ((1, 64), (1, 256)):
+    r60_py, _ = window_requests(tr, 8192, 60)
+    for workers, n_cli, rq in ((1, 64, reqs), (1, 256, reqs), (1, 64, [x.encode() for x in r60_py])):
         conf = valhalla.write_config(os.path.join(tmpdir, "reporter_bench_svc_%d.json" % os.getpid()), gpath, device=0,
                                      coalesce=True, coalesce_workers=workers)
         valhalla.Configure(conf)
         done = [0] * n_cli
 
+        nq = min(len(rq), 8192 if rq is not reqs else n_req)
+
         def client(c):
             m = valhalla.SegmentMatcher()
-            for q in range(c, n_req, n_cli):
-                m.Match(reqs[q])
+            for q in range(c, nq, n_cli):
+                m.Match(rq[q])
                 done[c] += 1
             m.close()
 
@@ -325,12 +388,25 @@ def extras(gpath, tr, json_traces, tmpdir):
         for th in ths:
             th.join()
         dt = time.perf_counter() - t
-        pts = int(tr["trace_off"][min(n_req, len(tr["trace_off"]) - 1)])
-        key = "service_throughput" if n_cli == 64 else "service_throughput_%d_clients" % n_cli
+        npt = 600 if rq is reqs else 60
+        pts = sum(done) * npt
+        key = "service_throughput" if (n_cli == 64 and npt == 600) else "service_throughput_%d_clients%s" % (
+            n_cli, "" if npt == 600 else "_60pt")
         out[key] = {
-            "what": "%d C2 /report requests (600 points each) from %d client threads through valhalla.SegmentMatcher()"
-                    ".Match with request coalescing, %d dispatcher(s)" % (sum(done), n_cli, workers),
+            "what": "%d C2 /report requests (%d points each) from %d Python client threads through "
+                    "valhalla.SegmentMatcher().Match with request coalescing, %d dispatcher(s)" % (
+                        sum(done), npt, n_cli, workers),
             "requests_per_s": sum(done) / dt, "points_per_s": pts / dt, "seconds": dt}
+    # the library's own ceiling under concurrent load: the C-ABI client (no GIL), 600-point C2
+    # requests and the Java batcher's ~60-point requests, 64 and 256 requests in flight
+    r60, p60 = window_requests(tr, 20000, 60)
+    for name, rq, nreq, cl in (("service_client_600pt_64", reqs, 8192, 64), ("service_client_600pt_256", reqs, 8192, 256),
+                               ("service_client_60pt_64", r60, 20000, 64), ("service_client_60pt_256", r60, 20000, 256)):
+        res = client_service(gpath, tmpdir, rq, cl, nreq, min(2048, nreq // 4))
+        res["what"] = ("reporter_amd/bin/rm_svc_client: %d C threads, one rm_matcher each, rm_match (coalescing on) on "
+                       "%d-point /report requests; the library's ceiling with no interpreter between calls"
+                       % (cl, 600 if "600" in name else 60))
+        out[name] = res
     return out
 
 

@@ -59,6 +59,10 @@ int rm_matcher_timing(const rm_matcher* m, double out[6]);
  * previous batch ran) and "coalesce_max_traces" (16384) shape the batches.
  * out: [0] batches run [1] requests served [2] largest batch [3] requests queued now. */
 int rm_coalesce_stats(uint64_t out[4]);
+/* Dispatcher wall time (ms, summed over the batches since rm_configure): [0] staging the parsed
+ * points into pinned memory, [1] the engine run (uploads, kernels, size read-backs), [2] the
+ * segment download, [3] reply formatting.  Parsing runs on the calling threads, not here. */
+int rm_coalesce_timing(double out[4]);
 
 /* ---------------- matcher options (layout of rm::MatchOptions) ---------------- */
 typedef struct {

@@ -91,6 +91,7 @@ PROTOTYPES = [
     ("rm_free", None, [P]),
     ("rm_matcher_timing", C.c_int, [P, P]),
     ("rm_coalesce_stats", C.c_int, [C.POINTER(C.c_uint64)]),
+    ("rm_coalesce_timing", C.c_int, [C.POINTER(C.c_double)]),
     ("rm_default_options", None, [C.POINTER(RmOptions)]),
     ("rm_default_world_params", None, [C.POINTER(RmWorldParams)]),
     ("rm_world_build", C.c_int, [C.POINTER(RmWorldParams), C.c_char_p]),

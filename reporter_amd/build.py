@@ -71,7 +71,26 @@ def build(force=False, verbose=False):
             raise RuntimeError("link failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
         if verbose:
             print("built", LIB)
+    build_tools(force)
     return LIB
+
+
+CLIENT = os.path.join(HERE, "bin", "rm_svc_client")
+
+
+def build_tools(force=False):
+    """The multi-threaded C-ABI service client bench.py measures the library with (no Python
+    between the calls): reporter_amd/bin/rm_svc_client, linked against the in-tree library."""
+    src = os.path.join(CSRC, "svc_client.cpp")
+    os.makedirs(os.path.dirname(CLIENT), exist_ok=True)
+    if not force and not _newer(CLIENT, [src, LIB, os.path.join(ROOT, "include", "reporter_match.h")]):
+        return CLIENT
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", src, "-o", CLIENT, "-L" + HERE, "-lreporter_match",
+           "-Wl,-rpath,$ORIGIN/..", "-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("client build failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
+    return CLIENT
 
 
 def build_oracle(force=False):

@@ -142,6 +142,7 @@ struct MatchRequest {
   ParsedTrace* trace;
   std::string out, err;
   bool done = false;
+  std::condition_variable cv;   // its caller waits here alone (no herd wake-up per batch)
 };
 
 class Coalescer {
@@ -170,13 +171,17 @@ class Coalescer {
     }
     cv_req_.notify_one();
     std::unique_lock<std::mutex> lk(mu_);
-    cv_done_.wait(lk, [&] { return r.done; });
+    r.cv.wait(lk, [&] { return r.done; });
     if (!r.err.empty()) throw std::runtime_error(r.err);
     return std::move(r.out);
   }
   void stats(uint64_t out[4]) {
     std::lock_guard<std::mutex> lk(mu_);
     out[0] = batches_; out[1] = requests_; out[2] = max_seen_; out[3] = (uint64_t)q_.size();
+  }
+  void timing(double out[4]) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int i = 0; i < 4; ++i) out[i] = tm_[i];
   }
 
  private:
@@ -185,10 +190,11 @@ class Coalescer {
   double window_ms_;
   size_t max_;
   std::mutex mu_;
-  std::condition_variable cv_req_, cv_done_;
+  std::condition_variable cv_req_;
   std::deque<MatchRequest*> q_;
   bool stop_ = false;
   uint64_t batches_ = 0, requests_ = 0, max_seen_ = 0;
+  double tm_[4] = {0, 0, 0, 0};   // dispatcher wall ms: staging, engine, download, formatting
   std::vector<std::thread> th_;
 };
 
@@ -208,8 +214,8 @@ struct HostStaging {
   size_t cap = 0;
   void ensure(size_t n) {
     if (n <= cap) return;
+    const size_t c = std::max(n + n / 4, cap + cap / 2) + 4096;
     release();
-    const size_t c = n + n / 4 + 4096;
     RM_HIP(hipHostMalloc((void**)&lon, c * 4, hipHostMallocDefault));
     RM_HIP(hipHostMalloc((void**)&lat, c * 4, hipHostMallocDefault));
     RM_HIP(hipHostMalloc((void**)&acc, c * 4, hipHostMallocDefault));
@@ -232,9 +238,9 @@ struct HostStaging {
 // parse and formatting around a batch are host work that a single thread makes the boundary's
 // limit); an exception is rethrown for the lowest failing index's chunk, as a serial loop would
 template <class F>
-void parallel_for(size_t n, F&& fn) {
+void parallel_for(size_t n, F&& fn, size_t per = 32) {
   HostPool& pool = HostPool::get();
-  const size_t nt = std::min<size_t>(pool.size(), (n + 31) / 32);
+  const size_t nt = std::min<size_t>(pool.size(), (n + per - 1) / per);
   if (nt <= 1) {
     for (size_t i = 0; i < n; ++i) fn(i);
     return;
@@ -245,7 +251,13 @@ void parallel_for(size_t n, F&& fn) {
   });
 }
 
-std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*>& pt, std::vector<std::string>* errs) {
+// tm (may be null) accumulates host wall ms: [0] staging, [1] engine run, [2] segment download,
+// [3] reply formatting
+std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*>& pt, std::vector<std::string>* errs,
+                                      double* tm = nullptr) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  clk::time_point t0 = clk::now();
   const size_t n = pt.size();
   std::vector<uint32_t> off(n + 1, 0), topt(n);
   std::vector<MatchOptions> opts(n);
@@ -270,12 +282,15 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
   RunParams rp;
   rp.do_report = 0;
   m.set_isolation(true);
+  if (tm) { tm[0] += ms_since(t0); t0 = clk::now(); }
   m.run(hb, rp);
+  if (tm) { tm[1] += ms_since(t0); t0 = clk::now(); }
   std::vector<uint32_t> terr(n, 0u);
   if (m.error_bits()) m.get_trace_errors(terr.data());
-  std::vector<uint32_t> soff(n + 1);
-  std::vector<SegmentRec> segs(m.count_segments());
-  m.get_segments(soff.data(), segs.data());
+  std::vector<uint32_t> soff;
+  std::vector<SegmentRec> segs;
+  m.get_segments(soff, segs);
+  if (tm) { tm[2] += ms_since(t0); t0 = clk::now(); }
   std::vector<std::string> out(n);
   if (errs) errs->assign(n, std::string());
   for (size_t i = 0; i < n; ++i) {
@@ -283,9 +298,11 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
     if (!errs) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
     (*errs)[i] = error_text(terr[i]);
   }
+  // replies of a coalesced batch (tens of requests, ~10 us each) over the pool in chunks of 4
   parallel_for(n, [&](size_t i) {
     if (!terr[i]) tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], out[i]);
-  });
+  }, 4);
+  if (tm) tm[3] += ms_since(t0);
   return out;
 }
 
@@ -293,7 +310,7 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
 // reported per trace by the engine; a whole-batch failure follows serve_policy.hpp: a batch too
 // large for the device is retried by halves (bounded), any other error fails every request in
 // it at once.  A failed run drops the matcher, so what follows starts on a fresh workspace.
-void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch) {
+void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch, double* tm) {
   int budget = kServeRetryBudget;
   auto run = [&](MatchRequest* const* reqs, size_t n) {
     try {
@@ -301,7 +318,7 @@ void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<Mat
       std::vector<ParsedTrace*> pt(n);
       for (size_t i = 0; i < n; ++i) pt[i] = reqs[i]->trace;
       std::vector<std::string> errs;
-      std::vector<std::string> outs = match_parsed(*m, pt, &errs);
+      std::vector<std::string> outs = match_parsed(*m, pt, &errs, tm);
       for (size_t i = 0; i < n; ++i) {
         if (!errs[i].empty()) reqs[i]->err = errs[i];
         else reqs[i]->out = std::move(outs[i]);
@@ -332,12 +349,16 @@ void Coalescer::loop() {
       requests_ += batch.size();
       max_seen_ = std::max<uint64_t>(max_seen_, batch.size());
     }
-    serve_batch(m, eng_.get(), batch);   // fills out / err of each request (not under the lock)
+    double tm[4] = {0, 0, 0, 0};
+    serve_batch(m, eng_.get(), batch, tm);   // fills out / err of each request (not under the lock)
     {
       std::lock_guard<std::mutex> lk(mu_);
-      for (MatchRequest* r : batch) r->done = true;
+      for (MatchRequest* r : batch) {
+        r->done = true;
+        r->cv.notify_one();   // under the lock: the request (and its cv) lives until its caller returns
+      }
+      for (int i = 0; i < 4; ++i) tm_[i] += tm[i];
     }
-    cv_done_.notify_all();
   }
 }
 
@@ -421,9 +442,9 @@ void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char**
     if (terr[i]) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
   m->ms[2] = ms_since(t2);
   const auto t3 = clk::now();
-  std::vector<uint32_t> soff(n + 1);
-  std::vector<SegmentRec> segs(mt.count_segments());
-  mt.get_segments(soff.data(), segs.data());
+  std::vector<uint32_t> soff;
+  std::vector<SegmentRec> segs;
+  mt.get_segments(soff, segs);
   m->ms[3] = ms_since(t3);
   const auto t4 = clk::now();
   pool.run(nt, [&](size_t t) {
@@ -507,7 +528,10 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
     bool coalesce = true;
     double window_ms = 0.0;
     size_t max_traces = 16384;
-    int workers = 1;   // reporter_amd.coalesce_workers (2 measured no faster: 18.1k vs 19.8k C2 requests/s)
+    // reporter_amd.coalesce_workers: dispatcher threads, each a matcher on its own stream, so one
+    // batch's latency-bound kernels overlap the next batch's (C-ABI client, 64 clients of 600-point
+    // requests: 1 -> 2 workers 23 -> 30 M points/s; round 3's Python clients saw no gain)
+    int workers = 2;
     double ball_radius_m = -1.0;   // < 0: engine default (automatic from the graph's density, or RM_BALL_RADIUS_M)
     if (const json::Value* ra = v.get("reporter_amd")) {
       if (const json::Value* br = ra->get("ball_radius"); br && br->is_num()) {
@@ -604,6 +628,18 @@ int rm_matcher_timing(const rm_matcher* m, double out[6]) {
   return guarded([&] {
     if (!m || !out) throw std::runtime_error("matcher or out is NULL");
     for (int i = 0; i < 6; ++i) out[i] = m->ms[i];
+  });
+}
+
+int rm_coalesce_timing(double out[4]) {
+  return guarded([&] {
+    std::shared_ptr<Config> c;
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      c = g_conf;
+    }
+    for (int i = 0; i < 4; ++i) out[i] = 0.0;
+    if (c && c->coalescer) c->coalescer->timing(out);
   });
 }
 

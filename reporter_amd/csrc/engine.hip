@@ -28,6 +28,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 #include <type_traits>
 
@@ -2172,7 +2173,313 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
 }
 
 
+// ------------------------------------------------------------------------------------------
+// K3 (round 2, v3): one wave per trace, one lane per transition.  A layer's K_A x K_B
+// transitions are spread over the wave as lane = (target j, source i) with W = 4, 8 or 16
+// source lanes per target (the smallest power of two >= K_A; 64/W targets per pass, one pass
+// for K_A <= 4 or K_A, K_B <= 8): every transition costs one fused multiply-add at once, the
+// minimum over sources is a DPP butterfly inside the W lanes (quad_perm, row_half_mirror,
+// row_mirror) and the arg-min a ballot of "c == min" (first set bit = lowest i, the strict-<
+// scan's tie rule).  10,000 C2 traces are 10,000 independent waves (8 per SIMD resident), so
+// the per-layer latency chain (LDS read -> fma -> butterfly -> ballot -> LDS write) of one
+// trace hides behind the others; all control flow is wave-uniform (scalar branches).
+// Routes reach LDS per chunk of <= 16 layers / kV3Routes routes as fp64 metres (+inf when
+// invalid, an +inf sentinel for idle lanes); the next chunk's routes and emission rows are
+// loaded into registers while this chunk runs, and the chunk after that is described then.
+// Measured on C2 (bit-exact): 1.01 ms against 0.75 ms for k_viterbi.  Per trace-layer it issues
+// 65 VALU + 70 SALU + 10 LDS instructions against 48 + 22 + 5 (C2's typical layer has K = 4,
+// so 16 of 64 lanes work either way, and the wave-uniform control is paid per trace instead of
+// per four), and 10,000 waves need two rounds of 8 per SIMD (8,000 traces: 0.75 ms).  Round 4:
+// it runs the small batches (launch_viterbi below), where its shorter layer chain wins.
+#ifndef RM_VIT3_WPE
+#define RM_VIT3_WPE 8
+#endif
+constexpr int kV3Routes = 384;               // routes per staged chunk
+constexpr int kV3Chunk = 16;                 // layers per staged chunk (one per lane 0..15)
+constexpr int kV3Regs = kV3Routes / kWave;   // route registers per lane for the next chunk
+struct Vit3Smem {
+  union {
+    double route_m[kV3Routes + 2];           // [kV3Routes] = +inf: the route of an idle lane
+    struct {
+      uint4 bst[kWave];                      // backtrace staging (64 back-pointer rows)
+      uint8_t ch[kWave];
+    } bt;
+  };
+  float sq[kV3Chunk][kMaxCand];
+  double cost[2][kMaxCand];                  // previous / next layer costs (ping-pong)
+  uint4 bpo[kV3Chunk];                       // this chunk's back-pointer rows
+  uint8_t cs[kV3Chunk];                      // this chunk's chain-start flags
+  uint32_t nch, done, w, pad;
+};
+static_assert(sizeof(Vit3Smem) <= 5120, "K3 v3 must keep 8 waves per SIMD (32 per CU) within LDS");
+
+struct V3Chunk {
+  uint32_t s0, C, nroutes, rbase;
+  uint32_t kbrel;   // lane t < C: K_B of layer s0 + t | offset of its routes in the chunk << 8
+  double gc;        // lane t < C: gc of layer s0 + t
+};
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// minimum over each aligned group of W lanes, in every lane of the group (all lanes active)
+template <int W>
+__device__ __forceinline__ double group_min(double c) {
+  c = __builtin_fmin(c, dpp_d<0xB1>(c));                      // quad_perm [1,0,3,2]
+  c = __builtin_fmin(c, dpp_d<0x4E>(c));                      // quad_perm [2,3,0,1]
+  if constexpr (W >= 8) c = __builtin_fmin(c, dpp_d<0x141>(c));   // row_half_mirror (x <-> 7-x)
+  if constexpr (W >= 16) c = __builtin_fmin(c, dpp_d<0x140>(c));  // row_mirror (x <-> 15-x)
+  return c;
+}
+
+__device__ __forceinline__ double readlane_d(double v, uint32_t l) {
+  const unsigned long long u = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), (int)l);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// chunk from s0: lanes 0..15 describe layers s0..s0+15 (d); the leading layers whose routes
+// fit kV3Routes form the chunk (at least one: a layer holds <= 256 routes)
+__device__ __forceinline__ V3Chunk v3_layout(const VitLayerDesc& d, uint32_t s0, uint32_t S, int lane) {
+  const int j = lane & 15;
+  uint32_t incl = d.cnt;
+#pragma unroll
+  for (int x = 1; x < 16; x <<= 1) {
+    const uint32_t u = __shfl_up(incl, x, 16);
+    if (j >= x) incl += u;
+  }
+  const uint32_t fit = (uint32_t)(__ballot(lane < 16 && s0 + (uint32_t)lane < S && incl <= (uint32_t)kV3Routes) & 0xffffull);
+  V3Chunk c;
+  c.s0 = s0;
+  // wave-uniform values live in SGPRs (the layer loop and its branches are scalar)
+  c.C = (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_ctz(~fit | 0x10000u));
+  c.nroutes = (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)c.C - 1);
+  c.rbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.off);
+  c.kbrel = d.kb | ((incl - d.cnt) << 8);
+  c.gc = d.gc;
+  return c;
+}
+
+__device__ __forceinline__ void v3_load(const DevBatch& b, uint32_t o, const V3Chunk& c, int lane,
+                                        uint32_t (&rv)[kV3Regs], float4& sv) {
+  const uint32_t rlast = c.nroutes ? c.nroutes - 1u : 0u;
+#pragma unroll
+  for (int x = 0; x < kV3Regs; ++x) {
+    rv[x] = kRouteInvalid;
+    if ((uint32_t)(kWave * x) < c.nroutes) rv[x] = b.route[c.rbase + min((uint32_t)(lane + kWave * x), rlast)];
+  }
+  const float4* src = reinterpret_cast<const float4*>(b.cand_sq) + (uint64_t)(o + c.s0) * (kMaxCand / 4);
+  sv = src[min((uint32_t)lane, c.C * (kMaxCand / 4) - 1u)];
+}
+
+__device__ __forceinline__ void v3_stage_routes(Vit3Smem& sm, const V3Chunk& c, int lane, const uint32_t (&rv)[kV3Regs]) {
+  const double INF = __longlong_as_double(0x7ff0000000000000ll);
+#pragma unroll
+  for (int x = 0; x < kV3Regs; ++x)
+    if ((uint32_t)(lane + kWave * x) < c.nroutes) sm.route_m[lane + kWave * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
+}
+
+// back-pointer rows / chain flags of chunk layers [0, n) to HBM
+__device__ __forceinline__ void v3_flush(const DevBatch& b, const Vit3Smem& sm, uint64_t l0, uint32_t n, int lane) {
+  if ((uint32_t)lane < n) {
+    *reinterpret_cast<uint4*>(b.bp + (l0 + lane) * kMaxCand) = sm.bpo[lane];
+    b.chain_start[l0 + lane] = sm.cs[lane];
+  }
+}
+
+// Backtrace of the chain ending at layer `end` whose costs are sm.cost[cb][0..K): winner =
+// lowest cost, ties to the lowest j; rows staged 64 layers at a time, lane 0 walks them.
+__device__ void v3_backtrace(const DevBatch& b, Vit3Smem& sm, uint32_t o, uint32_t end, uint32_t K, int cb, int lane) {
+  const double INF = __longlong_as_double(0x7ff0000000000000ll);
+  const double c = (uint32_t)lane < K ? sm.cost[cb][lane & 15] : INF;
+  const double m = group_min<16>(c);
+  const uint32_t eq = (uint32_t)(__ballot((uint32_t)lane < K && c == m) & 0xffffull);
+  uint32_t w = (uint32_t)__builtin_ctz(eq | 0x10000u);
+  __threadfence_block();  // this wave's bp stores are visible to its loads
+  int t = (int)end;
+  for (;;) {
+    const int lay = t - lane;
+    uint4 row = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+    if (lay >= 0) row = *reinterpret_cast<const uint4*>(b.bp + (uint64_t)(o + lay) * kMaxCand);
+    sm.bt.bst[lane] = row;
+    wave_sync();
+    if (lane == 0) {
+      uint32_t l = 0, done = 0;
+      for (; l < (uint32_t)kWave && t - (int)l >= 0;) {
+        sm.bt.ch[l] = (uint8_t)w;
+        const uint32_t nb = reinterpret_cast<const uint8_t*>(&sm.bt.bst[l])[w];
+        ++l;
+        if (nb == 255u) { done = 1; break; }
+        w = nb;
+      }
+      if (t - (int)l < 0) done = 1;
+      sm.nch = l; sm.done = done; sm.w = w;
+    }
+    wave_sync();
+    const uint32_t n = sm.nch;
+    if ((uint32_t)lane < n) b.choice[o + t - lane] = (int8_t)sm.bt.ch[lane];
+    const bool done = sm.done != 0;
+    w = sm.w;
+    t -= (int)n;
+    wave_sync();
+    if (done) break;
+  }
+}
+
+// one pass of layer t over targets [j0, j0 + 64/W): lane = (target j0 + lane/W, source lane%W);
+// heads (source lane 0) write the target's new cost and back-pointer byte
+template <int W>
+__device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, int lane, uint32_t j0, uint32_t KB, uint32_t KA,
+                                                      uint32_t rel, double gcl, double inv_beta, double inv2s2, int cb,
+                                                      uint32_t t) {
+  const double INF = __longlong_as_double(0x7ff0000000000000ll);
+  const uint32_t i = (uint32_t)lane & (W - 1), j = j0 + ((uint32_t)lane / W);
+  const bool valid = i < KA && j < KB;
+  const double rm = sm.route_m[valid ? rel + i * KB + j : (uint32_t)kV3Routes];
+  const double ci = sm.cost[cb][i];
+  // fma(|route_m - gc|, 1/beta, cost of source i): one rounding, as the oracle; an invalid
+  // route, an unreachable source and an idle lane are +inf
+  const double c = __builtin_fma(fabs(rm - gcl), inv_beta, ci);
+  const double m = group_min<W>(c);
+  const unsigned long long eq = __ballot(c == m && m < INF);
+  const uint32_t g = (uint32_t)(eq >> ((uint32_t)lane & ~(uint32_t)(W - 1))) & ((1u << W) - 1u);
+  const int arg = g ? __builtin_ctz(g) : -1;
+  const bool head = i == 0u && j < KB;
+  if (head) {
+    const double em = (double)sm.sq[t][j] * inv2s2;
+    sm.cost[cb ^ 1][j] = arg >= 0 ? m + em : INF;
+    reinterpret_cast<uint8_t*>(&sm.bpo[t])[j] = arg >= 0 ? (uint8_t)arg : (uint8_t)255;
+  }
+  return __ballot(head && arg >= 0);
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3_WPE))) k_viterbi_w(DevBatch b) {
+  __shared__ Vit3Smem sm;
+  const int lane = threadIdx.x;
+  const uint32_t k = blockIdx.x;
+  const uint32_t o = b.trace_off[k], S = b.n_states[k];
+  const MatchOptions op = b.opts[b.trace_opt[k]];
+  const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
+  const double inv_beta = 1.0 / (double)op.beta;
+  const double brk = (double)op.breakage_distance;
+  const double INF = __longlong_as_double(0x7ff0000000000000ll);
+  if (lane < 2 * kMaxCand) (&sm.cost[0][0])[lane] = INF;
+  if (lane == 0) sm.route_m[kV3Routes] = INF;
+  if (S == 0) return;
+  // chunk 0: describe, lay out, load; then describe chunk 1
+  V3Chunk cur = v3_layout(vit_describe(b, o, S, 0, lane & 15), 0, S, lane);
+  uint32_t rv[kV3Regs];
+  float4 sv;
+  v3_load(b, o, cur, lane, rv, sv);
+  VitLayerDesc dn{0u, 0u, 0u, 0.0};
+  if (cur.C < S) dn = vit_describe(b, o, S, cur.C, lane & 15);
+  bool prev_ok = false;
+  uint32_t prevK = 0;
+  int cb = 0;
+  for (;;) {
+    v3_stage_routes(sm, cur, lane, rv);
+    if ((uint32_t)lane < cur.C * (kMaxCand / 4)) reinterpret_cast<float4*>(&sm.sq[0][0])[lane] = sv;
+    // the next chunk's routes and emission rows load while this chunk runs
+    const uint32_t s1 = cur.s0 + cur.C;
+    const bool has_next = s1 < S;
+    V3Chunk nx{};
+    if (has_next) {
+      nx = v3_layout(dn, s1, S, lane);
+      v3_load(b, o, nx, lane, rv, sv);
+      if (s1 + nx.C < S) dn = vit_describe(b, o, S, s1 + nx.C, lane & 15);
+    }
+    wave_sync();
+    for (uint32_t t = 0; t < cur.C; ++t) {
+      const uint32_t s = cur.s0 + t;
+      int lane = threadIdx.x;
+      __asm__ volatile("" : "+v"(lane));   // per-pass lane maps are recomputed, not held in VGPRs
+      const uint32_t kr = (uint32_t)__builtin_amdgcn_readlane((int)cur.kbrel, (int)t);
+      const uint32_t KB = kr & 0xffu, rel = kr >> 8;
+      const double gcl = readlane_d(cur.gc, t);
+      if (lane == 0) sm.bpo[t] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+      bool start = !prev_ok || (s > 0 && gcl > brk);
+      if (KB && !start) {
+        unsigned long long any = 0ull;
+        if (prevK <= 4u) {
+          any = v3_pass<4>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+        } else if (prevK <= 8u) {
+          any = v3_pass<8>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          if (KB > 8u) any |= v3_pass<8>(sm, lane, 8u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+        } else {
+          for (uint32_t j0 = 0; j0 < KB; j0 += 4u)
+            any |= v3_pass<16>(sm, lane, j0, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+        }
+        if (any == 0ull) start = true;   // no valid transition into this layer
+      }
+      if (s > 0 && prev_ok && (KB == 0 || start)) {
+        // the chain ending at layer s - 1 is complete: its rows [.., s) must be in HBM
+        wave_sync();
+        v3_flush(b, sm, o + cur.s0, t, lane);
+        v3_backtrace(b, sm, o, s - 1, prevK, cb, lane);
+        if (t + 1 < cur.C) {   // the backtrace staged through route_m: bring the chunk back
+          uint32_t rr[kV3Regs];
+          const uint32_t rlast = cur.nroutes - 1u;
+          const uint32_t* rp = b.route + cur.rbase;
+          __asm__ volatile("" : "+s"(rp));   // rare path: keep its addresses out of the loop's registers
+#pragma unroll
+          for (int x = 0; x < kV3Regs; ++x) {
+            rr[x] = kRouteInvalid;
+            if ((uint32_t)(kWave * x) < cur.nroutes) rr[x] = rp[min((uint32_t)(lane + kWave * x), rlast)];
+          }
+          v3_stage_routes(sm, cur, lane, rr);
+        }
+      }
+      if (KB == 0) {
+        if (lane == 0) sm.cs[t] = 1;
+        prev_ok = false;
+        prevK = 0;
+        wave_sync();
+        continue;
+      }
+      if (start && lane < kMaxCand)   // a chain starts: cost = emission, back-pointers none
+        sm.cost[cb ^ 1][lane] = (uint32_t)lane < KB ? (double)sm.sq[t][lane] * inv2s2 : INF;
+      if (lane == 0) sm.cs[t] = start ? 1 : 0;
+      wave_sync();
+      prev_ok = true;
+      prevK = KB;
+      cb ^= 1;
+    }
+    wave_sync();
+    v3_flush(b, sm, o + cur.s0, cur.C, lane);
+    wave_sync();
+    if (!has_next) break;
+    cur = nx;
+  }
+  if (prev_ok) {
+    wave_sync();
+    v3_backtrace(b, sm, o, S - 1, prevK, cb, lane);
+  }
+}
+
+// Small batches (the coalesced service: tens to hundreds of traces) take the one-wave-per-trace
+// kernel: with a few waves on an empty GPU the per-layer latency is the time, and its layer
+// chain is shorter (C2 traces of 600 points: 0.49 -> 0.35 ms at 38 traces, 0.38 -> 0.32 ms for
+// one); large batches keep four traces per wave (fewer instructions per trace-layer, 0.75 vs
+// 1.01 ms on C2's 10 k traces; at 4,096 traces 0.52 vs 0.55 ms).  RM_VIT_WAVE_MAX overrides
+// the crossover.
+#ifndef RM_VIT_WAVE_MAX
+#define RM_VIT_WAVE_MAX 4096
+#endif
 void launch_viterbi(uint32_t T, hipStream_t st, const DevBatch& v) {
+  static const uint32_t wave_max = [] {
+    const char* e = std::getenv("RM_VIT_WAVE_MAX");
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)RM_VIT_WAVE_MAX;
+  }();
+  if (T <= wave_max) {
+    hipLaunchKernelGGL(k_viterbi_w, dim3(T), dim3(64), 0, st, v);
+    return;
+  }
   hipLaunchKernelGGL(k_viterbi, dim3((T + 3) / 4), dim3(64), 0, st, v);
 }
 
@@ -3421,9 +3728,12 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
     Workspace& w = ws_;
     if (points <= w.cap_points && traces <= w.cap_traces && nopts <= w.cap_opts && w.ctl) return;
     // grow everything sized by points/traces (trans/path pools are grown separately)
-    const uint64_t cp = std::max<uint64_t>(points, w.cap_points) + 64;
-    const uint64_t ct = std::max<uint64_t>(traces, w.cap_traces) + 16;
-    const uint64_t co = std::max<uint64_t>(nopts, w.cap_opts) + 4;
+    // grow by half again at least: a coalescing service sees batch sizes creep upwards, and each
+    // regrowth frees and reallocates the whole workspace (hipFree synchronises the device) --
+    // growing to each new maximum exactly cost a ~70 ms stall per new maximum (svc_client_probe)
+    const uint64_t cp = std::max<uint64_t>(points, w.cap_points + w.cap_points / 2) + 64;
+    const uint64_t ct = std::max<uint64_t>(traces, w.cap_traces + w.cap_traces / 2) + 16;
+    const uint64_t co = std::max<uint64_t>(nopts, w.cap_opts + w.cap_opts / 2) + 4;
     const uint64_t keep_trans = w.cap_trans, keep_path = w.cap_path, keep_segs = w.cap_segs, keep_src = w.cap_src;
     w.release();
     std::vector<void*>& L = w.allocs;
@@ -3985,7 +4295,7 @@ __global__ void __launch_bounds__(64) k_gather_recs(uint32_t T, const uint32_t* 
 }
 
 void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, const void* d_src, uint32_t words,
-                                 uint32_t* off, void* dst) {
+                                 uint32_t* off, void* dst, const std::function<void*(uint64_t)>& dst_for) {
   const uint32_t T = n_traces_;
   hipStream_t st = stream_;
   RM_HIP(hipSetDevice(eng_->device()));
@@ -4026,6 +4336,7 @@ void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, 
     at += hc[k];
   }
   off[T] = (uint32_t)at;
+  if (dst_for) dst = dst_for(at);   // the caller sizes its buffer from the total
   if (at == 0) return;
   const size_t recb = (size_t)at * words * 8;
   const size_t dev_need = offb + recb + 8;
@@ -4074,7 +4385,18 @@ void Matcher::get_segments(uint32_t* seg_off, SegmentRec* segs) {
   sync();
   if (!n_traces_) { seg_off[0] = 0; return; }
   static_assert(sizeof(SegmentRec) % 8 == 0, "records move as u64 words");
-  download_compacted(ws_.seg_base, ws_.seg_cnt, ws_.segs, sizeof(SegmentRec) / 8, seg_off, segs);
+  download_compacted(ws_.seg_base, ws_.seg_cnt, ws_.segs, sizeof(SegmentRec) / 8, seg_off, segs, nullptr);
+}
+void Matcher::get_segments(std::vector<uint32_t>& seg_off, std::vector<SegmentRec>& segs) {
+  sync();
+  seg_off.assign((size_t)n_traces_ + 1, 0u);
+  segs.clear();
+  if (!n_traces_) return;
+  download_compacted(ws_.seg_base, ws_.seg_cnt, ws_.segs, sizeof(SegmentRec) / 8, seg_off.data(), nullptr,
+                     [&](uint64_t n) -> void* {
+                       segs.resize(n);
+                       return segs.data();
+                     });
 }
 uint64_t Matcher::count_reports() {
   sync();
@@ -4091,7 +4413,7 @@ void Matcher::get_reports(uint32_t* rep_off, ReportRec* reps, ReportStats* stats
   if (!n_traces_) { rep_off[0] = 0; return; }
   RM_HIP(hipMemcpy(stats, ws_.stats, n_traces_ * sizeof(ReportStats), hipMemcpyDeviceToHost));
   static_assert(sizeof(ReportRec) % 8 == 0, "records move as u64 words");
-  download_compacted(ws_.seg_base, ws_.rep_cnt, ws_.reps, sizeof(ReportRec) / 8, rep_off, reps);
+  download_compacted(ws_.seg_base, ws_.rep_cnt, ws_.reps, sizeof(ReportRec) / 8, rep_off, reps, nullptr);
 }
 
 }  // namespace rm

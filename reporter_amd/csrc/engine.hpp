@@ -8,6 +8,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -256,6 +257,8 @@ class Matcher {
   void get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, uint32_t* route_dist);
   // segments compacted per trace: seg_off (T+1), segs (seg_off[T])
   void get_segments(uint32_t* seg_off, SegmentRec* segs);
+  // the same with the buffers sized from the device counts (one count read-back, not two)
+  void get_segments(std::vector<uint32_t>& seg_off, std::vector<SegmentRec>& segs);
   uint64_t count_segments();
   void get_reports(uint32_t* rep_off, ReportRec* reps, ReportStats* stats);
   uint64_t count_reports();
@@ -309,7 +312,7 @@ class Matcher {
   // per-trace record lists (base[k], cnt[k] in units of `words` u64) compacted on the device and
   // downloaded through pinned memory into dst; off gets the T+1 offsets
   void download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, const void* d_src, uint32_t words,
-                          uint32_t* off, void* dst);
+                          uint32_t* off, void* dst, const std::function<void*(uint64_t)>& dst_for);
 
   Engine* eng_;
   void* dl_dev_ = nullptr;     // grow-only device / pinned host buffers of download_compacted
