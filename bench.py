@@ -574,6 +574,9 @@ def main():
         # the tables when nothing was handed over), else the bounded searches
         if counts and ball_tier and tiers["ball_to_search"] == 0:
             abytes, formulation = mo.routes_ball_algorithmic_bytes(counts), "route-ball table probes"
+        elif counts and "settled_to_targets" in counts:
+            abytes = mo.routes_targets_algorithmic_bytes(counts)
+            formulation = "bounded searches stopped at their targets (label-setting order)"
         elif counts:
             abytes, formulation = mo.routes_algorithmic_bytes(counts), "bounded searches"
         else:

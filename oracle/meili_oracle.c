@@ -165,8 +165,12 @@ static uint64_t mk(uint32_t d, uint32_t t) { return ((uint64_t)d << 32) | t; }
  *      node's in-edges in edge-id order up to it) [16] route-ball rows the path stage reads, one
  *      per usable exit: the target road's once per chained transition, the predecessor road's
  *      per walked node, and each usable in-edge's on a scan (counted only after
- *      og_prepare_path_counters) */
-#define OG_NCNT 17
+ *      og_prepare_path_counters)
+ * [17] [18] [19] settled nodes, scanned edges and label writes of the same K2 searches stopped at
+ *      their targets (engine.hip SearchTargets): label-setting order settles nodes by key, and a
+ *      search that stops once every target's route key is below the next key settles exactly the
+ *      nodes with keys <= the largest target route key (all of them when a target is unreached) */
+#define OG_NCNT 20
 static uint64_t og_cnt[OG_NCNT];
 static uint32_t og_roots;   /* usable exits of the last search_from */
 static int og_counting = 0;
@@ -202,6 +206,8 @@ typedef struct {
   hitem* heap; uint32_t hn, hcap;
   uint32_t* touched; uint32_t nt, tcap;
   uint32_t* pred;        /* per node */
+  /* per settle, in settle order (counting only): key, cumulative scanned edges, label writes */
+  uint64_t* skey; uint64_t* sscan; uint64_t* swrite; uint32_t ns, scap;
 } search_ws;
 
 static int ws_init(search_ws* w, uint32_t n) {
@@ -213,10 +219,15 @@ static int ws_init(search_ws* w, uint32_t n) {
   w->pred = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
   w->hcap = 1024; w->heap = (hitem*)malloc(sizeof(hitem) * w->hcap);
   w->tcap = 1024; w->touched = (uint32_t*)malloc(sizeof(uint32_t) * w->tcap);
-  return w->label && w->rootkey && w->stamp && w->pred && w->heap && w->touched;
+  w->scap = 1024;
+  w->skey = (uint64_t*)malloc(sizeof(uint64_t) * w->scap);
+  w->sscan = (uint64_t*)malloc(sizeof(uint64_t) * w->scap);
+  w->swrite = (uint64_t*)malloc(sizeof(uint64_t) * w->scap);
+  return w->label && w->rootkey && w->stamp && w->pred && w->heap && w->touched && w->skey && w->sscan && w->swrite;
 }
 static void ws_free(search_ws* w) {
   free(w->label); free(w->rootkey); free(w->stamp); free(w->pred); free(w->heap); free(w->touched);
+  free(w->skey); free(w->sscan); free(w->swrite);
 }
 static uint64_t ws_get(const search_ws* w, uint32_t v) { return w->stamp[v] == w->gen ? w->label[v] : OG_KEY_INF; }
 static void ws_touch(search_ws* w, uint32_t v) {
@@ -256,7 +267,7 @@ static hitem heap_pop(search_ws* w) {
  * yields the same keys since integer keys make the minimum unique). */
 static void search_from(const og_graph* g, search_ws* w, uint32_t road, uint32_t s, int mode, uint32_t bound) {
   const uint32_t acc = mode_access(mode);
-  w->gen++; w->nt = 0; w->hn = 0;
+  w->gen++; w->nt = 0; w->hn = 0; w->ns = 0;
   if (w->gen == 0) { memset(w->stamp, 0, sizeof(uint32_t) * w->n); w->gen = 1; }
   const uint32_t L = g->road_len_cm[road];
   const uint32_t ef = g->road_fwd[road], er = g->road_rev[road];
@@ -281,6 +292,7 @@ static void search_from(const og_graph* g, search_ws* w, uint32_t road, uint32_t
     if (it.key != w->label[it.node]) continue;       /* stale */
     const uint32_t u = it.node;
     if (og_counting) { og_cnt[1]++; og_cnt[2] += g->node_off[u + 1] - g->node_off[u]; }
+    uint64_t writes = 0;
     for (uint32_t e = g->node_off[u]; e < g->node_off[u + 1]; ++e) {
       if (!e_ok(g, e, acc)) continue;
       const uint32_t len = e_len(g, e);
@@ -288,9 +300,33 @@ static void search_from(const og_graph* g, search_ws* w, uint32_t road, uint32_t
       if ((uint32_t)(nk >> 32) > bound) continue;
       const uint32_t v = e_target(g, e);
       ws_touch(w, v);
-      if (nk < w->label[v]) { w->label[v] = nk; heap_push(w, nk, v); if (og_counting) og_cnt[3]++; }
+      if (nk < w->label[v]) { w->label[v] = nk; heap_push(w, nk, v); if (og_counting) og_cnt[3]++; ++writes; }
+    }
+    if (og_counting) {
+      if (w->ns == w->scap) {
+        w->scap *= 2;
+        w->skey = (uint64_t*)realloc(w->skey, sizeof(uint64_t) * w->scap);
+        w->sscan = (uint64_t*)realloc(w->sscan, sizeof(uint64_t) * w->scap);
+        w->swrite = (uint64_t*)realloc(w->swrite, sizeof(uint64_t) * w->scap);
+      }
+      const uint64_t ps = w->ns ? w->sscan[w->ns - 1] : 0, pw = w->ns ? w->swrite[w->ns - 1] : 0;
+      w->skey[w->ns] = it.key;
+      w->sscan[w->ns] = ps + (g->node_off[u + 1] - g->node_off[u]);
+      w->swrite[w->ns] = pw + writes;
+      w->ns++;
     }
   }
+}
+
+/* counters [17..19]: the prefix of the last search's settles with keys <= kmax */
+static void count_to_targets(const search_ws* w, uint64_t kmax) {
+  uint32_t lo = 0, hi = w->ns;   /* first settle with key > kmax (keys settle in order) */
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (w->skey[mid] <= kmax) lo = mid + 1; else hi = mid;
+  }
+  og_cnt[17] += lo;
+  if (lo) { og_cnt[18] += w->sscan[lo - 1]; og_cnt[19] += w->swrite[lo - 1]; }
 }
 
 /* canonical predecessor: a root keeps its init key; otherwise the smallest
@@ -622,15 +658,18 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
       for (uint32_t i = 0; i < KA; ++i) {
         const uint32_t ra = R->cand_road[la * (uint64_t)OG_K + i], sa = R->cand_s[la * (uint64_t)OG_K + i];
         search_from(g, &ws, ra, sa, op->mode, bound);
+        uint64_t kmax = 0;
         for (uint32_t j = 0; j < KB; ++j) {
           const uint32_t rb = R->cand_road[lb * (uint64_t)OG_K + j], sb = R->cand_s[lb * (uint64_t)OG_K + j];
           if (e_ok(g, g->road_fwd[rb], mode_access(op->mode)) || e_ok(g, g->road_rev[rb], mode_access(op->mode)))
             og_cnt[8] += og_roots;
           const uint64_t key = route_to(g, &ws, ra, sa, rb, sb, op->mode, NULL);
+          if (key > kmax) kmax = key;
           uint32_t out = OG_ROUTE_INVALID;
           if (key != OG_KEY_INF && (uint32_t)(key >> 32) <= bound && (uint32_t)key <= tmax) out = (uint32_t)(key >> 32);
           R->route[R->trans_off[lb] + i * KB + j] = out;
         }
+        count_to_targets(&ws, kmax);
       }
     }
   }

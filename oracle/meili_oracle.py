@@ -69,7 +69,8 @@ def lib():
 
 COUNTER_NAMES = ("searches", "settled", "scanned", "label_writes", "target_lookups", "route_writes",
                  "cand_items", "states", "ball_rows", "desc_reads", "cands", "grid_rows", "chained", "path_edges",
-                 "segments", "path_in_edges", "path_rows")
+                 "segments", "path_in_edges", "path_rows", "settled_to_targets", "scanned_to_targets",
+                 "label_writes_to_targets")
 
 
 def prepare_path_counters(graph):
@@ -94,6 +95,14 @@ def routes_algorithmic_bytes(c):
     24 B per search (source candidate + its road record)."""
     return (8 * c["settled"] + 16 * c["scanned"] + 12 * c["label_writes"] + 8 * c["target_lookups"]
             + 4 * c["route_writes"] + 24 * c["searches"])
+
+
+def routes_targets_algorithmic_bytes(c):
+    """routes_algorithmic_bytes of the same searches stopped at their targets (the formulation the
+    search tiers run since round 4, engine.hip SearchTargets): the settles, scans and label writes
+    up to the largest target route key of each search (counters 17-19)."""
+    return (8 * c["settled_to_targets"] + 16 * c["scanned_to_targets"] + 12 * c["label_writes_to_targets"]
+            + 8 * c["target_lookups"] + 4 * c["route_writes"] + 24 * c["searches"])
 
 
 def routes_ball_algorithmic_bytes(c):

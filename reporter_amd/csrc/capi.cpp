@@ -364,21 +364,200 @@ void Coalescer::loop() {
 
 }  // namespace
 
+// a pinned host buffer, grow-only
+struct PinnedBytes {
+  char* p = nullptr;
+  size_t cap = 0;
+  void ensure(size_t n) {
+    if (n <= cap && p) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t c = std::max<size_t>(n + n / 4, 1u << 16);
+    RM_HIP(hipHostMalloc((void**)&p, c, hipHostMallocDefault));
+    cap = c;
+  }
+  PinnedBytes() = default;
+  PinnedBytes(const PinnedBytes&) = delete;
+  PinnedBytes& operator=(const PinnedBytes&) = delete;
+  PinnedBytes(PinnedBytes&& o) noexcept : p(o.p), cap(o.cap) { o.p = nullptr; o.cap = 0; }
+  ~PinnedBytes() { if (p) (void)hipHostFree(p); }
+};
+
 struct rm_matcher {
   std::shared_ptr<Config> conf;
   std::unique_ptr<Matcher> m;
   HostStaging stage;
   std::vector<tj::PointSink> sinks;   // per parse thread, grow-only (no page faults on a warm matcher)
+  std::vector<PinnedBytes> arenas;    // per parse thread: trace-array bytes for the device parser
   double ms[6] = {};   // the last rm_match_batch: parse, stage, engine, download, format, total
 };
 
 namespace {
+
+// The reply side of rm_match_batch (both parsers): per-trace failures fail the call naming the
+// trace, then the segments come down once and each pool thread formats its range of replies
+// straight into the caller's output strings.
+void finish_json_batch(rm_matcher* m, Matcher& mt, size_t n, size_t nt, char** outs) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  std::vector<uint32_t> terr(n, 0u);
+  if (mt.error_bits()) mt.get_trace_errors(terr.data());
+  for (size_t i = 0; i < n; ++i)
+    if (terr[i]) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
+  const auto t3 = clk::now();
+  std::vector<uint32_t> soff;
+  std::vector<SegmentRec> segs;
+  mt.get_segments(soff, segs);
+  m->ms[3] = ms_since(t3);
+  const auto t4 = clk::now();
+  HostPool::get().run(nt, [&](size_t t) {
+    const size_t a = n * t / nt, b = n * (t + 1) / nt;
+    std::string js;
+    for (size_t i = a; i < b; ++i) {
+      tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], js);
+      outs[i] = dup_string(js);
+    }
+  });
+  m->ms[4] = ms_since(t4);
+}
+
+// rm_match_batch with the trace arrays parsed on the device (engine.hip k_parse_json).  Each pool
+// thread reads its requests' structure on the host (parse_request_deferred) and copies their
+// trace-array bytes into its pinned arena; the arenas go up in request order (one contiguous span
+// per trace) and one wave per trace parses them into the workspace's point arrays.  A request the
+// host did not defer (not a compact-looking trace) keeps its host-parsed points.  A trace the
+// device flags is parsed again on the host.  Any failure, and a flagged trace whose point count
+// differs from its '{' count, returns false before anything ran: the caller then takes the host
+// path, which reports exactly the error the host reader gives.
+bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n, char** outs) {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  const auto t0 = clk::now();
+  HostPool& pool = HostPool::get();
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(pool.size(), (n + 15) / 16));
+  if (m->sinks.size() < nt) m->sinks.resize(nt);
+  while (m->arenas.size() < nt) m->arenas.emplace_back();
+  std::vector<uint32_t> cnt(n), topt(n);
+  std::vector<uint64_t> slen(n, 0), sink_at(n, 0);
+  std::vector<uint8_t> host_parsed(n, 0);
+  std::vector<size_t> used(nt, 0);
+  std::vector<MatchOptions> opts(n);
+  std::vector<char> failed(nt, 0);
+  const Config& conf = *m->conf;
+  pool.run(nt, [&](size_t t) {
+    const size_t a = n * t / nt, b = n * (t + 1) / nt;
+    std::vector<size_t> len(b - a);
+    size_t bytes = 0;
+    for (size_t i = a; i < b; ++i) bytes += len[i - a] = std::strlen(traces[i]);
+    PinnedBytes& ar = m->arenas[t];
+    ar.ensure(bytes + 1);
+    tj::PointSink& sk = m->sinks[t];
+    sk.clear();
+    size_t at = 0;
+    for (size_t i = a; i < b && !failed[t]; ++i) {
+      topt[i] = (uint32_t)i;
+      tj::TraceSpan sp;
+      const size_t before = sk.size();
+      try {
+        opts[i] = tj::parse_request_deferred(traces[i], len[i - a], conf.mode_defaults, sk, sp);
+      } catch (const std::exception&) {
+        try {
+          sp = tj::TraceSpan();
+          opts[i] = tj::parse_request(traces[i], len[i - a], conf.mode_defaults, sk);
+        } catch (const std::exception&) {
+          failed[t] = 1;   // the host path reports it (as the first failing request)
+          break;
+        }
+      }
+      if (sp.on) {
+        const size_t k = (size_t)(sp.e - sp.b);
+        std::memcpy(ar.p + at, sp.b, k);
+        at += k;
+        slen[i] = k;
+        cnt[i] = sp.n_open;
+      } else {
+        host_parsed[i] = 1;
+        sink_at[i] = before;
+        cnt[i] = (uint32_t)(sk.size() - before);
+      }
+    }
+    used[t] = at;
+  });
+  for (size_t t = 0; t < nt; ++t)
+    if (failed[t]) return false;
+  std::vector<uint32_t> off(n + 1, 0);
+  std::vector<uint64_t> span(n + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    if ((uint64_t)off[i] + cnt[i] >= 0xffffffffull) throw BatchTooLarge("batch too large (points >= 2^32)");
+    off[i + 1] = off[i] + cnt[i];
+    span[i + 1] = span[i] + slen[i];
+  }
+  const uint64_t P = off[n];
+  m->ms[0] = ms_since(t0);
+  const auto t1 = clk::now();
+  if (!m->m) m->m = std::make_unique<Matcher>(conf.engine.get());
+  Matcher& mt = *m->m;
+  mt.json_reserve(P, (uint32_t)n, (uint32_t)n, span[n]);
+  uint64_t base = 0;
+  for (size_t t = 0; t < nt; ++t) {
+    mt.json_upload(base, m->arenas[t].p, used[t]);
+    base += used[t];
+  }
+  std::vector<double> tsp(2 * n, 0.0);
+  auto host_points = [&](size_t i, const tj::PointSink& sk, size_t at) {
+    const size_t k = cnt[i];
+    mt.upload_points(off[i], k, sk.lon.data() + at, sk.lat.data() + at, sk.time.data() + at, sk.acc.data() + at);
+    if (k) { tsp[2 * i] = sk.time[at]; tsp[2 * i + 1] = sk.time[at + k - 1]; }
+  };
+  for (size_t t = 0; t < nt; ++t) {
+    const size_t a = n * t / nt, b = n * (t + 1) / nt;
+    for (size_t i = a; i < b; ++i)
+      if (host_parsed[i]) host_points(i, m->sinks[t], sink_at[i]);
+  }
+  std::vector<uint32_t> flags(n, 0u);
+  std::vector<double> dtsp(2 * n, 0.0);
+  mt.json_parse(span.data(), off.data(), (uint32_t)n, flags.data(), dtsp.data());
+  tj::PointSink fix;
+  for (size_t i = 0; i < n; ++i) {
+    if (host_parsed[i]) continue;
+    if (!flags[i]) { tsp[2 * i] = dtsp[2 * i]; tsp[2 * i + 1] = dtsp[2 * i + 1]; continue; }
+    // not the compact layout after all: the host reader's points, if they fit the trace's slots
+    fix.clear();
+    try {
+      opts[i] = tj::parse_request(traces[i], std::strlen(traces[i]), conf.mode_defaults, fix);
+    } catch (const std::exception&) {
+      return false;
+    }
+    if (fix.size() != cnt[i]) return false;
+    host_points(i, fix, 0);
+  }
+  m->ms[1] = ms_since(t1);
+  const auto t2 = clk::now();
+  RunParams rp;
+  rp.do_report = 0;
+  mt.set_isolation(true);
+  mt.run_parsed(off.data(), (uint32_t)n, opts.data(), (uint32_t)n, topt.data(), tsp.data(), rp);
+  m->ms[2] = ms_since(t2);
+  finish_json_batch(m, mt, n, nt, outs);
+  m->ms[5] = ms_since(t0);
+  return true;
+}
+
+bool json_device_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("RM_JSON_DEVICE");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
 
 // rm_match_batch without the coalescer: each pool thread parses a contiguous range of the
 // requests into its own point arrays, copies them into the matcher's pinned staging at their
 // batch offsets, and after the engine's run formats its range's replies straight into the
 // caller's output strings.  Any failing trace fails the call, naming the trace.
 void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs) {
+  if (n && json_device_enabled() && match_json_batch_device(m, traces, n, outs)) return;
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t0 = clk::now();
@@ -436,26 +615,8 @@ void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char**
   rp.do_report = 0;
   mt.set_isolation(true);
   mt.run(hb, rp);
-  std::vector<uint32_t> terr(n, 0u);
-  if (mt.error_bits()) mt.get_trace_errors(terr.data());
-  for (size_t i = 0; i < n; ++i)
-    if (terr[i]) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
   m->ms[2] = ms_since(t2);
-  const auto t3 = clk::now();
-  std::vector<uint32_t> soff;
-  std::vector<SegmentRec> segs;
-  mt.get_segments(soff, segs);
-  m->ms[3] = ms_since(t3);
-  const auto t4 = clk::now();
-  pool.run(nt, [&](size_t t) {
-    const size_t a = n * t / nt, b = n * (t + 1) / nt;
-    std::string js;
-    for (size_t i = a; i < b; ++i) {
-      tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], js);
-      outs[i] = dup_string(js);
-    }
-  });
-  m->ms[4] = ms_since(t4);
+  finish_json_batch(m, mt, n, nt, outs);
   m->ms[5] = ms_since(t0);
 }
 
@@ -951,11 +1112,12 @@ int rm_runner_sizes(rm_runner* r, uint64_t out[10]) {
     for (int i = 0; i < 4; ++i) out[6 + i] = t[i];
   });
 }
-int rm_runner_route_tiers(rm_runner* r, uint64_t out[6]) {
+int rm_runner_route_tiers(rm_runner* r, uint64_t out[8]) {
   return guarded([&] {
     uint32_t c[kCtlWords];
     r->m->ctl_words(c);
     out[0] = c[1]; out[1] = c[3]; out[2] = c[5]; out[3] = c[8]; out[4] = c[9]; out[5] = c[10];
+    out[6] = c[11]; out[7] = c[12];
   });
 }
 int rm_runner_get_states(rm_runner* r, uint32_t* a, uint32_t* b) { return guarded([&] { r->m->get_states(a, b); }); }

@@ -33,6 +33,7 @@
 #include <type_traits>
 
 #include "engine.hpp"
+#include "json_points.hpp"
 
 namespace rm {
 
@@ -44,6 +45,8 @@ namespace {
 constexpr uint32_t kEmpty = 0xffffffffu;
 constexpr int kWave = 64;
 constexpr int kBigH = 4096;     // LDS hash slots, retry tier (one source at a time)
+constexpr int kMidH = 512;      // LDS hash slots, first wave tier
+constexpr uint32_t kMidGrid = 4096;   // blocks of the 512-slot wave tiers (16 per CU)
 constexpr int kCandH = 256;     // road hash slots in the candidate kernel
 constexpr int kInlinePath = 8;  // path edges stored inline per slot (no allocation)
 constexpr int kReg2Grid = 512;  // blocks of the second register tiers (grid-stride over their work lists)
@@ -68,6 +71,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list [8] path ball hand-overs
   // [9] routes list C [10] paths list C (the global-memory search tier)
+  // [11] routes list B2 [12] paths list B2 (the 512-slot wave tier's hand-overs to the 4096-slot one)
   uint32_t* rl_routes_0;  // items the K2 ball tier hands to the search tiers (count ctl[1])
   uint32_t* ctl; uint32_t* rl_routes_a; uint32_t* rl_routes_b; uint32_t* rl_paths_a; uint32_t* rl_paths_b;
   uint32_t* rl_cand;
@@ -79,6 +83,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   // tables meets in one XCD's L2 instead of arriving in trace order from everywhere.
   const uint32_t* perm;
   const uint32_t* perm_paths;   // perm for the path stage too (null: the path stage takes slot order)
+  uint32_t search_delta;        // cm: the wave tiers' delta-stepping width (kNone: plain rounds)
 };
 
 // A failure that belongs to one trajectory (too many roads in a radius, a search beyond every
@@ -448,6 +453,37 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
   unsigned long long rbest[kMaxCand];
   uint32_t n = 0;
   bool ovf = false;
+#ifdef RM_K1_RUNS
+  // The current run of hits on one road (a cell lists a road's consecutive shape pieces next to
+  // each other): its minimum is kept here and merged into the per-road slots once per run, not
+  // once per hit piece.  min is order-independent, so the slots end the same.
+  uint32_t run_road = kNone, run_s = 0;
+  unsigned long long run_key = ~0ull;
+#define K1_FLUSH_RUN()                                                                  \
+  if (run_road != kNone) {                                                              \
+    bool found_ = false;                                                                \
+    _Pragma("unroll") for (int x = 0; x < kMaxCand; ++x) {                              \
+      if (K1_UNIFORM_STOP(x < (int)n)) break;                                           \
+      if (x < (int)n && rroad[x] == run_road) {                                         \
+        found_ = true;                                                                  \
+        if (run_key < rbest[x]) { rbest[x] = run_key; rs[x] = run_s; }                  \
+      }                                                                                 \
+    }                                                                                   \
+    if (!found_) {                                                                      \
+      if (n >= (uint32_t)kMaxCand) {                                                    \
+        ovf = true;                                                                     \
+      } else {                                                                          \
+        _Pragma("unroll") for (int x = 0; x < kMaxCand; ++x) {                          \
+          if (K1_UNIFORM_STOP(x <= (int)n)) break;                                      \
+          if (x == (int)n) { rroad[x] = run_road; rbest[x] = run_key; rs[x] = run_s; }  \
+        }                                                                               \
+        ++n;                                                                            \
+      }                                                                                 \
+    }                                                                                   \
+    run_road = kNone;                                                                   \
+    run_key = ~0ull;                                                                    \
+  }
+#endif
   if (!(fx1 < 0 || fy1 < 0 || fx0 > (double)(g.ncx - 1) || fy0 > (double)(g.ncy - 1))) {
     const uint32_t x0 = fx0 < 0 ? 0u : (uint32_t)fx0, y0 = fy0 < 0 ? 0u : (uint32_t)fy0;
     const uint32_t x1 = fx1 > (double)(g.ncx - 1) ? g.ncx - 1 : (uint32_t)fx1;
@@ -496,6 +532,12 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
           if (!(sq <= r2)) continue;
           const uint32_t road = r1[y].z & 0x1fffffffu;
           const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | r1[y].w;
+#ifdef RM_K1_RUNS
+          if (road != run_road) { K1_FLUSH_RUN() }
+          run_road = road;
+          if (key < run_key) { run_key = key; run_s = sc; }
+          continue;
+#endif
           bool found = false;
 #pragma unroll
           for (int x = 0; x < kMaxCand; ++x) {
@@ -517,6 +559,10 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
       }
     }
   }
+#ifdef RM_K1_RUNS
+  if (!ovf) { K1_FLUSH_RUN() }
+#undef K1_FLUSH_RUN
+#endif
   if (ovf) {
     const uint32_t q = atomicAdd(&b.ctl[7], 1u);
     b.rl_cand[q] = (uint32_t)p;
@@ -905,7 +951,7 @@ __device__ __forceinline__ void exit_keys(const uint4& a0, uint32_t bound, unsig
 // Bounded search shared by the wave tiers of K2 (routes) and of the path kernel.
 template <int H, bool PATH>
 struct SearchSmem {
-  using FIdx = typename std::conditional<(H > 65536), uint32_t, uint16_t>::type;
+  using FIdx = typename std::conditional<(H >= 65536), uint32_t, uint16_t>::type;
   uint32_t key[H];                 // (source << 28) | node
   unsigned long long lab[H];       // u64 (dist cm, time ms) key
   FIdx fa[H], fb[H];               // frontier (slot ids), ping-pong
@@ -965,14 +1011,54 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter) {
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
+template <int H, bool PATH>
+struct HashLabel {
+  const SearchSmem<H, PATH>& sm;
+  uint32_t srcbits;
+  __device__ unsigned long long operator()(uint32_t node) const { return h_label(sm, srcbits | node); }
+};
+
+// Early termination (round 4).  A search that serves known targets (a K2
+// item's K_B target candidates, a path's chosen target) stops as soon as their route keys are
+// final: at a round boundary every frontier label is >= F (the frontier minimum), and a node whose
+// label is < F is final (its shortest path runs through nodes of smaller keys, all expanded), so a
+// target whose current route key is < F can no longer improve.  When every target is below F the
+// rest of the ball (up to the pair's bound, typically 4-5x the targets' distance at 30 s sampling)
+// is never explored.  Strict <: a path's canonical predecessors (tight in-edges) of a node below F
+// are then all final and in the hash, exactly as in the full search.
+// `delta` (cm, kNone = off) limits a round to frontier nodes with keys <= F + delta; the others
+// wait in the frontier (label-correcting rounds in near-Dijkstra order: fewer nodes re-relaxed and
+// fewer touched beyond the targets).
+struct SearchTargets {
+  const uint4* tg;     // the targets' descriptors (global, 2 x uint4 each); null: none
+  uint32_t n;          // how many (<= 64)
+  uint32_t delta;      // cm, kNone: every frontier node every round
+};
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const unsigned long long o = ((unsigned long long)(uint32_t)__shfl_xor((int)(v >> 32), d, kWave) << 32) |
+                                 (uint32_t)__shfl_xor((int)(uint32_t)v, d, kWave);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
 // Exact lexicographic shortest (dist, time) keys from the exits of n_src source
 // candidates (descriptors src[0..n_src), source ids 0..n_src-1) to every node within
 // `bound` cm, by synchronous label-correcting rounds over an LDS frontier compacted by ballot
 // (wave_append).  All 64 lanes call it.
 // With src == nullptr the single root is node `root` at key 0 (route-ball build).
+// With targets (n_src == 1), the search may stop early: labels below the final frontier minimum
+// are exact, the others are upper bounds (see SearchTargets).
 template <int H, bool PATH>
 __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int mode, uint32_t bound,
-                               const uint4* src, uint32_t n_src, uint32_t root = 0) {
+                               const uint4* src, uint32_t n_src, uint32_t root = 0,
+                               SearchTargets tgt = SearchTargets{nullptr, 0u, kNone}) {
+  using FIdx = typename SearchSmem<H, PATH>::FIdx;
+  constexpr FIdx kDeferred = (FIdx)~(FIdx)0;
+  static_assert((uint64_t)H <= (uint64_t)kDeferred, "frontier index needs a spare value");
   const int lane = threadIdx.x;
   const uint32_t acc = mode_access(mode);
   for (int h = lane; h < H; h += kWave) {
@@ -980,13 +1066,18 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
     if (PATH) sm.pred[h] = kNone;
   }
   if (lane == 0) { sm.nf = 0; sm.nn = 0; sm.used = 0; sm.ovf = 0; }
+  // targets: lane j holds target j's descriptor
+  const bool has_tg = tgt.tg != nullptr && tgt.n != 0u;
+  uint4 t0 = make_uint4(0u, 0u, 0u, 0u), t1 = t0;
+  if (has_tg && (uint32_t)lane < tgt.n) { t0 = tgt.tg[2 * lane]; t1 = tgt.tg[2 * lane + 1]; }
+  const bool use_min = has_tg || tgt.delta != kNone;
   __syncthreads();
   if (!src) {
     if (lane == 0) {
       const int slot = h_insert(sm, root);
       sm.lab[slot] = 0ull;
       sm.inq[slot] = 1u;
-      sm.fa[sm.nf++] = (typename SearchSmem<H, PATH>::FIdx)slot;
+      sm.fa[sm.nf++] = (FIdx)slot;
     }
   } else if ((uint32_t)lane < 2u * n_src) {  // roots: two exits per source
     const uint32_t i = lane >> 1;
@@ -999,21 +1090,51 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
       const int slot = h_insert(sm, (i << 28) | node);
       if (slot >= 0) {
         const unsigned long long old = atomicMin(&sm.lab[slot], kk);
-        if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[wave_append(&sm.nf)] = (typename SearchSmem<H, PATH>::FIdx)slot;
+        if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[wave_append(&sm.nf)] = (FIdx)slot;
       }
     }
   }
   __syncthreads();
+  const uint4 sa0 = src ? src[0] : make_uint4(0u, 0u, 0u, 0u);
   for (int round = 0;; ++round) {
     const uint32_t nf = sm.nf;
     if (nf == 0 || sm.ovf) break;
     if (round > 4 * H) { if (lane == 0) sm.ovf = 2u; break; }
-    typename SearchSmem<H, PATH>::FIdx* cur = (round & 1) ? sm.fb : sm.fa;
-    typename SearchSmem<H, PATH>::FIdx* nxt = (round & 1) ? sm.fa : sm.fb;
-    for (uint32_t q = lane; q < nf; q += kWave) sm.inq[cur[q]] = 0u;
+    FIdx* cur = (round & 1) ? sm.fb : sm.fa;
+    FIdx* nxt = (round & 1) ? sm.fa : sm.fb;
+    unsigned long long thr = kKeyInf;
+    if (use_min) {
+      unsigned long long fm = kKeyInf;
+      for (uint32_t q = lane; q < nf; q += kWave) {
+        const unsigned long long l = sm.lab[cur[q]];
+        fm = l < fm ? l : fm;
+      }
+      fm = wave_min_u64(fm);
+      if (has_tg) {   // every target's route key below the frontier minimum: final
+        bool done = true;
+        if ((uint32_t)lane < tgt.n) done = route_key(HashLabel<H, PATH>{sm, 0u}, sa0, t0, t1, nullptr) < fm;
+        if (__ballot(!done) == 0ull) break;
+      }
+      if (tgt.delta != kNone) thr = fm + ((unsigned long long)tgt.delta << 32);
+    }
+    if (thr == kKeyInf) {
+      for (uint32_t q = lane; q < nf; q += kWave) sm.inq[cur[q]] = 0u;
+    } else {
+      for (uint32_t q = lane; q < nf; q += kWave) {
+        const FIdx slot = cur[q];
+        if (sm.lab[slot] > thr) {   // waits for a later round (stays queued)
+          nxt[wave_append(&sm.nn)] = slot;
+          cur[q] = kDeferred;
+        } else {
+          sm.inq[slot] = 0u;
+        }
+      }
+    }
     __syncthreads();
     for (uint32_t q = lane; q < nf; q += kWave) {
-      const int slot = cur[q];
+      const FIdx fs = cur[q];
+      if (fs == kDeferred) continue;
+      const int slot = fs;
       const uint32_t kk = sm.key[slot];
       const uint32_t node = kk & 0x0fffffffu, srcbits = kk & 0xf0000000u;
       const unsigned long long lab = sm.lab[slot];
@@ -1026,7 +1147,7 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
         const int t = h_insert(sm, srcbits | rec.x);
         if (t < 0) continue;
         const unsigned long long old = atomicMin(&sm.lab[t], nk);
-        if (nk < old && atomicExch(&sm.inq[t], 1u) == 0u) nxt[wave_append(&sm.nn)] = (typename SearchSmem<H, PATH>::FIdx)t;
+        if (nk < old && atomicExch(&sm.inq[t], 1u) == 0u) nxt[wave_append(&sm.nn)] = (FIdx)t;
       }
     }
     __syncthreads();
@@ -1035,13 +1156,6 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
   }
   __syncthreads();
 }
-
-template <int H, bool PATH>
-struct HashLabel {
-  const SearchSmem<H, PATH>& sm;
-  uint32_t srcbits;
-  __device__ unsigned long long operator()(uint32_t node) const { return h_label(sm, srcbits | node); }
-};
 
 // ------------------------------------------------------------------------------------------
 // Lane tiers: one lane runs one whole bounded Dijkstra.  Most searches settle a handful
@@ -1111,11 +1225,51 @@ struct StoreLabel {
   __device__ unsigned long long operator()(uint32_t node) const { return s.label(node); }
 };
 
-// bounded Dijkstra from the exits of the candidate described by (a0, a1)
-template <class L>
+struct NoStop {
+  template <class L>
+  __device__ bool operator()(const L&, unsigned long long) { return false; }
+};
+// a path search's single target: done once its route key is below the next settled key (labels
+// below it are final, and so are the tight predecessors of such a label: see SearchTargets)
+struct StopAtTarget {
+  uint4 a0, b0, b1;
+  template <class L>
+  __device__ bool operator()(const L& S, unsigned long long bk) {
+    return route_key(StoreLabel<L>{S}, a0, b0, b1, nullptr) < bk;
+  }
+};
+
+// a K2 item's K_B targets: done once every target's route key is below the next settled key.
+// Keys only fall, so a finite maximum stays an upper bound and is computed once; while some
+// target is unreached it is recomputed every fourth settle.
+constexpr uint32_t kStopMinBoundCm = 50000;   // pair bounds from which tier 2 stops at its targets
+struct StopAtTargets {
+  const uint4* tg;   // the pair's target descriptors (2 x uint4 each)
+  uint32_t n;
+  uint4 a0;
+  unsigned long long kmax;
+  uint32_t calls;
+  template <class L>
+  __device__ bool operator()(const L& S, unsigned long long bk) {
+    if (!n) return false;   // no targets given: never stops
+    if (kmax != kKeyInf && kmax != 0ull) return kmax < bk;
+    if (kmax == kKeyInf && (++calls & 3u)) return false;
+    unsigned long long m = 0ull;
+    for (uint32_t j = 0; j < n && m != kKeyInf; ++j) {
+      const unsigned long long k = route_key(StoreLabel<L>{S}, a0, tg[2 * j], tg[2 * j + 1], nullptr);
+      m = k > m ? k : m;
+    }
+    kmax = m == 0ull ? 1ull : m;   // 0 marks "not computed yet"
+    return m < bk;
+  }
+};
+
+// bounded Dijkstra from the exits of the candidate described by (a0, a1); `stop(S, k)` is asked
+// before each settle (k = the key about to be settled) and ends the search when true
+template <class L, class Stop = NoStop>
 __device__ __forceinline__ void lane_search(L& S, const DevGraph& g, const uint4* E, uint32_t bound,
                                             const uint4& a0, const uint4& a1, unsigned long long& rk1,
-                                            unsigned long long& rk0) {
+                                            unsigned long long& rk0, Stop stop = Stop{}) {
   S.init();
   exit_keys(a0, bound, rk1, rk0);
   const uint32_t r1 = rk1 != kKeyInf ? g.node_rng[a1.y] : 0u;
@@ -1125,6 +1279,7 @@ __device__ __forceinline__ void lane_search(L& S, const DevGraph& g, const uint4
   unsigned long long bk;
   uint32_t r = 0, u = 0, from = kNone;
   while (S.pick(bk, r, u, from)) {
+    if (stop(S, bk)) break;
     const uint32_t e0 = r >> 5, deg = r & 31u;
     for (uint32_t q0 = 0; q0 < deg; q0 += 4) {
       uint4 rec[4];
@@ -1375,6 +1530,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
   const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
   RegLabels S;
   unsigned long long rk1, rk0;
+  // no early stop here: at the bounds this tier completes (tens of metres) the targets' check
+  // costs more than the settles it saves (C2 --ball-radius 0: 2.1 -> 3.4 ms); tier 2 has it
   lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
   if (S.ovf) {
     b.rl_routes_a[atomicAdd(&b.ctl[3], 1u)] = t;
@@ -1405,7 +1562,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
     const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
     RegLabelsT<kTier2Cap> S;
     unsigned long long rk1, rk0;
-    lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
+    // the early stop pays from bounds of a few blocks (C3's 30 s pairs); at 1 Hz bounds its
+    // checks cost more than they save (C2 --ball-radius 0: 0.69 -> 1.0 ms)
+    lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0,
+                StopAtTargets{b.cand_desc + (uint64_t)p * kMaxCand * 2, bound >= kStopMinBoundCm ? KB : 0u, a0, 0ull, 0u});
     if (S.ovf) {
       const uint32_t x = atomicAdd(&b.ctl[5], 1u);
       b.rl_routes_b[x] = t;
@@ -1536,7 +1696,7 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
   const uint4 a0 = b.cand_desc[((p - 1) * kMaxCand + i) * 2], a1 = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + 1];
   const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
   unsigned long long rk1, rk0;
-  lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0);
+  lane_search(S, g, g.relax[mode], bound, a0, a1, rk1, rk0, StopAtTarget{a0, b0, b1});
   if (S.ovf) return false;
   int combo = -1;
   const unsigned long long key = route_key(StoreLabel<L>{S}, a0, b0, b1, &combo);
@@ -1795,7 +1955,8 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
   const uint32_t base = b.trans_off[p];
   if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
   __syncthreads();
-  bounded_search<H, false>(sm, g, mode, bound, s_src, 1);
+  bounded_search<H, false>(sm, g, mode, bound, s_src, 1, 0u,
+                           SearchTargets{b.cand_desc + p * kMaxCand * 2, KB, b.search_delta});
   const bool ok = !sm.ovf;
   if (ok) {
     for (uint32_t j = lane; j < KB; j += kWave) {
@@ -1810,12 +1971,26 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
   return ok;
 }
 
-__global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
-  __shared__ SearchSmem<kBigH, false> sm;
+// Two LDS sizes (round 4): the 512-slot tier (10 KB, 16 waves per CU) takes what outgrew the
+// register tiers -- with early termination most searches end a few blocks past their targets --
+// and hands what outgrows it (list B2 in rl_routes_a, free once tier 2 has run) to the 4096-slot
+// tier (80 KB, 2 waves per CU).
+__global__ void __launch_bounds__(64) k_routes_wave_s(DevGraph g, DevBatch b) {
+  __shared__ SearchSmem<kMidH, false> sm;
   __shared__ uint4 s_src[2];
   const uint32_t n_items = b.ctl[5];
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const uint32_t t = b.rl_routes_b[item];
+    if (!routes_search_item<kMidH>(sm, s_src, g, b, t) && threadIdx.x == 0) b.rl_routes_a[atomicAdd(&b.ctl[11], 1u)] = t;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
+  __shared__ SearchSmem<kBigH, false> sm;
+  __shared__ uint4 s_src[2];
+  const uint32_t n_items = b.ctl[11];
+  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const uint32_t t = b.rl_routes_a[item];
     if (!routes_search_item<kBigH>(sm, s_src, g, b, t) && threadIdx.x == 0) b.rl_routes_c[atomicAdd(&b.ctl[9], 1u)] = t;
   }
 }
@@ -2500,7 +2675,8 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
   if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
   __syncthreads();
   const uint4 a0 = s_src[0], a1 = s_src[1];
-  bounded_search<H, true>(sm, g, mode, bound, s_src, 1);
+  bounded_search<H, true>(sm, g, mode, bound, s_src, 1, 0u,
+                          SearchTargets{b.cand_desc + (p * kMaxCand + j) * 2, 1u, b.search_delta});
   if (sm.ovf) {
     __syncthreads();
     return false;
@@ -2576,12 +2752,22 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
   return true;
 }
 
-__global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
-  __shared__ SearchSmem<kBigH, true> sm;
+__global__ void __launch_bounds__(64) k_paths_wave_s(DevGraph g, DevBatch b) {
+  __shared__ SearchSmem<kMidH, true> sm;
   __shared__ uint4 s_src[2];
   const uint32_t n_items = b.ctl[6];
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
     const uint32_t p = b.rl_paths_b[item];
+    if (!paths_search_item<kMidH>(sm, s_src, g, b, p) && threadIdx.x == 0) b.rl_paths_a[atomicAdd(&b.ctl[12], 1u)] = p;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
+  __shared__ SearchSmem<kBigH, true> sm;
+  __shared__ uint4 s_src[2];
+  const uint32_t n_items = b.ctl[12];
+  for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
+    const uint32_t p = b.rl_paths_a[item];
     if (!paths_search_item<kBigH>(sm, s_src, g, b, p) && threadIdx.x == 0) b.rl_paths_c[atomicAdd(&b.ctl[10], 1u)] = p;
   }
 }
@@ -3719,6 +3905,8 @@ Matcher::~Matcher() {
   ws_.release();
   if (dl_dev_) (void)hipFree(dl_dev_);
   if (dl_host_) (void)hipHostFree(dl_host_);
+  for (void* q : {(void*)jdev_, jspan_, (void*)jflag_, jtsp_})
+    if (q) (void)hipFree(q);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (hctl_) (void)hipHostFree(hctl_);
 }
@@ -3869,6 +4057,20 @@ void Matcher::sync() {
   harvest_times();
 }
 
+// delta-stepping width of the wave search tiers (SearchTargets); RM_SEARCH_DELTA_M overrides
+// (0 or negative: plain synchronous rounds)
+#ifndef RM_SEARCH_DELTA_M
+#define RM_SEARCH_DELTA_M 0
+#endif
+uint32_t search_delta_cm() {
+  static const uint32_t d = [] {
+    const char* e = std::getenv("RM_SEARCH_DELTA_M");
+    const double m = e && *e ? std::strtod(e, nullptr) : (double)RM_SEARCH_DELTA_M;
+    return m > 0.0 ? (uint32_t)std::min(m * 100.0, 4.0e9) : kNone;
+  }();
+  return d;
+}
+
 static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   DevBatch v;
   v.T = T; v.P = P;
@@ -3890,7 +4092,28 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.rl_routes_c = w.rl_routes_c; v.rl_paths_c = w.rl_paths_c; v.trace_err = w.trace_err;
   v.perm = nullptr;   // run_device sets it when the locality order is on
   v.perm_paths = nullptr;
+  v.search_delta = search_delta_cm();
   return v;
+}
+
+// a batch's layout and options, checked before anything is uploaded; sets mode_mask_
+void Matcher::check_batch(uint32_t T, const uint32_t* trace_off, const MatchOptions* opts, uint32_t n_opts,
+                          const uint32_t* trace_opt) {
+  const uint64_t P = trace_off[T];
+  if (P >= 0xffffffffull) throw BatchTooLarge("batch too large (points >= 2^32)");
+  for (uint32_t k = 0; k < T; ++k) {
+    if (trace_off[k + 1] < trace_off[k]) throw std::runtime_error("trace offsets not monotone");
+    if (trace_opt[k] >= n_opts) throw std::runtime_error("trace option index out of range");
+  }
+  mode_mask_ = 0;
+  for (uint32_t q = 0; q < n_opts; ++q) {
+    if (opts[q].mode < 0 || opts[q].mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
+    // K3 divides by both (a zero 1/beta would turn an invalid route's +inf into NaN)
+    if (!(opts[q].sigma_z > 0.f) || !std::isfinite(opts[q].sigma_z)) throw std::runtime_error("sigma_z must be positive and finite");
+    if (!(opts[q].beta > 0.f) || !std::isfinite(opts[q].beta)) throw std::runtime_error("beta must be positive and finite");
+    if (!(opts[q].turn_penalty_factor == 0.f)) throw std::runtime_error(kTurnPenaltyError);
+    mode_mask_ |= 1u << opts[q].mode;
+  }
 }
 
 void Matcher::run(const HostBatch& hb, const RunParams& rp) {
@@ -3898,20 +4121,7 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
   const uint32_t T = hb.n_traces;
   if (T == 0) { n_traces_ = 0; n_points_ = 0; n_trans_ = 0; n_path_ = 0; seg_used_ = 0; return; }
   const uint64_t P = hb.trace_off[T];
-  if (P >= 0xffffffffull) throw BatchTooLarge("batch too large (points >= 2^32)");
-  for (uint32_t k = 0; k < T; ++k) {
-    if (hb.trace_off[k + 1] < hb.trace_off[k]) throw std::runtime_error("trace offsets not monotone");
-    if (hb.trace_opt[k] >= hb.n_opts) throw std::runtime_error("trace option index out of range");
-  }
-  mode_mask_ = 0;
-  for (uint32_t q = 0; q < hb.n_opts; ++q) {
-    if (hb.opts[q].mode < 0 || hb.opts[q].mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
-    // K3 divides by both (a zero 1/beta would turn an invalid route's +inf into NaN)
-    if (!(hb.opts[q].sigma_z > 0.f) || !std::isfinite(hb.opts[q].sigma_z)) throw std::runtime_error("sigma_z must be positive and finite");
-    if (!(hb.opts[q].beta > 0.f) || !std::isfinite(hb.opts[q].beta)) throw std::runtime_error("beta must be positive and finite");
-    if (!(hb.opts[q].turn_penalty_factor == 0.f)) throw std::runtime_error(kTurnPenaltyError);
-    mode_mask_ |= 1u << hb.opts[q].mode;
-  }
+  check_batch(T, hb.trace_off, hb.opts, hb.n_opts, hb.trace_opt);
   {
     // mean sampling interval of the batch: traces sampled sparsely (C3's 30 s) have no spatial
     // coherence from one point to the next, so the locality order pays even on small graphs;
@@ -3934,6 +4144,167 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
   RM_HIP(hipMemcpyAsync(w.acc, hb.accuracy, P * 4, hipMemcpyHostToDevice, st));
   RM_HIP(hipMemcpyAsync(w.opts, hb.opts, hb.n_opts * sizeof(MatchOptions), hipMemcpyHostToDevice, st));
   RM_HIP(hipMemcpyAsync(w.trace_opt, hb.trace_opt, T * 4ull, hipMemcpyHostToDevice, st));
+  n_traces_ = T;
+  n_points_ = P;
+  run_device(rp);
+}
+
+// ------------------------------------------------------------------------------------------
+// Device JSON parser (rm_match_batch, round 4; DESIGN.md "JSON boundary").  The host reads each
+// request's structure (trace_json.hpp parse_request_deferred) and hands over the bytes between
+// its trace array's '[' and ']'; here one wave per trace finds the points by their '{' and reads
+// them in point_compact's layout only: the keys lat, lon, time, accuracy once each, numbers of at
+// most 15 digits without exponent (the values Clinger's exact path gives on the host: one IEEE
+// division of two exact doubles), points separated by single commas, lat/lon in range.  Any other
+// byte flags the trace and the host parses that request again with the generic reader, so what a
+// request returns or fails with never depends on which parser read it.
+// The point rules are json_points.hpp's (shared with the host test).
+// A wave takes its span 4 KB at a time: the window (and the bytes the points starting in it can
+// reach) is copied to LDS with 16-byte loads; 64 ballots over consecutive 64-byte chunks list the
+// window's '{' positions in order (consecutive lanes read consecutive bytes: no bank conflicts),
+// and lane j reads the window's point j from LDS.
+constexpr uint32_t kJsonWin = 4096;     // bytes of span per window
+constexpr uint32_t kJsonReach = 256;    // bytes a point may reach past its window (a compact point is < 120)
+constexpr uint32_t kJsonLds = kJsonWin + kJsonReach + 16;
+constexpr uint64_t kJsonPad = kJsonLds + 64;   // readable bytes the buffer keeps past its last span
+constexpr uint32_t kJsonMaxStarts = 128;       // '{' per window (a compact point is >= 40 bytes: <= 103)
+
+__global__ void __launch_bounds__(64) k_parse_json(const uint8_t* s, const uint64_t* span, const uint32_t* trace_off,
+                                                   uint32_t T, float* lon, float* lat, double* time, float* acc,
+                                                   uint32_t* flag, double2* tspan) {
+  __shared__ uint4 win4[kJsonLds / 16];
+  __shared__ uint16_t starts[kJsonMaxStarts];
+  const uint8_t* win = reinterpret_cast<const uint8_t*>(win4);
+  const int lane = threadIdx.x;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (uint32_t k = blockIdx.x; k < T; k += gridDim.x) {
+    const uint64_t b = span[k], e = span[k + 1];
+    if (b == e) continue;   // parsed on the host
+    const uint32_t o = trace_off[k], n = trace_off[k + 1] - o;
+    bool bad = false;
+    uint32_t base = 0;
+    for (uint64_t w = b; w < e; w += kJsonWin) {
+      // window bytes [wa, wa + kJsonLds) -> LDS (the buffer is padded: kJsonPad)
+      const uint64_t wa = w & ~(uint64_t)15;
+      __syncthreads();
+      for (uint32_t x = lane; x < kJsonLds / 16; x += 64) win4[x] = reinterpret_cast<const uint4*>(s + wa)[x];
+      __syncthreads();
+      // positions relative to wa; the loaded bytes end at kJsonLds, the span at er (when inside)
+      const uint32_t er = e - wa < (uint64_t)kJsonLds ? (uint32_t)(e - wa) : kJsonLds;
+      const bool span_ends = e - wa <= (uint64_t)kJsonLds;
+      const uint32_t w0 = (uint32_t)(w - wa), w1 = min(w0 + kJsonWin, er);
+      uint32_t ns = 0;
+      for (uint32_t c0 = w0; c0 < w1; c0 += 64) {
+        const uint32_t pos = c0 + lane;
+        const bool open = pos < w1 && win[pos] == '{';
+        const unsigned long long m = __ballot(open);
+        const uint32_t at = ns + (uint32_t)__popcll(m & below);
+        if (open && at < kJsonMaxStarts) starts[at] = (uint16_t)pos;
+        ns += (uint32_t)__popcll(m);
+      }
+      if (ns > kJsonMaxStarts) { bad = true; break; }
+      __syncthreads();
+      for (uint32_t j = lane; j < ns; j += 64) {
+        uint64_t q = starts[j];
+        const uint32_t idx = base + j;
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+        // a point ending where the loaded bytes end (but not the span) is not read here: flagged
+        if (!jp::point(win, q, er, v0, v1, v2, v3) || !jp::point_follows(win, q, er) || (q == er && !span_ends) ||
+            !jp::in_range(v0, v1) || idx >= n) {
+          bad = true;
+          break;
+        }
+        lat[o + idx] = (float)v0;
+        lon[o + idx] = (float)v1;
+        time[o + idx] = v2;
+        acc[o + idx] = (float)v3;
+        if (idx == 0) tspan[k].x = v2;       // the trace's first and last times (the batch's
+        if (idx == n - 1) tspan[k].y = v2;   // mean sampling interval, Matcher::run_parsed)
+      }
+      base += ns;
+    }
+    if (base != n) bad = true;
+    const bool any_bad = __ballot(bad) != 0ull;
+    if (lane == 0) flag[k] = any_bad ? 1u : 0u;
+  }
+}
+
+void Matcher::json_reserve(uint64_t points, uint32_t traces, uint32_t nopts, uint64_t bytes) {
+  RM_HIP(hipSetDevice(eng_->device()));
+  ensure(points, traces, nopts);
+  if (bytes > jcap_ || !jdev_) {
+    if (jdev_) { RM_HIP(hipStreamSynchronize(stream_)); (void)hipFree(jdev_); jdev_ = nullptr; jcap_ = 0; }
+    const uint64_t c = std::max<uint64_t>(bytes + bytes / 4, 1u << 20);
+    grow_workspace([&] {
+      const hipError_t e = hipMalloc((void**)&jdev_, c + kJsonPad);   // windows read up to kJsonPad past a span
+      if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); jdev_ = nullptr; throw OutOfDeviceMemory("JSON buffer"); }
+      RM_HIP(e);
+    });
+    jcap_ = c;
+  }
+  if (traces + 1u > jtcap_ || !jspan_) {
+    if (jspan_) { RM_HIP(hipStreamSynchronize(stream_)); (void)hipFree(jspan_); (void)hipFree(jflag_); (void)hipFree(jtsp_); }
+    jspan_ = nullptr; jflag_ = nullptr; jtsp_ = nullptr;
+    const uint32_t c = std::max<uint32_t>(traces + traces / 4 + 1u, 1024u);
+    RM_HIP(hipMalloc((void**)&jspan_, (uint64_t)(c + 1u) * 8u));
+    RM_HIP(hipMalloc((void**)&jflag_, (uint64_t)c * 4u));
+    RM_HIP(hipMalloc((void**)&jtsp_, (uint64_t)c * 16u));
+    jtcap_ = c;
+  }
+}
+
+void Matcher::json_upload(uint64_t off, const void* src, uint64_t n) {
+  if (!n) return;
+  if (off + n > jcap_) throw std::runtime_error("json_upload past the reserved buffer");
+  RM_HIP(hipMemcpyAsync(jdev_ + off, src, n, hipMemcpyHostToDevice, stream_));
+}
+
+void Matcher::json_parse(const uint64_t* span_off, const uint32_t* trace_off, uint32_t T, uint32_t* flags, double* tspan) {
+  if (T + 1u > jtcap_ || (uint64_t)trace_off[T] > ws_.cap_points || span_off[T] > jcap_)
+    throw std::runtime_error("json_parse without json_reserve");
+  Workspace& w = ws_;
+  RM_HIP(hipMemcpyAsync(jspan_, span_off, (T + 1ull) * 8u, hipMemcpyHostToDevice, stream_));
+  RM_HIP(hipMemcpyAsync(w.trace_off, trace_off, (T + 1ull) * 4u, hipMemcpyHostToDevice, stream_));
+  RM_HIP(hipMemsetAsync(jflag_, 0, T * 4ull, stream_));
+  hipLaunchKernelGGL(k_parse_json, dim3(std::min<uint32_t>(T, 16384u)), dim3(64), 0, stream_, (const uint8_t*)jdev_,
+                     (const uint64_t*)jspan_, (const uint32_t*)w.trace_off, T, w.lon, w.lat, w.time, w.acc, jflag_,
+                     (double2*)jtsp_);
+  RM_HIP(hipGetLastError());
+  RM_HIP(hipMemcpyAsync(flags, jflag_, T * 4ull, hipMemcpyDeviceToHost, stream_));
+  RM_HIP(hipMemcpyAsync(tspan, jtsp_, T * 16ull, hipMemcpyDeviceToHost, stream_));
+  RM_HIP(hipStreamSynchronize(stream_));
+}
+
+void Matcher::upload_points(uint64_t first, uint64_t n, const float* lon, const float* lat, const double* time,
+                            const float* acc) {
+  if (!n) return;
+  if (first + n > ws_.cap_points) throw std::runtime_error("upload_points past the reserved points");
+  Workspace& w = ws_;
+  RM_HIP(hipMemcpyAsync(w.lon + first, lon, n * 4, hipMemcpyHostToDevice, stream_));
+  RM_HIP(hipMemcpyAsync(w.lat + first, lat, n * 4, hipMemcpyHostToDevice, stream_));
+  RM_HIP(hipMemcpyAsync(w.time + first, time, n * 8, hipMemcpyHostToDevice, stream_));
+  RM_HIP(hipMemcpyAsync(w.acc + first, acc, n * 4, hipMemcpyHostToDevice, stream_));
+}
+
+void Matcher::run_parsed(const uint32_t* trace_off, uint32_t T, const MatchOptions* opts, uint32_t n_opts,
+                         const uint32_t* trace_opt, const double* tspan, const RunParams& rp) {
+  RM_HIP(hipSetDevice(eng_->device()));
+  if (T == 0) { n_traces_ = 0; n_points_ = 0; n_trans_ = 0; n_path_ = 0; seg_used_ = 0; return; }
+  check_batch(T, trace_off, opts, n_opts, trace_opt);
+  const uint64_t P = trace_off[T];
+  double span = 0.0;
+  uint64_t gaps = 0;
+  for (uint32_t k = 0; k < T; ++k) {
+    const uint32_t a = trace_off[k], e = trace_off[k + 1];
+    if (e > a + 1) { span += tspan[2 * k + 1] - tspan[2 * k]; gaps += e - a - 1; }
+  }
+  batch_sparse_ = gaps && span / (double)gaps >= kLocalitySparseS;
+  ensure(P, T, n_opts);   // reserved by json_reserve: no reallocation here (the points are in place)
+  Workspace& w = ws_;
+  hipStream_t st = stream_;
+  RM_HIP(hipMemcpyAsync(w.trace_off, trace_off, (T + 1) * 4ull, hipMemcpyHostToDevice, st));
+  RM_HIP(hipMemcpyAsync(w.opts, opts, n_opts * sizeof(MatchOptions), hipMemcpyHostToDevice, st));
+  RM_HIP(hipMemcpyAsync(w.trace_opt, trace_opt, T * 4ull, hipMemcpyHostToDevice, st));
   n_traces_ = T;
   n_points_ = P;
   run_device(rp);
@@ -4049,6 +4420,7 @@ void Matcher::run_device(const RunParams& rp) {
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
   }
   hipLaunchKernelGGL(k_routes_reg2, dim3(kReg2Grid), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave_s, dim3(kMidGrid), dim3(64), 0, st, g, v);
   hipLaunchKernelGGL(k_routes_wave, dim3(1024), dim3(64), 0, st, g, v);
   // the global tier runs in line once its scratch exists; before that, a hand-over seen at the
   // path-stage read-back allocates it and re-runs K3 (rare: bounds of many kilometres)
@@ -4064,6 +4436,7 @@ void Matcher::run_device(const RunParams& rp) {
     if (attempt) {   // the first attempt starts from the zeroed control words
       RM_HIP(hipMemsetAsync(w.ctl + 8, 0, sizeof(uint32_t), st));    // path ball hand-overs
       RM_HIP(hipMemsetAsync(w.ctl + 10, 0, sizeof(uint32_t), st));   // paths list C
+      RM_HIP(hipMemsetAsync(w.ctl + 12, 0, sizeof(uint32_t), st));   // paths list B2
     }
     if (balls) {
       hipLaunchKernelGGL(k_paths_ball, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
@@ -4073,6 +4446,7 @@ void Matcher::run_device(const RunParams& rp) {
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 0);
     }
     hipLaunchKernelGGL(k_paths_reg2, dim3(kReg2Grid), dim3(256), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_wave_s, dim3(kMidGrid), dim3(64), 0, st, g, v);
     hipLaunchKernelGGL(k_paths_wave, dim3(1024), dim3(64), 0, st, g, v);
     if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
     toc(kKPaths);

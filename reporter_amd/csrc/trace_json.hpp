@@ -36,6 +36,17 @@ namespace rm {
 constexpr bool kX87LongDouble = std::numeric_limits<long double>::digits == 64 && sizeof(long double) >= 10;
 namespace tj {
 
+// A trace array left for the device parser (rm_match_batch, round 4): the bytes strictly between
+// its '[' and the first ']' after it, and the number of '{' in them.  Only a compact trace
+// (point_compact's layout, points separated by single commas) is kept by the device parser; it
+// flags anything else, and the request is then parsed again by the generic reader.
+struct TraceSpan {
+  const char* b = nullptr;
+  const char* e = nullptr;
+  uint32_t n_open = 0;
+  bool on = false;
+};
+
 // points of many traces, appended in order (one sink per host thread)
 struct PointSink {
   std::vector<float> lon, lat, acc;
@@ -56,8 +67,8 @@ inline int mode_index(const char* s, size_t n) {
 
 class Reader {
  public:
-  Reader(const char* s, size_t len, const MatchOptions* mode_defaults)
-      : p_(s), s0_(s), end_(s + len), defaults_(mode_defaults) {}
+  Reader(const char* s, size_t len, const MatchOptions* mode_defaults, TraceSpan* defer = nullptr)
+      : p_(s), s0_(s), end_(s + len), defaults_(mode_defaults), defer_(defer) {}
 
   // Parse one request; its points are appended to `sink` (only when the request is valid).
   MatchOptions request(PointSink& sink) {
@@ -87,7 +98,8 @@ class Reader {
       }
       if (err.empty()) {
         if (trace_state_ == 0 || trace_state_ == 2) err = "trace must be an array of points";
-        else if (sink.size() == n0 && point_err_.empty()) err = "trace must contain at least one point";
+        else if (sink.size() == n0 && point_err_.empty() && !(defer_ && defer_->on))
+          err = "trace must contain at least one point";
         else if (!point_err_.empty()) err = point_err_;
       }
       if (err.empty()) return o;
@@ -113,6 +125,7 @@ class Reader {
   const char* s0_;
   const char* end_;   // the terminating NUL (word-wide reads stay before it)
   const MatchOptions* defaults_;
+  TraceSpan* defer_;             // non-null: a trace array that may be compact is left to the device
   bool top_object_ = false;
   int trace_state_ = 0;          // 0 absent, 1 array seen, 2 first "trace" value not an array
   bool opts_seen_ = false;       // first "match_options" handled
@@ -229,6 +242,46 @@ class Reader {
       return;
     }
     while (digit(*p_)) { m = m * 10u + (uint64_t)(*p_ - '0'); ++p_; }
+  }
+  // up to eight digits at q into m (m * 10^n + their value); returns n (8: all eight were digits).
+  // The caller guarantees 8 readable bytes at q.
+  static unsigned run8(const char* q, uint64_t& m) {
+    static const uint64_t kPow10u[9] = {1u, 10u, 100u, 1000u, 10000u, 100000u, 1000000u, 10000000u, 100000000u};
+    uint64_t v;
+    std::memcpy(&v, q, 8);
+    const uint64_t a = v ^ 0x3030303030303030ull;
+    const uint64_t bad = (a & 0xF0F0F0F0F0F0F0F0ull) | (((a & 0x0F0F0F0F0F0F0F0Full) + 0x0606060606060606ull) & 0x1010101010101010ull);
+    const unsigned n = bad ? (unsigned)__builtin_ctzll(bad) >> 3 : 8u;
+    if (n == 8u) m = m * 100000000u + eight_value(v);
+    else if (n) m = m * kPow10u[n] + eight_value((v << (64 - 8 * n)) | (0x3030303030303030ull >> (8 * n)));
+    return n;
+  }
+  // number() for the common token, word-wide: [-]digits[.digits], at most 15 digits, no exponent,
+  // with 40 bytes readable at p_; false (p_ unchanged) for anything else, which number() reads
+  bool number_swar(double& out) {
+    if (end_ - p_ < 40) return false;
+    const char* q = p_;
+    const bool neg = *q == '-';
+    q += neg;
+    uint64_t m = 0;
+    unsigned ni = run8(q, m);
+    if (ni == 8u) { const unsigned x = run8(q + 8, m); if (x == 8u) return false; ni += x; }
+    if (!ni) return false;
+    q += ni;
+    unsigned fr = 0;
+    if (*q == '.') {
+      ++q;
+      fr = run8(q, m);
+      if (fr == 8u) { const unsigned x = run8(q + 8, m); if (x == 8u) return false; fr += x; }
+      if (!fr) return false;
+      q += fr;
+    }
+    if (ni + fr > 15u || *q == 'e' || *q == 'E') return false;
+    static const double kPow10s[16] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15};
+    const double v = fr ? (double)m / kPow10s[fr] : (double)m;
+    out = neg ? -v : v;
+    p_ = q;
+    return true;
   }
   double number() {
     // the common token first — [-]digits[.digits], at most 15 digits, no exponent: one pass, one
@@ -469,6 +522,20 @@ class Reader {
     ws();
     if (*p_ != '[') { trace_state_ = 2; skip(1); return; }
     trace_state_ = 1;
+    if (defer_) {
+      // a compact trace starts with its first point and has no ']' before its end, so the first
+      // ']' closes it; whether the bytes between are compact points is the device parser's check
+      const char* b = p_ + 1;
+      const char* close = *b == '{' ? static_cast<const char*>(std::memchr(b, ']', (size_t)(end_ - b))) : nullptr;
+      if (close) {
+        defer_->b = b;
+        defer_->e = close;
+        defer_->n_open = (uint32_t)std::count(b, close, '{');
+        defer_->on = true;
+        p_ = close + 1;
+        return;
+      }
+    }
     ++p_; ws();
     if (*p_ == ']') { ++p_; return; }
     std::string tmp;
@@ -504,16 +571,30 @@ class Reader {
       p_ += n;
       return true;
     };
+    // the four keys as little-endian words ("lat": and "lon": 6 bytes, "time": 7, "accuracy": 11)
+    constexpr uint64_t kLat = 0x3a2274616c22ull, kLon = 0x3a226e6f6c22ull, kTime = 0x3a22656d697422ull;
+    constexpr uint64_t kAcc0 = 0x6361727563636122ull, kAcc1 = 0x3a2279ull;
     for (;;) {
       int k;
-      if (lit("\"lat\":", 6)) k = 0;
+      if (end_ - p_ >= 16) {   // one word compare per key
+        uint64_t w;
+        uint32_t w2;
+        std::memcpy(&w, p_, 8);
+        std::memcpy(&w2, p_ + 8, 4);
+        const uint64_t w6 = w & 0xffffffffffffull, w7 = w & 0xffffffffffffffull;
+        if (w6 == kLat) { k = 0; p_ += 6; }
+        else if (w6 == kLon) { k = 1; p_ += 6; }
+        else if (w7 == kTime) { k = 2; p_ += 7; }
+        else if (w == kAcc0 && (w2 & 0xffffffu) == kAcc1) { k = 3; p_ += 11; }
+        else break;
+      } else if (lit("\"lat\":", 6)) k = 0;
       else if (lit("\"lon\":", 6)) k = 1;
       else if (lit("\"time\":", 7)) k = 2;
       else if (lit("\"accuracy\":", 11)) k = 3;
       else break;
       if (seen & (1u << k) || !(*p_ == '-' || digit(*p_))) break;
       seen |= 1u << k;
-      v[k] = number();
+      if (!number_swar(v[k])) v[k] = number();
       if (*p_ == ',') { ++p_; continue; }
       if (*p_ == '}' && seen == 15u) {
         ++p_;
@@ -583,6 +664,15 @@ class Reader {
 // the DOM reader's messages; on error nothing is appended.
 inline MatchOptions parse_request(const char* text, const MatchOptions mode_defaults[5], PointSink& sink) {
   Reader r(text, std::strlen(text), mode_defaults);
+  return r.request(sink);
+}
+// Parse one request leaving its trace array to the device parser where it may be compact
+// (span.on); throws on anything the structure alone fails (the caller then parses the request
+// with parse_request, which reports the generic reader's error).
+inline MatchOptions parse_request_deferred(const char* text, size_t len, const MatchOptions mode_defaults[5],
+                                           PointSink& sink, TraceSpan& span) {
+  span = TraceSpan();
+  Reader r(text, len, mode_defaults, &span);
   return r.request(sink);
 }
 // the same, with the text's length known (len = strlen(text): the NUL at text[len] ends it)

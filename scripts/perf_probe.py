@@ -11,6 +11,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--split", type=int, default=0, help="also time M concurrent runners (streams) over sub-batches")
 ap.add_argument("--ab-locality", action="store_true", help="also time the same batch with the locality order off / on")
 ap.add_argument("--ab-modes", default="0,1,0,1", help="locality modes the A/B cycles through")
+ap.add_argument("--ball-radius", type=float, default=None, help="route-ball radius in m (0: the search tiers alone)")
 a = ap.parse_args()
 c = dict(world.CONFIGS[a.config])
 if a.traces:
@@ -24,6 +25,8 @@ t = time.time()
 tr = world.generate_traces(gp, c["n_traces"], c["n_points"], c["rate_s"], c["noise_m"], seed=7)
 print("traces %d pts %.1fs" % (len(tr["lon"]), time.time() - t), flush=True)
 eng = engine.Engine(gp, 0)
+if a.ball_radius is not None:
+    eng.set_ball_radius(a.ball_radius)
 bm = engine.BatchMatcher(eng)
 opts = engine.default_options(1, search_radius=c["search_radius"])
 t = time.time()

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "json.hpp"
+#include "json_points.hpp"
 #include "trace_json.hpp"
 
 using namespace rm;
@@ -109,6 +110,78 @@ Parsed fast_parse(const char* text, const MatchOptions* defaults, tj::PointSink&
   return t;
 }
 
+// rm_match_batch's device path for one request (capi.cpp match_json_batch_device): the host reads
+// the structure leaving a compact-looking trace array to the device, the device rules
+// (json_points.hpp, here run on the host in k_parse_json's order) read its points, and anything
+// they reject is parsed again by the generic reader.  `accepted` counts requests the device kept.
+Parsed device_parse(const char* text, const MatchOptions* defaults, size_t& accepted) {
+  tj::PointSink sk;
+  tj::TraceSpan sp;
+  Parsed t;
+  try {
+    t.opt = tj::parse_request_deferred(text, std::strlen(text), defaults, sk, sp);
+  } catch (const std::exception&) {
+    tj::PointSink fresh;
+    return fast_parse(text, defaults, fresh);
+  }
+  if (!sp.on) {
+    t.ok = true;
+    t.lon = sk.lon; t.lat = sk.lat; t.acc = sk.acc; t.time = sk.time;
+    return t;
+  }
+  const uint8_t* s = reinterpret_cast<const uint8_t*>(sp.b);
+  const uint64_t e = (uint64_t)(sp.e - sp.b);
+  bool bad = false;
+  uint32_t idx = 0;
+  for (uint64_t i = 0; i < e && !bad; ++i) {
+    if (s[i] != '{') continue;
+    uint64_t q = i;
+    double la = 0, lo = 0, tm = 0, ac = 0;
+    if (!jp::point(s, q, e, la, lo, tm, ac) || !jp::point_follows(s, q, e) || !jp::in_range(la, lo) || idx >= sp.n_open) {
+      bad = true;
+      break;
+    }
+    t.lat.push_back((float)la); t.lon.push_back((float)lo); t.time.push_back(tm); t.acc.push_back((float)ac);
+    ++idx;
+  }
+  if (bad || idx != sp.n_open) {
+    tj::PointSink fresh;
+    return fast_parse(text, defaults, fresh);
+  }
+  ++accepted;
+  t.ok = true;
+  return t;
+}
+
+// requests in the layout bench.py and json.dumps(separators=(',', ':')) write: every trace compact
+std::string gen_compact(std::mt19937_64& rng, int npts) {
+  std::uniform_real_distribution<double> ulat(-89.0, 89.0), ulon(-179.0, 179.0), uacc(0.0, 120.0);
+  std::string s = "{\"uuid\":\"" + std::to_string(rng() % 100000) + "\",\"trace\":[";
+  char b[64];
+  for (int i = 0; i < npts; ++i) {
+    std::vector<std::string> kv;
+    const int f = (int)(rng() % 4);
+    auto num = [&](double x) {
+      if (f == 0) std::snprintf(b, sizeof b, "%.6f", x);
+      else if (f == 1) std::snprintf(b, sizeof b, "%.13g", x);
+      else if (f == 2) std::snprintf(b, sizeof b, "%.0f", x);
+      else std::snprintf(b, sizeof b, "%.9f", x);
+      return std::string(b);
+    };
+    kv.push_back("\"lat\":" + num(ulat(rng)));
+    kv.push_back("\"lon\":" + num(ulon(rng)));
+    kv.push_back("\"time\":" + std::to_string(1483228800 + i * (1 + rng() % 30)));
+    kv.push_back("\"accuracy\":" + num(uacc(rng)));
+    if (rng() % 3 == 0)
+      for (size_t a = kv.size(); a > 1; --a) std::swap(kv[a - 1], kv[rng() % a]);
+    s += i ? ",{" : "{";
+    for (size_t a = 0; a < kv.size(); ++a) s += (a ? "," : "") + kv[a];
+    s += "}";
+  }
+  s += "],\"match_options\":{\"mode\":\"" + std::string(kModes[rng() % 5]) + "\",\"report_levels\":[0,1]}}";
+  return s;
+}
+
 bool same_bits(const void* a, const void* b, size_t n) { return std::memcmp(a, b, n) == 0; }
 
 bool same(const Parsed& a, const Parsed& b, std::string& why) {
@@ -202,12 +275,18 @@ int main() {
   std::mt19937_64 rng(12345);
   tj::PointSink sink;
   std::string why;
-  size_t n_ok = 0, n_err = 0, n_docs = 0;
+  size_t n_ok = 0, n_err = 0, n_docs = 0, dev_kept = 0;
+  // every document also through the device path: the same result as the DOM reader
+  auto check_device = [&](const char* doc, const Parsed& want) {
+    const Parsed d = device_parse(doc, defaults, dev_kept);
+    return same(want, d, why);
+  };
   // 1. generated valid requests (+ their options), appended one after another to one sink
   for (int it = 0; it < 3000; ++it) {
     const std::string doc = gen_request(rng, 1 + (int)(rng() % 40));
     const Parsed a = dom_parse(doc.c_str(), defaults), b = fast_parse(doc.c_str(), defaults, sink);
     CHECK(same(a, b, why), why + " in " + doc.substr(0, 300));
+    CHECK(check_device(doc.c_str(), a), "device path: " + why + " in " + doc.substr(0, 300));
     ++n_docs;
     (a.ok ? n_ok : n_err)++;
   }
@@ -239,15 +318,37 @@ int main() {
     }
     const Parsed a = dom_parse(doc.c_str(), defaults), b = fast_parse(doc.c_str(), defaults, sink);
     CHECK(same(a, b, why), why + " in " + doc);
+    CHECK(check_device(doc.c_str(), a), "device path: " + why + " in " + doc);
     ++n_docs;
     (a.ok ? n_ok : n_err)++;
   }
+  // compact requests (the device parser's layout), whole and mutated
+  const size_t kept0 = dev_kept;
+  for (int it = 0; it < 3000; ++it) {
+    std::string doc = gen_compact(rng, 1 + (int)(rng() % 30));
+    if (it % 2) {
+      const size_t pos = rng() % doc.size();
+      const char ch = alphabet[rng() % std::strlen(alphabet)];
+      switch (rng() % 3) {
+        case 0: doc[pos] = ch; break;
+        case 1: doc.erase(pos, 1); break;
+        default: doc.insert(doc.begin() + (long)pos, ch); break;
+      }
+    }
+    const Parsed a = dom_parse(doc.c_str(), defaults), b = fast_parse(doc.c_str(), defaults, sink);
+    CHECK(same(a, b, why), why + " in " + doc.substr(0, 300));
+    CHECK(check_device(doc.c_str(), a), "device path: " + why + " in " + doc.substr(0, 300));
+    ++n_docs;
+    (a.ok ? n_ok : n_err)++;
+  }
+  CHECK(dev_kept - kept0 > 1400, "the device path kept too few compact requests: " + std::to_string(dev_kept - kept0));
   for (int it = 0; it < 60; ++it) {
     const std::string doc = gen_request(rng, 2);
     for (size_t k = 0; k <= doc.size(); ++k) {
       const std::string pre = doc.substr(0, k);
       const Parsed a = dom_parse(pre.c_str(), defaults), b = fast_parse(pre.c_str(), defaults, sink);
       CHECK(same(a, b, why), why + " in prefix " + pre);
+      CHECK(check_device(pre.c_str(), a), "device path: " + why + " in prefix " + pre);
       ++n_docs;
     }
   }
@@ -296,6 +397,7 @@ int main() {
   for (const char* c : cases) {
     const Parsed a = dom_parse(c, defaults), b = fast_parse(c, defaults, sink);
     CHECK(same(a, b, why), why + " in " + c);
+    CHECK(check_device(c, a), std::string("device path: ") + why + " in " + c);
     ++n_docs;
   }
   // 4. replies: to_chars digits parse back to the same doubles as %.17g
@@ -311,6 +413,7 @@ int main() {
     const double y = std::strtod(o.c_str(), nullptr), z = std::strtod(b17, nullptr);
     CHECK(std::memcmp(&y, &z, 8) == 0 && std::memcmp(&y, &x, 8) == 0, o + " vs " + b17);
   }
-  std::printf("trace json ok: %zu documents (%zu valid, %zu errors)\n", n_docs, n_ok, n_err);
+  std::printf("trace json ok: %zu documents (%zu valid, %zu errors), %zu kept by the device path\n", n_docs, n_ok,
+              n_err, dev_kept);
   return 0;
 }
