@@ -354,6 +354,11 @@ def extras(gpath, tr, json_traces, tmpdir):
                                     "JSON parse -> H2D -> every kernel -> D2H -> segment JSON" % (
                                         len(reqs), P, sum(map(len, reqs)) / 1e6),
                             "value": P / dt, "unit": "points/s", "seconds": dt, "json_build_s_untimed": build_s,
+                            "value_library": P / (steady_ms["total_ms"] * 1e-3) if steady_ms.get("total_ms") else None,
+                            "value_library_what": "the same call's rm_match_batch wall time alone (no Python list "
+                                                  "marshalling / reply decoding)",
+                            "trace_parse": "device (k_parse_json) for compact trace arrays"
+                                           if os.environ.get("RM_JSON_DEVICE", "1") != "0" else "host",
                             "reply_mb": sum(map(len, outs)) / 1e6, "host_threads": os.cpu_count() and min(16, os.cpu_count()),
                             "library_ms": steady_ms, "seconds_of_three_calls": [r[0] for r in runs],
                             "first_call": {"seconds": cold, "library_ms": cold_ms,

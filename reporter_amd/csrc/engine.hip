@@ -453,37 +453,6 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
   unsigned long long rbest[kMaxCand];
   uint32_t n = 0;
   bool ovf = false;
-#ifdef RM_K1_RUNS
-  // The current run of hits on one road (a cell lists a road's consecutive shape pieces next to
-  // each other): its minimum is kept here and merged into the per-road slots once per run, not
-  // once per hit piece.  min is order-independent, so the slots end the same.
-  uint32_t run_road = kNone, run_s = 0;
-  unsigned long long run_key = ~0ull;
-#define K1_FLUSH_RUN()                                                                  \
-  if (run_road != kNone) {                                                              \
-    bool found_ = false;                                                                \
-    _Pragma("unroll") for (int x = 0; x < kMaxCand; ++x) {                              \
-      if (K1_UNIFORM_STOP(x < (int)n)) break;                                           \
-      if (x < (int)n && rroad[x] == run_road) {                                         \
-        found_ = true;                                                                  \
-        if (run_key < rbest[x]) { rbest[x] = run_key; rs[x] = run_s; }                  \
-      }                                                                                 \
-    }                                                                                   \
-    if (!found_) {                                                                      \
-      if (n >= (uint32_t)kMaxCand) {                                                    \
-        ovf = true;                                                                     \
-      } else {                                                                          \
-        _Pragma("unroll") for (int x = 0; x < kMaxCand; ++x) {                          \
-          if (K1_UNIFORM_STOP(x <= (int)n)) break;                                      \
-          if (x == (int)n) { rroad[x] = run_road; rbest[x] = run_key; rs[x] = run_s; }  \
-        }                                                                               \
-        ++n;                                                                            \
-      }                                                                                 \
-    }                                                                                   \
-    run_road = kNone;                                                                   \
-    run_key = ~0ull;                                                                    \
-  }
-#endif
   if (!(fx1 < 0 || fy1 < 0 || fx0 > (double)(g.ncx - 1) || fy0 > (double)(g.ncy - 1))) {
     const uint32_t x0 = fx0 < 0 ? 0u : (uint32_t)fx0, y0 = fy0 < 0 ? 0u : (uint32_t)fy0;
     const uint32_t x1 = fx1 > (double)(g.ncx - 1) ? g.ncx - 1 : (uint32_t)fx1;
@@ -532,12 +501,6 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
           if (!(sq <= r2)) continue;
           const uint32_t road = r1[y].z & 0x1fffffffu;
           const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | r1[y].w;
-#ifdef RM_K1_RUNS
-          if (road != run_road) { K1_FLUSH_RUN() }
-          run_road = road;
-          if (key < run_key) { run_key = key; run_s = sc; }
-          continue;
-#endif
           bool found = false;
 #pragma unroll
           for (int x = 0; x < kMaxCand; ++x) {
@@ -559,10 +522,6 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
       }
     }
   }
-#ifdef RM_K1_RUNS
-  if (!ovf) { K1_FLUSH_RUN() }
-#undef K1_FLUSH_RUN
-#endif
   if (ovf) {
     const uint32_t q = atomicAdd(&b.ctl[7], 1u);
     b.rl_cand[q] = (uint32_t)p;
