@@ -438,20 +438,31 @@ bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n,
   const size_t nt = std::max<size_t>(1, std::min<size_t>(pool.size(), (n + 15) / 16));
   if (m->sinks.size() < nt) m->sinks.resize(nt);
   while (m->arenas.size() < nt) m->arenas.emplace_back();
-  std::vector<uint32_t> cnt(n), topt(n);
-  std::vector<uint64_t> slen(n, 0), sink_at(n, 0);
-  std::vector<uint8_t> host_parsed(n, 0);
-  std::vector<size_t> used(nt, 0);
-  std::vector<MatchOptions> opts(n);
-  std::vector<char> failed(nt, 0);
   const Config& conf = *m->conf;
+  if (!m->m) m->m = std::make_unique<Matcher>(conf.engine.get());
+  Matcher& mt = *m->m;
+  // the requests' lengths bound each thread's trace bytes: its region of the device buffer
+  std::vector<size_t> len(n);
+  std::vector<uint64_t> region(nt + 1, 0);
   pool.run(nt, [&](size_t t) {
     const size_t a = n * t / nt, b = n * (t + 1) / nt;
-    std::vector<size_t> len(b - a);
-    size_t bytes = 0;
-    for (size_t i = a; i < b; ++i) bytes += len[i - a] = std::strlen(traces[i]);
+    uint64_t bytes = 0;
+    for (size_t i = a; i < b; ++i) bytes += len[i] = std::strlen(traces[i]);
+    region[t + 1] = (bytes + 15) & ~(uint64_t)15;
+  });
+  for (size_t t = 0; t < nt; ++t) region[t + 1] += region[t];
+  mt.json_reserve_bytes(region[nt]);
+  std::vector<uint32_t> cnt(n), topt(n);
+  std::vector<uint64_t> span(2 * n, 0), sink_at(n, 0);
+  std::vector<uint8_t> host_parsed(n, 0);
+  std::vector<MatchOptions> opts(n);
+  std::vector<char> failed(nt, 0);
+  // each thread reads its requests' structure, copies their trace arrays into its pinned arena and
+  // sends the arena at once, so the copies overlap the other threads' parsing
+  pool.run(nt, [&](size_t t) {
+    const size_t a = n * t / nt, b = n * (t + 1) / nt;
     PinnedBytes& ar = m->arenas[t];
-    ar.ensure(bytes + 1);
+    ar.ensure(region[t + 1] - region[t] + 1);
     tj::PointSink& sk = m->sinks[t];
     sk.clear();
     size_t at = 0;
@@ -460,11 +471,11 @@ bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n,
       tj::TraceSpan sp;
       const size_t before = sk.size();
       try {
-        opts[i] = tj::parse_request_deferred(traces[i], len[i - a], conf.mode_defaults, sk, sp);
+        opts[i] = tj::parse_request_deferred(traces[i], len[i], conf.mode_defaults, sk, sp);
       } catch (const std::exception&) {
         try {
           sp = tj::TraceSpan();
-          opts[i] = tj::parse_request(traces[i], len[i - a], conf.mode_defaults, sk);
+          opts[i] = tj::parse_request(traces[i], len[i], conf.mode_defaults, sk);
         } catch (const std::exception&) {
           failed[t] = 1;   // the host path reports it (as the first failing request)
           break;
@@ -473,8 +484,9 @@ bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n,
       if (sp.on) {
         const size_t k = (size_t)(sp.e - sp.b);
         std::memcpy(ar.p + at, sp.b, k);
+        span[2 * i] = region[t] + at;
+        span[2 * i + 1] = region[t] + at + k;
         at += k;
-        slen[i] = k;
         cnt[i] = sp.n_open;
       } else {
         host_parsed[i] = 1;
@@ -482,28 +494,19 @@ bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n,
         cnt[i] = (uint32_t)(sk.size() - before);
       }
     }
-    used[t] = at;
+    if (!failed[t]) mt.json_upload(region[t], ar.p, at);
   });
   for (size_t t = 0; t < nt; ++t)
-    if (failed[t]) return false;
+    if (failed[t]) { mt.sync(); return false; }
   std::vector<uint32_t> off(n + 1, 0);
-  std::vector<uint64_t> span(n + 1, 0);
   for (size_t i = 0; i < n; ++i) {
     if ((uint64_t)off[i] + cnt[i] >= 0xffffffffull) throw BatchTooLarge("batch too large (points >= 2^32)");
     off[i + 1] = off[i] + cnt[i];
-    span[i + 1] = span[i] + slen[i];
   }
   const uint64_t P = off[n];
   m->ms[0] = ms_since(t0);
   const auto t1 = clk::now();
-  if (!m->m) m->m = std::make_unique<Matcher>(conf.engine.get());
-  Matcher& mt = *m->m;
-  mt.json_reserve(P, (uint32_t)n, (uint32_t)n, span[n]);
-  uint64_t base = 0;
-  for (size_t t = 0; t < nt; ++t) {
-    mt.json_upload(base, m->arenas[t].p, used[t]);
-    base += used[t];
-  }
+  mt.json_reserve(P, (uint32_t)n, (uint32_t)n);
   std::vector<double> tsp(2 * n, 0.0);
   auto host_points = [&](size_t i, const tj::PointSink& sk, size_t at) {
     const size_t k = cnt[i];
@@ -525,7 +528,7 @@ bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n,
     // not the compact layout after all: the host reader's points, if they fit the trace's slots
     fix.clear();
     try {
-      opts[i] = tj::parse_request(traces[i], std::strlen(traces[i]), conf.mode_defaults, fix);
+      opts[i] = tj::parse_request(traces[i], len[i], conf.mode_defaults, fix);
     } catch (const std::exception&) {
       return false;
     }

@@ -2007,8 +2007,8 @@ struct VitGroup {
   float sq[kVitChunk][16];
   double gc[kVitChunk];
   uint32_t kb[kVitChunk], rel[kVitChunk];
-  uint4 bpo[kVitChunk];           // this chunk's back-pointer rows (16 x u8)
-  uint8_t cs[kVitChunk];          // this chunk's chain-start flags
+  uint4 bpo[kVitChunk + 1];       // this chunk's back-pointer rows (16 x u8); + a spare row
+  uint8_t cs[kVitChunk + 1];      // this chunk's chain-start flags (+ spare)
   uint8_t ch[kVitBt];             // choices of one backtrace block
   uint32_t nch, done, w, pad;
 };
@@ -2222,7 +2222,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     if ((uint32_t)j < C) { gs.kb[j] = kb_here; gs.rel[j] = rel_here; gs.gc[j] = gc_here; }
     wave_sync();
     uint32_t maxC = max(C, (uint32_t)__shfl_xor((int)C, 16));
-    maxC = max(maxC, (uint32_t)__shfl_xor((int)maxC, 32));
+    maxC = (uint32_t)__builtin_amdgcn_readfirstlane(max(maxC, (uint32_t)__shfl_xor((int)maxC, 32)));   // wave-uniform: a scalar loop
     // layer parameters and the first four route rows run one layer ahead of their use
     uint32_t KBn = gs.kb[0], reln = gs.rel[0];
     double gcn = gs.gc[0];
@@ -2233,10 +2233,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
 #pragma unroll
       for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
     }
-    // ---- the layers of the chunk, in order, out of LDS (groups with fewer layers idle)
+    // ---- the layers of the chunk, in order, out of LDS.  The body is branch-free for the common
+    // layer: the recurrence over the first four sources runs for every group (a group that starts
+    // a chain, has no candidates or has run out of layers computes it and drops it), further
+    // sources under wave-uniform tests, and the state moves by selects; a group past its chunk
+    // writes its row to a spare slot.  Only a chain break (backtrace) branches.
     for (uint32_t t = 0; t < maxC; ++t) {
-      if (t >= C) continue;
-      const uint32_t s = s0 + t;
+      const bool in = t < C;
       const uint32_t KB = KBn, rel = reln;
       const double gcl = gcn;
       const float sqv = sqn;
@@ -2247,21 +2250,36 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         const uint32_t tn = min(t + 1u, (uint32_t)kVitChunk - 1u);
         KBn = gs.kb[tn]; reln = gs.rel[tn]; gcn = gs.gc[tn]; sqn = gs.sq[tn][j];
       }
-      bool start = !prev_ok || (s > 0 && gcl > brk);
+      // a chain starts after a layer without candidates (prev_ok false, also at s == 0) or a gap
+      // above breakage_distance
+      const bool brk_start = !prev_ok || gcl > brk;
       double best = INF;
       int arg = -1;
-      if (KB && !start) {
-        const uint32_t jj = min((uint32_t)j, KB - 1u);
-        // row i of the layer's K_A x K_B routes starts at rel + i * KB; an invalid route
-        // or an unreachable source gives +inf, which never wins
-        vit_min<0>(best, arg, cj, gs.route_m + rel + jj, KB, prevK, gcl, inv_beta, rm0);
-        if (j >= (int)KB) { best = INF; arg = -1; }
-        if (((__ballot(j < (int)KB && arg >= 0) >> gb) & 0xffffull) == 0ull) start = true;
+      {
+        const uint32_t jj = min((uint32_t)j, KB ? KB - 1u : 0u);
+        const double* dp = gs.route_m + min(rel, (uint32_t)kVitRoutes - 1u) + jj;
+        vit_src<0>(best, arg, cj, rm0[0], gcl, inv_beta);
+        vit_src<1>(best, arg, cj, rm0[1], gcl, inv_beta);
+        vit_src<2>(best, arg, cj, rm0[2], gcl, inv_beta);
+        vit_src<3>(best, arg, cj, rm0[3], gcl, inv_beta);
+        if (__ballot(in && prevK > 4u) != 0ull) {   // wave-uniform: sources 4.. of some group
+          const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
+          vit_min<1>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
+        }
       }
-      if (s > 0 && prev_ok && (KB == 0 || start)) {
-        wave_sync();                      // the group's row stores precede the flush
-        vit_flush(b, gs, o + s0, t, j);   // rows [s0, s) are needed by the backtrace
-        backtrace_chain(b, gs, o, s - 1, prevK, j, cj);
+      const bool valid_j = j < (int)KB;
+      const bool have = valid_j && arg >= 0;
+      // no transition into any candidate of the layer: the chain breaks here too
+      const bool none = ((__ballot(have) >> gb) & 0xffffull) == 0ull;
+      const bool start = brk_start || none;
+      const bool kb0 = KB == 0;
+      const bool bt = in && prev_ok && (kb0 || start);   // the chain that ends at s - 1 is complete
+      if (__ballot(bt) != 0ull) {
+        if (bt) {
+          wave_sync();                      // the group's row stores precede the flush
+          vit_flush(b, gs, o + s0, t, j);   // rows [s0, s) are needed by the backtrace
+          backtrace_chain(b, gs, o, s0 + t - 1, prevK, j, cj);
+        }
         // the backtrace staged through route_m: bring the chunk's routes back
 #pragma unroll
         for (int x = 0; x < kVitRoutes / 16; ++x)
@@ -2278,25 +2296,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
 #pragma unroll
         for (int x = 0; x < 4; ++x) rmn[x] = dp[x * kbs];
       }
-      uint8_t* row = reinterpret_cast<uint8_t*>(&gs.bpo[t]);
-      if (KB == 0) {
-        row[j] = 255;
-        gs.cs[t] = 1;   // every lane of the group writes the same byte
-        prev_ok = false;
-        prevK = 0;
-        cj = INF;
-        continue;
-      }
-      const double em = (j < (int)KB) ? (double)sqv * inv2s2 : INF;
-      double nc;
-      uint32_t bpj;
-      if (start) { nc = (j < (int)KB) ? em : INF; bpj = 255u; }
-      else { nc = (j < (int)KB && arg >= 0) ? best + em : INF; bpj = arg >= 0 ? (uint32_t)arg : 255u; }
-      cj = nc;
-      row[j] = (uint8_t)bpj;
-      gs.cs[t] = start ? 1 : 0;   // every lane of the group writes the same byte
-      prev_ok = true;
-      prevK = KB;
+      const double em = valid_j ? (double)sqv * inv2s2 : INF;
+      const double nc = kb0 ? INF : start ? em : (have ? best + em : INF);
+      const uint32_t bpj = (kb0 || start || !have) ? 255u : (uint32_t)arg;
+      const uint32_t slot = in ? t : (uint32_t)kVitChunk;   // a group past its chunk writes the spare row
+      reinterpret_cast<uint8_t*>(&gs.bpo[slot])[j] = (uint8_t)bpj;
+      gs.cs[slot] = (kb0 || start) ? 1 : 0;   // every lane of the group writes the same byte
+      cj = in ? nc : cj;
+      prev_ok = in ? !kb0 : prev_ok;
+      prevK = in ? KB : prevK;
     }
     wave_sync();
     vit_flush(b, gs, o + s0, C, j);
@@ -4137,7 +4145,7 @@ __global__ void __launch_bounds__(64) k_parse_json(const uint8_t* s, const uint6
   const int lane = threadIdx.x;
   const unsigned long long below = (1ull << lane) - 1ull;
   for (uint32_t k = blockIdx.x; k < T; k += gridDim.x) {
-    const uint64_t b = span[k], e = span[k + 1];
+    const uint64_t b = span[2 * k], e = span[2 * k + 1];   // [begin, end) in the byte buffer
     if (b == e) continue;   // parsed on the host
     const uint32_t o = trace_off[k], n = trace_off[k + 1] - o;
     bool bad = false;
@@ -4188,41 +4196,47 @@ __global__ void __launch_bounds__(64) k_parse_json(const uint8_t* s, const uint6
   }
 }
 
-void Matcher::json_reserve(uint64_t points, uint32_t traces, uint32_t nopts, uint64_t bytes) {
+void Matcher::json_reserve_bytes(uint64_t bytes) {
+  RM_HIP(hipSetDevice(eng_->device()));
+  if (bytes <= jcap_ && jdev_) return;
+  if (jdev_) { RM_HIP(hipStreamSynchronize(stream_)); (void)hipFree(jdev_); jdev_ = nullptr; jcap_ = 0; }
+  const uint64_t c = std::max<uint64_t>(bytes + bytes / 4, 1u << 20);
+  grow_workspace([&] {
+    const hipError_t e = hipMalloc((void**)&jdev_, c + kJsonPad);   // windows read up to kJsonPad past a span
+    if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); jdev_ = nullptr; throw OutOfDeviceMemory("JSON buffer"); }
+    RM_HIP(e);
+  });
+  jcap_ = c;
+}
+
+void Matcher::json_reserve(uint64_t points, uint32_t traces, uint32_t nopts) {
   RM_HIP(hipSetDevice(eng_->device()));
   ensure(points, traces, nopts);
-  if (bytes > jcap_ || !jdev_) {
-    if (jdev_) { RM_HIP(hipStreamSynchronize(stream_)); (void)hipFree(jdev_); jdev_ = nullptr; jcap_ = 0; }
-    const uint64_t c = std::max<uint64_t>(bytes + bytes / 4, 1u << 20);
-    grow_workspace([&] {
-      const hipError_t e = hipMalloc((void**)&jdev_, c + kJsonPad);   // windows read up to kJsonPad past a span
-      if (e == hipErrorOutOfMemory) { (void)hipGetLastError(); jdev_ = nullptr; throw OutOfDeviceMemory("JSON buffer"); }
-      RM_HIP(e);
-    });
-    jcap_ = c;
-  }
-  if (traces + 1u > jtcap_ || !jspan_) {
+  if (traces > jtcap_ || !jspan_) {
     if (jspan_) { RM_HIP(hipStreamSynchronize(stream_)); (void)hipFree(jspan_); (void)hipFree(jflag_); (void)hipFree(jtsp_); }
     jspan_ = nullptr; jflag_ = nullptr; jtsp_ = nullptr;
     const uint32_t c = std::max<uint32_t>(traces + traces / 4 + 1u, 1024u);
-    RM_HIP(hipMalloc((void**)&jspan_, (uint64_t)(c + 1u) * 8u));
+    RM_HIP(hipMalloc((void**)&jspan_, (uint64_t)c * 16u));
     RM_HIP(hipMalloc((void**)&jflag_, (uint64_t)c * 4u));
     RM_HIP(hipMalloc((void**)&jtsp_, (uint64_t)c * 16u));
     jtcap_ = c;
   }
 }
 
+// thread-safe: the pool threads of rm_match_batch send their arenas as soon as they are filled
 void Matcher::json_upload(uint64_t off, const void* src, uint64_t n) {
   if (!n) return;
   if (off + n > jcap_) throw std::runtime_error("json_upload past the reserved buffer");
+  RM_HIP(hipSetDevice(eng_->device()));
   RM_HIP(hipMemcpyAsync(jdev_ + off, src, n, hipMemcpyHostToDevice, stream_));
 }
 
-void Matcher::json_parse(const uint64_t* span_off, const uint32_t* trace_off, uint32_t T, uint32_t* flags, double* tspan) {
-  if (T + 1u > jtcap_ || (uint64_t)trace_off[T] > ws_.cap_points || span_off[T] > jcap_)
-    throw std::runtime_error("json_parse without json_reserve");
+void Matcher::json_parse(const uint64_t* span, const uint32_t* trace_off, uint32_t T, uint32_t* flags, double* tspan) {
+  if (T > jtcap_ || (uint64_t)trace_off[T] > ws_.cap_points) throw std::runtime_error("json_parse without json_reserve");
+  for (uint32_t k = 0; k < T; ++k)
+    if (span[2 * k + 1] < span[2 * k] || span[2 * k + 1] > jcap_) throw std::runtime_error("json_parse: span outside the buffer");
   Workspace& w = ws_;
-  RM_HIP(hipMemcpyAsync(jspan_, span_off, (T + 1ull) * 8u, hipMemcpyHostToDevice, stream_));
+  RM_HIP(hipMemcpyAsync(jspan_, span, T * 16ull, hipMemcpyHostToDevice, stream_));
   RM_HIP(hipMemcpyAsync(w.trace_off, trace_off, (T + 1ull) * 4u, hipMemcpyHostToDevice, stream_));
   RM_HIP(hipMemsetAsync(jflag_, 0, T * 4ull, stream_));
   hipLaunchKernelGGL(k_parse_json, dim3(std::min<uint32_t>(T, 16384u)), dim3(64), 0, stream_, (const uint8_t*)jdev_,

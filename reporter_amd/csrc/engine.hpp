@@ -242,13 +242,16 @@ class Matcher {
   void run(const HostBatch& b, const RunParams& rp);
   // Run every stage over the batch already resident in HBM (inputs of the last run()).
   void run_device(const RunParams& rp);
-  // rm_match_batch's device JSON path (engine.hip k_parse_json): reserve the batch's workspace and
-  // byte buffer, upload the trace-array bytes, parse them into the point arrays (flags[k] != 0:
+  // rm_match_batch's device JSON path (engine.hip k_parse_json): reserve the byte buffer, upload
+  // the trace-array bytes (from the parse threads, as their arenas fill), reserve the workspace,
+  // parse them into the point arrays (flags[k] != 0:
   // trace k was not in the compact layout and must be parsed on the host; tspan[2k], [2k+1]: its
   // first and last times), place host-parsed traces' points, then run with the points in place
-  void json_reserve(uint64_t points, uint32_t traces, uint32_t nopts, uint64_t bytes);
-  void json_upload(uint64_t off, const void* src, uint64_t n);
-  void json_parse(const uint64_t* span_off, const uint32_t* trace_off, uint32_t T, uint32_t* flags, double* tspan);
+  void json_reserve_bytes(uint64_t bytes);                               // the byte buffer
+  void json_reserve(uint64_t points, uint32_t traces, uint32_t nopts);     // workspace + per-trace arrays
+  void json_upload(uint64_t off, const void* src, uint64_t n);             // thread-safe
+  // span[2k], span[2k+1]: trace k's bytes [begin, end) in the buffer (begin == end: host-parsed)
+  void json_parse(const uint64_t* span, const uint32_t* trace_off, uint32_t T, uint32_t* flags, double* tspan);
   void upload_points(uint64_t first, uint64_t n, const float* lon, const float* lat, const double* time, const float* acc);
   void run_parsed(const uint32_t* trace_off, uint32_t T, const MatchOptions* opts, uint32_t n_opts,
                   const uint32_t* trace_opt, const double* tspan, const RunParams& rp);
