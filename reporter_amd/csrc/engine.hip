@@ -1349,21 +1349,42 @@ struct K2Src {
   uint32_t rel;                  // the item's first transition among the block's (block scan of K_B)
   uint32_t bound, tmax;          // pair bounds; bound = kNone: handed to the search tiers
   uint32_t ob;                   // the item's first route in b.route
+  uint32_t lim;                  // routes with distance <= lim are exact from the tables (ball_exact_limit)
 };
 struct K2Smem {
   K2Src src[kK2Items];
   uint8_t owner[kK2Items * kMaxCand];   // transition of the block -> item of the block
   uint32_t wsum[kK2Items / 64];
+  uint8_t redo[kK2Items];               // a route of the item was not exact from the tables
 };
 
+// Bounds beyond the ball radius (round 4).  A table holds every node within R of its exit, so a
+// node absent from exit x's table is more than R away from it and any route through it is longer
+// than rk_x + R.  A route key computed from the tables is therefore exact whenever its distance
+// is <= rk_x + R for every usable exit x -- whatever the pair's bound: the shorter routes all run
+// inside the tables, and (for the path stage) so do the canonical predecessors of every node on
+// them.  Items whose routes all pass are answered by the tables; the others go to the search
+// tiers.  With bound <= R the limit is never needed (every route within the bound is in the
+// tables): kNone.
+__device__ __forceinline__ uint32_t ball_exact_limit(uint32_t bound, uint32_t radius, unsigned long long rk1,
+                                                     unsigned long long rk0) {
+  if (bound <= radius) return kNone;
+  uint32_t lim = kNone;
+  if (rk1 != kKeyInf) lim = min(lim, key_dist(rk1) + radius);
+  if (rk0 != kKeyInf) lim = min(lim, key_dist(rk0) + radius);
+  return lim;
+}
+
 // route of item S to the target described by (t0, t1), from the target road's rows (r1, r0)
-// in the tables of S's two exits (kRouteInvalid when there is none within the bounds)
+// in the tables of S's two exits (kRouteInvalid when there is none within the bounds); `exact`
+// false when the tables cannot decide it (ball_exact_limit)
 __device__ __forceinline__ uint32_t k2_route(const K2Src& S, const uint4& t0, const uint4& t1, const uint4& r1,
-                                             const uint4& r0) {
+                                             const uint4& r0, bool& exact) {
   const unsigned long long lab0 = ball_label(S.rk1, row_key0(r1), S.rk0, row_key0(r0));
   const unsigned long long lab1 = ball_label(S.rk1, row_key1(r1), S.rk0, row_key1(r0));
   const uint4 a0 = make_uint4(S.road, S.s, 0u, 0u);   // route_key_vals reads the source's road and offset
   const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, nullptr);
+  exact = S.lim == kNone || (key != kKeyInf && key_dist(key) <= S.lim);
   return (key != kKeyInf && key_dist(key) <= S.bound && key_time(key) <= S.tmax) ? key_dist(key) : kRouteInvalid;
 }
 
@@ -1386,7 +1407,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     const int mode = (int)(pi.z >> 16);
     K2Src S;
     exit_keys(a0, pi.x, S.rk1, S.rk0);
-    const bool fits = pi.x <= g.ball_radius[mode] && ((g.ball_mask >> mode) & 1u);
+    // the mode's tables answer any bound: beyond their radius, the routes they decide
+    const bool fits = (g.ball_mask >> mode) & 1u;
+    S.lim = ball_exact_limit(pi.x, g.ball_radius[mode], S.rk1, S.rk0);
     S.h1 = S.h0 = make_uint2(0u, 1u);
     if (fits) {   // both headers loaded together, then kept where the exit is usable
       const uint2* hp = g.ball_hdr[mode];
@@ -1431,6 +1454,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     sm.src[threadIdx.x].rel = rel;
     for (uint32_t j = 0; j < KB; ++j) sm.owner[rel + j] = (uint8_t)threadIdx.x;
   }
+  sm.redo[threadIdx.x] = 0;
   __syncthreads();
   // ---- phase 2: the block's routes, two transitions per lane and step.  Every load of a step
   // is issued before any is used: the descriptors unconditionally (a handed-over item's
@@ -1462,9 +1486,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     const uint4 ea1 = ua1 ? la1 : none, ea0 = ua0 ? la0 : none, eb1 = ub1 ? lb1 : none, eb0 = ub0 ? lb0 : none;
     const uint4* ga = (const uint4*)A.ent;
     const uint4* gb = (const uint4*)B.ent;
-    if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm));
-    if (lb) b.route[B.ob + (qb - B.rel)] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm));
+    bool xa = true, xb = true;
+    if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm), xa);
+    if (lb) b.route[B.ob + (qb - B.rel)] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm), xb);
+    if (!xa) sm.redo[sm.owner[q]] = 1;
+    if (!xb) sm.redo[sm.owner[qB]] = 1;
   }
+  // items with a route the tables could not decide: the search tiers recompute all of its routes
+  __syncthreads();
+  if (live && sm.redo[threadIdx.x] && sm.src[threadIdx.x].bound != kNone) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
 }
 
 // K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
@@ -1829,7 +1859,7 @@ __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
   const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
   unsigned long long rk1, rk0;
   exit_keys(a0, bound, rk1, rk0);
-  const bool fits = bound <= g.ball_radius[mode] && ((g.ball_mask >> mode) & 1u);
+  const bool fits = (g.ball_mask >> mode) & 1u;   // beyond the radius: when the route is exact (ball_exact_limit)
   uint2 h1 = make_uint2(0u, 1u), h0 = h1;
   if (fits) {   // both headers loaded together
     const uint2* hp = g.ball_hdr[mode];
@@ -1849,6 +1879,11 @@ __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
   const unsigned long long lab1 = d_spr(b0) ? ball_label(rk1, row_key1(r1), rk0, row_key1(r0)) : kKeyInf;
   int combo = -1;
   const unsigned long long key = route_key_vals(a0, b0, b1, lab0, lab1, &combo);
+  const uint32_t lim = ball_exact_limit(bound, g.ball_radius[mode], rk1, rk0);
+  if (lim != kNone && (key == kKeyInf || key_dist(key) > lim)) {   // not decided by the tables
+    b.rl_routes_0[atomicAdd(&b.ctl[8], 1u)] = (uint32_t)p;
+    return;
+  }
   path_walk_ball(g, b, p, lab, mode, a0, a1, b0, b1, key, combo, (int)kBallMaxKeys, r1, r0);
 }
 

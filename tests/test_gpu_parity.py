@@ -71,6 +71,30 @@ def test_route_ball_tier_radius(small_world, radius_m):
     eng.close()
 
 
+def test_route_ball_beyond_radius(built_lib, tmpdir_session):
+    """Pairs whose bound exceeds the ball radius (30 s sampling: bounds up to 2 km, tables of
+    500 m) are answered by the tables when every route of the item is provably exact
+    (ball_exact_limit: distance <= exit key + radius), else by the search tiers.  Routes, paths
+    and segments equal the oracle's (full bounded searches), and the tables decide most items."""
+    path = str(tmpdir_session / "beyond.rmg")
+    world.build_world(path, 80, 80, 200.0, seed=5, cell_m=200.0)
+    g = graphfile.load(path)
+    eng = engine.Engine(path, 0)
+    eng.set_ball_radius(500.0)
+    tr = world.generate_traces(path, n_traces=400, n_points=40, rate_s=30.0, noise_m=5.0, seed=25)
+    opts = engine.default_options(1, search_radius=100.0)
+    bm, ref = _run_both(path, g, eng, tr, opts, np.zeros(400, np.uint32))
+    c = compare_all(bm, ref, tr["trace_off"])
+    tiers = bm.route_tiers()
+    items = int(sum(np.asarray(ref["cand_n"][:-1], np.int64)))   # an upper bound of the (pair, source) items
+    assert c["chained"] > 5000
+    assert 0 < tiers["ball_to_search"] < items // 2, (tiers, items)
+    assert tiers["paths_ball_to_search"] > 0
+    print("beyond radius", tiers, "items <=", items, c)
+    bm.close()
+    eng.close()
+
+
 def test_route_ball_nodes_without_table(small_world, monkeypatch):
     """Nodes whose ball is too large get no table; transitions leaving through them are
     handed to the search tiers (K2 and paths) with identical results."""
