@@ -1372,7 +1372,9 @@ __device__ __forceinline__ uint32_t ball_exact_limit(uint32_t bound, uint32_t ra
   uint32_t lim = kNone;
   if (rk1 != kKeyInf) lim = min(lim, key_dist(rk1) + radius);
   if (rk0 != kKeyInf) lim = min(lim, key_dist(rk0) + radius);
-  return lim;
+  // a route the tables miss is longer than lim: beyond the bound too when lim >= bound, so
+  // every result (valid or not) is the tables'
+  return lim >= bound ? kNone : lim;
 }
 
 // route of item S to the target described by (t0, t1), from the target road's rows (r1, r0)
@@ -3183,15 +3185,17 @@ __device__ __forceinline__ ReportStats report_wave(const SegmentRec* segs, uint3
 
 __global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uint32_t rmask, uint32_t tmask,
                                                uint32_t* hist, unsigned long long* dur) {
-  const uint32_t k = blockIdx.x;
-  const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
-  const ReportStats st = report_wave(b.segs + b.seg_base[k], b.seg_cnt[k], npts > 0, npts ? b.time[o + npts - 1] : 0.0,
-                                     threshold, rmask, tmask, b.reps + b.seg_base[k], hist, dur);
-  if (threadIdx.x == 0) {
-    b.rep_cnt[k] = (uint32_t)st.n_reports;
-    b.stats[k] = st;
+  for (uint32_t k = blockIdx.x; k < b.T; k += gridDim.x) {   // one block per trace (a grid-stride loop over fewer blocks was slower)
+    const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
+    const ReportStats st = report_wave(b.segs + b.seg_base[k], b.seg_cnt[k], npts > 0, npts ? b.time[o + npts - 1] : 0.0,
+                                       threshold, rmask, tmask, b.reps + b.seg_base[k], hist, dur);
+    if (threadIdx.x == 0) {
+      b.rep_cnt[k] = (uint32_t)st.n_reports;
+      b.stats[k] = st;
+    }
   }
 }
+
 
 // report() over host-supplied segment lists (rm_report_segments): per-trace end time,
 // threshold and level masks; reports of trace k start at seg_off[k]
