@@ -239,8 +239,9 @@ int rm_runner_sizes(rm_runner* r, uint64_t out[10]);
  * [1] items the register search tier passed on, [2] items the second register tier passed on,
  * [3] chosen transitions the path ball tier passed to the path search tiers,
  * [4] route items the LDS wave tier passed to the global-memory tier, [5] likewise for paths,
- * [6] route items the 512-slot wave tier passed to the 4096-slot one, [7] likewise for paths */
-int rm_runner_route_tiers(rm_runner* r, uint64_t out[8]);
+ * [6] route items the 16-lane group tier passed to the 512-slot wave tier, [7] likewise for paths,
+ * [8] route items the 512-slot wave tier passed to the 4096-slot one, [9] likewise for paths */
+int rm_runner_route_tiers(rm_runner* r, uint64_t out[10]);
 int rm_runner_get_states(rm_runner* r, uint32_t* n_states, uint32_t* state_orig);
 int rm_runner_get_candidates(rm_runner* r, uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
 int rm_runner_get_routes(rm_runner* r, uint32_t* trans_off, double* gc, uint32_t* route_cm);

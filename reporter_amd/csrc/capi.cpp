@@ -1115,12 +1115,12 @@ int rm_runner_sizes(rm_runner* r, uint64_t out[10]) {
     for (int i = 0; i < 4; ++i) out[6 + i] = t[i];
   });
 }
-int rm_runner_route_tiers(rm_runner* r, uint64_t out[8]) {
+int rm_runner_route_tiers(rm_runner* r, uint64_t out[10]) {
   return guarded([&] {
     uint32_t c[kCtlWords];
     r->m->ctl_words(c);
     out[0] = c[1]; out[1] = c[3]; out[2] = c[5]; out[3] = c[8]; out[4] = c[9]; out[5] = c[10];
-    out[6] = c[11]; out[7] = c[12];
+    out[6] = c[11]; out[7] = c[12]; out[8] = c[13]; out[9] = c[14];
   });
 }
 int rm_runner_get_states(rm_runner* r, uint32_t* a, uint32_t* b) { return guarded([&] { r->m->get_states(a, b); }); }

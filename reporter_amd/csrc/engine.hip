@@ -71,7 +71,8 @@ struct DevBatch {  // POD view of the workspace for kernels
   // control words: [0] path pool used [2] error flags [3] routes list A [4] paths list A
   // [5] routes list B [6] paths list B [7] candidates list [8] path ball hand-overs
   // [9] routes list C [10] paths list C (the global-memory search tier)
-  // [11] routes list B2 [12] paths list B2 (the 512-slot wave tier's hand-overs to the 4096-slot one)
+  // [11] routes list B2 [12] paths list B2 (the group tier's hand-overs to the 512-slot wave tier)
+  // [13] routes list B3 [14] paths list B3 (the 512-slot tier's hand-overs to the 4096-slot one)
   uint32_t* rl_routes_0;  // items the K2 ball tier hands to the search tiers (count ctl[1])
   uint32_t* ctl; uint32_t* rl_routes_a; uint32_t* rl_routes_b; uint32_t* rl_paths_a; uint32_t* rl_paths_b;
   uint32_t* rl_cand;
@@ -914,10 +915,17 @@ struct SearchSmem {
   uint32_t key[H];                 // (source << 28) | node
   unsigned long long lab[H];       // u64 (dist cm, time ms) key
   FIdx fa[H], fb[H];               // frontier (slot ids), ping-pong
-  uint32_t inq[H];
+  uint32_t inq[(H + 31) / 32];     // in-frontier bits (one word per 32 slots)
   uint32_t pred[PATH ? H : 1];
   uint32_t nf, nn, used, ovf;
 };
+
+// frontier membership bits: set returns true when this call set it (the slot joins the frontier)
+__device__ __forceinline__ bool inq_set(uint32_t* inq, uint32_t slot) {
+  const uint32_t bit = 1u << (slot & 31);
+  return (atomicOr(&inq[slot >> 5], bit) & bit) == 0u;
+}
+__device__ __forceinline__ void inq_clear(uint32_t* inq, uint32_t slot) { atomicAnd(&inq[slot >> 5], ~(1u << (slot & 31))); }
 
 template <int H, bool PATH>
 __device__ __forceinline__ int h_insert(SearchSmem<H, PATH>& sm, uint32_t key) {
@@ -994,11 +1002,51 @@ struct SearchTargets {
   uint32_t delta;      // cm, kNone: every frontier node every round
 };
 
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The LDS search runs with W lanes per search: W = 64, one search per wave (a one-wave block:
+// __syncthreads), or W = 16, four searches per wave (each group of 16 lanes on its own LDS
+// slice; group steps are ordered by wave_sync, ballots masked to the group).
+template <int W>
+__device__ __forceinline__ void grp_sync() {
+  if constexpr (W == kWave) __syncthreads();
+  else wave_sync();
+}
+template <int W>
+__device__ __forceinline__ int grp_lane() { return (int)(threadIdx.x & (W - 1)); }
+template <int W>
+__device__ __forceinline__ int grp_base() { return (int)(threadIdx.x & (kWave - 1) & ~(W - 1)); }
+template <int W>
+__device__ __forceinline__ unsigned long long grp_ballot(bool x) {
+  const unsigned long long m = __ballot(x);
+  if constexpr (W == kWave) return m;
+  else return (m >> grp_base<W>()) & ((1ull << W) - 1ull);
+}
+// wave_append for a group: one atomic per group and instruction
+template <int W>
+__device__ __forceinline__ uint32_t grp_append(uint32_t* counter) {
+  if constexpr (W == kWave) {
+    return wave_append(counter);
+  } else {
+    const unsigned long long m = grp_ballot<W>(true);
+    const int j = grp_lane<W>();
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (j == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, grp_base<W>() + leader, kWave);
+    return base + (uint32_t)__popcll(m & ((1ull << j) - 1ull));
+  }
+}
+template <int W>
+__device__ __forceinline__ unsigned long long grp_min_u64(unsigned long long v) {
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const unsigned long long o = ((unsigned long long)(uint32_t)__shfl_xor((int)(v >> 32), d, kWave) << 32) |
-                                 (uint32_t)__shfl_xor((int)(uint32_t)v, d, kWave);
+  for (int d = W / 2; d >= 1; d >>= 1) {
+    const unsigned long long o = ((unsigned long long)(uint32_t)__shfl_xor((int)(v >> 32), d, W) << 32) |
+                                 (uint32_t)__shfl_xor((int)(uint32_t)v, d, W);
     v = o < v ? o : v;
   }
   return v;
@@ -1011,17 +1059,19 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 // With src == nullptr the single root is node `root` at key 0 (route-ball build).
 // With targets (n_src == 1), the search may stop early: labels below the final frontier minimum
 // are exact, the others are upper bounds (see SearchTargets).
-template <int H, bool PATH>
+template <int H, bool PATH, int W = kWave>
 __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int mode, uint32_t bound,
                                const uint4* src, uint32_t n_src, uint32_t root = 0,
                                SearchTargets tgt = SearchTargets{nullptr, 0u, kNone}) {
   using FIdx = typename SearchSmem<H, PATH>::FIdx;
   constexpr FIdx kDeferred = (FIdx)~(FIdx)0;
   static_assert((uint64_t)H <= (uint64_t)kDeferred, "frontier index needs a spare value");
-  const int lane = threadIdx.x;
+  static_assert(W == kWave || W == 16, "64 or 16 lanes per search");
+  const int lane = grp_lane<W>();
   const uint32_t acc = mode_access(mode);
-  for (int h = lane; h < H; h += kWave) {
-    sm.key[h] = kEmpty; sm.lab[h] = kKeyInf; sm.inq[h] = 0u;
+  for (int h = lane; h < H; h += W) {
+    sm.key[h] = kEmpty; sm.lab[h] = kKeyInf;
+    if ((h & 31) == 0) sm.inq[h >> 5] = 0u;
     if (PATH) sm.pred[h] = kNone;
   }
   if (lane == 0) { sm.nf = 0; sm.nn = 0; sm.used = 0; sm.ovf = 0; }
@@ -1030,12 +1080,12 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
   uint4 t0 = make_uint4(0u, 0u, 0u, 0u), t1 = t0;
   if (has_tg && (uint32_t)lane < tgt.n) { t0 = tgt.tg[2 * lane]; t1 = tgt.tg[2 * lane + 1]; }
   const bool use_min = has_tg || tgt.delta != kNone;
-  __syncthreads();
+  grp_sync<W>();
   if (!src) {
     if (lane == 0) {
       const int slot = h_insert(sm, root);
       sm.lab[slot] = 0ull;
-      sm.inq[slot] = 1u;
+      sm.inq[slot >> 5] |= 1u << (slot & 31);
       sm.fa[sm.nf++] = (FIdx)slot;
     }
   } else if ((uint32_t)lane < 2u * n_src) {  // roots: two exits per source
@@ -1049,11 +1099,11 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
       const int slot = h_insert(sm, (i << 28) | node);
       if (slot >= 0) {
         const unsigned long long old = atomicMin(&sm.lab[slot], kk);
-        if (kk < old && atomicExch(&sm.inq[slot], 1u) == 0u) sm.fa[wave_append(&sm.nf)] = (FIdx)slot;
+        if (kk < old && inq_set(sm.inq, slot)) sm.fa[grp_append<W>(&sm.nf)] = (FIdx)slot;
       }
     }
   }
-  __syncthreads();
+  grp_sync<W>();
   const uint4 sa0 = src ? src[0] : make_uint4(0u, 0u, 0u, 0u);
   for (int round = 0;; ++round) {
     const uint32_t nf = sm.nf;
@@ -1064,33 +1114,33 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
     unsigned long long thr = kKeyInf;
     if (use_min) {
       unsigned long long fm = kKeyInf;
-      for (uint32_t q = lane; q < nf; q += kWave) {
+      for (uint32_t q = lane; q < nf; q += W) {
         const unsigned long long l = sm.lab[cur[q]];
         fm = l < fm ? l : fm;
       }
-      fm = wave_min_u64(fm);
+      fm = grp_min_u64<W>(fm);
       if (has_tg) {   // every target's route key below the frontier minimum: final
         bool done = true;
         if ((uint32_t)lane < tgt.n) done = route_key(HashLabel<H, PATH>{sm, 0u}, sa0, t0, t1, nullptr) < fm;
-        if (__ballot(!done) == 0ull) break;
+        if (grp_ballot<W>(!done) == 0ull) break;
       }
       if (tgt.delta != kNone) thr = fm + ((unsigned long long)tgt.delta << 32);
     }
     if (thr == kKeyInf) {
-      for (uint32_t q = lane; q < nf; q += kWave) sm.inq[cur[q]] = 0u;
+      for (uint32_t q = lane; q < nf; q += W) inq_clear(sm.inq, cur[q]);
     } else {
-      for (uint32_t q = lane; q < nf; q += kWave) {
+      for (uint32_t q = lane; q < nf; q += W) {
         const FIdx slot = cur[q];
         if (sm.lab[slot] > thr) {   // waits for a later round (stays queued)
-          nxt[wave_append(&sm.nn)] = slot;
+          nxt[grp_append<W>(&sm.nn)] = slot;
           cur[q] = kDeferred;
         } else {
-          sm.inq[slot] = 0u;
+          inq_clear(sm.inq, slot);
         }
       }
     }
-    __syncthreads();
-    for (uint32_t q = lane; q < nf; q += kWave) {
+    grp_sync<W>();
+    for (uint32_t q = lane; q < nf; q += W) {
       const FIdx fs = cur[q];
       if (fs == kDeferred) continue;
       const int slot = fs;
@@ -1106,14 +1156,14 @@ __device__ void bounded_search(SearchSmem<H, PATH>& sm, const DevGraph& g, int m
         const int t = h_insert(sm, srcbits | rec.x);
         if (t < 0) continue;
         const unsigned long long old = atomicMin(&sm.lab[t], nk);
-        if (nk < old && atomicExch(&sm.inq[t], 1u) == 0u) nxt[wave_append(&sm.nn)] = (FIdx)t;
+        if (nk < old && inq_set(sm.inq, (uint32_t)t)) nxt[grp_append<W>(&sm.nn)] = (FIdx)t;
       }
     }
-    __syncthreads();
+    grp_sync<W>();
     if (lane == 0) { sm.nf = sm.nn; sm.nn = 0; }
-    __syncthreads();
+    grp_sync<W>();
   }
-  __syncthreads();
+  grp_sync<W>();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1938,10 +1988,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
 // K2 wave tier: one wave per (pair, source) item that outgrew both lane tiers; the
 // source is searched alone in a hash of H (source, node) labels.  Returns false when the
 // search outgrew the hash (the caller hands the item to the next tier).
-template <int H>
+template <int H, int W = kWave>
 __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const DevGraph& g, const DevBatch& b,
                                    uint32_t t) {
-  const int lane = threadIdx.x;
+  const int lane = grp_lane<W>();
   const uint64_t p = b.src_item[t];
   const uint4 pi = b.pair_info[p];
   const uint32_t i = t - b.src_off[p];
@@ -1950,12 +2000,12 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
   const uint32_t bound = pi.x, tmax = pi.y;
   const uint32_t base = b.trans_off[p];
   if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
-  __syncthreads();
-  bounded_search<H, false>(sm, g, mode, bound, s_src, 1, 0u,
-                           SearchTargets{b.cand_desc + p * kMaxCand * 2, KB, b.search_delta});
+  grp_sync<W>();
+  bounded_search<H, false, W>(sm, g, mode, bound, s_src, 1, 0u,
+                              SearchTargets{b.cand_desc + p * kMaxCand * 2, KB, b.search_delta});
   const bool ok = !sm.ovf;
   if (ok) {
-    for (uint32_t j = lane; j < KB; j += kWave) {
+    for (uint32_t j = lane; j < KB; j += W) {
       const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
       const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, nullptr);
       uint32_t out = kRouteInvalid;
@@ -1963,30 +2013,54 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
       b.route[base + i * KB + j] = out;
     }
   }
-  __syncthreads();
+  grp_sync<W>();
   return ok;
 }
 
-// Two LDS sizes (round 4): the 512-slot tier (10 KB, 16 waves per CU) takes what outgrew the
-// register tiers -- with early termination most searches end a few blocks past their targets --
-// and hands what outgrows it (list B2 in rl_routes_a, free once tier 2 has run) to the 4096-slot
-// tier (80 KB, 2 waves per CU).
+// LDS tiers (round 4).  With early termination most searches end a few blocks past their targets
+// and touch tens of nodes: the group tier runs four of them per wave, 16 lanes and a kGrpH-slot
+// hash each (four searches in the LDS of one); what outgrows it goes to the 512-slot wave tier
+// (10 KB, 16 waves per CU), then to the 4096-slot one (80 KB, 2 waves per CU).  Hand-over lists:
+// group tier <- rl_routes_b (ctl[5]) -> rl_routes_a (ctl[11], free once tier 2 has run) -> 512
+// tier -> rl_routes_0 (ctl[13], free once the lane tier has run) -> 4096 tier -> rl_routes_c.
+#ifndef RM_GRP_H
+#define RM_GRP_H 256
+#endif
+#ifndef RM_GRP_PATH_H
+#define RM_GRP_PATH_H 128   // path searches are single-target: smaller (C3 radius 0: 10.3 -> 7.4 ms at 128)
+#endif
+constexpr int kGrpH = RM_GRP_H;
+constexpr int kGrpPathH = RM_GRP_PATH_H;
+constexpr int kGrpW = 16;
+constexpr uint32_t kGrpGrid = 4096;   // blocks of the group tiers (grid-stride over their lists)
+__global__ void __launch_bounds__(64) k_routes_grp(DevGraph g, DevBatch b) {
+  __shared__ SearchSmem<kGrpH, false> sm[kWave / kGrpW];
+  __shared__ uint4 s_src[kWave / kGrpW][2];
+  const int gi = threadIdx.x / kGrpW;
+  const uint32_t n_items = b.ctl[5];
+  for (uint32_t item = blockIdx.x * (kWave / kGrpW) + gi; item < n_items; item += gridDim.x * (kWave / kGrpW)) {
+    const uint32_t t = b.rl_routes_b[item];
+    if (!routes_search_item<kGrpH, kGrpW>(sm[gi], s_src[gi], g, b, t) && grp_lane<kGrpW>() == 0)
+      b.rl_routes_a[atomicAdd(&b.ctl[11], 1u)] = t;
+  }
+}
+
 __global__ void __launch_bounds__(64) k_routes_wave_s(DevGraph g, DevBatch b) {
   __shared__ SearchSmem<kMidH, false> sm;
   __shared__ uint4 s_src[2];
-  const uint32_t n_items = b.ctl[5];
+  const uint32_t n_items = b.ctl[11];
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const uint32_t t = b.rl_routes_b[item];
-    if (!routes_search_item<kMidH>(sm, s_src, g, b, t) && threadIdx.x == 0) b.rl_routes_a[atomicAdd(&b.ctl[11], 1u)] = t;
+    const uint32_t t = b.rl_routes_a[item];
+    if (!routes_search_item<kMidH>(sm, s_src, g, b, t) && threadIdx.x == 0) b.rl_routes_0[atomicAdd(&b.ctl[13], 1u)] = t;
   }
 }
 
 __global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
   __shared__ SearchSmem<kBigH, false> sm;
   __shared__ uint4 s_src[2];
-  const uint32_t n_items = b.ctl[11];
+  const uint32_t n_items = b.ctl[13];
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const uint32_t t = b.rl_routes_a[item];
+    const uint32_t t = b.rl_routes_0[item];
     if (!routes_search_item<kBigH>(sm, s_src, g, b, t) && threadIdx.x == 0) b.rl_routes_c[atomicAdd(&b.ctl[9], 1u)] = t;
   }
 }
@@ -2096,11 +2170,6 @@ __device__ __forceinline__ void vit_min(double& best, int& arg, double cj, const
   }
 }
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 __device__ __forceinline__ double shfl_xor_d(double v, int m, int width) {
   const unsigned long long u = __double_as_longlong(v);
@@ -2666,10 +2735,10 @@ void launch_viterbi(uint32_t T, hipStream_t st, const DevBatch& v) {
 // k_paths wave tiers: one wave per chosen transition whose search outgrew the lane tier;
 // re-run the search for (i*, j*), compute canonical predecessors and write the
 // directed-edge path.  Returns false when the search outgrew the hash (next tier).
-template <int H>
+template <int H, int W = kWave>
 __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const DevGraph& g, const DevBatch& b,
                                   uint64_t p) {
-  const int lane = threadIdx.x;
+  const int lane = grp_lane<W>();
   const uint4 pi = b.pair_info[p];
   const int mode = (int)(pi.z >> 16);
   const uint32_t acc = mode_access(mode);
@@ -2677,12 +2746,12 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
   const uint32_t i = (uint32_t)b.choice[p - 1], j = (uint32_t)b.choice[p];
   const uint4 b0 = b.cand_desc[(p * kMaxCand + j) * 2], b1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
   if (lane < 2) s_src[lane] = b.cand_desc[((p - 1) * kMaxCand + i) * 2 + lane];
-  __syncthreads();
+  grp_sync<W>();
   const uint4 a0 = s_src[0], a1 = s_src[1];
-  bounded_search<H, true>(sm, g, mode, bound, s_src, 1, 0u,
+  bounded_search<H, true, W>(sm, g, mode, bound, s_src, 1, 0u,
                           SearchTargets{b.cand_desc + (p * kMaxCand + j) * 2, 1u, b.search_delta});
   if (sm.ovf) {
-    __syncthreads();
+    grp_sync<W>();
     return false;
   }
   int combo = -1;
@@ -2692,7 +2761,7 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
   const uint32_t n1a = a1.y, n0a = a1.x;
   if (combo >= 2) {
     // canonical predecessors: min edge id among tight in-edges of non-root nodes
-    for (int h = lane; h < H; h += kWave) {
+    for (int h = lane; h < H; h += W) {
       const uint32_t ku = sm.key[h];
       if (ku == kEmpty) continue;
       const unsigned long long lu = sm.lab[h];
@@ -2709,7 +2778,7 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
         if (lu + edge_key(rec, mode) == lv) atomicMin(&sm.pred[hv], e);
       }
     }
-    __syncthreads();
+    grp_sync<W>();
   }
   // walk the canonical predecessors once (lane 0) into an LDS buffer that reuses the
   // frontier arrays (H u32), then copy in travel order: inline slot when short, pool else
@@ -2745,33 +2814,47 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
     sm.nf = n;
     sm.nn = at;
   }
-  __syncthreads();
+  grp_sync<W>();
   {
     const uint32_t n = sm.nf, at = sm.nn;
     uint32_t* dst = n <= (uint32_t)kInlinePath ? b.path_inline + p * kInlinePath : (at == kNone ? nullptr : b.path_pool + at);
     if (dst)
-      for (uint32_t q = lane; q < n; q += kWave) dst[q] = pbuf[n - 1 - q];
+      for (uint32_t q = lane; q < n; q += W) dst[q] = pbuf[n - 1 - q];
   }
-  __syncthreads();
+  grp_sync<W>();
   return true;
+}
+
+// path tiers, as the route tiers: group tier <- rl_paths_b (ctl[6]) -> rl_paths_a (ctl[12]) ->
+// 512 tier -> rl_routes_0 (ctl[14], free once the path lane tier has run) -> 4096 tier -> rl_paths_c
+__global__ void __launch_bounds__(64) k_paths_grp(DevGraph g, DevBatch b) {
+  __shared__ SearchSmem<kGrpPathH, true> sm[kWave / kGrpW];
+  __shared__ uint4 s_src[kWave / kGrpW][2];
+  const int gi = threadIdx.x / kGrpW;
+  const uint32_t n_items = b.ctl[6];
+  for (uint32_t item = blockIdx.x * (kWave / kGrpW) + gi; item < n_items; item += gridDim.x * (kWave / kGrpW)) {
+    const uint32_t p = b.rl_paths_b[item];
+    if (!paths_search_item<kGrpPathH, kGrpW>(sm[gi], s_src[gi], g, b, p) && grp_lane<kGrpW>() == 0)
+      b.rl_paths_a[atomicAdd(&b.ctl[12], 1u)] = p;
+  }
 }
 
 __global__ void __launch_bounds__(64) k_paths_wave_s(DevGraph g, DevBatch b) {
   __shared__ SearchSmem<kMidH, true> sm;
   __shared__ uint4 s_src[2];
-  const uint32_t n_items = b.ctl[6];
+  const uint32_t n_items = b.ctl[12];
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const uint32_t p = b.rl_paths_b[item];
-    if (!paths_search_item<kMidH>(sm, s_src, g, b, p) && threadIdx.x == 0) b.rl_paths_a[atomicAdd(&b.ctl[12], 1u)] = p;
+    const uint32_t p = b.rl_paths_a[item];
+    if (!paths_search_item<kMidH>(sm, s_src, g, b, p) && threadIdx.x == 0) b.rl_routes_0[atomicAdd(&b.ctl[14], 1u)] = p;
   }
 }
 
 __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
   __shared__ SearchSmem<kBigH, true> sm;
   __shared__ uint4 s_src[2];
-  const uint32_t n_items = b.ctl[12];
+  const uint32_t n_items = b.ctl[14];
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const uint32_t p = b.rl_paths_a[item];
+    const uint32_t p = b.rl_routes_0[item];
     if (!paths_search_item<kBigH>(sm, s_src, g, b, p) && threadIdx.x == 0) b.rl_paths_c[atomicAdd(&b.ctl[10], 1u)] = p;
   }
 }
@@ -4432,6 +4515,7 @@ void Matcher::run_device(const RunParams& rp) {
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
   }
   hipLaunchKernelGGL(k_routes_reg2, dim3(kReg2Grid), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_grp, dim3(kGrpGrid), dim3(64), 0, st, g, v);
   hipLaunchKernelGGL(k_routes_wave_s, dim3(kMidGrid), dim3(64), 0, st, g, v);
   hipLaunchKernelGGL(k_routes_wave, dim3(1024), dim3(64), 0, st, g, v);
   // the global tier runs in line once its scratch exists; before that, a hand-over seen at the
@@ -4449,6 +4533,7 @@ void Matcher::run_device(const RunParams& rp) {
       RM_HIP(hipMemsetAsync(w.ctl + 8, 0, sizeof(uint32_t), st));    // path ball hand-overs
       RM_HIP(hipMemsetAsync(w.ctl + 10, 0, sizeof(uint32_t), st));   // paths list C
       RM_HIP(hipMemsetAsync(w.ctl + 12, 0, sizeof(uint32_t), st));   // paths list B2
+      RM_HIP(hipMemsetAsync(w.ctl + 14, 0, sizeof(uint32_t), st));   // paths list B3
     }
     if (balls) {
       hipLaunchKernelGGL(k_paths_ball, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
@@ -4458,6 +4543,7 @@ void Matcher::run_device(const RunParams& rp) {
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 0);
     }
     hipLaunchKernelGGL(k_paths_reg2, dim3(kReg2Grid), dim3(256), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_grp, dim3(kGrpGrid), dim3(64), 0, st, g, v);
     hipLaunchKernelGGL(k_paths_wave_s, dim3(kMidGrid), dim3(64), 0, st, g, v);
     hipLaunchKernelGGL(k_paths_wave, dim3(1024), dim3(64), 0, st, g, v);
     if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);

@@ -243,13 +243,14 @@ class BatchMatcher:
                          "routes_tier3", "paths_tier2", "cand_tier2"), [int(x) for x in out]))
 
     def route_tiers(self):
-        """Hand-overs of the last run: K2 ball tier -> search, register tier -> tier 2, tier 2 -> wave
-        (512-slot), 512-slot -> 4096-slot wave tier, wave -> global; the same for the path stage."""
-        out = (C.c_uint64 * 8)()
+        """Hand-overs of the last run: K2 ball tier -> search, register tier -> tier 2, tier 2 -> the
+        LDS tiers (16-lane groups, then 512- and 4096-slot waves), wave -> global; the same for the
+        path stage."""
+        out = (C.c_uint64 * 10)()
         _lib.check(_lib.lib().rm_runner_route_tiers(self._h, out))
         return dict(zip(("ball_to_search", "lane_to_tier2", "tier2_to_wave", "paths_ball_to_search",
-                         "wave_to_global", "paths_wave_to_global", "wave512_to_wave4096",
-                         "paths_wave512_to_wave4096"), [int(x) for x in out]))
+                         "wave_to_global", "paths_wave_to_global", "group_to_wave512", "paths_group_to_wave512",
+                         "wave512_to_wave4096", "paths_wave512_to_wave4096"), [int(x) for x in out]))
 
     # ---- stage outputs (parity tests) ----
     def states(self):
