@@ -47,6 +47,10 @@ void rm_matcher_destroy(rm_matcher* m);
 int rm_match(rm_matcher* m, const char* trace_json, char** out_json);
 /* n traces at once (one GPU launch sequence); outs[i] must each be freed with rm_free. */
 int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs);
+/* rm_match_batch with the n replies in one malloc'd, NUL-terminated buffer: reply i is
+ * (*buf)[off[i], off[i+1]) (off: n+1 entries, caller-allocated).  One allocation and one free
+ * (rm_free(*buf)) instead of n: the Python binding reads the replies out of one memoryview. */
+int rm_match_batch_packed(rm_matcher* m, const char* const* traces, size_t n, char** buf, uint64_t* off);
 void rm_free(char* p);
 /* Host wall times (ms) of the matcher's last uncoalesced rm_match_batch: out[0] JSON parse
  * (single pass, up to 16 host threads), [1] staging into pinned host arrays, [2] engine run

@@ -88,6 +88,7 @@ PROTOTYPES = [
     ("rm_matcher_destroy", None, [P]),
     ("rm_match", C.c_int, [P, C.c_char_p, C.POINTER(P)]),
     ("rm_match_batch", C.c_int, [P, C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(P)]),
+    ("rm_match_batch_packed", C.c_int, [P, C.POINTER(C.c_char_p), C.c_size_t, C.POINTER(P), C.POINTER(C.c_uint64)]),
     ("rm_free", None, [P]),
     ("rm_matcher_timing", C.c_int, [P, P]),
     ("rm_coalesce_stats", C.c_int, [C.POINTER(C.c_uint64)]),

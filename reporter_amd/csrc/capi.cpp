@@ -398,7 +398,13 @@ namespace {
 // The reply side of rm_match_batch (both parsers): per-trace failures fail the call naming the
 // trace, then the segments come down once and each pool thread formats its range of replies
 // straight into the caller's output strings.
-void finish_json_batch(rm_matcher* m, Matcher& mt, size_t n, size_t nt, char** outs) {
+// replies packed into one buffer (rm_match_batch_packed): reply i is (*buf)[off[i], off[i+1])
+struct PackedOut {
+  char** buf;
+  uint64_t* off;
+};
+
+void finish_json_batch(rm_matcher* m, Matcher& mt, size_t n, size_t nt, char** outs, const PackedOut* pk = nullptr) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   std::vector<uint32_t> terr(n, 0u);
@@ -411,14 +417,38 @@ void finish_json_batch(rm_matcher* m, Matcher& mt, size_t n, size_t nt, char** o
   mt.get_segments(soff, segs);
   m->ms[3] = ms_since(t3);
   const auto t4 = clk::now();
-  HostPool::get().run(nt, [&](size_t t) {
-    const size_t a = n * t / nt, b = n * (t + 1) / nt;
-    std::string js;
-    for (size_t i = a; i < b; ++i) {
-      tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], js);
-      outs[i] = dup_string(js);
-    }
-  });
+  if (pk) {   // each thread formats its range into one string, then they are copied into one buffer
+    std::vector<std::string> part(nt);
+    std::vector<uint64_t> len(n);
+    HostPool::get().run(nt, [&](size_t t) {
+      const size_t a = n * t / nt, b = n * (t + 1) / nt;
+      part[t].reserve((size_t)(soff[b] - soff[a]) * 224 + (b - a) * 16);   // ~200 bytes per segment
+      std::string js;
+      for (size_t i = a; i < b; ++i) {
+        tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], js);
+        part[t] += js;
+        len[i] = js.size();
+      }
+    });
+    pk->off[0] = 0;
+    for (size_t i = 0; i < n; ++i) pk->off[i + 1] = pk->off[i] + len[i];
+    char* buf = static_cast<char*>(std::malloc(pk->off[n] + 1));
+    if (!buf) throw std::bad_alloc();
+    HostPool::get().run(nt, [&](size_t t) {
+      std::memcpy(buf + pk->off[n * t / nt], part[t].data(), part[t].size());
+    });
+    buf[pk->off[n]] = 0;
+    *pk->buf = buf;
+  } else {
+    HostPool::get().run(nt, [&](size_t t) {
+      const size_t a = n * t / nt, b = n * (t + 1) / nt;
+      std::string js;
+      for (size_t i = a; i < b; ++i) {
+        tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], js);
+        outs[i] = dup_string(js);
+      }
+    });
+  }
   m->ms[4] = ms_since(t4);
 }
 
@@ -430,7 +460,7 @@ void finish_json_batch(rm_matcher* m, Matcher& mt, size_t n, size_t nt, char** o
 // device flags is parsed again on the host.  Any failure, and a flagged trace whose point count
 // differs from its '{' count, returns false before anything ran: the caller then takes the host
 // path, which reports exactly the error the host reader gives.
-bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n, char** outs) {
+bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n, char** outs, const PackedOut* pk) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t0 = clk::now();
@@ -542,7 +572,7 @@ bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n,
   mt.set_isolation(true);
   mt.run_parsed(off.data(), (uint32_t)n, opts.data(), (uint32_t)n, topt.data(), tsp.data(), rp);
   m->ms[2] = ms_since(t2);
-  finish_json_batch(m, mt, n, nt, outs);
+  finish_json_batch(m, mt, n, nt, outs, pk);
   m->ms[5] = ms_since(t0);
   return true;
 }
@@ -559,8 +589,9 @@ bool json_device_enabled() {
 // requests into its own point arrays, copies them into the matcher's pinned staging at their
 // batch offsets, and after the engine's run formats its range's replies straight into the
 // caller's output strings.  Any failing trace fails the call, naming the trace.
-void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs) {
-  if (n && json_device_enabled() && match_json_batch_device(m, traces, n, outs)) return;
+void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char** outs,
+                      const PackedOut* pk = nullptr) {
+  if (n && json_device_enabled() && match_json_batch_device(m, traces, n, outs, pk)) return;
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
   const auto t0 = clk::now();
@@ -619,7 +650,7 @@ void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char**
   mt.set_isolation(true);
   mt.run(hb, rp);
   m->ms[2] = ms_since(t2);
-  finish_json_batch(m, mt, n, nt, outs);
+  finish_json_batch(m, mt, n, nt, outs, pk);
   m->ms[5] = ms_since(t0);
 }
 
@@ -777,6 +808,23 @@ int rm_match_batch(rm_matcher* m, const char* const* traces, size_t n, char** ou
       for (size_t i = 0; i < n; ++i) { std::free(outs[i]); outs[i] = nullptr; }
       throw;
     }
+  });
+}
+
+int rm_match_batch_packed(rm_matcher* m, const char* const* traces, size_t n, char** buf, uint64_t* off) {
+  return guarded([&] {
+    if (!m) throw std::runtime_error("matcher is NULL");
+    if (!buf || !off) throw std::runtime_error("buf / off is NULL");
+    *buf = nullptr;
+    off[0] = 0;
+    for (size_t i = 0; i < n; ++i)
+      if (!traces[i]) throw std::runtime_error("trace string is NULL");
+    if (n == 0) {
+      *buf = static_cast<char*>(std::calloc(1, 1));
+      return;
+    }
+    const PackedOut pk{buf, off};
+    match_json_batch(m, traces, n, nullptr, &pk);   // any failing trace fails the call, naming the trace
   });
 }
 

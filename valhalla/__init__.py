@@ -51,20 +51,27 @@ class SegmentMatcher(object):
             _lib.lib().rm_free(out)
 
     def MatchMany(self, trace_jsons):
-        """Batched Match: many traces in one GPU pass (request coalescing)."""
+        """Batched Match: many traces in one GPU pass.  The replies come back in one buffer
+        (rm_match_batch_packed) and are decoded out of one memoryview: one allocation and one free
+        for the batch instead of one string_at / decode / rm_free per reply."""
         n = len(trace_jsons)
         if n == 0:
             return []
-        arr = (C.c_char_p * n)(*[t.encode("utf-8") if isinstance(t, str) else t for t in trace_jsons])
-        outs = (C.c_void_p * n)()
-        rc = _lib.lib().rm_match_batch(self._h, arr, n, outs)
+        try:
+            arr = (C.c_char_p * n)(*trace_jsons)   # bytes, as the service receives them
+        except TypeError:
+            arr = (C.c_char_p * n)(*[t.encode("utf-8") if isinstance(t, str) else t for t in trace_jsons])
+        off = (C.c_uint64 * (n + 1))()
+        buf = C.c_void_p()
+        rc = _lib.lib().rm_match_batch_packed(self._h, arr, n, C.byref(buf), off)
         if rc != 0:
             raise RuntimeError(_lib.last_error())
         try:
-            return [C.string_at(o).decode("utf-8") for o in outs]
+            o = list(off)
+            mv = memoryview((C.c_char * o[n]).from_address(buf.value)).cast("B")
+            return [str(mv[o[i]:o[i + 1]], "utf-8") for i in range(n)]
         finally:
-            for o in outs:
-                _lib.lib().rm_free(o)
+            _lib.lib().rm_free(buf)
 
     def last_timing(self):
         """Host wall ms of the last uncoalesced MatchMany: parse, stage, engine, download, format, total."""
