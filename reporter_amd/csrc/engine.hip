@@ -2124,6 +2124,10 @@ struct VitGroup {
   uint32_t nch, done, w, pad;
 };
 
+static_assert(sizeof(VitGroup) >= (kVitRoutes + 15 + 3 * 16 + 1) * sizeof(double), "K3 prefetch reads stay inside VitGroup");
+
+static_assert(sizeof(VitGroup) >= (kVitRoutes + 15 + 3 * 16 + 1) * sizeof(double), "K3 prefetch reads stay inside VitGroup");
+
 // lane I of this lane's 16-lane row (DPP row_newbcast; rows are the K3 groups)
 template <int I>
 __device__ __forceinline__ double row_bcast(double v) {
@@ -2325,7 +2329,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       if ((uint32_t)j + 32u < nf) sqdst[j + 32] = sv2;
       if ((uint32_t)j + 48u < nf) sqdst[j + 48] = sv3;
     }
-    if ((uint32_t)j < C) { gs.kb[j] = kb_here; gs.rel[j] = rel_here; gs.gc[j] = gc_here; }
+    {   // every entry written (0 past the chunk) so the unclamped prefetch stays inside VitGroup
+      const bool inc = (uint32_t)j < C;
+      gs.kb[j] = inc ? kb_here : 0u;
+      gs.rel[j] = inc ? rel_here : 0u;
+      gs.gc[j] = gc_here;
+    }
     wave_sync();
     uint32_t maxC = max(C, (uint32_t)__shfl_xor((int)C, 16));
     maxC = (uint32_t)__builtin_amdgcn_readfirstlane(max(maxC, (uint32_t)__shfl_xor((int)maxC, 32)));   // wave-uniform: a scalar loop
@@ -2395,19 +2404,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
           if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
         wave_sync();
       }
-      {   // next layer's first route rows (after any re-staging above); past the chunk the
-          // stale parameters keep the reads inside this group's LDS (never used)
-        const double* dp = gs.route_m + min(reln, (uint32_t)kVitRoutes - 1u) + min((uint32_t)j, KBn ? KBn - 1u : 0u);
+      {   // next layer's first route rows (after any re-staging above).  Lanes past K_B and stale
+          // parameters past the chunk read other bytes of this group's VitGroup (offset <= 256 +
+          // 15 + 3 x 16 doubles, inside it: static_assert below VitGroup), never used: no clamps
+        const double* dp = gs.route_m + reln + j;
         const uint32_t kbs = min(KBn, (uint32_t)kMaxCand);
 #pragma unroll
         for (int x = 0; x < 4; ++x) rmn[x] = dp[x * kbs];
       }
+      // em is +inf past K_B (and for every lane of an empty layer, which also has `start`), and
+      // best is +inf where no source reached the lane, so best + em needs no further selects
       const double em = valid_j ? (double)sqv * inv2s2 : INF;
-      const double nc = kb0 ? INF : start ? em : (have ? best + em : INF);
-      const uint32_t bpj = (kb0 || start || !have) ? 255u : (uint32_t)arg;
+      const double nc = start ? em : best + em;
+      const uint32_t bpj = (start || !have) ? 255u : (uint32_t)arg;
       const uint32_t slot = in ? t : (uint32_t)kVitChunk;   // a group past its chunk writes the spare row
       reinterpret_cast<uint8_t*>(&gs.bpo[slot])[j] = (uint8_t)bpj;
-      gs.cs[slot] = (kb0 || start) ? 1 : 0;   // every lane of the group writes the same byte
+      gs.cs[slot] = start ? 1 : 0;   // every lane of the group writes the same byte
       cj = in ? nc : cj;
       prev_ok = in ? !kb0 : prev_ok;
       prevK = in ? KB : prevK;
