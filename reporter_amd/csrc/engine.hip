@@ -4346,9 +4346,12 @@ void Matcher::json_reserve_bytes(uint64_t bytes) {
 void Matcher::json_reserve(uint64_t points, uint32_t traces, uint32_t nopts) {
   RM_HIP(hipSetDevice(eng_->device()));
   ensure(points, traces, nopts);
-  if (traces > jtcap_ || !jspan_) {
-    if (jspan_) { RM_HIP(hipStreamSynchronize(stream_)); (void)hipFree(jspan_); (void)hipFree(jflag_); (void)hipFree(jtsp_); }
+  if (traces > jtcap_ || !jspan_ || !jflag_ || !jtsp_) {
+    RM_HIP(hipStreamSynchronize(stream_));
+    for (void* q : {jspan_, (void*)jflag_, jtsp_})
+      if (q) (void)hipFree(q);
     jspan_ = nullptr; jflag_ = nullptr; jtsp_ = nullptr;
+    jtcap_ = 0;   // a failed allocation below leaves nothing recorded
     const uint32_t c = std::max<uint32_t>(traces + traces / 4 + 1u, 1024u);
     RM_HIP(hipMalloc((void**)&jspan_, (uint64_t)c * 16u));
     RM_HIP(hipMalloc((void**)&jflag_, (uint64_t)c * 4u));

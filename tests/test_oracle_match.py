@@ -163,3 +163,19 @@ def test_path_walk_counters(small_world):
     assert c["path_in_edges"] >= walked
     assert c["path_rows"] <= 2 * c["path_in_edges"] + 4 * c["chained"]
     assert mo.paths_algorithmic_bytes(c) > 116 * c["chained"]
+
+
+def test_target_stopped_counters(small_world):
+    """Counters 17-19 (the search roofline's formulation since round 4): the settles, scans and label
+    writes of the same searches stopped at their targets are a prefix of the full searches', and at
+    sparse sampling (bounds far beyond the targets) a small part of them."""
+    tr = world.generate_traces(small_world, 40, 40, rate_s=30.0, noise_m=5.0, seed=9)
+    mo.reset_counters()
+    _run(small_world, tr, search_radius=100.0)
+    c = mo.counters()
+    assert c["searches"] > 1000
+    for a, b in (("settled_to_targets", "settled"), ("scanned_to_targets", "scanned"),
+                 ("label_writes_to_targets", "label_writes")):
+        assert 0 < c[a] <= c[b], (a, c)
+    assert c["settled_to_targets"] < 0.6 * c["settled"], c
+    assert mo.routes_targets_algorithmic_bytes(c) < mo.routes_algorithmic_bytes(c)
