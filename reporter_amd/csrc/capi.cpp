@@ -460,6 +460,13 @@ void finish_json_batch(rm_matcher* m, Matcher& mt, size_t n, size_t nt, char** o
 // device flags is parsed again on the host.  Any failure, and a flagged trace whose point count
 // differs from its '{' count, returns false before anything ran: the caller then takes the host
 // path, which reports exactly the error the host reader gives.
+// batches of fewer JSON bytes take the host parse (RM_JSON_DEVICE_MIN_MB, default 8; read per call)
+uint64_t json_device_min_bytes() {
+  const char* e = std::getenv("RM_JSON_DEVICE_MIN_MB");
+  const double mb = e && *e ? std::strtod(e, nullptr) : 8.0;
+  return (uint64_t)(std::max(0.0, mb) * 1048576.0);
+}
+
 bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n, char** outs, const PackedOut* pk) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
@@ -481,6 +488,9 @@ bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n,
     region[t + 1] = (bytes + 15) & ~(uint64_t)15;
   });
   for (size_t t = 0; t < nt; ++t) region[t + 1] += region[t];
+  // below a few MB the host threads parse faster than the device path's fixed cost (an upload, a
+  // kernel and a read-back: ~0.5 ms for one 1,000-point request against ~0.1 ms on the host)
+  if (region[nt] < json_device_min_bytes()) return false;
   mt.json_reserve_bytes(region[nt]);
   std::vector<uint32_t> cnt(n), topt(n);
   std::vector<uint64_t> span(2 * n, 0), sink_at(n, 0);

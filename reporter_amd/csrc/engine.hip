@@ -4529,10 +4529,13 @@ void Matcher::run_device(const RunParams& rp) {
   } else if (n_src) {
     hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
   }
-  hipLaunchKernelGGL(k_routes_reg2, dim3(kReg2Grid), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_grp, dim3(kGrpGrid), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave_s, dim3(kMidGrid), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave, dim3(1024), dim3(64), 0, st, g, v);
+  // the search tiers' grids (grid-stride over lists the host does not read) shrink with the batch:
+  // a coalesced service batch of ~15 k points launches them mostly empty
+  const auto tgrid = [P](uint32_t full) { return (uint32_t)std::max<uint64_t>(32u, std::min<uint64_t>(full, P / 64u)); };
+  hipLaunchKernelGGL(k_routes_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
   // the global tier runs in line once its scratch exists; before that, a hand-over seen at the
   // path-stage read-back allocates it and re-runs K3 (rare: bounds of many kilometres)
   bool routes_global_done = w.gsearch != nullptr;
@@ -4557,10 +4560,10 @@ void Matcher::run_device(const RunParams& rp) {
     } else {
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 0);
     }
-    hipLaunchKernelGGL(k_paths_reg2, dim3(kReg2Grid), dim3(256), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_grp, dim3(kGrpGrid), dim3(64), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_wave_s, dim3(kMidGrid), dim3(64), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_wave, dim3(1024), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
     if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
     toc(kKPaths);
     // traversal records are laid out by a scan of path_cnt (0 for slots without a chosen transition)

@@ -18,6 +18,13 @@ from reporter_amd import world
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _device_parse_for_small_batches(monkeypatch):
+    """These batches are ~1 MB of JSON, below the size from which rm_match_batch parses on the
+    device (RM_JSON_DEVICE_MIN_MB, 8 MB): force the device path."""
+    monkeypatch.setenv("RM_JSON_DEVICE_MIN_MB", "0")
+
+
 def _compact(tr, k, fmt="%.6f", order=("lat", "lon", "time", "accuracy")):
     o0, o1 = int(tr["trace_off"][k]), int(tr["trace_off"][k + 1])
     pts = []
