@@ -104,3 +104,21 @@ def test_device_path_errors_are_the_host_readers(small_world, tmp_path, requests
     # the matcher still serves afterwards
     assert len(sm.MatchMany(requests[:3])) == 3
     sm.close()
+
+
+def test_device_path_many_threads(small_world, tmp_path, monkeypatch):
+    """2,000 compact requests: every host pool thread fills and uploads its own arena (uploads
+    from 16 threads on one stream, overlapping the parse); the replies equal the host path's."""
+    import valhalla
+    tr = world.generate_traces(small_world, n_traces=2000, n_points=40, rate_s=1.0, noise_m=5.0, seed=71)
+    reqs = [_compact(tr, k) for k in range(2000)]
+    valhalla.Configure(valhalla.write_config(str(tmp_path / "nc3.json"), small_world, device=0, coalesce=False))
+    sm = valhalla.SegmentMatcher()
+    monkeypatch.setenv("RM_JSON_DEVICE_MIN_MB", "100000")   # host parse
+    want = sm.MatchMany(reqs)
+    monkeypatch.setenv("RM_JSON_DEVICE_MIN_MB", "0")        # device parse
+    got = sm.MatchMany(reqs)
+    assert got == want
+    assert sum(len(json.loads(w)["segments"]) for w in want) > 1000
+    assert sm.MatchMany(reqs[:1500]) == want[:1500]
+    sm.close()
