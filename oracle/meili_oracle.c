@@ -120,6 +120,66 @@ static double og_acos(double c) {
   return 0.5 * OG_PI - og_asin_half(c);
 }
 static float og_mlon(float lat) { return (float)(MPD_LON_EQ * og_cos((double)lat * DEG2RAD)); }
+
+static float f32_of(uint32_t bits);
+/* ---------------- turn costs (DESIGN.md §3 rule 3b; meili TransitionCostModel's turn term) ----------------
+ * meili adds turn_penalty_factor * exp(-degree / 45) per turn of a transition's route (degree 0 = a
+ * U-turn, 180 = straight on) to |route - gc| before dividing by beta.  Restated in integers: a turn
+ * of `d` degrees weighs og_tu[d] = round(65536 exp(-d/45)), a route's turns sum to an integer U, and
+ * the transition's turn cost is U * factor / 65536 metres. */
+/* atan(t), 0 <= t <= 1: atan(t) = pi/4 + atan((t-1)/(t+1)) above tan(pi/8), then the odd Taylor
+ * series to z^45 in Horner form in z^2 (coefficients (-1)^n/(2n+1)) */
+static double og_atan_unit(double t) {
+  double off = 0.0, z = t;
+  if (t > 0.41421356237309503) { z = (t - 1.0) / (t + 1.0); off = 0.25 * OG_PI; }
+  const double s = z * z;
+  double p = 1.0 / 45.0;
+  for (int n = 21; n >= 0; --n) p = p * s + ((n & 1) ? -1.0 : 1.0) / (double)(2 * n + 1);
+  return off + z * p;
+}
+/* compass bearing in degrees [0, 360] of (dx east, dy north) */
+static double og_bearing_deg(double dx, double dy) {
+  const double ax = fabs(dx), ay = fabs(dy);
+  if (ax == 0.0 && ay == 0.0) return 0.0;
+  const double a = ax <= ay ? og_atan_unit(ax / ay) : 0.5 * OG_PI - og_atan_unit(ay / ax);
+  double th;
+  if (dx >= 0.0) th = dy >= 0.0 ? a : OG_PI - a;
+  else th = dy < 0.0 ? OG_PI + a : 2.0 * OG_PI - a;
+  return th * (180.0 / OG_PI);
+}
+/* heading stored as Valhalla's NodeInfo does (8 bits, 360/255 degree steps) and expanded back to
+ * whole degrees 0..360 */
+static uint32_t og_heading(float lon_a, float lat_a, float lon_b, float lat_b) {
+  const double dx = ((double)lon_b - (double)lon_a) * (double)og_mlon(lat_a);
+  const double dy = ((double)lat_b - (double)lat_a) * MPD_LAT;
+  const uint32_t h8 = (uint32_t)(og_bearing_deg(dx, dy) * (255.0 / 360.0) + 0.5);
+  return (h8 * 360u + 127u) / 255u;
+}
+/* per road: heading at node0 into the road (H0) and at node1 into the road (H1), each toward the
+ * first shape vertex that differs from the node's */
+static void og_road_headings(const og_graph* g, uint16_t* H0, uint16_t* H1) {
+  for (uint32_t r = 0; r < g->n_roads; ++r) {
+    const uint32_t a = g->road_vert_off[r], b = g->road_vert_off[r + 1] - 1;
+    const uint32_t* V = g->verts;
+    uint32_t k = a + 1;
+    while (k < b && V[4 * k] == V[4 * a] && V[4 * k + 1] == V[4 * a + 1]) ++k;
+    H0[r] = (uint16_t)og_heading(f32_of(V[4 * a]), f32_of(V[4 * a + 1]), f32_of(V[4 * k]), f32_of(V[4 * k + 1]));
+    k = b - 1;
+    while (k > a && V[4 * k] == V[4 * b] && V[4 * k + 1] == V[4 * b + 1]) --k;
+    H1[r] = (uint16_t)og_heading(f32_of(V[4 * b]), f32_of(V[4 * b + 1]), f32_of(V[4 * k]), f32_of(V[4 * k + 1]));
+  }
+}
+static uint32_t og_tu[181];
+static void og_turn_table(void) {
+  for (int d = 0; d <= 180; ++d) og_tu[d] = (uint32_t)lround(65536.0 * exp(-(double)d / 45.0));
+}
+/* turn between an edge arriving with back heading hb (at the node, toward where it came from) and
+ * an edge leaving with heading hs */
+static uint32_t og_turn(uint32_t hb, uint32_t hs) {
+  uint32_t d = hb > hs ? hb - hs : hs - hb;
+  if (d > 180u) d = 360u - d;
+  return og_tu[d];
+}
 /* measurement distance: Valhalla PointLL::Distance (meili GreatCircleDistance), spherical law of
    cosines on the float coordinates, radius RAD_EARTH_M, rounded to float */
 static double og_gc(float lon_a, float lat_a, float lon_b, float lat_b) {
@@ -169,8 +229,11 @@ static uint64_t mk(uint32_t d, uint32_t t) { return ((uint64_t)d << 32) | t; }
  * [17] [18] [19] settled nodes, scanned edges and label writes of the same K2 searches stopped at
  *      their targets (engine.hip SearchTargets): label-setting order settles nodes by key, and a
  *      search that stops once every target's route key is below the next key settles exactly the
- *      nodes with keys <= the largest target route key (all of them when a target is unreached) */
-#define OG_NCNT 20
+ *      nodes with keys <= the largest target route key (all of them when a target is unreached)
+ * [20] transitions whose turn weight is read from a turn row (turn_penalty_factor > 0, a valid
+ *      route entering its target road from a node: one 8 B turn row each in the table formulation)
+ * [21] nodes those routes turn at (the canonical-path walk of the search formulation) */
+#define OG_NCNT 22
 static uint64_t og_cnt[OG_NCNT];
 static uint32_t og_roots;   /* usable exits of the last search_from */
 static int og_counting = 0;
@@ -189,7 +252,7 @@ struct og_result {
   uint64_t P, T, n_trans, n_path, n_seg;
   uint32_t* n_states; uint32_t* state_orig;
   uint8_t* cand_n; uint32_t* cand_road; uint32_t* cand_s; float* cand_sq;
-  uint32_t* trans_off; double* gc; uint32_t* route;
+  uint32_t* trans_off; double* gc; uint32_t* route; uint32_t* route_turn;
   int8_t* choice; uint8_t* chain_start;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_edges; uint32_t* route_dist;
   uint32_t* seg_off; og_segment* segs;
@@ -348,6 +411,38 @@ static void canonical_preds(const og_graph* g, search_ws* w, int mode) {
       if (ku + mk(len, t_ms(len, e_speed(g, e, mode))) == kv && e < w->pred[v]) w->pred[v] = e;
     }
   }
+}
+
+/* source node of directed edge e: binary search in the CSR */
+static uint32_t og_edge_src(const og_graph* g, uint32_t e) {
+  uint32_t lo = 0, hi = g->n_nodes;
+  while (hi - lo > 1) { const uint32_t mid = (lo + hi) / 2; if (g->node_off[mid] <= e) lo = mid; else hi = mid; }
+  return lo;
+}
+
+/* Turn weight U of the route from a searched source on road ra to a target entered by combination
+ * combo (2: road rb forward from its node0, 3: rb reverse from its node1): the route's canonical
+ * path (canonical_preds must have run) walked back from the entry node; every node on it is a
+ * turn, from the edge that arrives to the edge that leaves, the exit node's arriving edge being
+ * the source road in its exit direction (as the path stage's exit edge: forward when the node is
+ * ra's node1).  Direct combinations turn nowhere: U = 0. */
+static uint32_t og_turn_walk(const og_graph* g, const search_ws* w, const uint16_t* H0, const uint16_t* H1,
+                             uint32_t ra, uint32_t rb, int combo) {
+  if (combo < 2) return 0u;
+  uint32_t hs = combo == 2 ? H0[rb] : H1[rb];   /* heading of the entry edge where it leaves the node */
+  uint32_t v = combo == 2 ? g->road_node0[rb] : g->road_node1[rb];
+  uint32_t U = 0;
+  while (w->label[v] != w->rootkey[v]) {
+    const uint32_t e = w->pred[v];
+    const uint32_t rr = g->edges[4 * (size_t)e + 3] >> 1, rev = g->edges[4 * (size_t)e + 3] & 1u;
+    U += og_turn(rev ? H0[rr] : H1[rr], hs);     /* e arrives at v: its back heading there */
+    hs = rev ? H1[rr] : H0[rr];                  /* e leaves its source */
+    v = og_edge_src(g, e);
+    og_cnt[21]++;
+  }
+  U += og_turn(v == g->road_node1[ra] ? H1[ra] : H0[ra], hs);
+  og_cnt[21]++;
+  return U;
 }
 
 typedef struct { uint32_t road, s, sq_bits; float sq; uint32_t v; } cand_t;
@@ -628,11 +723,17 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
   }
   R->n_trans = nt;
   R->route = (uint32_t*)malloc(sizeof(uint32_t) * (nt ? nt : 1));
+  R->route_turn = (uint32_t*)calloc(nt ? nt : 1, sizeof(uint32_t));
+  uint16_t* H0 = (uint16_t*)malloc(sizeof(uint16_t) * (g->n_roads ? g->n_roads : 1));
+  uint16_t* H1 = (uint16_t*)malloc(sizeof(uint16_t) * (g->n_roads ? g->n_roads : 1));
+  og_road_headings(g, H0, H1);
+  og_turn_table();
 
   /* S2 routes */
   for (uint64_t k = 0; k < T; ++k) {
     const uint32_t o = b->trace_off[k];
     const og_options* op = &b->opts[b->trace_opt[k]];
+    const int turns = op->turn_penalty_factor > 0.0f;
     for (uint32_t s = 1; s < R->n_states[k]; ++s) {
       const uint32_t la = o + s - 1, lb = o + s;
       const uint32_t pa = o + R->state_orig[la], pb = o + R->state_orig[lb];
@@ -659,15 +760,22 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
         const uint32_t ra = R->cand_road[la * (uint64_t)OG_K + i], sa = R->cand_s[la * (uint64_t)OG_K + i];
         search_from(g, &ws, ra, sa, op->mode, bound);
         uint64_t kmax = 0;
+        int preds = 0;
         for (uint32_t j = 0; j < KB; ++j) {
           const uint32_t rb = R->cand_road[lb * (uint64_t)OG_K + j], sb = R->cand_s[lb * (uint64_t)OG_K + j];
           if (e_ok(g, g->road_fwd[rb], mode_access(op->mode)) || e_ok(g, g->road_rev[rb], mode_access(op->mode)))
             og_cnt[8] += og_roots;
-          const uint64_t key = route_to(g, &ws, ra, sa, rb, sb, op->mode, NULL);
+          int combo = -1;
+          const uint64_t key = route_to(g, &ws, ra, sa, rb, sb, op->mode, &combo);
           if (key > kmax) kmax = key;
           uint32_t out = OG_ROUTE_INVALID;
           if (key != OG_KEY_INF && (uint32_t)(key >> 32) <= bound && (uint32_t)key <= tmax) out = (uint32_t)(key >> 32);
           R->route[R->trans_off[lb] + i * KB + j] = out;
+          if (turns && out != OG_ROUTE_INVALID && combo >= 2) {
+            if (!preds) { canonical_preds(g, &ws, op->mode); preds = 1; }
+            R->route_turn[R->trans_off[lb] + i * KB + j] = og_turn_walk(g, &ws, H0, H1, ra, rb, combo);
+            og_cnt[20]++;
+          }
         }
         count_to_targets(&ws, kmax);
       }
@@ -683,6 +791,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
     const og_options* op = &b->opts[b->trace_opt[k]];
     const double inv2s2 = 1.0 / (2.0 * (double)op->sigma_z * (double)op->sigma_z);
     const double inv_beta = 1.0 / (double)op->beta;
+    const double tscale = (double)op->turn_penalty_factor * 0x1p-16;   /* metres per unit of turn weight */
     int prev_ok = 0;
     for (uint32_t s = 0; s < S; ++s) {
       const uint32_t l = o + s, KB = R->cand_n[l];
@@ -697,8 +806,10 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
             const double ci = cost[(l - 1) * (uint64_t)OG_K + i];
             const uint32_t rc = R->route[R->trans_off[l] + i * KB + j];
             if (ci == INFINITY || rc == OG_ROUTE_INVALID) continue;
-            /* one fused multiply-add: cost_i + |route_m - gc| / beta, rounded once */
-            const double c = fma(fabs((double)rc * 0.01 - R->gc[l]), inv_beta, ci);
+            /* one fused multiply-add: cost_i + (turn_m + |route_m - gc|) / beta, rounded once; turn_m
+             * = U * factor / 65536 is +0 without turn costs, and +0 + x == x */
+            const double tm = (double)R->route_turn[R->trans_off[l] + i * KB + j] * tscale;
+            const double c = fma(tm + fabs((double)rc * 0.01 - R->gc[l]), inv_beta, ci);
             if (c < best) { best = c; arg = (int)i; }
           }
           const double em = (double)R->cand_sq[l * (uint64_t)OG_K + j] * inv2s2;
@@ -851,7 +962,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
   og_cnt[14] += sv.n;
   R->path_edges = pool; R->n_path = pn;
   R->segs = sv.v; R->n_seg = sv.n;
-  free(tv.v); free(stack); free(cbuf);
+  free(tv.v); free(stack); free(cbuf); free(H0); free(H1);
   ws_free(&ws);
   return R;
 }
@@ -859,7 +970,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
 void og_free(og_result* r) {
   if (!r) return;
   free(r->n_states); free(r->state_orig); free(r->cand_n); free(r->cand_road); free(r->cand_s); free(r->cand_sq);
-  free(r->trans_off); free(r->gc); free(r->route); free(r->choice); free(r->chain_start);
+  free(r->trans_off); free(r->gc); free(r->route); free(r->route_turn); free(r->choice); free(r->chain_start);
   free(r->path_off); free(r->path_cnt); free(r->path_edges); free(r->route_dist); free(r->seg_off); free(r->segs);
   free(r);
 }
@@ -877,6 +988,8 @@ void og_get_candidates(const og_result* r, uint8_t* cand_n, uint32_t* road, uint
 void og_get_routes(const og_result* r, uint32_t* trans_off, double* gc, uint32_t* route_cm) {
   memcpy(trans_off, r->trans_off, 4 * r->P); memcpy(gc, r->gc, 8 * r->P); memcpy(route_cm, r->route, 4 * r->n_trans);
 }
+void og_get_route_turns(const og_result* r, uint32_t* route_turn) { memcpy(route_turn, r->route_turn, 4 * r->n_trans); }
+void og_road_heads(const og_graph* g, uint16_t* h0, uint16_t* h1) { og_road_headings(g, h0, h1); }
 void og_get_viterbi(const og_result* r, int8_t* choice, uint8_t* chain_start) {
   memcpy(choice, r->choice, r->P); memcpy(chain_start, r->chain_start, r->P);
 }

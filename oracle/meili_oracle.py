@@ -49,7 +49,7 @@ def lib():
         h.og_free.argtypes = [C.c_void_p]
         h.og_sizes.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 4
         for n, k in (("og_get_states", 2), ("og_get_candidates", 4), ("og_get_routes", 3), ("og_get_viterbi", 2),
-                     ("og_get_paths", 4), ("og_get_segments", 2)):
+                     ("og_get_paths", 4), ("og_get_segments", 2), ("og_get_route_turns", 1)):
             getattr(h, n).argtypes = [C.c_void_p] + [C.c_void_p] * k
         h.og_report_trace.restype = C.c_int
         h.og_report_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_double, C.c_double, C.c_uint32, C.c_uint32,
@@ -61,6 +61,7 @@ def lib():
         h.og_pipeline2.argtypes = [C.POINTER(OgGraph), C.POINTER(OgBatch), C.c_double, C.c_uint32, C.c_uint32,
                                    C.c_void_p, C.c_void_p]
         h.og_prepare_path_counters.argtypes = [C.POINTER(OgGraph)]
+        h.og_road_heads.argtypes = [C.POINTER(OgGraph), C.c_void_p, C.c_void_p]
         h.og_reset_counters.argtypes = []
         h.og_get_counters.argtypes = [C.c_void_p]
         _lib = h
@@ -70,7 +71,16 @@ def lib():
 COUNTER_NAMES = ("searches", "settled", "scanned", "label_writes", "target_lookups", "route_writes",
                  "cand_items", "states", "ball_rows", "desc_reads", "cands", "grid_rows", "chained", "path_edges",
                  "segments", "path_in_edges", "path_rows", "settled_to_targets", "scanned_to_targets",
-                 "label_writes_to_targets")
+                 "label_writes_to_targets", "turn_rows", "turn_nodes")
+
+
+def road_heads(graph):
+    """(H0, H1) per road: the headings at node0 / node1 into the road (DESIGN.md §3 rule 3b)."""
+    og = make_graph(graph)
+    n = og.n_roads
+    h0, h1 = np.empty(n, np.uint16), np.empty(n, np.uint16)
+    lib().og_road_heads(C.byref(og), h0.ctypes.data, h1.ctypes.data)
+    return h0, h1
 
 
 def prepare_path_counters(graph):
@@ -203,6 +213,9 @@ def match(graph, batch):
         out["route"] = np.empty(max(NT, 1), np.uint32)
         h.og_get_routes(r, out["trans_off"].ctypes.data, out["gc"].ctypes.data, out["route"].ctypes.data)
         out["route"] = out["route"][:NT]
+        out["route_turn"] = np.empty(max(NT, 1), np.uint32)
+        h.og_get_route_turns(r, out["route_turn"].ctypes.data)
+        out["route_turn"] = out["route_turn"][:NT]
         out["choice"] = np.empty(P, np.int8)
         out["chain_start"] = np.empty(P, np.uint8)
         h.og_get_viterbi(r, out["choice"].ctypes.data, out["chain_start"].ctypes.data)

@@ -702,21 +702,16 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
       conf->mode_defaults[m].mode = m;
       if (meili) apply_options(meili->get(kModeNames[m]), conf->mode_defaults[m]);
     }
-    // meili's turn costs are not implemented: a configured non-zero turn_penalty_factor (the stock
-    // valhalla_build_config sets 200 / 140 / 100 for auto / bicycle / pedestrian) fails Configure
-    // unless the operator accepts zero turn costs with reporter_amd.ignore_turn_penalty
+    // meili's turn costs (DESIGN.md §3 rule 3b): the stock valhalla_build_config sets 200 / 140 /
+    // 100 for auto / bicycle / pedestrian, and the engine applies them.  reporter_amd.ignore_turn_penalty
+    // (an explicit opt-out, e.g. to compare with a zero-turn-cost deployment) matches without them.
     bool ignore_turn = false;
     if (const json::Value* ra = v.get("reporter_amd"))
       if (const json::Value* it = ra->get("ignore_turn_penalty"); it && it->type == json::Value::Bool) ignore_turn = it->b;
     for (int m = 0; m < 5; ++m) {
-      if (conf->mode_defaults[m].turn_penalty_factor == 0.f) continue;
-      if (!ignore_turn)
-        throw std::runtime_error(std::string("meili ") + kModeNames[m] + " turn_penalty_factor is " +
-                                 std::to_string(conf->mode_defaults[m].turn_penalty_factor) +
-                                 ": this matcher does not implement turn costs; configure 0 (valhalla_build_config "
-                                 "--meili-" + kModeNames[m] + "-turn-penalty-factor 0) or set "
-                                 "reporter_amd.ignore_turn_penalty to true to match without them");
-      conf->mode_defaults[m].turn_penalty_factor = 0.f;
+      if (!turn_factor_ok(conf->mode_defaults[m].turn_penalty_factor))
+        throw std::runtime_error(std::string("meili ") + kModeNames[m] + ": " + kTurnPenaltyError);
+      if (ignore_turn) conf->mode_defaults[m].turn_penalty_factor = 0.f;
     }
     std::string graph;
     int device = g_device;
@@ -1186,6 +1181,7 @@ int rm_runner_get_candidates(rm_runner* r, uint8_t* a, uint32_t* b, uint32_t* c,
   return guarded([&] { r->m->get_candidates(a, b, c, d); });
 }
 int rm_runner_get_routes(rm_runner* r, uint32_t* a, double* b, uint32_t* c) { return guarded([&] { r->m->get_routes(a, b, c); }); }
+int rm_runner_get_route_turns(rm_runner* r, uint32_t* a) { return guarded([&] { r->m->get_route_turns(a); }); }
 int rm_runner_get_viterbi(rm_runner* r, int8_t* a, uint8_t* b) { return guarded([&] { r->m->get_viterbi(a, b); }); }
 int rm_runner_get_paths(rm_runner* r, uint32_t* a, uint32_t* b, uint32_t* c, uint32_t* d) {
   return guarded([&] { r->m->get_paths(a, b, c, d); });

@@ -61,6 +61,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint32_t* slot_trace; uint32_t* n_states; uint32_t* state_orig; double* state_time;
   uint8_t* cand_n; uint4* cand_desc; float* cand_sq;
   uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route; uint4* pair_info;
+  uint32_t* route_turn;   // per transition: turn weight (rule 3b); null when no trace of the batch has turn costs
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
@@ -846,8 +847,9 @@ __global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long l
       const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
       const double gc = b.gc[p];   // written by k_states (the rule's own measurement)
       const MatchOptions op = b.opts[b.trace_opt[k]];
+      // .w: the pair's routes carry turn weights (turn_penalty_factor > 0, rule 3b)
       b.pair_info[p] = make_uint4(route_bound(gc, op), time_bound(b.time[pb] - b.time[pa], op),
-                                  KA | (KB << 8) | ((uint32_t)op.mode << 16), 0u);
+                                  KA | (KB << 8) | ((uint32_t)op.mode << 16), op.turn_penalty_factor > 0.f ? 1u : 0u);
     }
     b.trans_cnt[p] = c;
     b.src_cnt[p] = ns;
@@ -983,6 +985,12 @@ struct HashLabel {
   const SearchSmem<H, PATH>& sm;
   uint32_t srcbits;
   __device__ unsigned long long operator()(uint32_t node) const { return h_label(sm, srcbits | node); }
+};
+// the same for walks that name a node with its road and side (single-source searches)
+template <int H, bool PATH>
+struct HashPathLabel {
+  const SearchSmem<H, PATH>& sm;
+  __device__ unsigned long long operator()(uint32_t node, uint32_t, uint32_t) const { return h_label(sm, node); }
 };
 
 // Early termination (round 4).  A search that serves known targets (a K2
@@ -1309,10 +1317,72 @@ __device__ __forceinline__ void lane_search(L& S, const DevGraph& g, const uint4
 // routes from source a0 to the KB targets of pair slot p; results staged in LDS
 // (res[j * stride]) and stored after the last load (a store before a load-use costs a
 // full round trip: gfx9 loads and stores share vmcnt)
-template <class Label>
-__device__ __forceinline__ void route_targets(const DevBatch& b, const Label& lab, const uint4& a0, uint64_t p,
-                                              uint32_t KB, uint32_t bound, uint32_t tmax, uint64_t ob, uint32_t* res,
-                                              int stride) {
+// labels for the path walk: label of node x, which is the `side` endpoint (0: node0,
+// 1: node1) of `road` (the ball tier probes by road; the search tiers ignore both)
+template <class L>
+struct SearchPathLabels {
+  const L& s;
+  __device__ unsigned long long operator()(uint32_t x, uint32_t, uint32_t) const { return s.label(x); }
+};
+
+// Turn weight (rule 3b) of the route of combination `combo` from source (a0, a1) to target
+// (b0, b1) in a search with labels `lab` (exit root keys rk1 / rk0): the canonical path walked back
+// from the entry node as the path stage walks it, one turn per node, the exit node's arriving edge
+// being the source road in the exit's direction.  0 for the direct combinations; ok false when a
+// predecessor is missing (not reached for a valid route).
+template <class PL>
+__device__ __forceinline__ uint32_t search_turn_walk(const DevGraph& g, const PL& lab, int mode, const uint4& a0,
+                                                     const uint4& a1, const uint4& b0, const uint4& b1,
+                                                     unsigned long long rk1, unsigned long long rk0, int combo, bool& ok) {
+  ok = true;
+  if (combo < 2) return 0u;
+  const uint32_t acc = mode_access(mode);
+  const uint32_t side = combo == 2 ? 0u : 1u;
+  uint32_t hs = head_start(g.road_head[b0.x], side);   // the entry edge leaves its node with this heading
+  uint32_t x = side ? b1.y : b1.x;
+  unsigned long long lx = lab(x, b0.x, side);
+  const uint32_t hwa = g.road_head[a0.x];
+  uint32_t U = 0;
+  for (uint32_t guard = 0; guard < (1u << 20); ++guard) {
+    if (lx == kKeyInf) break;
+    if (x == a1.y && lx == rk1) return U + g.turn_w[turn_degree(head_back(hwa, 0u), hs)];   // exit forward: node1
+    if (x == a1.x && lx == rk0) return U + g.turn_w[turn_degree(head_back(hwa, 1u), hs)];   // exit reverse: node0
+    bool found = false;
+    uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+    unsigned long long plu = kKeyInf;
+    for (uint32_t q = g.in_off[x], q1 = g.in_off[x + 1]; q < q1; ++q) {
+      const uint4 r = g.in_rec[q];
+      const uint32_t inf = g.in_info[q];
+      if (!edge_ok(inf, acc)) continue;
+      const unsigned long long lu = lab(r.y, r.z >> 1, r.z & 1u);
+      if (lu != kKeyInf && lu + make_key(r.w, time_ms_dev(r.w, mode_speed_dkph(mode, inf & 0xffffu))) == lx) {
+        rec = r; plu = lu; found = true;
+        break;
+      }
+    }
+    if (!found) break;
+    const uint32_t hw = g.road_head[rec.z >> 1], rev = rec.z & 1u;
+    U += g.turn_w[turn_degree(head_back(hw, rev), hs)];
+    hs = head_start(hw, rev);
+    x = rec.y;
+    lx = plu;
+  }
+  ok = false;
+  return 0u;
+}
+
+// the turn weights of a search's routes (rule 3b): what search_turn_walk needs besides the labels
+struct TurnCtx {
+  uint4 a1;                      // the source's second descriptor word (its road's endpoints)
+  unsigned long long rk1, rk0;   // exit root keys
+  int mode;
+  bool on;                       // the pair has turn costs (pair_info.w) and the batch a route_turn array
+};
+
+template <class Label, class PL>
+__device__ __forceinline__ void route_targets(const DevGraph& g, const DevBatch& b, const Label& lab, const PL& plab,
+                                              const uint4& a0, uint64_t p, uint32_t KB, uint32_t bound, uint32_t tmax,
+                                              uint64_t ob, uint32_t* res, int stride, const TurnCtx& tc) {
   const uint64_t brow = p * kMaxCand * 2;
   for (uint32_t j0 = 0; j0 < KB; j0 += 4) {
     uint4 t0[4], t1[4];
@@ -1324,10 +1394,18 @@ __device__ __forceinline__ void route_targets(const DevBatch& b, const Label& la
     }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
-      const unsigned long long key = route_key(lab, a0, t0[x], t1[x], nullptr);
+      int combo = -1;
+      const unsigned long long key = route_key(lab, a0, t0[x], t1[x], &combo);
       uint32_t r = kRouteInvalid;
       if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
       res[((j0 + x) & (kMaxCand - 1)) * stride] = r;
+      if (tc.on && j0 + x < KB) {   // rare (turn costs in a search tier): stored straight away
+        bool ok = true;
+        const uint32_t u = r == kRouteInvalid ? 0u
+                                              : search_turn_walk(g, plab, tc.mode, a0, tc.a1, t0[x], t1[x], tc.rk1, tc.rk0, combo, ok);
+        if (!ok) trace_fail(b, p, kErrRounds);
+        b.route_turn[ob + j0 + x] = u;
+      }
     }
   }
   for (uint32_t j = 0; j < KB; ++j) b.route[ob + j] = res[j * stride];
@@ -1347,6 +1425,18 @@ __device__ __forceinline__ uint4 ball_resolve(const uint4* ent, const uint2& h, 
   if ((e.x & rmask) == road || e.x == kNone) return e;
   const uint32_t mask = (1u << h.y) - 1u;
   uint32_t s = ball_slot(road, h.y);
+  for (;;) {
+    s = (s + 1u) & mask;
+    e = ent[ball_row0(h.x) + s];
+    if ((e.x & rmask) == road || e.x == kNone) return e;
+  }
+}
+
+// ball_resolve that also gives the row's slot (s: the first probe's slot on entry)
+__device__ __forceinline__ uint4 ball_resolve_at(const uint4* ent, const uint2& h, uint32_t road, uint4 e, uint32_t rmask,
+                                                 uint32_t& s) {
+  if ((e.x & rmask) == road || e.x == kNone) return e;
+  const uint32_t mask = (1u << h.y) - 1u;
   for (;;) {
     s = (s + 1u) & mask;
     e = ent[ball_row0(h.x) + s];
@@ -1401,11 +1491,19 @@ struct K2Src {
   uint32_t ob;                   // the item's first route in b.route
   uint32_t lim;                  // routes with distance <= lim are exact from the tables (ball_exact_limit)
 };
+// per item, with turn costs (rule 3b): the mode's turn rows and the source road's headings
+struct K2Turn {
+  unsigned long long trn;        // turn rows of the item's mode (a global address)
+  uint32_t hw;                   // heading word of the source road (rm_common.hpp head_back)
+  uint32_t on;                   // the item's routes carry turn weights
+};
+template <bool TURN>
 struct K2Smem {
   K2Src src[kK2Items];
   uint8_t owner[kK2Items * kMaxCand];   // transition of the block -> item of the block
   uint32_t wsum[kK2Items / 64];
   uint8_t redo[kK2Items];               // a route of the item was not exact from the tables
+  K2Turn tsrc[TURN ? kK2Items : 1];
 };
 
 // Bounds beyond the ball radius (round 4).  A table holds every node within R of its exit, so a
@@ -1440,8 +1538,43 @@ __device__ __forceinline__ uint32_t k2_route(const K2Src& S, const uint4& t0, co
   return (key != kKeyInf && key_dist(key) <= S.bound && key_time(key) <= S.tmax) ? key_dist(key) : kRouteInvalid;
 }
 
+// The turn weight of a route the tables answer (rule 3b, TURN): the label of the entry node comes
+// from one exit strictly (on a tie the canonical path may mix both exits' trees: the item goes to
+// the search tiers), that exit's turn row holds the weight of the path from the exit node on and
+// the heading it leaves the exit node with; the turn at the exit node is from the source road.
+__device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src& S, const K2Turn& T, const uint4& t0,
+                                                  const uint4& t1, const uint4& r1, const uint4& r0, uint32_t s1,
+                                                  uint32_t s0, bool& exact, uint32_t& U) {
+  const unsigned long long k10 = row_key0(r1), k00 = row_key0(r0), k11 = row_key1(r1), k01 = row_key1(r0);
+  const unsigned long long l10 = k10 != kKeyInf ? S.rk1 + k10 : kKeyInf, l00 = k00 != kKeyInf ? S.rk0 + k00 : kKeyInf;
+  const unsigned long long l11 = k11 != kKeyInf ? S.rk1 + k11 : kKeyInf, l01 = k01 != kKeyInf ? S.rk0 + k01 : kKeyInf;
+  const unsigned long long lab0 = l00 < l10 ? l00 : l10, lab1 = l01 < l11 ? l01 : l11;
+  const uint4 a0 = make_uint4(S.road, S.s, 0u, 0u);
+  int combo = -1;
+  const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, &combo);
+  exact = S.lim == kNone || (key != kKeyInf && key_dist(key) <= S.lim);
+  const bool valid = key != kKeyInf && key_dist(key) <= S.bound && key_time(key) <= S.tmax;
+  U = 0u;
+  if (T.on && valid && combo >= 2) {
+    const uint32_t side = (uint32_t)combo - 2u;
+    const unsigned long long la = side ? l11 : l10, lb = side ? l01 : l00;
+    if (la == lb) {
+      exact = false;
+    } else {
+      const bool e1 = la < lb;
+      const uint64_t row = e1 ? ball_row0(S.h1.x) + s1 : ball_row0(S.h0.x) + s0;
+      const uint2 tw = reinterpret_cast<const uint2*>(T.trn)[row];
+      const uint32_t w = side ? tw.y : tw.x;
+      if ((w & kTurnTMask) == kTurnNone) exact = false;
+      else U = g.turn_w[turn_degree(head_back(T.hw, e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
+    }
+  }
+  return valid ? key_dist(key) : kRouteInvalid;
+}
+
+template <bool TURN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_items) {
-  __shared__ K2Smem sm;
+  __shared__ K2Smem<TURN> sm;
   const uint32_t t0i = xcd_block(blockIdx.x, gridDim.x) * kK2Items;   // first item of the block
   const uint32_t t = t0i + threadIdx.x;
   const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;              // last item of the block
@@ -1477,7 +1610,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     S.bound = pi.x;
     S.tmax = pi.y;
     S.ob = ob;
-    if (!fits || S.h1.y == 0u || S.h0.y == 0u) {   // the search tiers take it (they run later)
+    bool turn_ok = true;
+    if constexpr (TURN) {
+      K2Turn T;
+      T.on = pi.w != 0u ? 1u : 0u;
+      T.trn = (unsigned long long)(uintptr_t)g.ball_turn[mode];
+      T.hw = T.on ? g.road_head[a0.x] : 0u;
+      turn_ok = !T.on || ((g.ball_turn_mask >> mode) & 1u);   // no turn rows: the search tiers weigh the turns
+      sm.tsrc[threadIdx.x] = T;
+    }
+    if (!fits || S.h1.y == 0u || S.h0.y == 0u || !turn_ok) {   // the search tiers take it (they run later)
       S.bound = kNone;
       b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
     }
@@ -1539,8 +1681,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     const uint4* ga = (const uint4*)A.ent;
     const uint4* gb = (const uint4*)B.ent;
     bool xa = true, xb = true;
-    if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm), xa);
-    if (lb) b.route[B.ob + (qb - B.rel)] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm), xb);
+    if constexpr (TURN) {
+      const K2Turn& TA = sm.tsrc[sm.owner[q]];
+      const K2Turn& TB = sm.tsrc[sm.owner[qB]];
+      if (la) {
+        uint32_t s1 = ball_slot(ta0.x, A.h1.y), s0 = ball_slot(ta0.x, A.h0.y), u = 0;
+        const uint4 r1 = ball_resolve_at(ga, A.h1, ta0.x, ea1, rm, s1), r0 = ball_resolve_at(ga, A.h0, ta0.x, ea0, rm, s0);
+        b.route[A.ob + (q - A.rel)] = k2_route_turn(g, A, TA, ta0, ta1, r1, r0, s1, s0, xa, u);
+        if (TA.on) b.route_turn[A.ob + (q - A.rel)] = u;
+      }
+      if (lb) {
+        uint32_t s1 = ball_slot(tb0.x, B.h1.y), s0 = ball_slot(tb0.x, B.h0.y), u = 0;
+        const uint4 r1 = ball_resolve_at(gb, B.h1, tb0.x, eb1, rm, s1), r0 = ball_resolve_at(gb, B.h0, tb0.x, eb0, rm, s0);
+        b.route[B.ob + (qb - B.rel)] = k2_route_turn(g, B, TB, tb0, tb1, r1, r0, s1, s0, xb, u);
+        if (TB.on) b.route_turn[B.ob + (qb - B.rel)] = u;
+      }
+    } else {
+      if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm), xa);
+      if (lb) b.route[B.ob + (qb - B.rel)] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm), xb);
+    }
     if (!xa) sm.redo[sm.owner[q]] = 1;
     if (!xb) sm.redo[sm.owner[qB]] = 1;
   }
@@ -1555,6 +1714,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
 // With `listed`, thread q takes the q-th item the ball tier handed over (rl_routes_0, ctl[1]).
 constexpr uint64_t kListedGrid = 4096;   // blocks of a grid-stride launch over hand-over lists
 
+// TURN: compiled with the turn-weight walks (rule 3b) only for batches with turn costs (they
+// cost the plain tier registers: scratch 12 -> 64 bytes per lane)
+template <bool TURN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items, int listed) {
   // grid-stride: a listed launch is sized for every item but usually finds few hand-overs
   const uint32_t n = listed ? b.ctl[1] : n_items;
@@ -1578,7 +1740,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
     b.rl_routes_a[atomicAdd(&b.ctl[3], 1u)] = t;
     continue;
   }
-  route_targets(b, StoreLabel<RegLabels>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256);
+  route_targets(g, b, StoreLabel<RegLabels>{S}, SearchPathLabels<RegLabels>{S}, a0, p, KB, bound, tmax,
+                (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256, TurnCtx{a1, rk1, rk0, mode, TURN && pi.w != 0u});
   }
 }
 
@@ -1612,22 +1775,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
       b.rl_routes_b[x] = t;
       continue;
     }
-    route_targets(b, StoreLabel<RegLabelsT<kTier2Cap>>{S}, a0, p, KB, bound, tmax, (uint64_t)base + i * KB,
-                  &s_res[0][threadIdx.x], 256);
+    route_targets(g, b, StoreLabel<RegLabelsT<kTier2Cap>>{S}, SearchPathLabels<RegLabelsT<kTier2Cap>>{S}, a0, p, KB,
+                  bound, tmax, (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256,
+                  TurnCtx{a1, rk1, rk0, mode, pi.w != 0u && b.route_turn});
   }
 }
 
 // path of one chosen transition (slot p) with a lane-resident search: canonical
 // predecessors (smallest-id tight in-edge from a labelled node) walked back from the
 // entry node.  Returns false when the search outgrew its label store (caller queues p).
-// labels for the path walk: label of node x, which is the `side` endpoint (0: node0,
-// 1: node1) of `road` (the ball tier probes by road; the search tiers ignore both)
-template <class L>
-struct SearchPathLabels {
-  const L& s;
-  __device__ unsigned long long operator()(uint32_t x, uint32_t, uint32_t) const { return s.label(x); }
-};
-
 // Canonical predecessor of node x (label lx): the smallest-id usable in-edge (u -> x) with
 // label(u) + key(edge) == lx, in ascending edge id.  Each in-edge is one self-contained record
 // (edge, source node, road|rev, length; info word): one round trip before its label probe
@@ -2005,12 +2161,24 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
                               SearchTargets{b.cand_desc + p * kMaxCand * 2, KB, b.search_delta});
   const bool ok = !sm.ovf;
   if (ok) {
+    const bool turn = pi.w != 0u && b.route_turn;
+    unsigned long long rk1 = kKeyInf, rk0 = kKeyInf;
+    if (turn) exit_keys(s_src[0], bound, rk1, rk0);
     for (uint32_t j = lane; j < KB; j += W) {
       const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
-      const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, nullptr);
+      int combo = -1;
+      const unsigned long long key = route_key(HashLabel<H, false>{sm, 0u}, s_src[0], t0, t1, &combo);
       uint32_t out = kRouteInvalid;
       if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) out = key_dist(key);
       b.route[base + i * KB + j] = out;
+      if (turn) {   // the route's turn weight (rule 3b) from the same labels
+        bool wok = true;
+        const uint32_t u = out == kRouteInvalid ? 0u
+                                                : search_turn_walk(g, HashPathLabel<H, false>{sm}, mode, s_src[0], s_src[1],
+                                                                   t0, t1, rk1, rk0, combo, wok);
+        if (!wok) trace_fail(b, p, kErrRounds);
+        b.route_turn[base + i * KB + j] = u;
+      }
     }
   }
   grp_sync<W>();
@@ -2126,8 +2294,6 @@ struct VitGroup {
 
 static_assert(sizeof(VitGroup) >= (kVitRoutes + 15 + 3 * 16 + 1) * sizeof(double), "K3 prefetch reads stay inside VitGroup");
 
-static_assert(sizeof(VitGroup) >= (kVitRoutes + 15 + 3 * 16 + 1) * sizeof(double), "K3 prefetch reads stay inside VitGroup");
-
 // lane I of this lane's 16-lane row (DPP row_newbcast; rows are the K3 groups)
 template <int I>
 __device__ __forceinline__ double row_bcast(double v) {
@@ -2141,35 +2307,42 @@ __device__ __forceinline__ double row_bcast(double v) {
 // each source costs a subtract, a fused multiply-add, a compare, a min and one select.  Sources past
 // prevK in the last block need no guard: lanes i >= prevK hold cj = +inf (every layer sets
 // cost +inf past its KB), and +inf (or NaN from the unstaged LDS they read) never wins.
-template <int I>
-__device__ __forceinline__ void vit_src(double& best, int& arg, double cj, double rm, double gcl, double inv_beta) {
+template <int I, bool TURN>
+__device__ __forceinline__ void vit_src(double& best, int& arg, double cj, double rm, double tm, double gcl, double inv_beta) {
   // fma(|route_m - gc|, 1/beta, cost of source i): one rounding, as the oracle's fma; an
-  // invalid route is +inf and stays +inf
-  const double c = __builtin_fma(fabs(rm - gcl), inv_beta, row_bcast<I>(cj));
+  // invalid route is +inf and stays +inf.  With turn costs (rule 3b) the route's turn cost in
+  // metres is added to |route_m - gc| first, as the oracle does.
+  const double d = TURN ? tm + fabs(rm - gcl) : fabs(rm - gcl);
+  const double c = __builtin_fma(d, inv_beta, row_bcast<I>(cj));
   const bool take = c < best;
   best = __builtin_fmin(best, c);   // = c exactly when take (no NaN reaches here, costs >= 0)
   arg = take ? I : arg;
 }
-template <int B>
-__device__ __forceinline__ void vit_min(double& best, int& arg, double cj, const double* dp, uint32_t KB,
-                                        uint32_t prevK, double gcl, double inv_beta, const double (&rm0)[4]) {
+template <int B, bool TURN>
+__device__ __forceinline__ void vit_min(double& best, int& arg, double cj, const double* dp, const double* tp, uint32_t KB,
+                                        uint32_t prevK, double gcl, double inv_beta, const double (&rm0)[4],
+                                        const double (&tm0)[4]) {
   if constexpr (B < 4) {
     if ((uint32_t)(4 * B) < prevK) {
-      double rm[4];
+      double rm[4], tm[4] = {0.0, 0.0, 0.0, 0.0};
       if constexpr (B == 0) {   // block 0 was loaded at the end of the previous layer
 #pragma unroll
-        for (int x = 0; x < 4; ++x) rm[x] = rm0[x];
+        for (int x = 0; x < 4; ++x) { rm[x] = rm0[x]; tm[x] = tm0[x]; }
       } else {
 #pragma unroll
         for (int x = 0; x < 4; ++x) rm[x] = dp[(4 * B + x) * KB];   // past prevK: never selected
+        if constexpr (TURN) {
+#pragma unroll
+          for (int x = 0; x < 4; ++x) tm[x] = tp[(4 * B + x) * KB];
+        }
 #pragma unroll
         for (int x = 0; x < 4; ++x) __asm__ volatile("" : "+v"(rm[x]));   // keep the loads together
       }
-      vit_src<4 * B + 0>(best, arg, cj, rm[0], gcl, inv_beta);
-      vit_src<4 * B + 1>(best, arg, cj, rm[1], gcl, inv_beta);
-      vit_src<4 * B + 2>(best, arg, cj, rm[2], gcl, inv_beta);
-      vit_src<4 * B + 3>(best, arg, cj, rm[3], gcl, inv_beta);
-      vit_min<B + 1>(best, arg, cj, dp, KB, prevK, gcl, inv_beta, rm0);
+      vit_src<4 * B + 0, TURN>(best, arg, cj, rm[0], tm[0], gcl, inv_beta);
+      vit_src<4 * B + 1, TURN>(best, arg, cj, rm[1], tm[1], gcl, inv_beta);
+      vit_src<4 * B + 2, TURN>(best, arg, cj, rm[2], tm[2], gcl, inv_beta);
+      vit_src<4 * B + 3, TURN>(best, arg, cj, rm[3], tm[3], gcl, inv_beta);
+      vit_min<B + 1, TURN>(best, arg, cj, dp, tp, KB, prevK, gcl, inv_beta, rm0, tm0);
     }
   }
 }
@@ -2261,17 +2434,23 @@ __device__ __forceinline__ VitLayerDesc vit_describe(const DevBatch& b, uint32_t
   return d;
 }
 
+// TURN: the batch has turn costs (rule 3b); each group also stages its chunk's turn costs in
+// metres (route_turn x factor / 65536), in an array padded so the unclamped prefetch stays inside
+template <bool TURN>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_WPE))) k_viterbi(DevBatch b) {
   __shared__ VitGroup smem[4];
+  __shared__ double s_turn[TURN ? 4 : 1][TURN ? kVitRoutes + 64 : 1];
   const int lane = threadIdx.x;
   const int j = lane & 15, gb = lane & 48;
   VitGroup& gs = smem[lane >> 4];
+  double* const turn_m = &s_turn[TURN ? (lane >> 4) : 0][0];
   const uint32_t k = blockIdx.x * 4 + (lane >> 4);
   const bool active = k < b.T;
   const uint32_t o = active ? b.trace_off[k] : 0u, S = active ? b.n_states[k] : 0u;
   const MatchOptions op = b.opts[active ? b.trace_opt[k] : 0u];
   const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
   const double inv_beta = 1.0 / (double)op.beta;
+  const double tscale = (double)op.turn_penalty_factor * 0x1p-16;   // metres per unit of turn weight
   const double brk = (double)op.breakage_distance;
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   bool prev_ok = false;
@@ -2302,11 +2481,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     const uint32_t nroutes = C ? (uint32_t)__shfl(incl, (int)C - 1, 16) : 0u;
     const uint32_t rbase = (uint32_t)__shfl(dq.off, 0, 16);                   // routes of layer s0 start here
     // ---- coalesced loads of the chunk's routes and emission rows
-    uint32_t rv[kVitRoutes / 16];
+    uint32_t rv[kVitRoutes / 16], tv[TURN ? kVitRoutes / 16 : 1];
     const uint32_t rlast = nroutes ? nroutes - 1u : 0u;
 #pragma unroll
     for (int x = 0; x < kVitRoutes / 16; ++x)
       if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
+    if constexpr (TURN) {
+#pragma unroll
+      for (int x = 0; x < kVitRoutes / 16; ++x)
+        if (16u * x < nroutes) tv[x] = b.route_turn[rbase + min((uint32_t)j + 16u * x, rlast)];
+    }
     // emission rows (16 floats per layer), four float4 per lane, clamped to the chunk
     const uint64_t f0 = C ? (uint64_t)(o + s0) * (kMaxCand / 4) : 0u;
     const uint64_t flast = f0 + (C ? (uint64_t)C * (kMaxCand / 4) - 1 : 0u);
@@ -2321,6 +2505,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
 #pragma unroll
     for (int x = 0; x < kVitRoutes / 16; ++x)
       if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
+    if constexpr (TURN) {
+#pragma unroll
+      for (int x = 0; x < kVitRoutes / 16; ++x)
+        if ((uint32_t)j + 16u * x < nroutes) turn_m[j + 16 * x] = (double)tv[x] * tscale;
+    }
     {
       float4* sqdst = reinterpret_cast<float4*>(&gs.sq[0][0]);
       const uint32_t nf = C * (kMaxCand / 4);
@@ -2342,11 +2531,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     uint32_t KBn = gs.kb[0], reln = gs.rel[0];
     double gcn = gs.gc[0];
     float sqn = gs.sq[0][j];
-    double rmn[4];
+    double rmn[4], tmn[4] = {0.0, 0.0, 0.0, 0.0};
     {
-      const double* dp = gs.route_m + reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
+      const uint32_t o0 = reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
+      const double* dp = gs.route_m + o0;
 #pragma unroll
       for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
+      if constexpr (TURN) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) tmn[x] = turn_m[o0 + x * KBn];
+      }
     }
     // ---- the layers of the chunk, in order, out of LDS.  The body is branch-free for the common
     // layer: the recurrence over the first four sources runs for every group (a group that starts
@@ -2358,9 +2552,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       const uint32_t KB = KBn, rel = reln;
       const double gcl = gcn;
       const float sqv = sqn;
-      double rm0[4];
+      double rm0[4], tm0[4];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) rm0[x] = rmn[x];
+      for (int x = 0; x < 4; ++x) { rm0[x] = rmn[x]; tm0[x] = tmn[x]; }
       {   // next layer's parameters, unconditionally (past the chunk: stale entries, never used)
         const uint32_t tn = min(t + 1u, (uint32_t)kVitChunk - 1u);
         KBn = gs.kb[tn]; reln = gs.rel[tn]; gcn = gs.gc[tn]; sqn = gs.sq[tn][j];
@@ -2372,14 +2566,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       int arg = -1;
       {
         const uint32_t jj = min((uint32_t)j, KB ? KB - 1u : 0u);
-        const double* dp = gs.route_m + min(rel, (uint32_t)kVitRoutes - 1u) + jj;
-        vit_src<0>(best, arg, cj, rm0[0], gcl, inv_beta);
-        vit_src<1>(best, arg, cj, rm0[1], gcl, inv_beta);
-        vit_src<2>(best, arg, cj, rm0[2], gcl, inv_beta);
-        vit_src<3>(best, arg, cj, rm0[3], gcl, inv_beta);
+        const uint32_t o1 = min(rel, (uint32_t)kVitRoutes - 1u) + jj;
+        const double* dp = gs.route_m + o1;
+        const double* tp = turn_m + (TURN ? o1 : 0u);
+        vit_src<0, TURN>(best, arg, cj, rm0[0], tm0[0], gcl, inv_beta);
+        vit_src<1, TURN>(best, arg, cj, rm0[1], tm0[1], gcl, inv_beta);
+        vit_src<2, TURN>(best, arg, cj, rm0[2], tm0[2], gcl, inv_beta);
+        vit_src<3, TURN>(best, arg, cj, rm0[3], tm0[3], gcl, inv_beta);
         if (__ballot(in && prevK > 4u) != 0ull) {   // wave-uniform: sources 4.. of some group
           const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
-          vit_min<1>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
+          vit_min<1, TURN>(best, arg, cj, dp, tp, kbs, prevK, gcl, inv_beta, rm0, tm0);
         }
       }
       const bool valid_j = j < (int)KB;
@@ -2411,6 +2607,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         const uint32_t kbs = min(KBn, (uint32_t)kMaxCand);
 #pragma unroll
         for (int x = 0; x < 4; ++x) rmn[x] = dp[x * kbs];
+        if constexpr (TURN) {   // the padded turn array: reln + j + 3 x 16 < kVitRoutes + 64
+#pragma unroll
+          for (int x = 0; x < 4; ++x) tmn[x] = turn_m[reln + j + x * kbs];
+        }
       }
       // em is +inf past K_B (and for every lane of an empty layer, which also has `start`), and
       // best is +inf where no source reached the lane, so best + em needs no further selects
@@ -2545,6 +2745,14 @@ __device__ __forceinline__ void v3_stage_routes(Vit3Smem& sm, const V3Chunk& c, 
     if ((uint32_t)(lane + kWave * x) < c.nroutes) sm.route_m[lane + kWave * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
 }
 
+// turn costs in metres of the chunk's routes (rule 3b), loaded when the chunk is staged (the
+// small-batch kernel with turn costs; [kV3Routes] is the idle lanes' 0)
+__device__ __forceinline__ void v3_stage_turns(double* turn_m, const DevBatch& b, const V3Chunk& c, int lane, double tscale) {
+#pragma unroll
+  for (int x = 0; x < kV3Regs; ++x)
+    if ((uint32_t)(lane + kWave * x) < c.nroutes) turn_m[lane + kWave * x] = (double)b.route_turn[c.rbase + lane + kWave * x] * tscale;
+}
+
 // back-pointer rows / chain flags of chunk layers [0, n) to HBM
 __device__ __forceinline__ void v3_flush(const DevBatch& b, const Vit3Smem& sm, uint64_t l0, uint32_t n, int lane) {
   if ((uint32_t)lane < n) {
@@ -2594,18 +2802,21 @@ __device__ void v3_backtrace(const DevBatch& b, Vit3Smem& sm, uint32_t o, uint32
 
 // one pass of layer t over targets [j0, j0 + 64/W): lane = (target j0 + lane/W, source lane%W);
 // heads (source lane 0) write the target's new cost and back-pointer byte
-template <int W>
-__device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, int lane, uint32_t j0, uint32_t KB, uint32_t KA,
-                                                      uint32_t rel, double gcl, double inv_beta, double inv2s2, int cb,
-                                                      uint32_t t) {
+template <int W, bool TURN>
+__device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, const double* turn_m, int lane, uint32_t j0, uint32_t KB,
+                                                      uint32_t KA, uint32_t rel, double gcl, double inv_beta, double inv2s2,
+                                                      int cb, uint32_t t) {
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   const uint32_t i = (uint32_t)lane & (W - 1), j = j0 + ((uint32_t)lane / W);
   const bool valid = i < KA && j < KB;
-  const double rm = sm.route_m[valid ? rel + i * KB + j : (uint32_t)kV3Routes];
+  const uint32_t at = valid ? rel + i * KB + j : (uint32_t)kV3Routes;
+  const double rm = sm.route_m[at];
   const double ci = sm.cost[cb][i];
   // fma(|route_m - gc|, 1/beta, cost of source i): one rounding, as the oracle; an invalid
-  // route, an unreachable source and an idle lane are +inf
-  const double c = __builtin_fma(fabs(rm - gcl), inv_beta, ci);
+  // route, an unreachable source and an idle lane are +inf.  Turn costs (rule 3b) are added to
+  // |route_m - gc| first.
+  const double d = TURN ? turn_m[at] + fabs(rm - gcl) : fabs(rm - gcl);
+  const double c = __builtin_fma(d, inv_beta, ci);
   const double m = group_min<W>(c);
   const unsigned long long eq = __ballot(c == m && m < INF);
   const uint32_t g = (uint32_t)(eq >> ((uint32_t)lane & ~(uint32_t)(W - 1))) & ((1u << W) - 1u);
@@ -2619,14 +2830,18 @@ __device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, int lane, ui
   return __ballot(head && arg >= 0);
 }
 
+template <bool TURN>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3_WPE))) k_viterbi_w(DevBatch b) {
   __shared__ Vit3Smem sm;
+  __shared__ double s_turn[TURN ? kV3Routes + 2 : 1];   // turn costs (metres) of the staged routes
   const int lane = threadIdx.x;
   const uint32_t k = blockIdx.x;
   const uint32_t o = b.trace_off[k], S = b.n_states[k];
   const MatchOptions op = b.opts[b.trace_opt[k]];
   const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
   const double inv_beta = 1.0 / (double)op.beta;
+  const double tscale = (double)op.turn_penalty_factor * 0x1p-16;
+  if (TURN && lane == 0) s_turn[kV3Routes] = 0.0;
   const double brk = (double)op.breakage_distance;
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   if (lane < 2 * kMaxCand) (&sm.cost[0][0])[lane] = INF;
@@ -2644,6 +2859,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
   int cb = 0;
   for (;;) {
     v3_stage_routes(sm, cur, lane, rv);
+    if constexpr (TURN) v3_stage_turns(s_turn, b, cur, lane, tscale);
     if ((uint32_t)lane < cur.C * (kMaxCand / 4)) reinterpret_cast<float4*>(&sm.sq[0][0])[lane] = sv;
     // the next chunk's routes and emission rows load while this chunk runs
     const uint32_t s1 = cur.s0 + cur.C;
@@ -2667,13 +2883,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
       if (KB && !start) {
         unsigned long long any = 0ull;
         if (prevK <= 4u) {
-          any = v3_pass<4>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          any = v3_pass<4, TURN>(sm, s_turn, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
         } else if (prevK <= 8u) {
-          any = v3_pass<8>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
-          if (KB > 8u) any |= v3_pass<8>(sm, lane, 8u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          any = v3_pass<8, TURN>(sm, s_turn, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          if (KB > 8u) any |= v3_pass<8, TURN>(sm, s_turn, lane, 8u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
         } else {
           for (uint32_t j0 = 0; j0 < KB; j0 += 4u)
-            any |= v3_pass<16>(sm, lane, j0, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+            any |= v3_pass<16, TURN>(sm, s_turn, lane, j0, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
         }
         if (any == 0ull) start = true;   // no valid transition into this layer
       }
@@ -2736,11 +2952,14 @@ void launch_viterbi(uint32_t T, hipStream_t st, const DevBatch& v) {
     const char* e = std::getenv("RM_VIT_WAVE_MAX");
     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)RM_VIT_WAVE_MAX;
   }();
+  const bool turn = v.route_turn != nullptr;   // the batch has turn costs (rule 3b)
   if (T <= wave_max) {
-    hipLaunchKernelGGL(k_viterbi_w, dim3(T), dim3(64), 0, st, v);
+    if (turn) hipLaunchKernelGGL(k_viterbi_w<true>, dim3(T), dim3(64), 0, st, v);
+    else hipLaunchKernelGGL(k_viterbi_w<false>, dim3(T), dim3(64), 0, st, v);
     return;
   }
-  hipLaunchKernelGGL(k_viterbi, dim3((T + 3) / 4), dim3(64), 0, st, v);
+  if (turn) hipLaunchKernelGGL(k_viterbi<true>, dim3((T + 3) / 4), dim3(64), 0, st, v);
+  else hipLaunchKernelGGL(k_viterbi<false>, dim3((T + 3) / 4), dim3(64), 0, st, v);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3521,6 +3740,78 @@ __global__ void k_ball_lookup(DevGraph g, int mode, uint64_t n, const uint32_t* 
   if (preds) { preds[2 * i] = (uint8_t)p0; preds[2 * i + 1] = (uint8_t)p1; }
 }
 
+// Turn row word of endpoint `side` of row e (road r) in the table of node x (rm_common.hpp
+// kTurnTMask): the canonical route x -> v walked back from v through the table's own rows -- the
+// predecessor stored in the row, or when that index was not stored a scan of v's in-edges for the
+// first usable tight one (as ball_pred_step) -- summing the turn at every node but x; at x the
+// heading the route leaves x with.  kTurnNone when v is outside the ball or the sum does not fit.
+__device__ uint32_t ball_turn_word(const DevGraph& g, int mode, uint32_t x, const uint2& h, const uint4* ent, uint32_t rm,
+                                   uint4 e, uint32_t side) {
+  unsigned long long kv = side ? row_key1(e) : row_key0(e);
+  if (e.x == kNone || kv == kKeyInf) return kTurnNone;
+  const uint32_t acc = mode_access(mode);
+  const uint32_t r = e.x & rm;
+  uint32_t hs = head_start(g.road_head[r], side);   // the entry edge onto r leaves v with this heading
+  uint32_t v = side ? g.road_node1[r] : g.road_node0[r];
+  uint32_t T = 0;
+  for (uint32_t guard = 0; guard <= kBallMaxKeysHost + 1u; ++guard) {
+    if (v == x) return T | hs << kTurnHeadShift;
+    const uint32_t q0 = g.in_off[v];
+    const uint32_t idx = ball_pred(e.x, side, rm);
+    uint4 rec = make_uint4(kNone, 0u, 0u, 0u);
+    if (idx < kBallPredNone) {
+      rec = g.in_rec[q0 + idx];
+    } else {
+      for (uint32_t q = q0, q1 = g.in_off[v + 1]; q < q1; ++q) {
+        const uint4 rr = g.in_rec[q];
+        const uint32_t inf = g.in_info[q];
+        if (!edge_ok(inf, acc)) continue;
+        const uint32_t r2 = rr.z >> 1;
+        const uint4 eu = ball_resolve(ent, h, r2, ent[ball_row0(h.x) + ball_slot(r2, h.y)], rm);
+        const unsigned long long ku = (rr.z & 1u) ? row_key1(eu) : row_key0(eu);
+        if (ku != kKeyInf && ku + make_key(rr.w, time_ms_dev(rr.w, mode_speed_dkph(mode, inf & 0xffffu))) == kv) {
+          rec = rr;
+          break;
+        }
+      }
+      if (rec.x == kNone) return kTurnNone;
+    }
+    const uint32_t r2 = rec.z >> 1, rev = rec.z & 1u;
+    const uint32_t hw = g.road_head[r2];
+    T += g.turn_w[turn_degree(head_back(hw, rev), hs)];
+    if (T >= kTurnNone) return kTurnNone;
+    hs = head_start(hw, rev);
+    v = rec.y;
+    if (v == x) return T | hs << kTurnHeadShift;
+    side = rev;   // the edge's source: node0 of its road when it runs forward
+    e = ball_resolve(ent, h, r2, ent[ball_row0(h.x) + ball_slot(r2, h.y)], rm);
+    kv = side ? row_key1(e) : row_key0(e);
+    if (e.x == kNone || kv == kKeyInf) return kTurnNone;
+  }
+  return kTurnNone;
+}
+
+// turn rows of one mode's tables: one wave per node, lanes over its table's slots
+__global__ void __launch_bounds__(64) k_ball_turns(DevGraph g, int mode, uint2* out) {
+  const uint2* hp = g.ball_hdr[mode];
+  const uint4* ent = g.ball_ent[mode];
+  const uint32_t rm = g.ball_road_mask;
+  for (uint32_t x = blockIdx.x; x < g.n_nodes; x += gridDim.x) {
+    const uint2 h = hp[x];
+    if (h.y == 0u) continue;
+    const uint64_t r0 = ball_row0(h.x);
+    for (uint32_t s = threadIdx.x; s < (1u << h.y); s += 64u) {
+      const uint4 e = ent[r0 + s];
+      uint2 w = make_uint2(kTurnNone, kTurnNone);
+      if (e.x != kNone) {
+        w.x = ball_turn_word(g, mode, x, h, ent, rm, e, 0u);
+        w.y = ball_turn_word(g, mode, x, h, ent, rm, e, 1u);
+      }
+      out[r0 + s] = w;
+    }
+  }
+}
+
 __global__ void k_fill_edge_src(const uint32_t* node_off, uint32_t n_nodes, uint32_t* edge_src) {
   const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= n_nodes) return;
@@ -3678,6 +3969,28 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   dg_.road_fwd = upload(allocs_, g.road_fwd);
   dg_.road_rev = upload(allocs_, g.road_rev);
   dg_.road_len = upload(allocs_, g.road_len_cm);
+  {
+    // turn costs (rule 3b): each road's headings at node0 and node1 into it, toward the first
+    // shape vertex off the node, and the turn weights round(65536 exp(-d/45))
+    std::vector<uint32_t> hw(g.num_roads());
+    const auto same = [&](uint32_t i, uint32_t j) {   // bitwise, as the oracle compares them
+      return std::memcmp(&g.verts[i].lon, &g.verts[j].lon, 4) == 0 && std::memcmp(&g.verts[i].lat, &g.verts[j].lat, 4) == 0;
+    };
+    for (uint32_t r = 0; r < g.num_roads(); ++r) {
+      const uint32_t a = g.road_vert_off[r], b = g.road_vert_off[r + 1] - 1;
+      uint32_t k = a + 1;
+      while (k < b && same(k, a)) ++k;
+      const uint32_t h0 = heading_deg(g.verts[a].lon, g.verts[a].lat, g.verts[k].lon, g.verts[k].lat);
+      k = b - 1;
+      while (k > a && same(k, b)) --k;
+      const uint32_t h1 = heading_deg(g.verts[b].lon, g.verts[b].lat, g.verts[k].lon, g.verts[k].lat);
+      hw[r] = h0 | h1 << 16;
+    }
+    dg_.road_head = upload(allocs_, hw);
+    std::vector<uint32_t> tw(kTurnDegrees);
+    for (int d = 0; d < kTurnDegrees; ++d) tw[d] = (uint32_t)std::lround(65536.0 * std::exp(-(double)d / 45.0));
+    dg_.turn_w = upload(allocs_, tw);
+  }
   dg_.verts = (const uint4*)upload(allocs_, g.verts);
   dg_.seg_id = (const unsigned long long*)upload(allocs_, g.seg_id);
   dg_.seg_len = upload(allocs_, g.seg_len_cm);
@@ -3871,6 +4184,51 @@ void Engine::ensure_balls(uint32_t mode_mask) {
   RM_HIP(hipDeviceSynchronize());
 }
 
+// Turn rows (rule 3b, k_ball_turns) of every mode in mode_mask whose tables are built: 8 bytes per
+// table slot, parallel to ball_ent, built on the GPU the first time a batch with turn costs needs
+// them.  A mode they do not fit (free HBM less a reserve) keeps none: its transitions with turn
+// costs run in the search tiers.  auto and bus share them as they share the tables.
+void Engine::ensure_turn_rows(uint32_t mode_mask) {
+  std::lock_guard<std::mutex> lk(ball_mu_);
+  const uint32_t todo = mode_mask & dg_.ball_mask & ~turn_tried_ & 0x1fu;
+  if (!todo) return;
+  RM_HIP(hipSetDevice(device_));
+  constexpr uint64_t kReserve = 4ull << 30;
+  for (int mode = 0; mode <= kModePedestrian; ++mode) {
+    if (!((todo >> mode) & 1u)) continue;
+    const uint32_t bit = 1u << mode;
+    turn_tried_ |= bit;
+    const int tw = ball_twin_mode(mode);
+    if (tw >= 0 && ((dg_.ball_turn_mask >> tw) & 1u) && dg_.ball_ent[tw] == dg_.ball_ent[mode]) {
+      dg_.ball_turn[mode] = dg_.ball_turn[tw];
+      dg_.ball_turn_mask |= bit;
+      continue;
+    }
+    const uint64_t slots = (uint64_t)ball_info_[mode][1];
+    size_t hbm_free = 0, hbm_total = 0;
+    RM_HIP(hipMemGetInfo(&hbm_free, &hbm_total));
+    if (slots == 0 || slots * sizeof(uint2) + kReserve > hbm_free) continue;
+    uint2* rows = nullptr;
+    try {
+      std::vector<void*> tmp;
+      rows = dalloc<uint2>(tmp, slots);
+    } catch (const OutOfDeviceMemory&) {
+      continue;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    DevGraph g = dg_;
+    hipLaunchKernelGGL(k_ball_turns, dim3(std::min<uint32_t>(std::max(1u, host_.num_nodes()), 65536u)), dim3(64), 0, 0, g,
+                       mode, rows);
+    RM_HIP(hipGetLastError());
+    RM_HIP(hipDeviceSynchronize());
+    allocs_.push_back(rows);
+    dg_.ball_turn[mode] = rows;
+    dg_.ball_turn_mask |= bit;
+    ball_bytes_ += slots * sizeof(uint2);
+    turn_ms_[mode] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+}
+
 // GPU route-ball build of one mode at radius_cm (k_ball_build); false (nothing changed) when
 // some ball outgrew the kernel's LDS hashes, and the caller builds on the host.  Throws
 // BallsTooLarge, allocating nothing, when the tables need more than avail_bytes (or rows
@@ -3964,8 +4322,9 @@ Workspace::~Workspace() { release(); }
 void Workspace::release() {
   for (void* p : allocs) (void)hipFree(p);
   allocs.clear();
-  cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = cap_src = cap_sort = 0;
+  cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = cap_src = cap_sort = cap_turn = 0;
   perm = loc_cursor = pcnt = nullptr;
+  route_turn = nullptr;
   loc_key = nullptr;
 }
 
@@ -4020,11 +4379,30 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
     // grow by half again at least: a coalescing service sees batch sizes creep upwards, and each
     // regrowth frees and reallocates the whole workspace (hipFree synchronises the device) --
     // growing to each new maximum exactly cost a ~70 ms stall per new maximum (svc_client_probe)
-    const uint64_t cp = std::max<uint64_t>(points, w.cap_points + w.cap_points / 2) + 64;
-    const uint64_t ct = std::max<uint64_t>(traces, w.cap_traces + w.cap_traces / 2) + 16;
-    const uint64_t co = std::max<uint64_t>(nopts, w.cap_opts + w.cap_opts / 2) + 4;
     const uint64_t keep_trans = w.cap_trans, keep_path = w.cap_path, keep_segs = w.cap_segs, keep_src = w.cap_src;
+    // the grown capacities first; when they do not fit in HBM but the batch's own sizes might, the
+    // exact sizes (a batch that fits must not fail because the previous one was large)
+    const uint64_t gp = std::max<uint64_t>(points, w.cap_points + w.cap_points / 2) + 64;
+    const uint64_t gt = std::max<uint64_t>(traces, w.cap_traces + w.cap_traces / 2) + 16;
+    const uint64_t go = std::max<uint64_t>(nopts, w.cap_opts + w.cap_opts / 2) + 4;
+    try {
+      alloc_points(gp, gt, go, keep_trans, keep_path, keep_segs, keep_src);
+    } catch (const OutOfDeviceMemory&) {
+      if (gp == points + 64 && gt == traces + 16 && go == nopts + 4) throw;
+      alloc_points(points + 64, traces + 16, nopts + 4, 1, 1, 1, 1);
+    }
+  });
+}
+
+void Matcher::alloc_points(uint64_t cp, uint64_t ct, uint64_t co, uint64_t keep_trans, uint64_t keep_path,
+                           uint64_t keep_segs, uint64_t keep_src) {
+  {
+    Workspace& w = ws_;
     w.release();
+    // test hook: a workspace of more than RM_TEST_WS_POINTS_LIMIT points fails as out of memory
+    // (tests/test_gpu_isolation.py: the grown size fails, the batch's own size must not)
+    if (const char* lim = std::getenv("RM_TEST_WS_POINTS_LIMIT"); lim && *lim && cp > std::strtoull(lim, nullptr, 10))
+      throw OutOfDeviceMemory("workspace above RM_TEST_WS_POINTS_LIMIT");
     std::vector<void*>& L = w.allocs;
     w.trace_off = dalloc<uint32_t>(L, ct + 1);
     w.lon = dalloc<float>(L, cp); w.lat = dalloc<float>(L, cp); w.time = dalloc<double>(L, cp);
@@ -4051,12 +4429,12 @@ void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
     w.tot_part = dalloc<unsigned long long>(L, 2 * ((cp + 255) / 256) + 2);
     w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
     w.gsearch = nullptr;
-    w.route = nullptr; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
+    w.route = nullptr; w.route_turn = nullptr; w.cap_turn = 0; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
     w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
-    ensure_trans(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
-    ensure_path(std::max<uint64_t>(keep_path, cp / 8 + 1024));
-    ensure_segs(std::max<uint64_t>(keep_segs, cp / 2 + 1024));
-  });
+    ensure_trans_raw(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
+    ensure_path_raw(std::max<uint64_t>(keep_path, cp / 8 + 1024));
+    ensure_segs_raw(std::max<uint64_t>(keep_segs, cp / 2 + 1024));
+  }
 }
 
 static void free_one(Workspace& w, void* q) {
@@ -4065,13 +4443,34 @@ static void free_one(Workspace& w, void* q) {
   w.allocs.erase(std::find(w.allocs.begin(), w.allocs.end(), q));
 }
 
-void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
+void Matcher::ensure_trans(uint64_t n, uint64_t n_src) { grow_workspace([&] { ensure_trans_raw(n, n_src); }); }
+void Matcher::ensure_path(uint64_t n) { grow_workspace([&] { ensure_path_raw(n); }); }
+void Matcher::ensure_segs(uint64_t n) { grow_workspace([&] { ensure_segs_raw(n); }); }
+
+// route_turn (turn weights of the transitions, K2 -> K3) for batches with turn costs: sized with
+// route, allocated the first time a batch needs it
+void Matcher::ensure_turns() {
   grow_workspace([&] {
+    Workspace& w = ws_;
+    if (w.route_turn && w.cap_turn >= w.cap_trans) return;
+    free_one(w, w.route_turn);
+    w.route_turn = nullptr;
+    w.cap_turn = 0;
+    w.route_turn = dalloc<uint32_t>(w.allocs, w.cap_trans);
+    w.cap_turn = w.cap_trans;
+  });
+}
+
+void Matcher::ensure_trans_raw(uint64_t n, uint64_t n_src) {
+  {
     Workspace& w = ws_;
     if (!(n <= w.cap_trans && w.route)) {
       free_one(w, w.route);
+      free_one(w, w.route_turn);
       w.route = nullptr;
+      w.route_turn = nullptr;
       w.cap_trans = 0;
+      w.cap_turn = 0;
       const uint64_t c = n + n / 4 + 1024;
       w.route = dalloc<uint32_t>(w.allocs, c);
       w.cap_trans = c;
@@ -4090,11 +4489,11 @@ void Matcher::ensure_trans(uint64_t n, uint64_t n_src) {
       w.rl_routes_c = dalloc<uint32_t>(w.allocs, c);
       w.cap_src = c;
     }
-  });
+  }
 }
 
-void Matcher::ensure_path(uint64_t n) {
-  grow_workspace([&] {
+void Matcher::ensure_path_raw(uint64_t n) {
+  {
     Workspace& w = ws_;
     if (n <= w.cap_path && w.path_pool) return;
     free_one(w, w.path_pool);
@@ -4103,11 +4502,11 @@ void Matcher::ensure_path(uint64_t n) {
     const uint64_t c = n + n / 4 + 1024;
     w.path_pool = dalloc<uint32_t>(w.allocs, c);
     w.cap_path = c;
-  });
+  }
 }
 
-void Matcher::ensure_segs(uint64_t n) {
-  grow_workspace([&] {
+void Matcher::ensure_segs_raw(uint64_t n) {
+  {
     Workspace& w = ws_;
     if (n <= w.cap_segs && w.segs) return;
     for (void** q : {(void**)&w.segs, (void**)&w.reps, (void**)&w.rec_slot}) {
@@ -4120,7 +4519,7 @@ void Matcher::ensure_segs(uint64_t n) {
     w.reps = dalloc<ReportRec>(w.allocs, c);
     w.rec_slot = dalloc<uint32_t>(w.allocs, c);
     w.cap_segs = c;
-  });
+  }
 }
 
 void Matcher::tic(int k) {
@@ -4180,6 +4579,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig; v.state_time = w.state_time;
   v.cand_n = w.cand_n; v.cand_desc = w.cand_desc; v.cand_sq = w.cand_sq;
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
+  v.route_turn = nullptr;   // run_device sets it for a batch with turn costs
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
@@ -4207,13 +4607,15 @@ void Matcher::check_batch(uint32_t T, const uint32_t* trace_off, const MatchOpti
     if (trace_opt[k] >= n_opts) throw std::runtime_error("trace option index out of range");
   }
   mode_mask_ = 0;
+  turn_mask_ = 0;
   for (uint32_t q = 0; q < n_opts; ++q) {
     if (opts[q].mode < 0 || opts[q].mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
     // K3 divides by both (a zero 1/beta would turn an invalid route's +inf into NaN)
     if (!(opts[q].sigma_z > 0.f) || !std::isfinite(opts[q].sigma_z)) throw std::runtime_error("sigma_z must be positive and finite");
     if (!(opts[q].beta > 0.f) || !std::isfinite(opts[q].beta)) throw std::runtime_error("beta must be positive and finite");
-    if (!(opts[q].turn_penalty_factor == 0.f)) throw std::runtime_error(kTurnPenaltyError);
+    if (!turn_factor_ok(opts[q].turn_penalty_factor)) throw std::runtime_error(kTurnPenaltyError);
     mode_mask_ |= 1u << opts[q].mode;
+    if (opts[q].turn_penalty_factor > 0.f) turn_mask_ |= 1u << opts[q].mode;
   }
 }
 
@@ -4455,6 +4857,7 @@ void Matcher::run_device(const RunParams& rp) {
   Workspace& w = ws_;
   hipStream_t st = stream_;
   eng_->ensure_balls(mode_mask_);
+  if (turn_mask_) eng_->ensure_turn_rows(turn_mask_);
   const DevGraph g = eng_->dev_snapshot();
   if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 32 * sizeof(uint32_t), hipHostMallocDefault));
   unsigned long long* htot = reinterpret_cast<unsigned long long*>(hctl_ + 16);
@@ -4510,6 +4913,10 @@ void Matcher::run_device(const RunParams& rp) {
   n_trans_ = total;
   ensure_trans(total, n_src);
   v.route = w.route;
+  if (turn_mask_) {   // turn weights of the transitions (rule 3b), read by K3
+    ensure_turns();
+    v.route_turn = w.route_turn;
+  }
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a;
   v.rl_routes_b = w.rl_routes_b;
@@ -4522,12 +4929,23 @@ void Matcher::run_device(const RunParams& rp) {
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
   if (n_src && balls) {
-    hipLaunchKernelGGL(k_routes_ball2, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st, g, v,
-                       (uint32_t)n_src);
-    hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)), dim3(256), 0,
-                       st, g, v, 0u, 1);
+    if (v.route_turn)
+      hipLaunchKernelGGL(k_routes_ball2<true>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
+                         g, v, (uint32_t)n_src);
+    else
+      hipLaunchKernelGGL(k_routes_ball2<false>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
+                         g, v, (uint32_t)n_src);
+    if (v.route_turn)
+      hipLaunchKernelGGL(k_routes_lane<true>, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)), dim3(256),
+                         0, st, g, v, 0u, 1);
+    else
+      hipLaunchKernelGGL(k_routes_lane<false>, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)),
+                         dim3(256), 0, st, g, v, 0u, 1);
   } else if (n_src) {
-    hipLaunchKernelGGL(k_routes_lane, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
+    if (v.route_turn)
+      hipLaunchKernelGGL(k_routes_lane<true>, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
+    else
+      hipLaunchKernelGGL(k_routes_lane<false>, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
   }
   // the search tiers' grids (grid-stride over lists the host does not read) shrink with the batch:
   // a coalesced service batch of ~15 k points launches them mostly empty
@@ -4706,6 +5124,12 @@ void Matcher::get_routes(uint32_t* trans_off, double* gc, uint32_t* route) {
   RM_HIP(hipMemcpy(trans_off, ws_.trans_off, n_points_ * 4, hipMemcpyDeviceToHost));
   RM_HIP(hipMemcpy(gc, ws_.gc, n_points_ * 8, hipMemcpyDeviceToHost));
   if (n_trans_) RM_HIP(hipMemcpy(route, ws_.route, n_trans_ * 4, hipMemcpyDeviceToHost));
+}
+void Matcher::get_route_turns(uint32_t* out) {
+  sync();
+  if (!n_trans_) return;
+  if (turn_mask_ && ws_.route_turn) RM_HIP(hipMemcpy(out, ws_.route_turn, n_trans_ * 4, hipMemcpyDeviceToHost));
+  else std::memset(out, 0, n_trans_ * 4);
 }
 void Matcher::get_viterbi(int8_t* choice, uint8_t* chain_start) {
   sync();

@@ -69,6 +69,15 @@ struct DevGraph {  // POD view of the graph in HBM, passed by value to kernels
   uint32_t ball_radius[5];
   uint32_t ball_mask;            // modes whose balls are built
   uint32_t ball_road_mask;       // road-id bits of a row's first word (rm_common.hpp ball_road_mask)
+  // turn costs (rule 3b): per road its two headings (rm_common.hpp head_start / head_back), the
+  // turn weight of each turn degree 0..180, and per mode the turn rows parallel to ball_ent
+  // ({node0 word, node1 word} per slot: the turn weight of the canonical route from the table's
+  // node to the road's endpoint, entering the road there, without the turn at the table's node
+  // | the heading the route leaves that node with << 23; k_ball_turns)
+  const uint32_t* road_head;
+  const uint32_t* turn_w;
+  const uint2* ball_turn[5];
+  uint32_t ball_turn_mask;       // modes whose turn rows are built
   double lon0, lat0, dlon, dlat;
   uint32_t ncx, ncy, n_nodes, n_edges, n_segments, pad;
 };
@@ -118,6 +127,8 @@ struct Workspace {
   // (sp* = mode-capped speed of the directed edge in 0.1 km/h, 0 when the mode cannot use it)
   uint8_t* cand_n = nullptr; uint4* cand_desc = nullptr; float* cand_sq = nullptr;
   uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr;
+  uint32_t* route_turn = nullptr;   // per transition: turn weight U (rule 3b), batches with turn costs only
+  uint64_t cap_turn = 0;
   uint4* pair_info = nullptr;  // per layer pair slot: {route bound cm, time bound ms, KA | KB << 8 | mode << 16, 0}
   uint32_t* src_cnt = nullptr; uint32_t* src_off = nullptr; uint32_t* src_item = nullptr;
   int8_t* choice = nullptr; uint8_t* chain_start = nullptr; uint8_t* bp = nullptr;
@@ -266,6 +277,7 @@ class Matcher {
   void get_states(uint32_t* n_states, uint32_t* state_orig);
   void get_candidates(uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
   void get_routes(uint32_t* trans_off, double* gc, uint32_t* route);
+  void get_route_turns(uint32_t* route_turn);   // n_trans() words (0 without turn costs)
   void get_viterbi(int8_t* choice, uint8_t* chain_start);
   void get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, uint32_t* route_dist);
   // segments compacted per trace: seg_off (T+1), segs (seg_off[T])
@@ -325,6 +337,13 @@ class Matcher {
   void ensure_trans(uint64_t n, uint64_t n_src);
   void ensure_path(uint64_t n);
   void ensure_segs(uint64_t n);
+  void ensure_turns();
+  // the same, throwing OutOfDeviceMemory (ensure() retries a failed grown size at the exact one)
+  void alloc_points(uint64_t cp, uint64_t ct, uint64_t co, uint64_t keep_trans, uint64_t keep_path, uint64_t keep_segs,
+                    uint64_t keep_src);
+  void ensure_trans_raw(uint64_t n, uint64_t n_src);
+  void ensure_path_raw(uint64_t n);
+  void ensure_segs_raw(uint64_t n);
   void ensure_global_search();
   void read_ctl();
   void tic(int k);
@@ -355,6 +374,7 @@ class Matcher {
   StageBufs sb_;
   bool from_points_ = false;
   uint32_t mode_mask_ = 0;   // travel modes of the batch (bit per Mode): which route balls K2 needs
+  uint32_t turn_mask_ = 0;   // modes of the batch with a turn_penalty_factor > 0: turn rows, route_turn
   void ensure_points(uint64_t n, uint32_t n_uuids, uint32_t n_opts);
   void ensure_rows(uint64_t n, uint32_t traces);
   struct Ev { hipEvent_t a, b; int k; };
@@ -380,6 +400,10 @@ class Engine {
   uint32_t n_segments() const { return host_.num_segments(); }
   // build (once) the route balls of every mode in `mode_mask` (bit per Mode); thread-safe
   void ensure_balls(uint32_t mode_mask);
+  // build (once) the turn rows of the built tables of every mode in `mode_mask`; thread-safe
+  void ensure_turn_rows(uint32_t mode_mask);
+  uint32_t turn_row_mask() const { return dg_.ball_turn_mask; }
+  double turn_build_ms(int mode) const { return mode >= 0 && mode <= kModePedestrian ? turn_ms_[mode] : 0.0; }
   // ball radius in cm for modes built from now on (0 disables the ball tier)
   void set_ball_radius(uint32_t radius_cm);
   uint32_t ball_radius() const { return ball_radius_cm_; }
@@ -413,6 +437,8 @@ class Engine {
   bool locality_default_ = false;
   uint32_t locality_shift_ = 0, locality_bits_ = 0;
   uint64_t ball_bytes_ = 0;             // bytes of the tables built so far (all modes)
+  uint32_t turn_tried_ = 0;             // modes whose turn rows were attempted (ensure_turn_rows)
+  double turn_ms_[5] = {};
   bool build_balls_gpu(int mode, uint32_t radius_cm, uint32_t max_keys, uint64_t avail_bytes);
   double ball_info_[5][4] = {};
 };

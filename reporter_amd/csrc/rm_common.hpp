@@ -146,6 +146,60 @@ RM_HD double gc_distance(float lon_a, float lat_a, float lon_b, float lat_b) {
   return gc_trig(lon_a, lat_a, lat_sin(lat_a), lat_cos(lat_a), lon_b, lat_b, lat_sin(lat_b), lat_cos(lat_b));
 }
 
+// ---- turn costs (meili TransitionCostModel's turn term; DESIGN.md §3 rule 3b) ----
+// meili adds turn_penalty_factor * exp(-d / 45) for every turn of d degrees (0 = U-turn, 180 =
+// straight on) of a transition's route to |route - gc| before dividing by beta.  Here a turn of d
+// degrees weighs kTurnWeight(d) = round(65536 exp(-d/45)) (turn_weight_table), a route's turns sum
+// to an integer U (associative: the route tables store partial sums), and the transition's turn
+// cost is U * factor * 2^-16 metres.  Headings are Valhalla NodeInfo headings: 8-bit steps of
+// 360/255 degrees, expanded back to whole degrees.
+//
+// atan(t), 0 <= t <= 1: atan(t) = pi/4 + atan((t-1)/(t+1)) above tan(pi/8), then the odd Taylor
+// series to z^45, Horner in z^2 with coefficients (-1)^n/(2n+1) computed by one IEEE division each
+RM_HD double det_atan_unit(double t) {
+  double off = 0.0, z = t;
+  if (t > 0.41421356237309503) { z = (t - 1.0) / (t + 1.0); off = 0.25 * kPi; }
+  const double s = z * z;
+  double p = 1.0 / 45.0;
+  for (int n = 21; n >= 0; --n) p = p * s + ((n & 1) ? -1.0 : 1.0) / (double)(2 * n + 1);
+  return off + z * p;
+}
+// compass bearing in degrees [0, 360] of (dx east, dy north), metres
+RM_HD double det_bearing_deg(double dx, double dy) {
+  const double ax = dx < 0.0 ? -dx : dx, ay = dy < 0.0 ? -dy : dy;
+  if (ax == 0.0 && ay == 0.0) return 0.0;
+  const double a = ax <= ay ? det_atan_unit(ax / ay) : 0.5 * kPi - det_atan_unit(ay / ax);
+  double th;
+  if (dx >= 0.0) th = dy >= 0.0 ? a : kPi - a;
+  else th = dy < 0.0 ? kPi + a : 2.0 * kPi - a;
+  return th * (180.0 / kPi);
+}
+// heading from a to b in whole degrees 0..360 through Valhalla's 8-bit storage
+RM_HD uint32_t heading_deg(float lon_a, float lat_a, float lon_b, float lat_b) {
+  const double dx = ((double)lon_b - (double)lon_a) * (double)(float)(kMetersPerDegLonEq * det_cos((double)lat_a * kDegToRad));
+  const double dy = ((double)lat_b - (double)lat_a) * kMetersPerDegLat;
+  const uint32_t h8 = (uint32_t)(det_bearing_deg(dx, dy) * (255.0 / 360.0) + 0.5);
+  return (h8 * 360u + 127u) / 255u;
+}
+// turn angle class between an edge arriving with back heading hb (at the node, pointing the way
+// it came) and an edge leaving with heading hs: 0 (U-turn) .. 180 (straight on)
+RM_HD uint32_t turn_degree(uint32_t hb, uint32_t hs) {
+  const uint32_t d = hb > hs ? hb - hs : hs - hb;
+  return d > 180u ? 360u - d : d;
+}
+constexpr int kTurnDegrees = 181;
+constexpr uint32_t kTurnScaleLog = 16;   // turn weight units per metre at factor 1: 2^16
+// a road's headings packed in one word: H0 (at node0, into the road) | H1 (at node1) << 16.  A
+// forward edge leaves node0 with H0 and arrives at node1 with back heading H1; a reverse edge the
+// other way round.
+RM_HD uint32_t head_start(uint32_t hw, uint32_t rev) { return rev ? hw >> 16 : hw & 0xffffu; }
+RM_HD uint32_t head_back(uint32_t hw, uint32_t rev) { return rev ? hw & 0xffffu : hw >> 16; }
+// Turn row word (route tables with turn costs, k_ball_turns): for the table of node x and an
+// endpoint v of the row's road, the turn weight T of the canonical route x -> v entering the road
+// at v (every turn on it but the one at x) | the heading the route leaves x with << 23.
+// T = kTurnNone: not stored (the route's transitions go to the search tiers).
+constexpr uint32_t kTurnTMask = 0x7fffffu, kTurnNone = 0x7fffffu, kTurnHeadShift = 23;
+
 // ---- directed-edge record (16 B, one dwordx4 load in the route kernel) ----
 // info bits: [0,16) speed in 0.1 km/h, [16,19) access mask, bit 19 internal, bit 20 service
 struct EdgeRec {
@@ -297,12 +351,11 @@ struct MatchOptions {
   float interpolation_distance;     // 10 m
   float max_route_distance_factor;  // 5
   float max_route_time_factor;      // 2
-  float turn_penalty_factor;        // 0: meili's turn costs are not implemented; any other value is an error
+  float turn_penalty_factor;        // meili's turn costs (rule 3b): 0 none; stock per-mode defaults 200 / 140 / 100
 };
-// A request (or configured mode) asking for turn costs fails with this message instead of being
-// answered without them (the value used to be parsed and dropped).
-constexpr const char* kTurnPenaltyError =
-    "turn_penalty_factor must be 0: this matcher does not implement meili's turn costs";
+// meili's TransitionCostModel refuses a negative factor; infinities and NaN would poison the costs
+constexpr const char* kTurnPenaltyError = "turn_penalty_factor must be non-negative and finite";
+RM_HD bool turn_factor_ok(float f) { return f >= 0.f && f - f == 0.f; }   // f - f is NaN for +inf
 
 RM_HD MatchOptions default_options() {
   MatchOptions o;

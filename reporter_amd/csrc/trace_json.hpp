@@ -94,7 +94,7 @@ class Reader {
         if (!(o.sigma_z > 0.f) || !std::isfinite(o.sigma_z)) err = "sigma_z must be positive";
         else if (!(o.beta > 0.f) || !std::isfinite(o.beta)) err = "beta must be positive";
         else if (!(o.search_radius >= 0.f)) err = "search_radius must be non-negative";
-        else if (!(o.turn_penalty_factor == 0.f)) err = kTurnPenaltyError;
+        else if (!turn_factor_ok(o.turn_penalty_factor)) err = kTurnPenaltyError;
       }
       if (err.empty()) {
         if (trace_state_ == 0 || trace_state_ == 2) err = "trace must be an array of points";

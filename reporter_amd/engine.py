@@ -278,6 +278,13 @@ class BatchMatcher:
         _lib.check(_lib.lib().rm_runner_get_routes(self._h, off.ctypes.data, gc.ctypes.data, route.ctypes.data))
         return off, gc, route[: sz["transitions"]]
 
+    def route_turns(self):
+        """Turn weight U of every transition (DESIGN.md §3 rule 3b; zeros without turn costs)."""
+        n = self.sizes()["transitions"]
+        out = np.empty(max(n, 1), np.uint32)
+        _lib.check(_lib.lib().rm_runner_get_route_turns(self._h, out.ctypes.data))
+        return out[:n]
+
     def viterbi(self):
         P = self.sizes()["points"]
         choice = np.empty(P, np.int8)

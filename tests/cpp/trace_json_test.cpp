@@ -48,7 +48,7 @@ void dom_apply(const json::Value* o, MatchOptions& m) {
   if (!(m.sigma_z > 0.f) || !std::isfinite(m.sigma_z)) throw std::runtime_error("sigma_z must be positive");
   if (!(m.beta > 0.f) || !std::isfinite(m.beta)) throw std::runtime_error("beta must be positive");
   if (!(m.search_radius >= 0.f)) throw std::runtime_error("search_radius must be non-negative");
-  if (!(m.turn_penalty_factor == 0.f)) throw std::runtime_error(kTurnPenaltyError);
+  if (!turn_factor_ok(m.turn_penalty_factor)) throw std::runtime_error(kTurnPenaltyError);
 }
 
 Parsed dom_parse(const char* text, const MatchOptions* defaults) {
@@ -291,17 +291,18 @@ int main() {
     (a.ok ? n_ok : n_err)++;
   }
   CHECK(n_ok > 2300, "too few valid documents");
-  // turn costs are not implemented: a request asking for them fails instead of being answered
-  // without them; 0 and null are accepted
+  // turn costs (DESIGN.md rule 3b): any non-negative finite factor is accepted (0, null, meili's
+  // per-mode 200 / 140 / 100); a negative one fails as meili's TransitionCostModel does, and so
+  // does one that overflows to infinity
   {
     const char* base = "{\"uuid\":\"1\",\"trace\":[{\"lat\":1,\"lon\":2,\"time\":3}],\"match_options\":{%s}}";
     char doc[256];
     for (const char* o : {"\"turn_penalty_factor\":200", "\"turn_penalty_factor\":-1e-30", "\"turn_penalty_factor\":0",
-                          "\"turn_penalty_factor\":null"}) {
+                          "\"turn_penalty_factor\":null", "\"turn_penalty_factor\":1e39", "\"turn_penalty_factor\":140.5"}) {
       std::snprintf(doc, sizeof doc, base, o);
       const Parsed a = dom_parse(doc, defaults), b = fast_parse(doc, defaults, sink);
       CHECK(same(a, b, why), why + " in " + doc);
-      const bool want_ok = std::strstr(o, ":0") || std::strstr(o, "null");
+      const bool want_ok = !std::strstr(o, ":-") && !std::strstr(o, "e39");
       CHECK(b.ok == want_ok && (want_ok || b.err == kTurnPenaltyError), std::string(doc) + " -> " + b.err);
     }
   }

@@ -45,6 +45,7 @@ def compare_all(gpu, ref, trace_off, check_reports=True):
     np.testing.assert_array_equal(toff[tm], ref["trans_off"][tm], "trans_off")
     np.testing.assert_array_equal(gc[tm].view(np.uint64), ref["gc"][tm].view(np.uint64), "gc bits")
     np.testing.assert_array_equal(route, ref["route"], "route_cm")
+    np.testing.assert_array_equal(gpu.route_turns(), ref["route_turn"], "route_turn")
 
     choice, cs = gpu.viterbi()
     np.testing.assert_array_equal(cs[sm], ref["chain_start"][sm], "chain_start")

@@ -197,3 +197,30 @@ def test_download_buffer_failure_then_retry(built_lib, small_world, monkeypatch)
     assert s.tobytes() == s_want.tobytes() and len(s) > 50
     bm.close()
     eng.close()
+
+
+def test_workspace_exact_size_fallback(built_lib, small_world, monkeypatch):
+    """the workspace grows to 1.5x its last capacity, and when that does not fit but
+    the batch's own size does, it allocates the exact size instead of failing the batch (the
+    hook RM_TEST_WS_POINTS_LIMIT makes larger workspaces fail as out of memory)."""
+    g = graphfile.load(small_world)
+    small = world.generate_traces(small_world, n_traces=8, n_points=125, rate_s=1.0, noise_m=5.0, seed=78)
+    big = world.generate_traces(small_world, n_traces=10, n_points=125, rate_s=1.0, noise_m=5.0, seed=79)
+    eng = engine.Engine(small_world, 0)
+    bm = engine.BatchMatcher(eng)
+    bm.run(small["trace_off"], small["lon"], small["lat"], small["time"], small["accuracy"])   # 1,000 points
+    # 1,250 points: the grown size is 1,000 * 1.5 + 64 points, the exact one 1,250 + 64
+    monkeypatch.setenv("RM_TEST_WS_POINTS_LIMIT", "1400")
+    bm.run(big["trace_off"], big["lon"], big["lat"], big["time"], big["accuracy"])
+    ref = mo.match(g, mo.Batch(big["trace_off"], big["lon"], big["lat"], big["time"], big["accuracy"],
+                               engine.default_options(1), np.zeros(10, np.uint32)))
+    compare_all(bm, ref, big["trace_off"])
+    # a batch whose own size does not fit still fails as too large for the device
+    monkeypatch.setenv("RM_TEST_WS_POINTS_LIMIT", "1000")
+    with pytest.raises(RuntimeError, match="does not fit in HBM"):
+        bm.run(big["trace_off"], big["lon"], big["lat"], big["time"], big["accuracy"])
+    monkeypatch.delenv("RM_TEST_WS_POINTS_LIMIT")
+    bm.run(big["trace_off"], big["lon"], big["lat"], big["time"], big["accuracy"])
+    compare_all(bm, ref, big["trace_off"])
+    bm.close()
+    eng.close()

@@ -1,18 +1,20 @@
-"""turn_penalty_factor is refused, not dropped.
+"""meili's turn costs (DESIGN.md §3 rule 3b), CPU side.
 
-meili adds turn costs to the transition cost when turn_penalty_factor > 0.  The reference's
-client sends the field (py/generate_test_trace.py:37,47).  The stock valhalla_build_config
-(reference Dockerfile:42-49) configures it per mode.  This matcher has no turn costs (DESIGN.md
-§3).  So a request asking for them fails: reporter_service.py:244-245 answers 500 and
-simple_reporter.py:169-173 skips the window.  A configured non-zero value fails Configure unless
-reporter_amd.ignore_turn_penalty accepts zero turn costs.  It used to be parsed and ignored.
+The reference configures them: stock valhalla_build_config (reference Dockerfile:42-49) writes
+meili's per-mode turn_penalty_factor (auto 200, bicycle 140, pedestrian 100), and the client
+sends the field (py/generate_test_trace.py:37,47).  Configure accepts such a config, a negative or
+infinite factor fails (meili's TransitionCostModel refuses a negative one), and the oracle's turn
+weights are pinned here by an independent pure-Python restatement on small cases.
 """
+import heapq
 import json
+import math
 
 import numpy as np
 import pytest
 
-from reporter_amd import engine, world
+import meili_oracle as mo
+from reporter_amd import engine, graphfile, world
 
 
 def _conf(tmp_path, meili, ra=None):
@@ -23,41 +25,220 @@ def _conf(tmp_path, meili, ra=None):
     return str(p)
 
 
-def test_configure_refuses_turn_costs(built_lib, tmp_path):
-    """Checked before the graph loads (no GPU needed): the message names the mode and the fix."""
+STOCK = {"default": {"turn_penalty_factor": 0, "sigma_z": 4.07, "beta": 3}, "auto": {"turn_penalty_factor": 200},
+         "bicycle": {"turn_penalty_factor": 140}, "pedestrian": {"turn_penalty_factor": 100, "search_radius": 50}}
+
+
+def test_configure_accepts_stock_turn_costs(built_lib, tmp_path):
+    """Checked before the graph loads (no GPU needed): the stock per-mode factors get as far as
+    the (missing) graph; a negative or infinite factor fails with its own message."""
     import valhalla
-    for meili in ({"auto": {"turn_penalty_factor": 200}}, {"default": {"turn_penalty_factor": 5}},
-                  {"pedestrian": {"turn_penalty_factor": 100, "search_radius": 50}}):
-        with pytest.raises(RuntimeError, match="turn_penalty_factor"):
-            valhalla.Configure(_conf(tmp_path, meili))
-    # accepted as zero with the opt-in: Configure gets as far as the (missing) graph
+    with pytest.raises(RuntimeError, match="missing.rmg"):
+        valhalla.Configure(_conf(tmp_path, STOCK))
     with pytest.raises(RuntimeError, match="missing.rmg"):
         valhalla.Configure(_conf(tmp_path, {"auto": {"turn_penalty_factor": 200}}, {"ignore_turn_penalty": True}))
-    with pytest.raises(RuntimeError, match="missing.rmg"):
-        valhalla.Configure(_conf(tmp_path, {"auto": {"turn_penalty_factor": 0}}))
+    for bad in (-1, -1e-30, 1e39):
+        with pytest.raises(RuntimeError, match="turn_penalty_factor must be non-negative"):
+            valhalla.Configure(_conf(tmp_path, {"bicycle": {"turn_penalty_factor": bad}}))
 
 
-@pytest.mark.gpu
-def test_request_with_turn_costs_fails_alone(small_world, tmp_path):
-    """Through the drop-in: a request with turn_penalty_factor 200 raises (the service's 500),
-    the same request with 0 is answered, and coalesced neighbours are unaffected; the batch API
-    refuses it too."""
-    import valhalla
-    conf = valhalla.write_config(str(tmp_path / "tp.json"), small_world, device=0, coalesce=True)
-    valhalla.Configure(conf)
-    sm = valhalla.SegmentMatcher()
-    tr = world.generate_traces(small_world, n_traces=2, n_points=120, rate_s=1.0, noise_m=5.0, seed=5)
-    ok = json.dumps(world.trace_to_request(tr, 0, turn_penalty_factor=0), separators=(",", ":"))
-    bad = json.dumps(world.trace_to_request(tr, 1, turn_penalty_factor=200), separators=(",", ":"))
-    with pytest.raises(RuntimeError, match="turn_penalty_factor must be 0"):
-        sm.Match(bad)
-    assert json.loads(sm.Match(ok))["segments"]
-    sm.close()
-    eng = engine.Engine(small_world, 0)
-    bm = engine.BatchMatcher(eng)
-    opts = engine.default_options(1)
-    opts[0]["turn_penalty_factor"] = 140.0
-    with pytest.raises(RuntimeError, match="turn_penalty_factor must be 0"):
-        bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts, np.zeros(2, np.uint32))
-    bm.close()
-    eng.close()
+# ---- an independent restatement of rule 3b (pure Python, small cases) ----
+
+def _heading(lon_a, lat_a, lon_b, lat_b):
+    """Heading in whole degrees through Valhalla's 8-bit storage, with math.atan2 (the oracle
+    uses its own deterministic atan): equal except within a hair of a 360/255-degree step."""
+    mlon = np.float32(111320.0 * math.cos(float(lat_a) * 0.017453292519943295))
+    dx = (float(lon_b) - float(lon_a)) * float(mlon)
+    dy = (float(lat_b) - float(lat_a)) * 110567.0
+    deg = math.degrees(math.atan2(dx, dy)) % 360.0 if (dx or dy) else 0.0
+    h8 = int(deg * 255.0 / 360.0 + 0.5)
+    return (h8 * 360 + 127) // 255
+
+
+def _road_heads(g):
+    verts = g["verts"].reshape(-1, 4)
+    lon, lat = verts[:, 0].view(np.float32), verts[:, 1].view(np.float32)
+    off = g["road_vert_off"]
+    h0 = np.empty(len(off) - 1, np.int64)
+    h1 = np.empty(len(off) - 1, np.int64)
+    for r in range(len(off) - 1):
+        a, b = int(off[r]), int(off[r + 1]) - 1
+        k = a + 1
+        while k < b and lon[k] == lon[a] and lat[k] == lat[a]:
+            k += 1
+        h0[r] = _heading(lon[a], lat[a], lon[k], lat[k])
+        k = b - 1
+        while k > a and lon[k] == lon[b] and lat[k] == lat[b]:
+            k -= 1
+        h1[r] = _heading(lon[b], lat[b], lon[k], lat[k])
+    return h0, h1
+
+
+def test_road_headings_match_atan2(built_lib, small_world):
+    g = graphfile.load(small_world)
+    h0, h1 = mo.road_heads(g)
+    p0, p1 = _road_heads(g)
+    for a, b in ((h0, p0), (h1, p1)):
+        d = np.abs(a.astype(np.int64) - b)
+        d = np.minimum(d, 360 - d)
+        assert int(d.max()) <= 2, int(d.max())            # one 360/255-degree step at most
+        assert (d == 0).mean() > 0.999
+    # a grid: roads leave their nodes along the four compass directions (+-20 % jitter)
+    q = np.concatenate([h0, h1]).astype(np.int64)
+    near = np.minimum.reduce([np.minimum(np.abs(q - c), 360 - np.abs(q - c)) for c in (0, 90, 180, 270)])
+    assert np.median(near) < 15
+
+
+def _tu(d):
+    return int(round(65536.0 * math.exp(-d / 45.0)))
+
+
+def _turn(hb, hs):
+    d = abs(int(hb) - int(hs))
+    return _tu(360 - d if d > 180 else d)
+
+
+def _py_route_turns(g, heads, ra, sa, rb, sb, mode_acc, speed_cap, bound):
+    """Rule 3b by brute force: bounded Dijkstra from the source's exits on (dist, time) keys,
+    canonical predecessors (smallest-id tight usable in-edge), the route's combination, and the
+    turn weight along the walk.  Returns (route dist cm or None, U)."""
+    E = g["edges"].reshape(-1, 4).astype(np.int64)
+    node_off = g["node_off"].astype(np.int64)
+    N = len(node_off) - 1
+    src = np.repeat(np.arange(N), np.diff(node_off))
+    h0, h1 = heads
+
+    def ok(e):
+        return e != 0xffffffff and ((int(E[e, 2]) >> 16) & 7) & mode_acc
+
+    def tms(d, e):
+        sp = min(int(E[e, 2]) & 0xffff, speed_cap)
+        return (d * 360) // max(sp, 1)
+
+    L = int(g["road_len_cm"][ra])
+    ef, er = int(g["road_fwd"][ra]), int(g["road_rev"][ra])
+    n0, n1 = int(g["road_node0"][ra]), int(g["road_node1"][ra])
+    lab, root = {}, {}
+    pq = []
+    if ok(ef) and L - sa <= bound:
+        k = ((L - sa) << 32) | tms(L - sa, ef)
+        root[n1] = k
+        lab[n1] = min(lab.get(n1, 1 << 64), k)
+    if ok(er) and sa <= bound:
+        k = (sa << 32) | tms(sa, er)
+        root[n0] = k
+        lab[n0] = min(lab.get(n0, 1 << 64), k)
+    for v, k in lab.items():
+        heapq.heappush(pq, (k, v))
+    done = set()
+    while pq:
+        k, u = heapq.heappop(pq)
+        if u in done or k != lab[u]:
+            continue
+        done.add(u)
+        for e in range(node_off[u], node_off[u + 1]):
+            if not ok(e):
+                continue
+            ln = int(E[e, 1])
+            nk = k + ((ln << 32) | tms(ln, e))
+            if (nk >> 32) > bound:
+                continue
+            v = int(E[e, 0])
+            if nk < lab.get(v, 1 << 64):
+                lab[v] = nk
+                heapq.heappush(pq, (nk, v))
+    Lb = int(g["road_len_cm"][rb])
+    bf, br = int(g["road_fwd"][rb]), int(g["road_rev"][rb])
+    best, combo = None, -1
+    if ra == rb:
+        if ok(bf) and sb >= sa:
+            best, combo = ((sb - sa) << 32) | tms(sb - sa, bf), 0
+        if ok(br) and sa >= sb:
+            k = ((sa - sb) << 32) | tms(sa - sb, br)
+            if best is None or k < best:
+                best, combo = k, 1
+    if ok(bf) and int(g["road_node0"][rb]) in lab:
+        k = lab[int(g["road_node0"][rb])] + ((sb << 32) | tms(sb, bf))
+        if best is None or k < best:
+            best, combo = k, 2
+    if ok(br) and int(g["road_node1"][rb]) in lab:
+        k = lab[int(g["road_node1"][rb])] + (((Lb - sb) << 32) | tms(Lb - sb, br))
+        if best is None or k < best:
+            best, combo = k, 3
+    if best is None or (best >> 32) > bound:
+        return None, 0
+    if combo < 2:
+        return best >> 32, 0
+    side = combo - 2
+    hs = h0[rb] if side == 0 else h1[rb]
+    v = int(g["road_node0"][rb]) if side == 0 else int(g["road_node1"][rb])
+    U = 0
+    while lab[v] != root.get(v):
+        tight = [e for e in range(len(E)) if E[e, 0] == v and ok(e) and int(src[e]) in lab
+                 and lab[int(src[e])] + ((int(E[e, 1]) << 32) | tms(int(E[e, 1]), e)) == lab[v]]
+        e = min(tight)
+        r2, rev = int(E[e, 3]) >> 1, int(E[e, 3]) & 1
+        U += _turn(h0[r2] if rev else h1[r2], hs)
+        hs = h1[r2] if rev else h0[r2]
+        v = int(src[e])
+    U += _turn(h1[ra] if v == n1 else h0[ra], hs)
+    return best >> 32, U
+
+
+def test_oracle_turn_weights_restated(built_lib, tmp_path):
+    """The oracle's per-transition turn weights against the brute-force restatement above, on
+    sampled transitions of 1 Hz and 30 s traces (every transition with a turn in a few traces)."""
+    path = str(tmp_path / "w.rmg")
+    world.build_world(path, 16, 16, 100.0, seed=3)
+    g = graphfile.load(path)
+    heads = mo.road_heads(g)
+    rng = np.random.default_rng(0)
+    checked = turned = 0
+    for rate, radius in ((1.0, 50.0), (30.0, 100.0)):
+        tr = world.generate_traces(path, n_traces=6, n_points=60 if rate == 1.0 else 16, rate_s=rate, noise_m=5.0, seed=4)
+        opts = engine.default_options(1, turn_penalty_factor=200.0, search_radius=radius)
+        T = len(tr["trace_off"]) - 1
+        ref = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts,
+                                   np.zeros(T, np.uint32)))
+        for k in range(T):
+            o = int(tr["trace_off"][k])
+            for s in range(1, int(ref["n_states"][k])):
+                la, lb = o + s - 1, o + s
+                KA, KB = int(ref["cand_n"][la]), int(ref["cand_n"][lb])
+                if not KA or not KB or rng.random() > 0.35:
+                    continue
+                gc = float(ref["gc"][lb])
+                bound = min(int(math.floor(min(gc * 5.0, 2000.0) * 100.0)), 100000000)
+                for i in range(KA):
+                    for j in range(KB):
+                        d, U = _py_route_turns(g, heads, int(ref["cand_road"][la][i]), int(ref["cand_s"][la][i]),
+                                               int(ref["cand_road"][lb][j]), int(ref["cand_s"][lb][j]), 1, 0xffff, bound)
+                        q = int(ref["trans_off"][lb]) + i * KB + j
+                        if ref["route"][q] == 0xffffffff:
+                            continue   # also beyond the time bound; no turn weight is used
+                        assert d == int(ref["route"][q]), (k, s, i, j)
+                        assert U == int(ref["route_turn"][q]), (k, s, i, j, U, int(ref["route_turn"][q]))
+                        checked += 1
+                        turned += U > 0
+    assert checked > 300 and turned > 100, (checked, turned)
+
+
+def test_turn_costs_change_some_choices_only(built_lib, small_world):
+    """Factor 0 gives zero weights and the previous matcher's choices; 200 weighs most routes that
+    leave their road and changes a few choices, never the routes themselves (rule 3b: turn costs
+    weigh a transition, they do not change its route)."""
+    g = graphfile.load(small_world)
+    tr = world.generate_traces(small_world, n_traces=24, n_points=200, rate_s=1.0, noise_m=8.0, seed=6)
+    T = len(tr["trace_off"]) - 1
+    res = {}
+    for f in (0.0, 200.0):
+        opts = engine.default_options(1, turn_penalty_factor=f)
+        res[f] = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts,
+                                      np.zeros(T, np.uint32)))
+    a, b = res[0.0], res[200.0]
+    assert not a["route_turn"].any()
+    np.testing.assert_array_equal(a["route"], b["route"])
+    valid = b["route"] != 0xffffffff
+    assert (b["route_turn"][valid] > 0).mean() > 0.2
+    diff = int((a["choice"] != b["choice"]).sum())
+    assert 0 < diff < 0.05 * len(a["choice"]), diff
