@@ -215,10 +215,11 @@ def test_workspace_exact_size_fallback(built_lib, small_world, monkeypatch):
     ref = mo.match(g, mo.Batch(big["trace_off"], big["lon"], big["lat"], big["time"], big["accuracy"],
                                engine.default_options(1), np.zeros(10, np.uint32)))
     compare_all(bm, ref, big["trace_off"])
-    # a batch whose own size does not fit still fails as too large for the device
-    monkeypatch.setenv("RM_TEST_WS_POINTS_LIMIT", "1000")
+    # a batch whose own size does not fit (1,750 points) still fails as too large for the device,
+    # and the matcher works again once memory allows
+    bigger = world.generate_traces(small_world, n_traces=14, n_points=125, rate_s=1.0, noise_m=5.0, seed=80)
     with pytest.raises(RuntimeError, match="does not fit in HBM"):
-        bm.run(big["trace_off"], big["lon"], big["lat"], big["time"], big["accuracy"])
+        bm.run(bigger["trace_off"], bigger["lon"], bigger["lat"], bigger["time"], bigger["accuracy"])
     monkeypatch.delenv("RM_TEST_WS_POINTS_LIMIT")
     bm.run(big["trace_off"], big["lon"], big["lat"], big["time"], big["accuracy"])
     compare_all(bm, ref, big["trace_off"])
