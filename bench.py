@@ -137,10 +137,13 @@ def cpu_baseline_leg(graph_path, tr, search_radius, procs, opts=None, trace_opt=
 # ---------------------------------------------------------------- launcher for --gpus N without torchrun
 def self_launch(n):
     port = str(29500 + (os.getpid() % 1000))
+    nonce = os.urandom(12).hex()
     procs = []
     for r in range(n):
+        # the rendezvous token names this launch and its nonce tells its id from one a crashed
+        # earlier launch with a reused pid left behind (dist.rendezvous)
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=port, RM_RDZV_TOKEN="%s_%s" % (port, os.getpid()))
+                   MASTER_PORT=port, RM_RDZV_TOKEN="%s_%s" % (port, os.getpid()), RM_RDZV_NONCE=nonce)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
     for p in procs:

@@ -1260,6 +1260,34 @@ void reduce_ranks(T* dst, const uint8_t* all, size_t count, int nranks, int op) 
   }
 }
 
+void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// The communicators are non-blocking (ncclConfig_t::blocking = 0), so that a rank whose peers
+// never join fails instead of blocking forever: a call may return
+// ncclInProgress, and its completion is polled here up to `limit_s` seconds (RM_COMM_TIMEOUT_S,
+// default 300); past it the communicator is aborted and the call throws.
+double comm_timeout_s() {
+  const char* e = std::getenv("RM_COMM_TIMEOUT_S");
+  const double s = e && *e ? std::atof(e) : 300.0;
+  return s > 0.0 ? s : 300.0;
+}
+void nccl_done(ncclComm_t comm, ncclResult_t r, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const double limit = comm_timeout_s();
+  while (r == ncclInProgress) {
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+      (void)ncclCommAbort(comm);
+      throw std::runtime_error(std::string(what) + ": no completion within " + std::to_string((int)limit) +
+                               " s (RM_COMM_TIMEOUT_S): a rank did not join; communicator aborted");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) break;
+  }
+  nccl_check(r, what);
+}
+
 // the tile stage's collectives over RCCL
 struct RcclTileComm final : TileComm {
   ncclComm_t nc;
@@ -1267,14 +1295,13 @@ struct RcclTileComm final : TileComm {
   RcclTileComm(rm_comm* c) : nc(c->comm), scratch(c->scratch) { rank = c->rank; nranks = c->nranks; }
   uint64_t max_u64(uint64_t v, hipStream_t st) override {
     RM_HIP(hipMemcpyAsync(scratch, &v, 8, hipMemcpyHostToDevice, st));
-    if (ncclAllReduce(scratch, scratch, 1, ncclUint64, ncclMax, nc, st) != ncclSuccess)
-      throw std::runtime_error("ncclAllReduce failed");
+    nccl_done(nc, ncclAllReduce(scratch, scratch, 1, ncclUint64, ncclMax, nc, st), "ncclAllReduce");
     RM_HIP(hipMemcpyAsync(&v, scratch, 8, hipMemcpyDeviceToHost, st));
     RM_HIP(hipStreamSynchronize(st));
     return v;
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
-    if (ncclAllGather(send, recv, bytes, ncclUint8, nc, st) != ncclSuccess) throw std::runtime_error("ncclAllGather failed");
+    nccl_done(nc, ncclAllGather(send, recv, bytes, ncclUint8, nc, st), "ncclAllGather");
   }
 };
 
@@ -1354,9 +1381,6 @@ int rm_runner_tiles(rm_runner* r, const rm_tile_params* p, rm_comm* comm, char**
 }  // extern "C"
 
 namespace {
-void nccl_check(ncclResult_t r, const char* what) {
-  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
-}
 }  // namespace
 
 extern "C" {
@@ -1379,7 +1403,16 @@ rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device) {
     RM_HIP(hipSetDevice(device));
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
-    nccl_check(ncclCommInitRank(&c->comm, nranks, uid, rank), "ncclCommInitRank");
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;   // a bounded wait for the peers (nccl_done), never a hang
+    const ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, uid, rank, &cfg);
+    if (r != ncclSuccess && r != ncclInProgress) { c->comm = nullptr; nccl_check(r, "ncclCommInitRank"); }
+    try {
+      nccl_done(c->comm, r, "ncclCommInitRank");
+    } catch (...) {
+      c->comm = nullptr;   // aborted (or failed): nothing left to destroy
+      throw;
+    }
     RM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     RM_HIP(hipMalloc(&c->scratch, 8));
     out = c.release();
@@ -1413,7 +1446,14 @@ int rm_tile_file_owner(uint64_t bucket, uint32_t tile, int nranks) { return tile
 void rm_comm_destroy(rm_comm* c) {
   if (!c) return;
   if (c->device >= 0) (void)hipSetDevice(c->device);
-  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->comm) {
+    try {
+      nccl_done(c->comm, ncclCommFinalize(c->comm), "ncclCommFinalize");
+      (void)ncclCommDestroy(c->comm);
+    } catch (const std::exception&) {
+      // aborted by nccl_done: the handle is gone
+    }
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->scratch) (void)hipFree(c->scratch);
   delete c;
@@ -1455,7 +1495,7 @@ int rm_comm_allreduce(rm_comm* c, void* buf, size_t count, int dtype, int op) {
     const ncclDataType_t dt = dtype == 0 ? ncclUint32 : (dtype == 1 ? ncclUint64 : ncclFloat64);
     const ncclRedOp_t ro = op == 0 ? ncclSum : ncclMax;
     RM_HIP(hipSetDevice(c->device));
-    nccl_check(ncclAllReduce(buf, buf, count, dt, ro, c->comm, c->stream), "ncclAllReduce");
+    nccl_done(c->comm, ncclAllReduce(buf, buf, count, dt, ro, c->comm, c->stream), "ncclAllReduce");
     RM_HIP(hipStreamSynchronize(c->stream));
   });
 }
@@ -1473,9 +1513,10 @@ int rm_comm_reduce_scatter(rm_comm* c, void* buf, size_t count_per_rank, int dty
     const size_t es = dtype == 0 ? 4 : 8;
     RM_HIP(hipSetDevice(c->device));
     // in place: this rank's chunk of the nranks-chunk buffer receives the reduction
-    nccl_check(ncclReduceScatter(buf, (uint8_t*)buf + lo * es, count_per_rank, dt, op == 0 ? ncclSum : ncclMax, c->comm,
-                                 c->stream),
-               "ncclReduceScatter");
+    nccl_done(c->comm,
+              ncclReduceScatter(buf, (uint8_t*)buf + lo * es, count_per_rank, dt, op == 0 ? ncclSum : ncclMax, c->comm,
+                                c->stream),
+              "ncclReduceScatter");
     RM_HIP(hipStreamSynchronize(c->stream));
   });
 }
@@ -1490,8 +1531,8 @@ int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op) {
     }
     RM_HIP(hipSetDevice(c->device));
     RM_HIP(hipMemcpyAsync(c->scratch, value, 8, hipMemcpyHostToDevice, c->stream));
-    nccl_check(ncclAllReduce(c->scratch, c->scratch, 1, ncclFloat64, op == 0 ? ncclSum : ncclMax, c->comm, c->stream),
-               "ncclAllReduce");
+    nccl_done(c->comm, ncclAllReduce(c->scratch, c->scratch, 1, ncclFloat64, op == 0 ? ncclSum : ncclMax, c->comm, c->stream),
+              "ncclAllReduce");
     RM_HIP(hipMemcpyAsync(value, c->scratch, 8, hipMemcpyDeviceToHost, c->stream));
     RM_HIP(hipStreamSynchronize(c->stream));
   });

@@ -353,10 +353,8 @@ struct CandSmem {
 // projection of the point onto the shape piece A->B in the point's local metric frame
 // (A = {lon, lat, cum_cm}, B likewise); squared distance in m^2 and the offset along
 // the road in cm.  Fixed operation order: bit-identical to oracle/meili_oracle.c.
-__device__ __forceinline__ void project(float alon, float alat, uint32_t acum, float blon, float blat, uint32_t bcum,
-                                        float lon, float lat, float mlon, float mlat, float& sq, uint32_t& s) {
-  const float ax = (alon - lon) * mlon, ay = (alat - lat) * mlat;
-  const float bx = (blon - lon) * mlon, by = (blat - lat) * mlat;
+__device__ __forceinline__ void project_rel(float ax, float ay, uint32_t acum, float bx, float by, uint32_t bcum,
+                                            float& sq, uint32_t& s) {
   const float dx = bx - ax, dy = by - ay;
   const float l2 = dx * dx + dy * dy;
   float t = 0.0f;
@@ -372,6 +370,18 @@ __device__ __forceinline__ void project(float alon, float alat, uint32_t acum, f
   if (v < acum) v = acum;
   if (v > bcum) v = bcum;
   s = v;
+}
+__device__ __forceinline__ void project(float alon, float alat, uint32_t acum, float blon, float blat, uint32_t bcum,
+                                        float lon, float lat, float mlon, float mlat, float& sq, uint32_t& s) {
+  project_rel((alon - lon) * mlon, (alat - lat) * mlat, acum, (blon - lon) * mlon, (blat - lat) * mlat, bcum, sq, s);
+}
+// An item whose two endpoints lie beyond the padded radius on the same side in x or in y
+//  cannot come within the radius: the projection lies between them, and the
+// fp32 rounding of the projected point is far below pad - r >= 0.5 m (a few ulps of coordinates
+// under 1000 km), so its sq exceeds r^2 with room to spare; rejecting it before the division is
+// bit-exact.
+__device__ __forceinline__ bool outside_pad(float ax, float ay, float bx, float by, float pad) {
+  return (ax > pad && bx > pad) || (ax < -pad && bx < -pad) || (ay > pad && by > pad) || (ay < -pad && by < -pad);
 }
 
 // time_ms on the device: below 2^32 cm*360 the IEEE double quotient truncates to the exact
@@ -497,9 +507,11 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
         for (int y = 0; y < 4; ++y) {
           if (q0 + y >= tot || ovf) break;
           if (!((r1[y].z >> 29) & acc)) continue;
+          const float ax = (as_f(r0[y].x) - lon) * mlon, ay = (as_f(r0[y].y) - lat) * mlat;
+          const float bx = (as_f(r0[y].z) - lon) * mlon, by = (as_f(r0[y].w) - lat) * mlat;
+          if (outside_pad(ax, ay, bx, by, pad)) continue;
           float sq; uint32_t sc;
-          project(as_f(r0[y].x), as_f(r0[y].y), r1[y].x, as_f(r0[y].z), as_f(r0[y].w), r1[y].y, lon, lat, mlon, mlat,
-                  sq, sc);
+          project_rel(ax, ay, r1[y].x, bx, by, r1[y].y, sq, sc);
           if (!(sq <= r2)) continue;
           const uint32_t road = r1[y].z & 0x1fffffffu;
           const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | r1[y].w;
@@ -611,8 +623,11 @@ __device__ void cand_wave_one(const DevGraph& g, const DevBatch& b, CandSmem& sm
         for (uint32_t it = lo + lane; it < hi; it += kWave) {
           const uint4 r0 = g.cell_rec[2 * (uint64_t)it], r1 = g.cell_rec[2 * (uint64_t)it + 1];
           if (!((r1.z >> 29) & acc)) continue;
+          const float ax = (as_f(r0.x) - lon) * mlon, ay = (as_f(r0.y) - lat) * mlat;
+          const float bx = (as_f(r0.z) - lon) * mlon, by = (as_f(r0.w) - lat) * mlat;
+          if (outside_pad(ax, ay, bx, by, pad)) continue;
           float sq; uint32_t sc;
-          project(as_f(r0.x), as_f(r0.y), r1.x, as_f(r0.z), as_f(r0.w), r1.y, lon, lat, mlon, mlat, sq, sc);
+          project_rel(ax, ay, r1.x, bx, by, r1.y, sq, sc);
           if (!(sq <= r2)) continue;
           const uint32_t road = r1.z & 0x1fffffffu, v = r1.w;
           // per-road min (sq, vertex) in the LDS hash

@@ -76,23 +76,54 @@ def _stdout_to_stderr(fn):
         os.close(saved)
 
 
+def _proc_start_ticks(pid):
+    """Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22): with
+    the pid it names one process instance, even after the pid is reused."""
+    try:
+        with open("/proc/%d/stat" % pid) as f:
+            return f.read().rsplit(")", 1)[1].split()[19]
+    except (OSError, IndexError):
+        return "0"
+
+
+def launch_nonce():
+    """What every rank of one launch agrees on and no other launch has: the launcher's
+    RM_RDZV_NONCE (bench.py self_launch sets a random one), else the parent process (torchrun's
+    agent, or whatever started the ranks) named by pid and start time."""
+    n = os.environ.get("RM_RDZV_NONCE")
+    if n:
+        return n
+    ppid = os.getppid()
+    return "%d:%s" % (ppid, _proc_start_ticks(ppid))
+
+
 def rendezvous_path(rdzv_dir=None, token=None):
     """Node-local file through which rank 0 hands its RCCL unique id to the other ranks."""
     rdzv_dir = rdzv_dir or os.environ.get("RM_RDZV_DIR", "/tmp")
-    token = token or "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+    token = token or os.environ.get("RM_RDZV_TOKEN") or "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
     return os.path.join(rdzv_dir, "rm_rdzv_%s.id" % token)
 
 
-def rendezvous(rank, path, make_id, size=128, timeout_s=300.0):
-    """Rank 0 writes make_id() (`size` bytes) atomically to `path`; every other rank polls
-    until the complete id is there.  Returns the id on every rank."""
+NONCE_BYTES = 64
+
+
+def rendezvous(rank, path, make_id, size=128, timeout_s=300.0, nonce=None):
+    """Rank 0 writes make_id() (`size` bytes) and the launch nonce atomically to `path`; every
+    other rank polls until a complete id carrying the same nonce is there.  A file a crashed
+    earlier launch left at the same path (same port, a reused pid) carries another nonce and is
+    ignored until rank 0 replaces it.  Returns the id on every rank."""
+    tag = (nonce if nonce is not None else launch_nonce()).encode()[:NONCE_BYTES].ljust(NONCE_BYTES, b"\0")
     if rank == 0:
         data = bytes(make_id())
         if len(data) != size:
             raise ValueError("rendezvous id must be %d bytes" % size)
+        try:
+            os.remove(path)   # whatever an earlier launch left
+        except FileNotFoundError:
+            pass
         tmp = "%s.%d.tmp" % (path, os.getpid())
         with open(tmp, "wb") as f:
-            f.write(data)
+            f.write(data + tag)
         os.replace(tmp, path)
         return data
     t0 = time.time()
@@ -100,12 +131,12 @@ def rendezvous(rank, path, make_id, size=128, timeout_s=300.0):
         try:
             with open(path, "rb") as f:
                 data = f.read()
-            if len(data) == size:
-                return data
+            if len(data) == size + NONCE_BYTES and data[size:] == tag:
+                return data[:size]
         except FileNotFoundError:
             pass
         if time.time() - t0 > timeout_s:
-            raise TimeoutError("rank %d: no rendezvous id at %s" % (rank, path))
+            raise TimeoutError("rank %d: no rendezvous id of this launch at %s" % (rank, path))
         time.sleep(0.05)
 
 

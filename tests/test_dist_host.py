@@ -94,7 +94,10 @@ def _rank_main(rank, world, port, graph_path, rdzv, out_dir):
         return [o.numpy().tobytes() for o in out]
 
     res = {}
-    # rendezvous: rank 0's id reaches every rank
+    # rendezvous: rank 0's id reaches every rank -- rank 0 comes late, so rank 1 first finds the
+    # stale id file the test planted (another launch's nonce) and must wait for the fresh one
+    if rank == 0:
+        time.sleep(1.0)
     res["rdzv"] = dist.rendezvous(rank, rdzv, lambda: os.urandom(128), 128, timeout_s=60).hex()
     # host communicator without a GPU: barrier + max-over-ranks timing exactly as bench.py times
     comm = dist.Comm(rank, world, -1, allgather=gloo_allgather)
@@ -150,6 +153,10 @@ def test_world2_host_comm_timing_and_tile_exchange(small_world, tmp_path, built_
     port = _free_port()
     ctx = mp.get_context("spawn")
     rdzv = str(tmp_path / "rdzv.id")
+    from reporter_amd import dist
+    stale = os.urandom(128)
+    with open(rdzv, "wb") as f:   # what a crashed earlier launch at the same path left behind
+        f.write(stale + b"1234:5678".ljust(dist.NONCE_BYTES, b"\0"))
     procs = [ctx.Process(target=_rank_main, args=(r, 2, port, small_world, rdzv, str(tmp_path))) for r in range(2)]
     for p in procs:
         p.start()
@@ -157,7 +164,7 @@ def test_world2_host_comm_timing_and_tile_exchange(small_world, tmp_path, built_
         p.join(280)
         assert p.exitcode == 0
     r0, r1 = (json.load(open(str(tmp_path / ("rank%d.json" % r)))) for r in range(2))
-    assert r0["rdzv"] == r1["rdzv"] and len(r0["rdzv"]) == 256
+    assert r0["rdzv"] == r1["rdzv"] and len(r0["rdzv"]) == 256 and r0["rdzv"] != stale.hex()
     assert r0["sum"] == r1["sum"] == 3.0 and r0["max"] == r1["max"] == 10.0
     want_ar = (np.arange(37, dtype=np.uint64) * 14 + 1000).tolist()
     assert r0["ar"] == r1["ar"] == want_ar
@@ -175,6 +182,26 @@ def test_world2_host_comm_timing_and_tile_exchange(small_world, tmp_path, built_
     want = _oracle_tiles(ref, tr, 2)
     assert len(want) > 3 and r0["files"] and r1["files"]
     assert union == want
+
+
+def test_rendezvous_ignores_a_stale_id(tmp_path):
+    """an id file at the launch's path written by another launch (a crashed
+    run whose pid and port recur) is not accepted; the fresh one is, and rank 0 replaces it."""
+    from reporter_amd import dist
+    path = str(tmp_path / "rm_rdzv_x.id")
+    stale = os.urandom(128)
+    with open(path, "wb") as f:
+        f.write(stale + b"old-launch".ljust(dist.NONCE_BYTES, b"\0"))
+    with pytest.raises(TimeoutError):
+        dist.rendezvous(1, path, None, 128, timeout_s=0.3, nonce="this-launch")
+    with open(path, "wb") as f:   # a round-4 file (no nonce at all)
+        f.write(stale)
+    with pytest.raises(TimeoutError):
+        dist.rendezvous(1, path, None, 128, timeout_s=0.3, nonce="this-launch")
+    fresh = dist.rendezvous(0, path, lambda: os.urandom(128), 128, nonce="this-launch")
+    assert fresh != stale and dist.rendezvous(1, path, None, 128, timeout_s=5, nonce="this-launch") == fresh
+    # the default nonce: the parent process named by pid and start time (shared by sibling ranks)
+    assert dist.launch_nonce().startswith("%d:" % os.getppid()) and dist.launch_nonce() != "%d:0" % os.getppid()
 
 
 def test_shard_ids_partition_one_workload():

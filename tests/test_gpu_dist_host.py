@@ -116,3 +116,27 @@ def test_two_ranks_one_gpu_tiles_and_histogram(small_world, tmp_path):
     np.testing.assert_array_equal(np.load(str(tmp_path / "hist.npy")), wh)
     np.testing.assert_array_equal(np.load(str(tmp_path / "dur.npy")), wd)
     assert wh.sum() > 0 and wd.sum() > 0
+
+
+_LONE_RANK = r"""
+import os, sys, time
+sys.path.insert(0, os.environ["RM_ROOT"])
+from reporter_amd import dist
+t0 = time.time()
+try:
+    dist.Comm(0, 2, 0, rdzv_dir=os.environ["RM_RDZV_DIR"], token="lone", timeout_s=5)
+except Exception as e:   # the library's RuntimeError, raised by the ctypes shim
+    print("FAILED after %.1f s: %s" % (time.time() - t0, e))
+    sys.exit(3)
+sys.exit(0)
+"""
+
+
+def test_comm_init_without_peers_fails_in_bounded_time(built_lib, tmp_path):
+    """rank 0 of a world of 2 whose peer never starts fails (non-zero exit,
+    an error naming the timeout) after RM_COMM_TIMEOUT_S instead of blocking in RCCL's init."""
+    import subprocess
+    env = dict(os.environ, RM_ROOT=ROOT, RM_RDZV_DIR=str(tmp_path), RM_COMM_TIMEOUT_S="4")
+    r = subprocess.run([sys.executable, "-c", _LONE_RANK], env=env, capture_output=True, text=True, timeout=90)
+    assert r.returncode == 3, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "RM_COMM_TIMEOUT_S" in r.stdout and "did not join" in r.stdout, r.stdout
