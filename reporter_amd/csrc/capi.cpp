@@ -1264,10 +1264,9 @@ void nccl_check(ncclResult_t r, const char* what) {
   if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-// The communicators are non-blocking (ncclConfig_t::blocking = 0), so that a rank whose peers
-// never join fails instead of blocking forever: a call may return
-// ncclInProgress, and its completion is polled here up to `limit_s` seconds (RM_COMM_TIMEOUT_S,
-// default 300); past it the communicator is aborted and the call throws.
+// A call that returns ncclInProgress (a non-blocking communicator's; rm_comm_init makes blocking
+// ones, so this is a guard) is polled to completion for up to RM_COMM_TIMEOUT_S seconds (default
+// 300); past it the communicator is aborted and the call throws.
 double comm_timeout_s() {
   const char* e = std::getenv("RM_COMM_TIMEOUT_S");
   const double s = e && *e ? std::atof(e) : 300.0;
@@ -1403,16 +1402,33 @@ rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device) {
     RM_HIP(hipSetDevice(device));
     ncclUniqueId uid;
     std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;   // a bounded wait for the peers (nccl_done), never a hang
-    const ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, uid, rank, &cfg);
-    if (r != ncclSuccess && r != ncclInProgress) { c->comm = nullptr; nccl_check(r, "ncclCommInitRank"); }
-    try {
-      nccl_done(c->comm, r, "ncclCommInitRank");
-    } catch (...) {
-      c->comm = nullptr;   // aborted (or failed): nothing left to destroy
-      throw;
+    // A bounded wait for the peers: a rank whose peers never join (a crashed
+    // launch, a stale rendezvous id) must fail, not block in the init forever.  RCCL's init cannot
+    // be cancelled once its bootstrap waits for the peers (aborting a non-blocking init hung in
+    // tests), so a watchdog ends the process with status 3 and a message after
+    // RM_COMM_TIMEOUT_S seconds (default 300) -- a failure of this rank, never a re-exec.
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    const double limit = comm_timeout_s();
+    std::thread watchdog([&] {
+      std::unique_lock<std::mutex> lk(mu);
+      if (!cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return done; })) {
+        std::fprintf(stderr, "rm_comm_init: rank %d of %d: the other ranks did not join within %d s (RM_COMM_TIMEOUT_S); "
+                             "exiting with status 3\n", rank, nranks, (int)limit);
+        std::fflush(stderr);
+        std::_Exit(3);
+      }
+    });
+    const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done = true;
     }
+    cv.notify_all();
+    watchdog.join();
+    if (r != ncclSuccess) c->comm = nullptr;
+    nccl_check(r, "ncclCommInitRank");
     RM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     RM_HIP(hipMalloc(&c->scratch, 8));
     out = c.release();
@@ -1446,14 +1462,7 @@ int rm_tile_file_owner(uint64_t bucket, uint32_t tile, int nranks) { return tile
 void rm_comm_destroy(rm_comm* c) {
   if (!c) return;
   if (c->device >= 0) (void)hipSetDevice(c->device);
-  if (c->comm) {
-    try {
-      nccl_done(c->comm, ncclCommFinalize(c->comm), "ncclCommFinalize");
-      (void)ncclCommDestroy(c->comm);
-    } catch (const std::exception&) {
-      // aborted by nccl_done: the handle is gone
-    }
-  }
+  if (c->comm) ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->scratch) (void)hipFree(c->scratch);
   delete c;

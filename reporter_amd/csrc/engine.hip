@@ -380,7 +380,11 @@ __device__ __forceinline__ void project(float alon, float alat, uint32_t acum, f
 // fp32 rounding of the projected point is far below pad - r >= 0.5 m (a few ulps of coordinates
 // under 1000 km), so its sq exceeds r^2 with room to spare; rejecting it before the division is
 // bit-exact.
+#ifndef RM_K1_REJECT
+#define RM_K1_REJECT 1   // 0: every item is projected (A/B of the reject)
+#endif
 __device__ __forceinline__ bool outside_pad(float ax, float ay, float bx, float by, float pad) {
+  if (!RM_K1_REJECT) return false;
   return (ax > pad && bx > pad) || (ax < -pad && bx < -pad) || (ay > pad && by > pad) || (ay < -pad && by < -pad);
 }
 

@@ -12,6 +12,7 @@ ap.add_argument("--split", type=int, default=0, help="also time M concurrent run
 ap.add_argument("--ab-locality", action="store_true", help="also time the same batch with the locality order off / on")
 ap.add_argument("--ab-modes", default="0,1,0,1", help="locality modes the A/B cycles through")
 ap.add_argument("--ball-radius", type=float, default=None, help="route-ball radius in m (0: the search tiers alone)")
+ap.add_argument("--turn", type=float, default=0.0, help="turn_penalty_factor of every trace (meili's auto default: 200)")
 a = ap.parse_args()
 c = dict(world.CONFIGS[a.config])
 if a.traces:
@@ -28,7 +29,7 @@ eng = engine.Engine(gp, 0)
 if a.ball_radius is not None:
     eng.set_ball_radius(a.ball_radius)
 bm = engine.BatchMatcher(eng)
-opts = engine.default_options(1, search_radius=c["search_radius"])
+opts = engine.default_options(1, search_radius=c["search_radius"], turn_penalty_factor=a.turn)
 t = time.time()
 bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts)
 print("first run %.3fs" % (time.time() - t), bm.sizes(), flush=True)

@@ -23,7 +23,8 @@ STOCK = {0: 200.0, 1: 200.0, 2: 0.0, 3: 140.0, 4: 100.0}   # meili's per-mode de
 
 
 def _turned(c):
-    ref = c["_ref"]
+    """Transitions with a valid route and a non-zero turn weight (the _ref is dropped from c)."""
+    ref = c.pop("_ref")
     valid = ref["route"] != 0xffffffff
     return int((ref["route_turn"][valid] > 0).sum())
 
@@ -45,9 +46,8 @@ def test_c2_auto_200(c2_graph, n_traces, n_points):
     tr = world.generate_traces(path, n_traces, n_points, cfg["rate_s"], cfg["noise_m"], seed=1200)
     opts = engine.default_options(1, search_radius=cfg["search_radius"], turn_penalty_factor=200.0)
     c = match_and_compare(path, tr, opts, None, hist=True, keep_ref=True)
-    assert _turned(c) > 10_000, c
-    assert c["segments"] > 10_000 and c["valid_reports"] > 1_000, c
-    c.pop("_ref")
+    assert _turned(c) > 10 * n_traces, c
+    assert c["segments"] > 2 * n_traces and c["valid_reports"] > n_traces // 10, c
     print("C2 turn 200 parity", c)
 
 
@@ -62,7 +62,6 @@ def test_search_tiers_and_mixed(built_lib, tmpdir_session, ball_radius):
     opts = engine.default_options(1, search_radius=100.0, turn_penalty_factor=200.0)
     c = match_and_compare(path, tr, opts, None, hist=True, ball_radius=ball_radius, keep_ref=True)
     assert _turned(c) > 5_000 and c["chained"] > 5_000, c
-    c.pop("_ref")
     print("30 s turn parity", ball_radius, c)
 
 
@@ -86,7 +85,6 @@ def test_modes_stock_factors_sigma(c2_graph):
     trace_opt = (np.arange(n) % len(opts)).astype(np.uint32)
     c = match_and_compare(path, tr, opts, trace_opt, hist=True, keep_ref=True)
     assert _turned(c) > 5_000, c
-    c.pop("_ref")
     print("modes x sigma turn parity", c)
 
 
@@ -105,7 +103,6 @@ def test_city_stock_factors(city, rate, radius, n, pts):
     opts = engine.default_options(1, search_radius=radius, turn_penalty_factor=200.0)
     c = match_and_compare(city, tr, opts, None, hist=True, keep_ref=True)
     assert _turned(c) > 2_000, c
-    c.pop("_ref")
     print("city turn parity", rate, c)
 
 
