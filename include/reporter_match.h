@@ -249,8 +249,10 @@ int rm_runner_route_tiers(rm_runner* r, uint64_t out[10]);
 int rm_runner_get_states(rm_runner* r, uint32_t* n_states, uint32_t* state_orig);
 int rm_runner_get_candidates(rm_runner* r, uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
 int rm_runner_get_routes(rm_runner* r, uint32_t* trans_off, double* gc, uint32_t* route_cm);
-/* turn weight U of every transition (DESIGN.md §3 rule 3b; all 0 when no trace had turn costs) */
-int rm_runner_get_route_turns(rm_runner* r, uint32_t* route_turn);
+/* with turn costs (DESIGN.md §3 rule 3b): every transition's distance term turn_m + |route_m - gc|
+ * in metres (+inf when invalid), as the Viterbi adds it; *present = 0 (nothing written) when no
+ * trace of the last run had turn costs */
+int rm_runner_get_route_terms(rm_runner* r, double* route_d, int* present);
 int rm_runner_get_viterbi(rm_runner* r, int8_t* choice, uint8_t* chain_start);
 int rm_runner_get_paths(rm_runner* r, uint32_t* path_off, uint32_t* path_cnt, uint32_t* path_edges, uint32_t* route_dist);
 /* segments: 56-byte records (rm::SegmentRec); seg_off has n_traces+1 entries */

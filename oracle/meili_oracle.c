@@ -252,7 +252,7 @@ struct og_result {
   uint64_t P, T, n_trans, n_path, n_seg;
   uint32_t* n_states; uint32_t* state_orig;
   uint8_t* cand_n; uint32_t* cand_road; uint32_t* cand_s; float* cand_sq;
-  uint32_t* trans_off; double* gc; uint32_t* route; uint32_t* route_turn;
+  uint32_t* trans_off; double* gc; uint32_t* route; uint32_t* route_turn; double* route_d;
   int8_t* choice; uint8_t* chain_start;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_edges; uint32_t* route_dist;
   uint32_t* seg_off; og_segment* segs;
@@ -724,6 +724,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
   R->n_trans = nt;
   R->route = (uint32_t*)malloc(sizeof(uint32_t) * (nt ? nt : 1));
   R->route_turn = (uint32_t*)calloc(nt ? nt : 1, sizeof(uint32_t));
+  R->route_d = (double*)malloc(sizeof(double) * (nt ? nt : 1));
   uint16_t* H0 = (uint16_t*)malloc(sizeof(uint16_t) * (g->n_roads ? g->n_roads : 1));
   uint16_t* H1 = (uint16_t*)malloc(sizeof(uint16_t) * (g->n_roads ? g->n_roads : 1));
   og_road_headings(g, H0, H1);
@@ -734,6 +735,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
     const uint32_t o = b->trace_off[k];
     const og_options* op = &b->opts[b->trace_opt[k]];
     const int turns = op->turn_penalty_factor > 0.0f;
+    const double tscale = (double)op->turn_penalty_factor * 0x1p-16;   /* metres per unit of turn weight */
     for (uint32_t s = 1; s < R->n_states[k]; ++s) {
       const uint32_t la = o + s - 1, lb = o + s;
       const uint32_t pa = o + R->state_orig[la], pb = o + R->state_orig[lb];
@@ -776,6 +778,12 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
             R->route_turn[R->trans_off[lb] + i * KB + j] = og_turn_walk(g, &ws, H0, H1, ra, rb, combo);
             og_cnt[20]++;
           }
+          /* the transition's distance term (rule 3b): turn_m + |route_m - gc|, turn_m = U * factor /
+           * 65536 (+0 without turn costs, and +0 + x == x); +inf for an invalid route */
+          R->route_d[R->trans_off[lb] + i * KB + j] =
+              out == OG_ROUTE_INVALID ? INFINITY
+                                      : (double)R->route_turn[R->trans_off[lb] + i * KB + j] * tscale +
+                                            fabs((double)out * 0.01 - gc);
         }
         count_to_targets(&ws, kmax);
       }
@@ -791,7 +799,6 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
     const og_options* op = &b->opts[b->trace_opt[k]];
     const double inv2s2 = 1.0 / (2.0 * (double)op->sigma_z * (double)op->sigma_z);
     const double inv_beta = 1.0 / (double)op->beta;
-    const double tscale = (double)op->turn_penalty_factor * 0x1p-16;   /* metres per unit of turn weight */
     int prev_ok = 0;
     for (uint32_t s = 0; s < S; ++s) {
       const uint32_t l = o + s, KB = R->cand_n[l];
@@ -806,10 +813,9 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
             const double ci = cost[(l - 1) * (uint64_t)OG_K + i];
             const uint32_t rc = R->route[R->trans_off[l] + i * KB + j];
             if (ci == INFINITY || rc == OG_ROUTE_INVALID) continue;
-            /* one fused multiply-add: cost_i + (turn_m + |route_m - gc|) / beta, rounded once; turn_m
-             * = U * factor / 65536 is +0 without turn costs, and +0 + x == x */
-            const double tm = (double)R->route_turn[R->trans_off[l] + i * KB + j] * tscale;
-            const double c = fma(tm + fabs((double)rc * 0.01 - R->gc[l]), inv_beta, ci);
+            /* one fused multiply-add: cost_i + (turn_m + |route_m - gc|) / beta, rounded once (the
+             * distance term formed with the route in S2) */
+            const double c = fma(R->route_d[R->trans_off[l] + i * KB + j], inv_beta, ci);
             if (c < best) { best = c; arg = (int)i; }
           }
           const double em = (double)R->cand_sq[l * (uint64_t)OG_K + j] * inv2s2;
@@ -970,7 +976,7 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
 void og_free(og_result* r) {
   if (!r) return;
   free(r->n_states); free(r->state_orig); free(r->cand_n); free(r->cand_road); free(r->cand_s); free(r->cand_sq);
-  free(r->trans_off); free(r->gc); free(r->route); free(r->route_turn); free(r->choice); free(r->chain_start);
+  free(r->trans_off); free(r->gc); free(r->route); free(r->route_turn); free(r->route_d); free(r->choice); free(r->chain_start);
   free(r->path_off); free(r->path_cnt); free(r->path_edges); free(r->route_dist); free(r->seg_off); free(r->segs);
   free(r);
 }
@@ -989,6 +995,7 @@ void og_get_routes(const og_result* r, uint32_t* trans_off, double* gc, uint32_t
   memcpy(trans_off, r->trans_off, 4 * r->P); memcpy(gc, r->gc, 8 * r->P); memcpy(route_cm, r->route, 4 * r->n_trans);
 }
 void og_get_route_turns(const og_result* r, uint32_t* route_turn) { memcpy(route_turn, r->route_turn, 4 * r->n_trans); }
+void og_get_route_terms(const og_result* r, double* route_d) { memcpy(route_d, r->route_d, 8 * r->n_trans); }
 void og_road_heads(const og_graph* g, uint16_t* h0, uint16_t* h1) { og_road_headings(g, h0, h1); }
 void og_get_viterbi(const og_result* r, int8_t* choice, uint8_t* chain_start) {
   memcpy(choice, r->choice, r->P); memcpy(chain_start, r->chain_start, r->P);

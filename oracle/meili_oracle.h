@@ -94,6 +94,8 @@ void og_get_candidates(const og_result* r, uint8_t* cand_n /*P*/, uint32_t* road
 void og_get_routes(const og_result* r, uint32_t* trans_off /*P*/, double* gc /*P*/, uint32_t* route_cm /*n_trans*/);
 /* turn weight U of every transition (0 without turn costs or along one road; DESIGN.md §3 rule 3b) */
 void og_get_route_turns(const og_result* r, uint32_t* route_turn /*n_trans*/);
+/* every transition's distance term turn_m + |route_m - gc| (metres; +inf invalid), as S3 adds it */
+void og_get_route_terms(const og_result* r, double* route_d /*n_trans*/);
 /* per road: the headings (whole degrees, 8-bit Valhalla steps) at node0 and node1 into the road */
 void og_road_heads(const og_graph* g, uint16_t* h0 /*n_roads*/, uint16_t* h1 /*n_roads*/);
 void og_get_viterbi(const og_result* r, int8_t* choice /*P*/, uint8_t* chain_start /*P*/);

@@ -49,7 +49,8 @@ def lib():
         h.og_free.argtypes = [C.c_void_p]
         h.og_sizes.argtypes = [C.c_void_p] + [C.POINTER(C.c_uint64)] * 4
         for n, k in (("og_get_states", 2), ("og_get_candidates", 4), ("og_get_routes", 3), ("og_get_viterbi", 2),
-                     ("og_get_paths", 4), ("og_get_segments", 2), ("og_get_route_turns", 1)):
+                     ("og_get_paths", 4), ("og_get_segments", 2), ("og_get_route_turns", 1),
+                     ("og_get_route_terms", 1)):
             getattr(h, n).argtypes = [C.c_void_p] + [C.c_void_p] * k
         h.og_report_trace.restype = C.c_int
         h.og_report_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_double, C.c_double, C.c_uint32, C.c_uint32,
@@ -216,6 +217,9 @@ def match(graph, batch):
         out["route_turn"] = np.empty(max(NT, 1), np.uint32)
         h.og_get_route_turns(r, out["route_turn"].ctypes.data)
         out["route_turn"] = out["route_turn"][:NT]
+        out["route_d"] = np.empty(max(NT, 1), np.float64)
+        h.og_get_route_terms(r, out["route_d"].ctypes.data)
+        out["route_d"] = out["route_d"][:NT]
         out["choice"] = np.empty(P, np.int8)
         out["chain_start"] = np.empty(P, np.uint8)
         h.og_get_viterbi(r, out["choice"].ctypes.data, out["chain_start"].ctypes.data)

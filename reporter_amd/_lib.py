@@ -129,7 +129,7 @@ PROTOTYPES = [
     ("rm_runner_get_states", C.c_int, [P, P, P]),
     ("rm_runner_get_candidates", C.c_int, [P, P, P, P, P]),
     ("rm_runner_get_routes", C.c_int, [P, P, P, P]),
-    ("rm_runner_get_route_turns", C.c_int, [P, P]),
+    ("rm_runner_get_route_terms", C.c_int, [P, P, P]),
     ("rm_runner_get_viterbi", C.c_int, [P, P, P]),
     ("rm_runner_get_paths", C.c_int, [P, P, P, P, P]),
     ("rm_runner_get_segments", C.c_int, [P, P, P]),

@@ -1181,7 +1181,9 @@ int rm_runner_get_candidates(rm_runner* r, uint8_t* a, uint32_t* b, uint32_t* c,
   return guarded([&] { r->m->get_candidates(a, b, c, d); });
 }
 int rm_runner_get_routes(rm_runner* r, uint32_t* a, double* b, uint32_t* c) { return guarded([&] { r->m->get_routes(a, b, c); }); }
-int rm_runner_get_route_turns(rm_runner* r, uint32_t* a) { return guarded([&] { r->m->get_route_turns(a); }); }
+int rm_runner_get_route_terms(rm_runner* r, double* a, int* present) {
+  return guarded([&] { *present = r->m->get_route_terms(a); });
+}
 int rm_runner_get_viterbi(rm_runner* r, int8_t* a, uint8_t* b) { return guarded([&] { r->m->get_viterbi(a, b); }); }
 int rm_runner_get_paths(rm_runner* r, uint32_t* a, uint32_t* b, uint32_t* c, uint32_t* d) {
   return guarded([&] { r->m->get_paths(a, b, c, d); });

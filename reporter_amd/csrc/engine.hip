@@ -61,7 +61,9 @@ struct DevBatch {  // POD view of the workspace for kernels
   uint32_t* slot_trace; uint32_t* n_states; uint32_t* state_orig; double* state_time;
   uint8_t* cand_n; uint4* cand_desc; float* cand_sq;
   uint32_t* trans_cnt; uint32_t* trans_off; double* gc; uint32_t* route; uint4* pair_info;
-  uint32_t* route_turn;   // per transition: turn weight (rule 3b); null when no trace of the batch has turn costs
+  // per transition with turn costs (rule 3b): the distance term K3 adds, turn_m + |route_m - gc| in
+  // metres (+inf for an invalid route); null when no trace of the batch has turn costs
+  double* route_d;
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
@@ -125,6 +127,14 @@ __device__ __forceinline__ uint32_t route_bound(double gc, const MatchOptions& o
   double bcm = floor(maxd * 100.0);
   if (!(bcm >= 0.0)) bcm = 0.0;
   return bcm > (double)kMaxBoundCm ? kMaxBoundCm : (uint32_t)bcm;
+}
+// The distance term of a transition with turn costs (rule 3b), exactly as the oracle's Viterbi
+// forms it: turn weight U x factor x 2^-16 metres, plus |route_m - gc|; +inf for an invalid route.
+// pair_info.w holds the pair's factor (float bits, 0: no turn costs).
+__device__ __forceinline__ double route_term(uint32_t route_cm, uint32_t U, uint32_t factor_bits, double gc) {
+  if (route_cm == kRouteInvalid) return __longlong_as_double(0x7ff0000000000000ll);
+  const double tm = (double)U * ((double)__uint_as_float(factor_bits) * 0x1p-16);
+  return tm + fabs((double)route_cm * 0.01 - gc);
 }
 __device__ __forceinline__ uint32_t time_bound(double dt, const MatchOptions& o) {
   if (!(dt > 0.0)) return 0xffffffffu;
@@ -866,9 +876,10 @@ __global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long l
       const uint32_t pa = o + b.state_orig[p - 1], pb = o + b.state_orig[p];
       const double gc = b.gc[p];   // written by k_states (the rule's own measurement)
       const MatchOptions op = b.opts[b.trace_opt[k]];
-      // .w: the pair's routes carry turn weights (turn_penalty_factor > 0, rule 3b)
+      // .w: the pair's turn_penalty_factor (float bits) when its routes carry turn costs (rule 3b), else 0
       b.pair_info[p] = make_uint4(route_bound(gc, op), time_bound(b.time[pb] - b.time[pa], op),
-                                  KA | (KB << 8) | ((uint32_t)op.mode << 16), op.turn_penalty_factor > 0.f ? 1u : 0u);
+                                  KA | (KB << 8) | ((uint32_t)op.mode << 16),
+                                  op.turn_penalty_factor > 0.f ? __float_as_uint(op.turn_penalty_factor) : 0u);
     }
     b.trans_cnt[p] = c;
     b.src_cnt[p] = ns;
@@ -1395,7 +1406,9 @@ struct TurnCtx {
   uint4 a1;                      // the source's second descriptor word (its road's endpoints)
   unsigned long long rk1, rk0;   // exit root keys
   int mode;
-  bool on;                       // the pair has turn costs (pair_info.w) and the batch a route_turn array
+  bool on;                       // the pair has turn costs (pair_info.w) and the batch a route_d array
+  uint32_t factor;               // pair_info.w
+  double gc;                     // the pair's measurement distance
 };
 
 template <class Label, class PL>
@@ -1418,12 +1431,13 @@ __device__ __forceinline__ void route_targets(const DevGraph& g, const DevBatch&
       uint32_t r = kRouteInvalid;
       if (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) r = key_dist(key);
       res[((j0 + x) & (kMaxCand - 1)) * stride] = r;
-      if (tc.on && j0 + x < KB) {   // rare (turn costs in a search tier): stored straight away
+      if (tc.on && j0 + x < KB) {   // a batch with turn costs (rare in a search tier): stored straight away
         bool ok = true;
-        const uint32_t u = r == kRouteInvalid ? 0u
-                                              : search_turn_walk(g, plab, tc.mode, a0, tc.a1, t0[x], t1[x], tc.rk1, tc.rk0, combo, ok);
+        const uint32_t u = (r == kRouteInvalid || !tc.factor)
+                               ? 0u
+                               : search_turn_walk(g, plab, tc.mode, a0, tc.a1, t0[x], t1[x], tc.rk1, tc.rk0, combo, ok);
         if (!ok) trace_fail(b, p, kErrRounds);
-        b.route_turn[ob + j0 + x] = u;
+        b.route_d[ob + j0 + x] = route_term(r, u, tc.factor, tc.gc);
       }
     }
   }
@@ -1510,11 +1524,14 @@ struct K2Src {
   uint32_t ob;                   // the item's first route in b.route
   uint32_t lim;                  // routes with distance <= lim are exact from the tables (ball_exact_limit)
 };
-// per item, with turn costs (rule 3b): the mode's turn rows and the source road's headings
+// per item of a batch with turn costs (rule 3b): the mode's turn rows, the source road's headings
+// and endpoints, the pair's factor
 struct K2Turn {
   unsigned long long trn;        // turn rows of the item's mode (a global address)
   uint32_t hw;                   // heading word of the source road (rm_common.hpp head_back)
-  uint32_t on;                   // the item's routes carry turn weights
+  uint32_t fac;                  // pair_info.w: the factor's float bits; 0: the item has no turn costs
+  uint32_t n0, n1;               // the source road's endpoints (the exits' nodes)
+  uint32_t mode, pad;
 };
 template <bool TURN>
 struct K2Smem {
@@ -1557,13 +1574,106 @@ __device__ __forceinline__ uint32_t k2_route(const K2Src& S, const uint4& t0, co
   return (key != kKeyInf && key_dist(key) <= S.bound && key_time(key) <= S.tmax) ? key_dist(key) : kRouteInvalid;
 }
 
-// The turn weight of a route the tables answer (rule 3b, TURN): the label of the entry node comes
-// from one exit strictly (on a tie the canonical path may mix both exits' trees: the item goes to
-// the search tiers), that exit's turn row holds the weight of the path from the exit node on and
-// the heading it leaves the exit node with; the turn at the exit node is from the source road.
+// labels from the route balls of the two exits (see k_routes_ball2)
+struct BallPathLabels {
+  const uint4* ent;
+  uint2 h1, h0;
+  unsigned long long rk1, rk0;
+  uint32_t rm;   // road-id bits of a row's first word
+  // both exits' rows of `road` (a dummy row for an unusable exit), first probes issued together
+  __device__ void rows(uint32_t road, uint4& r1, uint4& r0) const {
+    // both first probes issued together: an unusable exit reads row 0 (valid: the mode has
+    // tables) and its row is replaced by the empty row afterwards
+    const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
+    const uint64_t i1 = u1 ? ball_row0(h1.x) + ball_slot(road, h1.y) : 0u;
+    const uint64_t i0 = u0 ? ball_row0(h0.x) + ball_slot(road, h0.y) : 0u;
+    const uint4 l1 = ent[i1], l0 = ent[i0];
+    const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+    r1 = ball_resolve(ent, h1, road, u1 ? l1 : none, rm);
+    r0 = ball_resolve(ent, h0, road, u0 ? l0 : none, rm);
+  }
+  __device__ unsigned long long operator()(uint32_t, uint32_t road, uint32_t side) const {
+    uint4 r1, r0;
+    rows(road, r1, r0);
+    return side ? ball_label(rk1, row_key1(r1), rk0, row_key1(r0)) : ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
+  }
+};
+
+// One step of the ball-tier walk back from node x (label lx, rows r1/r0 of a road with x at
+// `side`): x's canonical predecessor in the two-exit search.  Where exactly one exit gives x
+// its label, the tight in-edges of the two-exit search are that exit's own and the canonical
+// one is the predecessor stored in its row; on a tie between the exits they are the union of
+// both, and the canonical one the smaller stored index (in_rec is in edge-id order).  Only
+// when that index was not stored (7 or more in-edges before it) are the in-edges scanned.
+// Returns false when no predecessor exists (not reached for a valid route).
+__device__ __forceinline__ bool ball_pred_step(const DevGraph& g, const BallPathLabels& lab, uint32_t acc, int mode,
+                                               uint32_t x, unsigned long long lx, const uint4& r1, const uint4& r0,
+                                               uint32_t side, uint4& rec, unsigned long long& plu) {
+  const uint32_t q0 = g.in_off[x];
+  const unsigned long long k1 = side ? row_key1(r1) : row_key0(r1), k0 = side ? row_key1(r0) : row_key0(r0);
+  uint32_t idx = kBallPredNone;
+  if (lab.rk1 != kKeyInf && k1 != kKeyInf && lab.rk1 + k1 == lx) idx = min(idx, ball_pred(r1.x, side, lab.rm));
+  if (lab.rk0 != kKeyInf && k0 != kKeyInf && lab.rk0 + k0 == lx) idx = min(idx, ball_pred(r0.x, side, lab.rm));
+  if (idx < kBallPredNone) {
+    rec = g.in_rec[q0 + idx];
+    plu = kKeyInf;   // the caller reads the predecessor's label from its rows
+    return true;
+  }
+  for (uint32_t q = q0, q1 = g.in_off[x + 1]; q < q1; ++q) {
+    const uint4 r = g.in_rec[q];
+    const uint32_t inf = g.in_info[q];
+    if (!edge_ok(inf, acc)) continue;
+    const unsigned long long lu = lab(r.y, r.z >> 1, r.z & 1u);
+    if (lu != kKeyInf && lu + make_key(r.w, time_ms_dev(r.w, mode_speed_dkph(mode, inf & 0xffffu))) == lx) {
+      rec = r;
+      plu = lu;
+      return true;
+    }
+  }
+  return false;
+}
+
+// Turn weight of a route the tables answer, by walking its two-exit canonical path back through
+// the tables (ball_pred_step, as the path stage walks): for the routes whose turn row cannot give it
+// -- a tie between the exits at the entry node (the canonical path may mix both exits' trees: a
+// source at a node whose route runs along its own road ties there), or a row without its sum.
+// x: the entry node (at `side` of road rb), r1 / r0: both exits' rows of rb.  ok false: no path.
+__device__ uint32_t ball_turn_walk(const DevGraph& g, const BallPathLabels& lab, const K2Turn& T, uint32_t rb,
+                                   uint32_t x, uint32_t side, uint4 r1, uint4 r0, bool& ok) {
+  const uint32_t acc = mode_access((int)T.mode);
+  uint32_t hs = head_start(g.road_head[rb], side);
+  unsigned long long lx = side ? ball_label(lab.rk1, row_key1(r1), lab.rk0, row_key1(r0))
+                               : ball_label(lab.rk1, row_key0(r1), lab.rk0, row_key0(r0));
+  uint32_t U = 0;
+  ok = true;
+  for (uint32_t guard = 0; guard <= 2u * kBallMaxKeysHost + 2u; ++guard) {
+    if (lx == kKeyInf) break;
+    if (x == T.n1 && lx == lab.rk1) return U + g.turn_w[turn_degree(head_back(T.hw, 0u), hs)];
+    if (x == T.n0 && lx == lab.rk0) return U + g.turn_w[turn_degree(head_back(T.hw, 1u), hs)];
+    uint4 rec;
+    unsigned long long plu;
+    if (!ball_pred_step(g, lab, acc, (int)T.mode, x, lx, r1, r0, side, rec, plu)) break;
+    const uint32_t hw = g.road_head[rec.z >> 1], rev = rec.z & 1u;
+    U += g.turn_w[turn_degree(head_back(hw, rev), hs)];
+    hs = head_start(hw, rev);
+    x = rec.y;
+    side = rev;   // the edge's start: node0 of its road when it runs forward
+    lab.rows(rec.z >> 1, r1, r0);
+    lx = side ? ball_label(lab.rk1, row_key1(r1), lab.rk0, row_key1(r0))
+              : ball_label(lab.rk1, row_key0(r1), lab.rk0, row_key0(r0));
+  }
+  ok = false;
+  return 0u;
+}
+
+// A route the tables answer in a batch with turn costs (rule 3b, TURN), and its distance term
+// d = turn_m + |route_m - gc| (route_term).  The turn weight: when one exit gives the entry node
+// its label strictly, that exit's turn row holds the weight of the path from the exit node on and
+// the heading it leaves the exit node with, and the turn at the exit node is from the source road;
+// otherwise (a tie, or a row without its sum) ball_turn_walk.
 __device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src& S, const K2Turn& T, const uint4& t0,
                                                   const uint4& t1, const uint4& r1, const uint4& r0, uint32_t s1,
-                                                  uint32_t s0, bool& exact, uint32_t& U) {
+                                                  uint32_t s0, double gc, bool& exact, double& d) {
   const unsigned long long k10 = row_key0(r1), k00 = row_key0(r0), k11 = row_key1(r1), k01 = row_key1(r0);
   const unsigned long long l10 = k10 != kKeyInf ? S.rk1 + k10 : kKeyInf, l00 = k00 != kKeyInf ? S.rk0 + k00 : kKeyInf;
   const unsigned long long l11 = k11 != kKeyInf ? S.rk1 + k11 : kKeyInf, l01 = k01 != kKeyInf ? S.rk0 + k01 : kKeyInf;
@@ -1573,22 +1683,29 @@ __device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src
   const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, &combo);
   exact = S.lim == kNone || (key != kKeyInf && key_dist(key) <= S.lim);
   const bool valid = key != kKeyInf && key_dist(key) <= S.bound && key_time(key) <= S.tmax;
-  U = 0u;
-  if (T.on && valid && combo >= 2) {
+  uint32_t U = 0u;
+  if (T.fac && valid && combo >= 2 && exact) {
     const uint32_t side = (uint32_t)combo - 2u;
     const unsigned long long la = side ? l11 : l10, lb = side ? l01 : l00;
-    if (la == lb) {
-      exact = false;
-    } else {
-      const bool e1 = la < lb;
+    uint32_t w = kTurnNone;
+    const bool e1 = la < lb;
+    if (la != lb) {
       const uint64_t row = e1 ? ball_row0(S.h1.x) + s1 : ball_row0(S.h0.x) + s0;
       const uint2 tw = reinterpret_cast<const uint2*>(T.trn)[row];
-      const uint32_t w = side ? tw.y : tw.x;
-      if ((w & kTurnTMask) == kTurnNone) exact = false;
-      else U = g.turn_w[turn_degree(head_back(T.hw, e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
+      w = side ? tw.y : tw.x;
+    }
+    if ((w & kTurnTMask) != kTurnNone) {
+      U = g.turn_w[turn_degree(head_back(T.hw, e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
+    } else {
+      const BallPathLabels lab{(const uint4*)S.ent, S.h1, S.h0, S.rk1, S.rk0, g.ball_road_mask};
+      bool ok = true;
+      U = ball_turn_walk(g, lab, T, t0.x, side ? t1.y : t1.x, side, r1, r0, ok);
+      if (!ok) exact = false;
     }
   }
-  return valid ? key_dist(key) : kRouteInvalid;
+  const uint32_t r = valid ? key_dist(key) : kRouteInvalid;
+  d = route_term(r, U, T.fac, gc);
+  return r;
 }
 
 template <bool TURN>
@@ -1632,10 +1749,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     bool turn_ok = true;
     if constexpr (TURN) {
       K2Turn T;
-      T.on = pi.w != 0u ? 1u : 0u;
+      T.fac = pi.w;
       T.trn = (unsigned long long)(uintptr_t)g.ball_turn[mode];
-      T.hw = T.on ? g.road_head[a0.x] : 0u;
-      turn_ok = !T.on || ((g.ball_turn_mask >> mode) & 1u);   // no turn rows: the search tiers weigh the turns
+      T.hw = T.fac ? g.road_head[a0.x] : 0u;
+      T.n0 = a1.x;
+      T.n1 = a1.y;
+      T.mode = (uint32_t)mode;
+      T.pad = 0u;
+      turn_ok = !T.fac || ((g.ball_turn_mask >> mode) & 1u);   // no turn rows: the search tiers weigh the turns
       sm.tsrc[threadIdx.x] = T;
     }
     if (!fits || S.h1.y == 0u || S.h0.y == 0u || !turn_ok) {   // the search tiers take it (they run later)
@@ -1704,16 +1825,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
       const K2Turn& TA = sm.tsrc[sm.owner[q]];
       const K2Turn& TB = sm.tsrc[sm.owner[qB]];
       if (la) {
-        uint32_t s1 = ball_slot(ta0.x, A.h1.y), s0 = ball_slot(ta0.x, A.h0.y), u = 0;
+        uint32_t s1 = ball_slot(ta0.x, A.h1.y), s0 = ball_slot(ta0.x, A.h0.y);
+        double d = 0.0;
         const uint4 r1 = ball_resolve_at(ga, A.h1, ta0.x, ea1, rm, s1), r0 = ball_resolve_at(ga, A.h0, ta0.x, ea0, rm, s0);
-        b.route[A.ob + (q - A.rel)] = k2_route_turn(g, A, TA, ta0, ta1, r1, r0, s1, s0, xa, u);
-        if (TA.on) b.route_turn[A.ob + (q - A.rel)] = u;
+        b.route[A.ob + (q - A.rel)] = k2_route_turn(g, A, TA, ta0, ta1, r1, r0, s1, s0, b.gc[A.tdesc / kMaxCand], xa, d);
+        b.route_d[A.ob + (q - A.rel)] = d;
       }
       if (lb) {
-        uint32_t s1 = ball_slot(tb0.x, B.h1.y), s0 = ball_slot(tb0.x, B.h0.y), u = 0;
+        uint32_t s1 = ball_slot(tb0.x, B.h1.y), s0 = ball_slot(tb0.x, B.h0.y);
+        double d = 0.0;
         const uint4 r1 = ball_resolve_at(gb, B.h1, tb0.x, eb1, rm, s1), r0 = ball_resolve_at(gb, B.h0, tb0.x, eb0, rm, s0);
-        b.route[B.ob + (qb - B.rel)] = k2_route_turn(g, B, TB, tb0, tb1, r1, r0, s1, s0, xb, u);
-        if (TB.on) b.route_turn[B.ob + (qb - B.rel)] = u;
+        b.route[B.ob + (qb - B.rel)] = k2_route_turn(g, B, TB, tb0, tb1, r1, r0, s1, s0, b.gc[B.tdesc / kMaxCand], xb, d);
+        b.route_d[B.ob + (qb - B.rel)] = d;
       }
     } else {
       if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm), xa);
@@ -1760,7 +1883,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
     continue;
   }
   route_targets(g, b, StoreLabel<RegLabels>{S}, SearchPathLabels<RegLabels>{S}, a0, p, KB, bound, tmax,
-                (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256, TurnCtx{a1, rk1, rk0, mode, TURN && pi.w != 0u});
+                (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256, TurnCtx{a1, rk1, rk0, mode, TURN, pi.w, TURN ? b.gc[p] : 0.0});
   }
 }
 
@@ -1796,7 +1919,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
     }
     route_targets(g, b, StoreLabel<RegLabelsT<kTier2Cap>>{S}, SearchPathLabels<RegLabelsT<kTier2Cap>>{S}, a0, p, KB,
                   bound, tmax, (uint64_t)base + i * KB, &s_res[0][threadIdx.x], 256,
-                  TurnCtx{a1, rk1, rk0, mode, pi.w != 0u && b.route_turn});
+                  TurnCtx{a1, rk1, rk0, mode, b.route_d != nullptr, pi.w, b.route_d ? b.gc[p] : 0.0});
   }
 }
 
@@ -1918,65 +2041,6 @@ __device__ __forceinline__ bool lane_path(const DevGraph& g, const DevBatch& b, 
   const unsigned long long key = route_key(StoreLabel<L>{S}, a0, b0, b1, &combo);
   path_walk(g, b, p, SearchPathLabels<L>{S}, mode, a0, a1, b0, b1, rk1, rk0, key, combo, cap);
   return true;
-}
-
-// labels from the route balls of the two exits (see k_routes_ball2)
-struct BallPathLabels {
-  const uint4* ent;
-  uint2 h1, h0;
-  unsigned long long rk1, rk0;
-  uint32_t rm;   // road-id bits of a row's first word
-  // both exits' rows of `road` (a dummy row for an unusable exit), first probes issued together
-  __device__ void rows(uint32_t road, uint4& r1, uint4& r0) const {
-    // both first probes issued together: an unusable exit reads row 0 (valid: the mode has
-    // tables) and its row is replaced by the empty row afterwards
-    const bool u1 = rk1 != kKeyInf, u0 = rk0 != kKeyInf;
-    const uint64_t i1 = u1 ? ball_row0(h1.x) + ball_slot(road, h1.y) : 0u;
-    const uint64_t i0 = u0 ? ball_row0(h0.x) + ball_slot(road, h0.y) : 0u;
-    const uint4 l1 = ent[i1], l0 = ent[i0];
-    const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
-    r1 = ball_resolve(ent, h1, road, u1 ? l1 : none, rm);
-    r0 = ball_resolve(ent, h0, road, u0 ? l0 : none, rm);
-  }
-  __device__ unsigned long long operator()(uint32_t, uint32_t road, uint32_t side) const {
-    uint4 r1, r0;
-    rows(road, r1, r0);
-    return side ? ball_label(rk1, row_key1(r1), rk0, row_key1(r0)) : ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
-  }
-};
-
-// One step of the ball-tier walk back from node x (label lx, rows r1/r0 of a road with x at
-// `side`): x's canonical predecessor in the two-exit search.  Where exactly one exit gives x
-// its label, the tight in-edges of the two-exit search are that exit's own and the canonical
-// one is the predecessor stored in its row; on a tie between the exits they are the union of
-// both, and the canonical one the smaller stored index (in_rec is in edge-id order).  Only
-// when that index was not stored (7 or more in-edges before it) are the in-edges scanned.
-// Returns false when no predecessor exists (not reached for a valid route).
-__device__ __forceinline__ bool ball_pred_step(const DevGraph& g, const BallPathLabels& lab, uint32_t acc, int mode,
-                                               uint32_t x, unsigned long long lx, const uint4& r1, const uint4& r0,
-                                               uint32_t side, uint4& rec, unsigned long long& plu) {
-  const uint32_t q0 = g.in_off[x];
-  const unsigned long long k1 = side ? row_key1(r1) : row_key0(r1), k0 = side ? row_key1(r0) : row_key0(r0);
-  uint32_t idx = kBallPredNone;
-  if (lab.rk1 != kKeyInf && k1 != kKeyInf && lab.rk1 + k1 == lx) idx = min(idx, ball_pred(r1.x, side, lab.rm));
-  if (lab.rk0 != kKeyInf && k0 != kKeyInf && lab.rk0 + k0 == lx) idx = min(idx, ball_pred(r0.x, side, lab.rm));
-  if (idx < kBallPredNone) {
-    rec = g.in_rec[q0 + idx];
-    plu = kKeyInf;   // the caller reads the predecessor's label from its rows
-    return true;
-  }
-  for (uint32_t q = q0, q1 = g.in_off[x + 1]; q < q1; ++q) {
-    const uint4 r = g.in_rec[q];
-    const uint32_t inf = g.in_info[q];
-    if (!edge_ok(inf, acc)) continue;
-    const unsigned long long lu = lab(r.y, r.z >> 1, r.z & 1u);
-    if (lu != kKeyInf && lu + make_key(r.w, time_ms_dev(r.w, mode_speed_dkph(mode, inf & 0xffffu))) == lx) {
-      rec = r;
-      plu = lu;
-      return true;
-    }
-  }
-  return false;
 }
 
 // path_walk for the ball tier: canonical predecessors from the rows (ball_pred_step), one
@@ -2180,9 +2244,10 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
                               SearchTargets{b.cand_desc + p * kMaxCand * 2, KB, b.search_delta});
   const bool ok = !sm.ovf;
   if (ok) {
-    const bool turn = pi.w != 0u && b.route_turn;
+    const bool turn = b.route_d != nullptr;   // the batch has turn costs: every route's distance term
     unsigned long long rk1 = kKeyInf, rk0 = kKeyInf;
-    if (turn) exit_keys(s_src[0], bound, rk1, rk0);
+    double gcp = 0.0;
+    if (turn) { exit_keys(s_src[0], bound, rk1, rk0); gcp = b.gc[p]; }
     for (uint32_t j = lane; j < KB; j += W) {
       const uint4 t0 = b.cand_desc[(p * kMaxCand + j) * 2], t1 = b.cand_desc[(p * kMaxCand + j) * 2 + 1];
       int combo = -1;
@@ -2192,11 +2257,12 @@ __device__ bool routes_search_item(SearchSmem<H, false>& sm, uint4* s_src, const
       b.route[base + i * KB + j] = out;
       if (turn) {   // the route's turn weight (rule 3b) from the same labels
         bool wok = true;
-        const uint32_t u = out == kRouteInvalid ? 0u
-                                                : search_turn_walk(g, HashPathLabel<H, false>{sm}, mode, s_src[0], s_src[1],
-                                                                   t0, t1, rk1, rk0, combo, wok);
+        const uint32_t u = (out == kRouteInvalid || !pi.w)
+                               ? 0u
+                               : search_turn_walk(g, HashPathLabel<H, false>{sm}, mode, s_src[0], s_src[1], t0, t1, rk1, rk0,
+                                                  combo, wok);
         if (!wok) trace_fail(b, p, kErrRounds);
-        b.route_turn[base + i * KB + j] = u;
+        b.route_d[base + i * KB + j] = route_term(out, u, pi.w, gcp);
       }
     }
   }
@@ -2327,41 +2393,36 @@ __device__ __forceinline__ double row_bcast(double v) {
 // prevK in the last block need no guard: lanes i >= prevK hold cj = +inf (every layer sets
 // cost +inf past its KB), and +inf (or NaN from the unstaged LDS they read) never wins.
 template <int I, bool TURN>
-__device__ __forceinline__ void vit_src(double& best, int& arg, double cj, double rm, double tm, double gcl, double inv_beta) {
+__device__ __forceinline__ void vit_src(double& best, int& arg, double cj, double rm, double gcl, double inv_beta) {
   // fma(|route_m - gc|, 1/beta, cost of source i): one rounding, as the oracle's fma; an
-  // invalid route is +inf and stays +inf.  With turn costs (rule 3b) the route's turn cost in
-  // metres is added to |route_m - gc| first, as the oracle does.
-  const double d = TURN ? tm + fabs(rm - gcl) : fabs(rm - gcl);
+  // invalid route is +inf and stays +inf.  With turn costs (rule 3b) the staged value is the
+  // distance term turn_m + |route_m - gc| itself (route_d, formed by K2 as the oracle forms it).
+  const double d = TURN ? rm : fabs(rm - gcl);
   const double c = __builtin_fma(d, inv_beta, row_bcast<I>(cj));
   const bool take = c < best;
   best = __builtin_fmin(best, c);   // = c exactly when take (no NaN reaches here, costs >= 0)
   arg = take ? I : arg;
 }
 template <int B, bool TURN>
-__device__ __forceinline__ void vit_min(double& best, int& arg, double cj, const double* dp, const double* tp, uint32_t KB,
-                                        uint32_t prevK, double gcl, double inv_beta, const double (&rm0)[4],
-                                        const double (&tm0)[4]) {
+__device__ __forceinline__ void vit_min(double& best, int& arg, double cj, const double* dp, uint32_t KB,
+                                        uint32_t prevK, double gcl, double inv_beta, const double (&rm0)[4]) {
   if constexpr (B < 4) {
     if ((uint32_t)(4 * B) < prevK) {
-      double rm[4], tm[4] = {0.0, 0.0, 0.0, 0.0};
+      double rm[4];
       if constexpr (B == 0) {   // block 0 was loaded at the end of the previous layer
 #pragma unroll
-        for (int x = 0; x < 4; ++x) { rm[x] = rm0[x]; tm[x] = tm0[x]; }
+        for (int x = 0; x < 4; ++x) rm[x] = rm0[x];
       } else {
 #pragma unroll
         for (int x = 0; x < 4; ++x) rm[x] = dp[(4 * B + x) * KB];   // past prevK: never selected
-        if constexpr (TURN) {
-#pragma unroll
-          for (int x = 0; x < 4; ++x) tm[x] = tp[(4 * B + x) * KB];
-        }
 #pragma unroll
         for (int x = 0; x < 4; ++x) __asm__ volatile("" : "+v"(rm[x]));   // keep the loads together
       }
-      vit_src<4 * B + 0, TURN>(best, arg, cj, rm[0], tm[0], gcl, inv_beta);
-      vit_src<4 * B + 1, TURN>(best, arg, cj, rm[1], tm[1], gcl, inv_beta);
-      vit_src<4 * B + 2, TURN>(best, arg, cj, rm[2], tm[2], gcl, inv_beta);
-      vit_src<4 * B + 3, TURN>(best, arg, cj, rm[3], tm[3], gcl, inv_beta);
-      vit_min<B + 1, TURN>(best, arg, cj, dp, tp, KB, prevK, gcl, inv_beta, rm0, tm0);
+      vit_src<4 * B + 0, TURN>(best, arg, cj, rm[0], gcl, inv_beta);
+      vit_src<4 * B + 1, TURN>(best, arg, cj, rm[1], gcl, inv_beta);
+      vit_src<4 * B + 2, TURN>(best, arg, cj, rm[2], gcl, inv_beta);
+      vit_src<4 * B + 3, TURN>(best, arg, cj, rm[3], gcl, inv_beta);
+      vit_min<B + 1, TURN>(best, arg, cj, dp, KB, prevK, gcl, inv_beta, rm0);
     }
   }
 }
@@ -2453,23 +2514,20 @@ __device__ __forceinline__ VitLayerDesc vit_describe(const DevBatch& b, uint32_t
   return d;
 }
 
-// TURN: the batch has turn costs (rule 3b); each group also stages its chunk's turn costs in
-// metres (route_turn x factor / 65536), in an array padded so the unclamped prefetch stays inside
+// TURN: the batch has turn costs (rule 3b): the chunk stages each route's distance term route_d
+// (turn_m + |route_m - gc|, formed by K2) instead of its metres
 template <bool TURN>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_WPE))) k_viterbi(DevBatch b) {
   __shared__ VitGroup smem[4];
-  __shared__ double s_turn[TURN ? 4 : 1][TURN ? kVitRoutes + 64 : 1];
   const int lane = threadIdx.x;
   const int j = lane & 15, gb = lane & 48;
   VitGroup& gs = smem[lane >> 4];
-  double* const turn_m = &s_turn[TURN ? (lane >> 4) : 0][0];
   const uint32_t k = blockIdx.x * 4 + (lane >> 4);
   const bool active = k < b.T;
   const uint32_t o = active ? b.trace_off[k] : 0u, S = active ? b.n_states[k] : 0u;
   const MatchOptions op = b.opts[active ? b.trace_opt[k] : 0u];
   const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
   const double inv_beta = 1.0 / (double)op.beta;
-  const double tscale = (double)op.turn_penalty_factor * 0x1p-16;   // metres per unit of turn weight
   const double brk = (double)op.breakage_distance;
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   bool prev_ok = false;
@@ -2500,15 +2558,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     const uint32_t nroutes = C ? (uint32_t)__shfl(incl, (int)C - 1, 16) : 0u;
     const uint32_t rbase = (uint32_t)__shfl(dq.off, 0, 16);                   // routes of layer s0 start here
     // ---- coalesced loads of the chunk's routes and emission rows
-    uint32_t rv[kVitRoutes / 16], tv[TURN ? kVitRoutes / 16 : 1];
+    uint32_t rv[TURN ? 1 : kVitRoutes / 16];
+    double dv[TURN ? kVitRoutes / 16 : 1];
     const uint32_t rlast = nroutes ? nroutes - 1u : 0u;
-#pragma unroll
-    for (int x = 0; x < kVitRoutes / 16; ++x)
-      if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
     if constexpr (TURN) {
 #pragma unroll
       for (int x = 0; x < kVitRoutes / 16; ++x)
-        if (16u * x < nroutes) tv[x] = b.route_turn[rbase + min((uint32_t)j + 16u * x, rlast)];
+        if (16u * x < nroutes) dv[x] = b.route_d[rbase + min((uint32_t)j + 16u * x, rlast)];
+    } else {
+#pragma unroll
+      for (int x = 0; x < kVitRoutes / 16; ++x)
+        if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
     }
     // emission rows (16 floats per layer), four float4 per lane, clamped to the chunk
     const uint64_t f0 = C ? (uint64_t)(o + s0) * (kMaxCand / 4) : 0u;
@@ -2521,13 +2581,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     // ---- descriptor of the next chunk (its loads overlap this chunk's work)
     if (live && s0 + C < S) dq = vit_describe(b, o, S, s0 + C, j);
     // ---- chunk -> LDS
-#pragma unroll
-    for (int x = 0; x < kVitRoutes / 16; ++x)
-      if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
     if constexpr (TURN) {
 #pragma unroll
       for (int x = 0; x < kVitRoutes / 16; ++x)
-        if ((uint32_t)j + 16u * x < nroutes) turn_m[j + 16 * x] = (double)tv[x] * tscale;
+        if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = dv[x];
+    } else {
+#pragma unroll
+      for (int x = 0; x < kVitRoutes / 16; ++x)
+        if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
     }
     {
       float4* sqdst = reinterpret_cast<float4*>(&gs.sq[0][0]);
@@ -2550,16 +2611,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     uint32_t KBn = gs.kb[0], reln = gs.rel[0];
     double gcn = gs.gc[0];
     float sqn = gs.sq[0][j];
-    double rmn[4], tmn[4] = {0.0, 0.0, 0.0, 0.0};
+    double rmn[4];
     {
-      const uint32_t o0 = reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
-      const double* dp = gs.route_m + o0;
+      const double* dp = gs.route_m + reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
 #pragma unroll
       for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
-      if constexpr (TURN) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x) tmn[x] = turn_m[o0 + x * KBn];
-      }
     }
     // ---- the layers of the chunk, in order, out of LDS.  The body is branch-free for the common
     // layer: the recurrence over the first four sources runs for every group (a group that starts
@@ -2571,9 +2627,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       const uint32_t KB = KBn, rel = reln;
       const double gcl = gcn;
       const float sqv = sqn;
-      double rm0[4], tm0[4];
+      double rm0[4];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) { rm0[x] = rmn[x]; tm0[x] = tmn[x]; }
+      for (int x = 0; x < 4; ++x) rm0[x] = rmn[x];
       {   // next layer's parameters, unconditionally (past the chunk: stale entries, never used)
         const uint32_t tn = min(t + 1u, (uint32_t)kVitChunk - 1u);
         KBn = gs.kb[tn]; reln = gs.rel[tn]; gcn = gs.gc[tn]; sqn = gs.sq[tn][j];
@@ -2585,16 +2641,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       int arg = -1;
       {
         const uint32_t jj = min((uint32_t)j, KB ? KB - 1u : 0u);
-        const uint32_t o1 = min(rel, (uint32_t)kVitRoutes - 1u) + jj;
-        const double* dp = gs.route_m + o1;
-        const double* tp = turn_m + (TURN ? o1 : 0u);
-        vit_src<0, TURN>(best, arg, cj, rm0[0], tm0[0], gcl, inv_beta);
-        vit_src<1, TURN>(best, arg, cj, rm0[1], tm0[1], gcl, inv_beta);
-        vit_src<2, TURN>(best, arg, cj, rm0[2], tm0[2], gcl, inv_beta);
-        vit_src<3, TURN>(best, arg, cj, rm0[3], tm0[3], gcl, inv_beta);
+        const double* dp = gs.route_m + min(rel, (uint32_t)kVitRoutes - 1u) + jj;
+        vit_src<0, TURN>(best, arg, cj, rm0[0], gcl, inv_beta);
+        vit_src<1, TURN>(best, arg, cj, rm0[1], gcl, inv_beta);
+        vit_src<2, TURN>(best, arg, cj, rm0[2], gcl, inv_beta);
+        vit_src<3, TURN>(best, arg, cj, rm0[3], gcl, inv_beta);
         if (__ballot(in && prevK > 4u) != 0ull) {   // wave-uniform: sources 4.. of some group
           const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
-          vit_min<1, TURN>(best, arg, cj, dp, tp, kbs, prevK, gcl, inv_beta, rm0, tm0);
+          vit_min<1, TURN>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
         }
       }
       const bool valid_j = j < (int)KB;
@@ -2611,12 +2665,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
           backtrace_chain(b, gs, o, s0 + t - 1, prevK, j, cj);
         }
         // the backtrace staged through route_m: bring the chunk's routes back
+        if constexpr (TURN) {
 #pragma unroll
-        for (int x = 0; x < kVitRoutes / 16; ++x)
-          if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
+          for (int x = 0; x < kVitRoutes / 16; ++x)
+            if (16u * x < nroutes) dv[x] = b.route_d[rbase + min((uint32_t)j + 16u * x, rlast)];
 #pragma unroll
-        for (int x = 0; x < kVitRoutes / 16; ++x)
-          if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
+          for (int x = 0; x < kVitRoutes / 16; ++x)
+            if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = dv[x];
+        } else {
+#pragma unroll
+          for (int x = 0; x < kVitRoutes / 16; ++x)
+            if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
+#pragma unroll
+          for (int x = 0; x < kVitRoutes / 16; ++x)
+            if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
+        }
         wave_sync();
       }
       {   // next layer's first route rows (after any re-staging above).  Lanes past K_B and stale
@@ -2626,10 +2689,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         const uint32_t kbs = min(KBn, (uint32_t)kMaxCand);
 #pragma unroll
         for (int x = 0; x < 4; ++x) rmn[x] = dp[x * kbs];
-        if constexpr (TURN) {   // the padded turn array: reln + j + 3 x 16 < kVitRoutes + 64
-#pragma unroll
-          for (int x = 0; x < 4; ++x) tmn[x] = turn_m[reln + j + x * kbs];
-        }
       }
       // em is +inf past K_B (and for every lane of an empty layer, which also has `start`), and
       // best is +inf where no source reached the lane, so best + em needs no further selects
@@ -2764,12 +2823,12 @@ __device__ __forceinline__ void v3_stage_routes(Vit3Smem& sm, const V3Chunk& c, 
     if ((uint32_t)(lane + kWave * x) < c.nroutes) sm.route_m[lane + kWave * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
 }
 
-// turn costs in metres of the chunk's routes (rule 3b), loaded when the chunk is staged (the
-// small-batch kernel with turn costs; [kV3Routes] is the idle lanes' 0)
-__device__ __forceinline__ void v3_stage_turns(double* turn_m, const DevBatch& b, const V3Chunk& c, int lane, double tscale) {
+// with turn costs (rule 3b): the chunk's distance terms route_d (turn_m + |route_m - gc|, +inf
+// when invalid) in place of its metres, loaded when the chunk is staged
+__device__ __forceinline__ void v3_stage_terms(Vit3Smem& sm, const DevBatch& b, const V3Chunk& c, int lane) {
 #pragma unroll
   for (int x = 0; x < kV3Regs; ++x)
-    if ((uint32_t)(lane + kWave * x) < c.nroutes) turn_m[lane + kWave * x] = (double)b.route_turn[c.rbase + lane + kWave * x] * tscale;
+    if ((uint32_t)(lane + kWave * x) < c.nroutes) sm.route_m[lane + kWave * x] = b.route_d[c.rbase + lane + kWave * x];
 }
 
 // back-pointer rows / chain flags of chunk layers [0, n) to HBM
@@ -2822,9 +2881,9 @@ __device__ void v3_backtrace(const DevBatch& b, Vit3Smem& sm, uint32_t o, uint32
 // one pass of layer t over targets [j0, j0 + 64/W): lane = (target j0 + lane/W, source lane%W);
 // heads (source lane 0) write the target's new cost and back-pointer byte
 template <int W, bool TURN>
-__device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, const double* turn_m, int lane, uint32_t j0, uint32_t KB,
-                                                      uint32_t KA, uint32_t rel, double gcl, double inv_beta, double inv2s2,
-                                                      int cb, uint32_t t) {
+__device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, int lane, uint32_t j0, uint32_t KB, uint32_t KA,
+                                                      uint32_t rel, double gcl, double inv_beta, double inv2s2, int cb,
+                                                      uint32_t t) {
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   const uint32_t i = (uint32_t)lane & (W - 1), j = j0 + ((uint32_t)lane / W);
   const bool valid = i < KA && j < KB;
@@ -2832,9 +2891,9 @@ __device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, const double
   const double rm = sm.route_m[at];
   const double ci = sm.cost[cb][i];
   // fma(|route_m - gc|, 1/beta, cost of source i): one rounding, as the oracle; an invalid
-  // route, an unreachable source and an idle lane are +inf.  Turn costs (rule 3b) are added to
-  // |route_m - gc| first.
-  const double d = TURN ? turn_m[at] + fabs(rm - gcl) : fabs(rm - gcl);
+  // route, an unreachable source and an idle lane are +inf.  With turn costs (rule 3b) the staged
+  // value is the distance term itself.
+  const double d = TURN ? rm : fabs(rm - gcl);
   const double c = __builtin_fma(d, inv_beta, ci);
   const double m = group_min<W>(c);
   const unsigned long long eq = __ballot(c == m && m < INF);
@@ -2852,15 +2911,12 @@ __device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, const double
 template <bool TURN>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3_WPE))) k_viterbi_w(DevBatch b) {
   __shared__ Vit3Smem sm;
-  __shared__ double s_turn[TURN ? kV3Routes + 2 : 1];   // turn costs (metres) of the staged routes
   const int lane = threadIdx.x;
   const uint32_t k = blockIdx.x;
   const uint32_t o = b.trace_off[k], S = b.n_states[k];
   const MatchOptions op = b.opts[b.trace_opt[k]];
   const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
   const double inv_beta = 1.0 / (double)op.beta;
-  const double tscale = (double)op.turn_penalty_factor * 0x1p-16;
-  if (TURN && lane == 0) s_turn[kV3Routes] = 0.0;
   const double brk = (double)op.breakage_distance;
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   if (lane < 2 * kMaxCand) (&sm.cost[0][0])[lane] = INF;
@@ -2877,8 +2933,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
   uint32_t prevK = 0;
   int cb = 0;
   for (;;) {
-    v3_stage_routes(sm, cur, lane, rv);
-    if constexpr (TURN) v3_stage_turns(s_turn, b, cur, lane, tscale);
+    if constexpr (TURN) v3_stage_terms(sm, b, cur, lane);
+    else v3_stage_routes(sm, cur, lane, rv);
     if ((uint32_t)lane < cur.C * (kMaxCand / 4)) reinterpret_cast<float4*>(&sm.sq[0][0])[lane] = sv;
     // the next chunk's routes and emission rows load while this chunk runs
     const uint32_t s1 = cur.s0 + cur.C;
@@ -2902,13 +2958,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
       if (KB && !start) {
         unsigned long long any = 0ull;
         if (prevK <= 4u) {
-          any = v3_pass<4, TURN>(sm, s_turn, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          any = v3_pass<4, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
         } else if (prevK <= 8u) {
-          any = v3_pass<8, TURN>(sm, s_turn, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
-          if (KB > 8u) any |= v3_pass<8, TURN>(sm, s_turn, lane, 8u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          any = v3_pass<8, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          if (KB > 8u) any |= v3_pass<8, TURN>(sm, lane, 8u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
         } else {
           for (uint32_t j0 = 0; j0 < KB; j0 += 4u)
-            any |= v3_pass<16, TURN>(sm, s_turn, lane, j0, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+            any |= v3_pass<16, TURN>(sm, lane, j0, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
         }
         if (any == 0ull) start = true;   // no valid transition into this layer
       }
@@ -2927,7 +2983,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
             rr[x] = kRouteInvalid;
             if ((uint32_t)(kWave * x) < cur.nroutes) rr[x] = rp[min((uint32_t)(lane + kWave * x), rlast)];
           }
-          v3_stage_routes(sm, cur, lane, rr);
+          if constexpr (TURN) v3_stage_terms(sm, b, cur, lane);
+          else v3_stage_routes(sm, cur, lane, rr);
         }
       }
       if (KB == 0) {
@@ -2971,7 +3028,7 @@ void launch_viterbi(uint32_t T, hipStream_t st, const DevBatch& v) {
     const char* e = std::getenv("RM_VIT_WAVE_MAX");
     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)RM_VIT_WAVE_MAX;
   }();
-  const bool turn = v.route_turn != nullptr;   // the batch has turn costs (rule 3b)
+  const bool turn = v.route_d != nullptr;   // the batch has turn costs (rule 3b)
   if (T <= wave_max) {
     if (turn) hipLaunchKernelGGL(k_viterbi_w<true>, dim3(T), dim3(64), 0, st, v);
     else hipLaunchKernelGGL(k_viterbi_w<false>, dim3(T), dim3(64), 0, st, v);
@@ -4343,7 +4400,7 @@ void Workspace::release() {
   allocs.clear();
   cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = cap_src = cap_sort = cap_turn = 0;
   perm = loc_cursor = pcnt = nullptr;
-  route_turn = nullptr;
+  route_d = nullptr;
   loc_key = nullptr;
 }
 
@@ -4448,7 +4505,7 @@ void Matcher::alloc_points(uint64_t cp, uint64_t ct, uint64_t co, uint64_t keep_
     w.tot_part = dalloc<unsigned long long>(L, 2 * ((cp + 255) / 256) + 2);
     w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
     w.gsearch = nullptr;
-    w.route = nullptr; w.route_turn = nullptr; w.cap_turn = 0; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
+    w.route = nullptr; w.route_d = nullptr; w.cap_turn = 0; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
     w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
     ensure_trans_raw(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
     ensure_path_raw(std::max<uint64_t>(keep_path, cp / 8 + 1024));
@@ -4466,16 +4523,16 @@ void Matcher::ensure_trans(uint64_t n, uint64_t n_src) { grow_workspace([&] { en
 void Matcher::ensure_path(uint64_t n) { grow_workspace([&] { ensure_path_raw(n); }); }
 void Matcher::ensure_segs(uint64_t n) { grow_workspace([&] { ensure_segs_raw(n); }); }
 
-// route_turn (turn weights of the transitions, K2 -> K3) for batches with turn costs: sized with
-// route, allocated the first time a batch needs it
+// route_d (the transitions' distance terms with turn costs, K2 -> K3) for batches with turn costs:
+// sized with route, allocated the first time a batch needs it
 void Matcher::ensure_turns() {
   grow_workspace([&] {
     Workspace& w = ws_;
-    if (w.route_turn && w.cap_turn >= w.cap_trans) return;
-    free_one(w, w.route_turn);
-    w.route_turn = nullptr;
+    if (w.route_d && w.cap_turn >= w.cap_trans) return;
+    free_one(w, w.route_d);
+    w.route_d = nullptr;
     w.cap_turn = 0;
-    w.route_turn = dalloc<uint32_t>(w.allocs, w.cap_trans);
+    w.route_d = dalloc<double>(w.allocs, w.cap_trans);
     w.cap_turn = w.cap_trans;
   });
 }
@@ -4485,9 +4542,9 @@ void Matcher::ensure_trans_raw(uint64_t n, uint64_t n_src) {
     Workspace& w = ws_;
     if (!(n <= w.cap_trans && w.route)) {
       free_one(w, w.route);
-      free_one(w, w.route_turn);
+      free_one(w, w.route_d);
       w.route = nullptr;
-      w.route_turn = nullptr;
+      w.route_d = nullptr;
       w.cap_trans = 0;
       w.cap_turn = 0;
       const uint64_t c = n + n / 4 + 1024;
@@ -4598,7 +4655,7 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig; v.state_time = w.state_time;
   v.cand_n = w.cand_n; v.cand_desc = w.cand_desc; v.cand_sq = w.cand_sq;
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
-  v.route_turn = nullptr;   // run_device sets it for a batch with turn costs
+  v.route_d = nullptr;   // run_device sets it for a batch with turn costs
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
@@ -4932,9 +4989,9 @@ void Matcher::run_device(const RunParams& rp) {
   n_trans_ = total;
   ensure_trans(total, n_src);
   v.route = w.route;
-  if (turn_mask_) {   // turn weights of the transitions (rule 3b), read by K3
+  if (turn_mask_) {   // the transitions' distance terms with turn costs (rule 3b), read by K3
     ensure_turns();
-    v.route_turn = w.route_turn;
+    v.route_d = w.route_d;
   }
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a;
@@ -4948,20 +5005,20 @@ void Matcher::run_device(const RunParams& rp) {
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
   if (n_src && balls) {
-    if (v.route_turn)
+    if (v.route_d)
       hipLaunchKernelGGL(k_routes_ball2<true>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
                          g, v, (uint32_t)n_src);
     else
       hipLaunchKernelGGL(k_routes_ball2<false>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
                          g, v, (uint32_t)n_src);
-    if (v.route_turn)
+    if (v.route_d)
       hipLaunchKernelGGL(k_routes_lane<true>, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)), dim3(256),
                          0, st, g, v, 0u, 1);
     else
       hipLaunchKernelGGL(k_routes_lane<false>, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)),
                          dim3(256), 0, st, g, v, 0u, 1);
   } else if (n_src) {
-    if (v.route_turn)
+    if (v.route_d)
       hipLaunchKernelGGL(k_routes_lane<true>, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
     else
       hipLaunchKernelGGL(k_routes_lane<false>, dim3((uint32_t)((n_src + 255) / 256)), dim3(256), 0, st, g, v, (uint32_t)n_src, 0);
@@ -5144,11 +5201,11 @@ void Matcher::get_routes(uint32_t* trans_off, double* gc, uint32_t* route) {
   RM_HIP(hipMemcpy(gc, ws_.gc, n_points_ * 8, hipMemcpyDeviceToHost));
   if (n_trans_) RM_HIP(hipMemcpy(route, ws_.route, n_trans_ * 4, hipMemcpyDeviceToHost));
 }
-void Matcher::get_route_turns(uint32_t* out) {
+int Matcher::get_route_terms(double* out) {
   sync();
-  if (!n_trans_) return;
-  if (turn_mask_ && ws_.route_turn) RM_HIP(hipMemcpy(out, ws_.route_turn, n_trans_ * 4, hipMemcpyDeviceToHost));
-  else std::memset(out, 0, n_trans_ * 4);
+  if (!turn_mask_ || !ws_.route_d) return 0;
+  if (n_trans_) RM_HIP(hipMemcpy(out, ws_.route_d, n_trans_ * 8, hipMemcpyDeviceToHost));
+  return 1;
 }
 void Matcher::get_viterbi(int8_t* choice, uint8_t* chain_start) {
   sync();

@@ -127,7 +127,7 @@ struct Workspace {
   // (sp* = mode-capped speed of the directed edge in 0.1 km/h, 0 when the mode cannot use it)
   uint8_t* cand_n = nullptr; uint4* cand_desc = nullptr; float* cand_sq = nullptr;
   uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr;
-  uint32_t* route_turn = nullptr;   // per transition: turn weight U (rule 3b), batches with turn costs only
+  double* route_d = nullptr;   // per transition: turn_m + |route_m - gc| (rule 3b), batches with turn costs only
   uint64_t cap_turn = 0;
   uint4* pair_info = nullptr;  // per layer pair slot: {route bound cm, time bound ms, KA | KB << 8 | mode << 16, 0}
   uint32_t* src_cnt = nullptr; uint32_t* src_off = nullptr; uint32_t* src_item = nullptr;
@@ -277,7 +277,8 @@ class Matcher {
   void get_states(uint32_t* n_states, uint32_t* state_orig);
   void get_candidates(uint8_t* cand_n, uint32_t* road, uint32_t* s_cm, float* sq);
   void get_routes(uint32_t* trans_off, double* gc, uint32_t* route);
-  void get_route_turns(uint32_t* route_turn);   // n_trans() words (0 without turn costs)
+  // the distance terms K3 used (n_trans() doubles); 0 (nothing written) when the batch had no turn costs
+  int get_route_terms(double* route_d);
   void get_viterbi(int8_t* choice, uint8_t* chain_start);
   void get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, uint32_t* route_dist);
   // segments compacted per trace: seg_off (T+1), segs (seg_off[T])
@@ -374,7 +375,7 @@ class Matcher {
   StageBufs sb_;
   bool from_points_ = false;
   uint32_t mode_mask_ = 0;   // travel modes of the batch (bit per Mode): which route balls K2 needs
-  uint32_t turn_mask_ = 0;   // modes of the batch with a turn_penalty_factor > 0: turn rows, route_turn
+  uint32_t turn_mask_ = 0;   // modes of the batch with a turn_penalty_factor > 0: turn rows, route_d
   void ensure_points(uint64_t n, uint32_t n_uuids, uint32_t n_opts);
   void ensure_rows(uint64_t n, uint32_t traces);
   struct Ev { hipEvent_t a, b; int k; };

@@ -278,12 +278,15 @@ class BatchMatcher:
         _lib.check(_lib.lib().rm_runner_get_routes(self._h, off.ctypes.data, gc.ctypes.data, route.ctypes.data))
         return off, gc, route[: sz["transitions"]]
 
-    def route_turns(self):
-        """Turn weight U of every transition (DESIGN.md §3 rule 3b; zeros without turn costs)."""
+    def route_terms(self):
+        """With turn costs (DESIGN.md §3 rule 3b): every transition's distance term turn_m +
+        |route_m - gc| (metres, inf when invalid) as the Viterbi adds it; None when the last run
+        had no turn costs."""
         n = self.sizes()["transitions"]
-        out = np.empty(max(n, 1), np.uint32)
-        _lib.check(_lib.lib().rm_runner_get_route_turns(self._h, out.ctypes.data))
-        return out[:n]
+        out = np.empty(max(n, 1), np.float64)
+        present = C.c_int(0)
+        _lib.check(_lib.lib().rm_runner_get_route_terms(self._h, out.ctypes.data, C.byref(present)))
+        return out[:n] if present.value else None
 
     def viterbi(self):
         P = self.sizes()["points"]
