@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--json-traces", type=int, default=10000, help="traces sent through rm_match_batch as JSON")
     ap.add_argument("--ball-radius", type=float, default=None,
                     help="route-ball radius in m (default: the config's, else the engine's automatic radius)")
+    ap.add_argument("--turn-penalty", type=float, default=0.0,
+                    help="turn_penalty_factor of every trace (meili's stock auto default is 200; DESIGN.md rule 3b); "
+                         "the default C2 run also measures the workload at 200 beside the value (turn_costs)")
     ap.add_argument("--traffic-json", default=None,
                     help="rocprofv3 PMC summary giving HBM bytes per stage launch (scripts/pmc_summary.py; default "
                          "profiles/r03/pmc_routes_<config>.json; used only when it was measured on this engine.hip "
@@ -460,6 +463,12 @@ def main():
         trace_opt = np.concatenate(tos)
     else:
         tr = W.generate_traces(gpath, 0, cfg["n_points"], cfg["rate_s"], cfg["noise_m"], seed=1000, ids=ids)
+    if a.turn_penalty > 0:   # meili's turn costs on every trace (rule 3b)
+        from reporter_amd import engine as E
+        if opts_all is None:
+            opts_all = E.default_options(1, search_radius=cfg["search_radius"])
+            trace_opt = np.zeros(len(ids), np.uint32)
+        opts_all["turn_penalty_factor"] = a.turn_penalty
     P = int(tr["trace_off"][-1])
     T = len(ids)
 
@@ -571,6 +580,26 @@ def main():
         dur_sum = int(comm.allreduce_host(float(dv[rank * cd:(rank + 1) * cd].sum()), dist.SUM))
     balls = eng.ball_stats(0)
     tiers = bm.route_tiers()
+    # the C2 workload with meili's stock auto turn costs (200, rule 3b), beside the value: the same
+    # points re-run with the factor on every trace, K2 timed live as in the official step
+    turn = None
+    if a.config == "C2" and world == 1 and a.turn_penalty == 0 and a.streams == 1 and not a.no_extras:
+        topts = engine.default_options(1, search_radius=cfg["search_radius"], turn_penalty_factor=200.0)
+        bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], topts, None, **rp)
+        for _ in range(a.warmup):
+            step()
+        bm.set_timing_stages(("routes",))
+        bm.reset_times()
+        t_turn = timed(step, a.steps, comm, sync)
+        kt_turn = bm.kernel_times()
+        bm.set_timing(True)
+        bm.reset_times()
+        timed(lambda: bm.rerun(**rp), a.steps, comm, sync)
+        kt_turn_all = bm.kernel_times()
+        bm.set_timing(False)
+        turn = {"t": t_turn, "routes_ms": kt_turn["routes"][0] / max(a.steps, 1),
+                "stages_ms": {k: v[0] / max(a.steps, 1) for k, v in kt_turn_all.items()},
+                "tiers": bm.route_tiers(), "turn_rows_built": eng.turn_rows()}
 
     out = None
     if rank == 0:
@@ -580,7 +609,10 @@ def main():
         ball_tier = balls["radius_m"] > 0 and balls["keys"] > 0
         # bytes of the formulation the launch runs: route-ball probes (every item answered by
         # the tables when nothing was handed over), else the bounded searches
-        if counts and ball_tier and tiers["ball_to_search"] == 0:
+        if counts and ball_tier and tiers["ball_to_search"] == 0 and a.turn_penalty > 0:
+            abytes = mo.routes_ball_turn_algorithmic_bytes(counts)
+            formulation = "route-ball table probes + turn rows (turn_penalty_factor %g)" % a.turn_penalty
+        elif counts and ball_tier and tiers["ball_to_search"] == 0:
             abytes, formulation = mo.routes_ball_algorithmic_bytes(counts), "route-ball table probes"
         elif counts and "settled_to_targets" in counts:
             abytes = mo.routes_targets_algorithmic_bytes(counts)
@@ -673,6 +705,18 @@ def main():
             "histogram_total": hist_sum,
             "duration_sum_total_s": dur_sum,
         }
+        if turn is not None:
+            kt2 = roofline("K2", "K2 route stage with turn costs: k_src_items + k_routes_ball2<turn> (turn rows, ties "
+                           "walked through the tables) + search tiers for hand-overs",
+                           mo.routes_ball_turn_algorithmic_bytes(counts) if counts and "turn_rows" in counts else None,
+                           turn["routes_ms"], "route-ball table probes + turn rows")
+            out["turn_costs"] = {
+                "what": "the same C2 points with meili's stock auto turn_penalty_factor 200 on every trace "
+                        "(valhalla_build_config's default, reference Dockerfile:42-49; DESIGN.md rule 3b): match + "
+                        "all-reduce per step, K2 timed live",
+                "value": total_points * a.steps / turn["t"], "unit": "points/s", "ms_per_step": turn["t"] / steps * 1e3,
+                "turn_penalty_factor": 200.0, "roofline": kt2, "kernels_ms_per_step": turn["stages_ms"],
+                "route_tiers": turn["tiers"], "turn_rows": turn["turn_rows_built"]}
         if comm_note:
             out["comm_note"] = comm_note
         if cpu:

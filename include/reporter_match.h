@@ -179,6 +179,8 @@ int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]);
  * chosen at upload to minimise the items a default-radius query reads (RM_GRID_SPLIT overrides).
  * It changes which grid items are read, never which roads are found. */
 int rm_engine_grid_split(const rm_engine* e, uint32_t* f);
+/* turn rows (DESIGN.md §3 rule 3b) built so far: bit per travel mode, and each mode's build ms */
+int rm_engine_turn_rows(const rm_engine* e, uint32_t* mode_mask, double* build_ms /*5*/);
 /* Host-only: the grid refinement an engine would choose for a graph file. */
 int rm_graph_grid_split(const char* graph_path, uint32_t* f);
 /* The engine's own tables of `mode` (built by a run that used the mode), probed on the device as

@@ -230,8 +230,9 @@ static uint64_t mk(uint32_t d, uint32_t t) { return ((uint64_t)d << 32) | t; }
  *      their targets (engine.hip SearchTargets): label-setting order settles nodes by key, and a
  *      search that stops once every target's route key is below the next key settles exactly the
  *      nodes with keys <= the largest target route key (all of them when a target is unreached)
- * [20] transitions whose turn weight is read from a turn row (turn_penalty_factor > 0, a valid
- *      route entering its target road from a node: one 8 B turn row each in the table formulation)
+ * [20] transitions whose turn weight a turn row gives when turn_penalty_factor > 0 (a valid route
+ *      entering its target road from a node: one 8 B turn row each in the table formulation);
+ *      counted at any factor (the routes do not depend on it)
  * [21] nodes those routes turn at (the canonical-path walk of the search formulation) */
 #define OG_NCNT 22
 static uint64_t og_cnt[OG_NCNT];
@@ -773,10 +774,10 @@ og_result* og_match(const og_graph* g, const og_batch* b) {
           uint32_t out = OG_ROUTE_INVALID;
           if (key != OG_KEY_INF && (uint32_t)(key >> 32) <= bound && (uint32_t)key <= tmax) out = (uint32_t)(key >> 32);
           R->route[R->trans_off[lb] + i * KB + j] = out;
+          if (out != OG_ROUTE_INVALID && combo >= 2) og_cnt[20]++;   /* factor-independent: counted always */
           if (turns && out != OG_ROUTE_INVALID && combo >= 2) {
             if (!preds) { canonical_preds(g, &ws, op->mode); preds = 1; }
             R->route_turn[R->trans_off[lb] + i * KB + j] = og_turn_walk(g, &ws, H0, H1, ra, rb, combo);
-            og_cnt[20]++;
           }
           /* the transition's distance term (rule 3b): turn_m + |route_m - gc|, turn_m = U * factor /
            * 65536 (+0 without turn costs, and +0 + x == x); +inf for an invalid route */

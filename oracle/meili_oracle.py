@@ -123,6 +123,14 @@ def routes_ball_algorithmic_bytes(c):
     return 16 * c["ball_rows"] + 32 * c["desc_reads"] + 16 * c["searches"] + 4 * c["route_writes"]
 
 
+def routes_ball_turn_algorithmic_bytes(c):
+    """routes_ball_algorithmic_bytes with turn costs (DESIGN.md §3 rule 3b, k_routes_ball2<true>):
+    + 8 B turn row per transition that enters its target road from a node, + 4 B heading word
+    of each source road, + 8 B distance term written per transition (route_d, read by K3 instead
+    of the 4 B route)."""
+    return routes_ball_algorithmic_bytes(c) + 8 * c["turn_rows"] + 4 * c["searches"] + 8 * c["route_writes"]
+
+
 def candidates_algorithmic_bytes(c):
     """K1 algorithmic bytes of the formulation k_candidates_lane runs: per state
     16 B (point lon/lat, slot, options index) + 1 B candidate count; 8 B item range per grid

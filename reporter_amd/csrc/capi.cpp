@@ -1012,6 +1012,12 @@ int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]) {
   });
 }
 
+int rm_engine_turn_rows(const rm_engine* e, uint32_t* mode_mask, double* build_ms) {
+  return guarded([&] {
+    *mode_mask = e->e->turn_row_mask();
+    for (int m = 0; m < 5; ++m) build_ms[m] = e->e->turn_build_ms(m);
+  });
+}
 int rm_engine_grid_split(const rm_engine* e, uint32_t* f) {
   return guarded([&] { *f = e->e->grid_split(); });
 }

@@ -88,6 +88,14 @@ class Engine:
         d["built_on_gpu"] = bool(out[5])
         return d
 
+    def turn_rows(self):
+        """Turn rows built so far (rule 3b): {mode name: build ms}."""
+        mask = C.c_uint32(0)
+        ms = np.zeros(5, np.float64)
+        _lib.check(_lib.lib().rm_engine_turn_rows(self._h, C.byref(mask), ms.ctypes.data))
+        names = ("auto", "bus", "motor_scooter", "bicycle", "pedestrian")
+        return {names[m]: float(ms[m]) for m in range(5) if (mask.value >> m) & 1}
+
     def grid_split(self):
         """K1 grid refinement f (each graph-file cell split f x f)."""
         out = np.zeros(1, np.uint32)
