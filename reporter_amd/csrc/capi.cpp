@@ -764,6 +764,12 @@ int rm_configure(const char* conf_json_path, char* err, size_t errlen) {
     conf->engine = std::make_shared<Engine>(g, device);
     if (ball_radius_m >= 0.0) conf->engine->set_ball_radius((uint32_t)(ball_radius_m * 100.0));
     conf->engine->ensure_balls(modes);
+    // and the turn rows of those whose configured turn_penalty_factor is > 0 (rule 3b), so the
+    // first request with turn costs does not build them either
+    uint32_t turn_modes = 0;
+    for (int m = 0; m < 5; ++m)
+      if (((modes >> m) & 1u) && conf->mode_defaults[m].turn_penalty_factor > 0.f) turn_modes |= 1u << m;
+    if (turn_modes) conf->engine->ensure_turn_rows(turn_modes);
     if (coalesce) conf->coalescer = std::make_unique<Coalescer>(conf->engine, window_ms, max_traces, workers);
     std::lock_guard<std::mutex> lk(g_mu);
     g_conf = conf;

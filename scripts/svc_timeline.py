@@ -23,12 +23,9 @@ if mf:
             copies.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Direction", "")))
 copies.sort()
 def short(n):
-    n = n.split("(")[0]
-    for k in ("k_", "__amd"):
-        i = n.find(k)
-        if i >= 0:
-            return n[i:]
-    return n[:40]
+    import re
+    m = re.search(r"(k_\w+(?:<[^>]*>)?|__amd\w+)", n)
+    return m.group(1) if m else n[:40]
 runs, cur = [], None
 for s, e, n, q in rows:
     sn = short(n)
