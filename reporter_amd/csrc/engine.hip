@@ -1540,6 +1540,7 @@ struct K2Smem {
   uint32_t wsum[kK2Items / 64];
   uint8_t redo[kK2Items];               // a route of the item was not exact from the tables
   K2Turn tsrc[TURN ? kK2Items : 1];
+  uint32_t tw[TURN ? kTurnDegrees : 1];  // the turn weights (DevGraph::turn_w) in LDS
 };
 
 // Bounds beyond the ball radius (round 4).  A table holds every node within R of its exit, so a
@@ -1671,9 +1672,12 @@ __device__ uint32_t ball_turn_walk(const DevGraph& g, const BallPathLabels& lab,
 // its label strictly, that exit's turn row holds the weight of the path from the exit node on and
 // the heading it leaves the exit node with, and the turn at the exit node is from the source road;
 // otherwise (a tie, or a row without its sum) ball_turn_walk.
+// pt1 / pt0: both exits' turn rows at the first-probe slots h1s / h0s, loaded with the probes (a
+// route resolved past a collision reloads its row); tw: the turn weights in LDS
 __device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src& S, const K2Turn& T, const uint4& t0,
                                                   const uint4& t1, const uint4& r1, const uint4& r0, uint32_t s1,
-                                                  uint32_t s0, double gc, bool& exact, double& d) {
+                                                  uint32_t s0, uint32_t h1s, uint32_t h0s, const uint2& pt1,
+                                                  const uint2& pt0, const uint32_t* tw, double gc, bool& exact, double& d) {
   const unsigned long long k10 = row_key0(r1), k00 = row_key0(r0), k11 = row_key1(r1), k01 = row_key1(r0);
   const unsigned long long l10 = k10 != kKeyInf ? S.rk1 + k10 : kKeyInf, l00 = k00 != kKeyInf ? S.rk0 + k00 : kKeyInf;
   const unsigned long long l11 = k11 != kKeyInf ? S.rk1 + k11 : kKeyInf, l01 = k01 != kKeyInf ? S.rk0 + k01 : kKeyInf;
@@ -1690,12 +1694,15 @@ __device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src
     uint32_t w = kTurnNone;
     const bool e1 = la < lb;
     if (la != lb) {
-      const uint64_t row = e1 ? ball_row0(S.h1.x) + s1 : ball_row0(S.h0.x) + s0;
-      const uint2 tw = reinterpret_cast<const uint2*>(T.trn)[row];
-      w = side ? tw.y : tw.x;
+      uint2 trow = e1 ? pt1 : pt0;
+      if ((e1 ? s1 != h1s : s0 != h0s)) {   // resolved past a collision: the row of the final slot
+        const uint64_t row = e1 ? ball_row0(S.h1.x) + s1 : ball_row0(S.h0.x) + s0;
+        trow = reinterpret_cast<const uint2*>(T.trn)[row];
+      }
+      w = side ? trow.y : trow.x;
     }
     if ((w & kTurnTMask) != kTurnNone) {
-      U = g.turn_w[turn_degree(head_back(T.hw, e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
+      U = tw[turn_degree(head_back(T.hw, e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
     } else {
       const BallPathLabels lab{(const uint4*)S.ent, S.h1, S.h0, S.rk1, S.rk0, g.ball_road_mask};
       bool ok = true;
@@ -1789,6 +1796,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     for (uint32_t j = 0; j < KB; ++j) sm.owner[rel + j] = (uint8_t)threadIdx.x;
   }
   sm.redo[threadIdx.x] = 0;
+  if constexpr (TURN) {
+    if (threadIdx.x < (uint32_t)kTurnDegrees) sm.tw[threadIdx.x] = g.turn_w[threadIdx.x];
+  }
   __syncthreads();
   // ---- phase 2: the block's routes, two transitions per lane and step.  Every load of a step
   // is issued before any is used: the descriptors unconditionally (a handed-over item's
@@ -1797,7 +1807,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
   // went through LDS is otherwise generic: flat loads, each waited for on its own).
   const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
   const uint32_t rm = g.ball_road_mask;
-  for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
+  if constexpr (TURN) {
+    // with turn costs: one transition per lane and step (the turn rows and the tie walk cost the
+    // two-per-step loop its registers); both exits' first probes and their turn rows issued together
+    typedef unsigned int k2_v2 __attribute__((ext_vector_type(2)));
+    typedef const k2_v2 __attribute__((address_space(1)))* k2_trow;
+    const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
+    for (uint32_t q = threadIdx.x; q < n; q += kK2Items) {
+      const uint32_t o = sm.owner[q];
+      const K2Src& A = sm.src[o];
+      const K2Turn& TA = sm.tsrc[o];
+      const bool la = A.bound != kNone;
+      const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(A.tdesc + (q - A.rel)));
+      const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1);
+      const double gc = b.gc[A.tdesc / kMaxCand];
+      const bool ua = la && ta0.w != 0u;
+      const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
+      const uint32_t h1s = ball_slot(ta0.x, A.h1.y), h0s = ball_slot(ta0.x, A.h0.y);
+      const uint64_t i1 = ball_row0(A.h1.x) + h1s, i0 = ball_row0(A.h0.x) + h0s;
+      const k2_gptr ea = (k2_gptr)A.ent;
+      const bool tt = TA.fac != 0u;   // the item weighs turns: its mode has turn rows
+      const k2_trow tra = (k2_trow)(const void*)(uintptr_t)TA.trn;
+      const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
+      const k2_v2 v1 = *(ua1 && tt ? tra + i1 : tdummy), v0 = *(ua0 && tt ? tra + i0 : tdummy);
+      const uint2 pt1 = make_uint2(v1.x, v1.y), pt0 = make_uint2(v0.x, v0.y);
+      if (!la) continue;
+      const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+      const uint4* ga = (const uint4*)A.ent;
+      uint32_t s1 = h1s, s0 = h0s;
+      const uint4 r1 = ball_resolve_at(ga, A.h1, ta0.x, ua1 ? la1 : none, rm, s1);
+      const uint4 r0 = ball_resolve_at(ga, A.h0, ta0.x, ua0 ? la0 : none, rm, s0);
+      bool xa = true;
+      double d = 0.0;
+      b.route[A.ob + (q - A.rel)] = k2_route_turn(g, A, TA, ta0, ta1, r1, r0, s1, s0, h1s, h0s, pt1, pt0, sm.tw, gc, xa, d);
+      b.route_d[A.ob + (q - A.rel)] = d;
+      if (!xa) sm.redo[o] = 1;
+    }
+  }
+  for (uint32_t q = threadIdx.x; q < (TURN ? 0u : n); q += 2 * kK2Items) {
     const uint32_t qb = q + kK2Items;
     const bool hb = qb < n;
     const uint32_t qB = hb ? qb : q;
@@ -1821,27 +1868,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     const uint4* ga = (const uint4*)A.ent;
     const uint4* gb = (const uint4*)B.ent;
     bool xa = true, xb = true;
-    if constexpr (TURN) {
-      const K2Turn& TA = sm.tsrc[sm.owner[q]];
-      const K2Turn& TB = sm.tsrc[sm.owner[qB]];
-      if (la) {
-        uint32_t s1 = ball_slot(ta0.x, A.h1.y), s0 = ball_slot(ta0.x, A.h0.y);
-        double d = 0.0;
-        const uint4 r1 = ball_resolve_at(ga, A.h1, ta0.x, ea1, rm, s1), r0 = ball_resolve_at(ga, A.h0, ta0.x, ea0, rm, s0);
-        b.route[A.ob + (q - A.rel)] = k2_route_turn(g, A, TA, ta0, ta1, r1, r0, s1, s0, b.gc[A.tdesc / kMaxCand], xa, d);
-        b.route_d[A.ob + (q - A.rel)] = d;
-      }
-      if (lb) {
-        uint32_t s1 = ball_slot(tb0.x, B.h1.y), s0 = ball_slot(tb0.x, B.h0.y);
-        double d = 0.0;
-        const uint4 r1 = ball_resolve_at(gb, B.h1, tb0.x, eb1, rm, s1), r0 = ball_resolve_at(gb, B.h0, tb0.x, eb0, rm, s0);
-        b.route[B.ob + (qb - B.rel)] = k2_route_turn(g, B, TB, tb0, tb1, r1, r0, s1, s0, b.gc[B.tdesc / kMaxCand], xb, d);
-        b.route_d[B.ob + (qb - B.rel)] = d;
-      }
-    } else {
-      if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm), xa);
-      if (lb) b.route[B.ob + (qb - B.rel)] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm), xb);
-    }
+    if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm), xa);
+    if (lb) b.route[B.ob + (qb - B.rel)] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm), xb);
     if (!xa) sm.redo[sm.owner[q]] = 1;
     if (!xb) sm.redo[sm.owner[qB]] = 1;
   }
