@@ -1878,6 +1878,136 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
   if (live && sm.redo[threadIdx.x] && sm.src[threadIdx.x].bound != kNone) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
 }
 
+// K2 ball tier, target-major (round 5 experiment, RM_K2_TGT): the block's (pair, source) items as
+// in k_routes_ball2, but phase 2 deals one lane per (pair in the block, target j): the target's
+// descriptor once, then every in-block source's two first probes of the target road issued
+// together, four sources at a time -- two dependent round trips for a pair's K_A transitions of
+// target j instead of two per two transitions.  Bit-identical routes (the same k2_route).
+#ifndef RM_K2_TGT
+#define RM_K2_TGT 0
+#endif
+struct K2TSmem {
+  K2Src src[kK2Items];
+  uint32_t pair[kK2Items];
+  uint8_t owner[kK2Items * kMaxCand];   // unit of the block -> head item (first in-block source) of its pair
+  uint8_t cnt[kK2Items];                // head item: in-block sources of its pair
+  uint32_t wsum[kK2Items / 64];
+  uint8_t redo[kK2Items];
+};
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball_t(DevGraph g, DevBatch b, uint32_t n_items) {
+  __shared__ K2TSmem sm;
+  const uint32_t t0i = xcd_block(blockIdx.x, gridDim.x) * kK2Items;
+  const uint32_t t = t0i + threadIdx.x;
+  const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;
+  const bool live = t <= tl;
+  uint32_t KB = 0, p = kNone;
+  if (live) {
+    p = b.src_item[t];
+    const uint4 pi = b.pair_info[p];
+    const uint32_t i = t - b.src_off[p];
+    KB = (pi.z >> 8) & 0xffu;
+    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+    const int mode = (int)(pi.z >> 16);
+    K2Src S;
+    exit_keys(a0, pi.x, S.rk1, S.rk0);
+    const bool fits = (g.ball_mask >> mode) & 1u;
+    S.lim = ball_exact_limit(pi.x, g.ball_radius[mode], S.rk1, S.rk0);
+    S.h1 = S.h0 = make_uint2(0u, 1u);
+    if (fits) {
+      const uint2* hp = g.ball_hdr[mode];
+      const uint2 x1 = hp[a1.y], x0 = hp[a1.x];
+      if (S.rk1 != kKeyInf) S.h1 = x1;
+      if (S.rk0 != kKeyInf) S.h0 = x0;
+    }
+    S.ent = (unsigned long long)(uintptr_t)g.ball_ent[mode];
+    S.road = a0.x;
+    S.s = a0.y;
+    S.tdesc = p * kMaxCand;
+    S.rel = 0;
+    S.bound = pi.x;
+    S.tmax = pi.y;
+    S.ob = b.trans_off[p] + i * KB;
+    if (!fits || S.h1.y == 0u || S.h0.y == 0u) {
+      S.bound = kNone;
+      b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+    }
+    sm.src[threadIdx.x] = S;
+  }
+  sm.pair[threadIdx.x] = p;
+  sm.redo[threadIdx.x] = 0;
+  __syncthreads();
+  // heads: the first in-block item of each pair; a head's units are its pair's targets
+  const bool head = live && (threadIdx.x == 0 || sm.pair[threadIdx.x - 1] != p);
+  uint32_t cnt = 0;
+  if (head) {
+    cnt = 1;
+    while (threadIdx.x + cnt < kK2Items && sm.pair[threadIdx.x + cnt] == p) ++cnt;
+    sm.cnt[threadIdx.x] = (uint8_t)cnt;
+  }
+  const uint32_t U = head ? KB : 0u;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = U;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += u;
+  }
+  if (lane == 63) sm.wsum[wv] = incl;
+  __syncthreads();
+  uint32_t wbase = 0, n = 0;
+#pragma unroll
+  for (int w = 0; w < kK2Items / 64; ++w) {
+    const uint32_t x = sm.wsum[w];
+    wbase += w < wv ? x : 0u;
+    n += x;
+  }
+  if (head) {
+    const uint32_t rel = wbase + incl - U;
+    sm.src[threadIdx.x].rel = rel;
+    for (uint32_t j = 0; j < U; ++j) sm.owner[rel + j] = (uint8_t)threadIdx.x;
+  }
+  __syncthreads();
+  const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
+  const uint32_t rm = g.ball_road_mask;
+  const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+  for (uint32_t u = threadIdx.x; u < n; u += kK2Items) {
+    const uint32_t h = sm.owner[u];
+    const K2Src& H = sm.src[h];
+    const uint32_t j = u - H.rel, c = sm.cnt[h];
+    const k2_gptr dt = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(H.tdesc + j));
+    const uint4 t0 = k2_ld(dt), t1 = k2_ld(dt + 1);
+    const bool usable = t0.w != 0u;
+    for (uint32_t c0 = 0; c0 < c; c0 += 4) {
+      uint4 r1[4], r0[4];
+      bool u1[4], u0[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {   // four sources' first probes issued together (clamped)
+        const K2Src& S = sm.src[h + min(c0 + (uint32_t)x, c - 1u)];
+        const bool ls = S.bound != kNone && usable;
+        u1[x] = ls && S.rk1 != kKeyInf;
+        u0[x] = ls && S.rk0 != kKeyInf;
+        const k2_gptr e = (k2_gptr)S.ent;
+        r1[x] = k2_ld(u1[x] ? e + (ball_row0(S.h1.x) + ball_slot(t0.x, S.h1.y)) : dummy);
+        r0[x] = k2_ld(u0[x] ? e + (ball_row0(S.h0.x) + ball_slot(t0.x, S.h0.y)) : dummy);
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        if (c0 + (uint32_t)x >= c) break;
+        const K2Src& S = sm.src[h + c0 + x];
+        if (S.bound == kNone) continue;
+        const uint4* ge = (const uint4*)S.ent;
+        bool ex = true;
+        b.route[S.ob + j] = k2_route(S, t0, t1, ball_resolve(ge, S.h1, t0.x, u1[x] ? r1[x] : none, rm),
+                                     ball_resolve(ge, S.h0, t0.x, u0[x] ? r0[x] : none, rm), ex);
+        if (!ex) sm.redo[h + c0 + x] = 1;
+      }
+    }
+  }
+  __syncthreads();
+  if (live && sm.redo[threadIdx.x] && sm.src[threadIdx.x].bound != kNone) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+}
+
 // K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
 // one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A search
 // that outgrows the registers is queued (as its item) for the LDS lane tier.
@@ -2403,6 +2533,9 @@ struct VitGroup {
   uint8_t cs[kVitChunk + 1];      // this chunk's chain-start flags (+ spare)
   uint8_t ch[kVitBt];             // choices of one backtrace block
   uint32_t nch, done, w, pad;
+#if defined(RM_VIT_PAD) && RM_VIT_PAD > 0
+  uint32_t padv[RM_VIT_PAD];      // A/B of the four groups' LDS bank alignment
+#endif
 };
 
 static_assert(sizeof(VitGroup) >= (kVitRoutes + 15 + 3 * 16 + 1) * sizeof(double), "K3 prefetch reads stay inside VitGroup");
@@ -5036,6 +5169,9 @@ void Matcher::run_device(const RunParams& rp) {
     if (v.route_d)
       hipLaunchKernelGGL(k_routes_ball2<true>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
                          g, v, (uint32_t)n_src);
+    else if (RM_K2_TGT)
+      hipLaunchKernelGGL(k_routes_ball_t, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st, g, v,
+                         (uint32_t)n_src);
     else
       hipLaunchKernelGGL(k_routes_ball2<false>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
                          g, v, (uint32_t)n_src);
