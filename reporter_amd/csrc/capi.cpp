@@ -281,6 +281,7 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
   hb.trace_opt = topt.data();
   RunParams rp;
   rp.do_report = 0;
+  rp.prefetch_segments = 1;   // the replies are the segments: a small run readies them itself
   m.set_isolation(true);
   if (tm) { tm[0] += ms_since(t0); t0 = clk::now(); }
   m.run(hb, rp);
@@ -657,6 +658,7 @@ void match_json_batch(rm_matcher* m, const char* const* traces, size_t n, char**
   hb.trace_opt = topt.data();
   RunParams rp;
   rp.do_report = 0;
+  rp.prefetch_segments = 1;
   mt.set_isolation(true);
   mt.run(hb, rp);
   m->ms[2] = ms_since(t2);

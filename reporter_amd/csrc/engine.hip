@@ -88,7 +88,21 @@ struct DevBatch {  // POD view of the workspace for kernels
   const uint32_t* perm;
   const uint32_t* perm_paths;   // perm for the path stage too (null: the path stage takes slot order)
   uint32_t search_delta;        // cm: the wave tiers' delta-stepping width (kNone: plain rounds)
+  // small runs (Matcher::run_small): the u64 totals the launches size themselves from on the
+  // device (Workspace::tot64), the traversal-record capacity, and gate bits -- 1: K4, the report
+  // and the segment gather skip a run whose path pool overflowed or whose records exceed seg_cap
+  // (the host then runs the batch the ordinary way); 2: also one that handed searches to the
+  // global-memory tier, which a small run does not launch before its scratch exists
+  const unsigned long long* tot;
+  uint64_t seg_cap;
+  uint32_t gate;
 };
+
+__device__ __forceinline__ bool small_abort(const DevBatch& b) {
+  if (!b.gate) return false;
+  const uint32_t* c = b.ctl;
+  return (c[2] & kErrPathOverflow) != 0u || ((b.gate & 2u) && (c[9] | c[10]) != 0u) || b.tot[2] > b.seg_cap;
+}
 
 // A failure that belongs to one trajectory (too many roads in a radius, a search beyond every
 // tier's capacity, a path that cannot be rebuilt) marks that trace only, as the reference fails
@@ -265,16 +279,26 @@ __global__ void __launch_bounds__(64) k_states(DevBatch b) {
   const uint32_t k = blockIdx.x;
   if (k >= b.T) return;
   const int lane = threadIdx.x;
+  // the run's control words and this trace's error bits start at zero (the first kernel of a run)
+  if (lane == 0) b.trace_err[k] = 0u;
+  if (k == 0 && lane < kCtlWords) b.ctl[lane] = 0u;
   const uint32_t o = b.trace_off[k], n = b.trace_off[k + 1] - o;
   const MatchOptions op = b.opts[b.trace_opt[k]];
   const double interp = (double)op.interpolation_distance;
   uint32_t ns = 0, last = 0;              // states so far, index of the last state
   float llon = 0.f, llat = 0.f;           // coordinates of the last state
   float c1lo = 0.f, c1la = 0.f, c2lo = 0.f, c2la = 0.f;   // points c0-1, c0-2
+  // each chunk's coordinates load one chunk ahead, unconditionally at a clamped index (a
+  // conditional load would be waited on where it is merged: a long trace's chunks then each
+  // paid a memory round trip before their first instruction)
+  const uint32_t nl = n ? n - 1u : 0u;
+  float nlo = b.lon[o + min((uint32_t)lane, nl)], nla = b.lat[o + min((uint32_t)lane, nl)];
   for (uint32_t c0 = 0; c0 < n; c0 += 64) {
     const uint32_t i = c0 + lane, m = min(64u, n - c0);
     const bool act = i < n;
-    const float lo = act ? b.lon[o + i] : 0.f, la = act ? b.lat[o + i] : 0.f;
+    const float lo = act ? nlo : 0.f, la = act ? nla : 0.f;
+    nlo = b.lon[o + min(i + 64u, nl)];
+    nla = b.lat[o + min(i + 64u, nl)];
     if (act) b.slot_trace[o + i] = k;
     float lo1 = __shfl_up(lo, 1, 64), la1 = __shfl_up(la, 1, 64);
     float lo2 = __shfl_up(lo, 2, 64), la2 = __shfl_up(la, 2, 64);
@@ -389,9 +413,11 @@ __device__ __forceinline__ void project(float alon, float alat, uint32_t acum, f
 //  cannot come within the radius: the projection lies between them, and the
 // fp32 rounding of the projected point is far below pad - r >= 0.5 m (a few ulps of coordinates
 // under 1000 km), so its sq exceeds r^2 with room to spare; rejecting it before the division is
-// bit-exact.
+// bit-exact.  Off by default: measured slower on C2 and CITY30 (the test diverges the lanes of
+// a cell, and the division it saves is not what K1 waits on -- DESIGN.md §6 dead ends);
+// -DRM_K1_REJECT=1 builds it.
 #ifndef RM_K1_REJECT
-#define RM_K1_REJECT 1   // 0: every item is projected (A/B of the reject)
+#define RM_K1_REJECT 0
 #endif
 __device__ __forceinline__ bool outside_pad(float ax, float ay, float bx, float by, float pad) {
   if (!RM_K1_REJECT) return false;
@@ -622,19 +648,36 @@ __device__ void cand_wave_one(const DevGraph& g, const DevBatch& b, CandSmem& sm
     const uint32_t x1 = fx1 > (double)(g.ncx - 1) ? g.ncx - 1 : (uint32_t)fx1;
     const uint32_t y1 = fy1 > (double)(g.ncy - 1) ? g.ncy - 1 : (uint32_t)fy1;
     const uint32_t nx = x1 - x0 + 1, ncell = nx * (y1 - y0 + 1);
-    // stage the covered cells' item ranges in LDS, 64 cells at a time
+    // the covered cells, 64 at a time: their item ranges and an inclusive scan of their item
+    // counts go to LDS, and the cells' items are walked as ONE sequence, a lane per item (a
+    // point's few cells cost one round of loads, not one per cell)
     for (uint32_t c0 = 0; c0 < ncell; c0 += kWave) {
       const uint32_t c = c0 + lane;
+      uint32_t lo = 0, cnt = 0;
       if (c < ncell) {
         const uint32_t cell = (y0 + c / nx) * g.ncx + (x0 + c % nx);
-        sm.cell_lo[lane] = g.cell_off[cell];
-        sm.cell_hi[lane] = g.cell_off[cell + 1];
+        lo = g.cell_off[cell];
+        cnt = g.cell_off[cell + 1] - lo;
       }
+      uint32_t incl = cnt;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t u = __shfl_up(incl, d, kWave);
+        if (lane >= d) incl += u;
+      }
+      const uint32_t tot = (uint32_t)__shfl((int)incl, kWave - 1, kWave);
+      sm.cell_lo[lane] = lo;
+      sm.cell_hi[lane] = incl;   // here: the inclusive item prefix of the staged cells
       __syncthreads();
-      const uint32_t nc = min(ncell - c0, (uint32_t)kWave);
-      for (uint32_t ci = 0; ci < nc; ++ci) {
-        const uint32_t lo = sm.cell_lo[ci], hi = sm.cell_hi[ci];
-        for (uint32_t it = lo + lane; it < hi; it += kWave) {
+      {
+        for (uint32_t f = lane; f < tot; f += kWave) {
+          uint32_t a = 0, e = kWave - 1;   // the staged cell holding item f: first prefix > f
+          while (a < e) {
+            const uint32_t mid = (a + e) >> 1;
+            if (sm.cell_hi[mid] > f) e = mid;
+            else a = mid + 1;
+          }
+          const uint32_t it = sm.cell_lo[a] + (f - (a ? sm.cell_hi[a - 1] : 0u));
           const uint4 r0 = g.cell_rec[2 * (uint64_t)it], r1 = g.cell_rec[2 * (uint64_t)it + 1];
           if (!((r1.z >> 29) & acc)) continue;
           const float ax = (as_f(r0.x) - lon) * mlon, ay = (as_f(r0.y) - lat) * mlat;
@@ -695,11 +738,18 @@ __device__ void cand_wave_one(const DevGraph& g, const DevBatch& b, CandSmem& sm
   if (lane == 0) b.cand_n[p] = (uint8_t)min(n_found, (uint32_t)kMaxCand);
 }
 
-__global__ void __launch_bounds__(64) k_candidates_wave(DevGraph g, DevBatch b) {
+// all = 0: the lane tier's hand-overs (ctl[7]); all = 1: every state slot of the batch (small
+// runs: one wave per state is a few rounds of loads where a lane walks its cells one by one)
+__global__ void __launch_bounds__(64) k_candidates_wave(DevGraph g, DevBatch b, int all) {
   __shared__ CandSmem sm;
-  const uint32_t n_items = min(b.ctl[7], (uint32_t)b.P);
+  const uint32_t n_items = all ? (uint32_t)b.P : min(b.ctl[7], (uint32_t)b.P);
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    cand_wave_one(g, b, sm, b.rl_cand[item]);
+    const uint32_t p = all ? item : b.rl_cand[item];
+    if (all) {
+      const uint32_t k = b.slot_trace[p];
+      if (p - b.trace_off[k] >= b.n_states[k]) continue;   // not a state slot (block-uniform)
+    }
+    cand_wave_one(g, b, sm, p);
     __syncthreads();
   }
 }
@@ -893,6 +943,125 @@ __global__ void k_src_items(DevBatch b) {
   if (p >= b.P) return;
   const uint32_t n = b.src_cnt[p], at = b.src_off[p];
   for (uint32_t i = 0; i < n; ++i) b.src_item[at + i] = (uint32_t)p;
+}
+
+// ---- small runs (Matcher::run_small): one kernel in place of k_scan_parts + an apply pass (+
+// k_src_items / k_rec_slot).  A small batch has at most a few hundred partials, so each block
+// folds the partials before its own (and block 0 all of them, for the totals) instead of
+// waiting for a separate one-block scan: three launches fewer per stage, ~5 us each.
+__device__ __forceinline__ void block_prefix_parts(const unsigned long long* part, uint32_t nb, uint32_t upto,
+                                                   unsigned long long* pre, unsigned long long* all) {
+  __shared__ unsigned long long s[4][4];
+  unsigned long long a = 0, c = 0, ta = 0, tc = 0;
+  const ulonglong2* pp = reinterpret_cast<const ulonglong2*>(part);
+  for (uint32_t q = threadIdx.x; q < nb; q += blockDim.x) {
+    const ulonglong2 v = pp[q];
+    ta += v.x; tc += v.y;
+    if (q < upto) { a += v.x; c += v.y; }
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    a += __shfl_down(a, d, 64); c += __shfl_down(c, d, 64);
+    ta += __shfl_down(ta, d, 64); tc += __shfl_down(tc, d, 64);
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { s[wv][0] = a; s[wv][1] = c; s[wv][2] = ta; s[wv][3] = tc; }
+  __syncthreads();
+  for (int j = 0; j < 4; ++j) {
+    unsigned long long x = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) x += s[w][j];
+    if (j < 2) pre[j] = x; else all[j - 2] = x;
+  }
+}
+
+// k_scan_apply2 + k_src_items over k_trans_count's partials (blocks of 256 pairs); totals to tot[0..1]
+__global__ void __launch_bounds__(256) k_trans_apply_small(DevBatch b, const unsigned long long* part, uint32_t nb,
+                                                           unsigned long long* tot) {
+  unsigned long long pre[2], all[2];
+  block_prefix_parts(part, nb, blockIdx.x, pre, all);
+  if (blockIdx.x == 0 && threadIdx.x == 0) { tot[0] = all[0]; tot[1] = all[1]; }
+  __shared__ uint32_t sa[4], sc[4];
+  const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint32_t va = p < b.P ? b.trans_cnt[p] : 0u, vc = p < b.P ? b.src_cnt[p] : 0u;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t ia = va, ic = vc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t ta = __shfl_up(ia, d, 64), tc = __shfl_up(ic, d, 64);
+    if (lane >= d) { ia += ta; ic += tc; }
+  }
+  if (lane == 63) { sa[wv] = ia; sc[wv] = ic; }
+  __syncthreads();
+  uint32_t ba = 0, bc = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    ba += w < wv ? sa[w] : 0u;
+    bc += w < wv ? sc[w] : 0u;
+  }
+  if (p < b.P) {
+    const uint32_t at = (uint32_t)pre[1] + bc + ic - vc;
+    b.trans_off[p] = (uint32_t)pre[0] + ba + ia - va;
+    b.src_off[p] = at;
+    for (uint32_t i = 0; i < vc; ++i) b.src_item[at + i] = (uint32_t)p;
+  }
+}
+
+// k_scan_apply4 + k_rec_slot over k_sum_u64's partials (blocks of 1024 slots); total to tot[2].
+// Records past seg_cap are not written (the run is then gated off: small_abort).
+__global__ void __launch_bounds__(256) k_path_apply_small(DevBatch b, const unsigned long long* part, uint32_t nb,
+                                                          unsigned long long* tot, uint32_t* rec_slot) {
+  unsigned long long pre[2], all[2];
+  block_prefix_parts(part, nb, blockIdx.x, pre, all);
+  if (blockIdx.x == 0 && threadIdx.x == 0) tot[2] = all[0];
+  __shared__ unsigned long long sa[4], sc[4];
+  const uint64_t n = b.P;
+  const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 4u;
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  for (uint64_t x = i; x < n && x < i + 4; ++x) v[x - i] = b.path_cnt[x];
+  unsigned long long ea, ec;
+  block_excl_scan2((unsigned long long)v[0] + v[1] + v[2] + v[3], 0ull, ea, ec, sa, sc, 4);
+  uint64_t o = pre[0] + ea;
+  for (uint64_t x = i; x < n && x < i + 4; ++x) {
+    b.trav_off[x] = (uint32_t)o;
+    const uint32_t c = v[x - i];
+    for (uint32_t q = 0; q < c; ++q)
+      if (o + q < b.seg_cap) rec_slot[o + q] = (uint32_t)x;
+    o += c;
+  }
+}
+
+// Compaction for the downloads: trace k's records [base[k], base[k] + cnt[k]) of a per-trace
+// pool (sized by traversal records, mostly empty) to dst[off[k] ..), one wave per trace, u64
+// words.  The boundary then moves only the records (C2: 15 MB of segments, not a 362 MB pool).
+__global__ void __launch_bounds__(64) k_gather_recs(uint32_t T, const uint32_t* base, const uint32_t* cnt,
+                                                    const uint32_t* off, const unsigned long long* src, uint32_t words,
+                                                    unsigned long long* dst) {
+  for (uint32_t k = blockIdx.x; k < T; k += gridDim.x) {
+    const uint64_t n = (uint64_t)cnt[k] * words;
+    const unsigned long long* s = src + (uint64_t)base[k] * words;
+    unsigned long long* d = dst + (uint64_t)off[k] * words;
+    for (uint64_t q = threadIdx.x; q < n; q += 64) d[q] = s[q];
+  }
+}
+
+// the per-trace segment offsets of a small run's reply (exclusive scan of seg_cnt, T + 1 words;
+// one block) -- all zero, and seg_cnt zeroed, when the run is gated off
+__global__ void __launch_bounds__(1024) k_seg_offsets_small(DevBatch b, uint32_t* off) {
+  __shared__ unsigned long long sa[16], sc[16];
+  const uint32_t T = b.T;
+  const bool off_gate = small_abort(b);
+  const uint32_t per = (T + 1023u) / 1024u;
+  const uint32_t k0 = min(threadIdx.x * per, T), k1 = min(k0 + per, T);
+  unsigned long long a = 0;
+  for (uint32_t k = k0; k < k1; ++k) a += off_gate ? 0u : b.seg_cnt[k];
+  unsigned long long ea, ec;
+  block_excl_scan2(a, 0ull, ea, ec, sa, sc, 16);
+  for (uint32_t k = k0; k < k1; ++k) {
+    off[k] = (uint32_t)ea;
+    if (off_gate) b.seg_cnt[k] = 0u;
+    else ea += b.seg_cnt[k];
+  }
+  if (threadIdx.x == 1023) off[T] = (uint32_t)ea;
 }
 
 // descriptor field access (see Workspace::cand_desc)
@@ -1716,9 +1885,12 @@ __device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src
 }
 
 template <bool TURN>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_items) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_arg) {
   __shared__ K2Smem<TURN> sm;
+  // kNone: a small run's launch, sized by the upper bound; the item count is on the device
+  const uint32_t n_items = n_arg != kNone ? n_arg : (uint32_t)b.tot[1];
   const uint32_t t0i = xcd_block(blockIdx.x, gridDim.x) * kK2Items;   // first item of the block
+  if (t0i >= n_items) return;
   const uint32_t t = t0i + threadIdx.x;
   const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;              // last item of the block
   const bool live = t <= tl;
@@ -1894,9 +2066,11 @@ struct K2TSmem {
   uint32_t wsum[kK2Items / 64];
   uint8_t redo[kK2Items];
 };
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball_t(DevGraph g, DevBatch b, uint32_t n_items) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball_t(DevGraph g, DevBatch b, uint32_t n_arg) {
   __shared__ K2TSmem sm;
+  const uint32_t n_items = n_arg != kNone ? n_arg : (uint32_t)b.tot[1];
   const uint32_t t0i = xcd_block(blockIdx.x, gridDim.x) * kK2Items;
+  if (t0i >= n_items) return;
   const uint32_t t = t0i + threadIdx.x;
   const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;
   const bool live = t <= tl;
@@ -2019,7 +2193,7 @@ constexpr uint64_t kListedGrid = 4096;   // blocks of a grid-stride launch over 
 template <bool TURN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items, int listed) {
   // grid-stride: a listed launch is sized for every item but usually finds few hand-overs
-  const uint32_t n = listed ? b.ctl[1] : n_items;
+  const uint32_t n = listed ? b.ctl[1] : (n_items != kNone ? n_items : (uint32_t)b.tot[1]);
   __shared__ uint32_t s_res[kMaxCand][256];
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
   const uint32_t t = listed ? b.rl_routes_0[q] : q;
@@ -2659,6 +2833,33 @@ struct VitLayerDesc {
   double gc;
 };
 
+// the loads behind a VitLayerDesc, kept raw: k_viterbi_w loads them a chunk ahead and forms the
+// description (vit_cook) only when it lays that chunk out, so nothing waits on them early
+struct VitLayerRaw {
+  uint32_t kb, ka, off;
+  double gc;
+};
+__device__ __forceinline__ VitLayerRaw vit_raw(const DevBatch& b, uint32_t o, uint32_t S, uint32_t s0, int j) {
+  const uint64_t lq = o + min(s0 + (uint32_t)j, S - 1);
+  const uint64_t lp = lq == o ? o : lq - 1;
+  VitLayerRaw r;
+  r.kb = b.cand_n[lq];
+  r.ka = b.cand_n[lp];
+  r.off = b.trans_off[lq];
+  r.gc = b.gc[lq];
+  return r;
+}
+__device__ __forceinline__ VitLayerDesc vit_cook(const VitLayerRaw& r, uint32_t S, uint32_t s0, int j) {
+  const uint32_t sl = s0 + j;
+  const bool vq = sl < S;
+  VitLayerDesc d;
+  d.off = r.off;
+  d.kb = vq ? r.kb : 0u;
+  d.cnt = (vq && sl >= 1) ? r.ka * d.kb : 0u;
+  d.gc = (vq && sl >= 1) ? r.gc : 0.0;
+  return d;
+}
+
 // layer s0 + j of a trace: candidate count, route count, route offset, gc
 __device__ __forceinline__ VitLayerDesc vit_describe(const DevBatch& b, uint32_t o, uint32_t S, uint32_t s0, int j) {
   const uint32_t sl = s0 + j;
@@ -2891,7 +3092,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
 // per four), and 10,000 waves need two rounds of 8 per SIMD (8,000 traces: 0.75 ms).  Round 4:
 // it runs the small batches (launch_viterbi below), where its shorter layer chain wins.
 #ifndef RM_VIT3_WPE
-#define RM_VIT3_WPE 8
+#define RM_VIT3_WPE 4   // it runs batches of <= 4,096 traces: <= 4 waves per SIMD; 128 VGPRs hold the prefetch
 #endif
 constexpr int kV3Routes = 384;               // routes per staged chunk
 constexpr int kV3Chunk = 16;                 // layers per staged chunk (one per lane 0..15)
@@ -2958,38 +3159,56 @@ __device__ __forceinline__ V3Chunk v3_layout(const VitLayerDesc& d, uint32_t s0,
   c.s0 = s0;
   // wave-uniform values live in SGPRs (the layer loop and its branches are scalar)
   c.C = (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_ctz(~fit | 0x10000u));
-  c.nroutes = (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)c.C - 1);
+  c.nroutes = c.C ? (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)c.C - 1) : 0u;   // C 0: past the trace
   c.rbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.off);
   c.kbrel = d.kb | ((incl - d.cnt) << 8);
   c.gc = d.gc;
   return c;
 }
 
-__device__ __forceinline__ void v3_load(const DevBatch& b, uint32_t o, const V3Chunk& c, int lane,
-                                        uint32_t (&rv)[kV3Regs], float4& sv) {
+// The next chunk's routes (or, with turn costs, its distance terms) and emission rows, loaded
+// into registers one chunk ahead.  Every load is unconditional, at a clamped address inside the
+// batch (a chunk past the trace's end reads its last layer again; staging ignores lanes past
+// nroutes): a conditional load leaves a register merge behind it, and the copy that merge
+// needs makes the wave wait for the load at once -- measured, each chunk then paid the full
+// memory latency before its first layer (C1's 1,000-layer trace: 0.52 ms in K3).
+// (the emission row as a native vector: HIP's float4 is a union-backed class, which the
+// compiler kept in scratch across the chunk loop -- one more wait per chunk)
+typedef float v3_f4 __attribute__((ext_vector_type(4)));
+template <bool TURN>
+struct V3Regs {
+  uint32_t rv[TURN ? 1 : kV3Regs];
+  double rd[TURN ? kV3Regs : 1];
+  v3_f4 sv;
+};
+
+template <bool TURN>
+__device__ __forceinline__ void v3_load(const DevBatch& b, uint32_t o, uint32_t S, const V3Chunk& c, int lane,
+                                        V3Regs<TURN>& r) {
   const uint32_t rlast = c.nroutes ? c.nroutes - 1u : 0u;
 #pragma unroll
   for (int x = 0; x < kV3Regs; ++x) {
-    rv[x] = kRouteInvalid;
-    if ((uint32_t)(kWave * x) < c.nroutes) rv[x] = b.route[c.rbase + min((uint32_t)(lane + kWave * x), rlast)];
+    const uint32_t q = c.rbase + min((uint32_t)(lane + kWave * x), rlast);
+    if constexpr (TURN) r.rd[x] = b.route_d[q];
+    else r.rv[x] = b.route[q];
   }
-  const float4* src = reinterpret_cast<const float4*>(b.cand_sq) + (uint64_t)(o + c.s0) * (kMaxCand / 4);
-  sv = src[min((uint32_t)lane, c.C * (kMaxCand / 4) - 1u)];
+  const uint32_t s0 = min(c.s0, S - 1u);
+  const uint32_t C = max(min(c.C, S - s0), 1u);
+  const v3_f4* src = reinterpret_cast<const v3_f4*>(b.cand_sq) + (uint64_t)(o + s0) * (kMaxCand / 4);
+  r.sv = src[min((uint32_t)lane, C * (kMaxCand / 4) - 1u)];
 }
 
-__device__ __forceinline__ void v3_stage_routes(Vit3Smem& sm, const V3Chunk& c, int lane, const uint32_t (&rv)[kV3Regs]) {
+template <bool TURN>
+__device__ __forceinline__ void v3_stage_routes(Vit3Smem& sm, const V3Chunk& c, int lane, const V3Regs<TURN>& r) {
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
 #pragma unroll
   for (int x = 0; x < kV3Regs; ++x)
-    if ((uint32_t)(lane + kWave * x) < c.nroutes) sm.route_m[lane + kWave * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
-}
-
-// with turn costs (rule 3b): the chunk's distance terms route_d (turn_m + |route_m - gc|, +inf
-// when invalid) in place of its metres, loaded when the chunk is staged
-__device__ __forceinline__ void v3_stage_terms(Vit3Smem& sm, const DevBatch& b, const V3Chunk& c, int lane) {
-#pragma unroll
-  for (int x = 0; x < kV3Regs; ++x)
-    if ((uint32_t)(lane + kWave * x) < c.nroutes) sm.route_m[lane + kWave * x] = b.route_d[c.rbase + lane + kWave * x];
+    if ((uint32_t)(lane + kWave * x) < c.nroutes) {
+      // with turn costs (rule 3b) the staged value is the distance term route_d (turn_m +
+      // |route_m - gc|, +inf when invalid) in place of the route's metres
+      if constexpr (TURN) sm.route_m[lane + kWave * x] = r.rd[x];
+      else sm.route_m[lane + kWave * x] = r.rv[x] == kRouteInvalid ? INF : (double)r.rv[x] * 0.01;
+    }
 }
 
 // back-pointer rows / chain flags of chunk layers [0, n) to HBM
@@ -3085,27 +3304,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
   if (S == 0) return;
   // chunk 0: describe, lay out, load; then describe chunk 1
   V3Chunk cur = v3_layout(vit_describe(b, o, S, 0, lane & 15), 0, S, lane);
-  uint32_t rv[kV3Regs];
-  float4 sv;
-  v3_load(b, o, cur, lane, rv, sv);
-  VitLayerDesc dn{0u, 0u, 0u, 0.0};
-  if (cur.C < S) dn = vit_describe(b, o, S, cur.C, lane & 15);
+  V3Regs<TURN> rg;
+  v3_load<TURN>(b, o, S, cur, lane, rg);
+  VitLayerRaw dn = vit_raw(b, o, S, cur.C, lane & 15);   // (past S: clamped; vit_cook gives kb 0)
   bool prev_ok = false;
   uint32_t prevK = 0;
   int cb = 0;
   for (;;) {
-    if constexpr (TURN) v3_stage_terms(sm, b, cur, lane);
-    else v3_stage_routes(sm, cur, lane, rv);
-    if ((uint32_t)lane < cur.C * (kMaxCand / 4)) reinterpret_cast<float4*>(&sm.sq[0][0])[lane] = sv;
-    // the next chunk's routes and emission rows load while this chunk runs
+    v3_stage_routes<TURN>(sm, cur, lane, rg);
+    if ((uint32_t)lane < cur.C * (kMaxCand / 4)) reinterpret_cast<v3_f4*>(&sm.sq[0][0])[lane] = rg.sv;
+    // the next chunk's routes and emission rows load while this chunk runs (unconditionally:
+    // past the trace's end they are never staged)
     const uint32_t s1 = cur.s0 + cur.C;
     const bool has_next = s1 < S;
-    V3Chunk nx{};
-    if (has_next) {
-      nx = v3_layout(dn, s1, S, lane);
-      v3_load(b, o, nx, lane, rv, sv);
-      if (s1 + nx.C < S) dn = vit_describe(b, o, S, s1 + nx.C, lane & 15);
-    }
+    const V3Chunk nx = v3_layout(vit_cook(dn, S, s1, lane & 15), s1, S, lane);
+    v3_load<TURN>(b, o, S, nx, lane, rg);
+    dn = vit_raw(b, o, S, s1 + nx.C, lane & 15);
     wave_sync();
     for (uint32_t t = 0; t < cur.C; ++t) {
       const uint32_t s = cur.s0 + t;
@@ -3135,17 +3349,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
         v3_flush(b, sm, o + cur.s0, t, lane);
         v3_backtrace(b, sm, o, s - 1, prevK, cb, lane);
         if (t + 1 < cur.C) {   // the backtrace staged through route_m: bring the chunk back
-          uint32_t rr[kV3Regs];
-          const uint32_t rlast = cur.nroutes - 1u;
+          const double INF = __longlong_as_double(0x7ff0000000000000ll);
           const uint32_t* rp = b.route + cur.rbase;
-          __asm__ volatile("" : "+s"(rp));   // rare path: keep its addresses out of the loop's registers
+          const double* dp = b.route_d + cur.rbase;
+          __asm__ volatile("" : "+s"(rp), "+s"(dp));   // rare path: keep its addresses out of the loop's registers
 #pragma unroll
           for (int x = 0; x < kV3Regs; ++x) {
-            rr[x] = kRouteInvalid;
-            if ((uint32_t)(kWave * x) < cur.nroutes) rr[x] = rp[min((uint32_t)(lane + kWave * x), rlast)];
+            const uint32_t q = (uint32_t)(lane + kWave * x);
+            if (q < cur.nroutes) {
+              if constexpr (TURN) sm.route_m[q] = dp[q];
+              else sm.route_m[q] = rp[q] == kRouteInvalid ? INF : (double)rp[q] * 0.01;
+            }
           }
-          if constexpr (TURN) v3_stage_terms(sm, b, cur, lane);
-          else v3_stage_routes(sm, cur, lane, rr);
         }
       }
       if (KB == 0) {
@@ -3460,9 +3675,10 @@ __device__ __forceinline__ bool piece_slow(unsigned long long md, double mtb, do
   return dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
 }
 
-__global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const uint32_t* rec_slot, uint32_t total) {
+__global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const uint32_t* rec_slot, uint32_t total_arg) {
   const uint32_t k = blockIdx.x;
-  if (k >= b.T) return;
+  if (k >= b.T || small_abort(b)) return;
+  const uint32_t total = total_arg != kNone ? total_arg : (uint32_t)b.tot[2];   // kNone: a small run's
   const int lane = threadIdx.x;
   const uint32_t o = b.trace_off[k], o1 = b.trace_off[k + 1];
   const uint32_t Rb = o < b.P ? b.trav_off[o] : total;
@@ -3736,6 +3952,7 @@ __device__ __forceinline__ ReportStats report_wave(const SegmentRec* segs, uint3
 
 __global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uint32_t rmask, uint32_t tmask,
                                                uint32_t* hist, unsigned long long* dur) {
+  if (small_abort(b)) return;   // a gated-off small run: the host runs the batch again
   for (uint32_t k = blockIdx.x; k < b.T; k += gridDim.x) {   // one block per trace (a grid-stride loop over fewer blocks was slower)
     const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
     const ReportStats st = report_wave(b.segs + b.seg_base[k], b.seg_cnt[k], npts > 0, npts ? b.time[o + npts - 1] : 0.0,
@@ -4606,6 +4823,9 @@ Matcher::~Matcher() {
     if (q) (void)hipFree(q);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (hctl_) (void)hipHostFree(hctl_);
+  if (hpack_) (void)hipHostFree(hpack_);
+  if (dpack_) (void)hipFree(dpack_);
+  if (hoff_) (void)hipHostFree(hoff_);
 }
 
 void Matcher::ensure(uint64_t points, uint32_t traces, uint32_t nopts) {
@@ -4808,11 +5028,11 @@ uint32_t search_delta_cm() {
   return d;
 }
 
-static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
+static DevBatch make_view(const Workspace& w, const InputView& in, uint32_t T, uint64_t P) {
   DevBatch v;
   v.T = T; v.P = P;
-  v.trace_off = w.trace_off; v.lon = w.lon; v.lat = w.lat; v.time = w.time; v.acc = w.acc;
-  v.opts = w.opts; v.trace_opt = w.trace_opt;
+  v.trace_off = in.trace_off; v.lon = in.lon; v.lat = in.lat; v.time = in.time; v.acc = in.acc;
+  v.opts = in.opts; v.trace_opt = in.trace_opt;
   v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig; v.state_time = w.state_time;
   v.cand_n = w.cand_n; v.cand_desc = w.cand_desc; v.cand_sq = w.cand_sq;
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
@@ -4831,6 +5051,9 @@ static DevBatch make_view(const Workspace& w, uint32_t T, uint64_t P) {
   v.perm = nullptr;   // run_device sets it when the locality order is on
   v.perm_paths = nullptr;
   v.search_delta = search_delta_cm();
+  v.tot = w.tot64;
+  v.seg_cap = w.cap_segs;
+  v.gate = 0;
   return v;
 }
 
@@ -4856,6 +5079,30 @@ void Matcher::check_batch(uint32_t T, const uint32_t* trace_off, const MatchOpti
   }
 }
 
+// batches of at most this many points take run_small (RM_SMALL_BATCH_POINTS; 0: never)
+static uint64_t small_batch_points() {
+  const char* e = std::getenv("RM_SMALL_BATCH_POINTS");
+  return e && *e ? std::strtoull(e, nullptr, 10) : 65536ull;
+}
+
+void Matcher::use_ws_inputs() {
+  in_.trace_off = ws_.trace_off; in_.lon = ws_.lon; in_.lat = ws_.lat; in_.time = ws_.time; in_.acc = ws_.acc;
+  in_.opts = ws_.opts; in_.trace_opt = ws_.trace_opt;
+}
+
+void Matcher::ensure_pack(uint64_t bytes) {
+  if (bytes <= pack_cap_ && hpack_ && dpack_) return;
+  RM_HIP(hipStreamSynchronize(stream_));   // the previous upload has left the staging
+  if (hpack_) (void)hipHostFree(hpack_);
+  if (dpack_) (void)hipFree(dpack_);
+  hpack_ = nullptr; dpack_ = nullptr; pack_cap_ = 0;
+  const uint64_t c = std::max<uint64_t>(bytes + bytes / 2, 1u << 20);
+  RM_HIP(hipHostMalloc((void**)&hpack_, c, hipHostMallocDefault));
+  std::vector<void*> one;
+  grow_workspace([&] { dpack_ = dalloc<char>(one, c); });
+  pack_cap_ = c;
+}
+
 void Matcher::run(const HostBatch& hb, const RunParams& rp) {
   RM_HIP(hipSetDevice(eng_->device()));
   const uint32_t T = hb.n_traces;
@@ -4877,13 +5124,39 @@ void Matcher::run(const HostBatch& hb, const RunParams& rp) {
   ensure(P, T, hb.n_opts);
   Workspace& w = ws_;
   hipStream_t st = stream_;
-  RM_HIP(hipMemcpyAsync(w.trace_off, hb.trace_off, (T + 1) * 4ull, hipMemcpyHostToDevice, st));
-  RM_HIP(hipMemcpyAsync(w.lon, hb.lon, P * 4, hipMemcpyHostToDevice, st));
-  RM_HIP(hipMemcpyAsync(w.lat, hb.lat, P * 4, hipMemcpyHostToDevice, st));
-  RM_HIP(hipMemcpyAsync(w.time, hb.time, P * 8, hipMemcpyHostToDevice, st));
-  RM_HIP(hipMemcpyAsync(w.acc, hb.accuracy, P * 4, hipMemcpyHostToDevice, st));
-  RM_HIP(hipMemcpyAsync(w.opts, hb.opts, hb.n_opts * sizeof(MatchOptions), hipMemcpyHostToDevice, st));
-  RM_HIP(hipMemcpyAsync(w.trace_opt, hb.trace_opt, T * 4ull, hipMemcpyHostToDevice, st));
+  if (P <= small_batch_points()) {
+    // a small batch goes up as one block through pinned staging: one DMA instead of seven
+    // copies (three of them from pageable memory), ~4 us of stream time each
+    auto al = [](uint64_t x) { return (x + 15u) & ~(uint64_t)15u; };
+    const uint64_t o_topt = (T + 1) * 4ull, o_opts = al(o_topt + T * 4ull);
+    const uint64_t o_lon = al(o_opts + hb.n_opts * sizeof(MatchOptions)), o_lat = al(o_lon + P * 4);
+    const uint64_t o_acc = al(o_lat + P * 4), o_time = al(o_acc + P * 4), bytes = o_time + P * 8;
+    ensure_pack(bytes);
+    std::memcpy(hpack_, hb.trace_off, (T + 1) * 4ull);
+    std::memcpy(hpack_ + o_topt, hb.trace_opt, T * 4ull);
+    std::memcpy(hpack_ + o_opts, hb.opts, hb.n_opts * sizeof(MatchOptions));
+    std::memcpy(hpack_ + o_lon, hb.lon, P * 4);
+    std::memcpy(hpack_ + o_lat, hb.lat, P * 4);
+    std::memcpy(hpack_ + o_acc, hb.accuracy, P * 4);
+    std::memcpy(hpack_ + o_time, hb.time, P * 8);
+    RM_HIP(hipMemcpyAsync(dpack_, hpack_, bytes, hipMemcpyHostToDevice, st));
+    in_.trace_off = (const uint32_t*)dpack_;
+    in_.trace_opt = (const uint32_t*)(dpack_ + o_topt);
+    in_.opts = (const MatchOptions*)(dpack_ + o_opts);
+    in_.lon = (const float*)(dpack_ + o_lon);
+    in_.lat = (const float*)(dpack_ + o_lat);
+    in_.acc = (const float*)(dpack_ + o_acc);
+    in_.time = (const double*)(dpack_ + o_time);
+  } else {
+    use_ws_inputs();
+    RM_HIP(hipMemcpyAsync(w.trace_off, hb.trace_off, (T + 1) * 4ull, hipMemcpyHostToDevice, st));
+    RM_HIP(hipMemcpyAsync(w.lon, hb.lon, P * 4, hipMemcpyHostToDevice, st));
+    RM_HIP(hipMemcpyAsync(w.lat, hb.lat, P * 4, hipMemcpyHostToDevice, st));
+    RM_HIP(hipMemcpyAsync(w.time, hb.time, P * 8, hipMemcpyHostToDevice, st));
+    RM_HIP(hipMemcpyAsync(w.acc, hb.accuracy, P * 4, hipMemcpyHostToDevice, st));
+    RM_HIP(hipMemcpyAsync(w.opts, hb.opts, hb.n_opts * sizeof(MatchOptions), hipMemcpyHostToDevice, st));
+    RM_HIP(hipMemcpyAsync(w.trace_opt, hb.trace_opt, T * 4ull, hipMemcpyHostToDevice, st));
+  }
   n_traces_ = T;
   n_points_ = P;
   run_device(rp);
@@ -5049,6 +5322,7 @@ void Matcher::run_parsed(const uint32_t* trace_off, uint32_t T, const MatchOptio
   }
   batch_sparse_ = gaps && span / (double)gaps >= kLocalitySparseS;
   ensure(P, T, n_opts);   // reserved by json_reserve: no reallocation here (the points are in place)
+  use_ws_inputs();
   Workspace& w = ws_;
   hipStream_t st = stream_;
   RM_HIP(hipMemcpyAsync(w.trace_off, trace_off, (T + 1) * 4ull, hipMemcpyHostToDevice, st));
@@ -5084,6 +5358,156 @@ const char* error_text(uint32_t bits) {
 constexpr uint64_t kMaxTransitions = 0xF0000000ull;
 constexpr uint64_t kMaxRecords = 1700000000ull;
 
+// the search tiers' grids (grid-stride over lists the host does not read) shrink with the batch:
+// a coalesced service batch of ~15 k points launches them mostly empty
+static uint32_t tier_grid(uint64_t P, uint32_t full) {
+  return (uint32_t)std::max<uint64_t>(32u, std::min<uint64_t>(full, P / 64u));
+}
+
+// Small batches (the coalesced service: a few to a few thousand requests per run).  Their cost
+// is latency, not bandwidth: ~45 launches of a few microseconds each, seven uploads and four
+// host round trips around ~0.1 ms of kernel work.  Here every pool is sized from upper bounds
+// instead of read-back totals (kMaxCand^2 transitions and kMaxCand sources per pair; kInlinePath
+// edges per slot in line plus the path pool), the launches that depend on those totals read
+// them from the device (DevBatch::tot), the scans fold their partials in one pass, and the
+// segment offsets and the compacted reply are prepared before the run's only read-back.  What
+// an upper bound cannot cover -- the path pool overflowing, a search handed to the global tier
+// before its scratch exists -- gates K4 and the report off on the device (small_abort) and
+// returns false: the caller then runs the batch the ordinary way.  Same kernels, same results.
+constexpr uint64_t kSmallWaveK1 = 32768;   // small runs up to this many points take K1 a wave per state
+bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
+  const uint32_t T = n_traces_;
+  const uint64_t P = n_points_;
+  Workspace& w = ws_;
+  hipStream_t st = stream_;
+  unsigned long long* htot = reinterpret_cast<unsigned long long*>(hctl_ + 16);
+  ensure_trans(P * kMaxCand * kMaxCand, P * kMaxCand);
+  if (turn_mask_) ensure_turns();
+  ensure_segs(P * kInlinePath + w.cap_path);
+  DevBatch v = make_view(w, in_, T, P);
+  v.route = w.route;
+  if (turn_mask_) v.route_d = w.route_d;
+  v.src_item = w.src_item;
+  v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
+  v.rl_routes_c = w.rl_routes_c;
+  v.segs = w.segs; v.reps = w.reps; v.seg_cap = w.cap_segs;
+  v.gate = w.gsearch ? 1u : 3u;
+  locality_used_ = false;   // a few thousand points: nothing to gain from the region order
+  const uint32_t count_grid = (uint32_t)((P + 255) / 256);
+  const uint32_t sum_grid = (uint32_t)((P + 1023) / 1024);
+  const uint64_t max_src = P * kMaxCand;
+  const uint32_t item_grid = (uint32_t)((max_src + kK2Items - 1) / kK2Items);
+  const uint32_t lane_grid = (uint32_t)((max_src + 255) / 256);
+  const auto tgrid = [P](uint32_t full) { return tier_grid(P, full); };
+
+  tic(kKStates);
+  hipLaunchKernelGGL(k_states, dim3(T), dim3(64), 0, st, v);
+  toc(kKStates);
+  tic(kKCandidates);
+  if (P <= kSmallWaveK1) {   // one wave per state
+    hipLaunchKernelGGL(k_candidates_wave, dim3((uint32_t)P), dim3(64), 0, st, g, v, 1);
+  } else {
+    hipLaunchKernelGGL(k_candidates_lane, dim3(count_grid), dim3(256), 0, st, g, v);
+    hipLaunchKernelGGL(k_candidates_wave, dim3(tgrid(2048)), dim3(64), 0, st, g, v, 0);
+  }
+  toc(kKCandidates);
+  tic(kKScan);
+  hipLaunchKernelGGL(k_trans_count, dim3(count_grid), dim3(256), 0, st, v, w.tot_part);
+  hipLaunchKernelGGL(k_trans_apply_small, dim3(count_grid), dim3(256), 0, st, v, (const unsigned long long*)w.tot_part,
+                     count_grid, w.tot64);
+  toc(kKScan);
+  const bool balls = (mode_mask_ & g.ball_mask) != 0u;
+  tic(kKRoutes);
+  if (balls) {
+    if (v.route_d)
+      hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
+    else
+      hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
+    const uint32_t lg = (uint32_t)std::min<uint64_t>(lane_grid, kListedGrid);
+    if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
+    else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
+  } else {
+    if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
+    else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
+  }
+  hipLaunchKernelGGL(k_routes_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  if (w.gsearch) hipLaunchKernelGGL(k_routes_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
+  toc(kKRoutes);
+  tic(kKViterbi);
+  launch_viterbi(T, st, v);
+  toc(kKViterbi);
+  tic(kKPaths);
+  if (balls) {
+    hipLaunchKernelGGL(k_paths_ball, dim3(count_grid), dim3(256), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>(count_grid, kListedGrid)), dim3(256), 0, st, g, v, 1);
+  } else {
+    hipLaunchKernelGGL(k_paths_lane, dim3(count_grid), dim3(256), 0, st, g, v, 0);
+  }
+  hipLaunchKernelGGL(k_paths_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
+  toc(kKPaths);
+  tic(kKSegments);
+  hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot_part);
+  hipLaunchKernelGGL(k_path_apply_small, dim3(sum_grid), dim3(256), 0, st, v, (const unsigned long long*)w.tot_part,
+                     sum_grid, w.tot64, w.rec_slot);
+  hipLaunchKernelGGL(k_seg_wave, dim3(T), dim3(64), 0, st, g, v, (const uint32_t*)w.rec_slot, kNone);
+  toc(kKSegments);
+  if (rp.do_report) {
+    if (rp.hist && rp.zero_hist)
+      RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)eng_->n_segments() * kHistBins * sizeof(uint32_t), st));
+    if (rp.dur && rp.zero_hist) RM_HIP(hipMemsetAsync(rp.dur, 0, (size_t)eng_->n_segments() * 8u, st));
+    tic(kKReport);
+    hipLaunchKernelGGL(k_report, dim3(T), dim3(64), 0, st, v, rp.threshold_sec, rp.report_mask,
+                       rp.transition_mask, rp.hist, rp.dur);
+    toc(kKReport);
+  }
+  // the reply's segments, compacted per trace on the device (get_segments then copies them down)
+  constexpr uint32_t kSegWords = sizeof(SegmentRec) / 8;
+  const size_t offb = ((T + 1) * 4ull + 7) & ~(size_t)7;
+  bool prefetch = rp.prefetch_segments != 0;
+  if (prefetch) {
+    try {
+      grow_dl_dev(offb + v.seg_cap * sizeof(SegmentRec));
+    } catch (const BatchTooLarge&) {
+      prefetch = false;   // the ordinary download sizes its buffer from the counts instead
+    }
+  }
+  if (prefetch) {
+    if (T + 1 > hoff_cap_) {
+      if (hoff_) RM_HIP(hipHostFree(hoff_));
+      hoff_ = nullptr; hoff_cap_ = 0;
+      const uint64_t c = std::max<uint64_t>(T + 1 + T / 2, 4096);
+      RM_HIP(hipHostMalloc((void**)&hoff_, c * 4, hipHostMallocDefault));
+      hoff_cap_ = c;
+    }
+    uint32_t* d_off = (uint32_t*)dl_dev_;
+    hipLaunchKernelGGL(k_seg_offsets_small, dim3(1), dim3(1024), 0, st, v, d_off);
+    hipLaunchKernelGGL(k_gather_recs, dim3(std::min<uint32_t>(T, 8192u)), dim3(64), 0, st, T, (const uint32_t*)w.seg_base,
+                       (const uint32_t*)w.seg_cnt, (const uint32_t*)d_off, (const unsigned long long*)w.segs, kSegWords,
+                       (unsigned long long*)((char*)dl_dev_ + offb));
+    RM_HIP(hipMemcpyAsync(hoff_, d_off, (T + 1) * 4ull, hipMemcpyDeviceToHost, st));
+  }
+  RM_HIP(hipGetLastError());
+  RM_HIP(hipMemcpyAsync(hctl_, w.ctl, kCtlWords * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  RM_HIP(hipMemcpyAsync(htot, w.tot64, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  sync();
+  if ((hctl_[2] & kErrPathOverflow) || (!w.gsearch && (hctl_[9] | hctl_[10])) || htot[2] > v.seg_cap) return false;
+  n_trans_ = htot[0];
+  n_path_ = htot[2];
+  seg_used_ = htot[2];
+  has_report_ = rp.do_report != 0;
+  seg_prefetched_ = prefetch;
+  err_bits_ = hctl_[2] & (kErrCandOverflow | kErrSearchOverflow | kErrRounds);
+  if (err_bits_ && !isolate_) throw std::runtime_error(error_text(err_bits_));
+  return true;
+}
+
 void Matcher::run_device(const RunParams& rp) {
   RM_HIP(hipSetDevice(eng_->device()));
   const uint32_t T = n_traces_;
@@ -5098,9 +5522,10 @@ void Matcher::run_device(const RunParams& rp) {
   const DevGraph g = eng_->dev_snapshot();
   if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 32 * sizeof(uint32_t), hipHostMallocDefault));
   unsigned long long* htot = reinterpret_cast<unsigned long long*>(hctl_ + 16);
-  RM_HIP(hipMemsetAsync(w.ctl, 0, kCtlWords * sizeof(uint32_t), st));
-  RM_HIP(hipMemsetAsync(w.trace_err, 0, T * sizeof(uint32_t), st));
-  DevBatch v = make_view(w, T, P);
+  seg_prefetched_ = false;
+  if (P <= small_batch_points() && run_small(rp, g)) return;
+  // (k_states zeroes the control words and the per-trace error bits)
+  DevBatch v = make_view(w, in_, T, P);
   const uint32_t count_grid = (uint32_t)((P + 255) / 256);
   const uint32_t sum_grid = (uint32_t)((P + 1023) / 1024);   // k_sum_u64: four counts per lane
 
@@ -5128,7 +5553,7 @@ void Matcher::run_device(const RunParams& rp) {
   }
   tic(kKCandidates);
   hipLaunchKernelGGL(k_candidates_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, g, v, 0);
   toc(kKCandidates);
   tic(kKScan);
   hipLaunchKernelGGL(k_trans_count, dim3(count_grid), dim3(256), 0, st, v, w.tot_part);
@@ -5189,7 +5614,7 @@ void Matcher::run_device(const RunParams& rp) {
   }
   // the search tiers' grids (grid-stride over lists the host does not read) shrink with the batch:
   // a coalesced service batch of ~15 k points launches them mostly empty
-  const auto tgrid = [P](uint32_t full) { return (uint32_t)std::max<uint64_t>(32u, std::min<uint64_t>(full, P / 64u)); };
+  const auto tgrid = [P](uint32_t full) { return tier_grid(P, full); };
   hipLaunchKernelGGL(k_routes_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
   hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
   hipLaunchKernelGGL(k_routes_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
@@ -5395,7 +5820,7 @@ void Matcher::get_paths(uint32_t* path_off, uint32_t* path_cnt, uint32_t* pool, 
     RM_HIP(hipMemcpy(ch.data(), ws_.choice, P, hipMemcpyDeviceToHost));
     RM_HIP(hipMemcpy(cs.data(), ws_.chain_start, P, hipMemcpyDeviceToHost));
     std::vector<uint32_t> tro(n_traces_ + 1), ns(n_traces_);
-    RM_HIP(hipMemcpy(tro.data(), ws_.trace_off, (n_traces_ + 1) * 4ull, hipMemcpyDeviceToHost));
+    RM_HIP(hipMemcpy(tro.data(), in_.trace_off, (n_traces_ + 1) * 4ull, hipMemcpyDeviceToHost));
     RM_HIP(hipMemcpy(ns.data(), ws_.n_states, n_traces_ * 4ull, hipMemcpyDeviceToHost));
     for (uint32_t k = 0; k < n_traces_; ++k)
       for (uint32_t s = 1; s < ns[k]; ++s) {
@@ -5434,18 +5859,58 @@ uint64_t Matcher::count_segments() {
   for (uint32_t c : cnt) t += c;
   return t;
 }
-// Compaction for the downloads: trace k's records [base[k], base[k] + cnt[k]) of a per-trace
-// pool (sized by traversal records, mostly empty) to dst[off[k] ..), one wave per trace, u64
-// words.  The boundary then moves only the records (C2: 15 MB of segments, not a 362 MB pool).
-__global__ void __launch_bounds__(64) k_gather_recs(uint32_t T, const uint32_t* base, const uint32_t* cnt,
-                                                    const uint32_t* off, const unsigned long long* src, uint32_t words,
-                                                    unsigned long long* dst) {
-  for (uint32_t k = blockIdx.x; k < T; k += gridDim.x) {
-    const uint64_t n = (uint64_t)cnt[k] * words;
-    const unsigned long long* s = src + (uint64_t)base[k] * words;
-    unsigned long long* d = dst + (uint64_t)off[k] * words;
-    for (uint64_t q = threadIdx.x; q < n; q += 64) d[q] = s[q];
+// grow-only pinned host buffer of the downloads: failing to pin it is a batch too large for
+// the host, which the coalescer splits (serve_policy.hpp), not a generic error
+void Matcher::grow_dl_host(size_t need) {
+  if (need <= dl_host_bytes_) return;
+  const size_t want = std::max(need, dl_host_bytes_ + dl_host_bytes_ / 2);
+  if (dl_host_) RM_HIP(hipHostFree(dl_host_));
+  dl_host_ = nullptr;
+  dl_host_bytes_ = 0;
+  void* p = nullptr;
+  size_t got = want;
+  hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+  if (e != hipSuccess && want > need) {
+    (void)hipGetLastError();
+    got = need;
+    e = hipHostMalloc(&p, need, hipHostMallocDefault);
   }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    throw BatchTooLarge("pinned download buffer of " + std::to_string(need) + " bytes: " + hipGetErrorString(e));
+  }
+  dl_host_ = p;
+  dl_host_bytes_ = got;
+}
+
+// grow-only device buffer of the downloads (offsets, then the compacted records)
+void Matcher::grow_dl_dev(size_t dev_need) {
+  if (dev_need <= dl_dev_bytes_) return;
+  const size_t want = std::max(dev_need, dl_dev_bytes_ + dl_dev_bytes_ / 2);
+  if (dl_dev_) RM_HIP(hipFree(dl_dev_));
+  dl_dev_ = nullptr;
+  dl_dev_bytes_ = 0;
+  // test hook: allocations above RM_TEST_DOWNLOAD_ALLOC_LIMIT bytes fail as out of memory
+  // (tests/test_gpu_isolation.py drives the failure and the call after it)
+  const char* lim = std::getenv("RM_TEST_DOWNLOAD_ALLOC_LIMIT");
+  const size_t limit = lim && *lim ? (size_t)std::strtoull(lim, nullptr, 10) : ~(size_t)0;
+  void* p = nullptr;
+  size_t got = 0;
+  for (const size_t sz : {want, dev_need}) {
+    if (sz > limit) continue;
+    std::vector<void*> buf;
+    try {
+      dalloc<char>(buf, sz);
+    } catch (const OutOfDeviceMemory&) {
+      continue;
+    }
+    p = buf[0];
+    got = sz;
+    break;
+  }
+  if (!p) throw BatchTooLarge("segment download buffer of " + std::to_string(dev_need) + " bytes does not fit in HBM");
+  dl_dev_ = p;
+  dl_dev_bytes_ = got;
 }
 
 void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, const void* d_src, uint32_t words,
@@ -5453,34 +5918,14 @@ void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, 
   const uint32_t T = n_traces_;
   hipStream_t st = stream_;
   RM_HIP(hipSetDevice(eng_->device()));
+  seg_prefetched_ = false;   // the device buffer is reused below
   const size_t offb = ((size_t)T + 1) * 4;
   // pinned: [0, offb) the counts then offsets, then the compacted records
   // The buffers grow by half again (or to the need).  The old buffer is released first and the
   // pointer / size pair only records a buffer that exists, so a failed allocation leaves (null, 0)
   // and the next call allocates again; running out of memory here is a batch too large for the
   // device, which the coalescer splits (serve_policy.hpp), not a generic error.
-  auto grow_host = [&](size_t need) {
-    if (need <= dl_host_bytes_) return;
-    const size_t want = std::max(need, dl_host_bytes_ + dl_host_bytes_ / 2);
-    if (dl_host_) RM_HIP(hipHostFree(dl_host_));
-    dl_host_ = nullptr;
-    dl_host_bytes_ = 0;
-    void* p = nullptr;
-    size_t got = want;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-    if (e != hipSuccess && want > need) {
-      (void)hipGetLastError();
-      got = need;
-      e = hipHostMalloc(&p, need, hipHostMallocDefault);
-    }
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      throw BatchTooLarge("pinned download buffer of " + std::to_string(need) + " bytes: " + hipGetErrorString(e));
-    }
-    dl_host_ = p;
-    dl_host_bytes_ = got;
-  };
-  grow_host(offb);
+  grow_dl_host(offb);
   uint32_t* hc = (uint32_t*)dl_host_;
   RM_HIP(hipMemcpyAsync(hc, d_cnt, T * 4ull, hipMemcpyDeviceToHost, st));
   RM_HIP(hipStreamSynchronize(st));
@@ -5494,34 +5939,8 @@ void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, 
   if (at == 0) return;
   const size_t recb = (size_t)at * words * 8;
   const size_t dev_need = offb + recb + 8;
-  if (dev_need > dl_dev_bytes_) {
-    const size_t want = std::max(dev_need, dl_dev_bytes_ + dl_dev_bytes_ / 2);
-    if (dl_dev_) RM_HIP(hipFree(dl_dev_));
-    dl_dev_ = nullptr;
-    dl_dev_bytes_ = 0;
-    // test hook: allocations above RM_TEST_DOWNLOAD_ALLOC_LIMIT bytes fail as out of memory
-    // (tests/test_gpu_isolation.py drives the failure and the call after it)
-    const char* lim = std::getenv("RM_TEST_DOWNLOAD_ALLOC_LIMIT");
-    const size_t limit = lim && *lim ? (size_t)std::strtoull(lim, nullptr, 10) : ~(size_t)0;
-    void* p = nullptr;
-    size_t got = 0;
-    for (const size_t sz : {want, dev_need}) {
-      if (sz > limit) continue;
-      std::vector<void*> buf;
-      try {
-        dalloc<char>(buf, sz);
-      } catch (const OutOfDeviceMemory&) {
-        continue;
-      }
-      p = buf[0];
-      got = sz;
-      break;
-    }
-    if (!p) throw BatchTooLarge("segment download buffer of " + std::to_string(dev_need) + " bytes does not fit in HBM");
-    dl_dev_ = p;
-    dl_dev_bytes_ = got;
-  }
-  grow_host(offb + recb + 8);
+  grow_dl_dev(dev_need);
+  grow_dl_host(offb + recb + 8);
   hc = (uint32_t*)dl_host_;
   std::memcpy(hc, off, offb);
   uint32_t* d_off = (uint32_t*)dl_dev_;
@@ -5535,10 +5954,29 @@ void Matcher::download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, 
   std::memcpy(dst, h_dst, recb);
 }
 
+// a small run's segments, compacted by the run itself (run_small): one copy down
+bool Matcher::download_prefetched(uint32_t* off, void* dst, const std::function<void*(uint64_t)>& dst_for) {
+  if (!seg_prefetched_) return false;
+  seg_prefetched_ = false;   // once: the buffers are shared with the other downloads
+  const uint32_t T = n_traces_;
+  std::memcpy(off, hoff_, ((size_t)T + 1) * 4);
+  const uint64_t at = off[T];
+  if (dst_for) dst = dst_for(at);
+  if (at == 0) return true;
+  const size_t offb = (((size_t)T + 1) * 4 + 7) & ~(size_t)7;
+  const size_t recb = (size_t)at * sizeof(SegmentRec);
+  grow_dl_host(recb);
+  RM_HIP(hipMemcpyAsync(dl_host_, (const char*)dl_dev_ + offb, recb, hipMemcpyDeviceToHost, stream_));
+  RM_HIP(hipStreamSynchronize(stream_));
+  std::memcpy(dst, dl_host_, recb);
+  return true;
+}
+
 void Matcher::get_segments(uint32_t* seg_off, SegmentRec* segs) {
   sync();
   if (!n_traces_) { seg_off[0] = 0; return; }
   static_assert(sizeof(SegmentRec) % 8 == 0, "records move as u64 words");
+  if (download_prefetched(seg_off, segs, nullptr)) return;
   download_compacted(ws_.seg_base, ws_.seg_cnt, ws_.segs, sizeof(SegmentRec) / 8, seg_off, segs, nullptr);
 }
 void Matcher::get_segments(std::vector<uint32_t>& seg_off, std::vector<SegmentRec>& segs) {
@@ -5546,6 +5984,11 @@ void Matcher::get_segments(std::vector<uint32_t>& seg_off, std::vector<SegmentRe
   seg_off.assign((size_t)n_traces_ + 1, 0u);
   segs.clear();
   if (!n_traces_) return;
+  if (download_prefetched(seg_off.data(), nullptr, [&](uint64_t n) -> void* {
+        segs.resize(n);
+        return segs.data();
+      }))
+    return;
   download_compacted(ws_.seg_base, ws_.seg_cnt, ws_.segs, sizeof(SegmentRec) / 8, seg_off.data(), nullptr,
                      [&](uint64_t n) -> void* {
                        segs.resize(n);

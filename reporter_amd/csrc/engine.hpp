@@ -103,6 +103,21 @@ struct RunParams {
   int do_report = 1;
   int zero_hist = 0;                    // memset hist (and dur) on the stream before the epilogue
   unsigned long long* dur = nullptr;    // device, n_segments u64 duration sums in whole seconds (may be null)
+  // a small batch (Matcher::run_small) also lays out and compacts its segments on the device
+  // before its one read-back, so get_segments is a single copy (the service's reply path)
+  int prefetch_segments = 0;
+};
+
+// Device addresses of a batch's inputs: the workspace's arrays, or (a small run()) the one
+// block its single upload filled
+struct InputView {
+  const uint32_t* trace_off = nullptr;
+  const float* lon = nullptr;
+  const float* lat = nullptr;
+  const double* time = nullptr;
+  const float* acc = nullptr;
+  const MatchOptions* opts = nullptr;
+  const uint32_t* trace_opt = nullptr;
 };
 
 // Kernel ids for per-kernel HIP-event timing.
@@ -248,8 +263,9 @@ class Matcher {
   Matcher(const Matcher&) = delete;
   Matcher& operator=(const Matcher&) = delete;
 
-  // Upload a batch and run every stage on this matcher's stream (asynchronous
-  // except for the two size read-backs).  Throws on error.
+  // Upload a batch and run every stage on this matcher's stream; returns when the run's control
+  // words are back (a large batch also reads its transition and path totals back between the
+  // stages; a small one sizes its pools from upper bounds instead: run_small).  Throws on error.
   void run(const HostBatch& b, const RunParams& rp);
   // Run every stage over the batch already resident in HBM (inputs of the last run()).
   void run_device(const RunParams& rp);
@@ -354,8 +370,22 @@ class Matcher {
   // downloaded through pinned memory into dst; off gets the T+1 offsets
   void download_compacted(const uint32_t* d_base, const uint32_t* d_cnt, const void* d_src, uint32_t words,
                           uint32_t* off, void* dst, const std::function<void*(uint64_t)>& dst_for);
+  void grow_dl_host(size_t need);
+  bool download_prefetched(uint32_t* off, void* dst, const std::function<void*(uint64_t)>& dst_for);
+  void grow_dl_dev(size_t need);
+  // small batches (run_small): no size read-back between the stages, one upload, one read-back
+  bool run_small(const RunParams& rp, const DevGraph& g);
+  void use_ws_inputs();
+  void ensure_pack(uint64_t bytes);
 
   Engine* eng_;
+  InputView in_;
+  char* hpack_ = nullptr;      // pinned staging and device block of a small run()'s inputs (grow-only)
+  char* dpack_ = nullptr;
+  uint64_t pack_cap_ = 0;
+  uint32_t* hoff_ = nullptr;   // pinned: a small run's per-trace segment offsets (T + 1), prefetched
+  uint64_t hoff_cap_ = 0;
+  bool seg_prefetched_ = false;
   void* dl_dev_ = nullptr;     // grow-only device / pinned host buffers of download_compacted
   void* dl_host_ = nullptr;
   size_t dl_dev_bytes_ = 0, dl_host_bytes_ = 0;

@@ -416,6 +416,7 @@ void Matcher::run_points(const PointsDesc& pd, const RunParams& rp) {
   n_points_ = P;
   if (T == 0) { n_trans_ = 0; n_path_ = 0; seg_used_ = 0; has_report_ = false; return; }
   ensure(P, T, pd.n_opts);
+  use_ws_inputs();
   Workspace& w = ws_;
   RM_HIP(hipMemcpyAsync(w.opts, pd.opts, pd.n_opts * sizeof(MatchOptions), hipMemcpyHostToDevice, st));
   hipLaunchKernelGGL(k_win_gather, dim3(grid(n)), dim3(256), 0, st, n, s.k1, s.v1, s.idx, s.flag, s.wstart, s.wflag, s.wofs,
@@ -436,12 +437,12 @@ void Matcher::get_trace_uuid(uint32_t* out) {
 void Matcher::get_batch(uint32_t* trace_off, float* lon, float* lat, double* time, float* acc) {
   sync();
   const uint64_t P = n_points_;
-  RM_HIP(hipMemcpy(trace_off, ws_.trace_off, (n_traces_ + 1) * 4ull, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(trace_off, in_.trace_off, (n_traces_ + 1) * 4ull, hipMemcpyDeviceToHost));
   if (!P) return;
-  RM_HIP(hipMemcpy(lon, ws_.lon, P * 4, hipMemcpyDeviceToHost));
-  RM_HIP(hipMemcpy(lat, ws_.lat, P * 4, hipMemcpyDeviceToHost));
-  RM_HIP(hipMemcpy(time, ws_.time, P * 8, hipMemcpyDeviceToHost));
-  RM_HIP(hipMemcpy(acc, ws_.acc, P * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(lon, in_.lon, P * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(lat, in_.lat, P * 4, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(time, in_.time, P * 8, hipMemcpyDeviceToHost));
+  RM_HIP(hipMemcpy(acc, in_.acc, P * 4, hipMemcpyDeviceToHost));
 }
 
 std::string Matcher::tiles(const TileParams& tp, TileComm* comm) {
@@ -455,7 +456,7 @@ std::string Matcher::tiles(const TileParams& tp, TileComm* comm) {
   hipStream_t st = stream_;
   const uint32_t T = n_traces_;
   ensure_rows(1, T);
-  TileArgs a{T, w.trace_off, w.time, w.reps, w.seg_base, w.rep_cnt, tp.quantisation};
+  TileArgs a{T, in_.trace_off, in_.time, w.reps, w.seg_base, w.rep_cnt, tp.quantisation};
   // ---- rows of this rank
   uint64_t R = 0;
   if (T) {
