@@ -562,18 +562,21 @@ bool match_json_batch_device(rm_matcher* m, const char* const* traces, size_t n,
   std::vector<uint32_t> flags(n, 0u);
   std::vector<double> dtsp(2 * n, 0.0);
   mt.json_parse(span.data(), off.data(), (uint32_t)n, flags.data(), dtsp.data());
-  tj::PointSink fix;
+  // one sink per flagged trace, alive until the run: their points go up with hipMemcpyAsync from
+  // pageable memory, so none is reused or freed before the stream has consumed it
+  std::deque<tj::PointSink> fixes;
   for (size_t i = 0; i < n; ++i) {
     if (host_parsed[i]) continue;
     if (!flags[i]) { tsp[2 * i] = dtsp[2 * i]; tsp[2 * i + 1] = dtsp[2 * i + 1]; continue; }
     // not the compact layout after all: the host reader's points, if they fit the trace's slots
-    fix.clear();
+    tj::PointSink& fix = fixes.emplace_back();
     try {
       opts[i] = tj::parse_request(traces[i], len[i], conf.mode_defaults, fix);
     } catch (const std::exception&) {
+      mt.sync();   // the uploads queued so far read host memory this function owns
       return false;
     }
-    if (fix.size() != cnt[i]) return false;
+    if (fix.size() != cnt[i]) { mt.sync(); return false; }
     host_points(i, fix, 0);
   }
   m->ms[1] = ms_since(t1);
@@ -834,6 +837,17 @@ int rm_match_batch_packed(rm_matcher* m, const char* const* traces, size_t n, ch
       if (!traces[i]) throw std::runtime_error("trace string is NULL");
     if (n == 0) {
       *buf = static_cast<char*>(std::calloc(1, 1));
+      return;
+    }
+    if (n == 1 && m->conf->coalescer) {   // one request: the coalescer, as rm_match
+      ParsedTrace pt = parse_trace(traces[0], *m->conf);
+      const std::string js = m->conf->coalescer->submit(&pt);
+      char* b = static_cast<char*>(std::malloc(js.size() + 1));
+      if (!b) throw std::bad_alloc();
+      std::memcpy(b, js.data(), js.size());
+      b[js.size()] = 0;
+      off[1] = js.size();
+      *buf = b;
       return;
     }
     const PackedOut pk{buf, off};

@@ -274,6 +274,12 @@ __global__ void __launch_bounds__(256) k_scan_apply_perm(const uint32_t* a, uint
 __device__ __forceinline__ float lane_f(float v, uint32_t q) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)q));
 }
+__device__ __forceinline__ double lane_d(double v, uint32_t q) {
+  const unsigned long long u = __double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, (int)q);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), (int)q);
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
 
 __global__ void __launch_bounds__(64) k_states(DevBatch b) {
   const uint32_t k = blockIdx.x;
@@ -287,19 +293,35 @@ __global__ void __launch_bounds__(64) k_states(DevBatch b) {
   const double interp = (double)op.interpolation_distance;
   uint32_t ns = 0, last = 0;              // states so far, index of the last state
   float llon = 0.f, llat = 0.f;           // coordinates of the last state
+  double lsin = 0.0, lcos = 0.0;          // and the sin / cos of its latitude (lat_sin / lat_cos)
   float c1lo = 0.f, c1la = 0.f, c2lo = 0.f, c2la = 0.f;   // points c0-1, c0-2
   // each chunk's coordinates load one chunk ahead, unconditionally at a clamped index (a
   // conditional load would be waited on where it is merged: a long trace's chunks then each
   // paid a memory round trip before their first instruction)
   const uint32_t nl = n ? n - 1u : 0u;
   float nlo = b.lon[o + min((uint32_t)lane, nl)], nla = b.lat[o + min((uint32_t)lane, nl)];
+  // a chunk's stores are issued at the top of the next chunk, before its prefetch: vmcnt counts
+  // loads and stores in issue order, so stores issued after a prefetch would make the next
+  // chunk's wait for that prefetch wait for them too
+  bool w_slot = false, w_state = false, w_gc = false;
+  uint32_t w_i = 0, w_si = 0;
+  double w_gcv = 0.0;
   for (uint32_t c0 = 0; c0 < n; c0 += 64) {
     const uint32_t i = c0 + lane, m = min(64u, n - c0);
     const bool act = i < n;
-    const float lo = act ? nlo : 0.f, la = act ? nla : 0.f;
+    float lo = act ? nlo : 0.f, la = act ? nla : 0.f;
+    // the previous prefetch is consumed here, before the stores below are issued (its wait then
+    // waits for nothing newer) and before the next prefetch (whose loads can then land in the
+    // same registers instead of being copied at the back edge, a copy that waits for them)
+    __asm__ volatile("" : "+v"(lo), "+v"(la) : : "memory");
+    if (w_slot) b.slot_trace[o + w_i] = k;
+    if (w_state) b.state_orig[o + w_si] = w_i;
+    if (w_gc) b.gc[o + w_si] = w_gcv;
+    __asm__ volatile("" : : : "memory");
     nlo = b.lon[o + min(i + 64u, nl)];
     nla = b.lat[o + min(i + 64u, nl)];
-    if (act) b.slot_trace[o + i] = k;
+    w_slot = act;
+    w_i = i;
     float lo1 = __shfl_up(lo, 1, 64), la1 = __shfl_up(la, 1, 64);
     float lo2 = __shfl_up(lo, 2, 64), la2 = __shfl_up(la, 2, 64);
     if (lane == 0) { lo1 = c1lo; la1 = c1la; lo2 = c2lo; la2 = c2la; }
@@ -345,8 +367,14 @@ __global__ void __launch_bounds__(64) k_states(DevBatch b) {
       // last state at once (one vector distance, the same function the one-point test used);
       // the first that is far enough is the next state, the ones before it are skipped
       float plo = llon, pla = llat;
-      if (last >= c0) { plo = lane_f(lo, last - c0); pla = lane_f(la, last - c0); }
-      const double dv = gc_distance(plo, pla, lo, la);
+      double ps = lsin, pc = lcos;
+      if (last >= c0) {
+        plo = lane_f(lo, last - c0); pla = lane_f(la, last - c0);
+        ps = lane_d(s0, last - c0); pc = lane_d(k0, last - c0);
+      }
+      // gc_distance(plo, pla, lo, la) with both latitudes' sin / cos already at hand (the same
+      // functions of the same floats: the same bits)
+      const double dv = gc_trig(plo, pla, ps, pc, lo, la, s0, k0);
       const unsigned long long far = __ballot(act && !(dv < interp)) & (~0ull << q);
       if (!far) { q = m; break; }   // the rest of the chunk is skipped
       const uint32_t nq = (uint32_t)__builtin_ctzll(far);
@@ -355,22 +383,31 @@ __global__ void __launch_bounds__(64) k_states(DevBatch b) {
       if (lane == (int)nq) dx = dv;
       q = nq + 1;
     }
-    if ((st >> lane) & 1ull) {
+    w_state = ((st >> lane) & 1ull) != 0ull;
+    w_gc = false;
+    if (w_state) {
       const unsigned long long below = st & ((1ull << lane) - 1ull);
       const uint32_t si = ns + (uint32_t)__popcll(below);
-      b.state_orig[o + si] = i;
+      w_si = si;   // state_orig[o + si] = i
       // gc from the previous state (the distance the rule just tested: d1, d2 or the explicit
       // one); k_trans_count and K3 read it instead of measuring it again
       if (si > 0) {
         const uint32_t prev = below ? c0 + 63u - (uint32_t)__builtin_clzll(below) : last0;
-        b.gc[o + si] = i - prev == 1u ? d1 : (i - prev == 2u ? d2 : dx);
+        w_gc = true;
+        w_gcv = i - prev == 1u ? d1 : (i - prev == 2u ? d2 : dx);
       }
     }
     ns += (uint32_t)__popcll(st);
-    if (last >= c0) { llon = lane_f(lo, last - c0); llat = lane_f(la, last - c0); }
+    if (last >= c0) {
+      llon = lane_f(lo, last - c0); llat = lane_f(la, last - c0);
+      lsin = lane_d(s0, last - c0); lcos = lane_d(k0, last - c0);
+    }
     c1lo = lane_f(lo, 63); c1la = lane_f(la, 63);
     c2lo = lane_f(lo, 62); c2la = lane_f(la, 62);
   }
+  if (w_slot) b.slot_trace[o + w_i] = k;
+  if (w_state) b.state_orig[o + w_si] = w_i;
+  if (w_gc) b.gc[o + w_si] = w_gcv;
   if (lane == 0) b.n_states[k] = ns;
 }
 
@@ -3263,7 +3300,7 @@ __device__ void v3_backtrace(const DevBatch& b, Vit3Smem& sm, uint32_t o, uint32
 template <int W, bool TURN>
 __device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, int lane, uint32_t j0, uint32_t KB, uint32_t KA,
                                                       uint32_t rel, double gcl, double inv_beta, double inv2s2, int cb,
-                                                      uint32_t t) {
+                                                      uint32_t t, double em4) {
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
   const uint32_t i = (uint32_t)lane & (W - 1), j = j0 + ((uint32_t)lane / W);
   const bool valid = i < KA && j < KB;
@@ -3281,7 +3318,9 @@ __device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, int lane, ui
   const int arg = g ? __builtin_ctz(g) : -1;
   const bool head = i == 0u && j < KB;
   if (head) {
-    const double em = (double)sm.sq[t][j] * inv2s2;
+    // W = 4 (one pass, j = lane / 4): the emission was read at the top of the layer, off the
+    // chain of this layer's cost reads
+    const double em = W == 4 ? em4 : (double)sm.sq[t][j] * inv2s2;
     sm.cost[cb ^ 1][j] = arg >= 0 ? m + em : INF;
     reinterpret_cast<uint8_t*>(&sm.bpo[t])[j] = arg >= 0 ? (uint8_t)arg : (uint8_t)255;
   }
@@ -3328,18 +3367,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
       const uint32_t kr = (uint32_t)__builtin_amdgcn_readlane((int)cur.kbrel, (int)t);
       const uint32_t KB = kr & 0xffu, rel = kr >> 8;
       const double gcl = readlane_d(cur.gc, t);
+      const double em4 = (double)sm.sq[t][lane >> 2] * inv2s2;   // target lane / 4 of a W = 4 pass
       if (lane == 0) sm.bpo[t] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
       bool start = !prev_ok || (s > 0 && gcl > brk);
       if (KB && !start) {
         unsigned long long any = 0ull;
         if (prevK <= 4u) {
-          any = v3_pass<4, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          any = v3_pass<4, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t, em4);
         } else if (prevK <= 8u) {
-          any = v3_pass<8, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
-          if (KB > 8u) any |= v3_pass<8, TURN>(sm, lane, 8u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+          any = v3_pass<8, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t, em4);
+          if (KB > 8u) any |= v3_pass<8, TURN>(sm, lane, 8u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t, em4);
         } else {
           for (uint32_t j0 = 0; j0 < KB; j0 += 4u)
-            any |= v3_pass<16, TURN>(sm, lane, j0, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t);
+            any |= v3_pass<16, TURN>(sm, lane, j0, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t, em4);
         }
         if (any == 0ull) start = true;   // no valid transition into this layer
       }
@@ -3675,6 +3715,25 @@ __device__ __forceinline__ bool piece_slow(unsigned long long md, double mtb, do
   return dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
 }
 
+// a traversal record's transition slot and the slot's data K4 reads (k_seg_wave's prefetch)
+struct K4Slot {
+  uint32_t l, ns, toff, pofs, D;
+  uint2 sab;
+  double ta, tbs;
+};
+__device__ __forceinline__ K4Slot k4_slot(const DevBatch& b, uint32_t l) {
+  K4Slot s;
+  s.l = l;
+  s.ns = b.path_cnt[l];
+  s.toff = b.trav_off[l];
+  s.pofs = b.path_off[l];
+  s.D = b.route_dist[l];
+  s.sab = b.path_sab[l];
+  s.ta = b.state_time[l - 1];   // a record's slot is a transition's target: l >= 1
+  s.tbs = b.state_time[l];
+  return s;
+}
+
 __global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const uint32_t* rec_slot, uint32_t total_arg) {
   const uint32_t k = blockIdx.x;
   if (k >= b.T || small_abort(b)) return;
@@ -3697,26 +3756,41 @@ __global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const u
   unsigned long long r_tot = 0, r_q = 0, p_md = 0;
   unsigned long long carry_x = 0;   // route distance of the transition that straddles the window start
   uint32_t runs = 0;
+  // The record build is a chain of dependent loads (record -> slot -> its transition's data ->
+  // path edge -> edge record).  Its first two links run ahead: a window's slots are loaded two
+  // windows early and their transition data one window early, every load unconditional at a
+  // clamped record index (a clamped lane's values are never used), and the next window's data is
+  // taken into registers before this window's segments are stored (loads and stores share
+  // vmcnt, in issue order: a wait after the stores would wait for them too).
+  const uint32_t rl = Re > 0u ? Re - 1u : 0u;
+  K4Slot cur{};
+  uint32_t la = 0;
+  if (Rb < Re) {
+    cur = k4_slot(b, rec_slot[min(Rb + (uint32_t)lane, rl)]);
+    la = rec_slot[min(Rb + 64u + (uint32_t)lane, rl)];
+  }
   for (uint32_t c0 = Rb; c0 < Re; c0 += 64) {
     const uint32_t n = min(64u, Re - c0);
     const bool last = c0 + n == Re;
     const bool act = (uint32_t)lane < n;
     // ---- build one traversal record per lane (seg_build_slot's arithmetic)
-    uint32_t l = 0, q = 0, e = 0, b0 = 0, b1 = 0, L = 0, sd = kNone, soff = 0, way = 0, slotf = 0;
-    double ta = 0.0, tbs = 0.0;
-    uint32_t D = 0;
+    const uint32_t l = cur.l;
+    const uint32_t q_ld = min(c0 + (uint32_t)lane, rl) - cur.toff;
+    const uint32_t q = act ? q_ld : 0u;
+    const uint32_t* pe = cur.ns <= (uint32_t)kInlinePath ? b.path_inline + (uint64_t)l * kInlinePath : b.path_pool + cur.pofs;
+    const uint32_t e_ld = pe[q_ld];
+    const uint4 sr = g.seg_rec[e_ld];
+    // the next windows' links (see above), issued behind this window's own loads
+    __asm__ volatile("" : : : "memory");
+    const K4Slot nxt = k4_slot(b, la);
+    la = rec_slot[min(c0 + 128u + (uint32_t)lane, rl)];
+    uint32_t e = 0, b0 = 0, b1 = 0, L = 0, sd = kNone, soff = 0, way = 0, slotf = 0;
+    const double ta = act ? cur.ta : 0.0, tbs = act ? cur.tbs : 0.0;
+    const uint32_t D = act ? cur.D : 0u;
     if (act) {
-      const uint32_t r = c0 + lane;
-      l = rec_slot[r];
-      const uint32_t ns = b.path_cnt[l];
-      q = r - b.trav_off[l];
-      const uint2 sab = b.path_sab[l];
-      ta = b.state_time[l - 1];
-      tbs = b.state_time[l];
-      D = b.route_dist[l];
-      const uint32_t* pe = ns <= (uint32_t)kInlinePath ? b.path_inline + (uint64_t)l * kInlinePath : b.path_pool + b.path_off[l];
-      e = pe[q];
-      const uint4 sr = g.seg_rec[e];
+      const uint32_t ns = cur.ns;
+      const uint2 sab = cur.sab;
+      e = e_ld;
       L = sr.x & 0x3fffffffu;
       const bool rev = (sr.x >> 31) != 0u;
       b1 = L;
@@ -3791,6 +3865,10 @@ __global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const u
     const uint32_t f_soff = rs >= 0 ? h_soff : r_fsoff;
     const double f_tb = rs >= 0 ? h_tb : r_tb;
     const bool f_int = rs >= 0 ? (f_slot & kTravInternal) != 0u : r_int;
+    // the next window's slot data into registers now, before this window's stores
+    cur = nxt;
+    __asm__ volatile("" : "+v"(cur.l), "+v"(cur.ns), "+v"(cur.toff), "+v"(cur.pofs), "+v"(cur.D), "+v"(cur.sab.x),
+                     "+v"(cur.sab.y), "+v"(cur.ta), "+v"(cur.tbs) : : "memory");
     // the run carried in closes before this window's first kept record when that is a head
     // (or, at the trace's end, when the window keeps nothing)
     if (r_open && ((K != 0ull && ((HD >> __builtin_ctzll(K)) & 1ull)) || (K == 0ull && last))) {

@@ -253,8 +253,9 @@ void derive_info(const std::map<std::string, std::string>& t, uint32_t& info_f, 
   // a roundabout is one-way in its drawing direction unless tagged otherwise (OSM convention)
   const std::string* jc = tag(t, "junction");
   const bool ring = jc && (*jc == "roundabout" || *jc == "circular") && !(ow && *ow == "no");
-  if (ring || (ow && (*ow == "yes" || *ow == "true" || *ow == "1"))) ar &= kAccessPedestrian;
-  else if (ow && *ow == "-1") af &= kAccessPedestrian;
+  // an explicit oneway=-1 wins over the roundabout's implied drawing direction
+  if (ow && *ow == "-1") af &= kAccessPedestrian;
+  else if (ring || (ow && (*ow == "yes" || *ow == "true" || *ow == "1"))) ar &= kAccessPedestrian;
   uint32_t flags = 0;
   if (hw == "service") flags |= kFlagService;
   if (hw.size() > 5 && hw.compare(hw.size() - 5, 5, "_link") == 0) flags |= kFlagInternal;

@@ -87,6 +87,24 @@ def test_generic_osm_is_split_at_intersections(built_lib, tmp_path):
     assert set(acc[ways == 300].tolist()) == {4}
 
 
+def test_roundabout_oneway_tags(built_lib, tmp_path):
+    """A roundabout is one-way in its drawing direction unless tagged: oneway=no keeps both
+    directions, and an explicit oneway=-1 wins over the implied direction."""
+    for tagv, fwd_auto, rev_auto in ((None, True, False), ("no", True, True), ("-1", False, True), ("yes", True, False)):
+        ow = '' if tagv is None else '<tag k="oneway" v="%s"/>' % tagv
+        x = tmp_path / ("r%s.osm" % tagv)
+        x.write_text(GENERIC.replace('<tag k="highway" v="residential"/><tag k="oneway" v="yes"/>',
+                                     '<tag k="highway" v="residential"/><tag k="junction" v="roundabout"/>' + ow))
+        g = graphfile.load(world.import_osm(str(x), str(tmp_path / ("r%s.rmg" % tagv)), cell_m=50.0))
+        e = g["edges"].reshape(-1, 4)
+        acc = (e[:, 2] >> 16) & 7
+        for a, w, r in zip(acc, g["edge_way"], e[:, 3]):
+            if w != 200:
+                continue
+            assert bool(a & 1) == (rev_auto if (r & 1) else fwd_auto), (tagv, int(a), int(r))
+            assert a & 4   # pedestrians both ways
+
+
 def test_pbf_export_import_is_bit_identical(built_lib, tmp_path):
     """the world as OSM PBF — the input valhalla_build_tiles reads — comes back
     bit-identical, and carries the same elements as the XML export."""
