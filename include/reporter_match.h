@@ -179,6 +179,10 @@ int rm_engine_ball_stats(const rm_engine* e, int mode, double out[6]);
  * chosen at upload to minimise the items a default-radius query reads (RM_GRID_SPLIT overrides).
  * It changes which grid items are read, never which roads are found. */
 int rm_engine_grid_split(const rm_engine* e, uint32_t* f);
+/* K1's second grid (engine.hip Engine::k1_grid): its split f (0: none) and the batch query
+ * radius (m) from which a batch takes it instead of the default one.  New in round 5: no
+ * reference call site (the reference has no grid index; Valhalla's meili owns its own). */
+int rm_engine_grid_alt(const rm_engine* e, uint32_t* f, float* radius_m);
 /* turn rows (DESIGN.md §3 rule 3b) built so far: bit per travel mode, and each mode's build ms */
 int rm_engine_turn_rows(const rm_engine* e, uint32_t* mode_mask, double* build_ms /*5*/);
 /* Host-only: the grid refinement an engine would choose for a graph file. */

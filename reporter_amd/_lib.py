@@ -112,6 +112,7 @@ PROTOTYPES = [
     ("rm_engine_set_ball_radius", C.c_int, [P, C.c_double]),
     ("rm_engine_ball_stats", C.c_int, [P, C.c_int, P]),
     ("rm_engine_grid_split", C.c_int, [P, P]),
+    ("rm_engine_grid_alt", C.c_int, [P, P, P]),
     ("rm_engine_turn_rows", C.c_int, [P, P, P]),
     ("rm_engine_ball_lookup", C.c_int, [P, C.c_int, C.c_uint64, P, P, P, P]),
     ("rm_runner_route_tiers", C.c_int, [P, P]),

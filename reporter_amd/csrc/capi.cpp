@@ -1040,6 +1040,13 @@ int rm_engine_turn_rows(const rm_engine* e, uint32_t* mode_mask, double* build_m
     for (int m = 0; m < 5; ++m) build_ms[m] = e->e->turn_build_ms(m);
   });
 }
+int rm_engine_grid_alt(const rm_engine* e, uint32_t* f, float* radius_m) {
+  return guarded([&] {
+    *f = e->e->grid_alt_split();
+    *radius_m = e->e->grid_alt_radius();
+  });
+}
+
 int rm_engine_grid_split(const rm_engine* e, uint32_t* f) {
   return guarded([&] { *f = e->e->grid_split(); });
 }

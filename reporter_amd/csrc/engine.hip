@@ -3715,6 +3715,20 @@ __device__ __forceinline__ bool piece_slow(unsigned long long md, double mtb, do
   return dt > 0.0 && ((double)md * 0.01) / dt < kQueueSpeedMps;
 }
 
+// K4's report() epilogue (round 5: fused into k_seg_wave; report_wave below): the wave that
+// formed a trace's segments reports them at once, from L2, instead of a second launch of one
+// wave per trace re-reading them (k_report was 0.20 ms per 125 k C3 traces)
+struct ReportArgs {
+  double threshold;
+  uint32_t rmask, tmask;
+  uint32_t* hist;
+  unsigned long long* dur;
+  int on;
+};
+__device__ __forceinline__ ReportStats report_wave(const SegmentRec* segs, uint32_t n, bool has_pts, double end_time,
+                                                   double threshold, uint32_t rmask, uint32_t tmask, ReportRec* out,
+                                                   uint32_t* hist, unsigned long long* dur);
+
 // a traversal record's transition slot and the slot's data K4 reads (k_seg_wave's prefetch)
 struct K4Slot {
   uint32_t l, ns, toff, pofs, D;
@@ -3734,7 +3748,7 @@ __device__ __forceinline__ K4Slot k4_slot(const DevBatch& b, uint32_t l) {
   return s;
 }
 
-__global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const uint32_t* rec_slot, uint32_t total_arg) {
+__global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const uint32_t* rec_slot, uint32_t total_arg, ReportArgs ra) {
   const uint32_t k = blockIdx.x;
   if (k >= b.T || small_abort(b)) return;
   const uint32_t total = total_arg != kNone ? total_arg : (uint32_t)b.tot[2];   // kNone: a small run's
@@ -3915,6 +3929,15 @@ __global__ void __launch_bounds__(64) k_seg_wave(DevGraph g, DevBatch b, const u
     b.seg_base[k] = Rb;
     b.seg_cnt[k] = runs;
   }
+  if (ra.on) {
+    __threadfence_block();   // this wave's segment stores are visible to its loads
+    const ReportStats st = report_wave(b.segs + Rb, runs, o1 > o, o1 > o ? b.time[o1 - 1] : 0.0, ra.threshold, ra.rmask,
+                                       ra.tmask, b.reps + Rb, ra.hist, ra.dur);
+    if (lane == 0) {
+      b.rep_cnt[k] = (uint32_t)st.n_reports;
+      b.stats[k] = st;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -4027,21 +4050,6 @@ __device__ __forceinline__ ReportStats report_wave(const SegmentRec* segs, uint3
   st.n_reports = nrep;
   return st;
 }
-
-__global__ void __launch_bounds__(64) k_report(DevBatch b, double threshold, uint32_t rmask, uint32_t tmask,
-                                               uint32_t* hist, unsigned long long* dur) {
-  if (small_abort(b)) return;   // a gated-off small run: the host runs the batch again
-  for (uint32_t k = blockIdx.x; k < b.T; k += gridDim.x) {   // one block per trace (a grid-stride loop over fewer blocks was slower)
-    const uint32_t o = b.trace_off[k], npts = b.trace_off[k + 1] - o;
-    const ReportStats st = report_wave(b.segs + b.seg_base[k], b.seg_cnt[k], npts > 0, npts ? b.time[o + npts - 1] : 0.0,
-                                       threshold, rmask, tmask, b.reps + b.seg_base[k], hist, dur);
-    if (threadIdx.x == 0) {
-      b.rep_cnt[k] = (uint32_t)st.n_reports;
-      b.stats[k] = st;
-    }
-  }
-}
-
 
 // report() over host-supplied segment lists (rm_report_segments): per-trace end time,
 // threshold and level masks; reports of trace k start at seg_off[k]
@@ -4396,6 +4404,10 @@ T* upload(std::vector<void*>& list, const std::vector<T>& v) {
 // 11.9 -> 6.1; 3 and 4 list long pieces in too many cells).
 uint32_t choose_grid_split(const Graph& g) {
   if (const char* e = std::getenv("RM_GRID_SPLIT")) return (uint32_t)std::min(8, std::max(1, std::atoi(e)));
+  return choose_grid_split_for(g, 50.f);
+}
+
+uint32_t choose_grid_split_for(const Graph& g, float radius_m) {
   const GridIndex& gi = g.grid;
   const size_t n = gi.cell_item.size();
   if (n == 0) return 1;
@@ -4408,7 +4420,7 @@ uint32_t choose_grid_split(const Graph& g) {
     const VertRec& A = g.verts[v];
     const VertRec& B = g.verts[v + 1];
     const float lon = 0.5f * (A.lon + B.lon), lat = 0.5f * (A.lat + B.lat);
-    const float pad = 50.f * 1.01f + 0.5f;   // K1's padded box for the default radius
+    const float pad = radius_m * 1.01f + 0.5f;   // K1's padded box for the radius
     const float qlon = pad / meters_per_lon(lat), qlat = pad / (float)kMetersPerDegLat;
     const double b0 = (double)(lon - qlon), b1 = (double)(lon + qlon), c0 = (double)(lat - qlat), c1 = (double)(lat + qlat);
     // distinct items of the graph-grid cells the box touches: a superset of any finer grid's
@@ -4526,21 +4538,27 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   dg_.verts = (const uint4*)upload(allocs_, g.verts);
   dg_.seg_id = (const unsigned long long*)upload(allocs_, g.seg_id);
   dg_.seg_len = upload(allocs_, g.seg_len_cm);
-  // K1's grid: the graph's own, or each of its cells split f x f (choose_grid_split)
-  GridIndex split;
+  // K1's grid: the graph's own, or each of its cells split f x f (choose_grid_split), chosen for
+  // the default 50 m query; and when wider queries (a batch radius of 75 m and up) read fewer
+  // items on another split, that grid too (CITY30's 100 m queries, f 1 vs 2)
+  if (g.num_roads() >= (1u << 29)) throw std::runtime_error("graph has too many roads (limit 2^29)");
   grid_split_ = choose_grid_split(g);
-  if (grid_split_ > 1) {
-    split.lon0 = g.grid.lon0; split.lat0 = g.grid.lat0;
-    split.dlon = g.grid.dlon / grid_split_; split.dlat = g.grid.dlat / grid_split_;
-    split.ncx = g.grid.ncx * grid_split_; split.ncy = g.grid.ncy * grid_split_;
-    build_grid_index(g.verts, split);
-  }
-  const GridIndex& gk = grid_split_ > 1 ? split : g.grid;
-  dg_.cell_off = upload(allocs_, gk.cell_off);
-  dg_.cell_item = nullptr;   // K1 reads the self-contained records below
+  uint32_t alt = grid_split_;
   {
+    const char* e = std::getenv("RM_GRID_ALT");   // 0: one grid (A/B)
+    if (!std::getenv("RM_GRID_SPLIT") && !(e && *e == '0')) alt = choose_grid_split_for(g, 100.f);
+  }
+  auto build_k1_grid = [&](uint32_t f, K1Grid& out) {
+    GridIndex split;
+    if (f > 1) {
+      split.lon0 = g.grid.lon0; split.lat0 = g.grid.lat0;
+      split.dlon = g.grid.dlon / f; split.dlat = g.grid.dlat / f;
+      split.ncx = g.grid.ncx * f; split.ncy = g.grid.ncy * f;
+      build_grid_index(g.verts, split);
+    }
+    const GridIndex& gk = f > 1 ? split : g.grid;
+    out.cell_off = upload(allocs_, gk.cell_off);
     // K1 reads cell items as self-contained records (no item -> vertex -> road chain)
-    if (g.num_roads() >= (1u << 29)) throw std::runtime_error("graph has too many roads (limit 2^29)");
     auto acc_of = [&](uint32_t e) { return e == kNone ? 0u : edge_access(g.edges[e].info); };
     std::vector<uint32_t> rec(8 * (size_t)gk.cell_item.size());
     for (size_t it = 0; it < gk.cell_item.size(); ++it) {
@@ -4554,7 +4572,21 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
       std::memcpy(r + 2, &B.lon, 4); std::memcpy(r + 3, &B.lat, 4);
       r[4] = A.cum_cm; r[5] = B.cum_cm; r[6] = road | (acc << 29); r[7] = v;
     }
-    dg_.cell_rec = (const uint4*)upload(allocs_, rec);
+    out.cell_rec = (const uint4*)upload(allocs_, rec);
+    out.lon0 = gk.lon0; out.lat0 = gk.lat0; out.dlon = gk.dlon; out.dlat = gk.dlat;
+    out.ncx = gk.ncx; out.ncy = gk.ncy; out.split = f;
+  };
+  build_k1_grid(grid_split_, grids_[0]);
+  if (alt != grid_split_) {
+    build_k1_grid(alt, grids_[1]);
+    n_grids_ = 2;
+    grid_alt_radius_ = 75.f;
+  }
+  const K1Grid& gk = grids_[0];
+  dg_.cell_off = gk.cell_off;
+  dg_.cell_item = nullptr;   // K1 reads the self-contained records
+  dg_.cell_rec = gk.cell_rec;
+  {
     // per-road record: both endpoints, length and both directed edges with their info words
     std::vector<uint32_t> rr(8 * (size_t)g.num_roads());
     for (uint32_t r = 0; r < g.num_roads(); ++r) {
@@ -4610,6 +4642,13 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
     RM_HIP(hipGetLastError());
   }
   RM_HIP(hipDeviceSynchronize());
+}
+
+void Engine::k1_grid(float radius_m, DevGraph& g) const {
+  const K1Grid& k = (n_grids_ > 1 && radius_m >= grid_alt_radius_) ? grids_[1] : grids_[0];
+  g.cell_off = k.cell_off; g.cell_rec = k.cell_rec;
+  g.lon0 = k.lon0; g.lat0 = k.lat0; g.dlon = k.dlon; g.dlat = k.dlat;
+  g.ncx = k.ncx; g.ncy = k.ncy;
 }
 
 Engine::~Engine() {
@@ -5144,9 +5183,16 @@ void Matcher::check_batch(uint32_t T, const uint32_t* trace_off, const MatchOpti
     if (trace_off[k + 1] < trace_off[k]) throw std::runtime_error("trace offsets not monotone");
     if (trace_opt[k] >= n_opts) throw std::runtime_error("trace option index out of range");
   }
+  scan_options(opts, n_opts);
+}
+
+// a batch's option sets, checked; sets mode_mask_, turn_mask_ and batch_radius_
+void Matcher::scan_options(const MatchOptions* opts, uint32_t n_opts) {
   mode_mask_ = 0;
   turn_mask_ = 0;
+  batch_radius_ = 0.f;
   for (uint32_t q = 0; q < n_opts; ++q) {
+    if (opts[q].search_radius > batch_radius_) batch_radius_ = std::min(opts[q].search_radius, kMaxSearchRadius);
     if (opts[q].mode < 0 || opts[q].mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
     // K3 divides by both (a zero 1/beta would turn an invalid route's +inf into NaN)
     if (!(opts[q].sigma_z > 0.f) || !std::isfinite(opts[q].sigma_z)) throw std::runtime_error("sigma_z must be positive and finite");
@@ -5452,7 +5498,21 @@ static uint32_t tier_grid(uint64_t P, uint32_t full) {
 // an upper bound cannot cover -- the path pool overflowing, a search handed to the global tier
 // before its scratch exists -- gates K4 and the report off on the device (small_abort) and
 // returns false: the caller then runs the batch the ordinary way.  Same kernels, same results.
-constexpr uint64_t kSmallWaveK1 = 32768;   // small runs up to this many points take K1 a wave per state
+// small runs up to this many points take K1 a wave per state (latency: a lone 1,000-point trace
+// 35 -> 10 us; throughput: the lane tier, C2 0.84 ms against 6.45 ms all in the wave tier)
+constexpr uint64_t kSmallWaveK1 = 4096;
+
+static ReportArgs report_args(const RunParams& rp) {
+  ReportArgs a;
+  a.threshold = rp.threshold_sec; a.rmask = rp.report_mask; a.tmask = rp.transition_mask;
+  a.hist = rp.hist; a.dur = rp.dur; a.on = rp.do_report ? 1 : 0;
+  return a;
+}
+
+void Matcher::zero_hist(const RunParams& rp) {
+  if (rp.hist) RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)eng_->n_segments() * kHistBins * sizeof(uint32_t), stream_));
+  if (rp.dur) RM_HIP(hipMemsetAsync(rp.dur, 0, (size_t)eng_->n_segments() * 8u, stream_));
+}
 bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   const uint32_t T = n_traces_;
   const uint64_t P = n_points_;
@@ -5482,11 +5542,13 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   hipLaunchKernelGGL(k_states, dim3(T), dim3(64), 0, st, v);
   toc(kKStates);
   tic(kKCandidates);
+  DevGraph gk = g;   // K1's grid for the batch's radius
+  eng_->k1_grid(batch_radius_, gk);
   if (P <= kSmallWaveK1) {   // one wave per state
-    hipLaunchKernelGGL(k_candidates_wave, dim3((uint32_t)P), dim3(64), 0, st, g, v, 1);
+    hipLaunchKernelGGL(k_candidates_wave, dim3((uint32_t)P), dim3(64), 0, st, gk, v, 1);
   } else {
-    hipLaunchKernelGGL(k_candidates_lane, dim3(count_grid), dim3(256), 0, st, g, v);
-    hipLaunchKernelGGL(k_candidates_wave, dim3(tgrid(2048)), dim3(64), 0, st, g, v, 0);
+    hipLaunchKernelGGL(k_candidates_lane, dim3(count_grid), dim3(256), 0, st, gk, v);
+    hipLaunchKernelGGL(k_candidates_wave, dim3(tgrid(2048)), dim3(64), 0, st, gk, v, 0);
   }
   toc(kKCandidates);
   tic(kKScan);
@@ -5534,17 +5596,9 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot_part);
   hipLaunchKernelGGL(k_path_apply_small, dim3(sum_grid), dim3(256), 0, st, v, (const unsigned long long*)w.tot_part,
                      sum_grid, w.tot64, w.rec_slot);
-  hipLaunchKernelGGL(k_seg_wave, dim3(T), dim3(64), 0, st, g, v, (const uint32_t*)w.rec_slot, kNone);
+  if (rp.do_report && rp.zero_hist) zero_hist(rp);
+  hipLaunchKernelGGL(k_seg_wave, dim3(T), dim3(64), 0, st, g, v, (const uint32_t*)w.rec_slot, kNone, report_args(rp));
   toc(kKSegments);
-  if (rp.do_report) {
-    if (rp.hist && rp.zero_hist)
-      RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)eng_->n_segments() * kHistBins * sizeof(uint32_t), st));
-    if (rp.dur && rp.zero_hist) RM_HIP(hipMemsetAsync(rp.dur, 0, (size_t)eng_->n_segments() * 8u, st));
-    tic(kKReport);
-    hipLaunchKernelGGL(k_report, dim3(T), dim3(64), 0, st, v, rp.threshold_sec, rp.report_mask,
-                       rp.transition_mask, rp.hist, rp.dur);
-    toc(kKReport);
-  }
   // the reply's segments, compacted per trace on the device (get_segments then copies them down)
   constexpr uint32_t kSegWords = sizeof(SegmentRec) / 8;
   const size_t offb = ((T + 1) * 4ull + 7) & ~(size_t)7;
@@ -5601,7 +5655,8 @@ void Matcher::run_device(const RunParams& rp) {
   if (!hctl_) RM_HIP(hipHostMalloc((void**)&hctl_, 32 * sizeof(uint32_t), hipHostMallocDefault));
   unsigned long long* htot = reinterpret_cast<unsigned long long*>(hctl_ + 16);
   seg_prefetched_ = false;
-  if (P <= small_batch_points() && run_small(rp, g)) return;
+  // (a forced locality order takes the ordinary path: the small one runs in slot order)
+  if (P <= small_batch_points() && locality_ <= 0 && run_small(rp, g)) return;
   // (k_states zeroes the control words and the per-trace error bits)
   DevBatch v = make_view(w, in_, T, P);
   const uint32_t count_grid = (uint32_t)((P + 255) / 256);
@@ -5630,8 +5685,15 @@ void Matcher::run_device(const RunParams& rp) {
     toc(kKLocality);
   }
   tic(kKCandidates);
-  hipLaunchKernelGGL(k_candidates_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, g, v, 0);
+  DevGraph gk = g;   // K1's grid for the batch's radius
+  eng_->k1_grid(batch_radius_, gk);
+  static const bool k1_wave_all = [] { const char* e = std::getenv("RM_K1_WAVE_ALL"); return e && *e == '1'; }();
+  if (k1_wave_all) {   // A/B: every state in the wave tier
+    hipLaunchKernelGGL(k_candidates_wave, dim3((uint32_t)std::min<uint64_t>(P, 1u << 20)), dim3(64), 0, st, gk, v, 1);
+  } else {
+    hipLaunchKernelGGL(k_candidates_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, gk, v);
+    hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, gk, v, 0);
+  }
   toc(kKCandidates);
   tic(kKScan);
   hipLaunchKernelGGL(k_trans_count, dim3(count_grid), dim3(256), 0, st, v, w.tot_part);
@@ -5775,22 +5837,15 @@ void Matcher::run_device(const RunParams& rp) {
   if (seg_total >= kMaxRecords) throw BatchTooLarge("batch too large (path edges >= 1.7e9); split it");
   n_path_ = seg_total;  // one traversal record (and at most one segment) per chosen path edge
   ensure_segs(seg_total);
-  v.segs = w.segs; v.reps = w.reps;
+  v.segs = w.segs; v.reps = w.reps; v.seg_cap = w.cap_segs;
   tic(kKSegments);
+  if (rp.do_report && rp.zero_hist) zero_hist(rp);
   if (T) {
     hipLaunchKernelGGL(k_rec_slot, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v, w.rec_slot);
-    hipLaunchKernelGGL(k_seg_wave, dim3(T), dim3(64), 0, st, g, v, (const uint32_t*)w.rec_slot, (uint32_t)seg_total);
+    hipLaunchKernelGGL(k_seg_wave, dim3(T), dim3(64), 0, st, g, v, (const uint32_t*)w.rec_slot, (uint32_t)seg_total,
+                       report_args(rp));
   }
   toc(kKSegments);
-  if (rp.do_report) {
-    if (rp.hist && rp.zero_hist)
-      RM_HIP(hipMemsetAsync(rp.hist, 0, (size_t)eng_->n_segments() * kHistBins * sizeof(uint32_t), st));
-    if (rp.dur && rp.zero_hist) RM_HIP(hipMemsetAsync(rp.dur, 0, (size_t)eng_->n_segments() * 8u, st));
-    tic(kKReport);
-    hipLaunchKernelGGL(k_report, dim3(T), dim3(64), 0, st, v, rp.threshold_sec, rp.report_mask,
-                       rp.transition_mask, rp.hist, rp.dur);
-    toc(kKReport);
-  }
   RM_HIP(hipGetLastError());
   RM_HIP(hipMemcpyAsync(hctl_, w.ctl, kCtlWords * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   sync();

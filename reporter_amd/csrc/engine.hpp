@@ -345,6 +345,7 @@ class Matcher {
   void ensure(uint64_t points, uint32_t traces, uint32_t nopts);
   void check_batch(uint32_t T, const uint32_t* trace_off, const MatchOptions* opts, uint32_t n_opts,
                    const uint32_t* trace_opt);
+  void scan_options(const MatchOptions* opts, uint32_t n_opts);
   char* jdev_ = nullptr;        // device JSON path: trace-array bytes (grow-only), per-trace spans,
   uint64_t jcap_ = 0;           // flags and first / last times
   void* jspan_ = nullptr;
@@ -375,6 +376,7 @@ class Matcher {
   void grow_dl_dev(size_t need);
   // small batches (run_small): no size read-back between the stages, one upload, one read-back
   bool run_small(const RunParams& rp, const DevGraph& g);
+  void zero_hist(const RunParams& rp);
   void use_ws_inputs();
   void ensure_pack(uint64_t bytes);
 
@@ -406,6 +408,7 @@ class Matcher {
   bool from_points_ = false;
   uint32_t mode_mask_ = 0;   // travel modes of the batch (bit per Mode): which route balls K2 needs
   uint32_t turn_mask_ = 0;   // modes of the batch with a turn_penalty_factor > 0: turn rows, route_d
+  float batch_radius_ = 0.f; // the batch's largest search_radius (m): K1's grid (Engine::k1_grid)
   void ensure_points(uint64_t n, uint32_t n_uuids, uint32_t n_opts);
   void ensure_rows(uint64_t n, uint32_t traces);
   struct Ev { hipEvent_t a, b; int k; };
@@ -416,6 +419,16 @@ class Matcher {
 
 // K1's grid refinement for a graph (host only; engine.hip): each graph-file cell split f x f
 uint32_t choose_grid_split(const Graph& g);
+// the same for queries of radius_m (the padded box of that radius)
+uint32_t choose_grid_split_for(const Graph& g, float radius_m);
+
+// one K1 grid in HBM: its cell ranges, self-contained cell records and geometry
+struct K1Grid {
+  const uint32_t* cell_off = nullptr;
+  const uint4* cell_rec = nullptr;
+  double lon0 = 0, lat0 = 0, dlon = 0, dlat = 0;
+  uint32_t ncx = 0, ncy = 0, split = 1;
+};
 
 class Engine {
  public:
@@ -449,6 +462,11 @@ class Engine {
   void ball_lookup(int mode, uint64_t n, const uint32_t* from, const uint32_t* road, uint64_t* keys, uint8_t* preds);
   // K1's grid: each cell of the graph's grid split f x f (1 = the graph's grid)
   uint32_t grid_split() const { return grid_split_; }
+  // K1's grid for a batch whose largest query radius is radius_m: the default one, or a second
+  // split built when wider queries read fewer items on it (grid_alt_radius() and up)
+  void k1_grid(float radius_m, DevGraph& g) const;
+  uint32_t grid_alt_split() const { return n_grids_ > 1 ? grids_[1].split : 0u; }
+  float grid_alt_radius() const { return grid_alt_radius_; }
   // locality order by default (Matcher::set_locality -1): graphs whose route tables and cell
   // records outgrow the L2s; and the shift from K1 grid cells to the coarse sort cells (~500 m)
   bool locality_default() const { return locality_default_; }
@@ -465,6 +483,9 @@ class Engine {
   uint32_t ball_built_ = 0;             // mode bits
   uint32_t ball_gpu_ = 0;               // mode bits built on the GPU
   uint32_t grid_split_ = 1;
+  K1Grid grids_[2];
+  int n_grids_ = 1;
+  float grid_alt_radius_ = 0.f;         // batches with a query radius from this take grids_[1]
   bool locality_default_ = false;
   uint32_t locality_shift_ = 0, locality_bits_ = 0;
   uint64_t ball_bytes_ = 0;             // bytes of the tables built so far (all modes)

@@ -361,11 +361,7 @@ void Matcher::run_points(const PointsDesc& pd, const RunParams& rp) {
   if (n == 0) { n_traces_ = 0; n_points_ = 0; n_trans_ = 0; n_path_ = 0; seg_used_ = 0; return; }
   if (n >= 0xffffffffull) throw std::runtime_error("point batch too large (>= 2^32 points)");
   if (pd.n_opts == 0 || !pd.opts) throw std::runtime_error("point batch needs at least one option set");
-  mode_mask_ = 0;
-  for (uint32_t q = 0; q < pd.n_opts; ++q) {
-    if (pd.opts[q].mode < 0 || pd.opts[q].mode > kModePedestrian) throw std::runtime_error("unknown travel mode");
-    mode_mask_ |= 1u << pd.opts[q].mode;
-  }
+  scan_options(pd.opts, pd.n_opts);   // the checks and batch masks of check_batch (turn costs too)
   double tmin = pd.time[0], tmax = pd.time[0];
   for (uint64_t k = 0; k < n; ++k) {
     if (pd.uuid[k] >= pd.n_uuids) throw std::runtime_error("point vehicle index out of range");

@@ -102,6 +102,13 @@ class Engine:
         _lib.check(_lib.lib().rm_engine_grid_split(self._h, out.ctypes.data))
         return int(out[0])
 
+    def grid_alt(self):
+        """K1's second grid: (split f, batch radius in m from which it is used); (0, 0) if none."""
+        f = np.zeros(1, np.uint32)
+        r = np.zeros(1, np.float32)
+        _lib.check(_lib.lib().rm_engine_grid_alt(self._h, f.ctypes.data, r.ctypes.data))
+        return int(f[0]), float(r[0])
+
     def ball_lookup(self, mode, from_nodes, roads, preds=False):
         """Keys (n, 2) from each node to the two endpoints of each road through the engine's
         device tables of `mode` (all-ones outside the ball / without a table); with preds, also

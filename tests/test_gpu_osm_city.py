@@ -13,7 +13,8 @@ one node pair, a bridged trunk road, and roads without OSMLR coverage.
 import numpy as np
 import pytest
 
-from parity_util import match_and_compare
+import meili_oracle as mo
+from parity_util import compare_all, match_and_compare
 from reporter_amd import engine, graphfile, world
 
 pytestmark = pytest.mark.gpu
@@ -82,3 +83,32 @@ def test_city_modes_sigma(city):
                           hist=True)
     assert c["traces"] == 9 * per and c["segments"] > 1_000, c
     print("city modes parity", c)
+
+
+def test_second_k1_grid_for_wide_queries(built_lib, city, monkeypatch):
+    """K1's grid is chosen per batch radius.  On the city the 50 m default
+    and 100 m queries prefer different splits, so the engine keeps both; a 100 m batch takes the
+    second one and every stage still equals the oracle (and the one-grid engine, RM_GRID_ALT=0)."""
+    g = graphfile.load(city)
+    tr = world.generate_traces(city, 300, 40, rate_s=30.0, noise_m=5.0, seed=95)
+    T = len(tr["trace_off"]) - 1
+    opts = engine.default_options(1, search_radius=100.0)
+    ref = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts,
+                               np.zeros(T, np.uint32)))
+    eng = engine.Engine(city, 0)
+    f_alt, r_alt = eng.grid_alt()
+    assert f_alt not in (0, eng.grid_split()) and 50.0 < r_alt <= 100.0, (eng.grid_split(), f_alt, r_alt)
+    bm = engine.BatchMatcher(eng)
+    bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts)
+    c = compare_all(bm, ref, tr["trace_off"])
+    assert c["segments"] > 200, c
+    bm.close()
+    eng.close()
+    monkeypatch.setenv("RM_GRID_ALT", "0")
+    eng = engine.Engine(city, 0)
+    assert eng.grid_alt() == (0, 0.0)
+    bm = engine.BatchMatcher(eng)
+    bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts)
+    compare_all(bm, ref, tr["trace_off"])
+    bm.close()
+    eng.close()

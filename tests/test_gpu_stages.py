@@ -41,14 +41,14 @@ def _stream(path, n_veh=40, n_pts=240, seed=3):
     return {k: v[perm] for k, v in d.items()}
 
 
-def _oracle(g, pts, inactivity=120):
+def _oracle(g, pts, inactivity=120, opts=None):
     wins = to.split_windows(list(pts["uuid"]), list(pts["time"]), inactivity)
     idx = np.concatenate([np.array(w, np.int64) for _, w in wins])
     off = np.zeros(len(wins) + 1, np.uint32)
     off[1:] = np.cumsum([len(w) for _, w in wins])
     tr = dict(trace_off=off, lon=pts["lon"][idx], lat=pts["lat"][idx], time=pts["time"][idx],
               accuracy=pts["accuracy"][idx])
-    opts = engine.default_options(1)
+    opts = engine.default_options(1) if opts is None else opts
     ref = mo.match(g, mo.Batch(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts,
                                np.zeros(len(wins), np.uint32)))
     return wins, tr, ref
@@ -99,6 +99,27 @@ def test_points_windows_match_and_tiles(small_world):
         assert got == want
         total += len(got)
     assert total > 0
+
+
+def test_points_with_turn_costs(small_world):
+    """run_points checks and applies a batch's options as run() does: with auto's stock turn
+    costs (200) every stage equals the oracle at 200, and a negative factor is refused."""
+    g = graphfile.load(small_world)
+    eng = engine.Engine(small_world, 0)
+    pts = _stream(small_world)
+    opts = engine.default_options(1, turn_penalty_factor=200.0)
+    bm = engine.BatchMatcher(eng)
+    bm.run_points(pts["uuid"], pts["time"], pts["lon"], pts["lat"], pts["accuracy"], inactivity=120, opts=opts)
+    wins, tr, ref = _oracle(g, pts, opts=opts)
+    valid = ref["route"] != 0xffffffff
+    assert int((ref["route_turn"][valid] > 0).sum()) > 1000
+    c = compare_all(bm, ref, tr["trace_off"])
+    assert c["segments"] > 100
+    with pytest.raises(RuntimeError, match="turn_penalty_factor"):
+        bm.run_points(pts["uuid"], pts["time"], pts["lon"], pts["lat"], pts["accuracy"],
+                      opts=engine.default_options(1, turn_penalty_factor=-1.0))
+    bm.close()
+    eng.close()
 
 
 def test_tiles_empty_and_errors(small_world):
