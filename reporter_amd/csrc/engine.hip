@@ -5519,9 +5519,13 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   Workspace& w = ws_;
   hipStream_t st = stream_;
   unsigned long long* htot = reinterpret_cast<unsigned long long*>(hctl_ + 16);
-  ensure_trans(P * kMaxCand * kMaxCand, P * kMaxCand);
+  // sized for the next power of two of points (>= 4,096): a service's batch sizes wander, and each
+  // regrowth frees and reallocates (hipFree synchronises the device: a stall of milliseconds)
+  uint64_t Pc = 4096;
+  while (Pc < P) Pc <<= 1;
+  ensure_trans(Pc * kMaxCand * kMaxCand, Pc * kMaxCand);
   if (turn_mask_) ensure_turns();
-  ensure_segs(P * kInlinePath + w.cap_path);
+  ensure_segs(Pc * kInlinePath + w.cap_path);
   DevBatch v = make_view(w, in_, T, P);
   v.route = w.route;
   if (turn_mask_) v.route_d = w.route_d;
