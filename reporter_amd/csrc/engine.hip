@@ -3145,7 +3145,6 @@ struct Vit3Smem {
   float sq[kV3Chunk][kMaxCand];
   double cost[2][kMaxCand];                  // previous / next layer costs (ping-pong)
   uint4 bpo[kV3Chunk];                       // this chunk's back-pointer rows
-  uint8_t cs[kV3Chunk];                      // this chunk's chain-start flags
   uint32_t nch, done, w, pad;
 };
 static_assert(sizeof(Vit3Smem) <= 5120, "K3 v3 must keep 8 waves per SIMD (32 per CU) within LDS");
@@ -3248,11 +3247,12 @@ __device__ __forceinline__ void v3_stage_routes(Vit3Smem& sm, const V3Chunk& c, 
     }
 }
 
-// back-pointer rows / chain flags of chunk layers [0, n) to HBM
-__device__ __forceinline__ void v3_flush(const DevBatch& b, const Vit3Smem& sm, uint64_t l0, uint32_t n, int lane) {
+// back-pointer rows / chain flags (csm: bit l = layer l starts a chain) of chunk layers [0, n) to HBM
+__device__ __forceinline__ void v3_flush(const DevBatch& b, const Vit3Smem& sm, uint64_t l0, uint32_t n, int lane,
+                                         uint32_t csm) {
   if ((uint32_t)lane < n) {
     *reinterpret_cast<uint4*>(b.bp + (l0 + lane) * kMaxCand) = sm.bpo[lane];
-    b.chain_start[l0 + lane] = sm.cs[lane];
+    b.chain_start[l0 + lane] = (uint8_t)((csm >> lane) & 1u);
   }
 }
 
@@ -3359,17 +3359,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
     const V3Chunk nx = v3_layout(vit_cook(dn, S, s1, lane & 15), s1, S, lane);
     v3_load<TURN>(b, o, S, nx, lane, rg);
     dn = vit_raw(b, o, S, s1 + nx.C, lane & 15);
+    // per chunk, once: the back-pointer rows start empty, and which layers' gaps break the chain
+    // (layer t of the chunk: bit t); the layers' chain-start flags collect in csm
+    if (lane < kV3Chunk) sm.bpo[lane] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+    const uint32_t brkm = (uint32_t)(__ballot(lane < 16 && (uint32_t)lane < cur.C && cur.s0 + (uint32_t)lane > 0u &&
+                                              cur.gc > brk) & 0xffffull);
+    uint32_t csm = 0u;
     wave_sync();
+    // the emission of target lane / 4 (a W = 4 pass) one layer ahead, off the layer's chain
+    double em4n = (double)sm.sq[0][lane >> 2] * inv2s2;
     for (uint32_t t = 0; t < cur.C; ++t) {
       const uint32_t s = cur.s0 + t;
-      int lane = threadIdx.x;
-      __asm__ volatile("" : "+v"(lane));   // per-pass lane maps are recomputed, not held in VGPRs
       const uint32_t kr = (uint32_t)__builtin_amdgcn_readlane((int)cur.kbrel, (int)t);
       const uint32_t KB = kr & 0xffu, rel = kr >> 8;
-      const double gcl = readlane_d(cur.gc, t);
-      const double em4 = (double)sm.sq[t][lane >> 2] * inv2s2;   // target lane / 4 of a W = 4 pass
-      if (lane == 0) sm.bpo[t] = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-      bool start = !prev_ok || (s > 0 && gcl > brk);
+      const double gcl = TURN ? 0.0 : readlane_d(cur.gc, t);   // (with turn costs the staged term holds it)
+      const double em4 = em4n;
+      bool start = !prev_ok || ((brkm >> t) & 1u) != 0u;
       if (KB && !start) {
         unsigned long long any = 0ull;
         if (prevK <= 4u) {
@@ -3383,10 +3388,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
         }
         if (any == 0ull) start = true;   // no valid transition into this layer
       }
+      em4n = (double)sm.sq[min(t + 1u, cur.C - 1u)][lane >> 2] * inv2s2;
       if (s > 0 && prev_ok && (KB == 0 || start)) {
         // the chain ending at layer s - 1 is complete: its rows [.., s) must be in HBM
         wave_sync();
-        v3_flush(b, sm, o + cur.s0, t, lane);
+        v3_flush(b, sm, o + cur.s0, t, lane, csm);
         v3_backtrace(b, sm, o, s - 1, prevK, cb, lane);
         if (t + 1 < cur.C) {   // the backtrace staged through route_m: bring the chunk back
           const double INF = __longlong_as_double(0x7ff0000000000000ll);
@@ -3404,7 +3410,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
         }
       }
       if (KB == 0) {
-        if (lane == 0) sm.cs[t] = 1;
+        csm |= 1u << t;
         prev_ok = false;
         prevK = 0;
         wave_sync();
@@ -3412,14 +3418,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
       }
       if (start && lane < kMaxCand)   // a chain starts: cost = emission, back-pointers none
         sm.cost[cb ^ 1][lane] = (uint32_t)lane < KB ? (double)sm.sq[t][lane] * inv2s2 : INF;
-      if (lane == 0) sm.cs[t] = start ? 1 : 0;
+      csm |= (start ? 1u : 0u) << t;
       wave_sync();
       prev_ok = true;
       prevK = KB;
       cb ^= 1;
     }
     wave_sync();
-    v3_flush(b, sm, o + cur.s0, cur.C, lane);
+    v3_flush(b, sm, o + cur.s0, cur.C, lane, csm);
     wave_sync();
     if (!has_next) break;
     cur = nx;
