@@ -3315,16 +3315,20 @@ __device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, int lane, ui
   const double m = group_min<W>(c);
   const unsigned long long eq = __ballot(c == m && m < INF);
   const uint32_t g = (uint32_t)(eq >> ((uint32_t)lane & ~(uint32_t)(W - 1))) & ((1u << W) - 1u);
-  const int arg = g ? __builtin_ctz(g) : -1;
   const bool head = i == 0u && j < KB;
+  // a group has an arg-min exactly when its minimum is finite (some lane equals it); the values
+  // are formed in every lane and only the heads store
+  const bool fin = m < INF;
+  const unsigned long long any = __ballot(head && fin);
+  // W = 4 (one pass, j = lane / 4): the emission was read a layer ahead, off this layer's chain
+  const double em = W == 4 ? em4 : (double)sm.sq[t][min(j, (uint32_t)kMaxCand - 1u)] * inv2s2;
+  const double nc = fin ? m + em : INF;
+  const uint8_t bpj = fin ? (uint8_t)__builtin_ctz(g | 0x10000u) : (uint8_t)255;
   if (head) {
-    // W = 4 (one pass, j = lane / 4): the emission was read at the top of the layer, off the
-    // chain of this layer's cost reads
-    const double em = W == 4 ? em4 : (double)sm.sq[t][j] * inv2s2;
-    sm.cost[cb ^ 1][j] = arg >= 0 ? m + em : INF;
-    reinterpret_cast<uint8_t*>(&sm.bpo[t])[j] = arg >= 0 ? (uint8_t)arg : (uint8_t)255;
+    sm.cost[cb ^ 1][j] = nc;
+    reinterpret_cast<uint8_t*>(&sm.bpo[t])[j] = bpj;
   }
-  return __ballot(head && arg >= 0);
+  return any;
 }
 
 template <bool TURN>
@@ -3375,11 +3379,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
       const double gcl = TURN ? 0.0 : readlane_d(cur.gc, t);   // (with turn costs the staged term holds it)
       const double em4 = em4n;
       bool start = !prev_ok || ((brkm >> t) & 1u) != 0u;
-      if (KB && !start) {
+      // the common layer (the chain goes on, K_A <= 4: one W = 4 pass) takes a path of its own
+      // past the chain-break, empty-layer and chain-start bookkeeping
+      if (KB && !start && prevK <= 4u) {
+        const unsigned long long any = v3_pass<4, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t, em4);
+        if (any != 0ull) {
+          em4n = (double)sm.sq[min(t + 1u, cur.C - 1u)][lane >> 2] * inv2s2;
+          wave_sync();
+          prevK = KB;
+          cb ^= 1;
+          continue;
+        }
+        start = true;   // no valid transition into this layer: the general path below breaks the chain
+      } else if (KB && !start) {   // K_A > 4
         unsigned long long any = 0ull;
-        if (prevK <= 4u) {
-          any = v3_pass<4, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t, em4);
-        } else if (prevK <= 8u) {
+        if (prevK <= 8u) {
           any = v3_pass<8, TURN>(sm, lane, 0u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t, em4);
           if (KB > 8u) any |= v3_pass<8, TURN>(sm, lane, 8u, KB, prevK, rel, gcl, inv_beta, inv2s2, cb, t, em4);
         } else {
