@@ -621,7 +621,12 @@ def main():
             abytes, formulation = mo.routes_algorithmic_bytes(counts), "bounded searches"
         else:
             abytes, formulation = None, None
-        tpath = a.traffic_json or os.path.join(ROOT, "profiles", "r04", "pmc_routes_%s.json" % a.config.lower())
+        tpath = a.traffic_json
+        if not tpath:   # the newest round's PMC summary of this workload (sha-checked by load_traffic)
+            for rnd in ("r05", "r04"):
+                tpath = os.path.join(ROOT, "profiles", rnd, "pmc_routes_%s.json" % a.config.lower())
+                if os.path.exists(tpath):
+                    break
         traffic, traffic_note = load_traffic(tpath, a.config, n_per, max(1, a.streams))
         tr_of = lambda st: (traffic.get(st) or {}).get("hbm_bytes_per_launch")
         va_of = lambda st: (traffic.get(st) or {}).get("valu_instrs")

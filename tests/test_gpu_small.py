@@ -96,3 +96,24 @@ def test_service_replies_through_small_runs(built_lib, small_world, tmp_path):
     for k in range(48):
         want = engine.segment_dicts(ref["segs"][ref["seg_off"][k]:ref["seg_off"][k + 1]])
         assert json.loads(outs[k])["segments"] == want, k
+
+
+def test_lone_caller_runs_inline(built_lib, small_world, tmp_path):
+    """A caller that sends one request at a time: after a streak of single-request batches the
+    coalescer runs each request on its caller's thread (Coalescer::submit); the replies stay the
+    oracle's, and the batch count still counts every request."""
+    import valhalla
+    g = graphfile.load(small_world)
+    tr = world.generate_traces(small_world, n_traces=24, n_points=60, rate_s=1.0, noise_m=5.0, seed=304)
+    ref = _ref(g, tr, engine.default_options(1))
+    conf = valhalla.write_config(str(tmp_path / "lone.json"), small_world, device=0, coalesce=True)
+    valhalla.Configure(conf)
+    sm = valhalla.SegmentMatcher()
+    before = valhalla.coalesce_stats()
+    for k in range(24):
+        got = json.loads(sm.Match(json.dumps(world.trace_to_request(tr, k), separators=(",", ":"))))["segments"]
+        want = engine.segment_dicts(ref["segs"][ref["seg_off"][k]:ref["seg_off"][k + 1]])
+        assert got == want, k
+    st = valhalla.coalesce_stats()
+    assert st["requests"] - before["requests"] == 24 and st["batches"] - before["batches"] == 24, (before, st)
+    sm.close()
