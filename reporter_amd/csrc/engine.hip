@@ -3450,6 +3450,213 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// K3 batch kernel, round 5 (k_viterbi_p): k_viterbi's layout and layer body, with the chunk
+// staging rebuilt the way k_viterbi_w's is.  k_viterbi loaded a chunk's routes and emission rows
+// at the chunk's start and waited for them there (one HBM round trip per chunk of ~10 layers,
+// under 2-3 waves per SIMD), and it guarded each of its 16 route loads and stores by its own
+// per-lane branch (~650 instructions per chunk: ~40 % of the kernel's).  Here the next chunk is
+// laid out and its routes and emission rows are loaded into registers while this chunk runs
+// (the chunk after that is described then), every load is unconditional at a clamped address
+// inside the batch, and staging writes every entry (past the chunk: copies of its last route /
+// row, never selected -- a source past prevK costs +inf, a target past K_B is discarded).
+template <bool TURN>
+struct VitRegs {
+  uint32_t rv[TURN ? 1 : kVitRoutes / 16];
+  double rd[TURN ? kVitRoutes / 16 : 1];
+  v3_f4 sv[4];
+};
+
+struct VitChunk {
+  uint32_t s0, C, nroutes, rbase;   // group-uniform (C: the smallest over the wave's live groups)
+  uint32_t kb, rel;                 // lane j < C: K_B of layer s0 + j, its routes' offset in the chunk
+  double gc;
+};
+
+// vit_raw for any trace: an empty trace (or a lane past the batch) reads layer 0 of the batch
+__device__ __forceinline__ VitLayerRaw vit_raw_any(const DevBatch& b, uint32_t o, uint32_t S, uint32_t s0, int j) {
+  const uint64_t lq = S ? o + min(s0 + (uint32_t)j, S - 1) : 0u;
+  const uint64_t lp = (S == 0 || lq == o) ? lq : lq - 1;
+  VitLayerRaw r;
+  r.kb = b.cand_n[lq];
+  r.ka = b.cand_n[lp];
+  r.off = b.trans_off[lq];
+  r.gc = b.gc[lq];
+  return r;
+}
+
+__device__ __forceinline__ VitChunk vit_layout(const VitLayerDesc& d, uint32_t s0, uint32_t S, int j, int gb) {
+  uint32_t incl = d.cnt;
+#pragma unroll
+  for (int x = 1; x < 16; x <<= 1) {
+    const uint32_t u = __shfl_up(incl, x, 16);
+    if (j >= x) incl += u;
+  }
+  const bool live = s0 < S;
+  const uint32_t fit = (uint32_t)((__ballot(live && s0 + (uint32_t)j < S && incl <= (uint32_t)kVitRoutes) >> gb) & 0xffffull);
+  const uint32_t Cg = live ? (uint32_t)__builtin_ctz(~fit | 0x10000u) : 0x10000u;   // leading layers that fit
+  uint32_t Cw = min(Cg, (uint32_t)__shfl_xor((int)Cg, 16));
+  Cw = min(Cw, (uint32_t)__shfl_xor((int)Cw, 32));
+  VitChunk c;
+  c.s0 = s0;
+  c.C = live ? Cw : 0u;
+  c.nroutes = c.C ? (uint32_t)__shfl(incl, (int)c.C - 1, 16) : 0u;
+  c.rbase = (uint32_t)__shfl(d.off, 0, 16);
+  const bool inc = (uint32_t)j < c.C;
+  c.kb = inc ? d.kb : 0u;
+  c.rel = inc ? incl - d.cnt : 0u;
+  c.gc = d.gc;
+  return c;
+}
+
+template <bool TURN>
+__device__ __forceinline__ void vit_load(const DevBatch& b, uint32_t o, const VitChunk& c, int j, VitRegs<TURN>& r) {
+  const uint32_t rlast = c.nroutes ? c.nroutes - 1u : 0u;
+#pragma unroll
+  for (int x = 0; x < kVitRoutes / 16; ++x) {
+    const uint32_t q = c.rbase + min((uint32_t)j + 16u * x, rlast);
+    if constexpr (TURN) r.rd[x] = b.route_d[q];
+    else r.rv[x] = b.route[q];
+  }
+  const uint32_t f0 = c.C ? (o + c.s0) * (kMaxCand / 4) : 0u;
+  const uint32_t flast = f0 + (c.C ? c.C * (kMaxCand / 4) - 1u : 0u);
+  const v3_f4* src = reinterpret_cast<const v3_f4*>(b.cand_sq);
+#pragma unroll
+  for (int x = 0; x < 4; ++x) r.sv[x] = src[min(f0 + (uint32_t)j + 16u * x, flast)];
+}
+
+template <bool TURN>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_WPE))) k_viterbi_p(DevBatch b) {
+  __shared__ VitGroup smem[4];
+  const int lane = threadIdx.x;
+  const int j = lane & 15, gb = lane & 48;
+  VitGroup& gs = smem[lane >> 4];
+  const uint32_t k = blockIdx.x * 4 + (lane >> 4);
+  const bool active = k < b.T;
+  const uint32_t o = active ? b.trace_off[k] : 0u, S = active ? b.n_states[k] : 0u;
+  const MatchOptions op = b.opts[active ? b.trace_opt[k] : 0u];
+  const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
+  const double inv_beta = 1.0 / (double)op.beta;
+  const double brk = (double)op.breakage_distance;
+  const double INF = __longlong_as_double(0x7ff0000000000000ll);
+  bool prev_ok = false;
+  uint32_t prevK = 0;
+  double cj = INF;   // cost of candidate j of the previous layer
+  // chunk 0: describe, lay out, load; then describe chunk 1
+  VitChunk cur = vit_layout(vit_cook(vit_raw_any(b, o, S, 0, j), S, 0, j), 0, S, j, gb);
+  VitRegs<TURN> rg;
+  vit_load<TURN>(b, o, cur, j, rg);
+  VitLayerRaw dn = vit_raw_any(b, o, S, cur.C, j);
+  for (;;) {
+    if (__ballot(cur.s0 < S) == 0ull) break;
+    const uint32_t C = cur.C, nroutes = cur.nroutes, rbase = cur.rbase;
+    // ---- this chunk -> LDS (its loads were issued a chunk ago); every entry written
+#pragma unroll
+    for (int x = 0; x < kVitRoutes / 16; ++x) {
+      if constexpr (TURN) gs.route_m[j + 16 * x] = rg.rd[x];
+      else gs.route_m[j + 16 * x] = rg.rv[x] == kRouteInvalid ? INF : (double)rg.rv[x] * 0.01;
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x) reinterpret_cast<v3_f4*>(&gs.sq[0][0])[j + 16 * x] = rg.sv[x];
+    gs.kb[j] = cur.kb;
+    gs.rel[j] = cur.rel;
+    gs.gc[j] = cur.gc;
+    // ---- the next chunk: lay out, load (overlapping this chunk's layers); describe the one after
+    {
+      const uint32_t s1 = cur.s0 + C;
+      cur = vit_layout(vit_cook(dn, S, s1, j), s1, S, j, gb);
+      vit_load<TURN>(b, o, cur, j, rg);
+      dn = vit_raw_any(b, o, S, s1 + cur.C, j);
+    }
+    const uint32_t s0 = cur.s0 - C;   // (cur is the next chunk from here on)
+    wave_sync();
+    uint32_t maxC = max(C, (uint32_t)__shfl_xor((int)C, 16));
+    maxC = (uint32_t)__builtin_amdgcn_readfirstlane(max(maxC, (uint32_t)__shfl_xor((int)maxC, 32)));   // wave-uniform: a scalar loop
+    // layer parameters and the first four route rows run one layer ahead of their use
+    uint32_t KBn = gs.kb[0], reln = gs.rel[0];
+    double gcn = gs.gc[0];
+    float sqn = gs.sq[0][j];
+    double rmn[4];
+    {
+      const double* dp = gs.route_m + reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
+    }
+    for (uint32_t t = 0; t < maxC; ++t) {
+      const bool in = t < C;
+      const uint32_t KB = KBn, rel = reln;
+      const double gcl = gcn;
+      const float sqv = sqn;
+      double rm0[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) rm0[x] = rmn[x];
+      {
+        const uint32_t tn = min(t + 1u, (uint32_t)kVitChunk - 1u);
+        KBn = gs.kb[tn]; reln = gs.rel[tn]; gcn = gs.gc[tn]; sqn = gs.sq[tn][j];
+      }
+      const bool brk_start = !prev_ok || gcl > brk;
+      double best = INF;
+      int arg = -1;
+      {
+        const uint32_t jj = min((uint32_t)j, KB ? KB - 1u : 0u);
+        const double* dp = gs.route_m + min(rel, (uint32_t)kVitRoutes - 1u) + jj;
+        vit_src<0, TURN>(best, arg, cj, rm0[0], gcl, inv_beta);
+        vit_src<1, TURN>(best, arg, cj, rm0[1], gcl, inv_beta);
+        vit_src<2, TURN>(best, arg, cj, rm0[2], gcl, inv_beta);
+        vit_src<3, TURN>(best, arg, cj, rm0[3], gcl, inv_beta);
+        if (__ballot(in && prevK > 4u) != 0ull) {
+          const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
+          vit_min<1, TURN>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
+        }
+      }
+      const bool valid_j = j < (int)KB;
+      const bool have = valid_j && arg >= 0;
+      const bool none = ((__ballot(have) >> gb) & 0xffffull) == 0ull;
+      const bool start = brk_start || none;
+      const bool kb0 = KB == 0;
+      const bool bt = in && prev_ok && (kb0 || start);
+      if (__ballot(bt) != 0ull) {
+        if (bt) {
+          wave_sync();
+          vit_flush(b, gs, o + s0, t, j);
+          backtrace_chain(b, gs, o, s0 + t - 1, prevK, j, cj);
+        }
+        // the backtrace staged through route_m: bring the chunk's routes back (rare path)
+        const uint32_t* rp = b.route + rbase;
+        const double* rdp = b.route_d ? b.route_d + rbase : nullptr;
+#pragma unroll
+        for (int x = 0; x < kVitRoutes / 16; ++x) {
+          const uint32_t q = (uint32_t)j + 16u * x;
+          if (q < nroutes) {
+            if constexpr (TURN) gs.route_m[q] = rdp[q];
+            else gs.route_m[q] = rp[q] == kRouteInvalid ? INF : (double)rp[q] * 0.01;
+          }
+        }
+        wave_sync();
+      }
+      {
+        const double* dp = gs.route_m + reln + j;
+        const uint32_t kbs = min(KBn, (uint32_t)kMaxCand);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) rmn[x] = dp[x * kbs];
+      }
+      const double em = valid_j ? (double)sqv * inv2s2 : INF;
+      const double nc = start ? em : best + em;
+      const uint32_t bpj = (start || !have) ? 255u : (uint32_t)arg;
+      const uint32_t slot = in ? t : (uint32_t)kVitChunk;
+      reinterpret_cast<uint8_t*>(&gs.bpo[slot])[j] = (uint8_t)bpj;
+      gs.cs[slot] = start ? 1 : 0;
+      cj = in ? nc : cj;
+      prev_ok = in ? !kb0 : prev_ok;
+      prevK = in ? KB : prevK;
+    }
+    wave_sync();
+    vit_flush(b, gs, o + s0, C, j);
+    wave_sync();
+  }
+  if (prev_ok) backtrace_chain(b, gs, o, S - 1, prevK, j, cj);
+}
+
 // Small batches (the coalesced service: tens to hundreds of traces) take the one-wave-per-trace
 // kernel: with a few waves on an empty GPU the per-layer latency is the time, and its layer
 // chain is shorter (C2 traces of 600 points: 0.49 -> 0.35 ms at 38 traces, 0.38 -> 0.32 ms for
@@ -3470,8 +3677,14 @@ void launch_viterbi(uint32_t T, hipStream_t st, const DevBatch& v) {
     else hipLaunchKernelGGL(k_viterbi_w<false>, dim3(T), dim3(64), 0, st, v);
     return;
   }
-  if (turn) hipLaunchKernelGGL(k_viterbi<true>, dim3((T + 3) / 4), dim3(64), 0, st, v);
-  else hipLaunchKernelGGL(k_viterbi<false>, dim3((T + 3) / 4), dim3(64), 0, st, v);
+  static const bool r4 = [] { const char* e = std::getenv("RM_VIT_R4"); return e && *e == '1'; }();   // A/B
+  if (r4) {
+    if (turn) hipLaunchKernelGGL(k_viterbi<true>, dim3((T + 3) / 4), dim3(64), 0, st, v);
+    else hipLaunchKernelGGL(k_viterbi<false>, dim3((T + 3) / 4), dim3(64), 0, st, v);
+    return;
+  }
+  if (turn) hipLaunchKernelGGL(k_viterbi_p<true>, dim3((T + 3) / 4), dim3(64), 0, st, v);
+  else hipLaunchKernelGGL(k_viterbi_p<false>, dim3((T + 3) / 4), dim3(64), 0, st, v);
 }
 
 // ------------------------------------------------------------------------------------------
