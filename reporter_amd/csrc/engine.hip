@@ -2814,6 +2814,15 @@ __device__ __forceinline__ void vit_flush(const DevBatch& b, const VitGroup& gs,
   }
 }
 
+// vit_flush with the chunk's chain-start flags as a mask (bit l: layer l starts a chain)
+__device__ __forceinline__ void vit_flush_m(const DevBatch& b, const VitGroup& gs, uint64_t l0, uint32_t n, int j,
+                                            uint32_t csm) {
+  if ((uint32_t)j < n) {
+    *reinterpret_cast<uint4*>(b.bp + (l0 + j) * kMaxCand) = gs.bpo[j];
+    b.chain_start[l0 + j] = (uint8_t)((csm >> j) & 1u);
+  }
+}
+
 // Backtrace of the chain ending at layer `end` (lane j holds cost j of that layer, K
 // candidates).  Winner = lowest cost, ties to the lowest j.  Rows are staged 64 layers
 // per block (four coalesced loads per lane); lane 0 of the group walks them in LDS and
@@ -3542,6 +3551,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
   bool prev_ok = false;
   uint32_t prevK = 0;
   double cj = INF;   // cost of candidate j of the previous layer
+  bool fok = false;  // the trace has ended with a chain (fK candidates, costs fcj) still to trace back
+  uint32_t fK = 0;
+  double fcj = INF;
   // chunk 0: describe, lay out, load; then describe chunk 1
   VitChunk cur = vit_layout(vit_cook(vit_raw_any(b, o, S, 0, j), S, 0, j), 0, S, j, gb);
   VitRegs<TURN> rg;
@@ -3582,8 +3594,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
 #pragma unroll
       for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
     }
+    // A live group runs every layer of the loop (maxC = C for each of them).  A finished group's
+    // layers have K_B = 0: at its first chunk past the end it keeps the chain its trace ended
+    // with for the final backtrace (all groups at once, after the loop) and drops prev_ok, so its
+    // layers neither trigger a backtrace nor need `in` selects
+    {
+      const bool fin = (C == 0u) & prev_ok;
+      fcj = fin ? cj : fcj;
+      fK = fin ? prevK : fK;
+      fok = fok | fin;
+      prev_ok = prev_ok & (C != 0u);
+    }
+    uint32_t csm = 0u;   // chain-start flags of the chunk's layers (bit t; the same in every lane of a group)
     for (uint32_t t = 0; t < maxC; ++t) {
-      const bool in = t < C;
       const uint32_t KB = KBn, rel = reln;
       const double gcl = gcn;
       const float sqv = sqn;
@@ -3594,7 +3617,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         const uint32_t tn = min(t + 1u, (uint32_t)kVitChunk - 1u);
         KBn = gs.kb[tn]; reln = gs.rel[tn]; gcn = gs.gc[tn]; sqn = gs.sq[tn][j];
       }
-      const bool brk_start = !prev_ok || gcl > brk;
       double best = INF;
       int arg = -1;
       {
@@ -3604,21 +3626,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         vit_src<1, TURN>(best, arg, cj, rm0[1], gcl, inv_beta);
         vit_src<2, TURN>(best, arg, cj, rm0[2], gcl, inv_beta);
         vit_src<3, TURN>(best, arg, cj, rm0[3], gcl, inv_beta);
-        if (__ballot(in && prevK > 4u) != 0ull) {
+        if (__ballot(prevK > 4u) != 0ull) {
           const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
           vit_min<1, TURN>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
         }
       }
       const bool valid_j = j < (int)KB;
       const bool have = valid_j && arg >= 0;
-      const bool none = ((__ballot(have) >> gb) & 0xffffull) == 0ull;
-      const bool start = brk_start || none;
+      // groups with no transition into this layer (the chain breaks there too), as a lane mask
+      // formed on the scalar unit
+      const unsigned long long hm = __ballot(have);
+      unsigned long long nm = 0ull;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (((hm >> (16 * g)) & 0xffffull) == 0ull) nm |= 0xffffull << (16 * g);
+      const bool none = __builtin_amdgcn_inverse_ballot_w64(nm);
+      const bool start = (!prev_ok) | (gcl > brk) | none;   // (bitwise: no short-circuit branch)
       const bool kb0 = KB == 0;
-      const bool bt = in && prev_ok && (kb0 || start);
+      const bool bt = prev_ok & (kb0 | start);   // the chain that ends at s - 1 is complete
       if (__ballot(bt) != 0ull) {
         if (bt) {
           wave_sync();
-          vit_flush(b, gs, o + s0, t, j);
+          vit_flush_m(b, gs, o + s0, t, j, csm);
           backtrace_chain(b, gs, o, s0 + t - 1, prevK, j, cj);
         }
         // the backtrace staged through route_m: bring the chunk's routes back (rare path)
@@ -3643,18 +3672,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       const double em = valid_j ? (double)sqv * inv2s2 : INF;
       const double nc = start ? em : best + em;
       const uint32_t bpj = (start || !have) ? 255u : (uint32_t)arg;
-      const uint32_t slot = in ? t : (uint32_t)kVitChunk;
-      reinterpret_cast<uint8_t*>(&gs.bpo[slot])[j] = (uint8_t)bpj;
-      gs.cs[slot] = start ? 1 : 0;
-      cj = in ? nc : cj;
-      prev_ok = in ? !kb0 : prev_ok;
-      prevK = in ? KB : prevK;
+      reinterpret_cast<uint8_t*>(&gs.bpo[t])[j] = (uint8_t)bpj;
+      csm |= (start ? 1u : 0u) << t;
+      cj = nc;
+      prev_ok = !kb0;
+      prevK = KB;
     }
     wave_sync();
-    vit_flush(b, gs, o + s0, C, j);
+    vit_flush_m(b, gs, o + s0, C, j, csm);
     wave_sync();
   }
-  if (prev_ok) backtrace_chain(b, gs, o, S - 1, prevK, j, cj);
+  if (fok | prev_ok) backtrace_chain(b, gs, o, S - 1, fok ? fK : prevK, j, fok ? fcj : cj);
 }
 
 // Small batches (the coalesced service: tens to hundreds of traces) take the one-wave-per-trace
