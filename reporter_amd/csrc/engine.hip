@@ -3495,22 +3495,23 @@ __device__ __forceinline__ VitLayerRaw vit_raw_any(const DevBatch& b, uint32_t o
 }
 
 __device__ __forceinline__ VitChunk vit_layout(const VitLayerDesc& d, uint32_t s0, uint32_t S, int j, int gb) {
+  // inclusive scan of the route counts inside the 16-lane row by DPP row_shr adds (bound_ctrl:
+  // a lane without a source adds 0), the groups' minimum by readlanes: no LDS round trips
   uint32_t incl = d.cnt;
-#pragma unroll
-  for (int x = 1; x < 16; x <<= 1) {
-    const uint32_t u = __shfl_up(incl, x, 16);
-    if (j >= x) incl += u;
-  }
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xf, 0xf, true);   // row_shr:1
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xf, 0xf, true);   // row_shr:2
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xf, 0xf, true);   // row_shr:4
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x118, 0xf, 0xf, true);   // row_shr:8
   const bool live = s0 < S;
   const uint32_t fit = (uint32_t)((__ballot(live && s0 + (uint32_t)j < S && incl <= (uint32_t)kVitRoutes) >> gb) & 0xffffull);
   const uint32_t Cg = live ? (uint32_t)__builtin_ctz(~fit | 0x10000u) : 0x10000u;   // leading layers that fit
-  uint32_t Cw = min(Cg, (uint32_t)__shfl_xor((int)Cg, 16));
-  Cw = min(Cw, (uint32_t)__shfl_xor((int)Cw, 32));
+  const uint32_t Cw = min(min((uint32_t)__builtin_amdgcn_readlane((int)Cg, 0), (uint32_t)__builtin_amdgcn_readlane((int)Cg, 16)),
+                          min((uint32_t)__builtin_amdgcn_readlane((int)Cg, 32), (uint32_t)__builtin_amdgcn_readlane((int)Cg, 48)));
   VitChunk c;
   c.s0 = s0;
   c.C = live ? Cw : 0u;
   c.nroutes = c.C ? (uint32_t)__shfl(incl, (int)c.C - 1, 16) : 0u;
-  c.rbase = (uint32_t)__shfl(d.off, 0, 16);
+  c.rbase = (uint32_t)__builtin_amdgcn_mov_dpp((int)d.off, 0x150, 0xf, 0xf, false);   // row_newbcast:0
   const bool inc = (uint32_t)j < c.C;
   c.kb = inc ? d.kb : 0u;
   c.rel = inc ? incl - d.cnt : 0u;
@@ -3518,20 +3519,25 @@ __device__ __forceinline__ VitChunk vit_layout(const VitLayerDesc& d, uint32_t s
   return c;
 }
 
+// The loads run past the chunk's last route / row without a clamp (one address per lane, the rest
+// immediate offsets): a chunk starts at most one past the batch's last route or layer and reads
+// <= 256 routes / 16 rows from there, inside the pools' slack (the route pools hold >= 1,024
+// entries past the batch's routes, the point arrays >= 64 points past its points: ensure /
+// ensure_trans_raw).  What lies past the chunk is staged but never selected.
 template <bool TURN>
 __device__ __forceinline__ void vit_load(const DevBatch& b, uint32_t o, const VitChunk& c, int j, VitRegs<TURN>& r) {
-  const uint32_t rlast = c.nroutes ? c.nroutes - 1u : 0u;
+  if constexpr (TURN) {
+    const double* rp = b.route_d + c.rbase + j;
 #pragma unroll
-  for (int x = 0; x < kVitRoutes / 16; ++x) {
-    const uint32_t q = c.rbase + min((uint32_t)j + 16u * x, rlast);
-    if constexpr (TURN) r.rd[x] = b.route_d[q];
-    else r.rv[x] = b.route[q];
+    for (int x = 0; x < kVitRoutes / 16; ++x) r.rd[x] = rp[16 * x];
+  } else {
+    const uint32_t* rp = b.route + c.rbase + j;
+#pragma unroll
+    for (int x = 0; x < kVitRoutes / 16; ++x) r.rv[x] = rp[16 * x];
   }
-  const uint32_t f0 = c.C ? (o + c.s0) * (kMaxCand / 4) : 0u;
-  const uint32_t flast = f0 + (c.C ? c.C * (kMaxCand / 4) - 1u : 0u);
-  const v3_f4* src = reinterpret_cast<const v3_f4*>(b.cand_sq);
+  const v3_f4* src = reinterpret_cast<const v3_f4*>(b.cand_sq) + (uint64_t)(c.C ? o + c.s0 : 0u) * (kMaxCand / 4) + j;
 #pragma unroll
-  for (int x = 0; x < 4; ++x) r.sv[x] = src[min(f0 + (uint32_t)j + 16u * x, flast)];
+  for (int x = 0; x < 4; ++x) r.sv[x] = src[16 * x];
 }
 
 template <bool TURN>
