@@ -2814,12 +2814,12 @@ __device__ __forceinline__ void vit_flush(const DevBatch& b, const VitGroup& gs,
   }
 }
 
-// vit_flush with the chunk's chain-start flags as a mask (bit l: layer l starts a chain)
+// vit_flush with the chunk's chain-start flags as a wave mask (bit `lane`: layer j of lane j's group)
 __device__ __forceinline__ void vit_flush_m(const DevBatch& b, const VitGroup& gs, uint64_t l0, uint32_t n, int j,
-                                            uint32_t csm) {
+                                            unsigned long long csm) {
   if ((uint32_t)j < n) {
     *reinterpret_cast<uint4*>(b.bp + (l0 + j) * kMaxCand) = gs.bpo[j];
-    b.chain_start[l0 + j] = (uint8_t)((csm >> j) & 1u);
+    b.chain_start[l0 + j] = __builtin_amdgcn_inverse_ballot_w64(csm) ? 1 : 0;
   }
 }
 
@@ -3554,7 +3554,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
   const double inv_beta = 1.0 / (double)op.beta;
   const double brk = (double)op.breakage_distance;
   const double INF = __longlong_as_double(0x7ff0000000000000ll);
-  bool prev_ok = false;
+  // wave masks (all lanes of a group alike): the group's previous layer had candidates (pok)
+  unsigned long long pok = 0ull;
   uint32_t prevK = 0;
   double cj = INF;   // cost of candidate j of the previous layer
   bool fok = false;  // the trace has ended with a chain (fK candidates, costs fcj) still to trace back
@@ -3605,13 +3606,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     // with for the final backtrace (all groups at once, after the loop) and drops prev_ok, so its
     // layers neither trigger a backtrace nor need `in` selects
     {
-      const bool fin = (C == 0u) & prev_ok;
+      const bool fin = __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_ballot_w64(C == 0u) & pok);
       fcj = fin ? cj : fcj;
       fK = fin ? prevK : fK;
       fok = fok | fin;
-      prev_ok = prev_ok & (C != 0u);
+      pok &= __builtin_amdgcn_ballot_w64(C != 0u);
     }
-    uint32_t csm = 0u;   // chain-start flags of the chunk's layers (bit t; the same in every lane of a group)
+    // chain-start flags of the chunk's layers: layer t of group g at bit 16 g + t (read back at
+    // bit `lane` by the flush: lane j of group g writes layer j's flag)
+    unsigned long long csm = 0ull;
     for (uint32_t t = 0; t < maxC; ++t) {
       const uint32_t KB = KBn, rel = reln;
       const double gcl = gcn;
@@ -3632,26 +3635,33 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         vit_src<1, TURN>(best, arg, cj, rm0[1], gcl, inv_beta);
         vit_src<2, TURN>(best, arg, cj, rm0[2], gcl, inv_beta);
         vit_src<3, TURN>(best, arg, cj, rm0[3], gcl, inv_beta);
-        if (__ballot(prevK > 4u) != 0ull) {
+        if (__builtin_amdgcn_ballot_w64(prevK > 4u) != 0ull) {
           const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
           vit_min<1, TURN>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
         }
       }
-      const bool valid_j = j < (int)KB;
-      const bool have = valid_j && arg >= 0;
-      // groups with no transition into this layer (the chain breaks there too), as a lane mask
-      // formed on the scalar unit
-      const unsigned long long hm = __ballot(have);
-      unsigned long long nm = 0ull;
+      // the next layer's first route rows, read while this layer's bookkeeping runs (read again
+      // after a backtrace, which stages through route_m).  Lanes past K_B and stale parameters
+      // past the chunk read other bytes of this group's VitGroup, never used: no clamps
+      const double* dpn = gs.route_m + reln + j;
+      const uint32_t kbn = min(KBn, (uint32_t)kMaxCand);
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        if (((hm >> (16 * g)) & 0xffffull) == 0ull) nm |= 0xffffull << (16 * g);
-      const bool none = __builtin_amdgcn_inverse_ballot_w64(nm);
-      const bool start = (!prev_ok) | (gcl > brk) | none;   // (bitwise: no short-circuit branch)
-      const bool kb0 = KB == 0;
-      const bool bt = prev_ok & (kb0 | start);   // the chain that ends at s - 1 is complete
-      if (__ballot(bt) != 0ull) {
-        if (bt) {
+      for (int x = 0; x < 4; ++x) rmn[x] = dpn[x * kbn];
+      // the layer's bookkeeping as wave masks on the scalar unit (each compare writes one)
+      const unsigned long long vm = __builtin_amdgcn_ballot_w64(j < (int)KB);      // valid targets
+      const unsigned long long hm = vm & __builtin_amdgcn_ballot_w64(arg >= 0);     // ... with a transition in
+      // groups with no transition into this layer (the chain breaks there too): fold each group's
+      // 16 bits onto its lowest bit, spread the groups without one back over their lanes
+      unsigned long long y = hm | (hm >> 1);
+      y |= y >> 2;
+      y |= y >> 4;
+      y |= y >> 8;
+      const unsigned long long g0 = y & 0x0001000100010001ull;
+      const unsigned long long stm = ~pok | __builtin_amdgcn_ballot_w64(gcl > brk) | ~((g0 << 16) - g0);   // chain starts
+      const unsigned long long kbm = __builtin_amdgcn_ballot_w64(KB == 0u);
+      const unsigned long long btm = pok & (kbm | stm);   // the chain that ends at s - 1 is complete
+      if (btm != 0ull) {
+        if (__builtin_amdgcn_inverse_ballot_w64(btm)) {
           wave_sync();
           vit_flush_m(b, gs, o + s0, t, j, csm);
           backtrace_chain(b, gs, o, s0 + t - 1, prevK, j, cj);
@@ -3668,27 +3678,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
           }
         }
         wave_sync();
-      }
-      {
-        const double* dp = gs.route_m + reln + j;
-        const uint32_t kbs = min(KBn, (uint32_t)kMaxCand);
 #pragma unroll
-        for (int x = 0; x < 4; ++x) rmn[x] = dp[x * kbs];
+        for (int x = 0; x < 4; ++x) rmn[x] = dpn[x * kbn];
       }
-      const double em = valid_j ? (double)sqv * inv2s2 : INF;
+      const bool start = __builtin_amdgcn_inverse_ballot_w64(stm);
+      const double em = __builtin_amdgcn_inverse_ballot_w64(vm) ? (double)sqv * inv2s2 : INF;
       const double nc = start ? em : best + em;
-      const uint32_t bpj = (start || !have) ? 255u : (uint32_t)arg;
+      const uint32_t bpj = __builtin_amdgcn_inverse_ballot_w64(stm | ~hm) ? 255u : (uint32_t)arg;
       reinterpret_cast<uint8_t*>(&gs.bpo[t])[j] = (uint8_t)bpj;
-      csm |= (start ? 1u : 0u) << t;
+      csm |= (stm & 0x0001000100010001ull) << t;
       cj = nc;
-      prev_ok = !kb0;
+      pok = ~kbm;
       prevK = KB;
     }
     wave_sync();
     vit_flush_m(b, gs, o + s0, C, j, csm);
     wave_sync();
   }
-  if (fok | prev_ok) backtrace_chain(b, gs, o, S - 1, fok ? fK : prevK, j, fok ? fcj : cj);
+  if (fok | __builtin_amdgcn_inverse_ballot_w64(pok)) backtrace_chain(b, gs, o, S - 1, fok ? fK : prevK, j, fok ? fcj : cj);
 }
 
 // Small batches (the coalesced service: tens to hundreds of traces) take the one-wave-per-trace
