@@ -2749,7 +2749,7 @@ struct VitGroup {
 #endif
 };
 
-static_assert(sizeof(VitGroup) >= (kVitRoutes + 15 + 3 * 16 + 1) * sizeof(double), "K3 prefetch reads stay inside VitGroup");
+static_assert(sizeof(VitGroup) >= (kVitRoutes + 15 + 7 * 16 + 1) * sizeof(double), "K3 prefetch reads (8 source rows) stay inside VitGroup");
 
 // lane I of this lane's 16-lane row (DPP row_newbcast; rows are the K3 groups)
 template <int I>
@@ -2777,7 +2777,7 @@ __device__ __forceinline__ void vit_src(double& best, int& arg, double cj, doubl
 }
 template <int B, bool TURN>
 __device__ __forceinline__ void vit_min(double& best, int& arg, double cj, const double* dp, uint32_t KB,
-                                        uint32_t prevK, double gcl, double inv_beta, const double (&rm0)[4]) {
+                                        uint32_t prevK, double gcl, double inv_beta, const double* rm0) {
   if constexpr (B < 4) {
     if ((uint32_t)(4 * B) < prevK) {
       double rm[4];
@@ -3595,11 +3595,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
     uint32_t KBn = gs.kb[0], reln = gs.rel[0];
     double gcn = gs.gc[0];
     float sqn = gs.sq[0][j];
-    double rmn[4];
+    double rmn[8];
     {
       const double* dp = gs.route_m + reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
 #pragma unroll
-      for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
+      for (int x = 0; x < 8; ++x) rmn[x] = dp[x * KBn];
     }
     // A live group runs every layer of the loop (maxC = C for each of them).  A finished group's
     // layers have K_B = 0: at its first chunk past the end it keeps the chain its trace ended
@@ -3619,9 +3619,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       const uint32_t KB = KBn, rel = reln;
       const double gcl = gcn;
       const float sqv = sqn;
-      double rm0[4];
+      double rm0[8];
 #pragma unroll
-      for (int x = 0; x < 4; ++x) rm0[x] = rmn[x];
+      for (int x = 0; x < 8; ++x) rm0[x] = rmn[x];
       {
         const uint32_t tn = min(t + 1u, (uint32_t)kVitChunk - 1u);
         KBn = gs.kb[tn]; reln = gs.rel[tn]; gcn = gs.gc[tn]; sqn = gs.sq[tn][j];
@@ -3635,9 +3635,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         vit_src<1, TURN>(best, arg, cj, rm0[1], gcl, inv_beta);
         vit_src<2, TURN>(best, arg, cj, rm0[2], gcl, inv_beta);
         vit_src<3, TURN>(best, arg, cj, rm0[3], gcl, inv_beta);
-        if (__builtin_amdgcn_ballot_w64(prevK > 4u) != 0ull) {
-          const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
-          vit_min<1, TURN>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
+        if (__builtin_amdgcn_ballot_w64(prevK > 4u) != 0ull) {   // sources 4..7: read a layer ahead too
+          vit_src<4, TURN>(best, arg, cj, rm0[4], gcl, inv_beta);
+          vit_src<5, TURN>(best, arg, cj, rm0[5], gcl, inv_beta);
+          vit_src<6, TURN>(best, arg, cj, rm0[6], gcl, inv_beta);
+          vit_src<7, TURN>(best, arg, cj, rm0[7], gcl, inv_beta);
+          if (__builtin_amdgcn_ballot_w64(prevK > 8u) != 0ull) {
+            const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
+            vit_min<2, TURN>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
+          }
         }
       }
       // the next layer's first route rows, read while this layer's bookkeeping runs (read again
@@ -3646,7 +3652,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
       const double* dpn = gs.route_m + reln + j;
       const uint32_t kbn = min(KBn, (uint32_t)kMaxCand);
 #pragma unroll
-      for (int x = 0; x < 4; ++x) rmn[x] = dpn[x * kbn];
+      for (int x = 0; x < 8; ++x) rmn[x] = dpn[x * kbn];
       // the layer's bookkeeping as wave masks on the scalar unit (each compare writes one)
       const unsigned long long vm = __builtin_amdgcn_ballot_w64(j < (int)KB);      // valid targets
       const unsigned long long hm = vm & __builtin_amdgcn_ballot_w64(arg >= 0);     // ... with a transition in
@@ -3679,7 +3685,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
         }
         wave_sync();
 #pragma unroll
-        for (int x = 0; x < 4; ++x) rmn[x] = dpn[x * kbn];
+        for (int x = 0; x < 8; ++x) rmn[x] = dpn[x * kbn];
       }
       const bool start = __builtin_amdgcn_inverse_ballot_w64(stm);
       const double em = __builtin_amdgcn_inverse_ballot_w64(vm) ? (double)sqv * inv2s2 : INF;
