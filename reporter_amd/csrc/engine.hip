@@ -2716,10 +2716,10 @@ __global__ void __launch_bounds__(64) k_routes_global(DevGraph g, DevBatch b, Gl
 // moves (no LDS round trip, no barrier), and routes are staged as fp64 metres (+inf when
 // invalid) so a source costs three fp64 operations and a compare.  Each group streams its trace through LDS in
 // chunks of <= 16 layers / <= kVitRoutes routes: one lane describes one layer, a 16-lane
-// scan lays the chunk out, and routes / emission rows arrive with coalesced loads while
-// the next chunk's descriptor is already in flight.  No global store is issued inside a
-// chunk (gfx9 loads and stores share vmcnt): back-pointer rows and chain flags are
-// buffered in LDS and flushed once per chunk.
+// scan lays the chunk out, and routes / emission rows arrive with coalesced loads a chunk
+// ahead (below, "the chunk pipeline").  No global store is issued inside a chunk (gfx9
+// loads and stores share vmcnt): back-pointer rows are buffered in LDS and flushed, with
+// the chunk's chain-start flags, once per chunk.
 constexpr int kVitChunk = 16;     // layers per staged chunk (one per lane of the group)
 #ifndef RM_VIT_WPE
 #define RM_VIT_WPE 3   // 2,500 C2 waves over 1,024 SIMDs must be resident at once (also LDS: VitGroup)
@@ -2806,15 +2806,8 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m, int width) {
   return __longlong_as_double(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// write back-pointer rows / chain flags of chunk layers [0, n) (layer l at slot l0 + l)
-__device__ __forceinline__ void vit_flush(const DevBatch& b, const VitGroup& gs, uint64_t l0, uint32_t n, int j) {
-  if ((uint32_t)j < n) {
-    *reinterpret_cast<uint4*>(b.bp + (l0 + j) * kMaxCand) = gs.bpo[j];
-    b.chain_start[l0 + j] = gs.cs[j];
-  }
-}
-
-// vit_flush with the chunk's chain-start flags as a wave mask (bit `lane`: layer j of lane j's group)
+// back-pointer rows and chain-start flags of chunk layers [0, n) to HBM (layer l at slot l0 + l;
+// csm: the chunk's chain-start flags as a wave mask, bit `lane` = layer j of lane j's group)
 __device__ __forceinline__ void vit_flush_m(const DevBatch& b, const VitGroup& gs, uint64_t l0, uint32_t n, int j,
                                             unsigned long long csm) {
   if ((uint32_t)j < n) {
@@ -2921,203 +2914,6 @@ __device__ __forceinline__ VitLayerDesc vit_describe(const DevBatch& b, uint32_t
   d.gc = (vq && sl >= 1) ? g_raw : 0.0;
   return d;
 }
-
-// TURN: the batch has turn costs (rule 3b): the chunk stages each route's distance term route_d
-// (turn_m + |route_m - gc|, formed by K2) instead of its metres
-template <bool TURN>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_WPE))) k_viterbi(DevBatch b) {
-  __shared__ VitGroup smem[4];
-  const int lane = threadIdx.x;
-  const int j = lane & 15, gb = lane & 48;
-  VitGroup& gs = smem[lane >> 4];
-  const uint32_t k = blockIdx.x * 4 + (lane >> 4);
-  const bool active = k < b.T;
-  const uint32_t o = active ? b.trace_off[k] : 0u, S = active ? b.n_states[k] : 0u;
-  const MatchOptions op = b.opts[active ? b.trace_opt[k] : 0u];
-  const double inv2s2 = 1.0 / (2.0 * (double)op.sigma_z * (double)op.sigma_z);
-  const double inv_beta = 1.0 / (double)op.beta;
-  const double brk = (double)op.breakage_distance;
-  const double INF = __longlong_as_double(0x7ff0000000000000ll);
-  bool prev_ok = false;
-  uint32_t prevK = 0;
-  double cj = INF;   // cost of candidate j of the previous layer
-  // chunk descriptor: lane j describes layer s0 + j (clamped, branch-free loads)
-  VitLayerDesc dq{0u, 0u, 0u, 0.0};
-  if (S) dq = vit_describe(b, o, S, 0, j);
-  uint32_t s0 = 0;
-  for (;;) {
-    const bool live = s0 < S;
-    if (__ballot(live) == 0ull) break;
-    // ---- lay the chunk out: inclusive scan of route counts over the group's 16 layers
-    uint32_t incl = dq.cnt;
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-      const uint32_t u = __shfl_up(incl, d, 16);
-      if (j >= d) incl += u;
-    }
-    const uint32_t excl = incl - dq.cnt;
-    const uint32_t fit = (uint32_t)((__ballot(live && s0 + j < S && incl <= (uint32_t)kVitRoutes) >> gb) & 0xffffull);
-    const uint32_t Cg = live ? (uint32_t)__builtin_ctz(~fit | 0x10000u) : 0x10000u;   // leading layers that fit
-    // every live group of the wave advances by the smallest of their chunk lengths, so no group
-    // idles through another's longer chunk (the routes staged past it are re-read next chunk)
-    uint32_t Cw = min(Cg, (uint32_t)__shfl_xor((int)Cg, 16));
-    Cw = min(Cw, (uint32_t)__shfl_xor((int)Cw, 32));
-    const uint32_t C = live ? Cw : 0u;
-    const uint32_t nroutes = C ? (uint32_t)__shfl(incl, (int)C - 1, 16) : 0u;
-    const uint32_t rbase = (uint32_t)__shfl(dq.off, 0, 16);                   // routes of layer s0 start here
-    // ---- coalesced loads of the chunk's routes and emission rows
-    uint32_t rv[TURN ? 1 : kVitRoutes / 16];
-    double dv[TURN ? kVitRoutes / 16 : 1];
-    const uint32_t rlast = nroutes ? nroutes - 1u : 0u;
-    if constexpr (TURN) {
-#pragma unroll
-      for (int x = 0; x < kVitRoutes / 16; ++x)
-        if (16u * x < nroutes) dv[x] = b.route_d[rbase + min((uint32_t)j + 16u * x, rlast)];
-    } else {
-#pragma unroll
-      for (int x = 0; x < kVitRoutes / 16; ++x)
-        if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
-    }
-    // emission rows (16 floats per layer), four float4 per lane, clamped to the chunk
-    const uint64_t f0 = C ? (uint64_t)(o + s0) * (kMaxCand / 4) : 0u;
-    const uint64_t flast = f0 + (C ? (uint64_t)C * (kMaxCand / 4) - 1 : 0u);
-    const float4* sqsrc = reinterpret_cast<const float4*>(b.cand_sq);
-    const float4 sv0 = sqsrc[min(f0 + j, flast)], sv1 = sqsrc[min(f0 + j + 16u, flast)];
-    const float4 sv2 = sqsrc[min(f0 + j + 32u, flast)], sv3 = sqsrc[min(f0 + j + 48u, flast)];
-    const uint32_t kb_here = dq.kb, rel_here = excl;
-    const double gc_here = dq.gc;
-    // ---- descriptor of the next chunk (its loads overlap this chunk's work)
-    if (live && s0 + C < S) dq = vit_describe(b, o, S, s0 + C, j);
-    // ---- chunk -> LDS
-    if constexpr (TURN) {
-#pragma unroll
-      for (int x = 0; x < kVitRoutes / 16; ++x)
-        if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = dv[x];
-    } else {
-#pragma unroll
-      for (int x = 0; x < kVitRoutes / 16; ++x)
-        if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
-    }
-    {
-      float4* sqdst = reinterpret_cast<float4*>(&gs.sq[0][0]);
-      const uint32_t nf = C * (kMaxCand / 4);
-      if ((uint32_t)j < nf) sqdst[j] = sv0;
-      if ((uint32_t)j + 16u < nf) sqdst[j + 16] = sv1;
-      if ((uint32_t)j + 32u < nf) sqdst[j + 32] = sv2;
-      if ((uint32_t)j + 48u < nf) sqdst[j + 48] = sv3;
-    }
-    {   // every entry written (0 past the chunk) so the unclamped prefetch stays inside VitGroup
-      const bool inc = (uint32_t)j < C;
-      gs.kb[j] = inc ? kb_here : 0u;
-      gs.rel[j] = inc ? rel_here : 0u;
-      gs.gc[j] = gc_here;
-    }
-    wave_sync();
-    uint32_t maxC = max(C, (uint32_t)__shfl_xor((int)C, 16));
-    maxC = (uint32_t)__builtin_amdgcn_readfirstlane(max(maxC, (uint32_t)__shfl_xor((int)maxC, 32)));   // wave-uniform: a scalar loop
-    // layer parameters and the first four route rows run one layer ahead of their use
-    uint32_t KBn = gs.kb[0], reln = gs.rel[0];
-    double gcn = gs.gc[0];
-    float sqn = gs.sq[0][j];
-    double rmn[4];
-    {
-      const double* dp = gs.route_m + reln + min((uint32_t)j, KBn ? KBn - 1u : 0u);
-#pragma unroll
-      for (int x = 0; x < 4; ++x) rmn[x] = dp[x * KBn];
-    }
-    // ---- the layers of the chunk, in order, out of LDS.  The body is branch-free for the common
-    // layer: the recurrence over the first four sources runs for every group (a group that starts
-    // a chain, has no candidates or has run out of layers computes it and drops it), further
-    // sources under wave-uniform tests, and the state moves by selects; a group past its chunk
-    // writes its row to a spare slot.  Only a chain break (backtrace) branches.
-    for (uint32_t t = 0; t < maxC; ++t) {
-      const bool in = t < C;
-      const uint32_t KB = KBn, rel = reln;
-      const double gcl = gcn;
-      const float sqv = sqn;
-      double rm0[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) rm0[x] = rmn[x];
-      {   // next layer's parameters, unconditionally (past the chunk: stale entries, never used)
-        const uint32_t tn = min(t + 1u, (uint32_t)kVitChunk - 1u);
-        KBn = gs.kb[tn]; reln = gs.rel[tn]; gcn = gs.gc[tn]; sqn = gs.sq[tn][j];
-      }
-      // a chain starts after a layer without candidates (prev_ok false, also at s == 0) or a gap
-      // above breakage_distance
-      const bool brk_start = !prev_ok || gcl > brk;
-      double best = INF;
-      int arg = -1;
-      {
-        const uint32_t jj = min((uint32_t)j, KB ? KB - 1u : 0u);
-        const double* dp = gs.route_m + min(rel, (uint32_t)kVitRoutes - 1u) + jj;
-        vit_src<0, TURN>(best, arg, cj, rm0[0], gcl, inv_beta);
-        vit_src<1, TURN>(best, arg, cj, rm0[1], gcl, inv_beta);
-        vit_src<2, TURN>(best, arg, cj, rm0[2], gcl, inv_beta);
-        vit_src<3, TURN>(best, arg, cj, rm0[3], gcl, inv_beta);
-        if (__ballot(in && prevK > 4u) != 0ull) {   // wave-uniform: sources 4.. of some group
-          const uint32_t kbs = min(KB, (uint32_t)kMaxCand);
-          vit_min<1, TURN>(best, arg, cj, dp, kbs, prevK, gcl, inv_beta, rm0);
-        }
-      }
-      const bool valid_j = j < (int)KB;
-      const bool have = valid_j && arg >= 0;
-      // no transition into any candidate of the layer: the chain breaks here too
-      const bool none = ((__ballot(have) >> gb) & 0xffffull) == 0ull;
-      const bool start = brk_start || none;
-      const bool kb0 = KB == 0;
-      const bool bt = in && prev_ok && (kb0 || start);   // the chain that ends at s - 1 is complete
-      if (__ballot(bt) != 0ull) {
-        if (bt) {
-          wave_sync();                      // the group's row stores precede the flush
-          vit_flush(b, gs, o + s0, t, j);   // rows [s0, s) are needed by the backtrace
-          backtrace_chain(b, gs, o, s0 + t - 1, prevK, j, cj);
-        }
-        // the backtrace staged through route_m: bring the chunk's routes back
-        if constexpr (TURN) {
-#pragma unroll
-          for (int x = 0; x < kVitRoutes / 16; ++x)
-            if (16u * x < nroutes) dv[x] = b.route_d[rbase + min((uint32_t)j + 16u * x, rlast)];
-#pragma unroll
-          for (int x = 0; x < kVitRoutes / 16; ++x)
-            if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = dv[x];
-        } else {
-#pragma unroll
-          for (int x = 0; x < kVitRoutes / 16; ++x)
-            if (16u * x < nroutes) rv[x] = b.route[rbase + min((uint32_t)j + 16u * x, rlast)];
-#pragma unroll
-          for (int x = 0; x < kVitRoutes / 16; ++x)
-            if ((uint32_t)j + 16u * x < nroutes) gs.route_m[j + 16 * x] = rv[x] == kRouteInvalid ? INF : (double)rv[x] * 0.01;
-        }
-        wave_sync();
-      }
-      {   // next layer's first route rows (after any re-staging above).  Lanes past K_B and stale
-          // parameters past the chunk read other bytes of this group's VitGroup (offset <= 256 +
-          // 15 + 3 x 16 doubles, inside it: static_assert below VitGroup), never used: no clamps
-        const double* dp = gs.route_m + reln + j;
-        const uint32_t kbs = min(KBn, (uint32_t)kMaxCand);
-#pragma unroll
-        for (int x = 0; x < 4; ++x) rmn[x] = dp[x * kbs];
-      }
-      // em is +inf past K_B (and for every lane of an empty layer, which also has `start`), and
-      // best is +inf where no source reached the lane, so best + em needs no further selects
-      const double em = valid_j ? (double)sqv * inv2s2 : INF;
-      const double nc = start ? em : best + em;
-      const uint32_t bpj = (start || !have) ? 255u : (uint32_t)arg;
-      const uint32_t slot = in ? t : (uint32_t)kVitChunk;   // a group past its chunk writes the spare row
-      reinterpret_cast<uint8_t*>(&gs.bpo[slot])[j] = (uint8_t)bpj;
-      gs.cs[slot] = start ? 1 : 0;   // every lane of the group writes the same byte
-      cj = in ? nc : cj;
-      prev_ok = in ? !kb0 : prev_ok;
-      prevK = in ? KB : prevK;
-    }
-    wave_sync();
-    vit_flush(b, gs, o + s0, C, j);
-    wave_sync();
-    s0 += C;
-  }
-  if (prev_ok) backtrace_chain(b, gs, o, S - 1, prevK, j, cj);
-}
-
 
 // ------------------------------------------------------------------------------------------
 // K3 (round 2, v3): one wave per trace, one lane per transition.  A layer's K_A x K_B
@@ -3460,15 +3256,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3
 }
 
 // ------------------------------------------------------------------------------------------
-// K3 batch kernel, round 5 (k_viterbi_p): k_viterbi's layout and layer body, with the chunk
-// staging rebuilt the way k_viterbi_w's is.  k_viterbi loaded a chunk's routes and emission rows
-// at the chunk's start and waited for them there (one HBM round trip per chunk of ~10 layers,
-// under 2-3 waves per SIMD), and it guarded each of its 16 route loads and stores by its own
-// per-lane branch (~650 instructions per chunk: ~40 % of the kernel's).  Here the next chunk is
-// laid out and its routes and emission rows are loaded into registers while this chunk runs
-// (the chunk after that is described then), every load is unconditional at a clamped address
-// inside the batch, and staging writes every entry (past the chunk: copies of its last route /
-// row, never selected -- a source past prevK costs +inf, a target past K_B is discarded).
+// K3 k_viterbi, the chunk pipeline (round 5).  Round 4's kernel loaded a chunk's routes and
+// emission rows at the chunk's start and waited for them there (one HBM round trip per chunk of
+// ~10 layers, under 2-3 waves per SIMD), and it guarded each of its 16 route loads and stores by
+// its own per-lane branch (~650 instructions per chunk: ~40 % of the kernel's).  Now the next
+// chunk is laid out and its routes and emission rows are loaded into registers while this chunk
+// runs (the chunk after that is described then), every load is unconditional (vit_load), and
+// staging writes every entry (past the chunk: routes / rows never selected -- a source past prevK
+// costs +inf, a target past K_B is discarded).  The layer's bookkeeping (chain starts, breaks,
+// the backtrace trigger, chain-start flags) is wave masks on the scalar unit.  C2: 0.65 -> 0.51 ms.
 template <bool TURN>
 struct VitRegs {
   uint32_t rv[TURN ? 1 : kVitRoutes / 16];
@@ -3541,7 +3337,7 @@ __device__ __forceinline__ void vit_load(const DevBatch& b, uint32_t o, const Vi
 }
 
 template <bool TURN>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_WPE))) k_viterbi_p(DevBatch b) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_WPE))) k_viterbi(DevBatch b) {
   __shared__ VitGroup smem[4];
   const int lane = threadIdx.x;
   const int j = lane & 15, gb = lane & 48;
@@ -3724,14 +3520,8 @@ void launch_viterbi(uint32_t T, hipStream_t st, const DevBatch& v) {
     else hipLaunchKernelGGL(k_viterbi_w<false>, dim3(T), dim3(64), 0, st, v);
     return;
   }
-  static const bool r4 = [] { const char* e = std::getenv("RM_VIT_R4"); return e && *e == '1'; }();   // A/B
-  if (r4) {
-    if (turn) hipLaunchKernelGGL(k_viterbi<true>, dim3((T + 3) / 4), dim3(64), 0, st, v);
-    else hipLaunchKernelGGL(k_viterbi<false>, dim3((T + 3) / 4), dim3(64), 0, st, v);
-    return;
-  }
-  if (turn) hipLaunchKernelGGL(k_viterbi_p<true>, dim3((T + 3) / 4), dim3(64), 0, st, v);
-  else hipLaunchKernelGGL(k_viterbi_p<false>, dim3((T + 3) / 4), dim3(64), 0, st, v);
+  if (turn) hipLaunchKernelGGL(k_viterbi<true>, dim3((T + 3) / 4), dim3(64), 0, st, v);
+  else hipLaunchKernelGGL(k_viterbi<false>, dim3((T + 3) / 4), dim3(64), 0, st, v);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -1,6 +1,7 @@
 #!/bin/bash
 # K3 batch kernel A/B: parity with the batch kernel forced on every size (RM_VIT_WAVE_MAX=0), then
-# C2 / C5 / C2-with-turn-costs stage times, new kernel against round 4.s (RM_VIT_R4=1).
+# C2 / C5 / C2-with-turn-costs stage times against round 4.s kernel (RM_VIT_R4=1 selected it until it
+# was removed; the A/B logs under profiles/r05/k3b are from then).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/k3b
