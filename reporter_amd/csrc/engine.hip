@@ -93,15 +93,24 @@ struct DevBatch {  // POD view of the workspace for kernels
   // and the segment gather skip a run whose path pool overflowed or whose records exceed seg_cap
   // (the host then runs the batch the ordinary way); 2: also one that handed searches to the
   // global-memory tier, which a small run does not launch before its scratch exists
+  // 4: a steady run (Matcher::run_steady) sized from the pools an earlier run of the matcher left:
+  // every stage after the transition scan skips a batch with more transitions or K2 sources than
+  // trans_cap / src_cap (steady_abort), and the host re-runs it the ordinary way
   const unsigned long long* tot;
   uint64_t seg_cap;
+  uint64_t trans_cap, src_cap;
   uint32_t gate;
 };
+
+__device__ __forceinline__ bool steady_abort(const DevBatch& b) {
+  return (b.gate & 4u) && (b.tot[0] > b.trans_cap || b.tot[1] > b.src_cap);
+}
 
 __device__ __forceinline__ bool small_abort(const DevBatch& b) {
   if (!b.gate) return false;
   const uint32_t* c = b.ctl;
-  return (c[2] & kErrPathOverflow) != 0u || ((b.gate & 2u) && (c[9] | c[10]) != 0u) || b.tot[2] > b.seg_cap;
+  return (c[2] & kErrPathOverflow) != 0u || ((b.gate & 2u) && (c[9] | c[10]) != 0u) || b.tot[2] > b.seg_cap ||
+         steady_abort(b);
 }
 
 // A failure that belongs to one trajectory (too many roads in a radius, a search beyond every
@@ -976,6 +985,7 @@ __global__ void __launch_bounds__(256) k_trans_count(DevBatch b, unsigned long l
 
 // one work item per (layer pair, source candidate): item -> pair slot
 __global__ void k_src_items(DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.P) return;
   const uint32_t n = b.src_cnt[p], at = b.src_off[p];
@@ -1923,11 +1933,15 @@ __device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src
 
 template <bool TURN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_arg) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ K2Smem<TURN> sm;
   // kNone: a small run's launch, sized by the upper bound; the item count is on the device
   const uint32_t n_items = n_arg != kNone ? n_arg : (uint32_t)b.tot[1];
-  const uint32_t t0i = xcd_block(blockIdx.x, gridDim.x) * kK2Items;   // first item of the block
-  if (t0i >= n_items) return;
+  // (blocks past the items' exit; the rest map onto XCDs by the item-block count, so a grid sized
+  // from an upper bound still spreads the work over every XCD)
+  const uint32_t nblk = (uint32_t)(((uint64_t)n_items + kK2Items - 1) / kK2Items);
+  if (blockIdx.x >= nblk) return;
+  const uint32_t t0i = xcd_block(blockIdx.x, nblk) * kK2Items;   // first item of the block
   const uint32_t t = t0i + threadIdx.x;
   const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;              // last item of the block
   const bool live = t <= tl;
@@ -2104,6 +2118,7 @@ struct K2TSmem {
   uint8_t redo[kK2Items];
 };
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball_t(DevGraph g, DevBatch b, uint32_t n_arg) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ K2TSmem sm;
   const uint32_t n_items = n_arg != kNone ? n_arg : (uint32_t)b.tot[1];
   const uint32_t t0i = xcd_block(blockIdx.x, gridDim.x) * kK2Items;
@@ -2229,6 +2244,7 @@ constexpr uint64_t kListedGrid = 4096;   // blocks of a grid-stride launch over 
 // cost the plain tier registers: scratch 12 -> 64 bytes per lane)
 template <bool TURN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_routes_lane(DevGraph g, DevBatch b, uint32_t n_items, int listed) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   // grid-stride: a listed launch is sized for every item but usually finds few hand-overs
   const uint32_t n = listed ? b.ctl[1] : (n_items != kNone ? n_items : (uint32_t)b.tot[1]);
   __shared__ uint32_t s_res[kMaxCand][256];
@@ -2263,6 +2279,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
 #endif
 constexpr int kTier2Cap = RM_TIER2_CAP;
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_routes_reg2(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ uint32_t s_res[kMaxCand][256];
   const uint32_t n_items = b.ctl[3];
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n_items; q += gridDim.x * blockDim.x) {
@@ -2496,6 +2513,7 @@ __device__ void path_walk_ball(const DevGraph& g, const DevBatch& b, uint64_t p,
 // path ball tier: one lane per chosen transition whose bound fits the ball radius; the
 // others go to the search tiers (rl_routes_0 reused after K2, count ctl[8])
 __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b.perm_paths) {   // locality order: the pair whose source state is the r-th sorted state
     const uint64_t r = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
@@ -2550,6 +2568,7 @@ __global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
 // path lane tier: one lane per chosen transition, labels in registers.  With `listed`,
 // thread q takes the q-th transition the ball tier handed over.
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LANE_WPE))) k_paths_lane(DevGraph g, DevBatch b, int listed) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   const uint64_t q0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t p = q0;
   if (listed) {   // grid-stride over the ball tier's hand-overs
@@ -2581,6 +2600,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_LAN
 
 // path second register tier
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_paths_reg2(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   const uint32_t n_items = b.ctl[4];
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n_items; q += gridDim.x * blockDim.x) {
     const uint32_t p = b.rl_paths_a[q];
@@ -2656,6 +2676,7 @@ constexpr int kGrpPathH = RM_GRP_PATH_H;
 constexpr int kGrpW = 16;
 constexpr uint32_t kGrpGrid = 4096;   // blocks of the group tiers (grid-stride over their lists)
 __global__ void __launch_bounds__(64) k_routes_grp(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kGrpH, false> sm[kWave / kGrpW];
   __shared__ uint4 s_src[kWave / kGrpW][2];
   const int gi = threadIdx.x / kGrpW;
@@ -2668,6 +2689,7 @@ __global__ void __launch_bounds__(64) k_routes_grp(DevGraph g, DevBatch b) {
 }
 
 __global__ void __launch_bounds__(64) k_routes_wave_s(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kMidH, false> sm;
   __shared__ uint4 s_src[2];
   const uint32_t n_items = b.ctl[11];
@@ -2678,6 +2700,7 @@ __global__ void __launch_bounds__(64) k_routes_wave_s(DevGraph g, DevBatch b) {
 }
 
 __global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kBigH, false> sm;
   __shared__ uint4 s_src[2];
   const uint32_t n_items = b.ctl[13];
@@ -2697,6 +2720,7 @@ using GlobalRouteSmem = SearchSmem<kGlobalH, false>;
 using GlobalPathSmem = SearchSmem<kGlobalH, true>;
 
 __global__ void __launch_bounds__(64) k_routes_global(DevGraph g, DevBatch b, GlobalPathSmem* scratch) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ uint4 s_src[2];
   GlobalRouteSmem& sm = *reinterpret_cast<GlobalRouteSmem*>(scratch + blockIdx.x);
   const uint32_t n_items = b.ctl[9];
@@ -3138,6 +3162,7 @@ __device__ __forceinline__ unsigned long long v3_pass(Vit3Smem& sm, int lane, ui
 
 template <bool TURN>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT3_WPE))) k_viterbi_w(DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ Vit3Smem sm;
   const int lane = threadIdx.x;
   const uint32_t k = blockIdx.x;
@@ -3338,6 +3363,7 @@ __device__ __forceinline__ void vit_load(const DevBatch& b, uint32_t o, const Vi
 
 template <bool TURN>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_WPE))) k_viterbi(DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ VitGroup smem[4];
   const int lane = threadIdx.x;
   const int j = lane & 15, gb = lane & 48;
@@ -3621,6 +3647,7 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
 // path tiers, as the route tiers: group tier <- rl_paths_b (ctl[6]) -> rl_paths_a (ctl[12]) ->
 // 512 tier -> rl_routes_0 (ctl[14], free once the path lane tier has run) -> 4096 tier -> rl_paths_c
 __global__ void __launch_bounds__(64) k_paths_grp(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kGrpPathH, true> sm[kWave / kGrpW];
   __shared__ uint4 s_src[kWave / kGrpW][2];
   const int gi = threadIdx.x / kGrpW;
@@ -3633,6 +3660,7 @@ __global__ void __launch_bounds__(64) k_paths_grp(DevGraph g, DevBatch b) {
 }
 
 __global__ void __launch_bounds__(64) k_paths_wave_s(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kMidH, true> sm;
   __shared__ uint4 s_src[2];
   const uint32_t n_items = b.ctl[12];
@@ -3643,6 +3671,7 @@ __global__ void __launch_bounds__(64) k_paths_wave_s(DevGraph g, DevBatch b) {
 }
 
 __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kBigH, true> sm;
   __shared__ uint4 s_src[2];
   const uint32_t n_items = b.ctl[14];
@@ -3653,6 +3682,7 @@ __global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
 }
 
 __global__ void __launch_bounds__(64) k_paths_global(DevGraph g, DevBatch b, GlobalPathSmem* scratch) {
+  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ uint4 s_src[2];
   GlobalPathSmem& sm = scratch[blockIdx.x];
   const uint32_t n_items = b.ctl[10];
@@ -3757,6 +3787,7 @@ template <class T>
 __device__ __forceinline__ T at_lane(T v, int src) { return __shfl(v, src < 0 ? 0 : src, 64); }
 
 __global__ void k_rec_slot(DevBatch b, uint32_t* rec_slot) {
+  if (small_abort(b)) return;   // (a steady run gated off: Matcher::run_steady)
   const uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= b.P) return;
   const uint32_t n = b.path_cnt[l], r0 = b.trav_off[l];
@@ -5240,6 +5271,7 @@ static DevBatch make_view(const Workspace& w, const InputView& in, uint32_t T, u
   v.search_delta = search_delta_cm();
   v.tot = w.tot64;
   v.seg_cap = w.cap_segs;
+  v.trans_cap = ~0ull; v.src_cap = ~0ull;
   v.gate = 0;
   return v;
 }
@@ -5714,6 +5746,116 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   return true;
 }
 
+// Large batches in steady state (round 5): the ordinary path reads two totals back in the middle
+// of a run -- the transitions and K2 sources after the candidate scan (to size the route pools and
+// K2's grid) and the traversal records after the path stage -- two host round trips of ~30 us
+// each (5 % of a C2 step's gaps).  A matcher whose previous run left its pools sized runs the
+// same kernels without them: K2's grid covers the previous run's sources and an eighth more and
+// reads the count on the device, the traversal records and the path-stage hand-overs are checked
+// on the device, and a batch that outgrows any of it is gated off after the scan (steady_abort:
+// every stage skips it; small_abort for K4 and the report) and run again the ordinary way.  No
+// locality order (its permuted K2 item scan stays on the ordinary path).  RM_STEADY=0: off.
+bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
+  const uint32_t T = n_traces_;
+  const uint64_t P = n_points_;
+  Workspace& w = ws_;
+  hipStream_t st = stream_;
+  unsigned long long* htot = reinterpret_cast<unsigned long long*>(hctl_ + 16);
+  if (turn_mask_) ensure_turns();
+  DevBatch v = make_view(w, in_, T, P);
+  v.route = w.route;
+  if (turn_mask_) v.route_d = w.route_d;
+  v.src_item = w.src_item;
+  v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
+  v.rl_routes_c = w.rl_routes_c;
+  v.segs = w.segs; v.reps = w.reps; v.seg_cap = w.cap_segs;
+  const uint64_t src_cover = std::min<uint64_t>(w.cap_src, steady_src_ + steady_src_ / 8 + 4096);
+  v.trans_cap = w.cap_trans;
+  v.src_cap = src_cover;
+  v.gate = (w.gsearch ? 1u : 3u) | 4u;
+  locality_used_ = false;
+  const uint32_t count_grid = (uint32_t)((P + 255) / 256);
+  const uint32_t sum_grid = (uint32_t)((P + 1023) / 1024);
+  const auto tgrid = [P](uint32_t full) { return tier_grid(P, full); };
+
+  tic(kKStates);
+  hipLaunchKernelGGL(k_states, dim3(T), dim3(64), 0, st, v);
+  toc(kKStates);
+  tic(kKCandidates);
+  DevGraph gk = g;
+  eng_->k1_grid(batch_radius_, gk);
+  hipLaunchKernelGGL(k_candidates_lane, dim3(count_grid), dim3(256), 0, st, gk, v);
+  hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, gk, v, 0);
+  toc(kKCandidates);
+  tic(kKScan);
+  hipLaunchKernelGGL(k_trans_count, dim3(count_grid), dim3(256), 0, st, v, w.tot_part);
+  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.tot_part, count_grid, w.tot64);
+  hipLaunchKernelGGL(k_scan_apply2, dim3(count_grid), dim3(256), 0, st, (const uint32_t*)w.trans_cnt,
+                     (const uint32_t*)w.src_cnt, P, (const unsigned long long*)w.tot_part, w.trans_off, w.src_off);
+  toc(kKScan);
+  const bool balls = (mode_mask_ & g.ball_mask) != 0u;
+  const uint32_t item_grid = (uint32_t)((src_cover + kK2Items - 1) / kK2Items);
+  const uint32_t lane_grid = (uint32_t)((src_cover + 255) / 256);
+  tic(kKRoutes);
+  hipLaunchKernelGGL(k_src_items, dim3(count_grid), dim3(256), 0, st, v);
+  if (balls) {
+    if (v.route_d) hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
+    else hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
+    const uint32_t lg = (uint32_t)std::min<uint64_t>(lane_grid, kListedGrid);
+    if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
+    else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
+  } else {
+    if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
+    else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
+  }
+  hipLaunchKernelGGL(k_routes_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  if (w.gsearch) hipLaunchKernelGGL(k_routes_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
+  toc(kKRoutes);
+  tic(kKViterbi);
+  launch_viterbi(T, st, v);
+  toc(kKViterbi);
+  tic(kKPaths);
+  if (balls) {
+    hipLaunchKernelGGL(k_paths_ball, dim3(count_grid), dim3(256), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>(count_grid, kListedGrid)), dim3(256), 0, st, g, v, 1);
+  } else {
+    hipLaunchKernelGGL(k_paths_lane, dim3(count_grid), dim3(256), 0, st, g, v, 0);
+  }
+  hipLaunchKernelGGL(k_paths_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
+  toc(kKPaths);
+  tic(kKSegments);
+  hipLaunchKernelGGL(k_sum_u64, dim3(sum_grid), dim3(256), 0, st, w.path_cnt, P, w.tot_part);
+  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, w.tot_part, sum_grid, w.tot64 + 2);
+  hipLaunchKernelGGL(k_scan_apply4, dim3(sum_grid), dim3(256), 0, st, (const uint32_t*)w.path_cnt, P,
+                     (const unsigned long long*)w.tot_part, w.trav_off);
+  if (rp.do_report && rp.zero_hist) zero_hist(rp);
+  hipLaunchKernelGGL(k_rec_slot, dim3(count_grid), dim3(256), 0, st, v, w.rec_slot);
+  hipLaunchKernelGGL(k_seg_wave, dim3(T), dim3(64), 0, st, g, v, (const uint32_t*)w.rec_slot, kNone, report_args(rp));
+  toc(kKSegments);
+  RM_HIP(hipGetLastError());
+  RM_HIP(hipMemcpyAsync(hctl_, w.ctl, kCtlWords * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  RM_HIP(hipMemcpyAsync(htot, w.tot64, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  sync();
+  if (htot[0] > w.cap_trans || htot[1] > src_cover || (hctl_[2] & kErrPathOverflow) ||
+      (!w.gsearch && (hctl_[9] | hctl_[10])) || htot[2] > v.seg_cap)
+    return false;
+  n_trans_ = htot[0];
+  n_path_ = htot[2];
+  seg_used_ = htot[2];
+  steady_src_ = htot[1];
+  has_report_ = rp.do_report != 0;
+  err_bits_ = hctl_[2] & (kErrCandOverflow | kErrSearchOverflow | kErrRounds);
+  if (err_bits_ && !isolate_) throw std::runtime_error(error_text(err_bits_));
+  return true;
+}
+
 void Matcher::run_device(const RunParams& rp) {
   RM_HIP(hipSetDevice(eng_->device()));
   const uint32_t T = n_traces_;
@@ -5731,6 +5873,15 @@ void Matcher::run_device(const RunParams& rp) {
   seg_prefetched_ = false;
   // (a forced locality order takes the ordinary path: the small one runs in slot order)
   if (P <= small_batch_points() && locality_ <= 0 && run_small(rp, g)) return;
+  const char* steady_env = std::getenv("RM_STEADY");   // (read per run: tests switch it)
+  const bool steady_on = !(steady_env && *steady_env == '0');
+  if (steady_on && steady_src_ && w.route && w.src_item && w.path_pool && w.segs && T > 0) {
+    int lm = locality_;
+    if (lm < 0) lm = eng_->locality_default() ? 2 : (batch_sparse_ ? 1 : 0);
+    if (eng_->locality_bits() == 0) lm = 0;
+    if (lm == 0 && run_steady(rp, g)) return;
+    steady_src_ = 0;   // (re-armed by the ordinary run below)
+  }
   // (k_states zeroes the control words and the per-trace error bits)
   DevBatch v = make_view(w, in_, T, P);
   const uint32_t count_grid = (uint32_t)((P + 255) / 256);
@@ -5786,6 +5937,7 @@ void Matcher::run_device(const RunParams& rp) {
   const uint64_t total = htot[0];
   const uint64_t n_src = htot[1];
   if (total >= kMaxTransitions) throw BatchTooLarge("batch too large (transitions >= 0xF0000000); split it");
+  uint64_t steady_next = n_src ? n_src : 1;   // a later batch may run steady (run_steady) from these pools
   n_trans_ = total;
   ensure_trans(total, n_src);
   v.route = w.route;
@@ -5925,6 +6077,7 @@ void Matcher::run_device(const RunParams& rp) {
   sync();
   seg_used_ = seg_total;
   has_report_ = rp.do_report != 0;
+  if (!locality_used_) steady_src_ = steady_next;
   err_bits_ = hctl_[2] & (kErrCandOverflow | kErrSearchOverflow | kErrRounds);
   if (err_bits_ && !isolate_) throw std::runtime_error(error_text(err_bits_));
 }

@@ -376,6 +376,9 @@ class Matcher {
   void grow_dl_dev(size_t need);
   // small batches (run_small): no size read-back between the stages, one upload, one read-back
   bool run_small(const RunParams& rp, const DevGraph& g);
+  // large batches once a run has sized the pools: no read-back between the stages (run_steady)
+  bool run_steady(const RunParams& rp, const DevGraph& g);
+  uint64_t steady_src_ = 0;    // the last ordinary / steady run's K2 sources (0: no steady run yet)
   void zero_hist(const RunParams& rp);
   void use_ws_inputs();
   void ensure_pack(uint64_t bytes);
