@@ -5776,7 +5776,15 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   locality_used_ = false;
   const uint32_t count_grid = (uint32_t)((P + 255) / 256);
   const uint32_t sum_grid = (uint32_t)((P + 1023) / 1024);
-  const auto tgrid = [P](uint32_t full) { return tier_grid(P, full); };
+  // the hand-over tiers' grids from the previous run's list lengths (each is a grid-stride loop:
+  // any grid is correct, and a list that grew runs on fewer blocks than it could): mostly empty
+  // launches of 64 blocks instead of up to 4,096
+  static const bool prev_grids = [] { const char* e = std::getenv("RM_STEADY_GRIDS"); return !(e && *e == '0'); }();   // A/B
+  const auto sgrid = [&](uint32_t full, int word, uint32_t per_block) {
+    if (!prev_grids) return (uint32_t)(full == 2048u ? 2048u : tier_grid(P, full));
+    const uint64_t want = 4ull * (((uint64_t)steady_ctl_[word] + per_block - 1) / per_block);
+    return (uint32_t)std::min<uint64_t>(tier_grid(P, full), std::max<uint64_t>(64u, want));
+  };
 
   tic(kKStates);
   hipLaunchKernelGGL(k_states, dim3(T), dim3(64), 0, st, v);
@@ -5785,7 +5793,7 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   DevGraph gk = g;
   eng_->k1_grid(batch_radius_, gk);
   hipLaunchKernelGGL(k_candidates_lane, dim3(count_grid), dim3(256), 0, st, gk, v);
-  hipLaunchKernelGGL(k_candidates_wave, dim3(2048), dim3(64), 0, st, gk, v, 0);
+  hipLaunchKernelGGL(k_candidates_wave, dim3(sgrid(2048, 7, 1)), dim3(64), 0, st, gk, v, 0);
   toc(kKCandidates);
   tic(kKScan);
   hipLaunchKernelGGL(k_trans_count, dim3(count_grid), dim3(256), 0, st, v, w.tot_part);
@@ -5801,17 +5809,17 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   if (balls) {
     if (v.route_d) hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
     else hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
-    const uint32_t lg = (uint32_t)std::min<uint64_t>(lane_grid, kListedGrid);
+    const uint32_t lg = std::min<uint32_t>(lane_grid, sgrid(kListedGrid, 1, 256));
     if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
     else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
   } else {
     if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
     else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
   }
-  hipLaunchKernelGGL(k_routes_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_reg2, dim3(sgrid(kReg2Grid, 3, 256)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_grp, dim3(sgrid(kGrpGrid, 5, kWave / kGrpW)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave_s, dim3(sgrid(kMidGrid, 11, 1)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave, dim3(sgrid(1024, 13, 1)), dim3(64), 0, st, g, v);
   if (w.gsearch) hipLaunchKernelGGL(k_routes_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
   toc(kKRoutes);
   tic(kKViterbi);
@@ -5820,14 +5828,14 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   tic(kKPaths);
   if (balls) {
     hipLaunchKernelGGL(k_paths_ball, dim3(count_grid), dim3(256), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>(count_grid, kListedGrid)), dim3(256), 0, st, g, v, 1);
+    hipLaunchKernelGGL(k_paths_lane, dim3(std::min<uint32_t>(count_grid, sgrid(kListedGrid, 8, 256))), dim3(256), 0, st, g, v, 1);
   } else {
     hipLaunchKernelGGL(k_paths_lane, dim3(count_grid), dim3(256), 0, st, g, v, 0);
   }
-  hipLaunchKernelGGL(k_paths_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_paths_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_paths_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_paths_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_reg2, dim3(sgrid(kReg2Grid, 4, 256)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_grp, dim3(sgrid(kGrpGrid, 6, kWave / kGrpW)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_wave_s, dim3(sgrid(kMidGrid, 12, 1)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_wave, dim3(sgrid(1024, 14, 1)), dim3(64), 0, st, g, v);
   if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
   toc(kKPaths);
   tic(kKSegments);
@@ -5850,6 +5858,7 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   n_path_ = htot[2];
   seg_used_ = htot[2];
   steady_src_ = htot[1];
+  std::memcpy(steady_ctl_, hctl_, sizeof(steady_ctl_));
   has_report_ = rp.do_report != 0;
   err_bits_ = hctl_[2] & (kErrCandOverflow | kErrSearchOverflow | kErrRounds);
   if (err_bits_ && !isolate_) throw std::runtime_error(error_text(err_bits_));
@@ -6077,7 +6086,10 @@ void Matcher::run_device(const RunParams& rp) {
   sync();
   seg_used_ = seg_total;
   has_report_ = rp.do_report != 0;
-  if (!locality_used_) steady_src_ = steady_next;
+  if (!locality_used_) {
+    steady_src_ = steady_next;
+    std::memcpy(steady_ctl_, hctl_, sizeof(steady_ctl_));
+  }
   err_bits_ = hctl_[2] & (kErrCandOverflow | kErrSearchOverflow | kErrRounds);
   if (err_bits_ && !isolate_) throw std::runtime_error(error_text(err_bits_));
 }

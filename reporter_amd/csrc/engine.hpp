@@ -379,6 +379,7 @@ class Matcher {
   // large batches once a run has sized the pools: no read-back between the stages (run_steady)
   bool run_steady(const RunParams& rp, const DevGraph& g);
   uint64_t steady_src_ = 0;    // the last ordinary / steady run's K2 sources (0: no steady run yet)
+  uint32_t steady_ctl_[16] = {0};   // ... and its control words (the hand-over lists' lengths)
   void zero_hist(const RunParams& rp);
   void use_ws_inputs();
   void ensure_pack(uint64_t bytes);
