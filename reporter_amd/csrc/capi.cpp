@@ -141,11 +141,16 @@ ParsedTrace parse_trace(const char* text, const Config& conf) {
 struct MatchRequest {
   ParsedTrace* trace;
   std::string out, err;
+  // a dispatched request's segments: its caller formats the reply itself after the batch (the
+  // dispatcher moves on to the next batch instead of formatting tens of replies)
+  std::vector<SegmentRec> segs;
+  bool raw = false;
   bool done = false;
   std::condition_variable cv;   // its caller waits here alone (no herd wake-up per batch)
 };
 
-void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch, double* tm);
+void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch, double* tm,
+                 bool defer_format = false);
 
 class Coalescer {
  public:
@@ -199,9 +204,12 @@ class Coalescer {
       return std::move(r.out);
     }
     cv_req_.notify_one();
-    std::unique_lock<std::mutex> lk(mu_);
-    r.cv.wait(lk, [&] { return r.done; });
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      r.cv.wait(lk, [&] { return r.done; });
+    }
     if (!r.err.empty()) throw std::runtime_error(r.err);
+    if (r.raw) tj::format_segments(r.segs.data(), (uint32_t)r.segs.size(), r.out);
     return std::move(r.out);
   }
   void stats(uint64_t out[4]) {
@@ -223,6 +231,10 @@ class Coalescer {
   std::deque<MatchRequest*> q_;
   bool stop_ = false;
   static constexpr int kLoneStreak = 8;
+  static bool fmt_callers() {   // RM_COALESCE_FORMAT=dispatcher: the dispatcher formats the replies (A/B)
+    static const bool on = [] { const char* e = std::getenv("RM_COALESCE_FORMAT"); return !(e && std::strcmp(e, "dispatcher") == 0); }();
+    return on;
+  }
   static bool inline_ok() {   // RM_COALESCE_INLINE=0: every request queues (A/B)
     static const bool on = [] { const char* e = std::getenv("RM_COALESCE_INLINE"); return !(e && *e == '0'); }();
     return on;
@@ -289,8 +301,10 @@ void parallel_for(size_t n, F&& fn, size_t per = 32) {
 
 // tm (may be null) accumulates host wall ms: [0] staging, [1] engine run, [2] segment download,
 // [3] reply formatting
+// raw (optional): each trace's segments instead of its formatted reply (the coalescer's callers
+// format their own)
 std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*>& pt, std::vector<std::string>* errs,
-                                      double* tm = nullptr) {
+                                      double* tm = nullptr, std::vector<std::vector<SegmentRec>>* raw = nullptr) {
   using clk = std::chrono::steady_clock;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   clk::time_point t0 = clk::now();
@@ -335,6 +349,13 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
     if (!errs) throw std::runtime_error("trace " + std::to_string(i) + ": " + error_text(terr[i]));
     (*errs)[i] = error_text(terr[i]);
   }
+  if (raw) {
+    raw->resize(n);
+    for (size_t i = 0; i < n; ++i)
+      if (!terr[i]) (*raw)[i].assign(segs.data() + soff[i], segs.data() + soff[i + 1]);
+    if (tm) tm[3] += ms_since(t0);
+    return out;
+  }
   // replies of a coalesced batch (tens of requests, ~10 us each) over the pool in chunks of 4
   parallel_for(n, [&](size_t i) {
     if (!terr[i]) tj::format_segments(segs.data() + soff[i], soff[i + 1] - soff[i], out[i]);
@@ -347,7 +368,8 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
 // reported per trace by the engine; a whole-batch failure follows serve_policy.hpp: a batch too
 // large for the device is retried by halves (bounded), any other error fails every request in
 // it at once.  A failed run drops the matcher, so what follows starts on a fresh workspace.
-void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch, double* tm) {
+void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch, double* tm,
+                 bool defer_format) {
   int budget = kServeRetryBudget;
   auto run = [&](MatchRequest* const* reqs, size_t n) {
     try {
@@ -355,10 +377,17 @@ void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<Mat
       std::vector<ParsedTrace*> pt(n);
       for (size_t i = 0; i < n; ++i) pt[i] = reqs[i]->trace;
       std::vector<std::string> errs;
-      std::vector<std::string> outs = match_parsed(*m, pt, &errs, tm);
+      std::vector<std::vector<SegmentRec>> raw;
+      std::vector<std::string> outs = match_parsed(*m, pt, &errs, tm, defer_format ? &raw : nullptr);
       for (size_t i = 0; i < n; ++i) {
-        if (!errs[i].empty()) reqs[i]->err = errs[i];
-        else reqs[i]->out = std::move(outs[i]);
+        if (!errs[i].empty()) {
+          reqs[i]->err = errs[i];
+        } else if (defer_format) {
+          reqs[i]->segs = std::move(raw[i]);
+          reqs[i]->raw = true;
+        } else {
+          reqs[i]->out = std::move(outs[i]);
+        }
       }
     } catch (...) {
       m.reset();
@@ -389,7 +418,7 @@ void Coalescer::loop() {
       ++busy_;
     }
     double tm[4] = {0, 0, 0, 0};
-    serve_batch(m, eng_.get(), batch, tm);   // fills out / err of each request (not under the lock)
+    serve_batch(m, eng_.get(), batch, tm, fmt_callers());   // out / err (or segs) of each request, not under the lock
     {
       std::lock_guard<std::mutex> lk(mu_);
       --busy_;
