@@ -3532,16 +3532,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RM_VIT_
 // one); large batches keep four traces per wave (fewer instructions per trace-layer, 0.75 vs
 // 1.01 ms on C2's 10 k traces; at 4,096 traces 0.52 vs 0.55 ms).  RM_VIT_WAVE_MAX overrides
 // the crossover.
+// Round 5: one to four traces fit the batch kernel's single wave, whose layer chain is now the
+// shorter one (C1's 1,000-point trace: K3 0.406 -> 0.387 ms, Match 0.72 -> 0.67 ms; a lone C2
+// trace even, 0.25 ms; at 38 traces the one-wave kernel still wins, 0.27 vs 0.30 ms).
+// RM_VIT_WAVE_MIN overrides that bound.
 #ifndef RM_VIT_WAVE_MAX
 #define RM_VIT_WAVE_MAX 4096
+#endif
+#ifndef RM_VIT_WAVE_MIN
+#define RM_VIT_WAVE_MIN 5
 #endif
 void launch_viterbi(uint32_t T, hipStream_t st, const DevBatch& v) {
   static const uint32_t wave_max = [] {
     const char* e = std::getenv("RM_VIT_WAVE_MAX");
     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)RM_VIT_WAVE_MAX;
   }();
+  static const uint32_t wave_min = [] {
+    const char* e = std::getenv("RM_VIT_WAVE_MIN");
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)RM_VIT_WAVE_MIN;
+  }();
   const bool turn = v.route_d != nullptr;   // the batch has turn costs (rule 3b)
-  if (T <= wave_max) {
+  if (T >= wave_min && T <= wave_max) {
     if (turn) hipLaunchKernelGGL(k_viterbi_w<true>, dim3(T), dim3(64), 0, st, v);
     else hipLaunchKernelGGL(k_viterbi_w<false>, dim3(T), dim3(64), 0, st, v);
     return;
