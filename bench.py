@@ -193,7 +193,7 @@ def roofline(name, kernels, abytes, ms, formulation, traffic=None, valu=None):
     return out
 
 
-def load_traffic(path, config, traces, streams):
+def load_traffic(path, config, traces, streams, turn_penalty=0.0):
     """Per-stage HBM bytes per launch from scripts/pmc_summary.py output, when it was measured on
     this engine.hip with the same workload; else ({}, reason)."""
     if not path or not os.path.exists(path):
@@ -204,7 +204,7 @@ def load_traffic(path, config, traces, streams):
     except (OSError, ValueError) as e:
         return {}, "unreadable PMC summary %s: %s" % (path, e)
     if not (tj.get("config") == config and tj.get("traces") == traces and tj.get("engine_sha") == engine_sha()
-            and tj.get("streams", 1) == streams):
+            and tj.get("streams", 1) == streams and float(tj.get("turn_penalty", 0.0)) == float(turn_penalty)):
         return {}, "PMC summary %s is of another build or workload (sha %s vs %s)" % (
             os.path.relpath(path, ROOT), tj.get("engine_sha"), engine_sha())
     stages = tj.get("stages") or {"routes": {"hbm_bytes_per_launch": tj.get("hbm_bytes_per_launch"),
@@ -623,11 +623,12 @@ def main():
             abytes, formulation = None, None
         tpath = a.traffic_json
         if not tpath:   # the newest round's PMC summary of this workload (sha-checked by load_traffic)
-            for rnd in ("r05", "r04"):
-                tpath = os.path.join(ROOT, "profiles", rnd, "pmc_routes_%s.json" % a.config.lower())
+            for rnd in ("r06", "r05", "r04"):
+                tpath = os.path.join(ROOT, "profiles", rnd, "pmc_routes_%s%s.json" % (
+                    a.config.lower(), "_turn%g" % a.turn_penalty if a.turn_penalty > 0 else ""))
                 if os.path.exists(tpath):
                     break
-        traffic, traffic_note = load_traffic(tpath, a.config, n_per, max(1, a.streams))
+        traffic, traffic_note = load_traffic(tpath, a.config, n_per, max(1, a.streams), a.turn_penalty)
         tr_of = lambda st: (traffic.get(st) or {}).get("hbm_bytes_per_launch")
         va_of = lambda st: (traffic.get(st) or {}).get("valu_instrs")
         k2 = roofline("K2", "K2 route stage: k_src_items + k_routes_ball2 + search tiers for hand-overs", abytes,
@@ -711,10 +712,20 @@ def main():
             "duration_sum_total_s": dur_sum,
         }
         if turn is not None:
+            ttraffic, tnote = {}, None
+            for rnd in ("r06", "r05"):
+                tp = os.path.join(ROOT, "profiles", rnd, "pmc_routes_c2_turn200.json")
+                if os.path.exists(tp):
+                    ttraffic, tnote = load_traffic(tp, a.config, n_per, 1, 200.0)
+                    break
             kt2 = roofline("K2", "K2 route stage with turn costs: k_src_items + k_routes_ball2<turn> (turn rows, ties "
                            "walked through the tables) + search tiers for hand-overs",
                            mo.routes_ball_turn_algorithmic_bytes(counts) if counts and "turn_rows" in counts else None,
-                           turn["routes_ms"], "route-ball table probes + turn rows")
+                           turn["routes_ms"], "route-ball table probes + turn rows",
+                           (ttraffic.get("routes") or {}).get("hbm_bytes_per_launch"),
+                           (ttraffic.get("routes") or {}).get("valu_instrs"))
+            kt2["l2_hit_rate"] = (ttraffic.get("routes") or {}).get("l2_hit_rate")
+            kt2["traffic_source"] = tnote
             out["turn_costs"] = {
                 "what": "the same C2 points with meili's stock auto turn_penalty_factor 200 on every trace "
                         "(valhalla_build_config's default, reference Dockerfile:42-49; DESIGN.md rule 3b): match + "

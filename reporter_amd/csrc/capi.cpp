@@ -168,9 +168,9 @@ class Coalescer {
     cv_req_.notify_all();
     for (auto& t : th_) t.join();
   }
-  // own: the caller's matcher.  While the service runs one request at a time (the last
+  // own: the caller allows the inline path.  While the service runs one request at a time (the last
   // kLoneStreak batches each held a single request) and is idle now, a request runs on its
-  // caller's thread and matcher through the same serve_batch: two thread hand-offs fewer on a
+  // caller's thread (on the coalescer's single inline matcher) through the same serve_batch: two thread hand-offs fewer on a
   // lone caller's latency (C1).  Under concurrent load batches hold many requests, the streak
   // is broken and every request queues (running requests inline there split the batches: 60-point
   // requests at 64 clients 7.6 -> 5.9 M points/s when any idle moment went inline).
@@ -194,7 +194,9 @@ class Coalescer {
     if (here) {
       double tm[4] = {0, 0, 0, 0};
       const std::vector<MatchRequest*> one{&r};
-      serve_batch(*own, eng_.get(), one, tm);   // fills r.out / r.err (serve_policy.hpp)
+      // on the coalescer's one inline matcher (inline_ == 1 here, so no other request uses it):
+      // callers do not each keep a workspace, pinned buffers and a stream for their one inline run
+      serve_batch(inline_m_, eng_.get(), one, tm);   // fills r.out / r.err (serve_policy.hpp)
       {
         std::lock_guard<std::mutex> lk(mu_);
         --inline_;
@@ -244,6 +246,7 @@ class Coalescer {
   uint64_t batches_ = 0, requests_ = 0, max_seen_ = 0;
   double tm_[4] = {0, 0, 0, 0};   // dispatcher wall ms: staging, engine, download, formatting
   std::vector<std::thread> th_;
+  std::unique_ptr<Matcher> inline_m_;   // the lone caller's runs (created on the first; guarded by inline_)
 };
 
 Config::~Config() { coalescer.reset(); }

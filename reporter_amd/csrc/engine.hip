@@ -1729,16 +1729,19 @@ __device__ __forceinline__ uint4 k2_ld(k2_gptr p) {
   const k2_v4 v = *p;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-struct K2Src {
-  unsigned long long rk1, rk0;   // exit root keys (kKeyInf: that exit is unusable)
-  uint2 h1, h0;                  // table headers of the exits (bits 0: no table)
+struct alignas(16) K2Src {
+  // four 16-byte groups, read as such by phase 2 (k2_issue / k2_finish)
+  uint32_t dbase;                // tdesc - rel: transition q of the block reads descriptor pair dbase + q
+  uint32_t obase;                // ob - rel: its route goes to b.route[obase + q]
   unsigned long long ent;        // the item's mode's table rows (a global address: see k2_gptr)
+  uint2 h1, h0;                  // table headers of the exits (bits 0: no table)
+  unsigned long long rk1, rk0;   // exit root keys (kKeyInf: that exit is unusable)
   uint32_t road, s;              // source road and offset on it (direct combinations)
-  uint32_t tdesc;                // the pair's first target descriptor (p * kMaxCand)
-  uint32_t rel;                  // the item's first transition among the block's (block scan of K_B)
   uint32_t bound, tmax;          // pair bounds; bound = kNone: handed to the search tiers
-  uint32_t ob;                   // the item's first route in b.route
   uint32_t lim;                  // routes with distance <= lim are exact from the tables (ball_exact_limit)
+  uint32_t tdesc;                // the pair's first target descriptor (p * kMaxCand)
+  uint32_t ob;                   // the item's first route in b.route
+  uint32_t rel;                  // the item's first transition among the block's (block scan of K_B)
 };
 // per item of a batch with turn costs (rule 3b): the mode's turn rows, the source road's headings
 // and endpoints, the pair's factor
@@ -1749,6 +1752,10 @@ struct K2Turn {
   uint32_t n0, n1;               // the source road's endpoints (the exits' nodes)
   uint32_t mode, pad;
 };
+#ifndef RM_K2_TURN2
+#define RM_K2_TURN2 2
+#endif
+constexpr uint32_t kK2Defer = 1024;   // walked turn weights listed per block (more: the item is searched)
 template <bool TURN>
 struct K2Smem {
   K2Src src[kK2Items];
@@ -1757,6 +1764,8 @@ struct K2Smem {
   uint8_t redo[kK2Items];               // a route of the item was not exact from the tables
   K2Turn tsrc[TURN ? kK2Items : 1];
   uint32_t tw[TURN ? kTurnDegrees : 1];  // the turn weights (DevGraph::turn_w) in LDS
+  uint32_t ndef;                         // transitions whose turn weight is walked after the loop
+  uint16_t def[TURN ? kK2Defer : 1];
 };
 
 // Bounds beyond the ball radius (round 4).  A table holds every node within R of its exit, so a
@@ -1931,6 +1940,264 @@ __device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src
   return r;
 }
 
+// ---- k_routes_ball2 phase 2 without turn costs, software-pipelined (round 6).
+// The round-3..5 loop was two transitions per lane and step with every load of a step issued before
+// any was used -- in the source.  Its ISA was not: the probe addresses went behind exec-mask
+// branches (a select of a pointer became a branch around its LDS reads, and ball_slot's table-size
+// test another), the second transition's probes waited for the first's, and the descriptor loads'
+// registers were reused while loads were pending (the ballast `t1.x/.y` were dead, so the next
+// load's destination overlapped them and the compiler waited for the first).  Now:
+//  * a step's loads are formed branch-free: every exit's header is valid (an unusable exit, or a
+//    handed-over item, reads row 0..1 of a valid array), ball_slot_bf forms both hashes and selects;
+//  * a descriptor is 24 bytes (the entry times only of its second half);
+//  * steps are pipelined two deep with two register sets (X, Y: no copies at the back edge): a
+//    step issues its probes, then the NEXT step's descriptor loads, then waits for its probes
+//    (vmcnt counts the later descriptor loads out) and finishes its two transitions.
+#ifndef RM_K2_PIPE
+#define RM_K2_PIPE 1
+#endif
+typedef unsigned int k2_u2 __attribute__((ext_vector_type(2)));
+typedef const k2_u2 __attribute__((address_space(1)))* k2_gptr2;
+__device__ __forceinline__ uint2 k2_ld2(k2_gptr2 p) {
+  const k2_u2 v = *p;
+  return make_uint2(v.x, v.y);
+}
+// ball_slot without the branch on the table size (bits >= 1)
+__device__ __forceinline__ uint32_t ball_slot_bf(uint32_t v, uint32_t bits) {
+#ifdef RM_BALL_SLOT_RANDOM
+  return ball_slot(v, bits);
+#else
+  const uint32_t a = (v * 2654435761u) >> (32u - bits);
+  const uint32_t sh = min(32u + kBallGroupLog - bits, 31u);
+  const uint32_t gr = ((((v >> kBallGroupLog) * 2654435761u) >> sh) << kBallGroupLog) | (v & ((1u << kBallGroupLog) - 1u));
+  return bits < kBallGroupBits ? a : gr;
+#endif
+}
+struct K2Step {   // a transition in flight: its target descriptor {road, s, L, spf | spr}, entry times
+  uint4 t0;
+  uint2 t1;
+};
+struct K2Probe {  // ... and both exits' first probes of the target road
+  uint4 e1, e0;
+};
+// the descriptor of block transition q (clamped: a lane past the block's range loads a valid
+// descriptor it never uses)
+template <class SM>
+__device__ __forceinline__ void k2_issue(const SM& sm, const DevBatch& b, uint32_t q, uint32_t n, K2Step& st) {
+  const uint32_t qc = min(q, n - 1u);
+  const uint32_t di = sm.src[sm.owner[qc]].dbase + qc;
+  const uint4* dp = b.cand_desc + 2 * (uint64_t)di;
+  st.t0 = k2_ld((k2_gptr)(const void*)dp);
+  st.t1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(dp + 1) + 1));
+}
+template <class SM>
+__device__ __forceinline__ void k2_probe(const SM& sm, uint32_t q, uint32_t n, uint32_t road, K2Probe& pr) {
+  const K2Src& S = sm.src[sm.owner[min(q, n - 1u)]];
+  const uint4 h = *reinterpret_cast<const uint4*>(&S.h1);   // h1, h0
+  const k2_gptr e = (k2_gptr)(const void*)(uintptr_t)S.ent;
+  pr.e1 = k2_ld(e + (ball_row0(h.x) + ball_slot_bf(road, max(h.y, 1u))));
+  pr.e0 = k2_ld(e + (ball_row0(h.z) + ball_slot_bf(road, max(h.w, 1u))));
+}
+// a row or the empty row, selected per word (a select of the aggregate went through scratch)
+__device__ __forceinline__ uint4 k2_row_or_none(bool use, const uint4& e) {
+  return make_uint4(use ? e.x : kNone, use ? e.y : kBallNoDist, use ? e.z : kBallNoDist, use ? e.w : 0u);
+}
+// ball_resolve through a global-address-space pointer
+__device__ __forceinline__ uint4 ball_resolve_g(k2_gptr ent, const uint2& h, uint32_t road, uint4 e, uint32_t rmask) {
+  if ((e.x & rmask) == road || e.x == kNone) return e;
+  const uint32_t mask = (1u << h.y) - 1u;
+  uint32_t s = ball_slot(road, h.y);
+  for (;;) {
+    s = (s + 1u) & mask;
+    e = k2_ld(ent + (ball_row0(h.x) + s));
+    if ((e.x & rmask) == road || e.x == kNone) return e;
+  }
+}
+template <class SM>
+__device__ __forceinline__ void k2_finish(SM& sm, const DevBatch& b, uint32_t q, uint32_t n, const K2Step& st,
+                                          const K2Probe& pr, uint32_t rm) {
+  // branch-free up to the store (a conditional return let the compiler sink this step's probe
+  // loads behind it, after the next step's descriptor loads)
+  const uint32_t o = sm.owner[min(q, n - 1u)];
+  const K2Src& S = sm.src[o];
+  const bool live = q < n && S.bound != kNone;
+  const bool u = live && st.t0.w != 0u;   // some direction of the target road is usable
+  const k2_gptr ge = (k2_gptr)(const void*)(uintptr_t)S.ent;
+  const uint4 r1 = ball_resolve_g(ge, S.h1, st.t0.x, k2_row_or_none(u && S.rk1 != kKeyInf, pr.e1), rm);
+  const uint4 r0 = ball_resolve_g(ge, S.h0, st.t0.x, k2_row_or_none(u && S.rk0 != kKeyInf, pr.e0), rm);
+  bool x = true;
+  const uint32_t r = k2_route(S, st.t0, make_uint4(0u, 0u, st.t1.x, st.t1.y), r1, r0, x);
+  if (live) {
+    b.route[S.obase + q] = r;
+    if (!x) sm.redo[o] = 1;
+  }
+}
+template <class SM>
+__device__ __forceinline__ void k2_phase2_pipe(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm) {
+  uint32_t q = threadIdx.x;
+  K2Step xa, xb, ya, yb;
+  K2Probe pa, pb;
+  k2_issue(sm, b, q, n, xa);
+  k2_issue(sm, b, q + kK2Items, n, xb);
+  while (q < n) {
+    k2_probe(sm, q, n, xa.t0.x, pa);
+    k2_probe(sm, q + kK2Items, n, xb.t0.x, pb);
+    k2_issue(sm, b, q + 2 * kK2Items, n, ya);
+    k2_issue(sm, b, q + 3 * kK2Items, n, yb);
+    k2_finish(sm, b, q, n, xa, pa, rm);
+    k2_finish(sm, b, q + kK2Items, n, xb, pb, rm);
+    q += 2 * kK2Items;
+    if (q >= n) break;
+    k2_probe(sm, q, n, ya.t0.x, pa);
+    k2_probe(sm, q + kK2Items, n, yb.t0.x, pb);
+    k2_issue(sm, b, q + 2 * kK2Items, n, xa);
+    k2_issue(sm, b, q + 3 * kK2Items, n, xb);
+    k2_finish(sm, b, q, n, ya, pa, rm);
+    k2_finish(sm, b, q + kK2Items, n, yb, pb, rm);
+    q += 2 * kK2Items;
+  }
+}
+
+// k_routes_ball2<true>'s two-per-step loop (round 6): the route of a transition from the tables,
+// and what its turn weight needs -- nothing (U = 0: no turn costs, an invalid or direct route, a
+// route the tables cannot decide), the turn row of the exit that strictly gives the entry node its
+// label (`row`, read after the probes), or the walk (a tie between the exits).  The same decisions
+// as k2_route_turn.
+struct K2TurnKey {
+  uint64_t row;      // need 1: the turn row's index (the winning exit's final slot)
+  uint32_t r;        // route cm or kRouteInvalid
+  uint32_t need;     // 0: U = 0, 1: from the row, 2: walk
+  uint32_t side;     // entry at node1 (combo 3)
+  uint32_t e1;       // the winning exit is the forward one (node1)
+  bool exact;
+};
+__device__ __forceinline__ K2TurnKey k2_turn_key(const K2Src& S, uint32_t fac, const uint4& t0, const uint4& t1,
+                                                 const uint4& r1, const uint4& r0, uint32_t s1, uint32_t s0) {
+  const unsigned long long k10 = row_key0(r1), k00 = row_key0(r0), k11 = row_key1(r1), k01 = row_key1(r0);
+  const unsigned long long l10 = k10 != kKeyInf ? S.rk1 + k10 : kKeyInf, l00 = k00 != kKeyInf ? S.rk0 + k00 : kKeyInf;
+  const unsigned long long l11 = k11 != kKeyInf ? S.rk1 + k11 : kKeyInf, l01 = k01 != kKeyInf ? S.rk0 + k01 : kKeyInf;
+  const unsigned long long lab0 = l00 < l10 ? l00 : l10, lab1 = l01 < l11 ? l01 : l11;
+  const uint4 a0 = make_uint4(S.road, S.s, 0u, 0u);
+  int combo = -1;
+  const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, &combo);
+  K2TurnKey k;
+  k.exact = S.lim == kNone || (key != kKeyInf && key_dist(key) <= S.lim);
+  const bool valid = key != kKeyInf && key_dist(key) <= S.bound && key_time(key) <= S.tmax;
+  k.r = valid ? key_dist(key) : kRouteInvalid;
+  k.need = 0u;
+  k.side = combo == 3 ? 1u : 0u;
+  const unsigned long long la = k.side ? l11 : l10, lb = k.side ? l01 : l00;
+  k.e1 = la < lb ? 1u : 0u;
+  k.row = k.e1 ? ball_row0(S.h1.x) + s1 : ball_row0(S.h0.x) + s0;
+  if (fac && valid && combo >= 2 && k.exact) k.need = la != lb ? 1u : 2u;
+  return k;
+}
+// the turn weight U from the winner's turn row (wx, wy: its node0 / node1 words), or kNone when
+// it must be walked (a tie, or a row without its sum)
+__device__ __forceinline__ uint32_t k2_turn_weight(const K2TurnKey& k, uint32_t hw, uint32_t wx, uint32_t wy,
+                                                   const uint32_t* tw) {
+  if (k.need == 0u) return 0u;
+  const uint32_t w = k.side ? wy : wx;
+  if (k.need == 2u || (w & kTurnTMask) == kTurnNone) return kNone;
+  return tw[turn_degree(head_back(hw, k.e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
+}
+
+// k_routes_ball2<true> phase 2 pipelined as k2_phase2_pipe (RM_K2_TURN2 2): a step issues its
+// probes and the next step's descriptors, then forms both transitions' keys, then reads both
+// winners' turn rows together (the one dependent load more than without turn costs).
+typedef unsigned int k2_v2 __attribute__((ext_vector_type(2)));
+typedef const k2_v2 __attribute__((address_space(1)))* k2_trow;
+struct K2StepT {
+  uint4 t0;
+  uint2 t1;
+  double gc;
+};
+template <class SM>
+__device__ __forceinline__ void k2_issue_t(const SM& sm, const DevBatch& b, uint32_t q, uint32_t n, K2StepT& st) {
+  const uint32_t qc = min(q, n - 1u);
+  const K2Src& S = sm.src[sm.owner[qc]];
+  const uint4* dp = b.cand_desc + 2 * (uint64_t)(S.dbase + qc);
+  st.t0 = k2_ld((k2_gptr)(const void*)dp);
+  st.t1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(dp + 1) + 1));
+  st.gc = b.gc[S.tdesc / kMaxCand];
+}
+__device__ __forceinline__ uint4 ball_resolve_at_g(k2_gptr ent, const uint2& h, uint32_t road, uint4 e, uint32_t rmask,
+                                                   uint32_t& s) {
+  if ((e.x & rmask) == road || e.x == kNone) return e;
+  const uint32_t mask = (1u << h.y) - 1u;
+  for (;;) {
+    s = (s + 1u) & mask;
+    e = k2_ld(ent + (ball_row0(h.x) + s));
+    if ((e.x & rmask) == road || e.x == kNone) return e;
+  }
+}
+template <class SM>
+__device__ __forceinline__ K2TurnKey k2_key_t(const SM& sm, uint32_t o, bool live, const K2StepT& st, const K2Probe& pr,
+                                              uint32_t rm) {
+  const K2Src& S = sm.src[o];
+  const bool u = live && st.t0.w != 0u;
+  const k2_gptr ge = (k2_gptr)(const void*)(uintptr_t)S.ent;
+  uint32_t s1 = ball_slot_bf(st.t0.x, max(S.h1.y, 1u)), s0 = ball_slot_bf(st.t0.x, max(S.h0.y, 1u));
+  const uint4 r1 = ball_resolve_at_g(ge, S.h1, st.t0.x, k2_row_or_none(u && S.rk1 != kKeyInf, pr.e1), rm, s1);
+  const uint4 r0 = ball_resolve_at_g(ge, S.h0, st.t0.x, k2_row_or_none(u && S.rk0 != kKeyInf, pr.e0), rm, s0);
+  return k2_turn_key(S, sm.tsrc[o].fac, st.t0, make_uint4(0u, 0u, st.t1.x, st.t1.y), r1, r0, s1, s0);
+}
+template <class SM>
+__device__ __forceinline__ void k2_store_t(SM& sm, const DevBatch& b, uint32_t q, uint32_t o, bool live,
+                                           const K2TurnKey& k, uint32_t U, double gc) {
+  if (!live) return;
+  const K2Src& S = sm.src[o];
+  if (U != kNone) {
+    b.route[S.obase + q] = k.r;
+    b.route_d[S.obase + q] = route_term(k.r, U, sm.tsrc[o].fac, gc);
+    if (!k.exact) sm.redo[o] = 1;
+  } else {
+    const uint32_t i = atomicAdd(&sm.ndef, 1u);
+    if (i < kK2Defer) sm.def[i] = (uint16_t)q;
+    else sm.redo[o] = 1;   // more walks than the list holds: the search tiers take the item
+  }
+}
+template <class SM>
+__device__ __forceinline__ void k2_finish_t2(SM& sm, const DevBatch& b, uint32_t q, uint32_t n, const K2StepT& sa,
+                                             const K2Probe& pa, const K2StepT& sb, const K2Probe& pb, uint32_t rm,
+                                             k2_trow tdummy) {
+  const uint32_t qb = q + kK2Items;
+  const uint32_t oa = sm.owner[min(q, n - 1u)], ob = sm.owner[min(qb, n - 1u)];
+  const bool la = q < n && sm.src[oa].bound != kNone, lb = qb < n && sm.src[ob].bound != kNone;
+  const K2TurnKey ka = k2_key_t(sm, oa, la, sa, pa, rm);
+  const K2TurnKey kb = k2_key_t(sm, ob, lb, sb, pb, rm);
+  const k2_v2 wa = *(la && ka.need == 1u ? (k2_trow)(const void*)(uintptr_t)sm.tsrc[oa].trn + ka.row : tdummy);
+  const k2_v2 wb = *(lb && kb.need == 1u ? (k2_trow)(const void*)(uintptr_t)sm.tsrc[ob].trn + kb.row : tdummy);
+  __asm__ volatile("" ::"v"(wa.x), "v"(wa.y), "v"(wb.x), "v"(wb.y));   // both rows in flight, then used
+  const uint32_t xa = k2_turn_weight(ka, sm.tsrc[oa].hw, wa.x, wa.y, sm.tw);
+  const uint32_t xb = k2_turn_weight(kb, sm.tsrc[ob].hw, wb.x, wb.y, sm.tw);
+  k2_store_t(sm, b, q, oa, la, ka, xa, sa.gc);
+  k2_store_t(sm, b, qb, ob, lb, kb, xb, sb.gc);
+}
+template <class SM>
+__device__ __forceinline__ void k2_phase2_pipe_t(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_trow tdummy) {
+  uint32_t q = threadIdx.x;
+  K2StepT xa, xb, ya, yb;
+  K2Probe pa, pb;
+  k2_issue_t(sm, b, q, n, xa);
+  k2_issue_t(sm, b, q + kK2Items, n, xb);
+  while (q < n) {
+    k2_probe(sm, q, n, xa.t0.x, pa);
+    k2_probe(sm, q + kK2Items, n, xb.t0.x, pb);
+    k2_issue_t(sm, b, q + 2 * kK2Items, n, ya);
+    k2_issue_t(sm, b, q + 3 * kK2Items, n, yb);
+    k2_finish_t2(sm, b, q, n, xa, pa, xb, pb, rm, tdummy);
+    q += 2 * kK2Items;
+    if (q >= n) break;
+    k2_probe(sm, q, n, ya.t0.x, pa);
+    k2_probe(sm, q + kK2Items, n, yb.t0.x, pb);
+    k2_issue_t(sm, b, q + 2 * kK2Items, n, xa);
+    k2_issue_t(sm, b, q + 3 * kK2Items, n, xb);
+    k2_finish_t2(sm, b, q, n, ya, pa, yb, pb, rm, tdummy);
+    q += 2 * kK2Items;
+  }
+}
+
 template <bool TURN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_arg) {
   if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
@@ -1991,6 +2258,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     }
     if (!fits || S.h1.y == 0u || S.h0.y == 0u || !turn_ok) {   // the search tiers take it (they run later)
       S.bound = kNone;
+      // phase 2 still forms its probe addresses (branch-free): rows 0..1 of a valid array
+      S.ent = (unsigned long long)(uintptr_t)b.cand_desc;
+      S.h1 = S.h0 = make_uint2(0u, 1u);
       b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
     }
     sm.src[threadIdx.x] = S;
@@ -2016,6 +2286,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
   if (live) {
     const uint32_t rel = wbase + incl - KB;
     sm.src[threadIdx.x].rel = rel;
+    sm.src[threadIdx.x].dbase = sm.src[threadIdx.x].tdesc - rel;
+    sm.src[threadIdx.x].obase = ob - rel;
     for (uint32_t j = 0; j < KB; ++j) sm.owner[rel + j] = (uint8_t)threadIdx.x;
   }
   sm.redo[threadIdx.x] = 0;
@@ -2031,12 +2303,90 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
   const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
   const uint32_t rm = g.ball_road_mask;
   if constexpr (TURN) {
+    const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
+#if RM_K2_TURN2 == 2
+    if (threadIdx.x == 0) sm.ndef = 0u;
+    __syncthreads();
+    k2_phase2_pipe_t(sm, b, n, rm, tdummy);
+    __syncthreads();
+    const uint32_t ndef = min(sm.ndef, (uint32_t)kK2Defer);
+    for (uint32_t z = threadIdx.x; z < ndef; z += kK2Items) {
+      const uint32_t q = sm.def[z];
+#elif RM_K2_TURN2
+    // with turn costs (round 6): two transitions per lane and step, as without them.  Only the
+    // winning exit's turn row is read, after the probes, and only for a valid route that enters its
+    // target road from a node (46 % of C2's transitions; round 5 read both exits' rows of every
+    // transition with the probes: +1.7 GB of lines per step).  Routes whose weight needs the walk
+    // (a tie between the exits, a row without its sum) are listed and walked after the loop by the
+    // one-per-step code below, so the walk's registers stay out of this loop.
+    if (threadIdx.x == 0) sm.ndef = 0u;
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
+      const uint32_t qb = q + kK2Items;
+      const bool hb = qb < n;
+      const uint32_t qB = hb ? qb : q;
+      const uint32_t oa = sm.owner[q], obb = sm.owner[qB];
+      const K2Src& A = sm.src[oa];
+      const K2Src& B = sm.src[obb];
+      const bool la = A.bound != kNone, lb = hb && B.bound != kNone;
+      const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(A.tdesc + (q - A.rel)));
+      const k2_gptr db = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(B.tdesc + (qB - B.rel)));
+      const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1), tb0 = k2_ld(db), tb1 = k2_ld(db + 1);
+      const double gca = b.gc[A.tdesc / kMaxCand], gcb = b.gc[B.tdesc / kMaxCand];
+      const bool ua = la && ta0.w != 0u, ub = lb && tb0.w != 0u;
+      const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
+      const bool ub1 = ub && B.rk1 != kKeyInf, ub0 = ub && B.rk0 != kKeyInf;
+      const k2_gptr ea = (k2_gptr)A.ent, eb = (k2_gptr)B.ent;
+      uint32_t sa1 = ball_slot(ta0.x, A.h1.y), sa0 = ball_slot(ta0.x, A.h0.y);
+      uint32_t sb1 = ball_slot(tb0.x, B.h1.y), sb0 = ball_slot(tb0.x, B.h0.y);
+      const uint4 la1 = k2_ld(ua1 ? ea + (ball_row0(A.h1.x) + sa1) : dummy), la0 = k2_ld(ua0 ? ea + (ball_row0(A.h0.x) + sa0) : dummy);
+      const uint4 lb1 = k2_ld(ub1 ? eb + (ball_row0(B.h1.x) + sb1) : dummy), lb0 = k2_ld(ub0 ? eb + (ball_row0(B.h0.x) + sb0) : dummy);
+      const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+      const uint4 ra1 = ball_resolve_at((const uint4*)A.ent, A.h1, ta0.x, ua1 ? la1 : none, rm, sa1);
+      const uint4 ra0 = ball_resolve_at((const uint4*)A.ent, A.h0, ta0.x, ua0 ? la0 : none, rm, sa0);
+      const uint4 rb1 = ball_resolve_at((const uint4*)B.ent, B.h1, tb0.x, ub1 ? lb1 : none, rm, sb1);
+      const uint4 rb0 = ball_resolve_at((const uint4*)B.ent, B.h0, tb0.x, ub0 ? lb0 : none, rm, sb0);
+      const K2Turn& TA = sm.tsrc[oa];
+      const K2Turn& TB = sm.tsrc[obb];
+      const K2TurnKey ka = k2_turn_key(A, TA.fac, ta0, ta1, ra1, ra0, sa1, sa0);
+      const K2TurnKey kb = k2_turn_key(B, TB.fac, tb0, tb1, rb1, rb0, sb1, sb0);
+      // the winners' turn rows (a transition without one reads a valid dummy row)
+      const k2_v2 wa = *(la && ka.need == 1u ? (const k2_trow)(const void*)(uintptr_t)TA.trn + ka.row : tdummy);
+      const k2_v2 wb = *(lb && kb.need == 1u ? (const k2_trow)(const void*)(uintptr_t)TB.trn + kb.row : tdummy);
+      const uint32_t xa = k2_turn_weight(ka, TA.hw, wa.x, wa.y, sm.tw), xb = k2_turn_weight(kb, TB.hw, wb.x, wb.y, sm.tw);
+      // xa / xb: the turn weight U, or kNone: walk it after the loop
+      if (la) {
+        if (xa != kNone) {
+          b.route[A.ob + (q - A.rel)] = ka.r;
+          b.route_d[A.ob + (q - A.rel)] = route_term(ka.r, xa, TA.fac, gca);
+          if (!ka.exact) sm.redo[oa] = 1;
+        } else {
+          const uint32_t i = atomicAdd(&sm.ndef, 1u);
+          if (i < kK2Defer) sm.def[i] = (uint16_t)q;
+          else sm.redo[oa] = 1;   // more ties than the list holds: the search tiers take the item
+        }
+      }
+      if (lb) {
+        if (xb != kNone) {
+          b.route[B.ob + (qb - B.rel)] = kb.r;
+          b.route_d[B.ob + (qb - B.rel)] = route_term(kb.r, xb, TB.fac, gcb);
+          if (!kb.exact) sm.redo[obb] = 1;
+        } else {
+          const uint32_t i = atomicAdd(&sm.ndef, 1u);
+          if (i < kK2Defer) sm.def[i] = (uint16_t)qb;
+          else sm.redo[obb] = 1;
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t ndef = min(sm.ndef, (uint32_t)kK2Defer);
+    for (uint32_t z = threadIdx.x; z < ndef; z += kK2Items) {
+      const uint32_t q = sm.def[z];
+#else
     // with turn costs: one transition per lane and step (the turn rows and the tie walk cost the
     // two-per-step loop its registers); both exits' first probes and their turn rows issued together
-    typedef unsigned int k2_v2 __attribute__((ext_vector_type(2)));
-    typedef const k2_v2 __attribute__((address_space(1)))* k2_trow;
-    const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
     for (uint32_t q = threadIdx.x; q < n; q += kK2Items) {
+#endif
       const uint32_t o = sm.owner[q];
       const K2Src& A = sm.src[o];
       const K2Turn& TA = sm.tsrc[o];
@@ -2067,7 +2417,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
       if (!xa) sm.redo[o] = 1;
     }
   }
+#if RM_K2_PIPE
+  if constexpr (!TURN) k2_phase2_pipe(sm, b, n, rm);
+  for (uint32_t q = threadIdx.x; q < 0u; q += 2 * kK2Items) {
+#else
   for (uint32_t q = threadIdx.x; q < (TURN ? 0u : n); q += 2 * kK2Items) {
+#endif
     const uint32_t qb = q + kK2Items;
     const bool hb = qb < n;
     const uint32_t qB = hb ? qb : q;

@@ -89,18 +89,31 @@ def _proc_start_ticks(pid):
 def launch_nonce():
     """What every rank of one launch agrees on and no other launch has: the launcher's
     RM_RDZV_NONCE (bench.py self_launch sets a random one), else the parent process (torchrun's
-    agent, or whatever started the ranks) named by pid and start time."""
+    agent, or whatever started the ranks) named by pid and start time -- plus torchrun's run id and
+    restart count when present: with --max-restarts the elastic agent is the same process across
+    restarts, so a crashed attempt's file would otherwise carry the restarted attempt's nonce."""
     n = os.environ.get("RM_RDZV_NONCE")
     if n:
         return n
     ppid = os.getppid()
-    return "%d:%s" % (ppid, _proc_start_ticks(ppid))
+    return "%d:%s%s" % (ppid, _proc_start_ticks(ppid), _elastic_attempt())
+
+
+def _elastic_attempt():
+    """':<run id>:<restart count>' under torch.distributed.run (TORCHELASTIC_*), else ''."""
+    run = os.environ.get("TORCHELASTIC_RUN_ID")
+    cnt = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+    if run is None and cnt is None:
+        return ""
+    return ":%s:%s" % (run or "", cnt or "0")
 
 
 def rendezvous_path(rdzv_dir=None, token=None):
     """Node-local file through which rank 0 hands its RCCL unique id to the other ranks."""
     rdzv_dir = rdzv_dir or os.environ.get("RM_RDZV_DIR", "/tmp")
-    token = token or os.environ.get("RM_RDZV_TOKEN") or "%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+    token = token or os.environ.get("RM_RDZV_TOKEN") or "%s_%s%s" % (
+        os.environ.get("MASTER_PORT", "0"), os.getppid(),
+        "_r" + os.environ["TORCHELASTIC_RESTART_COUNT"] if os.environ.get("TORCHELASTIC_RESTART_COUNT") else "")
     return os.path.join(rdzv_dir, "rm_rdzv_%s.id" % token)
 
 

@@ -18,7 +18,7 @@ for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_IN
   echo "$TAG pmc $name done"
 done
 cd $R
-python scripts/pmc_summary.py $O $O/summary --config $CFG --traces $TR --streams 1 --tag $TAG --what "python bench.py $ARGS --steps 5 --warmup 1 --no-cpu-baseline" > $O/summary.log 2>&1 || { echo "$TAG summary failed"; tail -5 $O/summary.log; exit 1; }
+python scripts/pmc_summary.py $O $O/summary --config $CFG --traces $TR --streams 1 --tag $TAG --turn-penalty ${TURN:-0} --what "python bench.py $ARGS --steps 5 --warmup 1 --no-cpu-baseline" > $O/summary.log 2>&1 || { echo "$TAG summary failed"; tail -5 $O/summary.log; exit 1; }
 timeout -k 10 600 python -u bench.py $ARGS --traffic-json $O/summary/pmc_$TAG.json > $O/bench.json 2> $O/bench.err || { echo "$TAG bench failed"; tail -20 $O/bench.err; exit 1; }
 python - <<PY
 import json; d = json.load(open("$O/bench.json"))

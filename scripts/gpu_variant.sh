@@ -17,7 +17,7 @@ for c in $CFGS; do
   IFS=, read -r cfg tr <<< "$c"
   for v in main "$@"; do
     lib=""; [ $v != main ] && lib=$R/variants/$v.so
-    REPORTER_MATCH_LIB=$lib timeout -k 10 300 python -u scripts/perf_probe.py --config $cfg ${tr:+--traces $tr} --reps 3 > $O/${cfg}_$v.log 2>&1 || { echo "probe $cfg $v failed"; tail -5 $O/${cfg}_$v.log; exit 1; }
+    REPORTER_MATCH_LIB=$lib timeout -k 10 300 python -u scripts/perf_probe.py --config $cfg ${tr:+--traces $tr} --reps 3 $PROBE_ARGS > $O/${cfg}_$v.log 2>&1 || { echo "probe $cfg $v failed"; tail -5 $O/${cfg}_$v.log; exit 1; }
     echo "== $cfg $v"; grep rerun $O/${cfg}_$v.log | tail -1
   done
 done

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--traces", type=int, default=10000)
     ap.add_argument("--streams", type=int, default=2, help="concurrent parts the profiled bench ran (bench --streams)")
+    ap.add_argument("--turn-penalty", type=float, default=0.0, help="turn_penalty_factor of the profiled bench")
     ap.add_argument("--tag", default=None, help="output pmc_<tag>.json instead of pmc_routes_<config>.json")
     ap.add_argument("--what", default="python bench.py --steps 10 --warmup 2 --no-cpu-baseline",
                     help="the profiled command, for the kernel-stats title")
@@ -96,6 +97,7 @@ def main():
     sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
     rt = dict(stages["routes"])
     rt.update({"config": a.config, "traces": a.traces, "streams": a.streams, "engine_sha": sha, "read_factor": 2,
+               "turn_penalty": a.turn_penalty,
                "stages": stages,
                "note": "per-step sums of per-dispatch averages from separate --pmc passes; read side doubled per "
                        "MI355X_MICROARCH.md HBM, which profiles/r02/calib confirms for 16-B random gathers "

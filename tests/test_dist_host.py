@@ -204,6 +204,27 @@ def test_rendezvous_ignores_a_stale_id(tmp_path):
     assert dist.launch_nonce().startswith("%d:" % os.getppid()) and dist.launch_nonce() != "%d:0" % os.getppid()
 
 
+def test_rendezvous_nonce_changes_across_elastic_restarts(monkeypatch, tmp_path):
+    """under torchrun --max-restarts the agent (the ranks' parent) survives a restart,
+    so the nonce and the rendezvous file name also carry TORCHELASTIC_RUN_ID / _RESTART_COUNT: a
+    crashed attempt's id file is not accepted by the next attempt's ranks."""
+    from reporter_amd import dist
+    monkeypatch.delenv("RM_RDZV_NONCE", raising=False)
+    monkeypatch.delenv("RM_RDZV_TOKEN", raising=False)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "job7")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "0")
+    n0, p0 = dist.launch_nonce(), dist.rendezvous_path(str(tmp_path))
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    n1, p1 = dist.launch_nonce(), dist.rendezvous_path(str(tmp_path))
+    assert n0 != n1 and p0 != p1 and n1.endswith(":job7:1")
+    # attempt 0's file at attempt 1's path (same pid, port) is ignored until rank 0 replaces it
+    dist.rendezvous(0, p1, lambda: os.urandom(128), 128, nonce=n0)
+    with pytest.raises(TimeoutError):
+        dist.rendezvous(1, p1, None, 128, timeout_s=0.3, nonce=n1)
+    fresh = dist.rendezvous(0, p1, lambda: os.urandom(128), 128, nonce=n1)
+    assert dist.rendezvous(1, p1, None, 128, timeout_s=5, nonce=n1) == fresh
+
+
 def test_shard_ids_partition_one_workload():
     """bench.shard_ids: every trace of the seeded N x n set on exactly one rank."""
     sys.path.insert(0, ROOT)
