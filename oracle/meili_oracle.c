@@ -147,27 +147,59 @@ static double og_bearing_deg(double dx, double dy) {
   else th = dy < 0.0 ? OG_PI + a : 2.0 * OG_PI - a;
   return th * (180.0 / OG_PI);
 }
-/* heading stored as Valhalla's NodeInfo does (8 bits, 360/255 degree steps) and expanded back to
- * whole degrees 0..360 */
-static uint32_t og_heading(float lon_a, float lat_a, float lon_b, float lat_b) {
-  const double dx = ((double)lon_b - (double)lon_a) * (double)og_mlon(lat_a);
-  const double dy = ((double)lat_b - (double)lat_a) * MPD_LAT;
-  const uint32_t h8 = (uint32_t)(og_bearing_deg(dx, dy) * (255.0 / 360.0) + 0.5);
-  return (h8 * 360u + 127u) / 255u;
+/* ---- headings: Valhalla's NodeInfo edge headings (mjolnir graph builder: round(PointLL::
+ * HeadingAlongPolyline(shape, kMetersOffsetForHeading = 30 m)), 8-bit storage round(h * 255/359),
+ * read back as round(h8 * 359/255)).  External (Valhalla 2.x, absent here) and restated from its
+ * published behaviour; DESIGN.md rule 3b.  PointLL::Heading is the initial great-circle bearing. */
+static double og_gc(float lon_a, float lat_a, float lon_b, float lat_b);
+static double og_initial_bearing(float lon_a, float lat_a, float lon_b, float lat_b) {
+  if (lon_a == lon_b && lat_a == lat_b) return 0.0;
+  const double p1 = (double)lat_a * DEG2RAD, p2 = (double)lat_b * DEG2RAD;
+  const double dl = ((double)lon_b - (double)lon_a) * DEG2RAD;
+  const double east = og_sin(dl) * og_cos(p2);
+  const double north = og_cos(p1) * og_sin(p2) - og_sin(p1) * og_cos(p2) * og_cos_wide(dl);
+  return og_bearing_deg(east, north);
 }
-/* per road: heading at node0 into the road (H0) and at node1 into the road (H1), each toward the
- * first shape vertex that differs from the node's */
-static void og_road_headings(const og_graph* g, uint16_t* H0, uint16_t* H1) {
-  for (uint32_t r = 0; r < g->n_roads; ++r) {
-    const uint32_t a = g->road_vert_off[r], b = g->road_vert_off[r + 1] - 1;
-    const uint32_t* V = g->verts;
-    uint32_t k = a + 1;
-    while (k < b && V[4 * k] == V[4 * a] && V[4 * k + 1] == V[4 * a + 1]) ++k;
-    H0[r] = (uint16_t)og_heading(f32_of(V[4 * a]), f32_of(V[4 * a + 1]), f32_of(V[4 * k]), f32_of(V[4 * k + 1]));
-    k = b - 1;
-    while (k > a && V[4 * k] == V[4 * b] && V[4 * k + 1] == V[4 * b + 1]) --k;
-    H1[r] = (uint16_t)og_heading(f32_of(V[4 * b]), f32_of(V[4 * b + 1]), f32_of(V[4 * k]), f32_of(V[4 * k + 1]));
+/* HeadingAlongPolyline over n >= 2 shape points xs/ys (start node first) */
+static double og_heading_along(const float* xs, const float* ys, uint32_t n) {
+  if (n == 2) return og_initial_bearing(xs[0], ys[0], xs[1], ys[1]);
+  double d = 0.0;
+  for (uint32_t i = 0; i + 1 < n && d < 30.0; ++i) {
+    const double seg = og_gc(xs[i], ys[i], xs[i + 1], ys[i + 1]);
+    if (d + seg > 30.0) {
+      const double f = (30.0 - d) / seg;
+      const float x = (float)((double)xs[i] + ((double)xs[i + 1] - (double)xs[i]) * f);
+      const float y = (float)((double)ys[i] + ((double)ys[i + 1] - (double)ys[i]) * f);
+      return og_initial_bearing(xs[0], ys[0], x, y);
+    }
+    d += seg;
   }
+  return og_initial_bearing(xs[0], ys[0], xs[n - 1], ys[n - 1]);
+}
+static uint32_t og_node_heading(double h) {
+  const uint32_t hd = (uint32_t)floor(h + 0.5) % 360u;
+  const uint32_t h8 = (uint32_t)floorf((float)hd * (255.0f / 359.0f) + 0.5f);
+  return (uint32_t)floorf((float)h8 * (359.0f / 255.0f) + 0.5f);
+}
+/* per road: the heading of its forward edge at node0 (H0) and of its reverse edge at node1 (H1) */
+static void og_road_headings(const og_graph* g, uint16_t* H0, uint16_t* H1) {
+  uint32_t cap = 0;
+  float *xs = NULL, *ys = NULL;
+  for (uint32_t r = 0; r < g->n_roads; ++r) {
+    const uint32_t a = g->road_vert_off[r], n = g->road_vert_off[r + 1] - a;
+    if (n > cap) {
+      cap = n * 2;
+      xs = (float*)realloc(xs, cap * sizeof(float));
+      ys = (float*)realloc(ys, cap * sizeof(float));
+    }
+    const uint32_t* V = g->verts;
+    for (uint32_t i = 0; i < n; ++i) { xs[i] = f32_of(V[4 * (a + i)]); ys[i] = f32_of(V[4 * (a + i) + 1]); }
+    H0[r] = (uint16_t)og_node_heading(og_heading_along(xs, ys, n));
+    for (uint32_t i = 0; i < n; ++i) { xs[i] = f32_of(V[4 * (a + n - 1 - i)]); ys[i] = f32_of(V[4 * (a + n - 1 - i) + 1]); }
+    H1[r] = (uint16_t)og_node_heading(og_heading_along(xs, ys, n));
+  }
+  free(xs);
+  free(ys);
 }
 static uint32_t og_tu[181];
 static void og_turn_table(void) {

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cctype>
 #include <chrono>
 #include <cmath>
@@ -1280,6 +1281,9 @@ int rm_runner_route_tiers(rm_runner* r, uint64_t out[10]) {
     r->m->ctl_words(c);
     out[0] = c[1]; out[1] = c[3]; out[2] = c[5]; out[3] = c[8]; out[4] = c[9]; out[5] = c[10];
     out[6] = c[11]; out[7] = c[12]; out[8] = c[13]; out[9] = c[14];
+#ifdef RM_K2_STATS
+    out[9] = c[15];   // diagnostic build: K2's walked turn weights
+#endif
   });
 }
 int rm_runner_get_states(rm_runner* r, uint32_t* a, uint32_t* b) { return guarded([&] { r->m->get_states(a, b); }); }
@@ -1343,15 +1347,97 @@ struct rm_comm {
   int rank = 0, nranks = 1;
   rm_host_allgather_fn host_fn = nullptr;   // set: every collective runs over this host transport
   void* host_ctx = nullptr;
+  std::atomic<bool> broken{false};          // a collective missed its deadline (library mode): unusable
 };
 
 namespace {
-// every rank's `bytes` host bytes, in rank order (host transport)
+double comm_timeout_s();
+// RM_COMM_TIMEOUT_EXIT (default 1): a rank whose peers miss the deadline ends its process with
+// status 3 (a failed rank, never a re-exec: what a launcher like torchrun expects); 0 (library
+// hosts such as the Python service): the call returns an error instead and the communicator is
+// left unusable -- every later call on it fails at once.
+bool comm_timeout_exit() {
+  const char* e = std::getenv("RM_COMM_TIMEOUT_EXIT");
+  return !(e && *e == '0');
+}
+
+// Every call that waits on the other ranks -- init, the collectives' enqueue and their stream
+// wait, a host transport's all-gather -- runs under one deadline, RM_COMM_TIMEOUT_S (VERDICT r05
+// item 9: round 5 bounded the init only).  Exit mode: fn runs on this thread and a watchdog thread
+// ends the process at the deadline.  Library mode: fn runs on a helper thread that owns everything
+// it touches (captured by value); at the deadline this call throws, the communicator is marked
+// broken and the helper is left behind, blocked where the peers left it.
+template <class F>
+void comm_bounded(rm_comm* c, int rank, int nranks, const char* what, F fn) {
+  if (c && c->broken.load()) throw std::runtime_error(std::string(what) + ": the communicator missed a deadline earlier and is unusable");
+  const double limit = comm_timeout_s();
+  struct St {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    std::exception_ptr err;
+  };
+  auto st = std::make_shared<St>();
+  if (comm_timeout_exit()) {
+    std::thread wd([st, limit, what, rank, nranks] {
+      std::unique_lock<std::mutex> lk(st->mu);
+      if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; })) {
+        std::fprintf(stderr, "%s: rank %d of %d: the other ranks did not complete within %d s (RM_COMM_TIMEOUT_S); "
+                             "exiting with status 3\n", what, rank, nranks, (int)limit);
+        std::fflush(stderr);
+        std::_Exit(3);
+      }
+    });
+    try {
+      fn();
+    } catch (...) {
+      st->err = std::current_exception();
+    }
+    {
+      std::lock_guard<std::mutex> lk(st->mu);
+      st->done = true;
+    }
+    st->cv.notify_all();
+    wd.join();
+    if (st->err) std::rethrow_exception(st->err);
+    return;
+  }
+  std::thread worker([st, fn]() mutable {
+    std::exception_ptr e;
+    try {
+      fn();
+    } catch (...) {
+      e = std::current_exception();
+    }
+    std::lock_guard<std::mutex> lk(st->mu);
+    st->err = e;
+    st->done = true;
+    st->cv.notify_all();
+  });
+  std::unique_lock<std::mutex> lk(st->mu);
+  if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; })) {
+    lk.unlock();
+    worker.detach();
+    if (c) c->broken = true;
+    throw std::runtime_error(std::string(what) + ": no completion within " + std::to_string((int)limit) +
+                             " s (RM_COMM_TIMEOUT_S): a rank stopped; the communicator is unusable");
+  }
+  lk.unlock();
+  worker.join();
+  if (st->err) std::rethrow_exception(st->err);
+}
+
+// every rank's `bytes` host bytes, in rank order (host transport), under the deadline
 std::vector<uint8_t> host_gather(rm_comm* c, const void* send, size_t bytes) {
-  std::vector<uint8_t> all(bytes * (size_t)c->nranks + 1);
-  if (c->host_fn(c->host_ctx, send, bytes, all.data()) != 0) throw std::runtime_error("host all-gather failed");
-  all.resize(bytes * (size_t)c->nranks);
-  return all;
+  auto all = std::make_shared<std::vector<uint8_t>>(bytes * (size_t)c->nranks + 1);
+  auto mine = std::make_shared<std::vector<uint8_t>>((const uint8_t*)send, (const uint8_t*)send + bytes);
+  const rm_host_allgather_fn fn = c->host_fn;
+  void* ctx = c->host_ctx;
+  comm_bounded(c, c->rank, c->nranks, "host all-gather", [fn, ctx, all, mine, bytes] {
+    if (fn(ctx, mine->data(), bytes, all->data()) != 0) throw std::runtime_error("host all-gather failed");
+  });
+  all->resize(bytes * (size_t)c->nranks);
+  return std::move(*all);
 }
 
 // element-wise reduction of every rank's buffer in rank order (host transport)
@@ -1397,18 +1483,28 @@ void nccl_done(ncclComm_t comm, ncclResult_t r, const char* what) {
 
 // the tile stage's collectives over RCCL
 struct RcclTileComm final : TileComm {
+  rm_comm* c;
   ncclComm_t nc;
   void* scratch;
-  RcclTileComm(rm_comm* c) : nc(c->comm), scratch(c->scratch) { rank = c->rank; nranks = c->nranks; }
+  RcclTileComm(rm_comm* cc) : c(cc), nc(cc->comm), scratch(cc->scratch) { rank = cc->rank; nranks = cc->nranks; }
   uint64_t max_u64(uint64_t v, hipStream_t st) override {
-    RM_HIP(hipMemcpyAsync(scratch, &v, 8, hipMemcpyHostToDevice, st));
-    nccl_done(nc, ncclAllReduce(scratch, scratch, 1, ncclUint64, ncclMax, nc, st), "ncclAllReduce");
-    RM_HIP(hipMemcpyAsync(&v, scratch, 8, hipMemcpyDeviceToHost, st));
-    RM_HIP(hipStreamSynchronize(st));
-    return v;
+    auto x = std::make_shared<uint64_t>(v);
+    ncclComm_t n = nc;
+    void* sc = scratch;
+    comm_bounded(c, rank, nranks, "tile all-reduce", [=] {
+      RM_HIP(hipMemcpyAsync(sc, x.get(), 8, hipMemcpyHostToDevice, st));
+      nccl_done(n, ncclAllReduce(sc, sc, 1, ncclUint64, ncclMax, n, st), "ncclAllReduce");
+      RM_HIP(hipMemcpyAsync(x.get(), sc, 8, hipMemcpyDeviceToHost, st));
+      RM_HIP(hipStreamSynchronize(st));
+    });
+    return *x;
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override {
-    nccl_done(nc, ncclAllGather(send, recv, bytes, ncclUint8, nc, st), "ncclAllGather");
+    ncclComm_t n = nc;
+    comm_bounded(c, rank, nranks, "tile all-gather", [=] {
+      nccl_done(n, ncclAllGather(send, recv, bytes, ncclUint8, n, st), "ncclAllGather");
+      RM_HIP(hipStreamSynchronize(st));
+    });
   }
 };
 
@@ -1513,29 +1609,15 @@ rm_comm* rm_comm_init(int nranks, int rank, const uint8_t id[128], int device) {
     // A bounded wait for the peers: a rank whose peers never join (a crashed
     // launch, a stale rendezvous id) must fail, not block in the init forever.  RCCL's init cannot
     // be cancelled once its bootstrap waits for the peers (aborting a non-blocking init hung in
-    // tests), so a watchdog ends the process with status 3 and a message after
-    // RM_COMM_TIMEOUT_S seconds (default 300) -- a failure of this rank, never a re-exec.
-    std::mutex mu;
-    std::condition_variable cv;
-    bool done = false;
-    const double limit = comm_timeout_s();
-    std::thread watchdog([&] {
-      std::unique_lock<std::mutex> lk(mu);
-      if (!cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return done; })) {
-        std::fprintf(stderr, "rm_comm_init: rank %d of %d: the other ranks did not join within %d s (RM_COMM_TIMEOUT_S); "
-                             "exiting with status 3\n", rank, nranks, (int)limit);
-        std::fflush(stderr);
-        std::_Exit(3);
-      }
+    // tests), so at RM_COMM_TIMEOUT_S seconds (default 300) the process ends with status 3, or
+    // (RM_COMM_TIMEOUT_EXIT=0) this call fails and the blocked init is left behind (comm_bounded).
+    auto res = std::make_shared<std::pair<ncclComm_t, ncclResult_t>>(nullptr, ncclSuccess);
+    comm_bounded(nullptr, rank, nranks, "rm_comm_init", [=] {
+      RM_HIP(hipSetDevice(device));
+      res->second = ncclCommInitRank(&res->first, nranks, uid, rank);
     });
-    const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      done = true;
-    }
-    cv.notify_all();
-    watchdog.join();
-    if (r != ncclSuccess) c->comm = nullptr;
+    const ncclResult_t r = res->second;
+    c->comm = r == ncclSuccess ? res->first : nullptr;
     nccl_check(r, "ncclCommInitRank");
     RM_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     RM_HIP(hipMalloc(&c->scratch, 8));
@@ -1611,9 +1693,14 @@ int rm_comm_allreduce(rm_comm* c, void* buf, size_t count, int dtype, int op) {
     }
     const ncclDataType_t dt = dtype == 0 ? ncclUint32 : (dtype == 1 ? ncclUint64 : ncclFloat64);
     const ncclRedOp_t ro = op == 0 ? ncclSum : ncclMax;
-    RM_HIP(hipSetDevice(c->device));
-    nccl_done(c->comm, ncclAllReduce(buf, buf, count, dt, ro, c->comm, c->stream), "ncclAllReduce");
-    RM_HIP(hipStreamSynchronize(c->stream));
+    const int dev = c->device;
+    ncclComm_t nc = c->comm;
+    hipStream_t cs = c->stream;
+    comm_bounded(c, c->rank, c->nranks, "rm_comm_allreduce", [=] {
+      RM_HIP(hipSetDevice(dev));
+      nccl_done(nc, ncclAllReduce(buf, buf, count, dt, ro, nc, cs), "ncclAllReduce");
+      RM_HIP(hipStreamSynchronize(cs));
+    });
   });
 }
 
@@ -1628,13 +1715,16 @@ int rm_comm_reduce_scatter(rm_comm* c, void* buf, size_t count_per_rank, int dty
     }
     const ncclDataType_t dt = dtype == 0 ? ncclUint32 : (dtype == 1 ? ncclUint64 : ncclFloat64);
     const size_t es = dtype == 0 ? 4 : 8;
-    RM_HIP(hipSetDevice(c->device));
-    // in place: this rank's chunk of the nranks-chunk buffer receives the reduction
-    nccl_done(c->comm,
-              ncclReduceScatter(buf, (uint8_t*)buf + lo * es, count_per_rank, dt, op == 0 ? ncclSum : ncclMax, c->comm,
-                                c->stream),
-              "ncclReduceScatter");
-    RM_HIP(hipStreamSynchronize(c->stream));
+    const int dev = c->device;
+    ncclComm_t nc = c->comm;
+    hipStream_t cs = c->stream;
+    comm_bounded(c, c->rank, c->nranks, "rm_comm_reduce_scatter", [=] {
+      RM_HIP(hipSetDevice(dev));
+      // in place: this rank's chunk of the nranks-chunk buffer receives the reduction
+      nccl_done(nc, ncclReduceScatter(buf, (uint8_t*)buf + lo * es, count_per_rank, dt, op == 0 ? ncclSum : ncclMax, nc, cs),
+                "ncclReduceScatter");
+      RM_HIP(hipStreamSynchronize(cs));
+    });
   });
 }
 
@@ -1646,12 +1736,19 @@ int rm_comm_allreduce_host_f64(rm_comm* c, double* value, int op) {
       reduce_ranks(value, all.data(), 1, c->nranks, op);
       return;
     }
-    RM_HIP(hipSetDevice(c->device));
-    RM_HIP(hipMemcpyAsync(c->scratch, value, 8, hipMemcpyHostToDevice, c->stream));
-    nccl_done(c->comm, ncclAllReduce(c->scratch, c->scratch, 1, ncclFloat64, op == 0 ? ncclSum : ncclMax, c->comm, c->stream),
-              "ncclAllReduce");
-    RM_HIP(hipMemcpyAsync(value, c->scratch, 8, hipMemcpyDeviceToHost, c->stream));
-    RM_HIP(hipStreamSynchronize(c->stream));
+    const int dev = c->device;
+    ncclComm_t nc = c->comm;
+    hipStream_t cs = c->stream;
+    void* scratch = c->scratch;
+    auto v = std::make_shared<double>(*value);
+    comm_bounded(c, c->rank, c->nranks, "rm_comm_allreduce_host_f64", [=] {
+      RM_HIP(hipSetDevice(dev));
+      RM_HIP(hipMemcpyAsync(scratch, v.get(), 8, hipMemcpyHostToDevice, cs));
+      nccl_done(nc, ncclAllReduce(scratch, scratch, 1, ncclFloat64, op == 0 ? ncclSum : ncclMax, nc, cs), "ncclAllReduce");
+      RM_HIP(hipMemcpyAsync(v.get(), scratch, 8, hipMemcpyDeviceToHost, cs));
+      RM_HIP(hipStreamSynchronize(cs));
+    });
+    *value = *v;
   });
 }
 

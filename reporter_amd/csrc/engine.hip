@@ -2310,6 +2310,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     k2_phase2_pipe_t(sm, b, n, rm, tdummy);
     __syncthreads();
     const uint32_t ndef = min(sm.ndef, (uint32_t)kK2Defer);
+#ifdef RM_K2_STATS
+    if (threadIdx.x == 0) atomicAdd(&b.ctl[15], sm.ndef);   // diagnostic: walked turn weights
+#endif
     for (uint32_t z = threadIdx.x; z < ndef; z += kK2Items) {
       const uint32_t q = sm.def[z];
 #elif RM_K2_TURN2
@@ -3700,8 +3703,31 @@ __device__ __forceinline__ VitChunk vit_layout(const VitLayerDesc& d, uint32_t s
 // <= 256 routes / 16 rows from there, inside the pools' slack (the route pools hold >= 1,024
 // entries past the batch's routes, the point arrays >= 64 points past its points: ensure /
 // ensure_trans_raw).  What lies past the chunk is staged but never selected.
+// Round 6: the loads past the chunk's routes and rows are clamped to its last
+// route / row (the same lines again) instead of reading kVitRoutes routes and 16 rows whatever the
+// chunk holds -- C2 K3 moved 1.73x its algorithmic bytes.  Still one unconditional load per slot
+// (a v_min, no branch, no register merge).
+#ifndef RM_VIT_CLAMP
+#define RM_VIT_CLAMP 1
+#endif
 template <bool TURN>
 __device__ __forceinline__ void vit_load(const DevBatch& b, uint32_t o, const VitChunk& c, int j, VitRegs<TURN>& r) {
+#if RM_VIT_CLAMP
+  const uint32_t rl = c.nroutes ? c.nroutes - 1u : 0u;                  // the chunk's last route
+  const uint32_t sl = c.C ? c.C * (kMaxCand / 4) - 1u : 0u;             // ... and its last row quarter
+  if constexpr (TURN) {
+    const double* rp = b.route_d + c.rbase;
+#pragma unroll
+    for (int x = 0; x < kVitRoutes / 16; ++x) r.rd[x] = rp[min((uint32_t)(16 * x + j), rl)];
+  } else {
+    const uint32_t* rp = b.route + c.rbase;
+#pragma unroll
+    for (int x = 0; x < kVitRoutes / 16; ++x) r.rv[x] = rp[min((uint32_t)(16 * x + j), rl)];
+  }
+  const v3_f4* src = reinterpret_cast<const v3_f4*>(b.cand_sq) + (uint64_t)(c.C ? o + c.s0 : 0u) * (kMaxCand / 4);
+#pragma unroll
+  for (int x = 0; x < 4; ++x) r.sv[x] = src[min((uint32_t)(16 * x + j), sl)];
+#else
   if constexpr (TURN) {
     const double* rp = b.route_d + c.rbase + j;
 #pragma unroll
@@ -3714,6 +3740,7 @@ __device__ __forceinline__ void vit_load(const DevBatch& b, uint32_t o, const Vi
   const v3_f4* src = reinterpret_cast<const v3_f4*>(b.cand_sq) + (uint64_t)(c.C ? o + c.s0 : 0u) * (kMaxCand / 4) + j;
 #pragma unroll
   for (int x = 0; x < 4; ++x) r.sv[x] = src[16 * x];
+#endif
 }
 
 template <bool TURN>
@@ -4981,20 +5008,16 @@ Engine::Engine(const Graph& g, int device) : device_(device), host_(g) {
   dg_.road_rev = upload(allocs_, g.road_rev);
   dg_.road_len = upload(allocs_, g.road_len_cm);
   {
-    // turn costs (rule 3b): each road's headings at node0 and node1 into it, toward the first
-    // shape vertex off the node, and the turn weights round(65536 exp(-d/45))
+    // turn costs (rule 3b): each road's headings at node0 and node1 into it, as Valhalla's
+    // NodeInfo holds them (heading_along: 30 m along the shape), and the turn weights
+    // round(65536 exp(-d/45))
     std::vector<uint32_t> hw(g.num_roads());
-    const auto same = [&](uint32_t i, uint32_t j) {   // bitwise, as the oracle compares them
-      return std::memcmp(&g.verts[i].lon, &g.verts[j].lon, 4) == 0 && std::memcmp(&g.verts[i].lat, &g.verts[j].lat, 4) == 0;
-    };
     for (uint32_t r = 0; r < g.num_roads(); ++r) {
-      const uint32_t a = g.road_vert_off[r], b = g.road_vert_off[r + 1] - 1;
-      uint32_t k = a + 1;
-      while (k < b && same(k, a)) ++k;
-      const uint32_t h0 = heading_deg(g.verts[a].lon, g.verts[a].lat, g.verts[k].lon, g.verts[k].lat);
-      k = b - 1;
-      while (k > a && same(k, b)) --k;
-      const uint32_t h1 = heading_deg(g.verts[b].lon, g.verts[b].lat, g.verts[k].lon, g.verts[k].lat);
+      const uint32_t a = g.road_vert_off[r], b = g.road_vert_off[r + 1] - 1, n = b - a + 1;
+      const auto fwd = [&](uint32_t i, float& lon, float& lat) { lon = g.verts[a + i].lon; lat = g.verts[a + i].lat; };
+      const auto rev = [&](uint32_t i, float& lon, float& lat) { lon = g.verts[b - i].lon; lat = g.verts[b - i].lat; };
+      const uint32_t h0 = node_heading_deg(heading_along(fwd, n));
+      const uint32_t h1 = node_heading_deg(heading_along(rev, n));
       hw[r] = h0 | h1 << 16;
     }
     dg_.road_head = upload(allocs_, hw);

@@ -10,6 +10,7 @@
 // without fast-math, so fp32/fp64 results are bit-identical between the host
 // oracle (gcc, SSE) and the device (hipcc, gfx950).
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #if defined(__HIP__) || defined(__HIPCC__)
@@ -174,12 +175,55 @@ RM_HD double det_bearing_deg(double dx, double dy) {
   else th = dy < 0.0 ? kPi + a : 2.0 * kPi - a;
   return th * (180.0 / kPi);
 }
-// heading from a to b in whole degrees 0..360 through Valhalla's 8-bit storage
-RM_HD uint32_t heading_deg(float lon_a, float lat_a, float lon_b, float lat_b) {
-  const double dx = ((double)lon_b - (double)lon_a) * (double)(float)(kMetersPerDegLonEq * det_cos((double)lat_a * kDegToRad));
-  const double dy = ((double)lat_b - (double)lat_a) * kMetersPerDegLat;
-  const uint32_t h8 = (uint32_t)(det_bearing_deg(dx, dy) * (255.0 / 360.0) + 0.5);
-  return (h8 * 360u + 127u) / 255u;
+// Round 6: an edge's heading at its start node as Valhalla's graph builder stores
+// it in NodeInfo -- round(PointLL::HeadingAlongPolyline(shape, kMetersOffsetForHeading = 30 m)):
+// the initial great-circle bearing from the node to the point 30 m along the edge's shape (the
+// segment that passes 30 m, by PointLL::Distance, interpolated linearly in lon/lat), or to the
+// shape's last point when the edge is shorter (two-point shapes: to the other end) -- kept in 8 bits
+// (round(h * 255/359)) and expanded back to degrees (round(h8 * 359/255)).  Curved ways turn by
+// their direction 30 m out, not by their first vertex.  Restated from Valhalla 2.x (external,
+// absent here): parity of these degrees with meili is unpinned (DESIGN.md rule 3b).
+constexpr double kHeadingOffsetM = 30.0;
+RM_HD double det_heading(float lon_a, float lat_a, float lon_b, float lat_b) {   // PointLL::Heading
+  if (lon_a == lon_b && lat_a == lat_b) return 0.0;
+  const double la = (double)lat_a * kDegToRad, lb = (double)lat_b * kDegToRad;
+  const double dl = ((double)lon_b - (double)lon_a) * kDegToRad;
+  const double y = det_sin(dl) * det_cos(lb);                                     // east
+  const double x = det_cos(la) * det_sin(lb) - det_sin(la) * det_cos(lb) * det_cos_wide(dl);   // north
+  return det_bearing_deg(y, x);
+}
+// pt(i, lon, lat): shape point i of the edge (0 = its start node), n >= 2 points
+template <class P>
+RM_HD double heading_along(const P& pt, uint32_t n) {   // PointLL::HeadingAlongPolyline
+  float lon0, lat0, lon1, lat1;
+  pt(0u, lon0, lat0);
+  if (n == 2u) {
+    pt(1u, lon1, lat1);
+    return det_heading(lon0, lat0, lon1, lat1);
+  }
+  double d = 0.0;
+  float la = lon0, ta = lat0;
+  for (uint32_t i = 0; i + 1u < n && d < kHeadingOffsetM; ++i) {
+    pt(i + 1u, lon1, lat1);
+    const double seg = gc_distance(la, ta, lon1, lat1);
+    if (d + seg > kHeadingOffsetM) {
+      const double pct = (kHeadingOffsetM - d) / seg;
+      const float lon = (float)((double)la + ((double)lon1 - (double)la) * pct);
+      const float lat = (float)((double)ta + ((double)lat1 - (double)ta) * pct);
+      return det_heading(lon0, lat0, lon, lat);
+    }
+    d += seg;
+    la = lon1;
+    ta = lat1;
+  }
+  pt(n - 1u, lon1, lat1);
+  return det_heading(lon0, lat0, lon1, lat1);
+}
+// whole degrees -> NodeInfo's 8 bits -> degrees 0..359
+RM_HD uint32_t node_heading_deg(double h) {
+  const uint32_t hd = (uint32_t)floor(h + 0.5) % 360u;
+  const uint32_t h8 = (uint32_t)floorf((float)hd * (255.0f / 359.0f) + 0.5f);
+  return (uint32_t)floorf((float)h8 * (359.0f / 255.0f) + 0.5f);
 }
 // turn angle class between an edge arriving with back heading hb (at the node, pointing the way
 // it came) and an edge leaving with heading hs: 0 (U-turn) .. 180 (straight on)

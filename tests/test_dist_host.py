@@ -280,3 +280,84 @@ def test_tcp_allgather_world3(tmp_path, built_lib):
     for r in res:
         assert r["parts"] == ["010101", "020202", "030303"]
         assert r["big_ok"] and r["sum"] == 7.0 and r["max"] == 2.0
+
+
+def _stall_rank(rank, world, port, exit_mode, out_dir):
+    """Rank 1 joins one all-reduce, then stops (never joins the second); rank 0 must fail within
+    RM_COMM_TIMEOUT_S -- by exiting with status 3 (exit mode) or with an error (library mode)."""
+    sys.path.insert(0, ROOT)
+    import datetime
+    import time
+
+    import torch
+    import torch.distributed as tdist
+
+    from reporter_amd import _lib, dist
+    os.environ["RM_COMM_TIMEOUT_S"] = "3"
+    os.environ["RM_COMM_TIMEOUT_EXIT"] = "1" if exit_mode else "0"
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+
+    def gloo_allgather(b):
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(world)]
+        tdist.all_gather(out, t)
+        return [o.numpy().tobytes() for o in out]
+
+    comm = dist.Comm(rank, world, -1, allgather=gloo_allgather)
+    h = np.arange(8, dtype=np.uint32) + rank
+    comm.allreduce(h.ctypes.data, h.size, dist.U32, dist.SUM)   # both ranks: completes
+    res = {"first": h.tolist()}
+    if rank == 1:
+        time.sleep(10)   # stopped: the second all-reduce never sees this rank
+        os._exit(0)
+    t0 = time.time()
+    try:
+        comm.allreduce(h.ctypes.data, h.size, dist.U32, dist.SUM)
+        res["second"] = "completed"
+    except _lib.RmError as e:
+        res["second"] = str(e)
+    res["elapsed"] = time.time() - t0
+    t1 = time.time()
+    try:   # the broken communicator fails at once
+        comm.allreduce_host(1.0, dist.SUM)
+        res["third"] = "completed"
+    except _lib.RmError as e:
+        res["third"] = str(e)
+    res["third_elapsed"] = time.time() - t1
+    with open(os.path.join(out_dir, "stall%d.json" % rank), "w") as f:
+        json.dump(res, f)
+    os._exit(0)   # the stuck helper thread and process group are left behind
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("exit_mode", [True, False])
+def test_collective_bounded_when_a_rank_stops(tmp_path, built_lib, exit_mode):
+    """every collective (not only the init) runs under RM_COMM_TIMEOUT_S.  A
+    rank whose peer stops mid-run fails within the bound: status 3 by default (a failed rank for
+    the launcher, never a re-exec), or with RM_COMM_TIMEOUT_EXIT=0 (library hosts) an error from
+    the call, after which the communicator refuses every call at once."""
+    import multiprocessing as mp
+    import time
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_rank, args=(r, 2, port, exit_mode, str(tmp_path))) for r in range(2)]
+    t0 = time.time()
+    for p in procs:
+        p.start()
+    procs[0].join(60)
+    elapsed = time.time() - t0
+    assert procs[0].exitcode is not None, "rank 0 did not fail within the bound"
+    if exit_mode:
+        assert procs[0].exitcode == 3 and elapsed < 45
+        assert not os.path.exists(str(tmp_path / "stall0.json"))
+    else:
+        assert procs[0].exitcode == 0
+        r0 = json.load(open(str(tmp_path / "stall0.json")))
+        assert r0["first"] == (np.arange(8) * 2 + 1).tolist()
+        assert "RM_COMM_TIMEOUT_S" in r0["second"] and 2.5 < r0["elapsed"] < 15, r0
+        assert "unusable" in r0["third"] and r0["third_elapsed"] < 1.0, r0
+    procs[1].join(20)
+    if procs[1].exitcode is None:
+        procs[1].kill()

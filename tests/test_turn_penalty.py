@@ -44,15 +44,54 @@ def test_configure_accepts_stock_turn_costs(built_lib, tmp_path):
 
 # ---- an independent restatement of rule 3b (pure Python, small cases) ----
 
-def _heading(lon_a, lat_a, lon_b, lat_b):
-    """Heading in whole degrees through Valhalla's 8-bit storage, with math.atan2 (the oracle
-    uses its own deterministic atan): equal except within a hair of a 360/255-degree step."""
-    mlon = np.float32(111320.0 * math.cos(float(lat_a) * 0.017453292519943295))
-    dx = (float(lon_b) - float(lon_a)) * float(mlon)
-    dy = (float(lat_b) - float(lat_a)) * 110567.0
-    deg = math.degrees(math.atan2(dx, dy)) % 360.0 if (dx or dy) else 0.0
-    h8 = int(deg * 255.0 / 360.0 + 0.5)
-    return (h8 * 360 + 127) // 255
+D2R = 0.017453292519943295
+
+
+def _gc32(lon_a, lat_a, lon_b, lat_b):
+    """PointLL::Distance with libm: law of cosines, rounded to float."""
+    if lon_a == lon_b and lat_a == lat_b:
+        return 0.0
+    a, c = float(lat_a) * D2R, float(lat_b) * D2R
+    dl = (float(lon_b) - float(lon_a)) * D2R
+    cb = math.sin(a) * math.sin(c) + math.cos(a) * math.cos(c) * math.cos(dl)
+    cb = min(1.0, max(-1.0, cb))
+    return float(np.float32(math.acos(cb) * 6378160.187))
+
+
+def _bearing(lon_a, lat_a, lon_b, lat_b):
+    """PointLL::Heading with math.atan2 (the oracle uses its own deterministic series)."""
+    if lon_a == lon_b and lat_a == lat_b:
+        return 0.0
+    p1, p2 = float(lat_a) * D2R, float(lat_b) * D2R
+    dl = (float(lon_b) - float(lon_a)) * D2R
+    y = math.sin(dl) * math.cos(p2)
+    x = math.cos(p1) * math.sin(p2) - math.sin(p1) * math.cos(p2) * math.cos(dl)
+    return math.degrees(math.atan2(y, x)) % 360.0
+
+
+def _heading_along(xs, ys):
+    """PointLL::HeadingAlongPolyline(shape, 30 m), then NodeInfo's 8-bit storage and back."""
+    n = len(xs)
+    if n == 2:
+        h = _bearing(xs[0], ys[0], xs[1], ys[1])
+    else:
+        d, h = 0.0, None
+        for i in range(n - 1):
+            if d >= 30.0:
+                break
+            seg = _gc32(xs[i], ys[i], xs[i + 1], ys[i + 1])
+            if d + seg > 30.0:
+                f = (30.0 - d) / seg
+                x = np.float32(float(xs[i]) + (float(xs[i + 1]) - float(xs[i])) * f)
+                y = np.float32(float(ys[i]) + (float(ys[i + 1]) - float(ys[i])) * f)
+                h = _bearing(xs[0], ys[0], x, y)
+                break
+            d += seg
+        if h is None:
+            h = _bearing(xs[0], ys[0], xs[-1], ys[-1])
+    hd = int(math.floor(h + 0.5)) % 360
+    h8 = int(math.floor(np.float32(hd) * (np.float32(255.0) / np.float32(359.0)) + np.float32(0.5)))
+    return int(math.floor(np.float32(h8) * (np.float32(359.0) / np.float32(255.0)) + np.float32(0.5)))
 
 
 def _road_heads(g):
@@ -62,26 +101,22 @@ def _road_heads(g):
     h0 = np.empty(len(off) - 1, np.int64)
     h1 = np.empty(len(off) - 1, np.int64)
     for r in range(len(off) - 1):
-        a, b = int(off[r]), int(off[r + 1]) - 1
-        k = a + 1
-        while k < b and lon[k] == lon[a] and lat[k] == lat[a]:
-            k += 1
-        h0[r] = _heading(lon[a], lat[a], lon[k], lat[k])
-        k = b - 1
-        while k > a and lon[k] == lon[b] and lat[k] == lat[b]:
-            k -= 1
-        h1[r] = _heading(lon[b], lat[b], lon[k], lat[k])
+        a, b = int(off[r]), int(off[r + 1])
+        h0[r] = _heading_along(lon[a:b], lat[a:b])
+        h1[r] = _heading_along(lon[a:b][::-1], lat[a:b][::-1])
     return h0, h1
 
 
 def test_road_headings_match_atan2(built_lib, small_world):
+    """The oracle's road headings (HeadingAlongPolyline at 30 m, 8-bit NodeInfo storage) against
+    the libm restatement above on a generated world."""
     g = graphfile.load(small_world)
     h0, h1 = mo.road_heads(g)
     p0, p1 = _road_heads(g)
     for a, b in ((h0, p0), (h1, p1)):
         d = np.abs(a.astype(np.int64) - b)
         d = np.minimum(d, 360 - d)
-        assert int(d.max()) <= 2, int(d.max())            # one 360/255-degree step at most
+        assert int(d.max()) <= 2, int(d.max())            # one 359/255-degree step at most
         assert (d == 0).mean() > 0.999
     # a grid: roads leave their nodes along the four compass directions (+-20 % jitter)
     q = np.concatenate([h0, h1]).astype(np.int64)
@@ -242,3 +277,37 @@ def test_turn_costs_change_some_choices_only(built_lib, small_world):
     assert (b["route_turn"][valid] > 0).mean() > 0.2
     diff = int((a["choice"] != b["choice"]).sum())
     assert 0 < diff < 0.05 * len(a["choice"]), diff
+
+
+CURVED = """<?xml version='1.0' encoding='UTF-8'?>
+<osm version="0.6" generator="hand">
+ <node id="1" lat="0.0000000" lon="0.0000000"/>
+ <node id="2" lat="0.0000000" lon="0.0000449"/>
+ <node id="3" lat="0.0009040" lon="0.0000449"/>
+ <node id="4" lat="0.0013040" lon="0.0004449"/>
+ <way id="7">
+  <nd ref="1"/><nd ref="2"/><nd ref="3"/><nd ref="4"/>
+  <tag k="highway" v="residential"/>
+ </way>
+</osm>
+"""
+
+
+def test_curved_way_headings_hand_derived(built_lib, tmp_path):
+    """a way that leaves its node 5 m east and then runs north.  Valhalla's NodeInfo
+    heading is taken 30 m along the shape (HeadingAlongPolyline), not toward the first vertex:
+    H0 = atan2(5.0 m east, 25.0 m north) = 11.3 deg -> 11 -> 8 bits round(11 * 255/359) = 8 -> back
+    round(8 * 359/255) = 11 (the first-vertex rule gave 90).  At the other end the first segment
+    is 62.9 m long: the heading toward node 3, atan2(-44.5, -44.2) = 225.2 deg -> 225 -> 160 -> 225."""
+    p = tmp_path / "curved.osm"
+    p.write_text(CURVED)
+    g = graphfile.load(world.import_osm(str(p), str(tmp_path / "curved.rmg"), cell_m=50.0))
+    assert len(g["road_len_cm"]) == 1
+    h0, h1 = mo.road_heads(g)
+    n0 = int(g["road_node0"][0])
+    lonn = g["node_lon"].view(np.float32) if g["node_lon"].dtype != np.float32 else g["node_lon"]
+    first_is_1 = float(lonn[n0]) == 0.0
+    at1, at4 = (h0[0], h1[0]) if first_is_1 else (h1[0], h0[0])
+    assert (int(at1), int(at4)) == (11, 225)
+    p0, p1 = _road_heads(g)
+    assert (int(p0[0]), int(p1[0])) == (int(h0[0]), int(h1[0]))
