@@ -1382,7 +1382,7 @@ void comm_bounded(rm_comm* c, int rank, int nranks, const char* what, F fn) {
     std::thread wd([st, limit, what, rank, nranks] {
       std::unique_lock<std::mutex> lk(st->mu);
       if (!st->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return st->done; })) {
-        std::fprintf(stderr, "%s: rank %d of %d: the other ranks did not complete within %d s (RM_COMM_TIMEOUT_S); "
+        std::fprintf(stderr, "%s: rank %d of %d: the other ranks did not join within %d s (RM_COMM_TIMEOUT_S); "
                              "exiting with status 3\n", what, rank, nranks, (int)limit);
         std::fflush(stderr);
         std::_Exit(3);

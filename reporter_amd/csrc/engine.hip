@@ -2149,6 +2149,9 @@ __device__ __forceinline__ void k2_store_t(SM& sm, const DevBatch& b, uint32_t q
   const K2Src& S = sm.src[o];
   if (U != kNone) {
     b.route[S.obase + q] = k.r;
+#if RM_K2_DIAG == 2   // diagnostic (wrong results): no distance term stored
+    if (gc == -1.0)
+#endif
     b.route_d[S.obase + q] = route_term(k.r, U, sm.tsrc[o].fac, gc);
     if (!k.exact) sm.redo[o] = 1;
   } else {
@@ -2166,8 +2169,12 @@ __device__ __forceinline__ void k2_finish_t2(SM& sm, const DevBatch& b, uint32_t
   const bool la = q < n && sm.src[oa].bound != kNone, lb = qb < n && sm.src[ob].bound != kNone;
   const K2TurnKey ka = k2_key_t(sm, oa, la, sa, pa, rm);
   const K2TurnKey kb = k2_key_t(sm, ob, lb, sb, pb, rm);
+#if RM_K2_DIAG == 1   // diagnostic (wrong results): no turn-row load
+  const k2_v2 wa = {ka.row == 7u ? 1u : 0u, 0u}, wb = {kb.row == 7u ? 1u : 0u, 0u};
+#else
   const k2_v2 wa = *(la && ka.need == 1u ? (k2_trow)(const void*)(uintptr_t)sm.tsrc[oa].trn + ka.row : tdummy);
   const k2_v2 wb = *(lb && kb.need == 1u ? (k2_trow)(const void*)(uintptr_t)sm.tsrc[ob].trn + kb.row : tdummy);
+#endif
   __asm__ volatile("" ::"v"(wa.x), "v"(wa.y), "v"(wb.x), "v"(wb.y));   // both rows in flight, then used
   const uint32_t xa = k2_turn_weight(ka, sm.tsrc[oa].hw, wa.x, wa.y, sm.tw);
   const uint32_t xb = k2_turn_weight(kb, sm.tsrc[ob].hw, wb.x, wb.y, sm.tw);

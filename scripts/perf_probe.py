@@ -13,6 +13,8 @@ ap.add_argument("--ab-locality", action="store_true", help="also time the same b
 ap.add_argument("--ab-modes", default="0,1,0,1", help="locality modes the A/B cycles through")
 ap.add_argument("--ball-radius", type=float, default=None, help="route-ball radius in m (0: the search tiers alone)")
 ap.add_argument("--turn", type=float, default=0.0, help="turn_penalty_factor of every trace (meili's auto default: 200)")
+ap.add_argument("--only", default="", help="time only these stages (comma list, bench.py style: e.g. routes); "
+                "with every stage timed the event pairs shift the stages by up to ~0.1 ms")
 a = ap.parse_args()
 c = dict(world.CONFIGS[a.config])
 if a.traces:
@@ -34,6 +36,25 @@ t = time.time()
 bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts)
 print("first run %.3fs" % (time.time() - t), bm.sizes(), flush=True)
 print("route tiers", bm.route_tiers(), "balls", eng.ball_stats(0), flush=True)
+if a.only:
+    import time as _t
+    for _ in range(3):
+        bm.rerun()
+    engine_sync = getattr(bm, "sync", None)
+    bm.set_timing(False)
+    t = _t.time()
+    for _ in range(a.reps):
+        bm.rerun()
+    wall = (_t.time() - t) / a.reps
+    bm.set_timing_stages(tuple(a.only.split(",")))
+    bm.reset_times()
+    for _ in range(a.reps):
+        bm.rerun()
+    kt = bm.kernel_times()
+    bm.set_timing(False)
+    print("only %.4f ms/step wall (untimed)  " % (wall * 1e3) +
+          " ".join("%s=%.3fms" % (k, kt[k][0] / a.reps) for k in a.only.split(",")), flush=True)
+    sys.exit(0)
 bm.set_timing(True)
 for r in range(a.reps):
     bm.reset_times()
