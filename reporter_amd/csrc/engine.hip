@@ -1729,19 +1729,15 @@ __device__ __forceinline__ uint4 k2_ld(k2_gptr p) {
   const k2_v4 v = *p;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-struct alignas(16) K2Src {
-  // four 16-byte groups, read as such by phase 2 (k2_issue / k2_finish)
-  uint32_t dbase;                // tdesc - rel: transition q of the block reads descriptor pair dbase + q
-  uint32_t obase;                // ob - rel: its route goes to b.route[obase + q]
+// A source item in full (the walked turn weights, k2_turn_walked / k2_route_turn, rebuild it
+// from the LDS records)
+struct K2Src {
   unsigned long long ent;        // the item's mode's table rows (a global address: see k2_gptr)
   uint2 h1, h0;                  // table headers of the exits (bits 0: no table)
   unsigned long long rk1, rk0;   // exit root keys (kKeyInf: that exit is unusable)
   uint32_t road, s;              // source road and offset on it (direct combinations)
   uint32_t bound, tmax;          // pair bounds; bound = kNone: handed to the search tiers
   uint32_t lim;                  // routes with distance <= lim are exact from the tables (ball_exact_limit)
-  uint32_t tdesc;                // the pair's first target descriptor (p * kMaxCand)
-  uint32_t ob;                   // the item's first route in b.route
-  uint32_t rel;                  // the item's first transition among the block's (block scan of K_B)
 };
 // per item of a batch with turn costs (rule 3b): the mode's turn rows, the source road's headings
 // and endpoints, the pair's factor
@@ -1752,17 +1748,36 @@ struct K2Turn {
   uint32_t n0, n1;               // the source road's endpoints (the exits' nodes)
   uint32_t mode, pad;
 };
-#ifndef RM_K2_TURN2
-#define RM_K2_TURN2 2
-#endif
-constexpr uint32_t kK2Defer = 1024;   // walked turn weights listed per block (more: the item is searched)
+constexpr uint32_t kK2Defer = 256;    // walked turn weights listed per block (more: the item is searched)
+// The item record of the kernel without turn costs, 60 bytes (round 6).  LDS sets this kernel's
+// occupancy: at 80 bytes per item (22.8 -> 24.9 KB per block) C2's K2 went 0.866 -> 0.935 ms with
+// the same loop (6 blocks of 4 waves per CU instead of 7); at 60 bytes a block fits 20 KB and a CU
+// holds 8 of them.  The mode's table base comes from a per-mode LDS table (the road word's top
+// bits), the root keys are split into words (4-byte alignment), and the descriptor and route
+// offsets are folded with the item's first transition (dbase, obase).
+struct K2SrcS {
+  uint32_t dbase;                // transition q of the block reads descriptor pair dbase + q
+  uint32_t obase;                // ... and writes b.route[obase + q]
+  uint32_t h1x, h1y, h0x, h0y;   // table headers of the exits (uint2 would align to 8)
+  uint32_t rk1l, rk1h, rk0l, rk0h;   // exit root keys, split
+  uint32_t roadm;                // source road | mode << 29
+  uint32_t s, bound, tmax, lim;
+};
+static_assert(sizeof(K2SrcS) == 60, "K2SrcS is 60 bytes");
+// with turn costs, per item besides its K2SrcS: the source road's heading word, the pair's factor
+// (float bits; 0: no turn costs) and the pair (its gc)
+struct K2TurnS {
+  uint32_t hw, fac, p;
+};
 template <bool TURN>
 struct K2Smem {
-  K2Src src[kK2Items];
+  K2SrcS src[kK2Items];
+  unsigned long long ent_mode[8];      // each mode's table rows (a mode without tables: a dummy array)
+  unsigned long long trn_mode[TURN ? 8 : 1];   // ... and turn rows
   uint8_t owner[kK2Items * kMaxCand];   // transition of the block -> item of the block
   uint32_t wsum[kK2Items / 64];
   uint8_t redo[kK2Items];               // a route of the item was not exact from the tables
-  K2Turn tsrc[TURN ? kK2Items : 1];
+  K2TurnS tsrc[TURN ? kK2Items : 1];
   uint32_t tw[TURN ? kTurnDegrees : 1];  // the turn weights (DevGraph::turn_w) in LDS
   uint32_t ndef;                         // transitions whose turn weight is walked after the loop
   uint16_t def[TURN ? kK2Defer : 1];
@@ -1790,14 +1805,19 @@ __device__ __forceinline__ uint32_t ball_exact_limit(uint32_t bound, uint32_t ra
 // route of item S to the target described by (t0, t1), from the target road's rows (r1, r0)
 // in the tables of S's two exits (kRouteInvalid when there is none within the bounds); `exact`
 // false when the tables cannot decide it (ball_exact_limit)
+__device__ __forceinline__ uint32_t k2_route_v(unsigned long long rk1, unsigned long long rk0, uint32_t road, uint32_t s,
+                                               uint32_t lim, uint32_t bound, uint32_t tmax, const uint4& t0,
+                                               const uint4& t1, const uint4& r1, const uint4& r0, bool& exact) {
+  const unsigned long long lab0 = ball_label(rk1, row_key0(r1), rk0, row_key0(r0));
+  const unsigned long long lab1 = ball_label(rk1, row_key1(r1), rk0, row_key1(r0));
+  const uint4 a0 = make_uint4(road, s, 0u, 0u);   // route_key_vals reads the source's road and offset
+  const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, nullptr);
+  exact = lim == kNone || (key != kKeyInf && key_dist(key) <= lim);
+  return (key != kKeyInf && key_dist(key) <= bound && key_time(key) <= tmax) ? key_dist(key) : kRouteInvalid;
+}
 __device__ __forceinline__ uint32_t k2_route(const K2Src& S, const uint4& t0, const uint4& t1, const uint4& r1,
                                              const uint4& r0, bool& exact) {
-  const unsigned long long lab0 = ball_label(S.rk1, row_key0(r1), S.rk0, row_key0(r0));
-  const unsigned long long lab1 = ball_label(S.rk1, row_key1(r1), S.rk0, row_key1(r0));
-  const uint4 a0 = make_uint4(S.road, S.s, 0u, 0u);   // route_key_vals reads the source's road and offset
-  const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, nullptr);
-  exact = S.lim == kNone || (key != kKeyInf && key_dist(key) <= S.lim);
-  return (key != kKeyInf && key_dist(key) <= S.bound && key_time(key) <= S.tmax) ? key_dist(key) : kRouteInvalid;
+  return k2_route_v(S.rk1, S.rk0, S.road, S.s, S.lim, S.bound, S.tmax, t0, t1, r1, r0, exact);
 }
 
 // labels from the route balls of the two exits (see k_routes_ball2)
@@ -1940,63 +1960,20 @@ __device__ __forceinline__ uint32_t k2_route_turn(const DevGraph& g, const K2Src
   return r;
 }
 
-// ---- k_routes_ball2 phase 2 without turn costs, software-pipelined (round 6).
-// The round-3..5 loop was two transitions per lane and step with every load of a step issued before
-// any was used -- in the source.  Its ISA was not: the probe addresses went behind exec-mask
-// branches (a select of a pointer became a branch around its LDS reads, and ball_slot's table-size
-// test another), the second transition's probes waited for the first's, and the descriptor loads'
-// registers were reused while loads were pending (the ballast `t1.x/.y` were dead, so the next
-// load's destination overlapped them and the compiler waited for the first).  Now:
-//  * a step's loads are formed branch-free: every exit's header is valid (an unusable exit, or a
-//    handed-over item, reads row 0..1 of a valid array), ball_slot_bf forms both hashes and selects;
-//  * a descriptor is 24 bytes (the entry times only of its second half);
-//  * steps are pipelined two deep with two register sets (X, Y: no copies at the back edge): a
-//    step issues its probes, then the NEXT step's descriptor loads, then waits for its probes
-//    (vmcnt counts the later descriptor loads out) and finishes its two transitions.
-#ifndef RM_K2_PIPE
-#define RM_K2_PIPE 1
-#endif
+// ---- k_routes_ball2 phase 2 (round 6, VERDICT r05 item 2: "take control of the waits").  A
+// software-pipelined loop was built and measured: the probe addresses formed branch-free (every
+// exit's header valid, ball_slot_bf), 24-byte descriptor reads, two register sets so a step issued
+// its probes, then the next step's descriptors, then waited for its own probes only (the ISA
+// checked: vmcnt(7)/(6) waits, no waits between the issue groups).  C2's K2 did not move (0.951 vs
+// 0.931 ms for the unpipelined loop on the same build, bench-style timing): the kernel is not bound
+// by where its waits sit but by occupancy and VALU (valu_frac 0.65).  What moved it was LDS: the
+// item records at 80 bytes gave 6 blocks per CU, at 72 bytes 7 (0.935 -> 0.866 ms), at 60 (K2SrcS)
+// 8.  The turn-cost kernel keeps the pipelined loop (k2_phase2_pipe_t).
 typedef unsigned int k2_u2 __attribute__((ext_vector_type(2)));
 typedef const k2_u2 __attribute__((address_space(1)))* k2_gptr2;
 __device__ __forceinline__ uint2 k2_ld2(k2_gptr2 p) {
   const k2_u2 v = *p;
   return make_uint2(v.x, v.y);
-}
-// ball_slot without the branch on the table size (bits >= 1)
-__device__ __forceinline__ uint32_t ball_slot_bf(uint32_t v, uint32_t bits) {
-#ifdef RM_BALL_SLOT_RANDOM
-  return ball_slot(v, bits);
-#else
-  const uint32_t a = (v * 2654435761u) >> (32u - bits);
-  const uint32_t sh = min(32u + kBallGroupLog - bits, 31u);
-  const uint32_t gr = ((((v >> kBallGroupLog) * 2654435761u) >> sh) << kBallGroupLog) | (v & ((1u << kBallGroupLog) - 1u));
-  return bits < kBallGroupBits ? a : gr;
-#endif
-}
-struct K2Step {   // a transition in flight: its target descriptor {road, s, L, spf | spr}, entry times
-  uint4 t0;
-  uint2 t1;
-};
-struct K2Probe {  // ... and both exits' first probes of the target road
-  uint4 e1, e0;
-};
-// the descriptor of block transition q (clamped: a lane past the block's range loads a valid
-// descriptor it never uses)
-template <class SM>
-__device__ __forceinline__ void k2_issue(const SM& sm, const DevBatch& b, uint32_t q, uint32_t n, K2Step& st) {
-  const uint32_t qc = min(q, n - 1u);
-  const uint32_t di = sm.src[sm.owner[qc]].dbase + qc;
-  const uint4* dp = b.cand_desc + 2 * (uint64_t)di;
-  st.t0 = k2_ld((k2_gptr)(const void*)dp);
-  st.t1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(dp + 1) + 1));
-}
-template <class SM>
-__device__ __forceinline__ void k2_probe(const SM& sm, uint32_t q, uint32_t n, uint32_t road, K2Probe& pr) {
-  const K2Src& S = sm.src[sm.owner[min(q, n - 1u)]];
-  const uint4 h = *reinterpret_cast<const uint4*>(&S.h1);   // h1, h0
-  const k2_gptr e = (k2_gptr)(const void*)(uintptr_t)S.ent;
-  pr.e1 = k2_ld(e + (ball_row0(h.x) + ball_slot_bf(road, max(h.y, 1u))));
-  pr.e0 = k2_ld(e + (ball_row0(h.z) + ball_slot_bf(road, max(h.w, 1u))));
 }
 // a row or the empty row, selected per word (a select of the aggregate went through scratch)
 __device__ __forceinline__ uint4 k2_row_or_none(bool use, const uint4& e) {
@@ -2013,49 +1990,62 @@ __device__ __forceinline__ uint4 ball_resolve_g(k2_gptr ent, const uint2& h, uin
     if ((e.x & rmask) == road || e.x == kNone) return e;
   }
 }
-template <class SM>
-__device__ __forceinline__ void k2_finish(SM& sm, const DevBatch& b, uint32_t q, uint32_t n, const K2Step& st,
-                                          const K2Probe& pr, uint32_t rm) {
-  // branch-free up to the store (a conditional return let the compiler sink this step's probe
-  // loads behind it, after the next step's descriptor loads)
-  const uint32_t o = sm.owner[min(q, n - 1u)];
-  const K2Src& S = sm.src[o];
-  const bool live = q < n && S.bound != kNone;
-  const bool u = live && st.t0.w != 0u;   // some direction of the target road is usable
-  const k2_gptr ge = (k2_gptr)(const void*)(uintptr_t)S.ent;
-  const uint4 r1 = ball_resolve_g(ge, S.h1, st.t0.x, k2_row_or_none(u && S.rk1 != kKeyInf, pr.e1), rm);
-  const uint4 r0 = ball_resolve_g(ge, S.h0, st.t0.x, k2_row_or_none(u && S.rk0 != kKeyInf, pr.e0), rm);
-  bool x = true;
-  const uint32_t r = k2_route(S, st.t0, make_uint4(0u, 0u, st.t1.x, st.t1.y), r1, r0, x);
-  if (live) {
-    b.route[S.obase + q] = r;
-    if (!x) sm.redo[o] = 1;
+// phase 2 without turn costs: two transitions per lane and step, every load of a step issued before
+// any is used (the descriptors unconditionally -- a handed-over item's descriptor is as valid an
+// address --, the four first probes branch-free with an unused probe reading a valid dummy row)
+__device__ __forceinline__ uint4 ball_resolve_at_g(k2_gptr ent, const uint2& h, uint32_t road, uint4 e, uint32_t rmask,
+                                                   uint32_t& s) {
+  if ((e.x & rmask) == road || e.x == kNone) return e;
+  const uint32_t mask = (1u << h.y) - 1u;
+  for (;;) {
+    s = (s + 1u) & mask;
+    e = k2_ld(ent + (ball_row0(h.x) + s));
+    if ((e.x & rmask) == road || e.x == kNone) return e;
   }
 }
 template <class SM>
-__device__ __forceinline__ void k2_phase2_pipe(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm) {
-  uint32_t q = threadIdx.x;
-  K2Step xa, xb, ya, yb;
-  K2Probe pa, pb;
-  k2_issue(sm, b, q, n, xa);
-  k2_issue(sm, b, q + kK2Items, n, xb);
-  while (q < n) {
-    k2_probe(sm, q, n, xa.t0.x, pa);
-    k2_probe(sm, q + kK2Items, n, xb.t0.x, pb);
-    k2_issue(sm, b, q + 2 * kK2Items, n, ya);
-    k2_issue(sm, b, q + 3 * kK2Items, n, yb);
-    k2_finish(sm, b, q, n, xa, pa, rm);
-    k2_finish(sm, b, q + kK2Items, n, xb, pb, rm);
-    q += 2 * kK2Items;
-    if (q >= n) break;
-    k2_probe(sm, q, n, ya.t0.x, pa);
-    k2_probe(sm, q + kK2Items, n, yb.t0.x, pb);
-    k2_issue(sm, b, q + 2 * kK2Items, n, xa);
-    k2_issue(sm, b, q + 3 * kK2Items, n, xb);
-    k2_finish(sm, b, q, n, ya, pa, rm);
-    k2_finish(sm, b, q + kK2Items, n, yb, pb, rm);
-    q += 2 * kK2Items;
+__device__ __forceinline__ void k2_phase2_slim(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_gptr dummy) {
+  const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+  for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
+    const uint32_t qb = q + kK2Items;
+    const bool hb = qb < n;
+    const uint32_t qB = hb ? qb : q;
+    const K2SrcS& A = sm.src[sm.owner[q]];
+    const K2SrcS& B = sm.src[sm.owner[qB]];
+    const bool la = A.bound != kNone, lb = hb && B.bound != kNone;
+    const uint4* pda = b.cand_desc + 2 * (uint64_t)(A.dbase + q);
+    const uint4* pdb = b.cand_desc + 2 * (uint64_t)(B.dbase + qB);
+    const uint4 ta0 = k2_ld((k2_gptr)(const void*)pda), tb0 = k2_ld((k2_gptr)(const void*)pdb);
+    // of the second half only the entry times
+    const uint2 ta1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pda + 1) + 1));
+    const uint2 tb1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pdb + 1) + 1));
+    const unsigned long long ak1 = (unsigned long long)A.rk1h << 32 | A.rk1l, ak0 = (unsigned long long)A.rk0h << 32 | A.rk0l;
+    const unsigned long long bk1 = (unsigned long long)B.rk1h << 32 | B.rk1l, bk0 = (unsigned long long)B.rk0h << 32 | B.rk0l;
+    const bool ua = la && ta0.w != 0u, ub = lb && tb0.w != 0u;   // some direction of the target road is usable
+    const bool ua1 = ua && ak1 != kKeyInf, ua0 = ua && ak0 != kKeyInf;
+    const bool ub1 = ub && bk1 != kKeyInf, ub0 = ub && bk0 != kKeyInf;
+    const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[A.roadm >> 29];
+    const k2_gptr eb = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[B.roadm >> 29];
+    const k2_gptr pa1 = ua1 ? ea + (ball_row0(A.h1x) + ball_slot(ta0.x, A.h1y)) : dummy;
+    const k2_gptr pa0 = ua0 ? ea + (ball_row0(A.h0x) + ball_slot(ta0.x, A.h0y)) : dummy;
+    const k2_gptr pb1 = ub1 ? eb + (ball_row0(B.h1x) + ball_slot(tb0.x, B.h1y)) : dummy;
+    const k2_gptr pb0 = ub0 ? eb + (ball_row0(B.h0x) + ball_slot(tb0.x, B.h0y)) : dummy;
+    const uint4 la1 = k2_ld(pa1), la0 = k2_ld(pa0), lb1 = k2_ld(pb1), lb0 = k2_ld(pb0);
+    bool xa = true, xb = true;
+    if (la)
+      b.route[A.obase + q] = k2_route_v(ak1, ak0, A.roadm & 0x1fffffffu, A.s, A.lim, A.bound, A.tmax, ta0,
+                                        make_uint4(0u, 0u, ta1.x, ta1.y),
+                                        ball_resolve_g(ea, make_uint2(A.h1x, A.h1y), ta0.x, k2_row_or_none(ua1, la1), rm),
+                                        ball_resolve_g(ea, make_uint2(A.h0x, A.h0y), ta0.x, k2_row_or_none(ua0, la0), rm), xa);
+    if (lb)
+      b.route[B.obase + qb] = k2_route_v(bk1, bk0, B.roadm & 0x1fffffffu, B.s, B.lim, B.bound, B.tmax, tb0,
+                                         make_uint4(0u, 0u, tb1.x, tb1.y),
+                                         ball_resolve_g(eb, make_uint2(B.h1x, B.h1y), tb0.x, k2_row_or_none(ub1, lb1), rm),
+                                         ball_resolve_g(eb, make_uint2(B.h0x, B.h0y), tb0.x, k2_row_or_none(ub0, lb0), rm), xb);
+    if (!xa) sm.redo[sm.owner[q]] = 1;
+    if (!xb) sm.redo[sm.owner[qB]] = 1;
   }
+  (void)none;
 }
 
 // k_routes_ball2<true>'s two-per-step loop (round 6): the route of a transition from the tables,
@@ -2071,13 +2061,14 @@ struct K2TurnKey {
   uint32_t e1;       // the winning exit is the forward one (node1)
   bool exact;
 };
-__device__ __forceinline__ K2TurnKey k2_turn_key(const K2Src& S, uint32_t fac, const uint4& t0, const uint4& t1,
-                                                 const uint4& r1, const uint4& r0, uint32_t s1, uint32_t s0) {
+__device__ __forceinline__ K2TurnKey k2_turn_key(const K2SrcS& S, unsigned long long rk1, unsigned long long rk0,
+                                                 uint32_t fac, const uint4& t0, const uint4& t1, const uint4& r1,
+                                                 const uint4& r0, uint32_t s1, uint32_t s0) {
   const unsigned long long k10 = row_key0(r1), k00 = row_key0(r0), k11 = row_key1(r1), k01 = row_key1(r0);
-  const unsigned long long l10 = k10 != kKeyInf ? S.rk1 + k10 : kKeyInf, l00 = k00 != kKeyInf ? S.rk0 + k00 : kKeyInf;
-  const unsigned long long l11 = k11 != kKeyInf ? S.rk1 + k11 : kKeyInf, l01 = k01 != kKeyInf ? S.rk0 + k01 : kKeyInf;
+  const unsigned long long l10 = k10 != kKeyInf ? rk1 + k10 : kKeyInf, l00 = k00 != kKeyInf ? rk0 + k00 : kKeyInf;
+  const unsigned long long l11 = k11 != kKeyInf ? rk1 + k11 : kKeyInf, l01 = k01 != kKeyInf ? rk0 + k01 : kKeyInf;
   const unsigned long long lab0 = l00 < l10 ? l00 : l10, lab1 = l01 < l11 ? l01 : l11;
-  const uint4 a0 = make_uint4(S.road, S.s, 0u, 0u);
+  const uint4 a0 = make_uint4(S.roadm & 0x1fffffffu, S.s, 0u, 0u);
   int combo = -1;
   const unsigned long long key = route_key_vals(a0, t0, t1, lab0, lab1, &combo);
   K2TurnKey k;
@@ -2088,7 +2079,7 @@ __device__ __forceinline__ K2TurnKey k2_turn_key(const K2Src& S, uint32_t fac, c
   k.side = combo == 3 ? 1u : 0u;
   const unsigned long long la = k.side ? l11 : l10, lb = k.side ? l01 : l00;
   k.e1 = la < lb ? 1u : 0u;
-  k.row = k.e1 ? ball_row0(S.h1.x) + s1 : ball_row0(S.h0.x) + s0;
+  k.row = k.e1 ? ball_row0(S.h1x) + s1 : ball_row0(S.h0x) + s0;
   if (fac && valid && combo >= 2 && k.exact) k.need = la != lb ? 1u : 2u;
   return k;
 }
@@ -2102,57 +2093,20 @@ __device__ __forceinline__ uint32_t k2_turn_weight(const K2TurnKey& k, uint32_t 
   return tw[turn_degree(head_back(hw, k.e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
 }
 
-// k_routes_ball2<true> phase 2 pipelined as k2_phase2_pipe (RM_K2_TURN2 2): a step issues its
-// probes and the next step's descriptors, then forms both transitions' keys, then reads both
-// winners' turn rows together (the one dependent load more than without turn costs).
+// phase 2 with turn costs (round 6): two transitions per lane and step, as without them.  Only the
+// winning exit's turn row is read, after the probes, and only for a valid route that enters its
+// target road from a node (46 % of C2's transitions; round 5 read both exits' rows of every
+// transition with the probes: +1.7 GB of lines per step).  A route whose weight needs the walk (a
+// tie between the exits, a row without its sum: 1.3 % of C2's) is listed and walked after the
+// loop (k2_turn_walked), so the walk's registers stay out of this loop.
 typedef unsigned int k2_v2 __attribute__((ext_vector_type(2)));
 typedef const k2_v2 __attribute__((address_space(1)))* k2_trow;
-struct K2StepT {
-  uint4 t0;
-  uint2 t1;
-  double gc;
-};
 template <class SM>
-__device__ __forceinline__ void k2_issue_t(const SM& sm, const DevBatch& b, uint32_t q, uint32_t n, K2StepT& st) {
-  const uint32_t qc = min(q, n - 1u);
-  const K2Src& S = sm.src[sm.owner[qc]];
-  const uint4* dp = b.cand_desc + 2 * (uint64_t)(S.dbase + qc);
-  st.t0 = k2_ld((k2_gptr)(const void*)dp);
-  st.t1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(dp + 1) + 1));
-  st.gc = b.gc[S.tdesc / kMaxCand];
-}
-__device__ __forceinline__ uint4 ball_resolve_at_g(k2_gptr ent, const uint2& h, uint32_t road, uint4 e, uint32_t rmask,
-                                                   uint32_t& s) {
-  if ((e.x & rmask) == road || e.x == kNone) return e;
-  const uint32_t mask = (1u << h.y) - 1u;
-  for (;;) {
-    s = (s + 1u) & mask;
-    e = k2_ld(ent + (ball_row0(h.x) + s));
-    if ((e.x & rmask) == road || e.x == kNone) return e;
-  }
-}
-template <class SM>
-__device__ __forceinline__ K2TurnKey k2_key_t(const SM& sm, uint32_t o, bool live, const K2StepT& st, const K2Probe& pr,
-                                              uint32_t rm) {
-  const K2Src& S = sm.src[o];
-  const bool u = live && st.t0.w != 0u;
-  const k2_gptr ge = (k2_gptr)(const void*)(uintptr_t)S.ent;
-  uint32_t s1 = ball_slot_bf(st.t0.x, max(S.h1.y, 1u)), s0 = ball_slot_bf(st.t0.x, max(S.h0.y, 1u));
-  const uint4 r1 = ball_resolve_at_g(ge, S.h1, st.t0.x, k2_row_or_none(u && S.rk1 != kKeyInf, pr.e1), rm, s1);
-  const uint4 r0 = ball_resolve_at_g(ge, S.h0, st.t0.x, k2_row_or_none(u && S.rk0 != kKeyInf, pr.e0), rm, s0);
-  return k2_turn_key(S, sm.tsrc[o].fac, st.t0, make_uint4(0u, 0u, st.t1.x, st.t1.y), r1, r0, s1, s0);
-}
-template <class SM>
-__device__ __forceinline__ void k2_store_t(SM& sm, const DevBatch& b, uint32_t q, uint32_t o, bool live,
-                                           const K2TurnKey& k, uint32_t U, double gc) {
-  if (!live) return;
-  const K2Src& S = sm.src[o];
+__device__ __forceinline__ void k2_turn_store(SM& sm, const DevBatch& b, uint32_t q, uint32_t o, const K2SrcS& S,
+                                              const K2TurnKey& k, uint32_t U, uint32_t fac, double gc) {
   if (U != kNone) {
     b.route[S.obase + q] = k.r;
-#if RM_K2_DIAG == 2   // diagnostic (wrong results): no distance term stored
-    if (gc == -1.0)
-#endif
-    b.route_d[S.obase + q] = route_term(k.r, U, sm.tsrc[o].fac, gc);
+    b.route_d[S.obase + q] = route_term(k.r, U, fac, gc);
     if (!k.exact) sm.redo[o] = 1;
   } else {
     const uint32_t i = atomicAdd(&sm.ndef, 1u);
@@ -2161,52 +2115,151 @@ __device__ __forceinline__ void k2_store_t(SM& sm, const DevBatch& b, uint32_t q
   }
 }
 template <class SM>
-__device__ __forceinline__ void k2_finish_t2(SM& sm, const DevBatch& b, uint32_t q, uint32_t n, const K2StepT& sa,
-                                             const K2Probe& pa, const K2StepT& sb, const K2Probe& pb, uint32_t rm,
-                                             k2_trow tdummy) {
-  const uint32_t qb = q + kK2Items;
-  const uint32_t oa = sm.owner[min(q, n - 1u)], ob = sm.owner[min(qb, n - 1u)];
-  const bool la = q < n && sm.src[oa].bound != kNone, lb = qb < n && sm.src[ob].bound != kNone;
-  const K2TurnKey ka = k2_key_t(sm, oa, la, sa, pa, rm);
-  const K2TurnKey kb = k2_key_t(sm, ob, lb, sb, pb, rm);
-#if RM_K2_DIAG == 1   // diagnostic (wrong results): no turn-row load
-  const k2_v2 wa = {ka.row == 7u ? 1u : 0u, 0u}, wb = {kb.row == 7u ? 1u : 0u, 0u};
-#else
-  const k2_v2 wa = *(la && ka.need == 1u ? (k2_trow)(const void*)(uintptr_t)sm.tsrc[oa].trn + ka.row : tdummy);
-  const k2_v2 wb = *(lb && kb.need == 1u ? (k2_trow)(const void*)(uintptr_t)sm.tsrc[ob].trn + kb.row : tdummy);
-#endif
-  __asm__ volatile("" ::"v"(wa.x), "v"(wa.y), "v"(wb.x), "v"(wb.y));   // both rows in flight, then used
-  const uint32_t xa = k2_turn_weight(ka, sm.tsrc[oa].hw, wa.x, wa.y, sm.tw);
-  const uint32_t xb = k2_turn_weight(kb, sm.tsrc[ob].hw, wb.x, wb.y, sm.tw);
-  k2_store_t(sm, b, q, oa, la, ka, xa, sa.gc);
-  k2_store_t(sm, b, qb, ob, lb, kb, xb, sb.gc);
-}
-template <class SM>
-__device__ __forceinline__ void k2_phase2_pipe_t(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_trow tdummy) {
-  uint32_t q = threadIdx.x;
-  K2StepT xa, xb, ya, yb;
-  K2Probe pa, pb;
-  k2_issue_t(sm, b, q, n, xa);
-  k2_issue_t(sm, b, q + kK2Items, n, xb);
-  while (q < n) {
-    k2_probe(sm, q, n, xa.t0.x, pa);
-    k2_probe(sm, q + kK2Items, n, xb.t0.x, pb);
-    k2_issue_t(sm, b, q + 2 * kK2Items, n, ya);
-    k2_issue_t(sm, b, q + 3 * kK2Items, n, yb);
-    k2_finish_t2(sm, b, q, n, xa, pa, xb, pb, rm, tdummy);
-    q += 2 * kK2Items;
-    if (q >= n) break;
-    k2_probe(sm, q, n, ya.t0.x, pa);
-    k2_probe(sm, q + kK2Items, n, yb.t0.x, pb);
-    k2_issue_t(sm, b, q + 2 * kK2Items, n, xa);
-    k2_issue_t(sm, b, q + 3 * kK2Items, n, xb);
-    k2_finish_t2(sm, b, q, n, ya, pa, yb, pb, rm, tdummy);
-    q += 2 * kK2Items;
+__device__ __forceinline__ void k2_phase2_turn(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_gptr dummy) {
+  const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
+  for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
+    const uint32_t qb = q + kK2Items;
+    const bool hb = qb < n;
+    const uint32_t qB = hb ? qb : q;
+    const uint32_t oa = sm.owner[q], obb = sm.owner[qB];
+    const K2SrcS& A = sm.src[oa];
+    const K2SrcS& B = sm.src[obb];
+    const bool la = A.bound != kNone, lb = hb && B.bound != kNone;
+    const uint4* pda = b.cand_desc + 2 * (uint64_t)(A.dbase + q);
+    const uint4* pdb = b.cand_desc + 2 * (uint64_t)(B.dbase + qB);
+    const uint4 ta0 = k2_ld((k2_gptr)(const void*)pda), tb0 = k2_ld((k2_gptr)(const void*)pdb);
+    const uint2 ta1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pda + 1) + 1));
+    const uint2 tb1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pdb + 1) + 1));
+    const K2TurnS TA = sm.tsrc[oa], TB = sm.tsrc[obb];
+    const double gca = b.gc[TA.p], gcb = b.gc[TB.p];
+    const unsigned long long ak1 = (unsigned long long)A.rk1h << 32 | A.rk1l, ak0 = (unsigned long long)A.rk0h << 32 | A.rk0l;
+    const unsigned long long bk1 = (unsigned long long)B.rk1h << 32 | B.rk1l, bk0 = (unsigned long long)B.rk0h << 32 | B.rk0l;
+    const bool ua = la && ta0.w != 0u, ub = lb && tb0.w != 0u;
+    const bool ua1 = ua && ak1 != kKeyInf, ua0 = ua && ak0 != kKeyInf;
+    const bool ub1 = ub && bk1 != kKeyInf, ub0 = ub && bk0 != kKeyInf;
+    const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[A.roadm >> 29];
+    const k2_gptr eb = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[B.roadm >> 29];
+    uint32_t sa1 = ball_slot(ta0.x, A.h1y), sa0 = ball_slot(ta0.x, A.h0y);
+    uint32_t sb1 = ball_slot(tb0.x, B.h1y), sb0 = ball_slot(tb0.x, B.h0y);
+    const uint4 la1 = k2_ld(ua1 ? ea + (ball_row0(A.h1x) + sa1) : dummy), la0 = k2_ld(ua0 ? ea + (ball_row0(A.h0x) + sa0) : dummy);
+    const uint4 lb1 = k2_ld(ub1 ? eb + (ball_row0(B.h1x) + sb1) : dummy), lb0 = k2_ld(ub0 ? eb + (ball_row0(B.h0x) + sb0) : dummy);
+    const uint4 ra1 = ball_resolve_at_g(ea, make_uint2(A.h1x, A.h1y), ta0.x, k2_row_or_none(ua1, la1), rm, sa1);
+    const uint4 ra0 = ball_resolve_at_g(ea, make_uint2(A.h0x, A.h0y), ta0.x, k2_row_or_none(ua0, la0), rm, sa0);
+    const uint4 rb1 = ball_resolve_at_g(eb, make_uint2(B.h1x, B.h1y), tb0.x, k2_row_or_none(ub1, lb1), rm, sb1);
+    const uint4 rb0 = ball_resolve_at_g(eb, make_uint2(B.h0x, B.h0y), tb0.x, k2_row_or_none(ub0, lb0), rm, sb0);
+    const K2TurnKey ka = k2_turn_key(A, ak1, ak0, TA.fac, ta0, make_uint4(0u, 0u, ta1.x, ta1.y), ra1, ra0, sa1, sa0);
+    const K2TurnKey kb = k2_turn_key(B, bk1, bk0, TB.fac, tb0, make_uint4(0u, 0u, tb1.x, tb1.y), rb1, rb0, sb1, sb0);
+    // the winners' turn rows (a transition without one reads a valid dummy row)
+    const k2_trow tra = (k2_trow)(const void*)(uintptr_t)sm.trn_mode[A.roadm >> 29];
+    const k2_trow trb = (k2_trow)(const void*)(uintptr_t)sm.trn_mode[B.roadm >> 29];
+    const k2_v2 wa = *(la && ka.need == 1u ? tra + ka.row : tdummy);
+    const k2_v2 wb = *(lb && kb.need == 1u ? trb + kb.row : tdummy);
+    const uint32_t xa = k2_turn_weight(ka, TA.hw, wa.x, wa.y, sm.tw), xb = k2_turn_weight(kb, TB.hw, wb.x, wb.y, sm.tw);
+    // xa / xb: the turn weight U, or kNone: walked after the loop
+    if (la) k2_turn_store(sm, b, q, oa, A, ka, xa, TA.fac, gca);
+    if (lb) k2_turn_store(sm, b, qb, obb, B, kb, xb, TB.fac, gcb);
   }
 }
+// The same with one transition per lane and step and both exits' turn rows read with the probes
+// at their first-probe slots (round 5's issue group: no dependent third load; a row resolved past
+// a collision -- rare -- reloads its turn row).  RM_K2_TURN_STEP selects this loop (1) or the
+// two-per-step one above (2).
+#ifndef RM_K2_TURN_STEP
+#define RM_K2_TURN_STEP 1
+#endif
+template <class SM>
+__device__ __forceinline__ void k2_phase2_turn1(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_gptr dummy) {
+  const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
+  for (uint32_t q = threadIdx.x; q < n; q += kK2Items) {
+    const uint32_t o = sm.owner[q];
+    const K2SrcS& A = sm.src[o];
+    const bool la = A.bound != kNone;
+    const uint4* pda = b.cand_desc + 2 * (uint64_t)(A.dbase + q);
+    const uint4 ta0 = k2_ld((k2_gptr)(const void*)pda);
+    const uint2 ta1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pda + 1) + 1));
+    const K2TurnS TA = sm.tsrc[o];
+    const double gca = b.gc[TA.p];
+    const unsigned long long ak1 = (unsigned long long)A.rk1h << 32 | A.rk1l, ak0 = (unsigned long long)A.rk0h << 32 | A.rk0l;
+    const bool ua = la && ta0.w != 0u;
+    const bool ua1 = ua && ak1 != kKeyInf, ua0 = ua && ak0 != kKeyInf;
+    const uint32_t mode = A.roadm >> 29;
+    const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[mode];
+    const k2_trow tra = (k2_trow)(const void*)(uintptr_t)sm.trn_mode[mode];
+    const bool tt = TA.fac != 0u;
+    const uint32_t h1s = ball_slot(ta0.x, A.h1y), h0s = ball_slot(ta0.x, A.h0y);
+    const uint64_t i1 = ball_row0(A.h1x) + h1s, i0 = ball_row0(A.h0x) + h0s;
+    const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
+    const k2_v2 v1 = *(ua1 && tt ? tra + i1 : tdummy), v0 = *(ua0 && tt ? tra + i0 : tdummy);
+    uint32_t s1 = h1s, s0 = h0s;
+    const uint4 r1 = ball_resolve_at_g(ea, make_uint2(A.h1x, A.h1y), ta0.x, k2_row_or_none(ua1, la1), rm, s1);
+    const uint4 r0 = ball_resolve_at_g(ea, make_uint2(A.h0x, A.h0y), ta0.x, k2_row_or_none(ua0, la0), rm, s0);
+    const K2TurnKey k = k2_turn_key(A, ak1, ak0, TA.fac, ta0, make_uint4(0u, 0u, ta1.x, ta1.y), r1, r0, s1, s0);
+    k2_v2 w = k.e1 ? v1 : v0;
+    if (k.need == 1u && (k.e1 ? s1 != h1s : s0 != h0s)) w = tra[k.row];   // resolved past a collision
+    const uint32_t x = k2_turn_weight(k, TA.hw, w.x, w.y, sm.tw);
+    if (la) k2_turn_store(sm, b, q, o, A, k, x, TA.fac, gca);
+  }
+}
+// a listed transition (its turn weight needs the walk): the route again, one lane, with both exits'
+// turn rows at their first-probe slots and the walk through the tables (k2_route_turn)
+template <class SM>
+__device__ void k2_turn_walked(const DevGraph& g, SM& sm, const DevBatch& b, uint32_t q, uint32_t rm) {
+  const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
+  const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
+  const uint32_t o = sm.owner[q];
+  const K2SrcS& Z = sm.src[o];
+  const K2TurnS TZ = sm.tsrc[o];
+  const uint32_t mode = Z.roadm >> 29;
+  K2Src A;
+  A.ent = sm.ent_mode[mode];
+  A.h1 = make_uint2(Z.h1x, Z.h1y);
+  A.h0 = make_uint2(Z.h0x, Z.h0y);
+  A.rk1 = (unsigned long long)Z.rk1h << 32 | Z.rk1l;
+  A.rk0 = (unsigned long long)Z.rk0h << 32 | Z.rk0l;
+  A.road = Z.roadm & 0x1fffffffu;
+  A.s = Z.s;
+  A.bound = Z.bound;
+  A.tmax = Z.tmax;
+  A.lim = Z.lim;
+  K2Turn T;
+  T.trn = sm.trn_mode[mode];
+  T.hw = TZ.hw;
+  T.fac = TZ.fac;
+  T.n0 = g.road_node0[A.road];
+  T.n1 = g.road_node1[A.road];
+  T.mode = mode;
+  T.pad = 0u;
+  const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(Z.dbase + q));
+  const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1);
+  const double gc = b.gc[TZ.p];
+  const bool ua = ta0.w != 0u;
+  const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
+  const uint32_t h1s = ball_slot(ta0.x, A.h1.y), h0s = ball_slot(ta0.x, A.h0.y);
+  const uint64_t i1 = ball_row0(A.h1.x) + h1s, i0 = ball_row0(A.h0.x) + h0s;
+  const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)A.ent;
+  const bool tt = T.fac != 0u;
+  const k2_trow tra = (k2_trow)(const void*)(uintptr_t)T.trn;
+  const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
+  const k2_v2 v1 = *(ua1 && tt ? tra + i1 : tdummy), v0 = *(ua0 && tt ? tra + i0 : tdummy);
+  uint32_t s1 = h1s, s0 = h0s;
+  const uint4 r1 = ball_resolve_at_g(ea, A.h1, ta0.x, k2_row_or_none(ua1, la1), rm, s1);
+  const uint4 r0 = ball_resolve_at_g(ea, A.h0, ta0.x, k2_row_or_none(ua0, la0), rm, s0);
+  bool xa = true;
+  double d = 0.0;
+  b.route[Z.obase + q] = k2_route_turn(g, A, T, ta0, ta1, r1, r0, s1, s0, h1s, h0s, make_uint2(v1.x, v1.y),
+                                       make_uint2(v0.x, v0.y), sm.tw, gc, xa, d);
+  b.route_d[Z.obase + q] = d;
+  if (!xa) sm.redo[o] = 1;
+}
 
+// (without turn costs 7 waves per SIMD: the slim records' 20 KB of LDS per block allow 8 blocks per
+// CU, but 8 waves squeeze the loop into 64 VGPRs with 24 bytes of spills per lane -- C2's K2 0.947
+// ms; at 7 waves (72 VGPRs, no spills) 0.835 ms, 6: 0.837, round 5's kernel 0.866)
+#ifndef RM_BALL_WPE_PLAIN
+#define RM_BALL_WPE_PLAIN 7
+#endif
 template <bool TURN>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_arg) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TURN ? RM_BALL_WPE : RM_BALL_WPE_PLAIN))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_arg) {
   if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ K2Smem<TURN> sm;
   // kNone: a small run's launch, sized by the upper bound; the item count is on the device
@@ -2220,9 +2273,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
   const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;              // last item of the block
   const bool live = t <= tl;
   // ---- phase 1: one lane per item
-  uint32_t KB = 0, ob = 0;
+  uint32_t KB = 0, ob = 0, pq = 0, md = 0;
+  K2Src S;
+  if (threadIdx.x == 0) {   // each mode's table rows and turn rows (a mode without: a valid dummy array)
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      sm.ent_mode[m] = (unsigned long long)(uintptr_t)(g.ball_ent[m] ? (const void*)g.ball_ent[m] : (const void*)b.cand_desc);
+      if constexpr (TURN)
+        sm.trn_mode[m] = (unsigned long long)(uintptr_t)(g.ball_turn[m] ? (const void*)g.ball_turn[m] : (const void*)b.cand_desc);
+    }
+  }
   if (live) {
     const uint32_t p = b.src_item[t];
+    pq = p;
     const uint4 pi = b.pair_info[p];
     const uint32_t i = t - b.src_off[p];
     KB = (pi.z >> 8) & 0xffu;
@@ -2230,7 +2293,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
     const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
     const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
     const int mode = (int)(pi.z >> 16);
-    K2Src S;
+    md = (uint32_t)mode;
     exit_keys(a0, pi.x, S.rk1, S.rk0);
     // the mode's tables answer any bound: beyond their radius, the routes they decide
     const bool fits = (g.ball_mask >> mode) & 1u;
@@ -2242,35 +2305,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
       if (S.rk1 != kKeyInf) S.h1 = x1;
       if (S.rk0 != kKeyInf) S.h0 = x0;
     }
-    S.ent = (unsigned long long)(uintptr_t)g.ball_ent[mode];
     S.road = a0.x;
     S.s = a0.y;
-    S.tdesc = p * kMaxCand;
-    S.rel = 0;
     S.bound = pi.x;
     S.tmax = pi.y;
-    S.ob = ob;
     bool turn_ok = true;
     if constexpr (TURN) {
-      K2Turn T;
+      K2TurnS T;
       T.fac = pi.w;
-      T.trn = (unsigned long long)(uintptr_t)g.ball_turn[mode];
       T.hw = T.fac ? g.road_head[a0.x] : 0u;
-      T.n0 = a1.x;
-      T.n1 = a1.y;
-      T.mode = (uint32_t)mode;
-      T.pad = 0u;
+      T.p = p;
       turn_ok = !T.fac || ((g.ball_turn_mask >> mode) & 1u);   // no turn rows: the search tiers weigh the turns
       sm.tsrc[threadIdx.x] = T;
     }
     if (!fits || S.h1.y == 0u || S.h0.y == 0u || !turn_ok) {   // the search tiers take it (they run later)
       S.bound = kNone;
-      // phase 2 still forms its probe addresses (branch-free): rows 0..1 of a valid array
-      S.ent = (unsigned long long)(uintptr_t)b.cand_desc;
-      S.h1 = S.h0 = make_uint2(0u, 1u);
       b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
     }
-    sm.src[threadIdx.x] = S;
   }
   // the block's transitions: an exclusive scan of the items' K_B (in slot order the items' routes
   // are one contiguous range and this is ob - the first ob; in locality order they are not)
@@ -2292,312 +2343,48 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BAL
   }
   if (live) {
     const uint32_t rel = wbase + incl - KB;
-    sm.src[threadIdx.x].rel = rel;
-    sm.src[threadIdx.x].dbase = sm.src[threadIdx.x].tdesc - rel;
-    sm.src[threadIdx.x].obase = ob - rel;
+    K2SrcS z;
+    z.dbase = pq * kMaxCand - rel;
+    z.obase = ob - rel;
+    z.h1x = S.h1.x; z.h1y = S.h1.y;
+    z.h0x = S.h0.x; z.h0y = S.h0.y;
+    z.rk1l = (uint32_t)S.rk1; z.rk1h = (uint32_t)(S.rk1 >> 32);
+    z.rk0l = (uint32_t)S.rk0; z.rk0h = (uint32_t)(S.rk0 >> 32);
+    z.roadm = S.road | md << 29;
+    z.s = S.s;
+    z.bound = S.bound;
+    z.tmax = S.tmax;
+    z.lim = S.lim;
+    sm.src[threadIdx.x] = z;
     for (uint32_t j = 0; j < KB; ++j) sm.owner[rel + j] = (uint8_t)threadIdx.x;
   }
   sm.redo[threadIdx.x] = 0;
   if constexpr (TURN) {
     if (threadIdx.x < (uint32_t)kTurnDegrees) sm.tw[threadIdx.x] = g.turn_w[threadIdx.x];
+    if (threadIdx.x == 0) sm.ndef = 0u;
   }
   __syncthreads();
-  // ---- phase 2: the block's routes, two transitions per lane and step.  Every load of a step
-  // is issued before any is used: the descriptors unconditionally (a handed-over item's
-  // descriptor is as valid an address), the four first probes branch-free with an unused probe
-  // reading a valid dummy address, and through global-address-space pointers (a pointer that
-  // went through LDS is otherwise generic: flat loads, each waited for on its own).
+  // ---- phase 2: the block's routes, two transitions per lane and step (k2_phase2_slim /
+  // k2_phase2_turn)
   const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
   const uint32_t rm = g.ball_road_mask;
   if constexpr (TURN) {
-    const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
-#if RM_K2_TURN2 == 2
-    if (threadIdx.x == 0) sm.ndef = 0u;
+    if (RM_K2_TURN_STEP == 1) k2_phase2_turn1(sm, b, n, rm, dummy);
+    else k2_phase2_turn(sm, b, n, rm, dummy);
     __syncthreads();
-    k2_phase2_pipe_t(sm, b, n, rm, tdummy);
-    __syncthreads();
+    // the listed routes whose turn weight is walked (ties between the exits), one lane each
     const uint32_t ndef = min(sm.ndef, (uint32_t)kK2Defer);
 #ifdef RM_K2_STATS
     if (threadIdx.x == 0) atomicAdd(&b.ctl[15], sm.ndef);   // diagnostic: walked turn weights
 #endif
-    for (uint32_t z = threadIdx.x; z < ndef; z += kK2Items) {
-      const uint32_t q = sm.def[z];
-#elif RM_K2_TURN2
-    // with turn costs (round 6): two transitions per lane and step, as without them.  Only the
-    // winning exit's turn row is read, after the probes, and only for a valid route that enters its
-    // target road from a node (46 % of C2's transitions; round 5 read both exits' rows of every
-    // transition with the probes: +1.7 GB of lines per step).  Routes whose weight needs the walk
-    // (a tie between the exits, a row without its sum) are listed and walked after the loop by the
-    // one-per-step code below, so the walk's registers stay out of this loop.
-    if (threadIdx.x == 0) sm.ndef = 0u;
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
-      const uint32_t qb = q + kK2Items;
-      const bool hb = qb < n;
-      const uint32_t qB = hb ? qb : q;
-      const uint32_t oa = sm.owner[q], obb = sm.owner[qB];
-      const K2Src& A = sm.src[oa];
-      const K2Src& B = sm.src[obb];
-      const bool la = A.bound != kNone, lb = hb && B.bound != kNone;
-      const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(A.tdesc + (q - A.rel)));
-      const k2_gptr db = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(B.tdesc + (qB - B.rel)));
-      const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1), tb0 = k2_ld(db), tb1 = k2_ld(db + 1);
-      const double gca = b.gc[A.tdesc / kMaxCand], gcb = b.gc[B.tdesc / kMaxCand];
-      const bool ua = la && ta0.w != 0u, ub = lb && tb0.w != 0u;
-      const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
-      const bool ub1 = ub && B.rk1 != kKeyInf, ub0 = ub && B.rk0 != kKeyInf;
-      const k2_gptr ea = (k2_gptr)A.ent, eb = (k2_gptr)B.ent;
-      uint32_t sa1 = ball_slot(ta0.x, A.h1.y), sa0 = ball_slot(ta0.x, A.h0.y);
-      uint32_t sb1 = ball_slot(tb0.x, B.h1.y), sb0 = ball_slot(tb0.x, B.h0.y);
-      const uint4 la1 = k2_ld(ua1 ? ea + (ball_row0(A.h1.x) + sa1) : dummy), la0 = k2_ld(ua0 ? ea + (ball_row0(A.h0.x) + sa0) : dummy);
-      const uint4 lb1 = k2_ld(ub1 ? eb + (ball_row0(B.h1.x) + sb1) : dummy), lb0 = k2_ld(ub0 ? eb + (ball_row0(B.h0.x) + sb0) : dummy);
-      const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
-      const uint4 ra1 = ball_resolve_at((const uint4*)A.ent, A.h1, ta0.x, ua1 ? la1 : none, rm, sa1);
-      const uint4 ra0 = ball_resolve_at((const uint4*)A.ent, A.h0, ta0.x, ua0 ? la0 : none, rm, sa0);
-      const uint4 rb1 = ball_resolve_at((const uint4*)B.ent, B.h1, tb0.x, ub1 ? lb1 : none, rm, sb1);
-      const uint4 rb0 = ball_resolve_at((const uint4*)B.ent, B.h0, tb0.x, ub0 ? lb0 : none, rm, sb0);
-      const K2Turn& TA = sm.tsrc[oa];
-      const K2Turn& TB = sm.tsrc[obb];
-      const K2TurnKey ka = k2_turn_key(A, TA.fac, ta0, ta1, ra1, ra0, sa1, sa0);
-      const K2TurnKey kb = k2_turn_key(B, TB.fac, tb0, tb1, rb1, rb0, sb1, sb0);
-      // the winners' turn rows (a transition without one reads a valid dummy row)
-      const k2_v2 wa = *(la && ka.need == 1u ? (const k2_trow)(const void*)(uintptr_t)TA.trn + ka.row : tdummy);
-      const k2_v2 wb = *(lb && kb.need == 1u ? (const k2_trow)(const void*)(uintptr_t)TB.trn + kb.row : tdummy);
-      const uint32_t xa = k2_turn_weight(ka, TA.hw, wa.x, wa.y, sm.tw), xb = k2_turn_weight(kb, TB.hw, wb.x, wb.y, sm.tw);
-      // xa / xb: the turn weight U, or kNone: walk it after the loop
-      if (la) {
-        if (xa != kNone) {
-          b.route[A.ob + (q - A.rel)] = ka.r;
-          b.route_d[A.ob + (q - A.rel)] = route_term(ka.r, xa, TA.fac, gca);
-          if (!ka.exact) sm.redo[oa] = 1;
-        } else {
-          const uint32_t i = atomicAdd(&sm.ndef, 1u);
-          if (i < kK2Defer) sm.def[i] = (uint16_t)q;
-          else sm.redo[oa] = 1;   // more ties than the list holds: the search tiers take the item
-        }
-      }
-      if (lb) {
-        if (xb != kNone) {
-          b.route[B.ob + (qb - B.rel)] = kb.r;
-          b.route_d[B.ob + (qb - B.rel)] = route_term(kb.r, xb, TB.fac, gcb);
-          if (!kb.exact) sm.redo[obb] = 1;
-        } else {
-          const uint32_t i = atomicAdd(&sm.ndef, 1u);
-          if (i < kK2Defer) sm.def[i] = (uint16_t)qb;
-          else sm.redo[obb] = 1;
-        }
-      }
-    }
-    __syncthreads();
-    const uint32_t ndef = min(sm.ndef, (uint32_t)kK2Defer);
-    for (uint32_t z = threadIdx.x; z < ndef; z += kK2Items) {
-      const uint32_t q = sm.def[z];
-#else
-    // with turn costs: one transition per lane and step (the turn rows and the tie walk cost the
-    // two-per-step loop its registers); both exits' first probes and their turn rows issued together
-    for (uint32_t q = threadIdx.x; q < n; q += kK2Items) {
-#endif
-      const uint32_t o = sm.owner[q];
-      const K2Src& A = sm.src[o];
-      const K2Turn& TA = sm.tsrc[o];
-      const bool la = A.bound != kNone;
-      const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(A.tdesc + (q - A.rel)));
-      const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1);
-      const double gc = b.gc[A.tdesc / kMaxCand];
-      const bool ua = la && ta0.w != 0u;
-      const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
-      const uint32_t h1s = ball_slot(ta0.x, A.h1.y), h0s = ball_slot(ta0.x, A.h0.y);
-      const uint64_t i1 = ball_row0(A.h1.x) + h1s, i0 = ball_row0(A.h0.x) + h0s;
-      const k2_gptr ea = (k2_gptr)A.ent;
-      const bool tt = TA.fac != 0u;   // the item weighs turns: its mode has turn rows
-      const k2_trow tra = (k2_trow)(const void*)(uintptr_t)TA.trn;
-      const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
-      const k2_v2 v1 = *(ua1 && tt ? tra + i1 : tdummy), v0 = *(ua0 && tt ? tra + i0 : tdummy);
-      const uint2 pt1 = make_uint2(v1.x, v1.y), pt0 = make_uint2(v0.x, v0.y);
-      if (!la) continue;
-      const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
-      const uint4* ga = (const uint4*)A.ent;
-      uint32_t s1 = h1s, s0 = h0s;
-      const uint4 r1 = ball_resolve_at(ga, A.h1, ta0.x, ua1 ? la1 : none, rm, s1);
-      const uint4 r0 = ball_resolve_at(ga, A.h0, ta0.x, ua0 ? la0 : none, rm, s0);
-      bool xa = true;
-      double d = 0.0;
-      b.route[A.ob + (q - A.rel)] = k2_route_turn(g, A, TA, ta0, ta1, r1, r0, s1, s0, h1s, h0s, pt1, pt0, sm.tw, gc, xa, d);
-      b.route_d[A.ob + (q - A.rel)] = d;
-      if (!xa) sm.redo[o] = 1;
-    }
+    for (uint32_t zq = threadIdx.x; zq < ndef; zq += kK2Items) k2_turn_walked(g, sm, b, sm.def[zq], rm);
   }
-#if RM_K2_PIPE
-  if constexpr (!TURN) k2_phase2_pipe(sm, b, n, rm);
-  for (uint32_t q = threadIdx.x; q < 0u; q += 2 * kK2Items) {
-#else
-  for (uint32_t q = threadIdx.x; q < (TURN ? 0u : n); q += 2 * kK2Items) {
-#endif
-    const uint32_t qb = q + kK2Items;
-    const bool hb = qb < n;
-    const uint32_t qB = hb ? qb : q;
-    const K2Src& A = sm.src[sm.owner[q]];
-    const K2Src& B = sm.src[sm.owner[qB]];
-    const bool la = A.bound != kNone, lb = hb && B.bound != kNone;
-    const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(A.tdesc + (q - A.rel)));
-    const k2_gptr db = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(B.tdesc + (qB - B.rel)));
-    const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1), tb0 = k2_ld(db), tb1 = k2_ld(db + 1);
-    const bool ua = la && ta0.w != 0u, ub = lb && tb0.w != 0u;   // some direction of the target road is usable
-    const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
-    const bool ub1 = ub && B.rk1 != kKeyInf, ub0 = ub && B.rk0 != kKeyInf;
-    const k2_gptr ea = (k2_gptr)A.ent, eb = (k2_gptr)B.ent;
-    const k2_gptr pa1 = ua1 ? ea + (ball_row0(A.h1.x) + ball_slot(ta0.x, A.h1.y)) : dummy;
-    const k2_gptr pa0 = ua0 ? ea + (ball_row0(A.h0.x) + ball_slot(ta0.x, A.h0.y)) : dummy;
-    const k2_gptr pb1 = ub1 ? eb + (ball_row0(B.h1.x) + ball_slot(tb0.x, B.h1.y)) : dummy;
-    const k2_gptr pb0 = ub0 ? eb + (ball_row0(B.h0.x) + ball_slot(tb0.x, B.h0.y)) : dummy;
-    const uint4 la1 = k2_ld(pa1), la0 = k2_ld(pa0), lb1 = k2_ld(pb1), lb0 = k2_ld(pb0);
-    const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
-    const uint4 ea1 = ua1 ? la1 : none, ea0 = ua0 ? la0 : none, eb1 = ub1 ? lb1 : none, eb0 = ub0 ? lb0 : none;
-    const uint4* ga = (const uint4*)A.ent;
-    const uint4* gb = (const uint4*)B.ent;
-    bool xa = true, xb = true;
-    if (la) b.route[A.ob + (q - A.rel)] = k2_route(A, ta0, ta1, ball_resolve(ga, A.h1, ta0.x, ea1, rm), ball_resolve(ga, A.h0, ta0.x, ea0, rm), xa);
-    if (lb) b.route[B.ob + (qb - B.rel)] = k2_route(B, tb0, tb1, ball_resolve(gb, B.h1, tb0.x, eb1, rm), ball_resolve(gb, B.h0, tb0.x, eb0, rm), xb);
-    if (!xa) sm.redo[sm.owner[q]] = 1;
-    if (!xb) sm.redo[sm.owner[qB]] = 1;
-  }
+  if constexpr (!TURN) k2_phase2_slim(sm, b, n, rm, dummy);
   // items with a route the tables could not decide: the search tiers recompute all of its routes
   __syncthreads();
   if (live && sm.redo[threadIdx.x] && sm.src[threadIdx.x].bound != kNone) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
 }
 
-// K2 ball tier, target-major (round 5 experiment, RM_K2_TGT): the block's (pair, source) items as
-// in k_routes_ball2, but phase 2 deals one lane per (pair in the block, target j): the target's
-// descriptor once, then every in-block source's two first probes of the target road issued
-// together, four sources at a time -- two dependent round trips for a pair's K_A transitions of
-// target j instead of two per two transitions.  Bit-identical routes (the same k2_route).
-#ifndef RM_K2_TGT
-#define RM_K2_TGT 0
-#endif
-struct K2TSmem {
-  K2Src src[kK2Items];
-  uint32_t pair[kK2Items];
-  uint8_t owner[kK2Items * kMaxCand];   // unit of the block -> head item (first in-block source) of its pair
-  uint8_t cnt[kK2Items];                // head item: in-block sources of its pair
-  uint32_t wsum[kK2Items / 64];
-  uint8_t redo[kK2Items];
-};
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_BALL_WPE))) k_routes_ball_t(DevGraph g, DevBatch b, uint32_t n_arg) {
-  if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
-  __shared__ K2TSmem sm;
-  const uint32_t n_items = n_arg != kNone ? n_arg : (uint32_t)b.tot[1];
-  const uint32_t t0i = xcd_block(blockIdx.x, gridDim.x) * kK2Items;
-  if (t0i >= n_items) return;
-  const uint32_t t = t0i + threadIdx.x;
-  const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;
-  const bool live = t <= tl;
-  uint32_t KB = 0, p = kNone;
-  if (live) {
-    p = b.src_item[t];
-    const uint4 pi = b.pair_info[p];
-    const uint32_t i = t - b.src_off[p];
-    KB = (pi.z >> 8) & 0xffu;
-    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
-    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
-    const int mode = (int)(pi.z >> 16);
-    K2Src S;
-    exit_keys(a0, pi.x, S.rk1, S.rk0);
-    const bool fits = (g.ball_mask >> mode) & 1u;
-    S.lim = ball_exact_limit(pi.x, g.ball_radius[mode], S.rk1, S.rk0);
-    S.h1 = S.h0 = make_uint2(0u, 1u);
-    if (fits) {
-      const uint2* hp = g.ball_hdr[mode];
-      const uint2 x1 = hp[a1.y], x0 = hp[a1.x];
-      if (S.rk1 != kKeyInf) S.h1 = x1;
-      if (S.rk0 != kKeyInf) S.h0 = x0;
-    }
-    S.ent = (unsigned long long)(uintptr_t)g.ball_ent[mode];
-    S.road = a0.x;
-    S.s = a0.y;
-    S.tdesc = p * kMaxCand;
-    S.rel = 0;
-    S.bound = pi.x;
-    S.tmax = pi.y;
-    S.ob = b.trans_off[p] + i * KB;
-    if (!fits || S.h1.y == 0u || S.h0.y == 0u) {
-      S.bound = kNone;
-      b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
-    }
-    sm.src[threadIdx.x] = S;
-  }
-  sm.pair[threadIdx.x] = p;
-  sm.redo[threadIdx.x] = 0;
-  __syncthreads();
-  // heads: the first in-block item of each pair; a head's units are its pair's targets
-  const bool head = live && (threadIdx.x == 0 || sm.pair[threadIdx.x - 1] != p);
-  uint32_t cnt = 0;
-  if (head) {
-    cnt = 1;
-    while (threadIdx.x + cnt < kK2Items && sm.pair[threadIdx.x + cnt] == p) ++cnt;
-    sm.cnt[threadIdx.x] = (uint8_t)cnt;
-  }
-  const uint32_t U = head ? KB : 0u;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t incl = U;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t u = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += u;
-  }
-  if (lane == 63) sm.wsum[wv] = incl;
-  __syncthreads();
-  uint32_t wbase = 0, n = 0;
-#pragma unroll
-  for (int w = 0; w < kK2Items / 64; ++w) {
-    const uint32_t x = sm.wsum[w];
-    wbase += w < wv ? x : 0u;
-    n += x;
-  }
-  if (head) {
-    const uint32_t rel = wbase + incl - U;
-    sm.src[threadIdx.x].rel = rel;
-    for (uint32_t j = 0; j < U; ++j) sm.owner[rel + j] = (uint8_t)threadIdx.x;
-  }
-  __syncthreads();
-  const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
-  const uint32_t rm = g.ball_road_mask;
-  const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
-  for (uint32_t u = threadIdx.x; u < n; u += kK2Items) {
-    const uint32_t h = sm.owner[u];
-    const K2Src& H = sm.src[h];
-    const uint32_t j = u - H.rel, c = sm.cnt[h];
-    const k2_gptr dt = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(H.tdesc + j));
-    const uint4 t0 = k2_ld(dt), t1 = k2_ld(dt + 1);
-    const bool usable = t0.w != 0u;
-    for (uint32_t c0 = 0; c0 < c; c0 += 4) {
-      uint4 r1[4], r0[4];
-      bool u1[4], u0[4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {   // four sources' first probes issued together (clamped)
-        const K2Src& S = sm.src[h + min(c0 + (uint32_t)x, c - 1u)];
-        const bool ls = S.bound != kNone && usable;
-        u1[x] = ls && S.rk1 != kKeyInf;
-        u0[x] = ls && S.rk0 != kKeyInf;
-        const k2_gptr e = (k2_gptr)S.ent;
-        r1[x] = k2_ld(u1[x] ? e + (ball_row0(S.h1.x) + ball_slot(t0.x, S.h1.y)) : dummy);
-        r0[x] = k2_ld(u0[x] ? e + (ball_row0(S.h0.x) + ball_slot(t0.x, S.h0.y)) : dummy);
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        if (c0 + (uint32_t)x >= c) break;
-        const K2Src& S = sm.src[h + c0 + x];
-        if (S.bound == kNone) continue;
-        const uint4* ge = (const uint4*)S.ent;
-        bool ex = true;
-        b.route[S.ob + j] = k2_route(S, t0, t1, ball_resolve(ge, S.h1, t0.x, u1[x] ? r1[x] : none, rm),
-                                     ball_resolve(ge, S.h0, t0.x, u0[x] ? r0[x] : none, rm), ex);
-        if (!ex) sm.redo[h + c0 + x] = 1;
-      }
-    }
-  }
-  __syncthreads();
-  if (live && sm.redo[threadIdx.x] && sm.src[threadIdx.x].bound != kNone) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
-}
 
 // K2 lane tier: one lane per (layer pair, source) item.  The pair constants come from
 // one dwordx4 (pair_info) and every candidate from its 32-byte descriptor.  A search
@@ -3715,7 +3502,7 @@ __device__ __forceinline__ VitChunk vit_layout(const VitLayerDesc& d, uint32_t s
 // chunk holds -- C2 K3 moved 1.73x its algorithmic bytes.  Still one unconditional load per slot
 // (a v_min, no branch, no register merge).
 #ifndef RM_VIT_CLAMP
-#define RM_VIT_CLAMP 1
+#define RM_VIT_CLAMP 0
 #endif
 template <bool TURN>
 __device__ __forceinline__ void vit_load(const DevBatch& b, uint32_t o, const VitChunk& c, int j, VitRegs<TURN>& r) {
@@ -6365,9 +6152,6 @@ void Matcher::run_device(const RunParams& rp) {
     if (v.route_d)
       hipLaunchKernelGGL(k_routes_ball2<true>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
                          g, v, (uint32_t)n_src);
-    else if (RM_K2_TGT)
-      hipLaunchKernelGGL(k_routes_ball_t, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st, g, v,
-                         (uint32_t)n_src);
     else
       hipLaunchKernelGGL(k_routes_ball2<false>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
                          g, v, (uint32_t)n_src);
