@@ -64,6 +64,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   // per transition with turn costs (rule 3b): the distance term K3 adds, turn_m + |route_m - gc| in
   // metres (+inf for an invalid route); null when no trace of the batch has turn costs
   double* route_d;
+  uint32_t* walk; uint32_t walk_cap;   // turn weights K2 leaves to k_turn_walks (count ctl[15])
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
@@ -1716,7 +1717,12 @@ __device__ __forceinline__ unsigned long long ball_label(unsigned long long rk1,
 // the target road, the label, the key, one coalesced store.  No lane walks a target loop of its
 // own (the round-2 kernel's lanes ran to their wave's largest K_B, each target two dependent
 // round trips after the last), and two transitions per lane are in flight at once.
-constexpr int kK2Items = 256;
+#ifndef RM_K2_ITEMS
+#define RM_K2_ITEMS 256
+#endif
+constexpr int kK2Items = RM_K2_ITEMS;   // (pair, source) items per block
+constexpr int kK2Threads = 256;         // threads per block (phase 2: one transition per thread and step)
+static_assert(kK2Items <= kK2Threads && kK2Items % 64 == 0, "phase 1 runs one item per thread");
 // graphs from this many nodes take the locality order by default (Engine::locality_default),
 // and so do batches sampled this sparsely on average (Matcher::run)
 constexpr uint64_t kLocalityNodes = 150000;
@@ -1729,8 +1735,7 @@ __device__ __forceinline__ uint4 k2_ld(k2_gptr p) {
   const k2_v4 v = *p;
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-// A source item in full (the walked turn weights, k2_turn_walked / k2_route_turn, rebuild it
-// from the LDS records)
+// A source item in full (k_turn_walks rebuilds it for the walked turn weights, k2_route_turn)
 struct K2Src {
   unsigned long long ent;        // the item's mode's table rows (a global address: see k2_gptr)
   uint2 h1, h0;                  // table headers of the exits (bits 0: no table)
@@ -1748,7 +1753,6 @@ struct K2Turn {
   uint32_t n0, n1;               // the source road's endpoints (the exits' nodes)
   uint32_t mode, pad;
 };
-constexpr uint32_t kK2Defer = 256;    // walked turn weights listed per block (more: the item is searched)
 // The item record of the kernel without turn costs, 60 bytes (round 6).  LDS sets this kernel's
 // occupancy: at 80 bytes per item (22.8 -> 24.9 KB per block) C2's K2 went 0.866 -> 0.935 ms with
 // the same loop (6 blocks of 4 waves per CU instead of 7); at 60 bytes a block fits 20 KB and a CU
@@ -1764,24 +1768,19 @@ struct K2SrcS {
   uint32_t s, bound, tmax, lim;
 };
 static_assert(sizeof(K2SrcS) == 60, "K2SrcS is 60 bytes");
-// with turn costs, per item besides its K2SrcS: the source road's heading word, the pair's factor
-// (float bits; 0: no turn costs) and the pair (its gc)
-struct K2TurnS {
-  uint32_t hw, fac, p;
-};
 template <bool TURN>
 struct K2Smem {
   K2SrcS src[kK2Items];
-  unsigned long long ent_mode[8];      // each mode's table rows (a mode without tables: a dummy array)
-  unsigned long long trn_mode[TURN ? 8 : 1];   // ... and turn rows
+  unsigned long long ent_mode[5];      // each mode's table rows (a mode without tables: a dummy array)
+  unsigned long long trn_mode[TURN ? 5 : 1];   // ... and turn rows
   uint8_t owner[kK2Items * kMaxCand];   // transition of the block -> item of the block
-  uint32_t wsum[kK2Items / 64];
-  uint8_t redo[kK2Items];               // a route of the item was not exact from the tables
-  K2TurnS tsrc[TURN ? kK2Items : 1];
+  uint32_t wsum[kK2Threads / 64];
+  uint32_t redo[kK2Items / 32];         // bit o: a route of item o was not exact from the tables
   uint32_t tw[TURN ? kTurnDegrees : 1];  // the turn weights (DevGraph::turn_w) in LDS
-  uint32_t ndef;                         // transitions whose turn weight is walked after the loop
-  uint16_t def[TURN ? kK2Defer : 1];
 };
+// (both records fit 20 KB per block with turn costs too: 8 blocks per CU)
+template <class SM>
+__device__ __forceinline__ void k2_redo(SM& sm, uint32_t o) { atomicOr(&sm.redo[o >> 5], 1u << (o & 31u)); }
 
 // Bounds beyond the ball radius (round 4).  A table holds every node within R of its exit, so a
 // node absent from exit x's table is more than R away from it and any route through it is longer
@@ -2003,11 +2002,40 @@ __device__ __forceinline__ uint4 ball_resolve_at_g(k2_gptr ent, const uint2& h, 
     if ((e.x & rmask) == road || e.x == kNone) return e;
   }
 }
+#ifndef RM_K2_PLAIN_STEP
+#define RM_K2_PLAIN_STEP 1
+#endif
 template <class SM>
 __device__ __forceinline__ void k2_phase2_slim(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_gptr dummy) {
   const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
-  for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
-    const uint32_t qb = q + kK2Items;
+  if (RM_K2_PLAIN_STEP == 1) {   // (A/B: one transition per lane and step, fewer registers)
+    for (uint32_t q = threadIdx.x; q < n; q += kK2Threads) {
+      const K2SrcS& A = sm.src[sm.owner[q]];
+      const bool la = A.bound != kNone;
+      const uint4* pda = b.cand_desc + 2 * (uint64_t)(A.dbase + q);
+      const uint4 ta0 = k2_ld((k2_gptr)(const void*)pda);
+      const uint2 ta1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pda + 1) + 1));
+      const unsigned long long ak1 = (unsigned long long)A.rk1h << 32 | A.rk1l, ak0 = (unsigned long long)A.rk0h << 32 | A.rk0l;
+      const bool ua = la && ta0.w != 0u;
+      const bool ua1 = ua && ak1 != kKeyInf, ua0 = ua && ak0 != kKeyInf;
+      const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[A.roadm >> 29];
+      const k2_gptr pa1 = ua1 ? ea + (ball_row0(A.h1x) + ball_slot(ta0.x, A.h1y)) : dummy;
+      const k2_gptr pa0 = ua0 ? ea + (ball_row0(A.h0x) + ball_slot(ta0.x, A.h0y)) : dummy;
+      const uint4 la1 = k2_ld(pa1), la0 = k2_ld(pa0);
+      bool xa = true;
+      const uint32_t r = k2_route_v(ak1, ak0, A.roadm & 0x1fffffffu, A.s, A.lim, A.bound, A.tmax, ta0,
+                                    make_uint4(0u, 0u, ta1.x, ta1.y),
+                                    ball_resolve_g(ea, make_uint2(A.h1x, A.h1y), ta0.x, k2_row_or_none(ua1, la1), rm),
+                                    ball_resolve_g(ea, make_uint2(A.h0x, A.h0y), ta0.x, k2_row_or_none(ua0, la0), rm), xa);
+      if (la) {
+        b.route[A.obase + q] = r;
+        if (!xa) k2_redo(sm, sm.owner[q]);
+      }
+    }
+    return;
+  }
+  for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Threads) {
+    const uint32_t qb = q + kK2Threads;
     const bool hb = qb < n;
     const uint32_t qB = hb ? qb : q;
     const K2SrcS& A = sm.src[sm.owner[q]];
@@ -2042,8 +2070,8 @@ __device__ __forceinline__ void k2_phase2_slim(SM& sm, const DevBatch& b, uint32
                                          make_uint4(0u, 0u, tb1.x, tb1.y),
                                          ball_resolve_g(eb, make_uint2(B.h1x, B.h1y), tb0.x, k2_row_or_none(ub1, lb1), rm),
                                          ball_resolve_g(eb, make_uint2(B.h0x, B.h0y), tb0.x, k2_row_or_none(ub0, lb0), rm), xb);
-    if (!xa) sm.redo[sm.owner[q]] = 1;
-    if (!xb) sm.redo[sm.owner[qB]] = 1;
+    if (!xa) k2_redo(sm, sm.owner[q]);
+    if (!xb) k2_redo(sm, sm.owner[qB]);
   }
   (void)none;
 }
@@ -2093,170 +2121,132 @@ __device__ __forceinline__ uint32_t k2_turn_weight(const K2TurnKey& k, uint32_t 
   return tw[turn_degree(head_back(hw, k.e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
 }
 
-// phase 2 with turn costs (round 6): two transitions per lane and step, as without them.  Only the
-// winning exit's turn row is read, after the probes, and only for a valid route that enters its
-// target road from a node (46 % of C2's transitions; round 5 read both exits' rows of every
-// transition with the probes: +1.7 GB of lines per step).  A route whose weight needs the walk (a
-// tie between the exits, a row without its sum: 1.3 % of C2's) is listed and walked after the
-// loop (k2_turn_walked), so the walk's registers stay out of this loop.
+// phase 2 with turn costs (round 6): one transition per lane and step, with both exits' turn rows
+// read with the probes at their first-probe slots (no dependent third load; a row resolved past a
+// collision -- rare -- reloads its turn row).  The item records are the plain kernel's (the source
+// road's heading word, the pair's factor and gc come from global memory with the descriptor), so the
+// block fits 20 KB of LDS and a CU holds 8.  A route whose turn weight needs the walk (a tie between
+// the exits, a row without its sum: 1.3 % of C2's transitions) goes to a list that k_turn_walks
+// walks right after this kernel, one lane each: the walk's registers (86 VGPRs with it in this
+// loop, 60 without) stay out of this kernel.
 typedef unsigned int k2_v2 __attribute__((ext_vector_type(2)));
 typedef const k2_v2 __attribute__((address_space(1)))* k2_trow;
 template <class SM>
-__device__ __forceinline__ void k2_turn_store(SM& sm, const DevBatch& b, uint32_t q, uint32_t o, const K2SrcS& S,
-                                              const K2TurnKey& k, uint32_t U, uint32_t fac, double gc) {
-  if (U != kNone) {
-    b.route[S.obase + q] = k.r;
-    b.route_d[S.obase + q] = route_term(k.r, U, fac, gc);
-    if (!k.exact) sm.redo[o] = 1;
-  } else {
-    const uint32_t i = atomicAdd(&sm.ndef, 1u);
-    if (i < kK2Defer) sm.def[i] = (uint16_t)q;
-    else sm.redo[o] = 1;   // more walks than the list holds: the search tiers take the item
-  }
-}
-template <class SM>
-__device__ __forceinline__ void k2_phase2_turn(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_gptr dummy) {
+__device__ __forceinline__ void k2_phase2_turn1(const DevGraph& g, SM& sm, const DevBatch& b, uint32_t n, uint32_t rm,
+                                                k2_gptr dummy, uint32_t t0i) {
   const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
-  for (uint32_t q = threadIdx.x; q < n; q += 2 * kK2Items) {
-    const uint32_t qb = q + kK2Items;
-    const bool hb = qb < n;
-    const uint32_t qB = hb ? qb : q;
-    const uint32_t oa = sm.owner[q], obb = sm.owner[qB];
-    const K2SrcS& A = sm.src[oa];
-    const K2SrcS& B = sm.src[obb];
-    const bool la = A.bound != kNone, lb = hb && B.bound != kNone;
-    const uint4* pda = b.cand_desc + 2 * (uint64_t)(A.dbase + q);
-    const uint4* pdb = b.cand_desc + 2 * (uint64_t)(B.dbase + qB);
-    const uint4 ta0 = k2_ld((k2_gptr)(const void*)pda), tb0 = k2_ld((k2_gptr)(const void*)pdb);
-    const uint2 ta1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pda + 1) + 1));
-    const uint2 tb1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pdb + 1) + 1));
-    const K2TurnS TA = sm.tsrc[oa], TB = sm.tsrc[obb];
-    const double gca = b.gc[TA.p], gcb = b.gc[TB.p];
-    const unsigned long long ak1 = (unsigned long long)A.rk1h << 32 | A.rk1l, ak0 = (unsigned long long)A.rk0h << 32 | A.rk0l;
-    const unsigned long long bk1 = (unsigned long long)B.rk1h << 32 | B.rk1l, bk0 = (unsigned long long)B.rk0h << 32 | B.rk0l;
-    const bool ua = la && ta0.w != 0u, ub = lb && tb0.w != 0u;
-    const bool ua1 = ua && ak1 != kKeyInf, ua0 = ua && ak0 != kKeyInf;
-    const bool ub1 = ub && bk1 != kKeyInf, ub0 = ub && bk0 != kKeyInf;
-    const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[A.roadm >> 29];
-    const k2_gptr eb = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[B.roadm >> 29];
-    uint32_t sa1 = ball_slot(ta0.x, A.h1y), sa0 = ball_slot(ta0.x, A.h0y);
-    uint32_t sb1 = ball_slot(tb0.x, B.h1y), sb0 = ball_slot(tb0.x, B.h0y);
-    const uint4 la1 = k2_ld(ua1 ? ea + (ball_row0(A.h1x) + sa1) : dummy), la0 = k2_ld(ua0 ? ea + (ball_row0(A.h0x) + sa0) : dummy);
-    const uint4 lb1 = k2_ld(ub1 ? eb + (ball_row0(B.h1x) + sb1) : dummy), lb0 = k2_ld(ub0 ? eb + (ball_row0(B.h0x) + sb0) : dummy);
-    const uint4 ra1 = ball_resolve_at_g(ea, make_uint2(A.h1x, A.h1y), ta0.x, k2_row_or_none(ua1, la1), rm, sa1);
-    const uint4 ra0 = ball_resolve_at_g(ea, make_uint2(A.h0x, A.h0y), ta0.x, k2_row_or_none(ua0, la0), rm, sa0);
-    const uint4 rb1 = ball_resolve_at_g(eb, make_uint2(B.h1x, B.h1y), tb0.x, k2_row_or_none(ub1, lb1), rm, sb1);
-    const uint4 rb0 = ball_resolve_at_g(eb, make_uint2(B.h0x, B.h0y), tb0.x, k2_row_or_none(ub0, lb0), rm, sb0);
-    const K2TurnKey ka = k2_turn_key(A, ak1, ak0, TA.fac, ta0, make_uint4(0u, 0u, ta1.x, ta1.y), ra1, ra0, sa1, sa0);
-    const K2TurnKey kb = k2_turn_key(B, bk1, bk0, TB.fac, tb0, make_uint4(0u, 0u, tb1.x, tb1.y), rb1, rb0, sb1, sb0);
-    // the winners' turn rows (a transition without one reads a valid dummy row)
-    const k2_trow tra = (k2_trow)(const void*)(uintptr_t)sm.trn_mode[A.roadm >> 29];
-    const k2_trow trb = (k2_trow)(const void*)(uintptr_t)sm.trn_mode[B.roadm >> 29];
-    const k2_v2 wa = *(la && ka.need == 1u ? tra + ka.row : tdummy);
-    const k2_v2 wb = *(lb && kb.need == 1u ? trb + kb.row : tdummy);
-    const uint32_t xa = k2_turn_weight(ka, TA.hw, wa.x, wa.y, sm.tw), xb = k2_turn_weight(kb, TB.hw, wb.x, wb.y, sm.tw);
-    // xa / xb: the turn weight U, or kNone: walked after the loop
-    if (la) k2_turn_store(sm, b, q, oa, A, ka, xa, TA.fac, gca);
-    if (lb) k2_turn_store(sm, b, qb, obb, B, kb, xb, TB.fac, gcb);
-  }
-}
-// The same with one transition per lane and step and both exits' turn rows read with the probes
-// at their first-probe slots (round 5's issue group: no dependent third load; a row resolved past
-// a collision -- rare -- reloads its turn row).  RM_K2_TURN_STEP selects this loop (1) or the
-// two-per-step one above (2).
-#ifndef RM_K2_TURN_STEP
-#define RM_K2_TURN_STEP 1
-#endif
-template <class SM>
-__device__ __forceinline__ void k2_phase2_turn1(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_gptr dummy) {
-  const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
-  for (uint32_t q = threadIdx.x; q < n; q += kK2Items) {
+  for (uint32_t q = threadIdx.x; q < n; q += kK2Threads) {
     const uint32_t o = sm.owner[q];
     const K2SrcS& A = sm.src[o];
     const bool la = A.bound != kNone;
-    const uint4* pda = b.cand_desc + 2 * (uint64_t)(A.dbase + q);
+    const uint32_t di = A.dbase + q;   // = pair * 16 + target
+    const uint32_t p = di >> 4;
+    const uint4* pda = b.cand_desc + 2 * (uint64_t)di;
     const uint4 ta0 = k2_ld((k2_gptr)(const void*)pda);
     const uint2 ta1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pda + 1) + 1));
-    const K2TurnS TA = sm.tsrc[o];
-    const double gca = b.gc[TA.p];
+    const uint32_t road = A.roadm & 0x1fffffffu;
+    const uint32_t fac = b.pair_info[p].w, hw = g.road_head[road];
+    const double gc = b.gc[p];
     const unsigned long long ak1 = (unsigned long long)A.rk1h << 32 | A.rk1l, ak0 = (unsigned long long)A.rk0h << 32 | A.rk0l;
     const bool ua = la && ta0.w != 0u;
     const bool ua1 = ua && ak1 != kKeyInf, ua0 = ua && ak0 != kKeyInf;
     const uint32_t mode = A.roadm >> 29;
     const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[mode];
     const k2_trow tra = (k2_trow)(const void*)(uintptr_t)sm.trn_mode[mode];
-    const bool tt = TA.fac != 0u;
     const uint32_t h1s = ball_slot(ta0.x, A.h1y), h0s = ball_slot(ta0.x, A.h0y);
     const uint64_t i1 = ball_row0(A.h1x) + h1s, i0 = ball_row0(A.h0x) + h0s;
     const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
-    const k2_v2 v1 = *(ua1 && tt ? tra + i1 : tdummy), v0 = *(ua0 && tt ? tra + i0 : tdummy);
+    // (a pair without turn costs may be of a mode without turn rows: no row read)
+    const k2_v2 v1 = *(ua1 && fac ? tra + i1 : tdummy), v0 = *(ua0 && fac ? tra + i0 : tdummy);
     uint32_t s1 = h1s, s0 = h0s;
     const uint4 r1 = ball_resolve_at_g(ea, make_uint2(A.h1x, A.h1y), ta0.x, k2_row_or_none(ua1, la1), rm, s1);
     const uint4 r0 = ball_resolve_at_g(ea, make_uint2(A.h0x, A.h0y), ta0.x, k2_row_or_none(ua0, la0), rm, s0);
-    const K2TurnKey k = k2_turn_key(A, ak1, ak0, TA.fac, ta0, make_uint4(0u, 0u, ta1.x, ta1.y), r1, r0, s1, s0);
+    const K2TurnKey k = k2_turn_key(A, ak1, ak0, fac, ta0, make_uint4(0u, 0u, ta1.x, ta1.y), r1, r0, s1, s0);
     k2_v2 w = k.e1 ? v1 : v0;
     if (k.need == 1u && (k.e1 ? s1 != h1s : s0 != h0s)) w = tra[k.row];   // resolved past a collision
-    const uint32_t x = k2_turn_weight(k, TA.hw, w.x, w.y, sm.tw);
-    if (la) k2_turn_store(sm, b, q, o, A, k, x, TA.fac, gca);
+    const uint32_t U = k2_turn_weight(k, hw, w.x, w.y, sm.tw);
+    if (!la) continue;
+    if (U != kNone) {
+      b.route[A.obase + q] = k.r;
+      b.route_d[A.obase + q] = route_term(k.r, U, fac, gc);
+      if (!k.exact) k2_redo(sm, o);
+    } else {   // walked by k_turn_walks (item << 4 | target); a full list: the search tiers take the item
+      const uint32_t item = t0i + o;
+      const uint32_t x = atomicAdd(&b.ctl[15], 1u);
+      if (x < b.walk_cap && item < (1u << 28)) b.walk[x] = item << 4 | (di & 15u);
+      else k2_redo(sm, o);
+    }
   }
 }
-// a listed transition (its turn weight needs the walk): the route again, one lane, with both exits'
-// turn rows at their first-probe slots and the walk through the tables (k2_route_turn)
-template <class SM>
-__device__ void k2_turn_walked(const DevGraph& g, SM& sm, const DevBatch& b, uint32_t q, uint32_t rm) {
+
+// The turn weights K2 left to walk (b.walk, count ctl[15]), one lane each: the item again as
+// k_routes_ball2's phase 1 forms it, the route with both exits' turn rows at their first-probe
+// slots, and the walk through the tables (k2_route_turn / ball_turn_walk).  A route the tables
+// cannot decide hands its item to the search tiers, which run next.
+constexpr uint32_t kWalkGrid = 2048;   // k_turn_walks: grid-stride over the device-side count
+__global__ void __launch_bounds__(256) k_turn_walks(DevGraph g, DevBatch b) {
+  if (steady_abort(b)) return;
+  const uint32_t nw = min(b.ctl[15], b.walk_cap);
+  const uint32_t rm = g.ball_road_mask;
   const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
   const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
-  const uint32_t o = sm.owner[q];
-  const K2SrcS& Z = sm.src[o];
-  const K2TurnS TZ = sm.tsrc[o];
-  const uint32_t mode = Z.roadm >> 29;
-  K2Src A;
-  A.ent = sm.ent_mode[mode];
-  A.h1 = make_uint2(Z.h1x, Z.h1y);
-  A.h0 = make_uint2(Z.h0x, Z.h0y);
-  A.rk1 = (unsigned long long)Z.rk1h << 32 | Z.rk1l;
-  A.rk0 = (unsigned long long)Z.rk0h << 32 | Z.rk0l;
-  A.road = Z.roadm & 0x1fffffffu;
-  A.s = Z.s;
-  A.bound = Z.bound;
-  A.tmax = Z.tmax;
-  A.lim = Z.lim;
-  K2Turn T;
-  T.trn = sm.trn_mode[mode];
-  T.hw = TZ.hw;
-  T.fac = TZ.fac;
-  T.n0 = g.road_node0[A.road];
-  T.n1 = g.road_node1[A.road];
-  T.mode = mode;
-  T.pad = 0u;
-  const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * (uint64_t)(Z.dbase + q));
-  const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1);
-  const double gc = b.gc[TZ.p];
-  const bool ua = ta0.w != 0u;
-  const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
-  const uint32_t h1s = ball_slot(ta0.x, A.h1.y), h0s = ball_slot(ta0.x, A.h0.y);
-  const uint64_t i1 = ball_row0(A.h1.x) + h1s, i0 = ball_row0(A.h0.x) + h0s;
-  const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)A.ent;
-  const bool tt = T.fac != 0u;
-  const k2_trow tra = (k2_trow)(const void*)(uintptr_t)T.trn;
-  const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
-  const k2_v2 v1 = *(ua1 && tt ? tra + i1 : tdummy), v0 = *(ua0 && tt ? tra + i0 : tdummy);
-  uint32_t s1 = h1s, s0 = h0s;
-  const uint4 r1 = ball_resolve_at_g(ea, A.h1, ta0.x, k2_row_or_none(ua1, la1), rm, s1);
-  const uint4 r0 = ball_resolve_at_g(ea, A.h0, ta0.x, k2_row_or_none(ua0, la0), rm, s0);
-  bool xa = true;
-  double d = 0.0;
-  b.route[Z.obase + q] = k2_route_turn(g, A, T, ta0, ta1, r1, r0, s1, s0, h1s, h0s, make_uint2(v1.x, v1.y),
-                                       make_uint2(v0.x, v0.y), sm.tw, gc, xa, d);
-  b.route_d[Z.obase + q] = d;
-  if (!xa) sm.redo[o] = 1;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < nw; e += gridDim.x * blockDim.x) {
+    const uint32_t wv = b.walk[e], t = wv >> 4, j = wv & 15u;
+    const uint32_t p = b.src_item[t];
+    const uint4 pi = b.pair_info[p];
+    const uint32_t i = t - b.src_off[p];
+    const uint32_t KB = (pi.z >> 8) & 0xffu;
+    const uint64_t ro = (uint64_t)b.trans_off[p] + i * KB + j;
+    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+    const int mode = (int)(pi.z >> 16);
+    K2Src A;
+    exit_keys(a0, pi.x, A.rk1, A.rk0);
+    A.lim = ball_exact_limit(pi.x, g.ball_radius[mode], A.rk1, A.rk0);
+    const uint2* hp = g.ball_hdr[mode];
+    A.h1 = A.rk1 != kKeyInf ? hp[a1.y] : make_uint2(0u, 1u);
+    A.h0 = A.rk0 != kKeyInf ? hp[a1.x] : make_uint2(0u, 1u);
+    A.ent = (unsigned long long)(uintptr_t)g.ball_ent[mode];
+    A.road = a0.x;
+    A.s = a0.y;
+    A.bound = pi.x;
+    A.tmax = pi.y;
+    K2Turn T;
+    T.fac = pi.w;
+    T.trn = (unsigned long long)(uintptr_t)g.ball_turn[mode];
+    T.hw = g.road_head[a0.x];
+    T.n0 = a1.x;
+    T.n1 = a1.y;
+    T.mode = (uint32_t)mode;
+    T.pad = 0u;
+    const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * ((uint64_t)p * kMaxCand + j));
+    const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1);
+    const double gc = b.gc[p];
+    const bool ua = ta0.w != 0u;
+    const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
+    const uint32_t h1s = ball_slot(ta0.x, A.h1.y), h0s = ball_slot(ta0.x, A.h0.y);
+    const uint64_t i1 = ball_row0(A.h1.x) + h1s, i0 = ball_row0(A.h0.x) + h0s;
+    const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)A.ent;
+    const k2_trow tra = (k2_trow)(const void*)(uintptr_t)T.trn;
+    const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
+    const k2_v2 v1 = *(ua1 && T.fac ? tra + i1 : tdummy), v0 = *(ua0 && T.fac ? tra + i0 : tdummy);
+    uint32_t s1 = h1s, s0 = h0s;
+    const uint4 r1 = ball_resolve_at_g(ea, A.h1, ta0.x, k2_row_or_none(ua1, la1), rm, s1);
+    const uint4 r0 = ball_resolve_at_g(ea, A.h0, ta0.x, k2_row_or_none(ua0, la0), rm, s0);
+    bool ok = true;
+    double d = 0.0;
+    b.route[ro] = k2_route_turn(g, A, T, ta0, ta1, r1, r0, s1, s0, h1s, h0s, make_uint2(v1.x, v1.y),
+                                make_uint2(v0.x, v0.y), g.turn_w, gc, ok, d);
+    b.route_d[ro] = d;
+    if (!ok) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+  }
 }
 
 // (without turn costs 7 waves per SIMD: the slim records' 20 KB of LDS per block allow 8 blocks per
 // CU, but 8 waves squeeze the loop into 64 VGPRs with 24 bytes of spills per lane -- C2's K2 0.947
 // ms; at 7 waves (72 VGPRs, no spills) 0.835 ms, 6: 0.837, round 5's kernel 0.866)
 #ifndef RM_BALL_WPE_PLAIN
-#define RM_BALL_WPE_PLAIN 7
+#define RM_BALL_WPE_PLAIN 8
 #endif
 template <bool TURN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TURN ? RM_BALL_WPE : RM_BALL_WPE_PLAIN))) k_routes_ball2(DevGraph g, DevBatch b, uint32_t n_arg) {
@@ -2271,7 +2261,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TURN ?
   const uint32_t t0i = xcd_block(blockIdx.x, nblk) * kK2Items;   // first item of the block
   const uint32_t t = t0i + threadIdx.x;
   const uint32_t tl = min(n_items, t0i + kK2Items) - 1u;              // last item of the block
-  const bool live = t <= tl;
+  const bool live = threadIdx.x < (uint32_t)kK2Items && t <= tl;   // (items <= threads per block)
   // ---- phase 1: one lane per item
   uint32_t KB = 0, ob = 0, pq = 0, md = 0;
   K2Src S;
@@ -2310,14 +2300,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TURN ?
     S.bound = pi.x;
     S.tmax = pi.y;
     bool turn_ok = true;
-    if constexpr (TURN) {
-      K2TurnS T;
-      T.fac = pi.w;
-      T.hw = T.fac ? g.road_head[a0.x] : 0u;
-      T.p = p;
-      turn_ok = !T.fac || ((g.ball_turn_mask >> mode) & 1u);   // no turn rows: the search tiers weigh the turns
-      sm.tsrc[threadIdx.x] = T;
-    }
+    if constexpr (TURN) turn_ok = !pi.w || ((g.ball_turn_mask >> mode) & 1u);   // no turn rows: the search tiers weigh the turns
     if (!fits || S.h1.y == 0u || S.h0.y == 0u || !turn_ok) {   // the search tiers take it (they run later)
       S.bound = kNone;
       b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
@@ -2336,7 +2319,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TURN ?
   __syncthreads();
   uint32_t wbase = 0, n = 0;
 #pragma unroll
-  for (int w = 0; w < kK2Items / 64; ++w) {
+  for (int w = 0; w < kK2Threads / 64; ++w) {
     const uint32_t x = sm.wsum[w];
     wbase += w < wv ? x : 0u;
     n += x;
@@ -2358,31 +2341,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TURN ?
     sm.src[threadIdx.x] = z;
     for (uint32_t j = 0; j < KB; ++j) sm.owner[rel + j] = (uint8_t)threadIdx.x;
   }
-  sm.redo[threadIdx.x] = 0;
+  if (threadIdx.x < (uint32_t)kK2Items / 32) sm.redo[threadIdx.x] = 0;
   if constexpr (TURN) {
     if (threadIdx.x < (uint32_t)kTurnDegrees) sm.tw[threadIdx.x] = g.turn_w[threadIdx.x];
-    if (threadIdx.x == 0) sm.ndef = 0u;
   }
   __syncthreads();
-  // ---- phase 2: the block's routes, two transitions per lane and step (k2_phase2_slim /
-  // k2_phase2_turn)
+  // ---- phase 2: the block's routes, one transition per lane and step (k2_phase2_slim /
+  // k2_phase2_turn1)
   const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
   const uint32_t rm = g.ball_road_mask;
-  if constexpr (TURN) {
-    if (RM_K2_TURN_STEP == 1) k2_phase2_turn1(sm, b, n, rm, dummy);
-    else k2_phase2_turn(sm, b, n, rm, dummy);
-    __syncthreads();
-    // the listed routes whose turn weight is walked (ties between the exits), one lane each
-    const uint32_t ndef = min(sm.ndef, (uint32_t)kK2Defer);
-#ifdef RM_K2_STATS
-    if (threadIdx.x == 0) atomicAdd(&b.ctl[15], sm.ndef);   // diagnostic: walked turn weights
-#endif
-    for (uint32_t zq = threadIdx.x; zq < ndef; zq += kK2Items) k2_turn_walked(g, sm, b, sm.def[zq], rm);
-  }
+  if constexpr (TURN) k2_phase2_turn1(g, sm, b, n, rm, dummy, t0i);
   if constexpr (!TURN) k2_phase2_slim(sm, b, n, rm, dummy);
   // items with a route the tables could not decide: the search tiers recompute all of its routes
   __syncthreads();
-  if (live && sm.redo[threadIdx.x] && sm.src[threadIdx.x].bound != kNone) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+  if (live && ((sm.redo[threadIdx.x >> 5] >> (threadIdx.x & 31u)) & 1u) && sm.src[threadIdx.x].bound != kNone)
+    b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
 }
 
 
@@ -5180,6 +5153,8 @@ void Workspace::release() {
   cap_points = cap_traces = cap_trans = cap_path = cap_opts = cap_segs = cap_src = cap_sort = cap_turn = 0;
   perm = loc_cursor = pcnt = nullptr;
   route_d = nullptr;
+  walk = nullptr;
+  cap_walk = 0;
   loc_key = nullptr;
 }
 
@@ -5287,7 +5262,7 @@ void Matcher::alloc_points(uint64_t cp, uint64_t ct, uint64_t co, uint64_t keep_
     w.tot_part = dalloc<unsigned long long>(L, 2 * ((cp + 255) / 256) + 2);
     w.cap_points = cp; w.cap_traces = ct; w.cap_opts = co;
     w.gsearch = nullptr;
-    w.route = nullptr; w.route_d = nullptr; w.cap_turn = 0; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
+    w.route = nullptr; w.route_d = nullptr; w.cap_turn = 0; w.walk = nullptr; w.cap_walk = 0; w.rl_routes_a = nullptr; w.rl_routes_b = nullptr; w.rl_routes_0 = nullptr; w.rl_routes_c = nullptr; w.path_pool = nullptr; w.segs = nullptr; w.reps = nullptr; w.src_item = nullptr; w.rec_slot = nullptr;
     w.cap_trans = 0; w.cap_path = 0; w.cap_segs = 0; w.cap_src = 0;
     ensure_trans_raw(std::max<uint64_t>(keep_trans, 1), std::max<uint64_t>(keep_src, 1));
     ensure_path_raw(std::max<uint64_t>(keep_path, cp / 8 + 1024));
@@ -5312,10 +5287,17 @@ void Matcher::ensure_turns() {
     Workspace& w = ws_;
     if (w.route_d && w.cap_turn >= w.cap_trans) return;
     free_one(w, w.route_d);
+    free_one(w, w.walk);
     w.route_d = nullptr;
+    w.walk = nullptr;
     w.cap_turn = 0;
+    w.cap_walk = 0;
     w.route_d = dalloc<double>(w.allocs, w.cap_trans);
     w.cap_turn = w.cap_trans;
+    // walked turn weights are ~1 % of the transitions (ties between the exits); a batch with more
+    // than an eighth hands the excess items to the search tiers
+    w.cap_walk = std::min<uint64_t>(w.cap_trans / 8 + 4096, 0xffffffffu);
+    w.walk = dalloc<uint32_t>(w.allocs, w.cap_walk);
   });
 }
 
@@ -5325,10 +5307,13 @@ void Matcher::ensure_trans_raw(uint64_t n, uint64_t n_src) {
     if (!(n <= w.cap_trans && w.route)) {
       free_one(w, w.route);
       free_one(w, w.route_d);
+      free_one(w, w.walk);
       w.route = nullptr;
       w.route_d = nullptr;
+      w.walk = nullptr;
       w.cap_trans = 0;
       w.cap_turn = 0;
+      w.cap_walk = 0;
       const uint64_t c = n + n / 4 + 1024;
       w.route = dalloc<uint32_t>(w.allocs, c);
       w.cap_trans = c;
@@ -5437,7 +5422,9 @@ static DevBatch make_view(const Workspace& w, const InputView& in, uint32_t T, u
   v.slot_trace = w.slot_trace; v.n_states = w.n_states; v.state_orig = w.state_orig; v.state_time = w.state_time;
   v.cand_n = w.cand_n; v.cand_desc = w.cand_desc; v.cand_sq = w.cand_sq;
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
-  v.route_d = nullptr;   // run_device sets it for a batch with turn costs
+  v.route_d = nullptr;   // run_device sets it (and walk) for a batch with turn costs
+  v.walk = nullptr;
+  v.walk_cap = 0;
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
@@ -5813,7 +5800,7 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   ensure_segs(Pc * kInlinePath + w.cap_path);
   DevBatch v = make_view(w, in_, T, P);
   v.route = w.route;
-  if (turn_mask_) v.route_d = w.route_d;
+  if (turn_mask_) { v.route_d = w.route_d; v.walk = w.walk; v.walk_cap = (uint32_t)w.cap_walk; }
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
   v.rl_routes_c = w.rl_routes_c;
@@ -5848,10 +5835,12 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   const bool balls = (mode_mask_ & g.ball_mask) != 0u;
   tic(kKRoutes);
   if (balls) {
-    if (v.route_d)
-      hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
-    else
-      hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
+    if (v.route_d) {
+      hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
+      hipLaunchKernelGGL(k_turn_walks, dim3(tgrid(kWalkGrid)), dim3(256), 0, st, g, v);
+    } else {
+      hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
+    }
     const uint32_t lg = (uint32_t)std::min<uint64_t>(lane_grid, kListedGrid);
     if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
     else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
@@ -5947,7 +5936,7 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   if (turn_mask_) ensure_turns();
   DevBatch v = make_view(w, in_, T, P);
   v.route = w.route;
-  if (turn_mask_) v.route_d = w.route_d;
+  if (turn_mask_) { v.route_d = w.route_d; v.walk = w.walk; v.walk_cap = (uint32_t)w.cap_walk; }
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
   v.rl_routes_c = w.rl_routes_c;
@@ -5990,8 +5979,12 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3(count_grid), dim3(256), 0, st, v);
   if (balls) {
-    if (v.route_d) hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
-    else hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Items), 0, st, g, v, kNone);
+    if (v.route_d) {
+      hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
+      hipLaunchKernelGGL(k_turn_walks, dim3(kWalkGrid), dim3(256), 0, st, g, v);
+    } else {
+      hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
+    }
     const uint32_t lg = std::min<uint32_t>(lane_grid, sgrid(kListedGrid, 1, 256));
     if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
     else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
@@ -6136,6 +6129,8 @@ void Matcher::run_device(const RunParams& rp) {
   if (turn_mask_) {   // the transitions' distance terms with turn costs (rule 3b), read by K3
     ensure_turns();
     v.route_d = w.route_d;
+    v.walk = w.walk;
+    v.walk_cap = (uint32_t)w.cap_walk;
   }
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a;
@@ -6149,11 +6144,12 @@ void Matcher::run_device(const RunParams& rp) {
   tic(kKRoutes);
   hipLaunchKernelGGL(k_src_items, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, v);
   if (n_src && balls) {
-    if (v.route_d)
-      hipLaunchKernelGGL(k_routes_ball2<true>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
+    if (v.route_d) {
+      hipLaunchKernelGGL(k_routes_ball2<true>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Threads), 0, st,
                          g, v, (uint32_t)n_src);
-    else
-      hipLaunchKernelGGL(k_routes_ball2<false>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Items), 0, st,
+      hipLaunchKernelGGL(k_turn_walks, dim3(kWalkGrid), dim3(256), 0, st, g, v);
+    } else
+      hipLaunchKernelGGL(k_routes_ball2<false>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Threads), 0, st,
                          g, v, (uint32_t)n_src);
     if (v.route_d)
       hipLaunchKernelGGL(k_routes_lane<true>, dim3((uint32_t)std::min<uint64_t>((n_src + 255) / 256, kListedGrid)), dim3(256),

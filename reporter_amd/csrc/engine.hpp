@@ -144,6 +144,8 @@ struct Workspace {
   uint32_t* trans_cnt = nullptr; uint32_t* trans_off = nullptr; double* gc = nullptr; uint32_t* route = nullptr;
   double* route_d = nullptr;   // per transition: turn_m + |route_m - gc| (rule 3b), batches with turn costs only
   uint64_t cap_turn = 0;
+  uint32_t* walk = nullptr;    // K2 -> k_turn_walks: transitions whose turn weight is walked (item << 4 | target)
+  uint64_t cap_walk = 0;
   uint4* pair_info = nullptr;  // per layer pair slot: {route bound cm, time bound ms, KA | KB << 8 | mode << 16, 0}
   uint32_t* src_cnt = nullptr; uint32_t* src_off = nullptr; uint32_t* src_item = nullptr;
   int8_t* choice = nullptr; uint8_t* chain_start = nullptr; uint8_t* bp = nullptr;
