@@ -64,7 +64,7 @@ struct DevBatch {  // POD view of the workspace for kernels
   // per transition with turn costs (rule 3b): the distance term K3 adds, turn_m + |route_m - gc| in
   // metres (+inf for an invalid route); null when no trace of the batch has turn costs
   double* route_d;
-  uint32_t* walk; uint32_t walk_cap;   // turn weights K2 leaves to k_turn_walks (count ctl[15])
+  uint32_t* walk;   // turn weights K2 leaves to k_turn_walks: per K2 block a count and its entries
   uint32_t* src_cnt; uint32_t* src_off; uint32_t* src_item;  // (pair, source) work items of K2
   int8_t* choice; uint8_t* chain_start; uint8_t* bp;
   uint32_t* path_off; uint32_t* path_cnt; uint32_t* path_inline; uint32_t* path_pool; uint64_t path_cap; uint32_t* route_dist;
@@ -522,7 +522,21 @@ __device__ __forceinline__ void put_cand(const DevGraph& g, const DevBatch& b, u
 #define RM_K1_ROWS 4
 #endif
 constexpr int kK1Rows = RM_K1_ROWS;   // grid rows whose items K1 walks as one sequence
-__global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b) {
+#ifndef RM_K1_BATCH
+#define RM_K1_BATCH 4
+#endif
+constexpr int kK1Batch = RM_K1_BATCH;  // cell records loaded together per lane
+// per-road minima the lane tier keeps in registers; a state with more roads inside its radius goes
+// to the wave tier (its LDS hash holds any number; the same candidates either way)
+#ifndef RM_K1_SLOTS
+#define RM_K1_SLOTS 16
+#endif
+constexpr int kK1Slots = RM_K1_SLOTS;
+static_assert(kK1Slots % 4 == 0 && kK1Slots <= kMaxCand, "K1 slots");
+#ifndef RM_K1_WPE
+#define RM_K1_WPE 1
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_K1_WPE))) k_candidates_lane(DevGraph g, DevBatch b) {
   uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b.perm) {   // locality order: each XCD walks one contiguous range of the sorted states
     const uint64_t r = (uint64_t)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
@@ -548,8 +562,8 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
   const double fx1 = floor(((double)(lon + qlon) - g.lon0) / g.dlon);
   const double fy0 = floor(((double)(lat - qlat) - g.lat0) / g.dlat);
   const double fy1 = floor(((double)(lat + qlat) - g.lat0) / g.dlat);
-  uint32_t rroad[kMaxCand], rs[kMaxCand];
-  unsigned long long rbest[kMaxCand];
+  uint32_t rroad[kK1Slots], rs[kK1Slots];
+  unsigned long long rbest[kK1Slots];
   uint32_t n = 0;
   bool ovf = false;
   if (!(fx1 < 0 || fy1 < 0 || fx0 > (double)(g.ncx - 1) || fy0 > (double)(g.ncy - 1))) {
@@ -577,10 +591,10 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
         tot += (uint32_t)r < nrow ? re[r] - ra[r] : 0u;
         end[r] = tot;
       }
-      for (uint32_t q0 = 0; q0 < tot && !ovf; q0 += 4) {
-        uint4 r0[4], r1[4];
+      for (uint32_t q0 = 0; q0 < tot && !ovf; q0 += kK1Batch) {
+        uint4 r0[kK1Batch], r1[kK1Batch];
 #pragma unroll
-        for (int y = 0; y < 4; ++y) {
+        for (int y = 0; y < kK1Batch; ++y) {
           const uint32_t q = min(q0 + (uint32_t)y, tot - 1u);
           uint32_t bq = base[0];
 #pragma unroll
@@ -591,7 +605,7 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
           r1[y] = g.cell_rec[2 * it + 1];
         }
 #pragma unroll
-        for (int y = 0; y < 4; ++y) {
+        for (int y = 0; y < kK1Batch; ++y) {
           if (q0 + y >= tot || ovf) break;
           if (!((r1[y].z >> 29) & acc)) continue;
           const float ax = (as_f(r0[y].x) - lon) * mlon, ay = (as_f(r0[y].y) - lat) * mlat;
@@ -604,7 +618,7 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
           const unsigned long long key = ((unsigned long long)__float_as_uint(sq) << 32) | r1[y].w;
           bool found = false;
 #pragma unroll
-          for (int x = 0; x < kMaxCand; ++x) {
+          for (int x = 0; x < kK1Slots; ++x) {
             if (K1_UNIFORM_STOP(x < (int)n)) break;   // no active lane holds slot x yet
             if (x < (int)n && rroad[x] == road) {
               found = true;
@@ -612,9 +626,9 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
             }
           }
           if (found) continue;
-          if (n >= (uint32_t)kMaxCand) { ovf = true; break; }
+          if (n >= (uint32_t)kK1Slots) { ovf = true; break; }
 #pragma unroll
-          for (int x = 0; x < kMaxCand; ++x) {
+          for (int x = 0; x < kK1Slots; ++x) {
             if (K1_UNIFORM_STOP(x <= (int)n)) break;
             if (x == (int)n) { rroad[x] = road; rbest[x] = key; rs[x] = sc; }
           }
@@ -632,7 +646,7 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
   // have all arrived (a store between two loads would serialise them: shared vmcnt)
   const uint32_t cacc = mode_access(op.mode);
 #pragma unroll
-  for (int x0 = 0; x0 < kMaxCand; x0 += 4) {
+  for (int x0 = 0; x0 < kK1Slots; x0 += 4) {
     if (K1_UNIFORM_STOP(x0 < (int)n)) break;
     if (x0 >= (int)n) break;
     uint4 ra[4], rc[4];
@@ -651,7 +665,7 @@ __global__ void __launch_bounds__(256) k_candidates_lane(DevGraph g, DevBatch b)
       const unsigned long long kx = ((unsigned long long)sqb << 32) | rroad[x];
       uint32_t rank = 0;
 #pragma unroll
-      for (int z = 0; z < kMaxCand; ++z) {
+      for (int z = 0; z < kK1Slots; ++z) {
         if (K1_UNIFORM_STOP(z < (int)n)) break;
         if (z >= (int)n) continue;
         rank += ((((rbest[z] >> 32) << 32) | rroad[z]) < kx) ? 1u : 0u;
@@ -1768,6 +1782,12 @@ struct K2SrcS {
   uint32_t s, bound, tmax, lim;
 };
 static_assert(sizeof(K2SrcS) == 60, "K2SrcS is 60 bytes");
+// walked turn weights (ties between the exits) a K2 block lists for k_turn_walks: each goes to the
+// block's own region of b.walk (an LDS counter, the count written first at the block's end; no
+// global atomics: 639 k appends per C2 step to one counter took K2 with turn costs from 1.5 to 3.1
+// ms); past kWalkPerBlock they are marked in place for k_turn_walks_marked
+constexpr uint32_t kWalkPerBlock = 512;
+constexpr uint32_t kRouteWalk = 0xfffffffeu;   // (a route left to k_turn_walks_marked)
 template <bool TURN>
 struct K2Smem {
   K2SrcS src[kK2Items];
@@ -1776,7 +1796,8 @@ struct K2Smem {
   uint8_t owner[kK2Items * kMaxCand];   // transition of the block -> item of the block
   uint32_t wsum[kK2Threads / 64];
   uint32_t redo[kK2Items / 32];         // bit o: a route of item o was not exact from the tables
-  uint32_t tw[TURN ? kTurnDegrees : 1];  // the turn weights (DevGraph::turn_w) in LDS
+  uint16_t tw16[TURN ? kTurnDegrees + 1 : 2];  // the turn weights (DevGraph::turn_w; k2_turn_weight)
+  uint32_t wn;                            // (with turn costs) the block's walked turn weights
 };
 // (both records fit 20 KB per block with turn costs too: 8 blocks per CU)
 template <class SM>
@@ -2113,12 +2134,14 @@ __device__ __forceinline__ K2TurnKey k2_turn_key(const K2SrcS& S, unsigned long 
 }
 // the turn weight U from the winner's turn row (wx, wy: its node0 / node1 words), or kNone when
 // it must be walked (a tie, or a row without its sum)
+// (tw16: the turn weights in 16 bits, the U-turn's 65536 stored as 0 -- K2's LDS budget)
 __device__ __forceinline__ uint32_t k2_turn_weight(const K2TurnKey& k, uint32_t hw, uint32_t wx, uint32_t wy,
-                                                   const uint32_t* tw) {
+                                                   const uint16_t* tw16) {
   if (k.need == 0u) return 0u;
   const uint32_t w = k.side ? wy : wx;
   if (k.need == 2u || (w & kTurnTMask) == kTurnNone) return kNone;
-  return tw[turn_degree(head_back(hw, k.e1 ? 0u : 1u), w >> kTurnHeadShift)] + (w & kTurnTMask);
+  const uint32_t d = turn_degree(head_back(hw, k.e1 ? 0u : 1u), w >> kTurnHeadShift);
+  return (d == 0u ? 65536u : (uint32_t)tw16[d]) + (w & kTurnTMask);
 }
 
 // phase 2 with turn costs (round 6): one transition per lane and step, with both exits' turn rows
@@ -2164,7 +2187,7 @@ __device__ __forceinline__ void k2_phase2_turn1(const DevGraph& g, SM& sm, const
     const K2TurnKey k = k2_turn_key(A, ak1, ak0, fac, ta0, make_uint4(0u, 0u, ta1.x, ta1.y), r1, r0, s1, s0);
     k2_v2 w = k.e1 ? v1 : v0;
     if (k.need == 1u && (k.e1 ? s1 != h1s : s0 != h0s)) w = tra[k.row];   // resolved past a collision
-    const uint32_t U = k2_turn_weight(k, hw, w.x, w.y, sm.tw);
+    const uint32_t U = k2_turn_weight(k, hw, w.x, w.y, sm.tw16);
     if (!la) continue;
     if (U != kNone) {
       b.route[A.obase + q] = k.r;
@@ -2172,73 +2195,104 @@ __device__ __forceinline__ void k2_phase2_turn1(const DevGraph& g, SM& sm, const
       if (!k.exact) k2_redo(sm, o);
     } else {   // walked by k_turn_walks (item << 4 | target); a full list: the search tiers take the item
       const uint32_t item = t0i + o;
-      const uint32_t x = atomicAdd(&b.ctl[15], 1u);
-      if (x < b.walk_cap && item < (1u << 28)) b.walk[x] = item << 4 | (di & 15u);
-      else k2_redo(sm, o);
+      const uint32_t x = atomicAdd(&sm.wn, 1u);
+      if (x < kWalkPerBlock && item < (1u << 28)) {
+        b.walk[(uint64_t)blockIdx.x * (kWalkPerBlock + 1) + 1 + x] = item << 4 | (di & 15u);
+      } else {   // marked in place for k_turn_walks_marked
+        b.route[A.obase + q] = kRouteWalk;
+        b.route_d[A.obase + q] = __longlong_as_double((long long)((unsigned long long)item << 4 | (di & 15u)));
+        b.ctl[15] = 1u;
+      }
     }
   }
 }
 
-// The turn weights K2 left to walk (b.walk, count ctl[15]), one lane each: the item again as
+// The turn weights K2 left to walk (each K2 block's region of b.walk), one lane each: the item again as
 // k_routes_ball2's phase 1 forms it, the route with both exits' turn rows at their first-probe
 // slots, and the walk through the tables (k2_route_turn / ball_turn_walk).  A route the tables
 // cannot decide hands its item to the search tiers, which run next.
-constexpr uint32_t kWalkGrid = 2048;   // k_turn_walks: grid-stride over the device-side count
-__global__ void __launch_bounds__(256) k_turn_walks(DevGraph g, DevBatch b) {
-  if (steady_abort(b)) return;
-  const uint32_t nw = min(b.ctl[15], b.walk_cap);
+// one walked turn weight: item t's route to its pair's target j (ro: its route index, known to the
+// marker scan; kNone: from the item)
+__device__ void k2_walk_one(const DevGraph& g, const DevBatch& b, uint32_t t, uint32_t j) {
   const uint32_t rm = g.ball_road_mask;
   const k2_gptr dummy = (k2_gptr)(const void*)b.cand_desc;
   const k2_trow tdummy = (k2_trow)(const void*)b.cand_desc;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < nw; e += gridDim.x * blockDim.x) {
-    const uint32_t wv = b.walk[e], t = wv >> 4, j = wv & 15u;
-    const uint32_t p = b.src_item[t];
-    const uint4 pi = b.pair_info[p];
-    const uint32_t i = t - b.src_off[p];
-    const uint32_t KB = (pi.z >> 8) & 0xffu;
-    const uint64_t ro = (uint64_t)b.trans_off[p] + i * KB + j;
-    const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
-    const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
-    const int mode = (int)(pi.z >> 16);
-    K2Src A;
-    exit_keys(a0, pi.x, A.rk1, A.rk0);
-    A.lim = ball_exact_limit(pi.x, g.ball_radius[mode], A.rk1, A.rk0);
-    const uint2* hp = g.ball_hdr[mode];
-    A.h1 = A.rk1 != kKeyInf ? hp[a1.y] : make_uint2(0u, 1u);
-    A.h0 = A.rk0 != kKeyInf ? hp[a1.x] : make_uint2(0u, 1u);
-    A.ent = (unsigned long long)(uintptr_t)g.ball_ent[mode];
-    A.road = a0.x;
-    A.s = a0.y;
-    A.bound = pi.x;
-    A.tmax = pi.y;
-    K2Turn T;
-    T.fac = pi.w;
-    T.trn = (unsigned long long)(uintptr_t)g.ball_turn[mode];
-    T.hw = g.road_head[a0.x];
-    T.n0 = a1.x;
-    T.n1 = a1.y;
-    T.mode = (uint32_t)mode;
-    T.pad = 0u;
-    const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * ((uint64_t)p * kMaxCand + j));
-    const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1);
-    const double gc = b.gc[p];
-    const bool ua = ta0.w != 0u;
-    const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
-    const uint32_t h1s = ball_slot(ta0.x, A.h1.y), h0s = ball_slot(ta0.x, A.h0.y);
-    const uint64_t i1 = ball_row0(A.h1.x) + h1s, i0 = ball_row0(A.h0.x) + h0s;
-    const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)A.ent;
-    const k2_trow tra = (k2_trow)(const void*)(uintptr_t)T.trn;
-    const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
-    const k2_v2 v1 = *(ua1 && T.fac ? tra + i1 : tdummy), v0 = *(ua0 && T.fac ? tra + i0 : tdummy);
-    uint32_t s1 = h1s, s0 = h0s;
-    const uint4 r1 = ball_resolve_at_g(ea, A.h1, ta0.x, k2_row_or_none(ua1, la1), rm, s1);
-    const uint4 r0 = ball_resolve_at_g(ea, A.h0, ta0.x, k2_row_or_none(ua0, la0), rm, s0);
-    bool ok = true;
-    double d = 0.0;
-    b.route[ro] = k2_route_turn(g, A, T, ta0, ta1, r1, r0, s1, s0, h1s, h0s, make_uint2(v1.x, v1.y),
-                                make_uint2(v0.x, v0.y), g.turn_w, gc, ok, d);
-    b.route_d[ro] = d;
-    if (!ok) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+  const uint32_t p = b.src_item[t];
+  const uint4 pi = b.pair_info[p];
+  const uint32_t i = t - b.src_off[p];
+  const uint32_t KB = (pi.z >> 8) & 0xffu;
+  const uint64_t ro = (uint64_t)b.trans_off[p] + i * KB + j;
+  const uint64_t arow = ((uint64_t)(p - 1) * kMaxCand + i) * 2;
+  const uint4 a0 = b.cand_desc[arow], a1 = b.cand_desc[arow + 1];
+  const int mode = (int)(pi.z >> 16);
+  K2Src A;
+  exit_keys(a0, pi.x, A.rk1, A.rk0);
+  A.lim = ball_exact_limit(pi.x, g.ball_radius[mode], A.rk1, A.rk0);
+  const uint2* hp = g.ball_hdr[mode];
+  A.h1 = A.rk1 != kKeyInf ? hp[a1.y] : make_uint2(0u, 1u);
+  A.h0 = A.rk0 != kKeyInf ? hp[a1.x] : make_uint2(0u, 1u);
+  A.ent = (unsigned long long)(uintptr_t)g.ball_ent[mode];
+  A.road = a0.x;
+  A.s = a0.y;
+  A.bound = pi.x;
+  A.tmax = pi.y;
+  K2Turn T;
+  T.fac = pi.w;
+  T.trn = (unsigned long long)(uintptr_t)g.ball_turn[mode];
+  T.hw = g.road_head[a0.x];
+  T.n0 = a1.x;
+  T.n1 = a1.y;
+  T.mode = (uint32_t)mode;
+  T.pad = 0u;
+  const k2_gptr da = (k2_gptr)(const void*)(b.cand_desc + 2 * ((uint64_t)p * kMaxCand + j));
+  const uint4 ta0 = k2_ld(da), ta1 = k2_ld(da + 1);
+  const double gc = b.gc[p];
+  const bool ua = ta0.w != 0u;
+  const bool ua1 = ua && A.rk1 != kKeyInf, ua0 = ua && A.rk0 != kKeyInf;
+  const uint32_t h1s = ball_slot(ta0.x, A.h1.y), h0s = ball_slot(ta0.x, A.h0.y);
+  const uint64_t i1 = ball_row0(A.h1.x) + h1s, i0 = ball_row0(A.h0.x) + h0s;
+  const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)A.ent;
+  const k2_trow tra = (k2_trow)(const void*)(uintptr_t)T.trn;
+  const uint4 la1 = k2_ld(ua1 ? ea + i1 : dummy), la0 = k2_ld(ua0 ? ea + i0 : dummy);
+  const k2_v2 v1 = *(ua1 && T.fac ? tra + i1 : tdummy), v0 = *(ua0 && T.fac ? tra + i0 : tdummy);
+  uint32_t s1 = h1s, s0 = h0s;
+  const uint4 r1 = ball_resolve_at_g(ea, A.h1, ta0.x, k2_row_or_none(ua1, la1), rm, s1);
+  const uint4 r0 = ball_resolve_at_g(ea, A.h0, ta0.x, k2_row_or_none(ua0, la0), rm, s0);
+  bool ok = true;
+  double d = 0.0;
+  b.route[ro] = k2_route_turn(g, A, T, ta0, ta1, r1, r0, s1, s0, h1s, h0s, make_uint2(v1.x, v1.y),
+                              make_uint2(v0.x, v0.y), g.turn_w, gc, ok, d);
+  b.route_d[ro] = d;
+  if (!ok) b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+}
+// (launched with K2's grid and n_arg, one block per K2 block: the block's region of b.walk)
+#ifndef RM_WALK_THREADS
+#define RM_WALK_THREADS 256
+#endif
+constexpr uint32_t kWalkThreads = RM_WALK_THREADS;
+__global__ void __launch_bounds__(kWalkThreads) k_turn_walks(DevGraph g, DevBatch b, uint32_t n_arg) {
+  if (steady_abort(b)) return;
+  const uint32_t n_items = n_arg != kNone ? n_arg : (uint32_t)b.tot[1];
+  const uint32_t nblk = (uint32_t)(((uint64_t)n_items + kK2Items - 1) / kK2Items);
+  if (blockIdx.x >= nblk) return;
+  const uint32_t* reg = b.walk + (uint64_t)blockIdx.x * (kWalkPerBlock + 1);
+  const uint32_t nw = reg[0];
+  for (uint32_t e = threadIdx.x; e < nw; e += blockDim.x) {
+    const uint32_t wv = reg[1 + e];
+    k2_walk_one(g, b, wv >> 4, wv & 15u);
+  }
+}
+constexpr uint32_t kWalkScanGrid = 2048;
+// the walks a K2 block could not list (more than kWalkPerBlock): marked in place -- route
+// kRouteWalk, route_d's bits the item and target -- and found by one scan of the routes, run only
+// when some block overflowed (ctl[15])
+__global__ void __launch_bounds__(256) k_turn_walks_marked(DevGraph g, DevBatch b) {
+  if (steady_abort(b) || b.ctl[15] == 0u) return;
+  const uint64_t n = b.tot[0];
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (uint64_t)gridDim.x * blockDim.x) {
+    if (b.route[x] != kRouteWalk) continue;
+    const unsigned long long wv = (unsigned long long)__double_as_longlong(b.route_d[x]);
+    k2_walk_one(g, b, (uint32_t)(wv >> 4), (uint32_t)(wv & 15u));
   }
 }
 
@@ -2343,7 +2397,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TURN ?
   }
   if (threadIdx.x < (uint32_t)kK2Items / 32) sm.redo[threadIdx.x] = 0;
   if constexpr (TURN) {
-    if (threadIdx.x < (uint32_t)kTurnDegrees) sm.tw[threadIdx.x] = g.turn_w[threadIdx.x];
+    if (threadIdx.x < (uint32_t)kTurnDegrees) sm.tw16[threadIdx.x] = (uint16_t)g.turn_w[threadIdx.x];   // (65536 -> 0)
+    if (threadIdx.x == 0) sm.wn = 0u;
   }
   __syncthreads();
   // ---- phase 2: the block's routes, one transition per lane and step (k2_phase2_slim /
@@ -2356,6 +2411,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TURN ?
   __syncthreads();
   if (live && ((sm.redo[threadIdx.x >> 5] >> (threadIdx.x & 31u)) & 1u) && sm.src[threadIdx.x].bound != kNone)
     b.rl_routes_0[atomicAdd(&b.ctl[1], 1u)] = t;
+  if constexpr (TURN) {   // the count of the block's region of b.walk
+    if (threadIdx.x == 0) b.walk[(uint64_t)blockIdx.x * (kWalkPerBlock + 1)] = min(sm.wn, kWalkPerBlock);
+  }
 }
 
 
@@ -2637,7 +2695,10 @@ __device__ void path_walk_ball(const DevGraph& g, const DevBatch& b, uint64_t p,
 
 // path ball tier: one lane per chosen transition whose bound fits the ball radius; the
 // others go to the search tiers (rl_routes_0 reused after K2, count ctl[8])
-__global__ void __launch_bounds__(256) k_paths_ball(DevGraph g, DevBatch b) {
+#ifndef RM_PATHS_WPE
+#define RM_PATHS_WPE 1
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RM_PATHS_WPE))) k_paths_ball(DevGraph g, DevBatch b) {
   if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b.perm_paths) {   // locality order: the pair whose source state is the r-th sorted state
@@ -5285,7 +5346,8 @@ void Matcher::ensure_segs(uint64_t n) { grow_workspace([&] { ensure_segs_raw(n);
 void Matcher::ensure_turns() {
   grow_workspace([&] {
     Workspace& w = ws_;
-    if (w.route_d && w.cap_turn >= w.cap_trans) return;
+    const uint64_t want_walk = (w.cap_src / kK2Items + 2) * (kWalkPerBlock + 1);
+    if (w.route_d && w.cap_turn >= w.cap_trans && w.cap_walk >= want_walk) return;
     free_one(w, w.route_d);
     free_one(w, w.walk);
     w.route_d = nullptr;
@@ -5294,9 +5356,8 @@ void Matcher::ensure_turns() {
     w.cap_walk = 0;
     w.route_d = dalloc<double>(w.allocs, w.cap_trans);
     w.cap_turn = w.cap_trans;
-    // walked turn weights are ~1 % of the transitions (ties between the exits); a batch with more
-    // than an eighth hands the excess items to the search tiers
-    w.cap_walk = std::min<uint64_t>(w.cap_trans / 8 + 4096, 0xffffffffu);
+    // one region per K2 block of the item pool: a count and kWalkPerBlock entries
+    w.cap_walk = want_walk;
     w.walk = dalloc<uint32_t>(w.allocs, w.cap_walk);
   });
 }
@@ -5424,7 +5485,6 @@ static DevBatch make_view(const Workspace& w, const InputView& in, uint32_t T, u
   v.trans_cnt = w.trans_cnt; v.trans_off = w.trans_off; v.gc = w.gc; v.route = w.route; v.pair_info = w.pair_info;
   v.route_d = nullptr;   // run_device sets it (and walk) for a batch with turn costs
   v.walk = nullptr;
-  v.walk_cap = 0;
   v.src_cnt = w.src_cnt; v.src_off = w.src_off; v.src_item = w.src_item;
   v.choice = w.choice; v.chain_start = w.chain_start; v.bp = w.bp;
   v.path_off = w.path_off; v.path_cnt = w.path_cnt; v.path_inline = w.path_inline;
@@ -5800,7 +5860,7 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   ensure_segs(Pc * kInlinePath + w.cap_path);
   DevBatch v = make_view(w, in_, T, P);
   v.route = w.route;
-  if (turn_mask_) { v.route_d = w.route_d; v.walk = w.walk; v.walk_cap = (uint32_t)w.cap_walk; }
+  if (turn_mask_) { v.route_d = w.route_d; v.walk = w.walk; }
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
   v.rl_routes_c = w.rl_routes_c;
@@ -5837,7 +5897,8 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   if (balls) {
     if (v.route_d) {
       hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
-      hipLaunchKernelGGL(k_turn_walks, dim3(tgrid(kWalkGrid)), dim3(256), 0, st, g, v);
+      hipLaunchKernelGGL(k_turn_walks, dim3(item_grid), dim3(kWalkThreads), 0, st, g, v, kNone);
+      hipLaunchKernelGGL(k_turn_walks_marked, dim3(kWalkScanGrid), dim3(256), 0, st, g, v);
     } else {
       hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
     }
@@ -5936,7 +5997,7 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   if (turn_mask_) ensure_turns();
   DevBatch v = make_view(w, in_, T, P);
   v.route = w.route;
-  if (turn_mask_) { v.route_d = w.route_d; v.walk = w.walk; v.walk_cap = (uint32_t)w.cap_walk; }
+  if (turn_mask_) { v.route_d = w.route_d; v.walk = w.walk; }
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a; v.rl_routes_b = w.rl_routes_b; v.rl_routes_0 = w.rl_routes_0;
   v.rl_routes_c = w.rl_routes_c;
@@ -5981,7 +6042,8 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
   if (balls) {
     if (v.route_d) {
       hipLaunchKernelGGL(k_routes_ball2<true>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
-      hipLaunchKernelGGL(k_turn_walks, dim3(kWalkGrid), dim3(256), 0, st, g, v);
+      hipLaunchKernelGGL(k_turn_walks, dim3(item_grid), dim3(kWalkThreads), 0, st, g, v, kNone);
+      hipLaunchKernelGGL(k_turn_walks_marked, dim3(kWalkScanGrid), dim3(256), 0, st, g, v);
     } else {
       hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
     }
@@ -6130,7 +6192,6 @@ void Matcher::run_device(const RunParams& rp) {
     ensure_turns();
     v.route_d = w.route_d;
     v.walk = w.walk;
-    v.walk_cap = (uint32_t)w.cap_walk;
   }
   v.src_item = w.src_item;
   v.rl_routes_a = w.rl_routes_a;
@@ -6147,7 +6208,9 @@ void Matcher::run_device(const RunParams& rp) {
     if (v.route_d) {
       hipLaunchKernelGGL(k_routes_ball2<true>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Threads), 0, st,
                          g, v, (uint32_t)n_src);
-      hipLaunchKernelGGL(k_turn_walks, dim3(kWalkGrid), dim3(256), 0, st, g, v);
+      hipLaunchKernelGGL(k_turn_walks, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kWalkThreads), 0, st, g, v,
+                         (uint32_t)n_src);
+      hipLaunchKernelGGL(k_turn_walks_marked, dim3(kWalkScanGrid), dim3(256), 0, st, g, v);
     } else
       hipLaunchKernelGGL(k_routes_ball2<false>, dim3((uint32_t)((n_src + kK2Items - 1) / kK2Items)), dim3(kK2Threads), 0, st,
                          g, v, (uint32_t)n_src);
