@@ -118,9 +118,11 @@ def routes_targets_algorithmic_bytes(c):
 
 def routes_ball_algorithmic_bytes(c):
     """K2 algorithmic bytes of the route-ball formulation: 16 B table row per
-    (source exit, target) probe, 32 B descriptor per candidate read (KA sources + KB targets
-    per layer pair), 16 B per source for its two exits' table headers, 4 B per route write."""
-    return 16 * c["ball_rows"] + 32 * c["desc_reads"] + 16 * c["searches"] + 4 * c["route_writes"]
+    (source exit, target) probe, per layer pair a 32 B descriptor per source (KA = the searches)
+    and 24 B per target (KB: road, offset, length, speeds + the two entry times; round 6 reads no
+    more of it), 16 B per source for its two exits' table headers, 4 B per route write."""
+    targets = c["desc_reads"] - c["searches"]
+    return 16 * c["ball_rows"] + 32 * c["searches"] + 24 * targets + 16 * c["searches"] + 4 * c["route_writes"]
 
 
 def routes_ball_turn_algorithmic_bytes(c):

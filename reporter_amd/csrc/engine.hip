@@ -2267,7 +2267,7 @@ __device__ void k2_walk_one(const DevGraph& g, const DevBatch& b, uint32_t t, ui
 }
 // (launched with K2's grid and n_arg, one block per K2 block: the block's region of b.walk)
 #ifndef RM_WALK_THREADS
-#define RM_WALK_THREADS 256
+#define RM_WALK_THREADS 64
 #endif
 constexpr uint32_t kWalkThreads = RM_WALK_THREADS;
 __global__ void __launch_bounds__(kWalkThreads) k_turn_walks(DevGraph g, DevBatch b, uint32_t n_arg) {
