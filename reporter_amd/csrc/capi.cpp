@@ -238,6 +238,10 @@ class Coalescer {
     static const bool on = [] { const char* e = std::getenv("RM_COALESCE_FORMAT"); return !(e && std::strcmp(e, "dispatcher") == 0); }();
     return on;
   }
+  static double trace_ms() {   // RM_COALESCE_TRACE=<ms>: a batch slower than that is printed to stderr
+    static const double v = [] { const char* e = std::getenv("RM_COALESCE_TRACE"); return e && *e ? std::strtod(e, nullptr) : 0.0; }();
+    return v;
+  }
   static bool inline_ok() {   // RM_COALESCE_INLINE=0: every request queues (A/B)
     static const bool on = [] { const char* e = std::getenv("RM_COALESCE_INLINE"); return !(e && *e == '0'); }();
     return on;
@@ -423,6 +427,9 @@ void Coalescer::loop() {
     }
     double tm[4] = {0, 0, 0, 0};
     serve_batch(m, eng_.get(), batch, tm, fmt_callers());   // out / err (or segs) of each request, not under the lock
+    if (trace_ms() > 0 && tm[0] + tm[1] + tm[2] + tm[3] > trace_ms())
+      std::fprintf(stderr, "coalesce: batch of %zu requests: staging %.3f engine %.3f download %.3f format %.3f ms\n",
+                   batch.size(), tm[0], tm[1], tm[2], tm[3]);
     {
       std::lock_guard<std::mutex> lk(mu_);
       --busy_;

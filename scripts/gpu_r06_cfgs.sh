@@ -6,7 +6,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 if [ "$1" = pmc ]; then
-  for ct in ${CFGS:-"C3:125000 C4:125000 CITY30:100000"}; do
+  for ct in ${CFGS:-C3:125000 C4:125000 CITY30:100000}; do
     c=${ct%%:*}; t=${ct##*:}; lc=$(echo $c | tr A-Z a-z)
     bash scripts/gpu_pmc_cfg.sh $c $t r06_$lc || exit 1
   done
