@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <sys/resource.h>
 #include <cctype>
 #include <chrono>
 #include <cmath>
@@ -147,7 +148,10 @@ struct MatchRequest {
   std::vector<SegmentRec> segs;
   bool raw = false;
   bool done = false;
-  std::condition_variable cv;   // its caller waits here alone (no herd wake-up per batch)
+  // its caller waits here alone, on the request's own mutex: a batch's callers wake without
+  // queueing on the coalescer's lock (at 256 clients that convoy cost ~0.1 ms of CPU per request)
+  std::mutex mu;
+  std::condition_variable cv;
 };
 
 void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<MatchRequest*>& batch, double* tm,
@@ -208,7 +212,7 @@ class Coalescer {
     }
     cv_req_.notify_one();
     {
-      std::unique_lock<std::mutex> lk(mu_);
+      std::unique_lock<std::mutex> lk(r.mu);
       r.cv.wait(lk, [&] { return r.done; });
     }
     if (!r.err.empty()) throw std::runtime_error(r.err);
@@ -288,6 +292,17 @@ struct HostStaging {
   ~HostStaging() { release(); }
 };
 
+// pageable staging of a small batch's arrays (grow-only, geometric)
+struct PageableStaging {
+  std::vector<float> lon, lat, acc;
+  std::vector<double> time;
+  void ensure(size_t n) {
+    if (n <= lon.size()) return;
+    const size_t c = std::max<size_t>(n, 2 * lon.size()) + 1024;
+    lon.resize(c); lat.resize(c); acc.resize(c); time.resize(c);
+  }
+};
+
 // run a list of parsed traces as one batch on matcher m; per-trace JSON replies, and per-trace
 // error messages (non-empty = that trace failed alone; its reply is empty)
 // fn(i) for i in [0, n) over the host pool (up to 16 threads) in contiguous chunks (the JSON
@@ -321,21 +336,36 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
   std::vector<MatchOptions> opts(n);
   for (size_t i = 0; i < n; ++i) { off[i + 1] = off[i] + (uint32_t)pt[i]->pts.size(); opts[i] = pt[i]->opt; topt[i] = (uint32_t)i; }
   const uint64_t P = off[n];
-  // the dispatcher thread's pinned staging (grow-only): the batch's uploads run as DMA instead of
-  // staged pageable copies, which cost a small coalesced batch more than its kernels
-  static thread_local HostStaging staging;
-  HostStaging& hs = staging;   // the pool threads below must see this thread's instance
-  hs.ensure(P);
-  parallel_for(n, [&](size_t i) {
+  // a large batch goes up from this thread's pinned staging (grow-only): its uploads run as DMA
+  // instead of staged pageable copies.  A small one (a coalesced service batch) is packed into the
+  // matcher's own pinned block by Matcher::run, so it stages in pageable memory here: no pinned
+  // allocation on a caller's thread (the inline path) and none freed when that thread exits --
+  // pinning maps and unmaps pages under the process's memory lock, which stalled every other
+  // thread of a 256-client service for tens of milliseconds (p99 60-80 ms).
+  constexpr uint64_t kPinnedStagingMin = 65536;   // Matcher::run's small-run limit (RM_SMALL_BATCH_POINTS)
+  float *lon, *lat, *acc;
+  double* time;
+  if (P > kPinnedStagingMin) {
+    static thread_local HostStaging staging;
+    staging.ensure(P);
+    lon = staging.lon; lat = staging.lat; acc = staging.acc; time = staging.time;
+  } else {
+    static thread_local PageableStaging staging;
+    staging.ensure(P);
+    lon = staging.lon.data(); lat = staging.lat.data(); acc = staging.acc.data(); time = staging.time.data();
+  }
+  auto stage = [&](size_t i) {
     const tj::PointSink& q = pt[i]->pts;
-    std::copy(q.lon.begin(), q.lon.end(), hs.lon + off[i]);
-    std::copy(q.lat.begin(), q.lat.end(), hs.lat + off[i]);
-    std::copy(q.acc.begin(), q.acc.end(), hs.acc + off[i]);
-    std::copy(q.time.begin(), q.time.end(), hs.time + off[i]);
-  });
+    std::copy(q.lon.begin(), q.lon.end(), lon + off[i]);
+    std::copy(q.lat.begin(), q.lat.end(), lat + off[i]);
+    std::copy(q.acc.begin(), q.acc.end(), acc + off[i]);
+    std::copy(q.time.begin(), q.time.end(), time + off[i]);
+  };
+  if (P > kPinnedStagingMin) parallel_for(n, stage);   // (a small batch copies in microseconds: no pool hand-off)
+  else for (size_t i = 0; i < n; ++i) stage(i);
   HostBatch hb;
-  hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = hs.lon; hb.lat = hs.lat;
-  hb.time = hs.time; hb.accuracy = hs.acc; hb.n_opts = (uint32_t)n; hb.opts = opts.data();
+  hb.n_traces = (uint32_t)n; hb.trace_off = off.data(); hb.lon = lon; hb.lat = lat;
+  hb.time = time; hb.accuracy = acc; hb.n_opts = (uint32_t)n; hb.opts = opts.data();
   hb.trace_opt = topt.data();
   RunParams rp;
   rp.do_report = 0;
@@ -408,6 +438,7 @@ void serve_batch(std::unique_ptr<Matcher>& m, Engine* eng, const std::vector<Mat
 
 void Coalescer::loop() {
   std::unique_ptr<Matcher> m;
+  uint64_t traced = 0;
   for (;;) {
     std::vector<MatchRequest*> batch;
     {
@@ -427,17 +458,27 @@ void Coalescer::loop() {
     }
     double tm[4] = {0, 0, 0, 0};
     serve_batch(m, eng_.get(), batch, tm, fmt_callers());   // out / err (or segs) of each request, not under the lock
-    if (trace_ms() > 0 && tm[0] + tm[1] + tm[2] + tm[3] > trace_ms())
-      std::fprintf(stderr, "coalesce: batch of %zu requests: staging %.3f engine %.3f download %.3f format %.3f ms\n",
-                   batch.size(), tm[0], tm[1], tm[2], tm[3]);
+    if (trace_ms() > 0) {
+      if (tm[0] + tm[1] + tm[2] + tm[3] > trace_ms())
+        std::fprintf(stderr, "coalesce: batch of %zu requests: staging %.3f engine %.3f download %.3f format %.3f ms\n",
+                     batch.size(), tm[0], tm[1], tm[2], tm[3]);
+      if (++traced % 1024 == 0) {   // this dispatcher's own CPU time so far
+        rusage u{};
+        getrusage(RUSAGE_THREAD, &u);
+        std::fprintf(stderr, "coalesce: dispatcher after %llu batches: cpu %.3f s (user %.3f)\n", (unsigned long long)traced,
+                     u.ru_utime.tv_sec + u.ru_utime.tv_usec * 1e-6 + u.ru_stime.tv_sec + u.ru_stime.tv_usec * 1e-6,
+                     u.ru_utime.tv_sec + u.ru_utime.tv_usec * 1e-6);
+      }
+    }
     {
       std::lock_guard<std::mutex> lk(mu_);
       --busy_;
-      for (MatchRequest* r : batch) {
-        r->done = true;
-        r->cv.notify_one();   // under the lock: the request (and its cv) lives until its caller returns
-      }
       for (int i = 0; i < 4; ++i) tm_[i] += tm[i];
+    }
+    for (MatchRequest* r : batch) {
+      std::lock_guard<std::mutex> lk(r->mu);
+      r->done = true;
+      r->cv.notify_one();   // under its lock: the request (and its cv) lives until its caller returns
     }
   }
 }

@@ -21,6 +21,8 @@
 #include <thread>
 #include <vector>
 
+#include <sys/resource.h>
+
 #include "../../include/reporter_match.h"
 
 namespace {
@@ -29,6 +31,24 @@ size_t count_points(const std::string& s) {
   size_t n = 0;
   for (size_t at = s.find("\"lat\""); at != std::string::npos; at = s.find("\"lat\"", at + 5)) ++n;
   return n;
+}
+
+// the process's CPU seconds (user + system) and the cgroup's CPU throttling counters (cgroup v2
+// cpu.stat; zeros when absent): a service stalled by a CPU quota shows up in throttled_us
+double cpu_seconds() {
+  rusage u{};
+  getrusage(RUSAGE_SELF, &u);
+  return (double)u.ru_utime.tv_sec + u.ru_utime.tv_usec * 1e-6 + (double)u.ru_stime.tv_sec + u.ru_stime.tv_usec * 1e-6;
+}
+void cgroup_throttle(unsigned long long* periods, unsigned long long* usec) {
+  *periods = 0; *usec = 0;
+  std::ifstream f("/sys/fs/cgroup/cpu.stat");
+  std::string k;
+  unsigned long long v;
+  while (f >> k >> v) {
+    if (k == "nr_throttled") *periods = v;
+    else if (k == "throttled_usec") *usec = v;
+  }
 }
 
 }  // namespace
@@ -63,6 +83,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   // one pass of `n` requests over `clients` threads; per-request latency in microseconds
+  std::atomic<long> client_us{0};   // CPU time of the client threads themselves (parse, wait, reply)
   auto run = [&](size_t n, std::vector<double>* lat, size_t* npts, size_t* nerr) {
     std::atomic<size_t> next{0}, points{0}, errors{0};
     std::vector<std::vector<double>> lats(clients);
@@ -86,6 +107,9 @@ int main(int argc, char** argv) {
           lats[c].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
         }
         rm_matcher_destroy(m);
+        rusage u{};
+        getrusage(RUSAGE_THREAD, &u);
+        client_us += u.ru_utime.tv_sec * 1000000L + u.ru_utime.tv_usec + u.ru_stime.tv_sec * 1000000L + u.ru_stime.tv_usec;
       });
     for (auto& t : th) t.join();
     if (lat) for (auto& v : lats) lat->insert(lat->end(), v.begin(), v.end());
@@ -99,9 +123,19 @@ int main(int argc, char** argv) {
   rm_coalesce_timing(m0);
   std::vector<double> lat;
   size_t npts = 0, nerr = 0;
+  unsigned long long thr0 = 0, thu0 = 0, thr1 = 0, thu1 = 0;
+  cgroup_throttle(&thr0, &thu0);
+  const double cpu0 = cpu_seconds();
+  client_us = 0;
+  rusage r0{};
+  getrusage(RUSAGE_SELF, &r0);
   const auto t0 = std::chrono::steady_clock::now();
   run(total, &lat, &npts, &nerr);
   const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const double cpu1 = cpu_seconds();
+  rusage r1{};
+  getrusage(RUSAGE_SELF, &r1);
+  cgroup_throttle(&thr1, &thu1);
   rm_coalesce_stats(s1);
   rm_coalesce_timing(m1);
   std::sort(lat.begin(), lat.end());
@@ -111,12 +145,14 @@ int main(int argc, char** argv) {
               "\"points_per_s\": %.1f, \"points_per_request\": %.1f, \"latency_ms\": {\"p50\": %.3f, \"p90\": %.3f, "
               "\"p99\": %.3f, \"max\": %.3f}, \"batches\": %.0f, \"requests_per_batch\": %.2f, "
               "\"ms_per_batch\": %.4f, \"largest_batch\": %llu, \"dispatcher_ms_per_batch\": {\"staging\": %.4f, "
-              "\"engine\": %.4f, \"download\": %.4f, \"format\": %.4f}}\n",
+              "\"engine\": %.4f, \"download\": %.4f, \"format\": %.4f}, \"cpu_seconds\": %.3f, \"client_cpu_seconds\": %.3f, "
+              "\"context_switches\": {\"voluntary\": %ld, \"involuntary\": %ld}, \"cgroup_throttled_periods\": %llu, \"cgroup_throttled_ms\": %.1f}\n",
               clients, total, nerr, sec, (double)total / sec, (double)npts / sec, (double)npts / (double)total,
               pct(0.5), pct(0.9), pct(0.99), lat.empty() ? 0.0 : lat.back() / 1e3, batches,
               batches > 0 ? (double)(s1[1] - s0[1]) / batches : 0.0, batches > 0 ? sec * 1e3 / batches : 0.0,
               (unsigned long long)s1[2], batches > 0 ? (m1[0] - m0[0]) / batches : 0.0,
               batches > 0 ? (m1[1] - m0[1]) / batches : 0.0, batches > 0 ? (m1[2] - m0[2]) / batches : 0.0,
-              batches > 0 ? (m1[3] - m0[3]) / batches : 0.0);
+              batches > 0 ? (m1[3] - m0[3]) / batches : 0.0, cpu1 - cpu0, client_us.load() * 1e-6,
+              r1.ru_nvcsw - r0.ru_nvcsw, r1.ru_nivcsw - r0.ru_nivcsw, thr1 - thr0, (thu1 - thu0) / 1e3);
   return nerr ? 1 : 0;
 }
