@@ -376,7 +376,9 @@ def extras(gpath, tr, json_traces, tmpdir):
     # so the throughput follows the number of requests in flight)
     n_req = min(len(reqs), 4096)
     r60_py, _ = window_requests(tr, 8192, 60)
-    for workers, n_cli, rq in ((1, 64, reqs), (1, 256, reqs), (1, 64, [x.encode() for x in r60_py])):
+    # (the 60-point line, round 6: the library's default two dispatchers and one untimed pass of
+    # 1,024 requests first, as the C client's lines; the 600-point lines as in earlier rounds)
+    for workers, n_cli, rq in ((1, 64, reqs), (1, 256, reqs), (None, 64, [x.encode() for x in r60_py])):
         conf = valhalla.write_config(os.path.join(tmpdir, "reporter_bench_svc_%d.json" % os.getpid()), gpath, device=0,
                                      coalesce=True, coalesce_workers=workers)
         valhalla.Configure(conf)
@@ -384,14 +386,21 @@ def extras(gpath, tr, json_traces, tmpdir):
 
         nq = min(len(rq), 8192 if rq is not reqs else n_req)
 
-        def client(c):
+        def client(c, lo=0, hi=None, count=True):
             m = valhalla.SegmentMatcher()
-            for q in range(c, nq, n_cli):
+            for q in range(lo + c, nq if hi is None else hi, n_cli):
                 m.Match(rq[q])
-                done[c] += 1
+                if count:
+                    done[c] += 1
             m.close()
 
         import threading
+        if workers is None:
+            warm = [threading.Thread(target=client, args=(c, 0, 1024, False)) for c in range(n_cli)]
+            for th in warm:
+                th.start()
+            for th in warm:
+                th.join()
         ths = [threading.Thread(target=client, args=(c,)) for c in range(n_cli)]
         t = time.perf_counter()
         for th in ths:
@@ -405,8 +414,9 @@ def extras(gpath, tr, json_traces, tmpdir):
             n_cli, "" if npt == 600 else "_60pt")
         out[key] = {
             "what": "%d C2 /report requests (%d points each) from %d Python client threads through "
-                    "valhalla.SegmentMatcher().Match with request coalescing, %d dispatcher(s)" % (
-                        sum(done), npt, n_cli, workers),
+                    "valhalla.SegmentMatcher().Match with request coalescing, %s dispatcher(s)%s" % (
+                        sum(done), npt, n_cli, workers or "2 (default)",
+                        "; 1,024 requests untimed first" if workers is None else ""),
             "requests_per_s": sum(done) / dt, "points_per_s": pts / dt, "seconds": dt}
     # the library's own ceiling under concurrent load: the C-ABI client (no GIL), 600-point C2
     # requests and the Java batcher's ~60-point requests, 64 and 256 requests in flight
