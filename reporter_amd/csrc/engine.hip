@@ -2861,14 +2861,19 @@ constexpr int kGrpH = RM_GRP_H;
 constexpr int kGrpPathH = RM_GRP_PATH_H;
 constexpr int kGrpW = 16;
 constexpr uint32_t kGrpGrid = 4096;   // blocks of the group tiers (grid-stride over their lists)
-__global__ void __launch_bounds__(64) k_routes_grp(DevGraph g, DevBatch b) {
+// short: a small run's short hand-over chain (Matcher::run_small, round 6): the group tier takes
+// the ball tier's hand-overs (rl_routes_0, ctl[1]) itself and the 4096-slot tier takes the group
+// tier's; the lane, second register and 512-slot tiers are not launched (three launches fewer;
+// every tier is exact, so the routes are the same)
+__global__ void __launch_bounds__(64) k_routes_grp(DevGraph g, DevBatch b, int short_chain) {
   if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kGrpH, false> sm[kWave / kGrpW];
   __shared__ uint4 s_src[kWave / kGrpW][2];
   const int gi = threadIdx.x / kGrpW;
-  const uint32_t n_items = b.ctl[5];
+  const uint32_t n_items = short_chain ? b.ctl[1] : b.ctl[5];
+  const uint32_t* list = short_chain ? b.rl_routes_0 : b.rl_routes_b;
   for (uint32_t item = blockIdx.x * (kWave / kGrpW) + gi; item < n_items; item += gridDim.x * (kWave / kGrpW)) {
-    const uint32_t t = b.rl_routes_b[item];
+    const uint32_t t = list[item];
     if (!routes_search_item<kGrpH, kGrpW>(sm[gi], s_src[gi], g, b, t) && grp_lane<kGrpW>() == 0)
       b.rl_routes_a[atomicAdd(&b.ctl[11], 1u)] = t;
   }
@@ -2885,13 +2890,14 @@ __global__ void __launch_bounds__(64) k_routes_wave_s(DevGraph g, DevBatch b) {
   }
 }
 
-__global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b) {
+__global__ void __launch_bounds__(64) k_routes_wave(DevGraph g, DevBatch b, int short_chain) {
   if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kBigH, false> sm;
   __shared__ uint4 s_src[2];
-  const uint32_t n_items = b.ctl[13];
+  const uint32_t n_items = short_chain ? b.ctl[11] : b.ctl[13];   // (short: the group tier's hand-overs)
+  const uint32_t* list = short_chain ? b.rl_routes_a : b.rl_routes_0;
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const uint32_t t = b.rl_routes_0[item];
+    const uint32_t t = list[item];
     if (!routes_search_item<kBigH>(sm, s_src, g, b, t) && threadIdx.x == 0) b.rl_routes_c[atomicAdd(&b.ctl[9], 1u)] = t;
   }
 }
@@ -3867,14 +3873,16 @@ __device__ bool paths_search_item(SearchSmem<H, true>& sm, uint4* s_src, const D
 
 // path tiers, as the route tiers: group tier <- rl_paths_b (ctl[6]) -> rl_paths_a (ctl[12]) ->
 // 512 tier -> rl_routes_0 (ctl[14], free once the path lane tier has run) -> 4096 tier -> rl_paths_c
-__global__ void __launch_bounds__(64) k_paths_grp(DevGraph g, DevBatch b) {
+// (short_chain: the path ball tier's hand-overs, rl_routes_0 / ctl[8], as k_routes_grp's)
+__global__ void __launch_bounds__(64) k_paths_grp(DevGraph g, DevBatch b, int short_chain) {
   if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kGrpPathH, true> sm[kWave / kGrpW];
   __shared__ uint4 s_src[kWave / kGrpW][2];
   const int gi = threadIdx.x / kGrpW;
-  const uint32_t n_items = b.ctl[6];
+  const uint32_t n_items = short_chain ? b.ctl[8] : b.ctl[6];
+  const uint32_t* list = short_chain ? b.rl_routes_0 : b.rl_paths_b;
   for (uint32_t item = blockIdx.x * (kWave / kGrpW) + gi; item < n_items; item += gridDim.x * (kWave / kGrpW)) {
-    const uint32_t p = b.rl_paths_b[item];
+    const uint32_t p = list[item];
     if (!paths_search_item<kGrpPathH, kGrpW>(sm[gi], s_src[gi], g, b, p) && grp_lane<kGrpW>() == 0)
       b.rl_paths_a[atomicAdd(&b.ctl[12], 1u)] = p;
   }
@@ -3891,13 +3899,14 @@ __global__ void __launch_bounds__(64) k_paths_wave_s(DevGraph g, DevBatch b) {
   }
 }
 
-__global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b) {
+__global__ void __launch_bounds__(64) k_paths_wave(DevGraph g, DevBatch b, int short_chain) {
   if (steady_abort(b)) return;   // a steady run whose pools the batch outgrew (Matcher::run_steady)
   __shared__ SearchSmem<kBigH, true> sm;
   __shared__ uint4 s_src[2];
-  const uint32_t n_items = b.ctl[14];
+  const uint32_t n_items = short_chain ? b.ctl[12] : b.ctl[14];
+  const uint32_t* list = short_chain ? b.rl_paths_a : b.rl_routes_0;
   for (uint32_t item = blockIdx.x; item < n_items; item += gridDim.x) {
-    const uint32_t p = b.rl_routes_0[item];
+    const uint32_t p = list[item];
     if (!paths_search_item<kBigH>(sm, s_src, g, b, p) && threadIdx.x == 0) b.rl_paths_c[atomicAdd(&b.ctl[10], 1u)] = p;
   }
 }
@@ -5893,6 +5902,11 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
                      count_grid, w.tot64);
   toc(kKScan);
   const bool balls = (mode_mask_ & g.ball_mask) != 0u;
+  // the short hand-over chain (k_routes_grp): with the route tables most small batches hand over
+  // nothing, and the five-tier chain's launches were a sixth of their engine time;
+  // RM_SMALL_SHORT_CHAIN=0 launches every tier (A/B)
+  const char* sc_env = std::getenv("RM_SMALL_SHORT_CHAIN");   // (read per run: tests switch it)
+  const bool short_chain = balls && !(sc_env && *sc_env == '0');
   tic(kKRoutes);
   if (balls) {
     if (v.route_d) {
@@ -5902,17 +5916,19 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
     } else {
       hipLaunchKernelGGL(k_routes_ball2<false>, dim3(item_grid), dim3(kK2Threads), 0, st, g, v, kNone);
     }
-    const uint32_t lg = (uint32_t)std::min<uint64_t>(lane_grid, kListedGrid);
-    if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
-    else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
+    if (!short_chain) {
+      const uint32_t lg = (uint32_t)std::min<uint64_t>(lane_grid, kListedGrid);
+      if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
+      else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lg), dim3(256), 0, st, g, v, 0u, 1);
+    }
   } else {
     if (v.route_d) hipLaunchKernelGGL(k_routes_lane<true>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
     else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
   }
-  hipLaunchKernelGGL(k_routes_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  if (!short_chain) hipLaunchKernelGGL(k_routes_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v, short_chain ? 1 : 0);
+  if (!short_chain) hipLaunchKernelGGL(k_routes_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v, short_chain ? 1 : 0);
   if (w.gsearch) hipLaunchKernelGGL(k_routes_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
   toc(kKRoutes);
   tic(kKViterbi);
@@ -5921,14 +5937,15 @@ bool Matcher::run_small(const RunParams& rp, const DevGraph& g) {
   tic(kKPaths);
   if (balls) {
     hipLaunchKernelGGL(k_paths_ball, dim3(count_grid), dim3(256), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>(count_grid, kListedGrid)), dim3(256), 0, st, g, v, 1);
+    if (!short_chain)
+      hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)std::min<uint64_t>(count_grid, kListedGrid)), dim3(256), 0, st, g, v, 1);
   } else {
     hipLaunchKernelGGL(k_paths_lane, dim3(count_grid), dim3(256), 0, st, g, v, 0);
   }
-  hipLaunchKernelGGL(k_paths_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_paths_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_paths_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_paths_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  if (!short_chain) hipLaunchKernelGGL(k_paths_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v, short_chain ? 1 : 0);
+  if (!short_chain) hipLaunchKernelGGL(k_paths_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v, short_chain ? 1 : 0);
   if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
   toc(kKPaths);
   tic(kKSegments);
@@ -6055,9 +6072,9 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
     else hipLaunchKernelGGL(k_routes_lane<false>, dim3(lane_grid), dim3(256), 0, st, g, v, kNone, 0);
   }
   hipLaunchKernelGGL(k_routes_reg2, dim3(sgrid(kReg2Grid, 3, 256)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_grp, dim3(sgrid(kGrpGrid, 5, kWave / kGrpW)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_grp, dim3(sgrid(kGrpGrid, 5, kWave / kGrpW)), dim3(64), 0, st, g, v, 0);
   hipLaunchKernelGGL(k_routes_wave_s, dim3(sgrid(kMidGrid, 11, 1)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave, dim3(sgrid(1024, 13, 1)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave, dim3(sgrid(1024, 13, 1)), dim3(64), 0, st, g, v, 0);
   if (w.gsearch) hipLaunchKernelGGL(k_routes_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
   toc(kKRoutes);
   tic(kKViterbi);
@@ -6071,9 +6088,9 @@ bool Matcher::run_steady(const RunParams& rp, const DevGraph& g) {
     hipLaunchKernelGGL(k_paths_lane, dim3(count_grid), dim3(256), 0, st, g, v, 0);
   }
   hipLaunchKernelGGL(k_paths_reg2, dim3(sgrid(kReg2Grid, 4, 256)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_paths_grp, dim3(sgrid(kGrpGrid, 6, kWave / kGrpW)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_grp, dim3(sgrid(kGrpGrid, 6, kWave / kGrpW)), dim3(64), 0, st, g, v, 0);
   hipLaunchKernelGGL(k_paths_wave_s, dim3(sgrid(kMidGrid, 12, 1)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_paths_wave, dim3(sgrid(1024, 14, 1)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_paths_wave, dim3(sgrid(1024, 14, 1)), dim3(64), 0, st, g, v, 0);
   if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
   toc(kKPaths);
   tic(kKSegments);
@@ -6230,9 +6247,9 @@ void Matcher::run_device(const RunParams& rp) {
   // a coalesced service batch of ~15 k points launches them mostly empty
   const auto tgrid = [P](uint32_t full) { return tier_grid(P, full); };
   hipLaunchKernelGGL(k_routes_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v, 0);
   hipLaunchKernelGGL(k_routes_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
-  hipLaunchKernelGGL(k_routes_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+  hipLaunchKernelGGL(k_routes_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v, 0);
   // the global tier runs in line once its scratch exists; before that, a hand-over seen at the
   // path-stage read-back allocates it and re-runs K3 (rare: bounds of many kilometres)
   bool routes_global_done = w.gsearch != nullptr;
@@ -6258,9 +6275,9 @@ void Matcher::run_device(const RunParams& rp) {
       hipLaunchKernelGGL(k_paths_lane, dim3((uint32_t)((P + 255) / 256)), dim3(256), 0, st, g, v, 0);
     }
     hipLaunchKernelGGL(k_paths_reg2, dim3(tgrid(kReg2Grid)), dim3(256), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_grp, dim3(tgrid(kGrpGrid)), dim3(64), 0, st, g, v, 0);
     hipLaunchKernelGGL(k_paths_wave_s, dim3(tgrid(kMidGrid)), dim3(64), 0, st, g, v);
-    hipLaunchKernelGGL(k_paths_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v);
+    hipLaunchKernelGGL(k_paths_wave, dim3(tgrid(1024)), dim3(64), 0, st, g, v, 0);
     if (w.gsearch) hipLaunchKernelGGL(k_paths_global, dim3(kGlobalGrid), dim3(64), 0, st, g, v, (GlobalPathSmem*)w.gsearch);
     toc(kKPaths);
     // traversal records are laid out by a scan of path_cnt (0 for slots without a chosen transition)

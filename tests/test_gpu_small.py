@@ -117,3 +117,36 @@ def test_lone_caller_runs_inline(built_lib, small_world, tmp_path):
     st = valhalla.coalesce_stats()
     assert st["requests"] - before["requests"] == 24 and st["batches"] - before["batches"] == 24, (before, st)
     sm.close()
+
+
+@pytest.mark.parametrize("rate,turn", [(15.0, 0.0), (30.0, 200.0)])
+def test_small_run_short_chain_hand_overs(built_lib, small_world, monkeypatch, rate, turn):
+    """Round 6: a ball-covered small run hands the K2 / path ball tiers' leftovers straight to the
+    16-lane group tier and its leftovers to the 4096-slot tier (RM_SMALL_SHORT_CHAIN, default on).
+    With 100 m route balls and sparse sampling most searches are handed over; the short chain, the
+    full five-tier chain (RM_SMALL_SHORT_CHAIN=0) and the oracle agree at every stage."""
+    g = graphfile.load(small_world)
+    tr = world.generate_traces(small_world, n_traces=40, n_points=16, rate_s=rate, noise_m=5.0, seed=305)
+    opts = engine.default_options(1, turn_penalty_factor=turn)
+    ref = _ref(g, tr, opts)
+    eng = engine.Engine(small_world, 0)
+    eng.set_ball_radius(100.0)
+    bm = engine.BatchMatcher(eng)
+    got, tiers = {}, {}
+    # (the first run may outgrow a fresh matcher's path pool and take the ordinary path, which
+    # sizes it: the short chain's own run is the second)
+    for short in ("1", "1", "0"):
+        monkeypatch.setenv("RM_SMALL_SHORT_CHAIN", short)
+        bm.run(tr["trace_off"], tr["lon"], tr["lat"], tr["time"], tr["accuracy"], opts)
+        tiers[short] = bm.route_tiers()
+        c = compare_all(bm, ref, tr["trace_off"])
+        assert c["segments"] > 40, c
+        off, segs = bm.segments()
+        got[short] = (off, segs.tobytes())
+    print(tiers)
+    assert tiers["1"]["ball_to_search"] > 100 and tiers["1"]["paths_ball_to_search"] > 20, tiers
+    assert tiers["1"]["lane_to_tier2"] == 0, tiers   # the lane tier did not run
+    assert got["1"][1] == got["0"][1]
+    np.testing.assert_array_equal(got["1"][0], got["0"][0])
+    bm.close()
+    eng.close()
