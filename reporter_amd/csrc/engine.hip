@@ -2023,12 +2023,55 @@ __device__ __forceinline__ uint4 ball_resolve_at_g(k2_gptr ent, const uint2& h, 
     if ((e.x & rmask) == road || e.x == kNone) return e;
   }
 }
+// phase 2 without turn costs: 3 (default, round 6) one transition per lane and step with the next
+// step's descriptor loaded ahead; 1 the same without the prefetch; 2 two transitions per step
 #ifndef RM_K2_PLAIN_STEP
-#define RM_K2_PLAIN_STEP 1
+#define RM_K2_PLAIN_STEP 3
 #endif
 template <class SM>
 __device__ __forceinline__ void k2_phase2_slim(SM& sm, const DevBatch& b, uint32_t n, uint32_t rm, k2_gptr dummy) {
   const uint4 none = make_uint4(kNone, kBallNoDist, kBallNoDist, 0u);
+  if (RM_K2_PLAIN_STEP == 3) {   // one transition per step, the next step's descriptor loaded ahead
+    // (its loads are in flight with this step's probes: one memory round trip per step instead of
+    // two; 54 VGPRs, 8 waves per SIMD; C2 routes 0.782 -> 0.766 ms)
+    uint32_t q = threadIdx.x;
+    uint4 ta0 = make_uint4(0u, 0u, 0u, 0u);
+    uint2 ta1 = make_uint2(0u, 0u);
+    if (q < n) {
+      const K2SrcS& A0 = sm.src[sm.owner[q]];
+      const uint4* pd = b.cand_desc + 2 * (uint64_t)(A0.dbase + q);
+      ta0 = k2_ld((k2_gptr)(const void*)pd);
+      ta1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pd + 1) + 1));
+    }
+    for (; q < n; q += kK2Threads) {
+      const K2SrcS& A = sm.src[sm.owner[q]];
+      const uint32_t qn = q + kK2Threads < n ? q + kK2Threads : q;   // clamped: a valid address
+      const K2SrcS& An = sm.src[sm.owner[qn]];
+      const uint4* pdn = b.cand_desc + 2 * (uint64_t)(An.dbase + qn);
+      const uint4 nt0 = k2_ld((k2_gptr)(const void*)pdn);
+      const uint2 nt1 = k2_ld2((k2_gptr2)(const void*)(reinterpret_cast<const uint2*>(pdn + 1) + 1));
+      const bool la = A.bound != kNone;
+      const unsigned long long ak1 = (unsigned long long)A.rk1h << 32 | A.rk1l, ak0 = (unsigned long long)A.rk0h << 32 | A.rk0l;
+      const bool ua = la && ta0.w != 0u;
+      const bool ua1 = ua && ak1 != kKeyInf, ua0 = ua && ak0 != kKeyInf;
+      const k2_gptr ea = (k2_gptr)(const void*)(uintptr_t)sm.ent_mode[A.roadm >> 29];
+      const k2_gptr pa1 = ua1 ? ea + (ball_row0(A.h1x) + ball_slot(ta0.x, A.h1y)) : dummy;
+      const k2_gptr pa0 = ua0 ? ea + (ball_row0(A.h0x) + ball_slot(ta0.x, A.h0y)) : dummy;
+      const uint4 la1 = k2_ld(pa1), la0 = k2_ld(pa0);
+      bool xa = true;
+      const uint32_t r = k2_route_v(ak1, ak0, A.roadm & 0x1fffffffu, A.s, A.lim, A.bound, A.tmax, ta0,
+                                    make_uint4(0u, 0u, ta1.x, ta1.y),
+                                    ball_resolve_g(ea, make_uint2(A.h1x, A.h1y), ta0.x, k2_row_or_none(ua1, la1), rm),
+                                    ball_resolve_g(ea, make_uint2(A.h0x, A.h0y), ta0.x, k2_row_or_none(ua0, la0), rm), xa);
+      if (la) {
+        b.route[A.obase + q] = r;
+        if (!xa) k2_redo(sm, sm.owner[q]);
+      }
+      ta0 = nt0;
+      ta1 = nt1;
+    }
+    return;
+  }
   if (RM_K2_PLAIN_STEP == 1) {   // (A/B: one transition per lane and step, fewer registers)
     for (uint32_t q = threadIdx.x; q < n; q += kK2Threads) {
       const K2SrcS& A = sm.src[sm.owner[q]];
