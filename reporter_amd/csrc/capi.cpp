@@ -339,9 +339,8 @@ std::vector<std::string> match_parsed(Matcher& m, const std::vector<ParsedTrace*
   // a large batch goes up from this thread's pinned staging (grow-only): its uploads run as DMA
   // instead of staged pageable copies.  A small one (a coalesced service batch) is packed into the
   // matcher's own pinned block by Matcher::run, so it stages in pageable memory here: no pinned
-  // allocation on a caller's thread (the inline path) and none freed when that thread exits --
-  // pinning maps and unmaps pages under the process's memory lock, which stalled every other
-  // thread of a 256-client service for tens of milliseconds (p99 60-80 ms).
+  // allocation (and no pool hand-off) on a caller's thread (the inline path), and none freed when
+  // that thread exits.
   constexpr uint64_t kPinnedStagingMin = 65536;   // Matcher::run's small-run limit (RM_SMALL_BATCH_POINTS)
   float *lon, *lat, *acc;
   double* time;
