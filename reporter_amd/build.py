@@ -72,7 +72,27 @@ def build(force=False, verbose=False):
         if verbose:
             print("built", LIB)
     build_tools(force)
+    build_python_ext(force)
     return LIB
+
+
+def build_python_ext(force=False):
+    """valhalla/_match (SegmentMatcher.Match in one CPython call), linked against the in-tree
+    library; skipped when the Python headers are absent (Match then stays on ctypes)."""
+    import sysconfig
+    inc = sysconfig.get_paths().get("include")
+    if not inc or not os.path.exists(os.path.join(inc, "Python.h")):
+        return None
+    src = os.path.join(ROOT, "valhalla", "_match.c")
+    out = os.path.join(ROOT, "valhalla", "_match" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    if not force and not _newer(out, [src, LIB, os.path.join(ROOT, "include", "reporter_match.h")]):
+        return out
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-Wall", "-I" + inc, src, "-o", out, "-L" + HERE, "-lreporter_match",
+           "-Wl,-rpath,$ORIGIN/../reporter_amd"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("valhalla._match build failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
+    return out
 
 
 CLIENT = os.path.join(HERE, "bin", "rm_svc_client")

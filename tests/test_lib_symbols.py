@@ -41,3 +41,23 @@ def test_errors_are_reported_without_gpu(built_lib, tmp_path):
 def test_valhalla_module_surface(built_lib):
     import valhalla
     assert callable(valhalla.Configure) and hasattr(valhalla.SegmentMatcher, "Match")
+
+
+def test_fast_match_extension_loads_the_in_tree_library(built_lib):
+    """valhalla._match (Match in one CPython call) is built beside the library, Match uses it, the
+    process holds one copy of libreporter_match.so, and a closed matcher fails as on the ctypes
+    path (RuntimeError "matcher is NULL"); no GPU call."""
+    import pytest
+    import valhalla
+    from reporter_amd import _lib
+    assert valhalla._fast is not None and hasattr(valhalla._fast, "match")
+    _lib.lib()
+    with open("/proc/self/maps") as f:
+        libs = {line.split()[-1] for line in f if "libreporter_match" in line}
+    assert len(libs) == 1, libs
+    m = valhalla.SegmentMatcher.__new__(valhalla.SegmentMatcher)
+    m._h = None
+    with pytest.raises(RuntimeError, match="matcher is NULL"):
+        m.Match('{"trace": []}')
+    with pytest.raises(TypeError):
+        valhalla._fast.match(1, 5)

@@ -20,6 +20,18 @@ from reporter_amd import _lib
 
 __all__ = ["Configure", "SegmentMatcher", "coalesce_stats"]
 
+# Match in one CPython call (valhalla/_match.c, built beside the library by reporter_amd.build):
+# the ctypes path below costs a 60-point request ~15 us of GIL-held Python under 64 threads.  Only
+# with the in-tree library: the extension links that one, and a second copy (REPORTER_MATCH_LIB)
+# would not share its configuration.  RM_PY_CTYPES=1 keeps the ctypes path (A/B).
+_fast = None
+if not _os.environ.get("RM_PY_CTYPES") and _os.path.abspath(_lib.LIB_PATH) == _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
+                                                    "reporter_amd", "libreporter_match.so"):
+    try:
+        from valhalla import _match as _fast
+    except ImportError:   # not built (a source tree): the ctypes path below
+        _fast = None
+
 
 def Configure(conf_path):
     """Load the matcher config + graph into HBM (process-global)."""
@@ -39,6 +51,8 @@ class SegmentMatcher(object):
 
     def Match(self, trace_json):
         """trace JSON string in, {"segments": [...]} JSON string out."""
+        if _fast is not None:
+            return _fast.match(self._h or 0, trace_json)
         if isinstance(trace_json, str):
             trace_json = trace_json.encode("utf-8")
         out = C.c_void_p()
